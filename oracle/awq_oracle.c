@@ -1,0 +1,228 @@
+/*
+ * awq_oracle.c — CPU restatement of the reference's group quantizer.
+ *
+ * TEST INFRASTRUCTURE ONLY.  This file is the *checker* the parity tests,
+ * __graft_entry__.smoke() and bench.py's cpu_baseline leg compare the HIP path
+ * against.  Nothing in the product (awq-converter_amd/) links, loads or calls
+ * it; the product has no CPU fallback.
+ *
+ * Pinned against tests/golden/ (outputs of the reference awq.py imported in
+ * the build container by tests/golden/make_golden.py); see
+ * tests/test_oracle_golden.py.
+ *
+ * What it restates (reference = shanefitch/AWQ-Converter, src/awq_quantizer):
+ *   quantization/awq.py:173-213  _compute_scale_zp_for_group  (min/max, sym
+ *                                 abs-max, scale, clamp 1e-10, zero point)
+ *   quantization/awq.py:215-250  _quantize_tensor  (round(x/s + z), clamp)
+ *   quantization/awq.py:286-374  _quantize_per_group (rows = dim 0, rest
+ *                                 flattened, tail group zero-padded)
+ *   quantization/awq.py:130-171  _calculate_scale_zp (numel < group_size:
+ *                                 whole tensor or whole rows, no padding)
+ *   quantization/awq.py:409-412  result dtypes (int32 / fp16 / int32)
+ *   quantization/awq.py:459-539  dequantize ((q - z) * fp16 scale -> fp16)
+ *
+ * Arithmetic model (torch CPU eager semantics for one element-wise op on a
+ * reduced-precision dtype D): compute in fp32 (fp64 for D = fp64), round the
+ * result to D with round-to-nearest-even after EVERY op.  torch.round is
+ * round-half-even; min/max/clamp propagate NaN; float->int32 of NaN gives
+ * INT_MIN (x86 cvtt*).  fp64 scales are stored through an fp32 tensor
+ * (awq.py:327) before .to(float16), i.e. RN_f16(RN_f32(s)).
+ *
+ * Build: make -C oracle   (gcc, no fast-math, -ffp-contract=off)
+ */
+#include <math.h>
+#include <stdint.h>
+#include <string.h>
+
+#include "awq_oracle.h"
+
+/* ---------------- rounding helpers ---------------- */
+
+static inline uint32_t f2u(float f) { uint32_t u; memcpy(&u, &f, 4); return u; }
+static inline float u2f(uint32_t u) { float f; memcpy(&f, &u, 4); return f; }
+
+/* fp32 -> bf16 bits, round-to-nearest-even (c10::BFloat16 semantics; NaN -> 0x7FC0) */
+uint16_t oracle_f32_to_bf16(float f) {
+    if (isnan(f)) return 0x7FC0;
+    uint32_t u = f2u(f);
+    u += 0x7FFFu + ((u >> 16) & 1u);
+    return (uint16_t)(u >> 16);
+}
+float oracle_bf16_to_f32(uint16_t h) { return u2f((uint32_t)h << 16); }
+
+/* fp32 -> fp16 bits, round-to-nearest-even, subnormals kept, overflow -> inf */
+uint16_t oracle_f32_to_f16(float f) {
+    uint32_t x = f2u(f);
+    uint16_t sign = (uint16_t)((x >> 16) & 0x8000u);
+    uint32_t ax = x & 0x7FFFFFFFu;
+    if (ax > 0x7F800000u) return (uint16_t)(sign | 0x7E00u | ((ax >> 13) & 0x3FFu));
+    if (ax >= 0x47800000u) return (uint16_t)(sign | 0x7C00u);          /* >= 65536 (and inf) */
+    if (ax >= 0x38800000u) {                                             /* normal fp16 range */
+        uint32_t e = (ax >> 23) - 127u + 15u;
+        uint32_t m = ax & 0x7FFFFFu;
+        uint32_t h = (e << 10) | (m >> 13);
+        uint32_t rem = m & 0x1FFFu;
+        if (rem > 0x1000u || (rem == 0x1000u && (h & 1u))) h++;          /* may carry to inf */
+        return (uint16_t)(sign | h);
+    }
+    /* subnormal / zero: units of 2^-24, exact scaling then RNE */
+    float m = nearbyintf(u2f(ax) * 16777216.0f);
+    return (uint16_t)(sign | (uint16_t)m);
+}
+
+float oracle_f16_to_f32(uint16_t h) {
+    uint32_t sign = ((uint32_t)h & 0x8000u) << 16;
+    uint32_t e = (h >> 10) & 0x1Fu, m = h & 0x3FFu;
+    if (e == 0x1F) return u2f(sign | 0x7F800000u | (m << 13));
+    if (e == 0) {
+        float v = (float)m * (1.0f / 16777216.0f);
+        return sign ? -v : v;
+    }
+    return u2f(sign | ((e - 15u + 127u) << 23) | (m << 13));
+}
+
+/* Round a compute-type value to the storage dtype and back. */
+static inline double rn(double v, int dtype) {
+    switch (dtype) {
+    case AWQ_ORACLE_BF16: return (double)oracle_bf16_to_f32(oracle_f32_to_bf16((float)v));
+    case AWQ_ORACLE_F16: return (double)oracle_f16_to_f32(oracle_f32_to_f16((float)v));
+    case AWQ_ORACLE_F32: return (double)(float)v;
+    default: return v;
+    }
+}
+
+/* One binary op of the reference, evaluated the way torch CPU does for dtype D:
+ * fp32 math for bf16/f16/f32 (the operands are exact fp32 values), fp64 for f64. */
+static inline double op_add(double a, double b, int d) {
+    if (d == AWQ_ORACLE_F64) return a + b;
+    return rn((double)((float)a + (float)b), d);
+}
+static inline double op_sub(double a, double b, int d) {
+    if (d == AWQ_ORACLE_F64) return a - b;
+    return rn((double)((float)a - (float)b), d);
+}
+static inline double op_div(double a, double b, int d) {
+    if (d == AWQ_ORACLE_F64) return a / b;
+    return rn((double)((float)a / (float)b), d);
+}
+static inline double op_round(double a, int d) {            /* torch.round: half-to-even */
+    if (d == AWQ_ORACLE_F64) return nearbyint(a);
+    return rn((double)nearbyintf((float)a), d);
+}
+static inline double op_clamp(double a, double lo, double hi) {   /* NaN propagates */
+    if (isnan(a)) return a;
+    if (a < lo) a = lo;
+    if (a > hi) a = hi;
+    return a;
+}
+static inline int32_t to_i32(double v) {                    /* x86 cvtt: NaN -> INT_MIN */
+    if (isnan(v)) return INT32_MIN;
+    return (int32_t)v;
+}
+
+static inline double load_elem(const void* x, int dtype, int64_t i) {
+    switch (dtype) {
+    case AWQ_ORACLE_BF16: return (double)oracle_bf16_to_f32(((const uint16_t*)x)[i]);
+    case AWQ_ORACLE_F16: return (double)oracle_f16_to_f32(((const uint16_t*)x)[i]);
+    case AWQ_ORACLE_F32: return (double)((const float*)x)[i];
+    default: return ((const double*)x)[i];
+    }
+}
+
+/* awq.py:173-213 — scale and zero point of one group (values already in compute type). */
+static void group_scale_zp(double mn, double mx, int dtype, int qmin, int qmax, int sym,
+                           double* s_out, double* z_out) {
+    if (sym) {                                   /* awq.py:196-199, Python builtin max() */
+        double amn = fabs(mn), amx = fabs(mx);
+        double a = (amx > amn) ? amx : amn;
+        mn = -a;
+        mx = a;
+    }
+    double s = op_div(op_sub(mx, mn, dtype), (double)(qmax - qmin), dtype);   /* awq.py:202 */
+    double lo = rn(1e-10, dtype);                                             /* awq.py:205 */
+    if (!isnan(s) && s < lo) s = lo;
+    double z;
+    if (sym) {
+        z = 0.0;                                                              /* awq.py:208 */
+    } else {
+        z = op_sub((double)qmin, op_div(mn, s, dtype), dtype);                /* awq.py:210 */
+        z = op_clamp(op_round(z, dtype), qmin, qmax);                         /* awq.py:211 */
+    }
+    *s_out = s;
+    *z_out = z;
+}
+
+int oracle_quantize(const void* x, int dtype, int64_t rows, int64_t K, int64_t L, int bits,
+                    int sym, int32_t* tensor_q, uint16_t* scales_f16, int32_t* zeros) {
+    if (!x || rows < 0 || K < 0 || L <= 0 || (bits != 4 && bits != 8)) return -1;
+    int qmin = sym ? -(1 << (bits - 1)) : 0;                                  /* awq.py:114-128 */
+    int qmax = sym ? (1 << (bits - 1)) - 1 : (1 << bits) - 1;
+    int64_t G = (K + L - 1) / L;
+    for (int64_t r = 0; r < rows; ++r) {
+        for (int64_t g = 0; g < G; ++g) {
+            int64_t k0 = g * L, k1 = k0 + L;
+            int padded = k1 > K;                                              /* awq.py:337-339 */
+            if (k1 > K) k1 = K;
+            double mn = padded ? 0.0 : INFINITY, mx = padded ? 0.0 : -INFINITY;
+            int nan = 0;
+            for (int64_t k = k0; k < k1; ++k) {
+                double v = load_elem(x, dtype, r * K + k);
+                if (isnan(v)) nan = 1;
+                if (v < mn) mn = v;
+                if (v > mx) mx = v;
+            }
+            if (nan) { mn = NAN; mx = NAN; }
+            double s, z;
+            group_scale_zp(mn, mx, dtype, qmin, qmax, sym, &s, &z);
+            if (scales_f16) scales_f16[r * G + g] = oracle_f32_to_f16((float)s);
+            if (zeros) zeros[r * G + g] = to_i32(z);
+            if (tensor_q) {
+                for (int64_t k = k0; k < k1; ++k) {
+                    double v = load_elem(x, dtype, r * K + k);
+                    double t = op_add(op_div(v, s, dtype), z, dtype);          /* awq.py:245 */
+                    t = op_clamp(op_round(t, dtype), qmin, qmax);              /* awq.py:248 */
+                    tensor_q[r * K + k] = to_i32(t);
+                }
+            }
+        }
+    }
+    return 0;
+}
+
+/* awq.py:459-539: dq = (q - z) [int32] * scale [fp16 0-d]  -> fp16 math -> stored fp32 */
+int oracle_dequantize(const int32_t* tensor_q, const uint16_t* scales_f16, const int32_t* zeros,
+                      int64_t rows, int64_t K, int64_t L, float* out) {
+    if (!tensor_q || !scales_f16 || !zeros || !out || L <= 0) return -1;
+    int64_t G = (K + L - 1) / L;
+    for (int64_t r = 0; r < rows; ++r) {
+        for (int64_t k = 0; k < K; ++k) {
+            int64_t g = k / L;
+            int32_t diff = (int32_t)((uint32_t)tensor_q[r * K + k] - (uint32_t)zeros[r * G + g]);
+            float h = oracle_f16_to_f32(oracle_f32_to_f16((float)diff));
+            float s = oracle_f16_to_f32(scales_f16[r * G + g]);
+            out[r * K + k] = oracle_f16_to_f32(oracle_f32_to_f16(h * s));
+        }
+    }
+    return 0;
+}
+
+/* Row-major pack used by the product's packed outputs (no reference counterpart:
+ * the reference returns unpacked int32).  nibble/byte j of word c holds
+ * (v[c*per + j] - qmin) masked to `bits`; positions past n are 0. */
+int oracle_pack_rows(const int32_t* v, int64_t rows, int64_t n, int bits, int qmin, int32_t* packed) {
+    if (!v || !packed || (bits != 4 && bits != 8)) return -1;
+    int per = 32 / bits;
+    uint32_t mask = (1u << bits) - 1u;
+    int64_t words = (n + per - 1) / per;
+    for (int64_t r = 0; r < rows; ++r) {
+        for (int64_t c = 0; c < words; ++c) {
+            uint32_t w = 0;
+            for (int j = 0; j < per; ++j) {
+                int64_t i = c * per + j;
+                if (i < n) w |= (((uint32_t)v[r * n + i] - (uint32_t)qmin) & mask) << (bits * j);
+            }
+            packed[r * words + c] = (int32_t)w;
+        }
+    }
+    return 0;
+}

@@ -1,0 +1,47 @@
+/* verify_recip.c — exhaustive check of the identity the bf16 HIP fast path relies on
+ * (TEST INFRASTRUCTURE ONLY):
+ *
+ *   for every finite bf16 x and every finite bf16 s >= RN_bf16(1e-10):
+ *       RN_bf16( x * RN_f32(1/s) ) == RN_bf16( RN_f32(x / s) )
+ *
+ * i.e. one correctly rounded reciprocal per group + one fp32 multiply per element
+ * reproduces awq.py:245's `tensor / scale` (torch bf16 divide = fp32 divide + RNE)
+ * and awq.py:210's `t_min / scale` bit for bit.  Also reports the fp16 analogue
+ * (expected to FAIL, which is why fp16 inputs use a true division).
+ * Usage: verify_recip [bf16|f16]   -> prints mismatches, exit 0 iff none (bf16). */
+#include <math.h>
+#include <stdio.h>
+#include <stdint.h>
+#include <string.h>
+#include "awq_oracle.h"
+
+static int finite16(uint16_t h, int bf) {
+    return bf ? ((h & 0x7F80u) != 0x7F80u) : ((h & 0x7C00u) != 0x7C00u);
+}
+static float dec(uint16_t h, int bf) { return bf ? oracle_bf16_to_f32(h) : oracle_f16_to_f32(h); }
+static uint16_t enc(float f, int bf) { return bf ? oracle_f32_to_bf16(f) : oracle_f32_to_f16(f); }
+
+int main(int argc, char** argv) {
+    int bf = !(argc > 1 && strcmp(argv[1], "f16") == 0);
+    float lo = dec(enc(1e-10f, bf), bf);
+    long long mismatches = 0, pairs = 0;
+#pragma omp parallel for reduction(+ : mismatches, pairs) schedule(dynamic, 64)
+    for (int si = 0; si < 65536; ++si) {
+        uint16_t sh = (uint16_t)si;
+        if (!finite16(sh, bf)) continue;
+        float s = dec(sh, bf);
+        if (!(s >= lo) || s <= 0.0f) continue;
+        volatile float one = 1.0f;
+        float r = one / s;
+        for (int xi = 0; xi < 65536; ++xi) {
+            uint16_t xh = (uint16_t)xi;
+            if (!finite16(xh, bf)) continue;
+            float x = dec(xh, bf);
+            uint16_t a = enc(x * r, bf), b = enc(x / s, bf);
+            pairs++;
+            if (a != b) mismatches++;
+        }
+    }
+    printf("%s: pairs=%lld mismatches=%lld\n", bf ? "bf16" : "f16", pairs, mismatches);
+    return (bf && mismatches == 0) ? 0 : 1;
+}

@@ -1,0 +1,57 @@
+"""Pin the CPU oracle (oracle/) against the reference's own outputs (tests/golden/).
+
+The fixtures were produced by importing the reference awq.py in the build
+container (tests/golden/make_golden.py).  Every case must match bit for bit
+(int32 tensor_q/zero_points, fp16 scales, fp32 dequantize); the only latitude is
+NaN payload/sign in floating outputs (see golden_io.same_bits_nan_eq).
+"""
+import pytest
+import torch
+
+import golden_io as gio
+from oracle import awq_oracle as orc
+
+
+@pytest.mark.parametrize("case", gio.ok_cases(), ids=lambda c: c["name"])
+def test_oracle_matches_reference_case(case):
+    x = gio.case_input(case)
+    p = case["params"]
+    res = orc.quantize(x, bits=p["bits"], group_size=p["group_size"], symmetric=p["symmetric"],
+                       per_channel=p.get("per_channel", True))
+    T = gio.tensors()
+    name = case["name"]
+    assert torch.equal(res["tensor_q"], T[name + ".tensor_q"]), "tensor_q"
+    assert torch.equal(res["zero_points"], T[name + ".zero_points"]), "zero_points"
+    assert gio.same_bits_nan_eq(res["scales"], T[name + ".scales"]), "scales"
+    if "out_shapes" in case:
+        assert list(res["scales"].shape) == case["out_shapes"]["scales"]
+    if name + ".dq" in T:
+        dq = orc.dequantize(res)
+        assert gio.same_bits_nan_eq(dq, T[name + ".dq"]), "dequantize"
+    elif case.get("dequantize") == "IndexError":
+        with pytest.raises(IndexError):
+            orc.dequantize(res)
+
+
+@pytest.mark.parametrize("rec", gio.manifest()["hashed"], ids=lambda r: r["name"])
+def test_oracle_matches_reference_hashed(rec):
+    x = gio.hashed_input(rec)
+    assert gio.sha(x) == rec["sha_x"], "input regeneration drifted"
+    p = rec["params"]
+    res = orc.quantize(x, bits=p["bits"], group_size=p["group_size"], symmetric=p["symmetric"])
+    assert gio.sha(res["tensor_q"]) == rec["sha_tensor_q"]
+    assert gio.sha(res["scales"]) == rec["sha_scales"]
+    assert gio.sha(res["zero_points"]) == rec["sha_zero_points"]
+    if rec.get("sha_dq"):
+        assert gio.sha(orc.dequantize(res)) == rec["sha_dq"]
+
+
+def test_exhaustive_bf16_reciprocal_identity():
+    """The bf16 fast path's x*RN(1/s) == x/s identity, over all 1.35e9 (x, s) pairs."""
+    import os
+    import subprocess
+    subprocess.run(["make", "-s", "-C", os.path.dirname(orc.__file__), "verify_recip"], check=True)
+    out = subprocess.run([os.path.join(os.path.dirname(orc.__file__), "verify_recip"), "bf16"],
+                         capture_output=True, text=True, timeout=600)
+    assert out.returncode == 0, out.stdout + out.stderr
+    assert "mismatches=0" in out.stdout

@@ -1,0 +1,86 @@
+"""Ragged multi-tensor launch: many tensors, one kernel (include/awq_hip.h
+awq_plan_ragged / awq_quantize_ragged).
+
+A model's tensor set (e.g. opt-125m: 196 tensors, 110 of them 768-element biases) is
+quantized by ONE launch of the streaming kernel over all tensors' tiles instead of one
+launch (or, in the reference, ~20 ATen dispatches per 128-element group,
+awq.py:345-368) per tensor.  The descriptor table is planned once on the host,
+uploaded once, and can be re-launched any number of times (bench.py does).
+"""
+from typing import Dict, Optional
+
+import torch
+
+from .. import _hip
+
+
+class PackedBatch:
+    """Device-resident inputs + packed outputs of one ragged launch.
+
+    inputs: name -> contiguous bf16 device tensor ([rows, ...] or 1-D), K % 128 == 0.
+    parity=True additionally produces the reference's unpacked int32 tensor_q and
+    zero_points (6.05 B/element of output traffic instead of 0.52).
+    """
+
+    def __init__(self, inputs: Dict[str, torch.Tensor], bits: int = 4, symmetric: bool = False,
+                 parity: bool = False, packed: bool = True):
+        if not inputs:
+            raise ValueError("PackedBatch needs at least one tensor")
+        self.bits, self.symmetric, self.parity = bits, bool(symmetric), parity
+        self.names = list(inputs)
+        dev = next(iter(inputs.values())).device
+        _hip.require_device(dev)
+        self.device = dev
+        self.inputs = inputs
+        per = 32 // bits
+        self.out = {}
+        descs = []
+        for name in self.names:
+            x = inputs[name]
+            if x.device != dev or x.dtype != torch.bfloat16 or not x.is_contiguous():
+                raise ValueError(f"{name}: inputs must be contiguous bf16 tensors on {dev}")
+            rows = 1 if x.dim() <= 1 else x.shape[0]
+            K = x.numel() // rows
+            if not _hip.ragged_eligible(x.dtype, rows, K, 128):
+                raise ValueError(f"{name}: shape {tuple(x.shape)} is not eligible for a ragged launch")
+            G = K // 128
+            o = {"scales": torch.empty((rows, G), dtype=torch.float16, device=dev)}
+            if packed:
+                o["qweight"] = torch.empty((rows, -(-K // per)), dtype=torch.int32, device=dev)
+                o["qzeros"] = torch.empty((rows, -(-G // per)), dtype=torch.int32, device=dev)
+            if parity:
+                o["tensor_q"] = torch.empty(x.shape, dtype=torch.int32, device=dev)
+                o["zero_points"] = torch.empty((rows, G), dtype=torch.int32, device=dev)
+            self.out[name] = o
+            p = lambda k: o[k].data_ptr() if k in o else None
+            descs.append(_hip.TensorDesc(x.data_ptr(), rows, K, p("qweight"), p("qzeros"), p("scales"),
+                                         p("tensor_q"), p("zero_points"), 0, 0))
+        self.total_tiles = _hip.plan_ragged(descs, bits)
+        self.descs = descs
+        self.descs_dev = _hip.descs_to_device(descs, dev)
+        self.elements = sum(inputs[n].numel() for n in self.names)
+
+    def run(self, stream: Optional[torch.cuda.Stream] = None) -> None:
+        s = stream if stream is not None else torch.cuda.current_stream(self.device)
+        _hip.quantize_ragged(self.descs_dev, len(self.descs), self.total_tiles, self.bits, self.symmetric,
+                             s.cuda_stream)
+
+    def results(self) -> Dict[str, Dict[str, torch.Tensor]]:
+        res = {}
+        for name in self.names:
+            o = dict(self.out[name])
+            o["bits"] = torch.tensor(self.bits, dtype=torch.int32)
+            o["group_size"] = torch.tensor(128, dtype=torch.int32)
+            o["symmetric"] = torch.tensor(self.symmetric, dtype=torch.bool)
+            o["shape"] = torch.tensor(list(self.inputs[name].shape), dtype=torch.int64)
+            res[name] = o
+        return res
+
+    def algorithmic_bytes(self) -> int:
+        """HBM bytes one launch must move: bf16 in + packed out (+ parity outputs)."""
+        b = 0
+        for name in self.names:
+            b += self.inputs[name].numel() * 2
+            for t in self.out[name].values():
+                b += t.numel() * t.element_size()
+        return b

@@ -1,0 +1,173 @@
+// awq_capi.hip — the extern "C" boundary of libawq_hip.so (declared in include/awq_hip.h).
+//
+// Validates arguments, picks the kernel, launches on the caller's stream and reports
+// errors through a thread-local message.  No allocation, no synchronisation, no global
+// mutable state: one instance may be called from many host threads at once (the
+// reference's CLI shares one quantizer between its worker threads, main.py:609-621).
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+
+#include "awq_internal.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
+int fail(int code, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
+
+int hip_status(hipError_t e, const char* what) {
+    if (e == hipSuccess) return AWQ_OK;
+    return fail(AWQ_EHIP, "%s: %s", what, hipGetErrorString(e));
+}
+
+bool aligned(const void* p, size_t a) { return ((uintptr_t)p % a) == 0; }
+
+int check_common(int64_t rows, int64_t K, int64_t group_size, int bits) {
+    if (bits != 4 && bits != 8) return fail(AWQ_EINVAL, "Unsupported bit width: %d. Supported: 4, 8.", bits);
+    if (group_size <= 0) return fail(AWQ_EINVAL, "Group size must be a positive integer: %lld", (long long)group_size);
+    if (rows < 0 || K < 0) return fail(AWQ_EINVAL, "negative shape (%lld, %lld)", (long long)rows, (long long)K);
+    return AWQ_OK;
+}
+
+bool fast_eligible(int dtype, int64_t rows, int64_t K, int64_t group_size) {
+    return dtype == AWQ_DTYPE_BF16 && group_size == awq::kGroup && awq::fast_shape_ok(rows, K);
+}
+
+}  // namespace
+
+extern "C" {
+
+int awq_abi_version(void) { return AWQ_HIP_ABI_VERSION; }
+
+const char* awq_last_error(void) { return g_err.c_str(); }
+
+int awq_device_check(char* arch, int len) {
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return fail(AWQ_ENODEV, "no HIP device: %s", hipGetErrorString(e));
+    hipDeviceProp_t prop;
+    e = hipGetDeviceProperties(&prop, dev);
+    if (e != hipSuccess) return fail(AWQ_ENODEV, "hipGetDeviceProperties: %s", hipGetErrorString(e));
+    if (arch && len > 0) {
+        std::strncpy(arch, prop.gcnArchName, (size_t)len - 1);
+        arch[len - 1] = 0;
+    }
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+        return fail(AWQ_ENODEV, "libawq_hip.so is built for gfx950 (MI355X); device %d is %s", dev,
+                    prop.gcnArchName);
+    return AWQ_OK;
+}
+
+int awq_ragged_eligible(int dtype, int64_t rows, int64_t K, int64_t group_size) {
+    return fast_eligible(dtype, rows, K, group_size) ? 1 : 0;
+}
+
+int awq_quantize_groups(const void* w, int dtype, int64_t rows, int64_t K, int64_t group_size,
+                        int bits, int symmetric, int32_t* qweight, int32_t* qzeros,
+                        uint16_t* scales, int32_t* tensor_q, int32_t* zeros, void* stream) {
+    g_err.clear();
+    if (int rc = check_common(rows, K, group_size, bits)) return rc;
+    if (dtype < AWQ_DTYPE_BF16 || dtype > AWQ_DTYPE_F64) return fail(AWQ_EINVAL, "unknown dtype code %d", dtype);
+    if (!qweight && !qzeros && !scales && !tensor_q && !zeros) return fail(AWQ_EINVAL, "no output requested");
+    if (rows * K == 0) return AWQ_OK;
+    if (!w) return fail(AWQ_EINVAL, "null input");
+    hipStream_t s = (hipStream_t)stream;
+    const int qmin = symmetric ? -(1 << (bits - 1)) : 0;
+    if (fast_eligible(dtype, rows, K, group_size) && aligned(w, 16) && (!qweight || aligned(qweight, 8)) &&
+        (!tensor_q || aligned(tensor_q, 16)) && (!zeros || aligned(zeros, 4)) && (!qzeros || aligned(qzeros, 4)) &&
+        (!scales || aligned(scales, 2))) {
+        awq_tensor_desc d{};
+        d.w = w; d.rows = rows; d.K = K; d.qweight = qweight; d.qzeros = qzeros; d.scales = scales;
+        d.tensor_q = tensor_q; d.zeros = zeros; d.tile_begin = 0;
+        d.tile_count = awq::fast_tiles(rows, K, bits);
+        return hip_status(awq::launch_fast(nullptr, &d, 1, d.tile_count, bits, symmetric, s), "awq fast kernel");
+    }
+    // generic path: per-group int32 values first, then packing (needs tensor_q / zeros buffers)
+    if ((qweight && !tensor_q) || (qzeros && !zeros))
+        return fail(AWQ_EINVAL, "this shape/dtype takes the generic kernel: packed outputs need the int32 "
+                                "tensor_q/zeros buffers as staging (pass them too)");
+    if (int rc = hip_status(awq::launch_generic(w, dtype, rows, K, group_size, bits, symmetric, tensor_q,
+                                                scales, zeros, s), "awq generic kernel"))
+        return rc;
+    const int64_t G = (K + group_size - 1) / group_size;
+    if (qweight)
+        if (int rc = hip_status(awq::launch_pack(tensor_q, rows, K, bits, qmin, qweight, s), "awq pack"))
+            return rc;
+    if (qzeros)
+        if (int rc = hip_status(awq::launch_pack(zeros, rows, G, bits, qmin, qzeros, s), "awq pack"))
+            return rc;
+    return AWQ_OK;
+}
+
+int64_t awq_plan_ragged(awq_tensor_desc* descs, int n, int bits) {
+    g_err.clear();
+    if (n < 0 || (n > 0 && !descs)) return fail(AWQ_EINVAL, "bad descriptor array"), -1;
+    if (bits != 4 && bits != 8) return fail(AWQ_EINVAL, "Unsupported bit width: %d. Supported: 4, 8.", bits), -1;
+    int64_t total = 0;
+    for (int i = 0; i < n; ++i) {
+        awq_tensor_desc& d = descs[i];
+        if (!fast_eligible(AWQ_DTYPE_BF16, d.rows, d.K, awq::kGroup))
+            return fail(AWQ_EINVAL, "tensor %d (%lld x %lld) is not eligible for a ragged launch", i,
+                        (long long)d.rows, (long long)d.K), -1;
+        if (!d.w || !aligned(d.w, 16) || (d.qweight && !aligned(d.qweight, 8)) ||
+            (d.tensor_q && !aligned(d.tensor_q, 16)) || (d.zeros && !aligned(d.zeros, 4)) ||
+            (d.qzeros && !aligned(d.qzeros, 4)) || (d.scales && !aligned(d.scales, 2)))
+            return fail(AWQ_EINVAL, "tensor %d: null or misaligned pointer", i), -1;
+        d.tile_begin = total;
+        d.tile_count = awq::fast_tiles(d.rows, d.K, bits);
+        total += d.tile_count;
+    }
+    return total;
+}
+
+int awq_quantize_ragged(const awq_tensor_desc* descs_device, int n, int64_t total_tiles, int bits,
+                        int symmetric, void* stream) {
+    g_err.clear();
+    if (bits != 4 && bits != 8) return fail(AWQ_EINVAL, "Unsupported bit width: %d. Supported: 4, 8.", bits);
+    if (n <= 0 || total_tiles <= 0) return AWQ_OK;
+    if (!descs_device) return fail(AWQ_EINVAL, "null descriptor array");
+    return hip_status(awq::launch_fast(descs_device, nullptr, n, total_tiles, bits, symmetric,
+                                       (hipStream_t)stream), "awq ragged kernel");
+}
+
+int awq_dequantize(const int32_t* tensor_q, const uint16_t* scales, const int32_t* zeros, int64_t rows,
+                   int64_t K, int64_t group_size, float* out, void* stream) {
+    g_err.clear();
+    if (group_size <= 0) return fail(AWQ_EINVAL, "Group size must be a positive integer: %lld", (long long)group_size);
+    if (rows * K == 0) return AWQ_OK;
+    if (!tensor_q || !scales || !zeros || !out) return fail(AWQ_EINVAL, "null argument");
+    return hip_status(awq::launch_dequant(tensor_q, nullptr, scales, zeros, nullptr, rows, K, group_size, 4, 0,
+                                          out, (hipStream_t)stream), "awq dequant kernel");
+}
+
+int awq_dequantize_packed(const int32_t* qweight, const int32_t* qzeros, const uint16_t* scales, int64_t rows,
+                          int64_t K, int64_t group_size, int bits, int symmetric, float* out, void* stream) {
+    g_err.clear();
+    if (int rc = check_common(rows, K, group_size, bits)) return rc;
+    if (rows * K == 0) return AWQ_OK;
+    if (!qweight || !scales || !qzeros || !out) return fail(AWQ_EINVAL, "null argument");
+    const int qmin = symmetric ? -(1 << (bits - 1)) : 0;
+    return hip_status(awq::launch_dequant(nullptr, qweight, scales, nullptr, qzeros, rows, K, group_size, bits,
+                                          qmin, out, (hipStream_t)stream), "awq dequant kernel");
+}
+
+int awq_pack_rows(const int32_t* v, int64_t rows, int64_t n, int bits, int qmin, int32_t* packed, void* stream) {
+    g_err.clear();
+    if (bits != 4 && bits != 8) return fail(AWQ_EINVAL, "Unsupported bit width: %d. Supported: 4, 8.", bits);
+    if (rows * n == 0) return AWQ_OK;
+    if (!v || !packed) return fail(AWQ_EINVAL, "null argument");
+    return hip_status(awq::launch_pack(v, rows, n, bits, qmin, packed, (hipStream_t)stream), "awq pack");
+}
+
+}  // extern "C"

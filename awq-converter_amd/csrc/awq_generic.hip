@@ -1,0 +1,275 @@
+// awq_generic.hip — any-dtype / any-group-size quantizer, packer and dequantizer (gfx950).
+//
+// Covers every case the streaming kernel (awq_fast.hip) does not: fp16/fp32/fp64 inputs,
+// group sizes other than 128, K not a multiple of the group size (zero-padded tail group,
+// reference awq.py:337-339) and the small-tensor path (numel < group_size, awq.py:130-171,
+// expressed by the caller as one group per row: group_size = K).
+//
+// One wave per group: lanes stride over the group's elements, min/max/NaN reduced across
+// the wave with cross-lane shuffles, then a second pass (L1/L2-hot) quantizes.  Each
+// element-wise op of the reference is evaluated the way torch's CPU kernels do for the
+// input dtype D: fp32 math (fp64 for D = fp64), then round-to-nearest-even to D
+// (software RNE here — independent of the hardware conversions the fast kernel uses),
+// and a true IEEE division for x / s.
+#include "awq_internal.h"
+
+namespace awq {
+namespace {
+
+// ---- software RNE conversions (bit-exact with c10::BFloat16 / c10::Half) ----
+__device__ __forceinline__ float sw_rn_bf16(float f) {
+    if (__builtin_isnan(f)) return f;
+    uint32_t u = __float_as_uint(f);
+    u += 0x7FFFu + ((u >> 16) & 1u);
+    return __uint_as_float(u & 0xFFFF0000u);
+}
+
+__device__ __forceinline__ uint16_t sw_f32_to_f16(float f) {
+    uint32_t x = __float_as_uint(f);
+    uint16_t sign = (uint16_t)((x >> 16) & 0x8000u);
+    uint32_t ax = x & 0x7FFFFFFFu;
+    if (ax > 0x7F800000u) return (uint16_t)(sign | 0x7E00u | ((ax >> 13) & 0x3FFu));
+    if (ax >= 0x47800000u) return (uint16_t)(sign | 0x7C00u);
+    if (ax >= 0x38800000u) {
+        uint32_t e = (ax >> 23) - 127u + 15u;
+        uint32_t m = ax & 0x7FFFFFu;
+        uint32_t h = (e << 10) | (m >> 13);
+        uint32_t rem = m & 0x1FFFu;
+        if (rem > 0x1000u || (rem == 0x1000u && (h & 1u))) h++;
+        return (uint16_t)(sign | h);
+    }
+    float m = __builtin_rintf(__uint_as_float(ax) * 16777216.0f);
+    return (uint16_t)(sign | (uint16_t)m);
+}
+
+__device__ __forceinline__ float sw_f16_to_f32(uint16_t h) {
+    uint32_t sign = ((uint32_t)h & 0x8000u) << 16;
+    uint32_t e = (h >> 10) & 0x1Fu, m = h & 0x3FFu;
+    if (e == 0x1F) return __uint_as_float(sign | 0x7F800000u | (m << 13));
+    if (e == 0) {
+        float v = (float)m * (1.0f / 16777216.0f);
+        return sign ? -v : v;
+    }
+    return __uint_as_float(sign | ((e - 15u + 127u) << 23) | (m << 13));
+}
+
+__device__ __forceinline__ uint16_t canon_f16(float s) {
+    return __builtin_isnan(s) ? (uint16_t)0x7E00 : sw_f32_to_f16(s);
+}
+
+// ---- dtype traits: storage type, compute type, per-op rounding ----
+template <int DT> struct Traits;
+template <> struct Traits<AWQ_DTYPE_BF16> {
+    typedef uint16_t S; typedef float C;
+    static __device__ float load(const S* p, int64_t i) { return __uint_as_float((uint32_t)p[i] << 16); }
+    static __device__ float rn(float v) { return sw_rn_bf16(v); }
+    static __device__ float lo() { return __uint_as_float(0x2EDC0000u); }   // RN_bf16(1e-10)
+};
+template <> struct Traits<AWQ_DTYPE_F16> {
+    typedef uint16_t S; typedef float C;
+    static __device__ float load(const S* p, int64_t i) { return sw_f16_to_f32(p[i]); }
+    static __device__ float rn(float v) { return sw_f16_to_f32(sw_f32_to_f16(v)); }
+    static __device__ float lo() { return 0.0f; }                           // RN_f16(1e-10) = 0
+};
+template <> struct Traits<AWQ_DTYPE_F32> {
+    typedef float S; typedef float C;
+    static __device__ float load(const S* p, int64_t i) { return p[i]; }
+    static __device__ float rn(float v) { return v; }
+    static __device__ float lo() { return 1e-10f; }
+};
+template <> struct Traits<AWQ_DTYPE_F64> {
+    typedef double S; typedef double C;
+    static __device__ double load(const S* p, int64_t i) { return p[i]; }
+    static __device__ double rn(double v) { return v; }
+    static __device__ double lo() { return 1e-10; }
+};
+
+template <typename C> __device__ __forceinline__ C wave_min(C v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) { C t = __shfl_xor(v, o, 64); v = t < v ? t : v; }
+    return v;
+}
+template <typename C> __device__ __forceinline__ C wave_max(C v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) { C t = __shfl_xor(v, o, 64); v = t > v ? t : v; }
+    return v;
+}
+__device__ __forceinline__ int wave_or(int v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v |= __shfl_xor(v, o, 64);
+    return v;
+}
+
+__device__ __forceinline__ float rnd(float v) { return __builtin_rintf(v); }
+__device__ __forceinline__ double rnd(double v) { return __builtin_rint(v); }
+
+template <typename C> __device__ __forceinline__ C clampq(C v, C lo, C hi) {   // NaN propagates
+    if (v != v) return v;
+    return v < lo ? lo : (v > hi ? hi : v);
+}
+template <typename C> __device__ __forceinline__ int32_t to_i32(C v) {         // NaN -> INT_MIN
+    return (v != v) ? INT32_MIN : (int32_t)v;
+}
+
+template <int DT>
+__global__ __launch_bounds__(256) void awq_generic_kernel(const void* __restrict__ wv, int64_t rows,
+                                                          int64_t K, int64_t L, int qmin, int qmax,
+                                                          int sym, int32_t* __restrict__ tensor_q,
+                                                          uint16_t* __restrict__ scales,
+                                                          int32_t* __restrict__ zeros) {
+    typedef Traits<DT> T;
+    typedef typename T::C C;
+    const typename T::S* w = (const typename T::S*)wv;
+    const int lane = threadIdx.x & 63;
+    const int64_t G = (K + L - 1) / L;
+    const int64_t ngroups = rows * G;
+    const int64_t wave = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int64_t nwaves = (int64_t)gridDim.x * 4;
+    for (int64_t gi = wave; gi < ngroups; gi += nwaves) {
+        const int64_t r = gi / G, g = gi - r * G;
+        const int64_t k0 = g * L;
+        int64_t k1 = k0 + L;
+        const bool padded = k1 > K;                  // awq.py:337-339 zero padding
+        if (k1 > K) k1 = K;
+        const int64_t base = r * K;
+        C mn = padded ? (C)0 : (C)INFINITY, mx = padded ? (C)0 : (C)-INFINITY;
+        int nan = 0;
+        for (int64_t k = k0 + lane; k < k1; k += 64) {
+            C v = T::load(w, base + k);
+            nan |= (v != v);
+            mn = v < mn ? v : mn;
+            mx = v > mx ? v : mx;
+        }
+        mn = wave_min(mn);
+        mx = wave_max(mx);
+        nan = wave_or(nan);
+        if (nan) { mn = (C)NAN; mx = (C)NAN; }
+        if (sym) {                                   // awq.py:196-199 (Python max)
+            C amn = mn < 0 ? -mn : mn, amx = mx < 0 ? -mx : mx;
+            if (nan) { amn = mn; amx = mx; }
+            C a = (amx > amn) ? amx : amn;
+            mn = -a;
+            mx = a;
+        }
+        C s = T::rn(T::rn(mx - mn) / (C)(qmax - qmin));          // awq.py:202
+        if (!(s != s) && s < T::lo()) s = T::lo();                 // awq.py:205
+        C z = (C)0;
+        if (!sym) {                                                // awq.py:210-211
+            C y = T::rn(mn / s);
+            z = T::rn((C)qmin - y);
+            z = clampq(T::rn(rnd(z)), (C)qmin, (C)qmax);
+        }
+        if (lane == 0) {
+            if (scales) scales[gi] = canon_f16((float)s);         // fp64: via fp32 (awq.py:327)
+            if (zeros) zeros[gi] = to_i32(z);
+        }
+        if (tensor_q) {
+            for (int64_t k = k0 + lane; k < k1; k += 64) {
+                C v = T::load(w, base + k);
+                C t = T::rn(T::rn(v / s) + z);                     // awq.py:245
+                t = clampq(T::rn(rnd(t)), (C)qmin, (C)qmax);   // awq.py:248
+                tensor_q[base + k] = to_i32(t);
+            }
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void awq_pack_kernel(const int32_t* __restrict__ v, int64_t rows,
+                                                       int64_t n, int bits, int qmin,
+                                                       int32_t* __restrict__ packed) {
+    const int per = 32 / bits;
+    const uint32_t mask = (1u << bits) - 1u;
+    const int64_t words = (n + per - 1) / per;
+    const int64_t total = rows * words;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t r = i / words, c = i - r * words;
+        uint32_t wd = 0;
+        for (int j = 0; j < per; ++j) {
+            const int64_t k = c * per + j;
+            if (k < n) wd |= (((uint32_t)v[r * n + k] - (uint32_t)qmin) & mask) << (bits * j);
+        }
+        packed[i] = (int32_t)wd;
+    }
+}
+
+// awq.py:459-539: dq = fp16(fp16(q - z) * s) stored fp32; q/z from int32 arrays or packed.
+__global__ __launch_bounds__(256) void awq_dequant_kernel(
+    const int32_t* __restrict__ tensor_q, const int32_t* __restrict__ qweight,
+    const uint16_t* __restrict__ scales, const int32_t* __restrict__ zeros,
+    const int32_t* __restrict__ qzeros, int64_t rows, int64_t K, int64_t L, int bits, int qmin,
+    float* __restrict__ out) {
+    const int64_t G = (K + L - 1) / L;
+    const int per = 32 / bits;
+    const uint32_t mask = (1u << bits) - 1u;
+    const int64_t wpr = (K + per - 1) / per, zpr = (G + per - 1) / per;
+    const int64_t total = rows * K;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t r = i / K, k = i - r * K, g = k / L;
+        int32_t q, z;
+        if (tensor_q) {
+            q = tensor_q[i];
+            z = zeros[r * G + g];
+        } else {
+            q = (int32_t)((((uint32_t)qweight[r * wpr + k / per]) >> (bits * (k % per))) & mask) + qmin;
+            z = (int32_t)((((uint32_t)qzeros[r * zpr + g / per]) >> (bits * (g % per))) & mask) + qmin;
+        }
+        const int32_t diff = (int32_t)((uint32_t)q - (uint32_t)z);
+        const float h = sw_f16_to_f32(sw_f32_to_f16((float)diff));
+        const float s = sw_f16_to_f32(scales[r * G + g]);
+        out[i] = sw_f16_to_f32(sw_f32_to_f16(h * s));
+    }
+}
+
+inline unsigned grid_for(int64_t work, int64_t per_block, int64_t cap) {
+    int64_t b = (work + per_block - 1) / per_block;
+    if (b < 1) b = 1;
+    if (b > cap) b = cap;
+    return (unsigned)b;
+}
+
+}  // namespace
+
+hipError_t launch_generic(const void* w, int dtype, int64_t rows, int64_t K, int64_t L, int bits,
+                          int symmetric, int32_t* tensor_q, uint16_t* scales, int32_t* zeros,
+                          hipStream_t stream) {
+    const int qmin = symmetric ? -(1 << (bits - 1)) : 0;
+    const int qmax = symmetric ? (1 << (bits - 1)) - 1 : (1 << bits) - 1;
+    const int64_t G = (K + L - 1) / L;
+    const unsigned grid = grid_for(rows * G, 4, 256 * 16);
+#define AWQ_GEN(D) \
+    hipLaunchKernelGGL(awq_generic_kernel<D>, dim3(grid), dim3(256), 0, stream, w, rows, K, L, qmin, \
+                       qmax, symmetric, tensor_q, scales, zeros)
+    switch (dtype) {
+    case AWQ_DTYPE_BF16: AWQ_GEN(AWQ_DTYPE_BF16); break;
+    case AWQ_DTYPE_F16: AWQ_GEN(AWQ_DTYPE_F16); break;
+    case AWQ_DTYPE_F32: AWQ_GEN(AWQ_DTYPE_F32); break;
+    case AWQ_DTYPE_F64: AWQ_GEN(AWQ_DTYPE_F64); break;
+    default: return hipErrorInvalidValue;
+    }
+#undef AWQ_GEN
+    return hipPeekAtLastError();
+}
+
+hipError_t launch_pack(const int32_t* v, int64_t rows, int64_t n, int bits, int qmin,
+                       int32_t* packed, hipStream_t stream) {
+    const int per = 32 / bits;
+    const int64_t total = rows * ((n + per - 1) / per);
+    if (total <= 0) return hipSuccess;
+    hipLaunchKernelGGL(awq_pack_kernel, dim3(grid_for(total, 256, 256 * 16)), dim3(256), 0, stream, v,
+                       rows, n, bits, qmin, packed);
+    return hipPeekAtLastError();
+}
+
+hipError_t launch_dequant(const int32_t* tensor_q, const int32_t* qweight, const uint16_t* scales,
+                          const int32_t* zeros, const int32_t* qzeros, int64_t rows, int64_t K,
+                          int64_t L, int bits, int qmin, float* out, hipStream_t stream) {
+    const int64_t total = rows * K;
+    if (total <= 0) return hipSuccess;
+    hipLaunchKernelGGL(awq_dequant_kernel, dim3(grid_for(total, 256, 256 * 16)), dim3(256), 0, stream,
+                       tensor_q, qweight, scales, zeros, qzeros, rows, K, L, bits, qmin, out);
+    return hipPeekAtLastError();
+}
+
+}  // namespace awq

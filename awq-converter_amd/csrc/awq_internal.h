@@ -1,0 +1,75 @@
+// awq_internal.h — shared host/device definitions of libawq_hip.so (gfx950 only).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/awq_hip.h"
+
+namespace awq {
+
+// ---------------------------------------------------------------------------
+// Fast-kernel tile geometry (bf16, group_size 128, K % 128 == 0).
+//
+// A tensor [R, K] is a flat sequence of R*G groups of 128 bf16 (256 B).  qzeros packs
+// C = 32/bits consecutive groups of ONE row per word, so a row has WPR = ceil(G/C)
+// words.  A wave-tile is WPT consecutive words (<= 16 groups): every qzeros word is
+// produced inside one tile, and the groups of a tile are one contiguous byte range.
+//   WPR == 1 (G <= C): WPT = 16 / G whole rows per tile
+//   else            : WPT = 16 / C words (= 16 groups when every word is full)
+// ---------------------------------------------------------------------------
+constexpr int kGroup = 128;          // elements per group on the fast path
+constexpr int kSlots = 16;           // group slots per wave-tile (4 loads x 4 lane-rows)
+constexpr int kWavesPerBlock = 4;    // 256-thread workgroups
+
+struct TensorGeom {
+    uint32_t G;    // groups per row
+    uint32_t C;    // groups per qzeros word
+    uint32_t WPR;  // qzeros words per row
+    uint32_t WPT;  // words per tile
+    uint32_t words;  // R * WPR
+};
+
+__host__ __device__ inline TensorGeom fast_geom(int64_t R, int64_t K, int bits) {
+    TensorGeom g;
+    g.G = (uint32_t)(K / kGroup);
+    g.C = 32u / (uint32_t)bits;
+    g.WPR = (g.G + g.C - 1) / g.C;
+    g.WPT = (g.WPR == 1) ? (kSlots / g.G) : (kSlots / g.C);
+    g.words = (uint32_t)R * g.WPR;
+    return g;
+}
+
+__host__ __device__ inline int64_t fast_tiles(int64_t R, int64_t K, int bits) {
+    if (R <= 0 || K <= 0) return 0;
+    TensorGeom g = fast_geom(R, K, bits);
+    return ((int64_t)g.words + g.WPT - 1) / g.WPT;
+}
+
+// first flat group of qzeros word w
+__host__ __device__ inline uint32_t word_group(const TensorGeom& g, uint32_t w) {
+    uint32_t row = w / g.WPR;
+    uint32_t wi = w - row * g.WPR;
+    return row * g.G + wi * g.C;
+}
+
+// Limits of the fast path: flat group indices must fit 32 bits.
+__host__ __device__ inline bool fast_shape_ok(int64_t R, int64_t K) {
+    if (R <= 0 || K <= 0 || (K % kGroup) != 0) return false;
+    int64_t G = K / kGroup;
+    return R * G < (int64_t)0x7FFFFFFF && R * (G + 1) < (int64_t)0x7FFFFFFF;
+}
+
+// launchers (awq_fast.hip / awq_generic.hip)
+hipError_t launch_fast(const awq_tensor_desc* descs_dev, const awq_tensor_desc* single, int n,
+                       int64_t total_tiles, int bits, int symmetric, hipStream_t stream);
+hipError_t launch_generic(const void* w, int dtype, int64_t rows, int64_t K, int64_t L, int bits,
+                          int symmetric, int32_t* tensor_q, uint16_t* scales, int32_t* zeros,
+                          hipStream_t stream);
+hipError_t launch_pack(const int32_t* v, int64_t rows, int64_t n, int bits, int qmin,
+                       int32_t* packed, hipStream_t stream);
+hipError_t launch_dequant(const int32_t* tensor_q, const int32_t* qweight, const uint16_t* scales,
+                          const int32_t* zeros, const int32_t* qzeros, int64_t rows, int64_t K,
+                          int64_t L, int bits, int qmin, float* out, hipStream_t stream);
+
+}  // namespace awq

@@ -1,0 +1,215 @@
+#!/usr/bin/env python3
+"""Throughput bench of the AWQ group-quantize hot path on MI355X.
+
+Metric (BASELINE.json): bf16 GB quantized/sec at group_size=128 (input bytes, 2 B/elem),
+plus the HBM-roofline fraction of the quantize+pack kernel.
+
+A *step* = one ragged launch of the streaming kernel over a whole synthetic tensor set
+with the exact shapes of the named model, bits=4, group_size=128,
+asymmetric (the CLI default, reference main.py:59-63), outputs = packed qweight/qzeros +
+fp16 scales, inputs resident in HBM.  Multi-GPU: one process per GPU (torchrun); every
+rank quantizes its own replica of the tensor set (weak scaling, no data-path collective:
+tensors are independent).  value = all ranks' input bytes / max-over-ranks time.
+
+Usage: python bench.py [--gpus N --steps K --warmup W --workload opt-125m]
+       N>1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+for _p in (ROOT, os.path.join(ROOT, "awq-converter_amd")):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+import torch  # noqa: E402
+
+METRIC = "bf16 GB quantized/sec at group_size=128, 1/2/4/8 MI355X; % HBM roofline"
+HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec peak (MI355X_MICROARCH.md); 6.29 TB/s measured copy
+
+# Shape manifests (every float tensor with numel >= 128 = the
+# reference CLI's filter, main.py:244-253).
+WORKLOADS = {
+    "c1": [((1024, 4096), 1)],
+    "opt-125m": [((768,), 110), ((768, 768), 48), ((3072, 768), 12), ((3072,), 12), ((768, 3072), 12),
+                 ((50272, 768), 1), ((2050, 768), 1)],
+    "opt-350m": [((1024,), 216), ((1024, 1024), 96), ((4096, 1024), 24), ((4096,), 24), ((1024, 4096), 24),
+                 ((50272, 512), 1), ((2050, 1024), 1), ((512, 1024), 1), ((1024, 512), 1)],
+    "llama3-8b": [((4096,), 65), ((4096, 4096), 64), ((1024, 4096), 64), ((14336, 4096), 64),
+                  ((4096, 14336), 32), ((128256, 4096), 2)],
+    "llama3-70b": [((8192,), 161), ((8192, 8192), 160), ((1024, 8192), 160), ((28672, 8192), 160),
+                   ((8192, 28672), 80), ((128256, 8192), 2)],
+}
+DESCR = {"c1": "single 1024x4096 linear", "opt-125m": "facebook/opt-125m tensor set (196 tensors, 125.24M params)",
+         "opt-350m": "facebook/opt-350m tensor set (388 tensors, 331.2M params)",
+         "llama3-8b": "Llama-3-8B tensor set (291 tensors, 8.03B params)",
+         "llama3-70b": "Llama-3-70B tensor set (723 tensors, 70.55B params)"}
+
+
+def shapes_of(workload):
+    out = []
+    for shape, count in WORKLOADS[workload]:
+        out += [shape] * count
+    # processing order of the reference CLI: bytes descending, stable (main.py:259)
+    return sorted(out, key=lambda s: -int(torch.Size(s).numel()))
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--workload", default="opt-125m", choices=sorted(WORKLOADS))
+    ap.add_argument("--bits", type=int, default=4, choices=[4, 8])
+    ap.add_argument("--symmetric", action="store_true")
+    ap.add_argument("--parity", action="store_true", help="also write unpacked int32 tensor_q/zero_points")
+    ap.add_argument("--replicas", type=int, default=0,
+                    help="input replicas rotated across steps (0 = enough to exceed the 256 MiB Infinity Cache)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-sample-seconds", type=float, default=15.0)
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
+    return ap.parse_args()
+
+
+def make_set(shapes, seed0, dev):
+    g = torch.Generator(device=dev)
+    tensors = {}
+    for i, s in enumerate(shapes):
+        g.manual_seed(seed0 + i)
+        tensors[f"t{i:04d}"] = (torch.randn(*s, generator=g, device=dev, dtype=torch.float32) * 0.02).to(torch.bfloat16)
+    return tensors
+
+
+def cpu_baseline(shapes, budget_s):
+    """The oracle (oracle/awq_oracle.c, single thread) on a bounded sample of the SAME
+    workload: whole tensors in processing order, then rows of the next one, until about
+    budget_s of CPU work.  Returns GB/s of bf16 input."""
+    from oracle import awq_oracle as orc
+    orc.lib()
+    g = torch.Generator().manual_seed(1234)
+    done_bytes, t_total, parts = 0, 0.0, []
+    for s in shapes:
+        rows = 1 if len(s) == 1 else s[0]
+        K = int(torch.Size(s).numel()) // rows
+        # time one row-block first to size the sample
+        take = rows
+        est = 3e-8 * rows * K
+        remaining = budget_s - t_total
+        if remaining <= 0.2:
+            break
+        if est > remaining:
+            take = max(1, int(rows * remaining / est))
+        x = (torch.randn(take, K, generator=g) * 0.02).to(torch.bfloat16)
+        t0 = time.perf_counter()
+        orc.quantize_groups(x, take, K, 128, 4, False)
+        t_total += time.perf_counter() - t0
+        done_bytes += x.numel() * 2
+        parts.append(f"{take}x{K}")
+    return done_bytes / t_total / 1e9, t_total, done_bytes, len(parts)
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    from awq_quantizer import _hip
+    from awq_quantizer.quantization.batch import PackedBatch
+    _hip.require_device(dev)
+
+    shapes = shapes_of(args.workload)
+    elems = sum(int(torch.Size(s).numel()) for s in shapes)
+    in_bytes = elems * 2
+    reps = args.replicas or max(1, -(-(1 << 30) // in_bytes))   # >= 1 GiB of inputs in rotation
+    batches = []
+    for r in range(reps):
+        seed0 = (rank * 64 + r) * 100003
+        inputs = make_set(shapes, seed0, dev)
+        batches.append(PackedBatch(inputs, bits=args.bits, symmetric=args.symmetric, parity=args.parity))
+    torch.cuda.synchronize()
+    algo_bytes = batches[0].algorithmic_bytes()
+
+    def barrier():
+        if world > 1:
+            import torch.distributed as dist
+            dist.barrier()
+
+    stream = torch.cuda.current_stream(dev)
+    for i in range(args.warmup):
+        batches[i % reps].run(stream)
+    torch.cuda.synchronize()
+
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        ev[i][0].record(stream)
+        batches[i % reps].run(stream)
+        ev[i][1].record(stream)
+    torch.cuda.synchronize()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    kern_ms = [a.elapsed_time(b) for a, b in ev]
+    kern_avg_s = sum(kern_ms) / len(kern_ms) / 1e3
+
+    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if world > 1:
+        import torch.distributed as dist
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = float(t.item())
+
+    if rank != 0:
+        if world > 1:
+            import torch.distributed as dist
+            dist.destroy_process_group()
+        return
+
+    value = in_bytes * world * args.steps / elapsed / 1e9
+    achieved = algo_bytes / kern_avg_s / 1e9
+    traffic = None
+    try:
+        with open(args.traffic_json) as f:
+            tj = json.load(f)
+        key = f"{args.workload}.b{args.bits}.{'sym' if args.symmetric else 'asym'}.{'parity' if args.parity else 'packed'}"
+        traffic = tj.get(key, {}).get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        pass
+    line = {
+        "metric": METRIC, "value": round(value, 3), "unit": "GB/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "bf16", "data": "synthetic",
+        "config": {"workload": f"{args.workload}: {DESCR[args.workload]}", "tensors": len(shapes),
+                   "elements": elems, "group_size": 128, "bits": args.bits, "symmetric": args.symmetric,
+                   "outputs": "qweight+qzeros+fp16 scales" + (" + int32 tensor_q/zero_points" if args.parity else ""),
+                   "launches_per_step": 1, "input_replicas_rotated": reps,
+                   "parallelism": f"dp{world} (each rank quantizes its own replica of the tensor set)"},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                     "algorithmic_bytes_per_launch": algo_bytes,
+                     "kernel_avg_us": round(kern_avg_s * 1e6, 2)},
+    }
+    if not args.no_cpu_baseline:
+        gbs, secs, nbytes, nparts = cpu_baseline(shapes, args.cpu_sample_seconds)
+        line["cpu_baseline"] = {"value": round(gbs, 5), "unit": "GB/s", "cores": 1, "kind": "port",
+                                "sample": f"oracle/awq_oracle.c on {nbytes / 1e6:.1f} MB of the {args.workload} "
+                                          f"set ({nparts} tensors/row-blocks in processing order, {secs:.1f} s, "
+                                          f"1 thread); reference awq.py itself: 4.6 MB/s on 1 core (BASELINE.md)"}
+    print(json.dumps(line), flush=True)
+    if world > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

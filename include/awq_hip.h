@@ -1,0 +1,115 @@
+/*
+ * awq_hip.h — C ABI of libawq_hip.so, the MI355X (gfx950) group quantizer.
+ *
+ * The reference (shanefitch/AWQ-Converter) has no FFI: its hot path is the Python
+ * method AWQQuantizer._quantize_per_group (src/awq_quantizer/quantization/awq.py:286-374),
+ * reached from AWQQuantizer.quantize (awq.py:376-433) and from the CLI's
+ * quantize_tensor_batch (src/awq_quantizer/main.py:374).  These entry points replace
+ * that method's arithmetic; the drop-in Python class (awq-converter_amd/awq_quantizer/
+ * quantization/awq.py) binds them with ctypes.  See INTEGRATION.md.
+ *
+ * Conventions (all entry points):
+ *   - plain pointers and sizes; every pointer argument is DEVICE memory allocated by the
+ *     caller unless stated otherwise; the library never allocates or frees device memory
+ *     and keeps no global mutable state (re-entrant; one stream per call);
+ *   - `stream` is a hipStream_t (NULL = legacy default stream); launches are asynchronous
+ *     on that stream, nothing synchronises;
+ *   - return 0 on success, an AWQ_E* code otherwise; awq_last_error() (thread-local)
+ *     then holds a message.  Invalid arguments are reported before anything is launched.
+ *
+ * Layout: the input is [rows, K] row-major (the reference's dim 0 = rows, remaining dims
+ * flattened = K, awq.py:306-320).  Groups are `group_size` consecutive elements along K;
+ * a tail group shorter than group_size is zero-padded for its min/max (awq.py:337-339).
+ * G = ceil(K / group_size).
+ *
+ * Outputs (each may be NULL when not wanted; at least one must be non-NULL):
+ *   scales    fp16 bits [rows, G]            (awq.py:411, value = fp16(scale))
+ *   zeros     int32     [rows, G]            (awq.py:412, reference zero_points)
+ *   tensor_q  int32     [rows, K]            (awq.py:410, reference tensor_q)
+ *   qweight   int32     [rows, ceil(K*bits/32)]  packed: element k of a row sits in word
+ *             k/(32/bits), bits [bits*(k%(32/bits)), +bits), value (q - qmin) & (2^bits-1)
+ *   qzeros    int32     [rows, ceil(G*bits/32)]  same packing of the zero points
+ * NaN groups/elements follow the reference: int32 outputs are INT32_MIN (x86 cvtt), packed
+ * fields hold (INT32_MIN - qmin) & mask, NaN scales are 0x7E00.
+ */
+#ifndef AWQ_HIP_H
+#define AWQ_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define AWQ_HIP_ABI_VERSION 1
+
+/* dtype codes of the input weights (torch dtypes the reference accepts, awq.py:397) */
+enum { AWQ_DTYPE_BF16 = 0, AWQ_DTYPE_F16 = 1, AWQ_DTYPE_F32 = 2, AWQ_DTYPE_F64 = 3 };
+
+/* status codes */
+enum { AWQ_OK = 0, AWQ_EINVAL = 1, AWQ_EUNSUPPORTED = 2, AWQ_EHIP = 3, AWQ_ENODEV = 4 };
+
+/* One tensor of a ragged (multi-tensor) launch.  Same meaning as the awq_quantize_groups
+ * arguments.  tile_begin / tile_count are filled by awq_plan_ragged. */
+typedef struct awq_tensor_desc {
+    const void* w;
+    int64_t rows;
+    int64_t K;
+    int32_t* qweight;
+    int32_t* qzeros;
+    uint16_t* scales;
+    int32_t* tensor_q;
+    int32_t* zeros;
+    int64_t tile_begin;
+    int64_t tile_count;
+} awq_tensor_desc;
+
+/* ABI version (AWQ_HIP_ABI_VERSION). */
+int awq_abi_version(void);
+
+/* Message of the last failing call on this thread ("" if none). */
+const char* awq_last_error(void);
+
+/* AWQ_OK if the current HIP device is a gfx950 (MI355X), AWQ_ENODEV otherwise.
+ * Host-only query; writes the device's gcnArchName into arch (if arch != NULL, len > 0). */
+int awq_device_check(char* arch, int len);
+
+/* Quantize one [rows, K] tensor (replaces awq.py:286-374 incl. the small-tensor
+ * path awq.py:130-171, which a caller expresses as group_size = K).
+ * bits in {4, 8}; symmetric selects qmin/qmax per awq.py:114-128.
+ * bf16 with group_size == 128 and K % 128 == 0 takes the streaming fast kernel; every
+ * other shape/dtype takes the generic kernel (same results). */
+int awq_quantize_groups(const void* w, int dtype, int64_t rows, int64_t K, int64_t group_size,
+                        int bits, int symmetric, int32_t* qweight, int32_t* qzeros,
+                        uint16_t* scales, int32_t* tensor_q, int32_t* zeros, void* stream);
+
+/* True (1) if a tensor of this dtype/shape is eligible for awq_quantize_ragged. */
+int awq_ragged_eligible(int dtype, int64_t rows, int64_t K, int64_t group_size);
+
+/* HOST helper: fills descs[i].tile_begin / tile_count (host array) for a ragged launch
+ * and returns the total tile count (< 0 on error).  All tensors must be eligible. */
+int64_t awq_plan_ragged(awq_tensor_desc* descs_host, int n, int bits);
+
+/* Quantize n eligible tensors in ONE launch.  descs_device: device copy of the array
+ * planned by awq_plan_ragged (the caller uploads it; it can be reused across calls). */
+int awq_quantize_ragged(const awq_tensor_desc* descs_device, int n, int64_t total_tiles,
+                        int bits, int symmetric, void* stream);
+
+/* Reference dequantize (awq.py:459-539): out fp32 [rows, K] =
+ * fp16( fp16(tensor_q - zeros) * scales ) per element. */
+int awq_dequantize(const int32_t* tensor_q, const uint16_t* scales, const int32_t* zeros,
+                   int64_t rows, int64_t K, int64_t group_size, float* out, void* stream);
+
+/* Same from the packed outputs (qweight/qzeros/scales) of the same bits/symmetric. */
+int awq_dequantize_packed(const int32_t* qweight, const int32_t* qzeros, const uint16_t* scales,
+                          int64_t rows, int64_t K, int64_t group_size, int bits, int symmetric,
+                          float* out, void* stream);
+
+/* Pack int32 values [rows, n] into [rows, ceil(n*bits/32)] words ((v - qmin) & mask). */
+int awq_pack_rows(const int32_t* v, int64_t rows, int64_t n, int bits, int qmin, int32_t* packed,
+                  void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* AWQ_HIP_H */

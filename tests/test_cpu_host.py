@@ -1,0 +1,115 @@
+"""CPU-only tests: the C-ABI library loads and exports every declared symbol, and the
+drop-in host layer keeps the reference's interface (validation, defaults, errors,
+skip semantics) — no kernel is launched here."""
+import ctypes
+import os
+import re
+
+import pytest
+import torch
+
+import golden_io as gio
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def declared_symbols():
+    with open(os.path.join(ROOT, "include", "awq_hip.h")) as f:
+        src = f.read()
+    return sorted(set(re.findall(r"^\s*(?:int|int64_t|const char\*)\s+(awq_\w+)\s*\(", src, re.M)))
+
+
+def test_library_exports_every_declared_symbol():
+    from awq_quantizer import _hip
+    lib = _hip.load_library()
+    syms = declared_symbols()
+    assert len(syms) >= 10
+    for s in syms:
+        assert hasattr(lib, s), s
+    assert set(syms) == set(_hip.SIGNATURES), "python binding out of sync with include/awq_hip.h"
+    assert lib.awq_abi_version() == 1
+
+
+def test_library_is_gfx950_code_object():
+    from awq_quantizer import _hip
+    data = open(_hip.LIB_PATH, "rb").read()
+    assert b"gfx950" in data
+
+
+def test_host_helpers_without_gpu():
+    from awq_quantizer import _hip
+    lib = _hip.load_library()
+    assert lib.awq_ragged_eligible(0, 1024, 4096, 128) == 1
+    assert lib.awq_ragged_eligible(0, 1024, 4000, 128) == 0
+    assert lib.awq_ragged_eligible(1, 1024, 4096, 128) == 0
+    d = [_hip.TensorDesc(4096 * 16, 1024, 4096, 0, 0, 2 * 4096, 0, 0, 0, 0),
+         _hip.TensorDesc(4096 * 32, 1, 768, 0, 0, 2 * 8192, 0, 0, 0, 0),
+         _hip.TensorDesc(4096 * 48, 50, 768, 0, 0, 2 * 16384, 0, 0, 0, 0)]
+    total = _hip.plan_ragged(d, 4)
+    # 1024 rows x G=32 -> 4 words/row -> 2048 tiles; G=6 -> 1 word/row, 2 rows/tile
+    assert d[0].tile_count == 2048 and d[1].tile_count == 1 and d[2].tile_count == 25
+    assert total == 2048 + 1 + 25 and d[2].tile_begin == 2049
+    # validation errors come back with a message, nothing launched
+    assert lib.awq_quantize_groups(None, 0, 4, 256, 128, 3, 0, None, None, None, None, None, None) != 0
+    assert "bit width" in _hip.last_error()
+    assert lib.awq_quantize_groups(None, 0, 4, 256, 0, 4, 0, None, None, None, None, None, None) != 0
+    assert "Group size" in _hip.last_error()
+
+
+@pytest.mark.parametrize("rec", gio.manifest()["validation"], ids=lambda r: str(r.get("params", r.get("quantize_arg"))))
+def test_validation_matches_reference(rec):
+    from awq_quantizer.quantization import AWQQuantizer
+    if "params" in rec:
+        with pytest.raises(ValueError) as e:
+            AWQQuantizer(device="cpu", logger_level="ERROR", **rec["params"])
+        assert str(e.value) == rec["message"]
+    else:
+        q = AWQQuantizer(device="cpu", logger_level="ERROR")
+        arg = [1.0, 2.0] if rec["quantize_arg"] == "list" else torch.arange(256, dtype=torch.int32)
+        with pytest.raises(ValueError) as e:
+            q.quantize(arg)
+        assert str(e.value) == rec["message"]
+
+
+def test_defaults_and_ranges():
+    from awq_quantizer.quantization import AWQQuantizer
+    q = AWQQuantizer(logger_level="ERROR")
+    assert (q.bits, q.group_size, q.symmetric, q.zero_point, q.scale_method, q.per_channel) == \
+        (4, 128, True, "minmax", "mse", True)
+    assert (q.qmin, q.qmax) == (-8, 7)
+    assert AWQQuantizer(symmetric=False, logger_level="ERROR")._calculate_qmin_qmax() == (0, 15)
+    assert AWQQuantizer(bits=8, symmetric=False, logger_level="ERROR")._calculate_qmin_qmax() == (0, 255)
+    assert AWQQuantizer(bits=8, logger_level="ERROR")._calculate_qmin_qmax() == (-128, 127)
+    if not torch.cuda.is_available():
+        assert q.device == "cpu"
+        assert AWQQuantizer(device="cuda:3", logger_level="ERROR").device == "cpu"
+
+
+@pytest.mark.skipif(torch.cuda.is_available(), reason="checks the no-GPU behaviour")
+def test_no_cpu_fallback():
+    from awq_quantizer import _hip
+    from awq_quantizer.quantization import AWQQuantizer
+    q = AWQQuantizer(device="cpu", logger_level="ERROR")
+    with pytest.raises(_hip.HipUnavailable):
+        q.quantize(torch.randn(4, 256, dtype=torch.bfloat16))
+    # quantize_model keeps the reference's skip-and-log behaviour: nothing quantized
+    assert q.quantize_model({"a": torch.randn(4, 256, dtype=torch.bfloat16)}) == {}
+
+
+def test_small_and_empty_errors_before_device():
+    from awq_quantizer.quantization import AWQQuantizer
+    q = AWQQuantizer(device="cpu", logger_level="ERROR")
+    with pytest.raises(RuntimeError):
+        q.quantize(torch.zeros(0, dtype=torch.bfloat16))
+    with pytest.raises(TypeError):
+        AWQQuantizer(device="cpu", zero_point="percentile", logger_level="ERROR").quantize(
+            torch.randn(4, 256, dtype=torch.bfloat16))
+
+
+def test_packed_shapes():
+    from awq_quantizer.quantization import AWQQuantizer
+    q = AWQQuantizer(bits=4, logger_level="ERROR")
+    sh = q.packed_shapes((4096, 14336))
+    assert sh["qweight"] == (4096, 1792) and sh["qzeros"] == (4096, 14) and sh["scales"] == (4096, 112)
+    sh = AWQQuantizer(bits=8, logger_level="ERROR").packed_shapes((768,))
+    assert sh["qweight"] == (1, 192) and sh["qzeros"] == (1, 2) and sh["scales"] == (1, 6)

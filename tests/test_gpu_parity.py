@@ -1,0 +1,224 @@
+"""Parity of the HIP path (libawq_hip.so via the drop-in AWQQuantizer) with the oracle
+and the reference's golden outputs.  Needs a gfx950 GPU: `pytest -m gpu`.
+
+Bar: bit-exact int32 tensor_q / zero_points, fp16 scales (NaN payload excepted), fp32
+dequantize; packed qweight/qzeros equal the oracle's packing of the oracle's values.
+"""
+import os
+
+import pytest
+import torch
+
+import golden_io as gio
+from oracle import awq_oracle as orc
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from awq_quantizer import _hip
+    _hip.require_device(torch.device("cuda", 0))   # raises unless gfx950 + library present
+
+
+def Q(**kw):
+    from awq_quantizer.quantization import AWQQuantizer
+    kw.setdefault("device", DEV)
+    return AWQQuantizer(logger_level="ERROR", **kw)
+
+
+def rand_bf16(shape, seed, scale=1.0, dtype=torch.bfloat16):
+    g = torch.Generator().manual_seed(seed)
+    return (torch.randn(*shape, generator=g) * scale).to(dtype)
+
+
+# ---------------------------------------------------------------- golden fixtures
+@pytest.mark.parametrize("case", gio.ok_cases(), ids=lambda c: c["name"])
+def test_golden_case(case):
+    x = gio.case_input(case)
+    p = dict(case["params"])
+    res = Q(**p).quantize(x)
+    T = gio.tensors()
+    name = case["name"]
+    assert torch.equal(res["tensor_q"], T[name + ".tensor_q"])
+    assert torch.equal(res["zero_points"], T[name + ".zero_points"])
+    assert gio.same_bits_nan_eq(res["scales"], T[name + ".scales"])
+    assert res["tensor_q"].dtype == torch.int32 and res["scales"].dtype == torch.float16
+    if name + ".dq" in T:
+        dq = Q(**p).dequantize(res)
+        assert gio.same_bits_nan_eq(dq, T[name + ".dq"])
+    elif case.get("dequantize") == "IndexError":
+        with pytest.raises(IndexError):
+            Q(**p).dequantize(res)
+
+
+@pytest.mark.parametrize("rec", gio.manifest()["hashed"], ids=lambda r: r["name"])
+def test_golden_hashed(rec):
+    x = gio.hashed_input(rec)
+    assert gio.sha(x) == rec["sha_x"]
+    q = Q(**rec["params"])
+    res = q.quantize(x)
+    assert gio.sha(res["tensor_q"]) == rec["sha_tensor_q"]
+    assert gio.sha(res["scales"]) == rec["sha_scales"]
+    assert gio.sha(res["zero_points"]) == rec["sha_zero_points"]
+    assert gio.sha(q.dequantize(res)) == rec["sha_dq"]
+
+
+def test_percentile_mode_raises_like_reference():
+    with pytest.raises(TypeError):
+        Q(zero_point="percentile").quantize(rand_bf16((4, 256), 0))
+    assert Q(zero_point="percentile").quantize_model({"a": rand_bf16((4, 256), 0)}) == {}
+
+
+def test_quantize_model_skip_semantics():
+    m = {"w": rand_bf16((8, 256), 30), "i": torch.arange(256, dtype=torch.int32),
+         "s": rand_bf16((10, 10), 31), "e": torch.zeros(0, dtype=torch.bfloat16), "b": rand_bf16((256,), 32)}
+    out = Q(symmetric=False).quantize_model(m)
+    assert sorted(out) == gio.manifest()["quantize_model"]["asym"]
+
+
+# ---------------------------------------------------------------- oracle, random shapes
+FAST_SHAPES = [(1024, 4096), (4096, 768), (768,), (3072,), (7, 1792), (3, 1280), (5, 384), (9, 128),
+               (33, 11 * 128), (2, 8, 256), (64, 14336), (1, 65536)]
+
+
+@pytest.mark.parametrize("bits", [4, 8])
+@pytest.mark.parametrize("sym", [False, True])
+@pytest.mark.parametrize("shape", FAST_SHAPES, ids=str)
+def test_fast_path_vs_oracle(shape, sym, bits):
+    x = rand_bf16(shape, hash((shape, sym, bits)) & 0xFFFF, 0.02)
+    ref = orc.quantize(x, bits=bits, group_size=128, symmetric=sym)
+    q = Q(bits=bits, symmetric=sym)
+    res = q.quantize(x)
+    assert torch.equal(res["tensor_q"], ref["tensor_q"])
+    assert torch.equal(res["zero_points"], ref["zero_points"])
+    assert gio.same_bits_nan_eq(res["scales"], ref["scales"])
+    pk = q.quantize_packed(x)
+    qmin = q.qmin
+    assert torch.equal(pk["qweight"].cpu(), orc.pack_rows(ref["tensor_q"], bits, qmin))
+    zz = ref["zero_points"]
+    assert torch.equal(pk["qzeros"].cpu(), orc.pack_rows(zz, bits, qmin))
+    assert gio.same_bits_nan_eq(pk["scales"].cpu(), ref["scales"])
+    dq_packed = q.dequantize_packed(pk).cpu()
+    assert gio.same_bits_nan_eq(dq_packed, orc.dequantize(ref))
+
+
+def special_tensor(shape, seed):
+    """bf16 with NaN, +-inf, huge, subnormal and constant groups sprinkled in."""
+    x = rand_bf16(shape, seed, 1.0).float()
+    flat = x.view(-1)
+    g = torch.Generator().manual_seed(seed + 1)
+    n = flat.numel()
+    idx = torch.randperm(n, generator=g)[: max(8, n // 500)]
+    kinds = [float("nan"), float("inf"), float("-inf"), 3e38, -3e38, 1e-39, 0.0, -0.0]
+    for i, j in enumerate(idx.tolist()):
+        flat[j] = kinds[i % len(kinds)]
+    x[0, :128] = 0.0                        # all-zero group
+    x[min(1, shape[0] - 1), 128:256] = 1e-6  # constant tiny group
+    return x.to(torch.bfloat16)
+
+
+@pytest.mark.parametrize("bits", [4, 8])
+@pytest.mark.parametrize("sym", [False, True])
+def test_fast_path_special_values(sym, bits):
+    x = special_tensor((64, 1024), 7 + bits + sym)
+    ref = orc.quantize(x, bits=bits, group_size=128, symmetric=sym)
+    q = Q(bits=bits, symmetric=sym)
+    res = q.quantize(x)
+    assert torch.equal(res["tensor_q"], ref["tensor_q"])
+    assert torch.equal(res["zero_points"], ref["zero_points"])
+    assert gio.same_bits_nan_eq(res["scales"], ref["scales"])
+    pk = q.quantize_packed(x)
+    assert torch.equal(pk["qweight"].cpu(), orc.pack_rows(ref["tensor_q"], bits, q.qmin))
+    assert torch.equal(pk["qzeros"].cpu(), orc.pack_rows(ref["zero_points"], bits, q.qmin))
+
+
+GENERIC = [(torch.float16, (33, 300), 128), (torch.float32, (17, 1000), 64), (torch.float64, (5, 777), 100),
+           (torch.bfloat16, (12, 4000), 256), (torch.bfloat16, (12, 300), 128), (torch.float16, (256, 4096), 128),
+           (torch.bfloat16, (3, 2, 50), 32), (torch.float32, (1, 5000), 1000)]
+
+
+@pytest.mark.parametrize("dtype,shape,gs", GENERIC, ids=str)
+@pytest.mark.parametrize("sym", [False, True])
+def test_generic_path_vs_oracle(dtype, shape, gs, sym):
+    x = rand_bf16(shape, 99, 0.5, dtype)
+    ref = orc.quantize(x, bits=4, group_size=gs, symmetric=sym)
+    q = Q(bits=4, group_size=gs, symmetric=sym)
+    res = q.quantize(x)
+    assert torch.equal(res["tensor_q"], ref["tensor_q"])
+    assert torch.equal(res["zero_points"], ref["zero_points"])
+    assert gio.same_bits_nan_eq(res["scales"], ref["scales"])
+    pk = q.quantize_packed(x)
+    assert torch.equal(pk["qweight"].cpu(), orc.pack_rows(ref["tensor_q"], 4, q.qmin))
+    assert torch.equal(pk["qzeros"].cpu(), orc.pack_rows(ref["zero_points"], 4, q.qmin))
+
+
+# ---------------------------------------------------------------- ragged launch
+def test_ragged_batch_matches_single_and_oracle():
+    from awq_quantizer.quantization.batch import PackedBatch
+    shapes = [(768,)] * 5 + [(768, 768), (3072, 768), (768, 3072), (2050, 768), (3072,), (128,), (9, 1792),
+                             (4, 128), (1, 640)]
+    dev = torch.device(DEV, 0)
+    inputs = {f"t{i}": rand_bf16(s, 200 + i, 0.02).to(dev) for i, s in enumerate(shapes)}
+    for bits in (4, 8):
+        for sym in (False, True):
+            b = PackedBatch(inputs, bits=bits, symmetric=sym, parity=True)
+            b.run()
+            torch.cuda.synchronize()
+            q = Q(bits=bits, symmetric=sym)
+            for name, res in b.results().items():
+                x = inputs[name].cpu()
+                ref = orc.quantize(x, bits=bits, group_size=128, symmetric=sym)
+                assert torch.equal(res["tensor_q"].cpu(), ref["tensor_q"]), name
+                assert torch.equal(res["zero_points"].cpu(), ref["zero_points"]), name
+                assert gio.same_bits_nan_eq(res["scales"].cpu(), ref["scales"]), name
+                assert torch.equal(res["qweight"].cpu(), orc.pack_rows(ref["tensor_q"], bits, q.qmin)), name
+                assert torch.equal(res["qzeros"].cpu(), orc.pack_rows(ref["zero_points"], bits, q.qmin)), name
+
+
+def test_ragged_rerun_idempotent():
+    from awq_quantizer.quantization.batch import PackedBatch
+    dev = torch.device(DEV, 0)
+    inputs = {f"t{i}": rand_bf16(s, 300 + i).to(dev) for i, s in enumerate([(1024, 4096), (4096,), (50, 768)])}
+    b = PackedBatch(inputs, bits=4, symmetric=False)
+    b.run()
+    first = {k: {kk: vv.clone() for kk, vv in v.items()} for k, v in b.out.items()}
+    for _ in range(3):
+        b.run()
+    torch.cuda.synchronize()
+    for k, v in b.out.items():
+        for kk, vv in v.items():
+            assert torch.equal(vv, first[k][kk])
+
+
+# ---------------------------------------------------------------- full-size properties
+@pytest.mark.parametrize("shape", [(14336, 4096), (4096, 14336), (128256, 4096)], ids=str)
+def test_full_size_properties(shape):
+    """BASELINE-size tensors (Llama-3-8B MLP / embedding): single launch == ragged launch
+    bitwise; dequantized error <= s/2 per element (RTN bound) except clamped extremes;
+    a row sample matches the oracle bit for bit."""
+    from awq_quantizer.quantization.batch import PackedBatch
+    dev = torch.device(DEV, 0)
+    g = torch.Generator(device=dev).manual_seed(5)
+    x = (torch.randn(*shape, generator=g, device=dev) * 0.02).to(torch.bfloat16)
+    q = Q(bits=4, symmetric=False)
+    pk = q.quantize_packed(x)
+    b = PackedBatch({"x": x}, bits=4, symmetric=False)
+    b.run()
+    torch.cuda.synchronize()
+    assert torch.equal(b.out["x"]["qweight"], pk["qweight"])
+    assert torch.equal(b.out["x"]["qzeros"], pk["qzeros"])
+    assert torch.equal(b.out["x"]["scales"], pk["scales"])
+    dq = q.dequantize_packed(pk)
+    s = pk["scales"].float().repeat_interleave(128, dim=1)
+    err = (dq - x.float()).abs()
+    assert bool((err <= s * 0.6 + 1e-6).all())   # RTN: s/2 + bf16 rounding of x/s and x/s+z
+    rows = torch.tensor([0, 1, shape[0] // 2, shape[0] - 1])
+    xs = x[rows].cpu()
+    ref = orc.quantize(xs, bits=4, group_size=128, symmetric=False)
+    assert torch.equal(pk["qweight"][rows].cpu(), orc.pack_rows(ref["tensor_q"], 4, 0))
+    assert torch.equal(pk["scales"][rows].cpu(), ref["scales"])

@@ -1,0 +1,352 @@
+"""
+awq_quantizer command line — drop-in for the reference CLI (src/awq_quantizer/main.py).
+
+Same flags and defaults (reference main.py:22-159), same tensor filter (floating point,
+numel >= 128, main.py:244-253), same processing / output order (bytes descending,
+stable, main.py:259), same output layout (model_chunk_NNNN.pt holding nested result
+dicts + metadata.json, main.py:430-512) and exit codes (0 ok; 1 on load failure, no
+tensor quantized, or save failure).
+
+What changes underneath, MI355X-first:
+  * weights are streamed: headers are read first, then one tensor at a time is read
+    from its (memory-mapped) file by a prefetch thread while the GPU quantizes the
+    previous one (the reference loads every file whole, then copies every tensor to
+    the device eagerly, main.py:296-307);
+  * --multi_gpu / --device all really shards: the tensor list is LPT-partitioned over
+    the GPUs (the reference's own partition_tensors, main.py:395-427, which it never
+    calls; instead every device re-quantizes every tensor, main.py:596-606), one host
+    thread per GPU;
+  * the arithmetic is the HIP kernels behind include/awq_hip.h;
+  * --save_safetensors works (the reference passes nested dicts to save_file and
+    always fails, main.py:488-490): result dicts are flattened to "<name>.<field>";
+  * --output_format packed writes qweight/qzeros/scales (int4/int8 packed) instead of
+    the reference's unpacked int32 tensor_q (8x smaller on disk at 4 bits).
+"""
+
+import argparse
+import json
+import logging
+import os
+import sys
+import threading
+import time
+from collections import deque
+from concurrent.futures import ThreadPoolExecutor
+from typing import Dict, List, Optional, Tuple
+
+import torch
+
+from .model_loading import TensorInfo, load_model_from_hub
+from .quantization.awq import AWQQuantizer
+from .utils.logger import get_logger
+
+
+def build_parser() -> argparse.ArgumentParser:
+    p = argparse.ArgumentParser(description="AWQ Quantizer CLI")
+    p.add_argument("--model_id", type=str, required=True, help="Model ID on HuggingFace Hub or path to local model")
+    p.add_argument("--output_dir", type=str, required=True, help="Directory to save quantized model")
+    p.add_argument("--bits", type=int, default=4, choices=[4, 8], help="Number of bits for quantization")
+    p.add_argument("--group_size", type=int, default=128, help="Group size for quantization")
+    p.add_argument("--symmetric", action="store_true", help="Use symmetric quantization")
+    p.add_argument("--zero_point", type=str, default="minmax", choices=["none", "minmax", "percentile"],
+                   help="Zero point calibration method")
+    p.add_argument("--percentile", type=float, default=0.99, help="Percentile for zero point calibration")
+    p.add_argument("--scale_method", type=str, default="mse", choices=["minmax", "mse"],
+                   help="Scale calibration method")
+    p.add_argument("--per_channel", action="store_true", help="Use per-channel quantization")
+    p.add_argument("--device", type=str, default="cuda" if torch.cuda.is_available() else "cpu",
+                   help="Device to use for quantization (cuda, cuda:0, cuda:1, cpu, or 'all' for all GPUs)")
+    p.add_argument("--num_workers", type=int, default=4,
+                   help="Number of host threads reading weights ahead of the GPU (per GPU)")
+    p.add_argument("--max_memory", type=float, default=0.8,
+                   help="Maximum fraction of GPU memory to use (0.0-1.0)")
+    p.add_argument("--multi_gpu", action="store_true", help="Use all available GPUs for processing (overrides --device)")
+    p.add_argument("--batch_size", type=int, default=10, help="Number of tensors to process in each batch")
+    p.add_argument("--prefetch_factor", type=int, default=2,
+                   help="Batches of tensors read ahead of the GPU (higher values use more host memory)")
+    p.add_argument("--memory_efficient", action="store_true",
+                   help="Enable memory-efficient mode (release cached GPU memory after every batch)")
+    p.add_argument("--log_level", type=str, default="INFO", choices=["DEBUG", "INFO", "WARNING", "ERROR", "CRITICAL"],
+                   help="Logging level")
+    p.add_argument("--log_file", type=str, help="Log file path")
+    p.add_argument("--save_safetensors", action="store_true", help="Save in safetensors format instead of pytorch format")
+    p.add_argument("--chunk_size", type=int, default=10, help="Number of tensors to save in each chunk (for large models)")
+    # extension (not in the reference)
+    p.add_argument("--output_format", type=str, default="reference", choices=["reference", "packed"],
+                   help="reference: int32 tensor_q/zero_points + fp16 scales per tensor (reference layout); "
+                        "packed: int32 qweight/qzeros (bits-packed) + fp16 scales")
+    return p
+
+
+def parse_args(argv: Optional[List[str]] = None) -> argparse.Namespace:
+    """Command-line arguments (reference main.py:22-159)."""
+    return build_parser().parse_args(argv)
+
+
+def get_available_gpus(logger=None) -> List[str]:
+    """["cuda:0", ...] for every visible GPU (reference main.py:162-186)."""
+    if not torch.cuda.is_available():
+        if logger:
+            logger.warning("No CUDA devices available")
+        return []
+    devs = []
+    for i in range(torch.cuda.device_count()):
+        if logger:
+            logger.info(f"Found CUDA device {i}: {torch.cuda.get_device_name(i)}")
+        devs.append(f"cuda:{i}")
+    return devs
+
+
+def get_device_memory_info(device_idx: int) -> Tuple[float, float]:
+    """(total GB, free GB) of a device (reference main.py:189-213)."""
+    if not torch.cuda.is_available():
+        return 0.0, 0.0
+    try:
+        free, total = torch.cuda.mem_get_info(device_idx)
+        return total / 1024 ** 3, free / 1024 ** 3
+    except Exception:  # noqa: BLE001
+        return 0.0, 0.0
+
+
+def select_tensors(index: List[TensorInfo], logger=None) -> List[TensorInfo]:
+    """Filter + order of reference main.py:241-259, on header information only."""
+    keep = []
+    for info in index:
+        if info.dtype is None or not info.dtype.is_floating_point or info.numel == 0:
+            if logger:
+                logger.warning(f"Skipping invalid tensor: {info.name}")
+            continue
+        if info.numel < 128:
+            if logger:
+                logger.warning(f"Skipping tensor too small for grouping: {info.name}")
+            continue
+        keep.append(info)
+    keep.sort(key=lambda i: i.nbytes, reverse=True)   # stable
+    return keep
+
+
+def prepare_tensors_for_quantization(tensors: Dict[str, torch.Tensor], device: str, max_memory_fraction: float = 0.8,
+                                     batch_size: int = 10, logger=None) -> List[Dict[str, torch.Tensor]]:
+    """In-memory API of reference main.py:216-330: filtered, size-ordered batches of at most
+    batch_size tensors.  Tensors stay where they are (they are moved to the GPU one at a
+    time when quantized, not all at once)."""
+    infos = []
+    for name, t in tensors.items():
+        if not isinstance(t, torch.Tensor):
+            if logger:
+                logger.warning(f"Skipping invalid tensor: {name}")
+            continue
+        infos.append(TensorInfo(name, None, t.dtype, t.shape))
+    ordered = select_tensors(infos, logger)
+    batches, cur = [], {}
+    for info in ordered:
+        if len(cur) >= batch_size:
+            batches.append(cur)
+            cur = {}
+        cur[info.name] = tensors[info.name]
+    if cur:
+        batches.append(cur)
+    if logger:
+        logger.info(f"Created {len(batches)} batches with {sum(len(b) for b in batches)} total tensors")
+    return batches
+
+
+def partition_tensors(items, num_partitions: int):
+    """Greedy LPT by bytes (reference main.py:395-427).  `items` is a dict name->tensor or a
+    list of TensorInfo; returns num_partitions collections of the same kind."""
+    if num_partitions <= 1:
+        return [items]
+    if isinstance(items, dict):
+        sizes = [(n, t.numel() * t.element_size()) for n, t in items.items()]
+    else:
+        sizes = [(i, i.nbytes) for i in items]
+    sizes.sort(key=lambda x: x[1], reverse=True)
+    parts = [dict() if isinstance(items, dict) else [] for _ in range(num_partitions)]
+    load = [0] * num_partitions
+    for key, size in sizes:
+        k = load.index(min(load))
+        if isinstance(items, dict):
+            parts[k][key] = items[key]
+        else:
+            parts[k].append(key)
+        load[k] += size
+    return parts
+
+
+def _flatten(tensors: Dict[str, Dict[str, torch.Tensor]]) -> Dict[str, torch.Tensor]:
+    flat = {}
+    for name, d in tensors.items():
+        for k, v in d.items():
+            flat[f"{name}.{k}"] = v.contiguous()
+    return flat
+
+
+def save_model_in_chunks(tensors: Dict[str, Dict[str, torch.Tensor]], output_dir: str, chunk_size: int = 10,
+                         use_safetensors: bool = False, logger=None) -> None:
+    """model_chunk_NNNN.{pt|safetensors} + metadata.json (reference main.py:430-512)."""
+    os.makedirs(output_dir, exist_ok=True)
+    names = list(tensors)
+    num_chunks = (len(names) + chunk_size - 1) // chunk_size
+    if logger:
+        logger.info(f"Saving model in {num_chunks} chunks with {chunk_size} tensors per chunk")
+    first = next(iter(tensors.values()))
+    qparams = {k: (first[k].item() if k in first else None) for k in ("bits", "group_size", "symmetric")}
+    tensor_to_chunk = {}
+    for c in range(num_chunks):
+        chunk_names = names[c * chunk_size:(c + 1) * chunk_size]
+        chunk = {n: tensors[n] for n in chunk_names}
+        for n in chunk_names:
+            tensor_to_chunk[n] = c
+        path = os.path.join(output_dir, f"model_chunk_{c:04d}")
+        if use_safetensors:
+            from safetensors.torch import save_file
+            save_file(_flatten(chunk), path + ".safetensors")
+            if logger:
+                logger.info(f"Saved chunk {c + 1}/{num_chunks} with {len(chunk)} tensors in safetensors format")
+        else:
+            torch.save(chunk, path + ".pt")
+            if logger:
+                logger.info(f"Saved chunk {c + 1}/{num_chunks} with {len(chunk)} tensors in PyTorch format")
+    meta = {"num_chunks": num_chunks, "chunk_size": chunk_size, "tensor_to_chunk": tensor_to_chunk,
+            "format": "safetensors" if use_safetensors else "pytorch", "num_tensors": len(names),
+            "quantization_params": qparams}
+    with open(os.path.join(output_dir, "metadata.json"), "w") as f:
+        json.dump(meta, f, indent=2)
+    if logger:
+        logger.info("Saved metadata file with tensor mapping")
+
+
+def _to_cpu(d: Dict[str, torch.Tensor]) -> Dict[str, torch.Tensor]:
+    return {k: (v.cpu() if isinstance(v, torch.Tensor) else v) for k, v in d.items()}
+
+
+def quantize_stream(loader, infos: List[TensorInfo], quantizer: AWQQuantizer, device: str, readers: int,
+                    lookahead: int, packed: bool, out: Dict, lock: threading.Lock, logger,
+                    memory_efficient: bool = False) -> None:
+    """Quantize `infos` on one device: `readers` threads read tensors from disk up to
+    `lookahead` ahead of the GPU; each tensor is quantized as soon as it is read and its
+    results are copied back to host memory."""
+    if device.startswith("cuda") and torch.cuda.is_available():
+        torch.cuda.set_device(torch.device(device))
+    pending = deque()
+    it = iter(infos)
+
+    def read(info):
+        return loader.read(info)
+
+    with ThreadPoolExecutor(max_workers=max(1, readers)) as pool:
+        for info in it:
+            pending.append((info, pool.submit(read, info)))
+            if len(pending) >= max(1, lookahead):
+                break
+        while pending:
+            info, fut = pending.popleft()
+            nxt = next(it, None)
+            if nxt is not None:
+                pending.append((nxt, pool.submit(read, nxt)))
+            try:
+                t = fut.result()
+                if logger:
+                    logger.info(f"Quantizing tensor: {info.name} on {device}")
+                res = quantizer.quantize_packed(t) if packed else quantizer.quantize(t)
+                res = _to_cpu(res)
+                with lock:
+                    out[info.name] = res
+                if logger:
+                    logger.info(f"Successfully quantized tensor: {info.name} on {device}")
+            except Exception as e:  # reference: log and continue (main.py:387-390)
+                if logger:
+                    logger.error(f"Failed to quantize tensor {info.name} on {device}: {e}")
+            if memory_efficient and device.startswith("cuda"):
+                torch.cuda.empty_cache()
+
+
+def main(argv: Optional[List[str]] = None) -> int:
+    logger = None
+    try:
+        args = parse_args(argv)
+        logger = get_logger(name="awq_quantizer", level=args.log_level, to_file=args.log_file is not None,
+                            file_path=args.log_file)
+        os.makedirs(args.output_dir, exist_ok=True)
+
+        if args.multi_gpu or args.device.lower() == "all":
+            devices = get_available_gpus(logger)
+            if not devices:
+                logger.warning("No CUDA devices available, falling back to CPU")
+                devices = ["cpu"]
+            else:
+                logger.info(f"Using {len(devices)} GPU(s) for processing")
+        else:
+            devices = [args.device]
+        for d in devices:
+            if d.startswith("cuda") and torch.cuda.is_available():
+                idx = int(d.split(":")[1]) if ":" in d else 0
+                total, free = get_device_memory_info(idx)
+                logger.info(f"Using GPU {d}: {torch.cuda.get_device_name(idx)}")
+                logger.info(f"  Total memory: {total:.2f} GB")
+                logger.info(f"  Free memory: {free:.2f} GB")
+            elif d.startswith("cuda"):
+                logger.warning(f"CUDA device {d} requested but not available, falling back to CPU")
+                devices = ["cpu"]
+            elif d == "cpu":
+                logger.info("Using CPU for quantization")
+
+        logger.info(f"Loading model from {args.model_id}")
+        try:
+            loader = load_model_from_hub(args.model_id, logger_level=args.log_level)
+            index = loader.tensor_index()
+        except Exception as e:  # noqa: BLE001
+            logger.error(f"Failed to load model: {e}")
+            return 1
+
+        logger.info("Preparing tensors for quantization")
+        start = time.time()
+        ordered = select_tensors(index, logger)
+        parts = partition_tensors(ordered, len(devices))
+        quantizers = {d: AWQQuantizer(bits=args.bits, group_size=args.group_size, symmetric=args.symmetric,
+                                      zero_point=args.zero_point, percentile=args.percentile,
+                                      scale_method=args.scale_method, per_channel=args.per_channel, device=d,
+                                      logger_name=f"awq_quantizer_{d}", logger_level=args.log_level,
+                                      logger_to_file=args.log_file is not None, logger_file_path=args.log_file)
+                      for d in devices}
+        results: Dict[str, Dict[str, torch.Tensor]] = {}
+        lock = threading.Lock()
+        lookahead = max(1, args.prefetch_factor * args.batch_size)
+        packed = args.output_format == "packed"
+        threads = []
+        for d, part in zip(devices, parts):
+            logger.info(f"Processing {len(part)} tensors on {d}")
+            th = threading.Thread(target=quantize_stream, args=(loader, part, quantizers[d], d, args.num_workers,
+                                                                lookahead, packed, results, lock, logger,
+                                                                args.memory_efficient))
+            th.start()
+            threads.append(th)
+        for th in threads:
+            th.join()
+
+        quantized = {i.name: results[i.name] for i in ordered if i.name in results}   # size-descending
+        if not quantized:
+            logger.error("No tensors were successfully quantized")
+            return 1
+        logger.info(f"Successfully quantized {len(quantized)} tensors")
+        logger.info(f"Saving quantized model to {args.output_dir}")
+        try:
+            save_model_in_chunks(quantized, args.output_dir, chunk_size=args.chunk_size,
+                                 use_safetensors=args.save_safetensors, logger=logger)
+        except Exception as e:  # noqa: BLE001
+            logger.error(f"Failed to save quantized model: {e}")
+            return 1
+        logger.info(f"Quantization complete in {time.time() - start:.2f} seconds")
+        return 0
+    except SystemExit:
+        raise
+    except Exception as e:  # noqa: BLE001
+        if logger is None:
+            logging.getLogger("awq_quantizer").error(f"Error during quantization: {e}")
+        else:
+            logger.error(f"Error during quantization: {e}")
+        return 1
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -24,6 +24,8 @@
 //     range check (no per-lane masks, no OOB access, tensors > 4 GB are fine).
 // Ragged launches: one grid over the tiles of many tensors (descriptor table in HBM);
 // waves grid-stride over tiles and advance a tensor cursor monotonically.
+#include <cstdlib>
+
 #include "awq_internal.h"
 
 namespace awq {
@@ -327,7 +329,11 @@ hipError_t launch_fast(const awq_tensor_desc* descs_dev, const awq_tensor_desc* 
                        int64_t total_tiles, int bits, int symmetric, hipStream_t stream) {
     if (total_tiles <= 0) return hipSuccess;
     // grid: enough waves to keep ~8 x 16 KiB of loads in flight per CU, grid-stride beyond
-    const int64_t max_blocks = 256 * 8;
+    int64_t max_blocks = 256 * 8;
+    if (const char* e = getenv("AWQ_HIP_MAX_BLOCKS")) {   // testing: force grid-stride loops
+        long v = atol(e);
+        if (v > 0) max_blocks = v;
+    }
     int64_t blocks = (total_tiles + kWavesPerBlock - 1) / kWavesPerBlock;
     if (blocks > max_blocks) blocks = max_blocks;
     awq_tensor_desc one{};

@@ -100,6 +100,8 @@ __device__ __forceinline__ int wave_or(int v) {
     return v;
 }
 
+__device__ __forceinline__ float absv(float v) { return __builtin_fabsf(v); }
+__device__ __forceinline__ double absv(double v) { return __builtin_fabs(v); }
 __device__ __forceinline__ float rnd(float v) { return __builtin_rintf(v); }
 __device__ __forceinline__ double rnd(double v) { return __builtin_rint(v); }
 
@@ -145,7 +147,7 @@ __global__ __launch_bounds__(256) void awq_generic_kernel(const void* __restrict
         nan = wave_or(nan);
         if (nan) { mn = (C)NAN; mx = (C)NAN; }
         if (sym) {                                   // awq.py:196-199 (Python max)
-            C amn = mn < 0 ? -mn : mn, amx = mx < 0 ? -mx : mx;
+            C amn = absv(mn), amx = absv(mx);   // torch.abs(-0) = +0
             if (nan) { amn = mn; amx = mx; }
             C a = (amx > amn) ? amx : amn;
             mn = -a;

@@ -216,9 +216,34 @@ def test_full_size_properties(shape):
     dq = q.dequantize_packed(pk)
     s = pk["scales"].float().repeat_interleave(128, dim=1)
     err = (dq - x.float()).abs()
-    assert bool((err <= s * 0.6 + 1e-6).all())   # RTN: s/2 + bf16 rounding of x/s and x/s+z
+    # RTN bound of the reference arithmetic: s/2, plus the bf16 rounding of mn/s inside the
+    # zero point (z can land 0.53 away from -mn/s) and of x/s + z; measured max 0.616 s
+    assert bool((err <= s * 0.7 + 1e-6).all())
     rows = torch.tensor([0, 1, shape[0] // 2, shape[0] - 1])
     xs = x[rows].cpu()
     ref = orc.quantize(xs, bits=4, group_size=128, symmetric=False)
     assert torch.equal(pk["qweight"][rows].cpu(), orc.pack_rows(ref["tensor_q"], 4, 0))
     assert torch.equal(pk["scales"][rows].cpu(), ref["scales"])
+
+
+@pytest.mark.parametrize("blocks", ["1", "3", "8"])
+def test_grid_stride_loop(blocks, monkeypatch):
+    """Force a tiny grid (AWQ_HIP_MAX_BLOCKS) so every wave walks many tiles/tensors."""
+    from awq_quantizer.quantization.batch import PackedBatch
+    monkeypatch.setenv("AWQ_HIP_MAX_BLOCKS", blocks)
+    dev = torch.device(DEV, 0)
+    shapes = [(300, 4096), (768,), (50, 768), (7, 1792), (4096,), (33, 384)]
+    inputs = {f"t{i}": rand_bf16(s, 400 + i, 0.02).to(dev) for i, s in enumerate(shapes)}
+    b = PackedBatch(inputs, bits=4, symmetric=False, parity=True)
+    b.run()
+    torch.cuda.synchronize()
+    q = Q(bits=4, symmetric=False)
+    for name, x in inputs.items():
+        ref = orc.quantize(x.cpu(), bits=4, group_size=128, symmetric=False)
+        o = b.out[name]
+        assert torch.equal(o["tensor_q"].cpu(), ref["tensor_q"]), name
+        assert torch.equal(o["qweight"].cpu(), orc.pack_rows(ref["tensor_q"], 4, 0)), name
+        assert torch.equal(o["qzeros"].cpu(), orc.pack_rows(ref["zero_points"], 4, 0)), name
+        assert torch.equal(o["scales"].cpu(), ref["scales"]), name
+        pk = q.quantize_packed(x)        # single-tensor launch, same tiny grid
+        assert torch.equal(pk["qweight"], o["qweight"]), name

@@ -44,6 +44,7 @@ SIGNATURES = {
     "awq_dequantize": (_I32, [_P, _P, _P, _I64, _I64, _I64, _P, _P]),
     "awq_dequantize_packed": (_I32, [_P, _P, _P, _I64, _I64, _I64, _I32, _I32, _P, _P]),
     "awq_pack_rows": (_I32, [_P, _I64, _I64, _I32, _I32, _P, _P]),
+    "awq_selftest": (_I32, [_I32, _P, _P]),
 }
 
 _lib = None
@@ -168,3 +169,10 @@ def pack_rows(v, rows, n, bits, qmin, out) -> None:
     rc = load_library().awq_pack_rows(ptr(v), rows, n, bits, qmin, ptr(out),
                                       ctypes.c_void_p(stream_ptr(out.device)))
     check(rc, "awq_pack_rows")
+
+
+def selftest(which: int, device: torch.device) -> int:
+    """Run a device self-test (include/awq_hip.h awq_selftest); returns the mismatch count."""
+    out = torch.zeros(1, dtype=torch.int64, device=device)
+    check(load_library().awq_selftest(which, ptr(out), ctypes.c_void_p(stream_ptr(device))), "awq_selftest")
+    return int(out.item())

@@ -170,4 +170,11 @@ int awq_pack_rows(const int32_t* v, int64_t rows, int64_t n, int bits, int qmin,
     return hip_status(awq::launch_pack(v, rows, n, bits, qmin, packed, (hipStream_t)stream), "awq pack");
 }
 
+int awq_selftest(int which, unsigned long long* result, void* stream) {
+    g_err.clear();
+    if (!result) return fail(AWQ_EINVAL, "null result pointer");
+    if (which != 0) return fail(AWQ_EINVAL, "unknown self-test %d", which);
+    return hip_status(awq::launch_selftest(which, result, (hipStream_t)stream), "awq selftest");
+}
+
 }  // extern "C"

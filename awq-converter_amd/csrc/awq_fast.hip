@@ -7,26 +7,39 @@
 // tensor_q / zero_points).
 //
 // Mapping (HBM-bound, no MFMA):
-//   * one group = 128 bf16 = 256 B = 16 lanes x one 16-B buffer_load_dwordx4;
-//     a wave covers 4 groups per load, 4 loads in flight per lane = one 16-group tile;
+//   * one group = 128 bf16 = 256 B = 16 lanes x one 16-B buffer_load_dwordx4; a wave
+//     covers 4 groups per load and 4 loads (16 groups, 4 KiB) per tile; the next tile's
+//     loads are in flight while the current one is computed (register double buffer);
 //   * per-group min/max in the integer domain: bf16 bits -> order-preserving int16 key
-//     (v_bitop3), v_pk_max_i16/v_pk_min_i16, then max/~min packed in one dword and reduced
-//     across the 16-lane DPP row (quad_perm, row_half_mirror, row_mirror) — no LDS;
-//     NaN is detected from the keys (a NaN key lies beyond +/-inf);
-//   * scale/zero point per group, computed redundantly by the 16 lanes of the row, with
-//     the reference's per-op bf16 rounding (RNE after each op: v_cvt_pk_bf16_f32);
+//     (v_pk_ashrrev_i16 + v_bitop3), v_pk_max_i16/v_pk_min_i16, then (max, ~min) packed in
+//     one dword and reduced across the 16-lane DPP row — no LDS; NaN is detected from the
+//     keys (a NaN key lies beyond +/-inf);
+//   * the scale / zero point of the tile's 16 groups are computed ONCE, by 16 different
+//     lanes (lane (row, c) with c = j owns group 4j + row), with the reference's per-op
+//     bf16 rounding, then broadcast back to the group's 16 lanes with DPP row_newbcast;
 //   * per element: RN_bf16(x * RN_f32(1/s)) == RN_bf16(x / s) for every bf16 x and every
 //     bf16 s >= RN_bf16(1e-10) (verified exhaustively: oracle/verify_recip.c), so one
-//     v_pk_mul_f32 replaces the division; + z, RNE, round-half-even, clamp, pack;
-//   * each lane emits exactly one packed int32 (4-bit) — 256 B contiguous per store;
+//     multiply replaces the division; RNE to bf16 is one v_cvt_pk_bf16_f32 with a zero
+//     low half (the dword IS the rounded f32); + z, round-half-even, clamp, and
+//     v_cvt_pk_u8_f32 packs nibble pairs / bytes;
+//   * each lane emits exactly one packed int32 (4-bit): 256 B contiguous per store;
 //   * buffer descriptors are based at the tile start with the tile's byte length, so
 //     slots past the tile end read zeros and their stores are dropped by the hardware
 //     range check (no per-lane masks, no OOB access, tensors > 4 GB are fine).
 // Ragged launches: one grid over the tiles of many tensors (descriptor table in HBM);
-// waves grid-stride over tiles and advance a tensor cursor monotonically.
+// each wave walks a contiguous tile range and advances a tensor cursor.
 #include <cstdlib>
 
 #include "awq_internal.h"
+
+// cache-policy bits of the buffer loads/stores (aux operand; gfx950: 2 = nt).  Build-time
+// knobs for tuning (scripts/kbench.py compares variants); defaults measured best.
+#ifndef AWQ_LOAD_AUX
+#define AWQ_LOAD_AUX 0
+#endif
+#ifndef AWQ_STORE_AUX
+#define AWQ_STORE_AUX 0
+#endif
 
 namespace awq {
 namespace {
@@ -53,24 +66,42 @@ __device__ __forceinline__ float key_to_f32(int key16) {
     return __uint_as_float(h << 16);
 }
 
-__device__ __forceinline__ f2 rn_bf16x2(f2 v) {
-    b2 h = __builtin_convertvector(v, b2);
-    return __builtin_convertvector(h, f2);
+// RN_bf16 of an fp32 value, returned as fp32: v_cvt_pk_bf16_f32 dst, 0, a puts
+// bf16(a) in the high half and zero in the low half — which is bf16(a) as an fp32.
+// Hardware RNE; NaN stays NaN.
+__device__ __forceinline__ float rn_bf16(float a) {
+    b2 h = __builtin_convertvector((f2){0.0f, a}, b2);
+    return __builtin_bit_cast(float, h);
 }
-
-__device__ __forceinline__ float rn_bf16(float v) { return (float)(__bf16)v; }
 
 template <int CTRL>
 __device__ __forceinline__ s2 dpp_max(s2 w) {
-    int o = __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, w), CTRL, 0xF, 0xF, false);
+    const int x = __builtin_bit_cast(int, w);
+    const int o = __builtin_amdgcn_update_dpp(x, x, CTRL, 0xF, 0xF, false);
     return __builtin_elementwise_max(w, __builtin_bit_cast(s2, o));
 }
 
+// value of lane (row, J) broadcast to the 16 lanes of each row (DPP row_newbcast:J)
+template <int J>
+__device__ __forceinline__ float row_bcast(float v) {
+    const int x = __builtin_bit_cast(int, v);
+    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(x, x, 0x150 + J, 0xF, 0xF, false));
+}
+
+// RN_f32(1/s) for a bf16-valued s: v_rcp_f32 + one Newton step with fma is correctly
+// rounded for every bf16 s < 2^126 (checked exhaustively on the GPU by awq_selftest);
+// larger, inf and NaN go through the IEEE division.
+__device__ __forceinline__ float recip_bf16(float s) {
+    if (__builtin_expect(!(s < 0x1p126f), 0)) return 1.0f / s;
+    const float r0 = __builtin_amdgcn_rcpf(s);
+    const float e = __builtin_fmaf(-s, r0, 1.0f);
+    return __builtin_fmaf(r0, e, r0);
+}
+
 struct GroupParams {
-    float r;        // RN_f32(1 / s)
-    float z;        // zero point (integral float; NaN possible only when special)
-    float s;        // scale (bf16 value)
-    bool special;   // s not finite: NaN/inf semantics needed per element
+    float r;   // RN_f32(1 / s); 0 or NaN <=> s not finite ("special" group)
+    float z;   // zero point (integral float; NaN only in special groups)
+    float s;   // scale (bf16 value)
 };
 
 // awq.py:192-211 on one group, from the row-reduced keys.  QR = qmax - qmin.
@@ -79,9 +110,9 @@ __device__ __forceinline__ GroupParams group_params(s2 w) {
     constexpr float QR = (float)((1 << BITS) - 1);
     constexpr float INV_QR = 1.0f / QR;               // RN_f32(1/15), RN_f32(1/255)
     const float LO = __uint_as_float(0x2EDC0000u);    // RN_bf16(1e-10) = 1.0004442e-10
-    int mxk = (int)w.x;
-    int mnk = ~(int)w.y;
-    bool nan = (mxk > 0x7F80) || (mnk < -32641);      // keys beyond +inf / -inf
+    const int mxk = (int)w.x;
+    const int mnk = ~(int)w.y;
+    const bool nan = (mxk > 0x7F80) || (mnk < -32641);   // keys beyond +inf / -inf
     float mx = key_to_f32(mxk), mn = key_to_f32(mnk);
     if (nan) { mx = __builtin_nanf(""); mn = mx; }   // torch min/max both propagate NaN
     if (SYM) {                                        // awq.py:196-199
@@ -90,51 +121,71 @@ __device__ __forceinline__ GroupParams group_params(s2 w) {
         mn = -a;
         mx = a;
     }
-    float d = rn_bf16(mx - mn);                       // awq.py:202  bf16 subtract
-    float s = rn_bf16(d * INV_QR);                    //             bf16 / (qmax-qmin)
+    // awq.py:202: bf16 subtract, bf16 / (qmax-qmin) (== * RN(1/QR), same identity)
+    float s = rn_bf16(rn_bf16(mx - mn) * INV_QR);
     if (!__builtin_isnan(s)) s = __builtin_fmaxf(s, LO);   // awq.py:205 clamp(min=1e-10)
     GroupParams p;
     p.s = s;
-    p.r = 1.0f / s;                                   // correctly rounded (no fast-math)
+    p.r = recip_bf16(s);
     if (SYM) {
         p.z = 0.0f;                                   // awq.py:208
     } else {
-        float y = rn_bf16(mn * p.r);                  // == RN_bf16(mn / s)
+        const float y = rn_bf16(mn * p.r);            // == RN_bf16(mn / s)
         float z = __builtin_rintf(-y);                // awq.py:210-211 (qmin = 0)
         if (!__builtin_isnan(z)) z = __builtin_fminf(__builtin_fmaxf(z, 0.0f), QR);
         p.z = z;
     }
-    p.special = !__builtin_isfinite(s);
     return p;
 }
 
-// Quantize the 8 bf16 of one lane (awq.py:245-248).  nib[i] = q_i - qmin.
+// Quantize the 8 bf16 of one lane (awq.py:245-248) for a group with a finite scale and
+// pack them: 4-bit -> w.x, 8-bit -> (w.x, w.y).  Field value = q - qmin.
 template <int BITS, bool SYM>
-__device__ __forceinline__ void quant8_fast(const u4 v, const GroupParams& p, uint32_t (&nib)[8]) {
+__device__ __forceinline__ u2v quant8_fast(const u4 v, float r, float z) {
     constexpr float QR = (float)((1 << BITS) - 1);
     constexpr float HALF = (float)(1 << (BITS - 1));
     const uint32_t src[4] = {v.x, v.y, v.z, v.w};
+    float q[8];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-        f2 x = {__uint_as_float(src[i] << 16), __uint_as_float(src[i] & 0xFFFF0000u)};
-        f2 t = rn_bf16x2(x * p.r);                   // RN_bf16(x / s)
-        f2 u;
+        const float x0 = __uint_as_float(src[i] << 16), x1 = __uint_as_float(src[i] & 0xFFFF0000u);
+        float t0 = rn_bf16(x0 * r), t1 = rn_bf16(x1 * r);            // RN_bf16(x / s)
+        float u0, u1;
         if (SYM) {
-            u = t + HALF;                             // rint(t)+8 == rint(t+8): exact shift
+            u0 = t0 + HALF;                                          // rint(t)+8 == rint(t+8)
+            u1 = t1 + HALF;
         } else {
-            u = rn_bf16x2(t + p.z);                   // RN_bf16(x/s + z)
+            u0 = rn_bf16(t0 + z);                                    // RN_bf16(x/s + z)
+            u1 = rn_bf16(t1 + z);
         }
-        float u0 = __builtin_fminf(__builtin_fmaxf(__builtin_rintf(u.x), 0.0f), QR);
-        float u1 = __builtin_fminf(__builtin_fmaxf(__builtin_rintf(u.y), 0.0f), QR);
-        nib[2 * i] = (uint32_t)u0;
-        nib[2 * i + 1] = (uint32_t)u1;
+        q[2 * i] = __builtin_fminf(__builtin_fmaxf(__builtin_rintf(u0), 0.0f), QR);
+        q[2 * i + 1] = __builtin_fminf(__builtin_fmaxf(__builtin_rintf(u1), 0.0f), QR);
     }
+    u2v w;
+    if (BITS == 4) {
+        uint32_t acc = 0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)   // nibble pair as one exact float in [0, 255] -> byte i
+            acc = __builtin_amdgcn_cvt_pk_u8_f32(__builtin_fmaf(q[2 * i + 1], 16.0f, q[2 * i]), i, acc);
+        w.x = acc;
+        w.y = 0;
+    } else {
+        uint32_t a = 0, b = 0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            a = __builtin_amdgcn_cvt_pk_u8_f32(q[i], i, a);
+            b = __builtin_amdgcn_cvt_pk_u8_f32(q[4 + i], i, b);
+        }
+        w.x = a;
+        w.y = b;
+    }
+    return w;
 }
 
 // Same with the reference's NaN/inf semantics (groups whose scale is inf or NaN).
 template <int BITS, bool SYM>
-__device__ __forceinline__ void quant8_special(const u4 v, const GroupParams& p, uint32_t (&nib)[8],
-                                            int32_t (&q)[8]) {
+__device__ __forceinline__ void quant8_special(const u4 v, float r, float z, uint32_t (&nib)[8],
+                                               int32_t (&q)[8]) {
     constexpr int QMIN = SYM ? -(1 << (BITS - 1)) : 0;
     constexpr int QMAX = SYM ? (1 << (BITS - 1)) - 1 : (1 << BITS) - 1;
     constexpr uint32_t MASK = (1u << BITS) - 1u;
@@ -143,15 +194,15 @@ __device__ __forceinline__ void quant8_special(const u4 v, const GroupParams& p,
     for (int i = 0; i < 8; ++i) {
         uint32_t bits = (i & 1) ? (src[i >> 1] & 0xFFFF0000u) : (src[i >> 1] << 16);
         float x = __uint_as_float(bits);
-        float t = rn_bf16(x * p.r);
-        float u = SYM ? t : rn_bf16(t + p.z);
-        float r = __builtin_rintf(u);
+        float t = rn_bf16(x * r);
+        float u = SYM ? t : rn_bf16(t + z);
+        float rr = __builtin_rintf(u);
         int32_t qi;
-        if (__builtin_isnan(r)) {
+        if (__builtin_isnan(rr)) {
             qi = INT32_MIN;
         } else {
-            r = __builtin_fminf(__builtin_fmaxf(r, (float)QMIN), (float)QMAX);
-            qi = (int32_t)r;
+            rr = __builtin_fminf(__builtin_fmaxf(rr, (float)QMIN), (float)QMAX);
+            qi = (int32_t)rr;
         }
         q[i] = qi;
         nib[i] = ((uint32_t)qi - (uint32_t)QMIN) & MASK;
@@ -164,133 +215,181 @@ __device__ __forceinline__ uint16_t f16_bits(float s) {
     return __builtin_bit_cast(uint16_t, h);
 }
 
-template <int BITS, bool SYM>
-__device__ __forceinline__ void do_tile(const awq_tensor_desc& d, uint32_t tile, uint32_t* zw) {
-    constexpr int QMIN = SYM ? -(1 << (BITS - 1)) : 0;
-    const int lane = threadIdx.x & 63;
-    const int row = lane >> 4;       // lane-row: 16 lanes = one group
-    const int c = lane & 15;         // 16-B chunk of the group
+// ---------------------------------------------------------------------------------------
+// Tile context: everything a wave needs about one tile, all wave-uniform (SGPRs).
+// ---------------------------------------------------------------------------------------
+struct TileCtx {
+    const uint16_t* wp;  // first input element of the tile
+    int32_t* qweight;    // tensor bases of the outputs (nullptr = not wanted)
+    int32_t* qzeros;
+    uint16_t* scales;
+    int32_t* tensor_q;
+    int32_t* zeros;
+    uint32_t start;      // flat group index of the tile's first group
+    uint32_t ng;         // groups in the tile (<= 16)
+    uint32_t w0, nw;     // qzeros word range
+    uint32_t G, WPR;     // geometry (see awq_internal.h)
+    uint32_t r0, g0;     // row / group-in-row of the tile's first group
+};
 
+template <int BITS>
+__device__ __forceinline__ TileCtx make_ctx(const awq_tensor_desc& d, uint32_t tile) {
     const TensorGeom g = fast_geom(d.rows, d.K, BITS);
+    TileCtx c;
     const uint32_t w0 = tile * g.WPT;
     const uint32_t w1 = min(w0 + g.WPT, g.words);
-    const uint32_t start = word_group(g, w0);
+    const uint32_t r0 = w0 / g.WPR;
+    c.r0 = r0;
+    c.g0 = (w0 - r0 * g.WPR) * g.C;
+    c.start = r0 * g.G + c.g0;
     const uint32_t end = (w1 == g.words) ? (uint32_t)d.rows * g.G : word_group(g, w1);
-    const uint32_t ng = end - start;            // groups in this tile (<= 16)
+    c.ng = end - c.start;
+    c.w0 = w0;
+    c.nw = w1 - w0;
+    c.G = g.G;
+    c.WPR = g.WPR;
+    c.wp = (const uint16_t*)d.w + (uint64_t)c.start * kGroup;
+    c.qweight = d.qweight;
+    c.qzeros = d.qzeros;
+    c.scales = d.scales;
+    c.tensor_q = d.tensor_q;
+    c.zeros = d.zeros;
+    return c;
+}
 
-    const uint16_t* wp = (const uint16_t*)d.w + (uint64_t)start * kGroup;
-    const __amdgpu_buffer_rsrc_t rw = rsrc(wp, ng * 256u);
-
-    u4 v[4];
+// 4 x 16-B loads per lane: slot 4j + row, 16-B chunk c of the group.  Slots past the tile
+// end fall outside the descriptor's range and read as zero.
+__device__ __forceinline__ void load_tile(const TileCtx& c, u4 (&v)[4]) {
+    const int lane = threadIdx.x & 63;
+    const int row = lane >> 4, ch = lane & 15;
+    const __amdgpu_buffer_rsrc_t rw = rsrc(c.wp, c.ng * 256u);
 #pragma unroll
     for (int j = 0; j < 4; ++j)
-        v[j] = __builtin_amdgcn_raw_buffer_load_b128(rw, (uint32_t)((4 * j + row) * 256 + c * 16), 0, 0);
+        v[j] = __builtin_amdgcn_raw_buffer_load_b128(rw, (uint32_t)((4 * j + row) * 256 + ch * 16), 0, AWQ_LOAD_AUX);
+}
 
-    float sc[4];
-    float zz[4];
-    const bool want_tq = d.tensor_q != nullptr;
-    const bool want_qz = d.qzeros != nullptr;
-    if (want_qz && lane < 16) zw[lane] = 0u;
+template <int BITS, bool SYM>
+__device__ __forceinline__ void compute_tile(const TileCtx& c, const u4 (&v)[4], uint32_t* zw) {
+    constexpr int QMIN = SYM ? -(1 << (BITS - 1)) : 0;
+    constexpr uint32_t C = 32u / BITS;   // groups per qzeros word
+    const int lane = threadIdx.x & 63;
+    const int row = lane >> 4;           // lane-row: 16 lanes = one group
+    const int ch = lane & 15;            // 16-B chunk of the group
+    const uint32_t ng = c.ng;
 
+    // ---- 1. group min/max (awq.py:192-193) of the 4 groups this row holds ----
+    s2 wv[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-        const int slot = 4 * j + row;
-        // ---- group min/max (awq.py:192-193) ----
         s2 k0 = key2(v[j].x), k1 = key2(v[j].y), k2 = key2(v[j].z), k3 = key2(v[j].w);
         s2 mx = __builtin_elementwise_max(__builtin_elementwise_max(k0, k1), __builtin_elementwise_max(k2, k3));
         s2 mn = __builtin_elementwise_min(__builtin_elementwise_min(k0, k1), __builtin_elementwise_min(k2, k3));
         s2 a = {mx.x, (short)~mn.x};
         s2 b = {mx.y, (short)~mn.y};
-        s2 wv = __builtin_elementwise_max(a, b);
-        wv = dpp_max<0xB1>(wv);    // quad_perm [1,0,3,2]
-        wv = dpp_max<0x4E>(wv);    // quad_perm [2,3,0,1]
-        wv = dpp_max<0x141>(wv);   // row_half_mirror
-        wv = dpp_max<0x140>(wv);   // row_mirror: all 16 lanes hold the group's (max, ~min)
-        const GroupParams p = group_params<BITS, SYM>(wv);
-        sc[j] = p.s;
-        zz[j] = p.z;
+        s2 w = __builtin_elementwise_max(a, b);
+        w = dpp_max<0xB1>(w);    // quad_perm [1,0,3,2]
+        w = dpp_max<0x4E>(w);    // quad_perm [2,3,0,1]
+        w = dpp_max<0x141>(w);   // row_half_mirror
+        wv[j] = dpp_max<0x140>(w);   // row_mirror: the 16 lanes hold the group's (max, ~min)
+    }
+    // ---- 2. scale / zero point: lane (row, ch) computes group 4*(ch&3) + row ----
+    const int jj = ch & 3;
+    s2 wsel = wv[0];
+#pragma unroll
+    for (int j = 1; j < 4; ++j)
+        if (jj == j) wsel = wv[j];
+    const GroupParams p = group_params<BITS, SYM>(wsel);
+    const uint32_t my_slot = 4u * (uint32_t)jj + (uint32_t)row;
 
-        uint32_t nib[8];
-        int32_t q[8];
-        if (__builtin_expect(p.special, 0)) {
-            quant8_special<BITS, SYM>(v[j], p, nib, q);
-        } else {
-            quant8_fast<BITS, SYM>(v[j], p, nib);
-#pragma unroll
-            for (int i = 0; i < 8; ++i) q[i] = (int32_t)nib[i] + QMIN;
+    // ---- 3. per-group scalars out: lanes ch < 4 hold slots 0..15 (one store each) ----
+    if (ch < 4) {
+        if (c.scales) {
+            __amdgpu_buffer_rsrc_t rs = rsrc(c.scales + c.start, ng * 2u);
+            __builtin_amdgcn_raw_buffer_store_b16(f16_bits(p.s), rs, my_slot * 2u, 0, AWQ_STORE_AUX);
         }
-        // ---- packed qweight: 4-bit -> one dword per lane, 8-bit -> two ----
-        if (d.qweight) {
-            if (BITS == 4) {
-                uint32_t word = 0;
-#pragma unroll
-                for (int i = 0; i < 8; ++i) word |= nib[i] << (4 * i);
-                __amdgpu_buffer_rsrc_t rq = rsrc(d.qweight + (uint64_t)start * 16, ng * 64u);
-                __builtin_amdgcn_raw_buffer_store_b32(word, rq, (uint32_t)((slot * 16 + c) * 4), 0, 0);
-            } else {
-                u2v word;
-                word.x = nib[0] | (nib[1] << 8) | (nib[2] << 16) | (nib[3] << 24);
-                word.y = nib[4] | (nib[5] << 8) | (nib[6] << 16) | (nib[7] << 24);
-                __amdgpu_buffer_rsrc_t rq = rsrc(d.qweight + (uint64_t)start * 32, ng * 128u);
-                __builtin_amdgcn_raw_buffer_store_b64(word, rq, (uint32_t)((slot * 32 + 2 * c) * 4), 0, 0);
+        if (c.zeros) {
+            __amdgpu_buffer_rsrc_t rz = rsrc(c.zeros + c.start, ng * 4u);
+            int32_t zi = __builtin_isnan(p.z) ? INT32_MIN : (int32_t)p.z;
+            __builtin_amdgcn_raw_buffer_store_b32((uint32_t)zi, rz, my_slot * 4u, 0, AWQ_STORE_AUX);
+        }
+    }
+    // qzeros: each slot's field OR-ed into its word (wave-private LDS), then stored
+    if (c.qzeros) {
+        if (lane < 16) zw[lane] = 0u;
+        if (ch < 4 && my_slot < ng) {
+            uint32_t g = c.g0 + my_slot, r = c.r0;
+            if (g >= c.G) {                 // slot lies in a later row of the tile
+                const uint32_t k = g / c.G;
+                r += k;
+                g -= k * c.G;
             }
-        }
-        // ---- reference-layout int32 tensor_q (parity mode) ----
-        if (want_tq) {
-            __amdgpu_buffer_rsrc_t rt = rsrc(d.tensor_q + (uint64_t)start * kGroup, ng * 512u);
-            u4 lo = {(uint32_t)q[0], (uint32_t)q[1], (uint32_t)q[2], (uint32_t)q[3]};
-            u4 hi = {(uint32_t)q[4], (uint32_t)q[5], (uint32_t)q[6], (uint32_t)q[7]};
-            __builtin_amdgcn_raw_buffer_store_b128(lo, rt, (uint32_t)((slot * kGroup + 8 * c) * 4), 0, 0);
-            __builtin_amdgcn_raw_buffer_store_b128(hi, rt, (uint32_t)((slot * kGroup + 8 * c) * 4 + 16), 0, 0);
-        }
-        // ---- qzeros nibble into the tile's word (LDS, wave-private) ----
-        if (want_qz && c == 0 && (uint32_t)slot < ng) {
-            const uint32_t fg = start + (uint32_t)slot;
-            uint32_t wi, pos;
-            if (g.G % g.C == 0) {
-                wi = fg / g.C;
-                pos = fg % g.C;
-            } else {
-                uint32_t r = fg / g.G;
-                uint32_t gg = fg - r * g.G;
-                wi = r * g.WPR + gg / g.C;
-                pos = gg % g.C;
-            }
+            const uint32_t wi = r * c.WPR + g / C;
+            const uint32_t pos = g % C;
             uint32_t zn = __builtin_isnan(p.z) ? (uint32_t)(0u - (uint32_t)QMIN) : (uint32_t)((int)p.z - QMIN);
             zn &= (1u << BITS) - 1u;
-            atomicOr(&zw[wi - w0], zn << (BITS * pos));
+            atomicOr(&zw[wi - c.w0], zn << (BITS * pos));
+        }
+        if ((uint32_t)lane < c.nw) {
+            __amdgpu_buffer_rsrc_t rz = rsrc(c.qzeros + c.w0, c.nw * 4u);
+            __builtin_amdgcn_raw_buffer_store_b32(zw[lane], rz, (uint32_t)lane * 4u, 0, AWQ_STORE_AUX);
         }
     }
-    // ---- per-group scalars: lane (c == j) of row `row` writes slot 4j+row (one store) ----
-    {
-        const int jj = c & 3;
-        float s_sel = sc[0], z_sel = zz[0];
+    // ---- 4. quantize + pack the 4 groups of this row ----
+    float rj[4], zj[4];
+    rj[0] = row_bcast<0>(p.r); zj[0] = row_bcast<0>(p.z);
+    rj[1] = row_bcast<1>(p.r); zj[1] = row_bcast<1>(p.z);
+    rj[2] = row_bcast<2>(p.r); zj[2] = row_bcast<2>(p.z);
+    rj[3] = row_bcast<3>(p.r); zj[3] = row_bcast<3>(p.z);
 #pragma unroll
-        for (int j = 1; j < 4; ++j) {
-            if (jj == j) { s_sel = sc[j]; z_sel = zz[j]; }
-        }
-        const uint32_t slot = 4u * (uint32_t)jj + (uint32_t)row;
-        if (c < 4) {
-            if (d.scales) {
-                __amdgpu_buffer_rsrc_t rs = rsrc(d.scales + start, ng * 2u);
-                __builtin_amdgcn_raw_buffer_store_b16(f16_bits(s_sel), rs, slot * 2u, 0, 0);
+    for (int j = 0; j < 4; ++j) {
+        const int slot = 4 * j + row;
+        u2v word = quant8_fast<BITS, SYM>(v[j], rj[j], zj[j]);
+        const bool special = !(rj[j] > 0.0f);         // s = inf (r = 0) or NaN (r = NaN)
+        int32_t q[8];
+        if (__builtin_expect(special, 0)) {
+            uint32_t nib[8];
+            quant8_special<BITS, SYM>(v[j], rj[j], zj[j], nib, q);
+            if (BITS == 4) {
+                uint32_t acc = 0;
+#pragma unroll
+                for (int i = 0; i < 8; ++i) acc |= nib[i] << (4 * i);
+                word.x = acc;
+            } else {
+                word.x = nib[0] | (nib[1] << 8) | (nib[2] << 16) | (nib[3] << 24);
+                word.y = nib[4] | (nib[5] << 8) | (nib[6] << 16) | (nib[7] << 24);
             }
-            if (d.zeros) {
-                __amdgpu_buffer_rsrc_t rz = rsrc(d.zeros + start, ng * 4u);
-                int32_t zi = __builtin_isnan(z_sel) ? INT32_MIN : (int32_t)z_sel;
-                __builtin_amdgcn_raw_buffer_store_b32((uint32_t)zi, rz, slot * 4u, 0, 0);
+        }
+        if (c.qweight) {
+            if (BITS == 4) {
+                __amdgpu_buffer_rsrc_t rq = rsrc(c.qweight + (uint64_t)c.start * 16, ng * 64u);
+                __builtin_amdgcn_raw_buffer_store_b32(word.x, rq, (uint32_t)((slot * 16 + ch) * 4), 0, AWQ_STORE_AUX);
+            } else {
+                __amdgpu_buffer_rsrc_t rq = rsrc(c.qweight + (uint64_t)c.start * 32, ng * 128u);
+                __builtin_amdgcn_raw_buffer_store_b64(word, rq, (uint32_t)((slot * 32 + 2 * ch) * 4), 0, AWQ_STORE_AUX);
             }
         }
-    }
-    if (want_qz) {
-        const uint32_t nw = w1 - w0;
-        if ((uint32_t)lane < nw) {
-            __amdgpu_buffer_rsrc_t rz = rsrc(d.qzeros + w0, nw * 4u);
-            __builtin_amdgcn_raw_buffer_store_b32(zw[lane], rz, (uint32_t)lane * 4u, 0, 0);
+        if (c.tensor_q) {   // reference-layout int32 tensor_q (parity mode)
+            if (!special) {
+#pragma unroll
+                for (int i = 0; i < 8; ++i) {
+                    const uint32_t wd = (BITS == 4) ? word.x : (i < 4 ? word.x : word.y);
+                    const uint32_t sh = (BITS == 4) ? 4 * i : 8 * (i & 3);
+                    q[i] = (int32_t)((wd >> sh) & ((1u << BITS) - 1u)) + QMIN;
+                }
+            }
+            __amdgpu_buffer_rsrc_t rt = rsrc(c.tensor_q + (uint64_t)c.start * kGroup, ng * 512u);
+            u4 lo = {(uint32_t)q[0], (uint32_t)q[1], (uint32_t)q[2], (uint32_t)q[3]};
+            u4 hi = {(uint32_t)q[4], (uint32_t)q[5], (uint32_t)q[6], (uint32_t)q[7]};
+            __builtin_amdgcn_raw_buffer_store_b128(lo, rt, (uint32_t)((slot * kGroup + 8 * ch) * 4), 0, AWQ_STORE_AUX);
+            __builtin_amdgcn_raw_buffer_store_b128(hi, rt, (uint32_t)((slot * kGroup + 8 * ch) * 4 + 16), 0, AWQ_STORE_AUX);
         }
     }
 }
 
+// Wave-level driver.  Each wave owns a contiguous range of tiles (consecutive tiles are
+// consecutive bytes of one tensor, crossing into the next tensor at its end); the next
+// tile's 4 loads are issued before the current tile is computed (register double buffer),
+// so every wave keeps 4 KiB of HBM reads in flight while it computes.
 template <int BITS, bool SYM>
 __global__ __launch_bounds__(256) void awq_fast_kernel(const awq_tensor_desc* __restrict__ descs,
                                                        awq_tensor_desc single, int n,
@@ -301,26 +400,76 @@ __global__ __launch_bounds__(256) void awq_fast_kernel(const awq_tensor_desc* __
     const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int64_t wave = (int64_t)blockIdx.x * kWavesPerBlock + wid;
     const int64_t nwaves = (int64_t)gridDim.x * kWavesPerBlock;
-    int64_t t = wave;
-    if (t >= total_tiles) return;
-    if (descs == nullptr) {
-        for (; t < total_tiles; t += nwaves) do_tile<BITS, SYM>(single, (uint32_t)t, zwords[wid]);
-        return;
+    const int64_t per = (total_tiles + nwaves - 1) / nwaves;
+    int64_t t = wave * per;
+    const int64_t t_end = min(t + per, total_tiles);
+    if (t >= t_end) return;
+    uint32_t* zw = zwords[wid];
+
+    int cur = 0;
+    awq_tensor_desc d = single;
+    if (descs != nullptr) {
+        int lo = 0, hi = n - 1;   // tensor owning tile t: binary search on tile_begin (sorted)
+        while (lo < hi) {
+            int mid = (lo + hi + 1) >> 1;
+            if (descs[mid].tile_begin <= t) lo = mid; else hi = mid - 1;
+        }
+        cur = lo;
+        d = descs[cur];
     }
-    // first tensor of this wave: binary search on tile_begin (sorted, uniform)
-    int lo = 0, hi = n - 1;
-    while (lo < hi) {
-        int mid = (lo + hi + 1) >> 1;
-        if (descs[mid].tile_begin <= t) lo = mid; else hi = mid - 1;
+    TileCtx ctx = make_ctx<BITS>(d, (uint32_t)(t - d.tile_begin));
+    u4 va[4];
+    load_tile(ctx, va);
+    for (; t < t_end; ++t) {
+        const bool more = t + 1 < t_end;
+        TileCtx nctx = ctx;
+        u4 vb[4] = {};
+        if (more) {
+            if (descs != nullptr && cur + 1 < n && descs[cur + 1].tile_begin <= t + 1) {
+                ++cur;
+                d = descs[cur];
+            }
+            nctx = make_ctx<BITS>(d, (uint32_t)(t + 1 - d.tile_begin));
+            load_tile(nctx, vb);
+        }
+        compute_tile<BITS, SYM>(ctx, va, zw);
+        ctx = nctx;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) va[j] = vb[j];
     }
-    int cur = lo;
-    awq_tensor_desc d = descs[cur];
-    for (; t < total_tiles; t += nwaves) {
-        bool moved = false;
-        while (cur + 1 < n && descs[cur + 1].tile_begin <= t) { ++cur; moved = true; }
-        if (moved) d = descs[cur];
-        do_tile<BITS, SYM>(d, (uint32_t)(t - d.tile_begin), zwords[wid]);
+}
+
+// Exhaustive self-test of recip_bf16 over every non-negative bf16 bit pattern
+// s >= RN_bf16(1e-10) (incl. inf / NaN): counts results that differ bitwise from the
+// IEEE division.
+__global__ void awq_selftest_recip_kernel(unsigned long long* mismatches) {
+    const uint32_t h = blockIdx.x * blockDim.x + threadIdx.x;
+    if (h >= 0x8000u) return;
+    const float s = __uint_as_float(h << 16);
+    if (!(s >= __uint_as_float(0x2EDC0000u)) && !__builtin_isnan(s)) return;
+    const float a = recip_bf16(s);
+    const float b = 1.0f / s;
+    if (__float_as_uint(a) != __float_as_uint(b) && !(__builtin_isnan(a) && __builtin_isnan(b)))
+        atomicAdd(mismatches, 1ull);
+}
+
+int resident_blocks(const void* fn, int variant) {
+    // workgroups the device can hold at once for this kernel (grid = one full wave of
+    // workgroups; every wave then walks a contiguous tile range)
+    static int cache[64][4];
+    static bool init[64][4];
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 0;
+    if (!init[dev][variant]) {
+        int cus = 0, per_cu = 0;
+        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, 256, 0);
+        if (cus <= 0) cus = 256;
+        if (per_cu <= 0) per_cu = 4;
+        cache[dev][variant] = cus * per_cu;
+        init[dev][variant] = true;
     }
+    return cache[dev][variant];
 }
 
 }  // namespace
@@ -328,9 +477,11 @@ __global__ __launch_bounds__(256) void awq_fast_kernel(const awq_tensor_desc* __
 hipError_t launch_fast(const awq_tensor_desc* descs_dev, const awq_tensor_desc* single, int n,
                        int64_t total_tiles, int bits, int symmetric, hipStream_t stream) {
     if (total_tiles <= 0) return hipSuccess;
-    // grid: enough waves to keep ~8 x 16 KiB of loads in flight per CU, grid-stride beyond
-    int64_t max_blocks = 256 * 8;
-    if (const char* e = getenv("AWQ_HIP_MAX_BLOCKS")) {   // testing: force grid-stride loops
+    const void* fns[4] = {(const void*)awq_fast_kernel<4, false>, (const void*)awq_fast_kernel<4, true>,
+                          (const void*)awq_fast_kernel<8, false>, (const void*)awq_fast_kernel<8, true>};
+    const int variant = (bits == 8 ? 2 : 0) + (symmetric ? 1 : 0);
+    int64_t max_blocks = resident_blocks(fns[variant], variant);
+    if (const char* e = getenv("AWQ_HIP_MAX_BLOCKS")) {   // testing / tuning: override the grid
         long v = atol(e);
         if (v > 0) max_blocks = v;
     }
@@ -341,11 +492,19 @@ hipError_t launch_fast(const awq_tensor_desc* descs_dev, const awq_tensor_desc* 
     dim3 grid((unsigned)blocks), block(256);
 #define AWQ_LAUNCH(B, S) \
     hipLaunchKernelGGL((awq_fast_kernel<B, S>), grid, block, 0, stream, descs_dev, one, n, total_tiles)
-    if (bits == 4 && !symmetric) AWQ_LAUNCH(4, false);
-    else if (bits == 4) AWQ_LAUNCH(4, true);
-    else if (!symmetric) AWQ_LAUNCH(8, false);
-    else AWQ_LAUNCH(8, true);
+    switch (variant) {
+    case 0: AWQ_LAUNCH(4, false); break;
+    case 1: AWQ_LAUNCH(4, true); break;
+    case 2: AWQ_LAUNCH(8, false); break;
+    default: AWQ_LAUNCH(8, true); break;
+    }
 #undef AWQ_LAUNCH
+    return hipPeekAtLastError();
+}
+
+hipError_t launch_selftest(int which, unsigned long long* out, hipStream_t stream) {
+    if (which != 0) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(awq_selftest_recip_kernel, dim3(0x8000 / 256), dim3(256), 0, stream, out);
     return hipPeekAtLastError();
 }
 

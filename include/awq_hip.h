@@ -109,6 +109,11 @@ int awq_dequantize_packed(const int32_t* qweight, const int32_t* qzeros, const u
 int awq_pack_rows(const int32_t* v, int64_t rows, int64_t n, int bits, int qmin, int32_t* packed,
                   void* stream);
 
+/* Device self-test (diagnostics).  which = 0: the fast reciprocal used by the streaming
+ * kernel against IEEE 1/s over every bf16 s >= RN_bf16(1e-10); adds the number of
+ * mismatches to *result (device unsigned long long, caller-zeroed). */
+int awq_selftest(int which, unsigned long long* result, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,131 @@
+#!/usr/bin/env python3
+"""Kernel-level bench for tuning: per-launch time of the ragged quantize kernel on several
+tensor sets, for one or more library builds (--lib) and grid caps (--blocks), interleaved
+in ONE process (guide §5.4 rule 24).  Prints a table + JSON lines.
+
+  python scripts/kbench.py --sets opt-125m,llama3-8b-mlp --blocks 0,1536 --libs a.so,b.so
+"""
+import argparse
+import ctypes
+import json
+import os
+import statistics
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "awq-converter_amd")]
+import torch  # noqa: E402
+
+import bench  # noqa: E402  (shape manifests)
+
+SETS = dict(bench.WORKLOADS)
+SETS["llama3-8b-mlp"] = [((14336, 4096), 8), ((4096, 14336), 4)]      # 705 M elements
+SETS["c1x64"] = [((1024, 4096), 64)]
+SETS["k768"] = [((50272, 768), 4)]
+
+
+def shapes_of(name):
+    out = []
+    for s, c in SETS[name]:
+        out += [s] * c
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--sets", default="opt-125m,c1x64,llama3-8b-mlp,k768")
+    ap.add_argument("--libs", default="")
+    ap.add_argument("--blocks", default="0")
+    ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--bits", type=int, default=4)
+    ap.add_argument("--symmetric", action="store_true")
+    ap.add_argument("--parity", action="store_true")
+    args = ap.parse_args()
+    from awq_quantizer import _hip
+    from awq_quantizer.quantization.batch import PackedBatch
+    dev = torch.device("cuda", 0)
+    libs = [p for p in args.libs.split(",") if p] or [_hip.LIB_PATH]
+    handles = {}
+    for p in libs:
+        lib = ctypes.CDLL(os.path.abspath(p))
+        for name, (res, argt) in _hip.SIGNATURES.items():
+            fn = getattr(lib, name, None)
+            if fn is not None:
+                fn.restype = res
+                fn.argtypes = argt
+        handles[p] = lib
+    _hip.load_library()
+    _hip.require_device(dev)
+
+    # copy ceiling: 1 GiB bf16 copy (read 1 GiB + write 1 GiB)
+    a = torch.empty(1 << 29, dtype=torch.bfloat16, device=dev).normal_()
+    b = torch.empty_like(a)
+    for _ in range(3):
+        b.copy_(a)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(10):
+        b.copy_(a)
+    e1.record()
+    torch.cuda.synchronize()
+    copy_gbs = 2 * a.numel() * 2 * 10 / (e0.elapsed_time(e1) / 1e3) / 1e9
+    print(json.dumps({"copy_ceiling_GBs": round(copy_gbs, 1)}))
+    del a, b
+
+    batches = {}
+    for sname in args.sets.split(","):
+        shapes = shapes_of(sname)
+        nbytes = sum(int(torch.Size(s).numel()) * 2 for s in shapes)
+        reps = max(1, -(-(1 << 30) // nbytes))
+        bl = []
+        for r in range(reps):
+            g = torch.Generator(device=dev)
+            inputs = {}
+            for i, s in enumerate(shapes):
+                g.manual_seed(r * 1000 + i)
+                inputs[f"t{i}"] = (torch.randn(*s, generator=g, device=dev) * 0.02).to(torch.bfloat16)
+            bl.append(PackedBatch(inputs, bits=args.bits, symmetric=args.symmetric, parity=args.parity))
+        batches[sname] = bl
+    torch.cuda.synchronize()
+
+    stream = torch.cuda.current_stream(dev)
+    results = {}
+    for rnd in range(args.rounds):
+        for sname, bl in batches.items():
+            for lp, lib in handles.items():
+                for blk in args.blocks.split(","):
+                    if blk != "0":
+                        os.environ["AWQ_HIP_MAX_BLOCKS"] = blk
+                    else:
+                        os.environ.pop("AWQ_HIP_MAX_BLOCKS", None)
+                    evs = []
+                    for it in range(args.iters + 3):
+                        bt = bl[it % len(bl)]
+                        s0, s1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                        s0.record(stream)
+                        rc = lib.awq_quantize_ragged(ctypes.c_void_p(bt.descs_dev.data_ptr()), len(bt.descs),
+                                                     bt.total_tiles, bt.bits, int(bt.symmetric),
+                                                     ctypes.c_void_p(stream.cuda_stream))
+                        s1.record(stream)
+                        assert rc == 0, lib.awq_last_error()
+                        if it >= 3:
+                            evs.append((s0, s1))
+                    torch.cuda.synchronize()
+                    us = [a.elapsed_time(b) * 1e3 for a, b in evs]
+                    key = (sname, os.path.basename(lp), blk)
+                    results.setdefault(key, []).append(statistics.median(us))
+    os.environ.pop("AWQ_HIP_MAX_BLOCKS", None)
+    print(f"{'set':16s} {'lib':28s} {'blocks':>6s} {'us':>9s} {'algoGB/s':>9s} {'inGB/s':>8s} {'frac8T':>6s}")
+    for (sname, lname, blk), v in results.items():
+        bt = batches[sname][0]
+        us = min(v)
+        algo = bt.algorithmic_bytes() / (us / 1e6) / 1e9
+        inp = bt.elements * 2 / (us / 1e6) / 1e9
+        print(f"{sname:16s} {lname:28s} {blk:>6s} {us:9.1f} {algo:9.1f} {inp:8.1f} {algo / 8000:6.3f}")
+        print(json.dumps({"set": sname, "lib": lname, "blocks": blk, "us": round(us, 2), "algo_GBs": round(algo, 1),
+                          "in_GBs": round(inp, 1), "rounds_us": [round(x, 1) for x in v]}))
+
+
+if __name__ == "__main__":
+    main()

@@ -247,3 +247,9 @@ def test_grid_stride_loop(blocks, monkeypatch):
         assert torch.equal(o["scales"].cpu(), ref["scales"]), name
         pk = q.quantize_packed(x)        # single-tensor launch, same tiny grid
         assert torch.equal(pk["qweight"], o["qweight"]), name
+
+
+def test_selftest_fast_reciprocal_exhaustive():
+    """recip_bf16 (v_rcp + Newton) == IEEE 1/s for every bf16 scale value."""
+    from awq_quantizer import _hip
+    assert _hip.selftest(0, torch.device(DEV, 0)) == 0

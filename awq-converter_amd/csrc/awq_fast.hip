@@ -35,10 +35,19 @@
 // cache-policy bits of the buffer loads/stores (aux operand; gfx950: 2 = nt).  Build-time
 // knobs for tuning (scripts/kbench.py compares variants); defaults measured best.
 #ifndef AWQ_LOAD_AUX
-#define AWQ_LOAD_AUX 0
+#define AWQ_LOAD_AUX 2
 #endif
 #ifndef AWQ_STORE_AUX
-#define AWQ_STORE_AUX 0
+#define AWQ_STORE_AUX 2
+#endif
+// register double buffer: the next tile's loads are issued before the current tile is
+// computed (1) or not (0)
+#ifndef AWQ_PREFETCH
+#define AWQ_PREFETCH 1
+#endif
+// tile -> wave assignment: 1 = interleaved (tile t on wave t mod nwaves), 0 = contiguous
+#ifndef AWQ_ASSIGN_STRIDED
+#define AWQ_ASSIGN_STRIDED 1
 #endif
 
 namespace awq {
@@ -74,18 +83,26 @@ __device__ __forceinline__ float rn_bf16(float a) {
     return __builtin_bit_cast(float, h);
 }
 
+// one step of a 16-lane row reduction: max with a DPP-permuted copy (full row/bank masks,
+// every source lane valid) — LLVM folds the mov into v_max_i32_dpp (one instruction)
 template <int CTRL>
-__device__ __forceinline__ s2 dpp_max(s2 w) {
-    const int x = __builtin_bit_cast(int, w);
-    const int o = __builtin_amdgcn_update_dpp(x, x, CTRL, 0xF, 0xF, false);
-    return __builtin_elementwise_max(w, __builtin_bit_cast(s2, o));
+__device__ __forceinline__ int dpp_max(int v) {
+    return max(v, __builtin_amdgcn_mov_dpp(v, CTRL, 0xF, 0xF, true));
+}
+
+template <int CTRL>
+__device__ __forceinline__ int row_max16(int v) {   // all 16 lanes of the row get the max
+    (void)CTRL;
+    v = dpp_max<0xB1>(v);    // quad_perm [1,0,3,2]
+    v = dpp_max<0x4E>(v);    // quad_perm [2,3,0,1]
+    v = dpp_max<0x141>(v);   // row_half_mirror
+    return dpp_max<0x140>(v);   // row_mirror
 }
 
 // value of lane (row, J) broadcast to the 16 lanes of each row (DPP row_newbcast:J)
 template <int J>
 __device__ __forceinline__ float row_bcast(float v) {
-    const int x = __builtin_bit_cast(int, v);
-    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(x, x, 0x150 + J, 0xF, 0xF, false));
+    return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x150 + J, 0xF, 0xF, true));
 }
 
 // RN_f32(1/s) for a bf16-valued s: v_rcp_f32 + one Newton step with fma is correctly
@@ -106,12 +123,10 @@ struct GroupParams {
 
 // awq.py:192-211 on one group, from the row-reduced keys.  QR = qmax - qmin.
 template <int BITS, bool SYM>
-__device__ __forceinline__ GroupParams group_params(s2 w) {
+__device__ __forceinline__ GroupParams group_params(int mxk, int mnk) {
     constexpr float QR = (float)((1 << BITS) - 1);
     constexpr float INV_QR = 1.0f / QR;               // RN_f32(1/15), RN_f32(1/255)
     const float LO = __uint_as_float(0x2EDC0000u);    // RN_bf16(1e-10) = 1.0004442e-10
-    const int mxk = (int)w.x;
-    const int mnk = ~(int)w.y;
     const bool nan = (mxk > 0x7F80) || (mnk < -32641);   // keys beyond +inf / -inf
     float mx = key_to_f32(mxk), mn = key_to_f32(mnk);
     if (nan) { mx = __builtin_nanf(""); mn = mx; }   // torch min/max both propagate NaN
@@ -276,29 +291,46 @@ __device__ __forceinline__ void compute_tile(const TileCtx& c, const u4 (&v)[4],
     const int row = lane >> 4;           // lane-row: 16 lanes = one group
     const int ch = lane & 15;            // 16-B chunk of the group
     const uint32_t ng = c.ng;
+#ifdef AWQ_TRIVIAL_COMPUTE
+    // timing-only build (scripts/kbench.py): same loads and stores, no arithmetic
+    if (c.qweight) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint32_t word = v[j].x ^ v[j].y ^ v[j].z ^ v[j].w;
+            __amdgpu_buffer_rsrc_t rq = rsrc(c.qweight + (uint64_t)c.start * 16, ng * 64u);
+            __builtin_amdgcn_raw_buffer_store_b32(word, rq, (uint32_t)(((4 * j + row) * 16 + ch) * 4), 0, AWQ_STORE_AUX);
+        }
+    }
+    if (ch < 4 && c.scales) {
+        __amdgpu_buffer_rsrc_t rs = rsrc(c.scales + c.start, ng * 2u);
+        __builtin_amdgcn_raw_buffer_store_b16((uint16_t)v[0].x, rs, (4u * ch + row) * 2u, 0, AWQ_STORE_AUX);
+    }
+    if (c.qzeros && (uint32_t)lane < c.nw) {
+        __amdgpu_buffer_rsrc_t rz = rsrc(c.qzeros + c.w0, c.nw * 4u);
+        __builtin_amdgcn_raw_buffer_store_b32(v[1].y, rz, (uint32_t)lane * 4u, 0, AWQ_STORE_AUX);
+    }
+    return;
+#endif
 
-    // ---- 1. group min/max (awq.py:192-193) of the 4 groups this row holds ----
-    s2 wv[4];
+    // ---- 1. group min/max (awq.py:192-193) of the 4 groups this row holds: int16 keys,
+    //         packed max/min over the lane's 8 values, then max and ~min (= max of ~key)
+    //         reduced over the 16-lane row with DPP-fused v_max_i32 ----
+    int kmax[4], knmin[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
         s2 k0 = key2(v[j].x), k1 = key2(v[j].y), k2 = key2(v[j].z), k3 = key2(v[j].w);
         s2 mx = __builtin_elementwise_max(__builtin_elementwise_max(k0, k1), __builtin_elementwise_max(k2, k3));
         s2 mn = __builtin_elementwise_min(__builtin_elementwise_min(k0, k1), __builtin_elementwise_min(k2, k3));
-        s2 a = {mx.x, (short)~mn.x};
-        s2 b = {mx.y, (short)~mn.y};
-        s2 w = __builtin_elementwise_max(a, b);
-        w = dpp_max<0xB1>(w);    // quad_perm [1,0,3,2]
-        w = dpp_max<0x4E>(w);    // quad_perm [2,3,0,1]
-        w = dpp_max<0x141>(w);   // row_half_mirror
-        wv[j] = dpp_max<0x140>(w);   // row_mirror: the 16 lanes hold the group's (max, ~min)
+        kmax[j] = row_max16<0>(max((int)mx.x, (int)mx.y));
+        knmin[j] = row_max16<0>(~min((int)mn.x, (int)mn.y));
     }
     // ---- 2. scale / zero point: lane (row, ch) computes group 4*(ch&3) + row ----
     const int jj = ch & 3;
-    s2 wsel = wv[0];
+    int mxsel = kmax[0], nmnsel = knmin[0];
 #pragma unroll
     for (int j = 1; j < 4; ++j)
-        if (jj == j) wsel = wv[j];
-    const GroupParams p = group_params<BITS, SYM>(wsel);
+        if (jj == j) { mxsel = kmax[j]; nmnsel = knmin[j]; }
+    const GroupParams p = group_params<BITS, SYM>(mxsel, ~nmnsel);
     const uint32_t my_slot = 4u * (uint32_t)jj + (uint32_t)row;
 
     // ---- 3. per-group scalars out: lanes ch < 4 hold slots 0..15 (one store each) ----
@@ -386,6 +418,26 @@ __device__ __forceinline__ void compute_tile(const TileCtx& c, const u4 (&v)[4],
     }
 }
 
+// Index of the tensor owning tile t, searching descs[base..n) (tile_begin ascending,
+// descs[base].tile_begin <= t).  64 lanes probe 64 evenly spaced descriptors per round
+// and a ballot narrows the range: one dependent load per round, 1 round for <= 64
+// candidates, 2 for <= 4096 — instead of a chain of scalar loads through every tiny
+// tensor (a model has ~100 1-tile bias tensors next to each other).
+__device__ __forceinline__ int find_tensor(const awq_tensor_desc* __restrict__ descs, int n, int base,
+                                           int64_t t) {
+    const int lane = threadIdx.x & 63;
+    int span = n - base;
+    while (span > 1) {
+        const int stride = (span + 63) >> 6;
+        const int idx = base + lane * stride;
+        const bool ok = (idx < base + span) && descs[min(idx, n - 1)].tile_begin <= t;
+        const int cnt = __builtin_popcountll(__ballot(ok));   // ok lanes form a prefix
+        base += (cnt - 1) * stride;
+        span = min(stride, n - base);
+    }
+    return __builtin_amdgcn_readfirstlane(base);
+}
+
 // Wave-level driver.  Each wave owns a contiguous range of tiles (consecutive tiles are
 // consecutive bytes of one tensor, crossing into the next tensor at its end); the next
 // tile's 4 loads are issued before the current tile is computed (register double buffer),
@@ -400,36 +452,54 @@ __global__ __launch_bounds__(256) void awq_fast_kernel(const awq_tensor_desc* __
     const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int64_t wave = (int64_t)blockIdx.x * kWavesPerBlock + wid;
     const int64_t nwaves = (int64_t)gridDim.x * kWavesPerBlock;
+#if AWQ_ASSIGN_STRIDED
+    // interleaved: at any moment the waves of the chip read one compact window of memory
+    int64_t t = wave;
+    const int64_t step = nwaves;
+    const int64_t t_end = total_tiles;
+#else
     const int64_t per = (total_tiles + nwaves - 1) / nwaves;
     int64_t t = wave * per;
+    const int64_t step = 1;
     const int64_t t_end = min(t + per, total_tiles);
+#endif
     if (t >= t_end) return;
     uint32_t* zw = zwords[wid];
 
     int cur = 0;
     awq_tensor_desc d = single;
     if (descs != nullptr) {
-        int lo = 0, hi = n - 1;   // tensor owning tile t: binary search on tile_begin (sorted)
-        while (lo < hi) {
-            int mid = (lo + hi + 1) >> 1;
-            if (descs[mid].tile_begin <= t) lo = mid; else hi = mid - 1;
-        }
-        cur = lo;
+        cur = find_tensor(descs, n, 0, t);
         d = descs[cur];
     }
     TileCtx ctx = make_ctx<BITS>(d, (uint32_t)(t - d.tile_begin));
+#if !AWQ_PREFETCH
+    // single-buffered: occupancy hides the latency (fewer VGPRs -> more waves)
+    for (; t < t_end; t += step) {
+        if (descs != nullptr && cur + 1 < n && descs[cur + 1].tile_begin <= t) {
+            cur = find_tensor(descs, n, cur + 1, t);
+            d = descs[cur];
+        }
+        ctx = make_ctx<BITS>(d, (uint32_t)(t - d.tile_begin));
+        u4 va[4];
+        load_tile(ctx, va);
+        compute_tile<BITS, SYM>(ctx, va, zw);
+    }
+    return;
+#endif
     u4 va[4];
     load_tile(ctx, va);
-    for (; t < t_end; ++t) {
-        const bool more = t + 1 < t_end;
+    for (; t < t_end; t += step) {
+        const int64_t tn = t + step;
+        const bool more = tn < t_end;
         TileCtx nctx = ctx;
         u4 vb[4] = {};
         if (more) {
-            if (descs != nullptr && cur + 1 < n && descs[cur + 1].tile_begin <= t + 1) {
-                ++cur;
+            if (descs != nullptr && cur + 1 < n && descs[cur + 1].tile_begin <= tn) {
+                cur = find_tensor(descs, n, cur + 1, tn);
                 d = descs[cur];
             }
-            nctx = make_ctx<BITS>(d, (uint32_t)(t + 1 - d.tile_begin));
+            nctx = make_ctx<BITS>(d, (uint32_t)(tn - d.tile_begin));
             load_tile(nctx, vb);
         }
         compute_tile<BITS, SYM>(ctx, va, zw);

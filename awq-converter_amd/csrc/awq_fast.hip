@@ -40,10 +40,18 @@
 #ifndef AWQ_STORE_AUX
 #define AWQ_STORE_AUX 2
 #endif
-// register double buffer: the next tile's loads are issued before the current tile is
-// computed (1) or not (0)
+// next-tile prefetch: 2 = LDS-DMA staging slot per wave, 1 = register double buffer,
+// 0 = none (occupancy alone hides the latency)
 #ifndef AWQ_PREFETCH
-#define AWQ_PREFETCH 1
+#define AWQ_PREFETCH 2
+#endif
+// __launch_bounds__ minimum waves per SIMD (8 = 32 waves per CU: <= 64 VGPRs, <= 80 SGPRs)
+#ifndef AWQ_MIN_WAVES
+#define AWQ_MIN_WAVES 8
+#endif
+// group min/max from raw bf16 bits (1) or from order-preserving int16 keys (0)
+#ifndef AWQ_RAW_MINMAX
+#define AWQ_RAW_MINMAX 1
 #endif
 // tile -> wave assignment: 1 = interleaved (tile t on wave t mod nwaves), 0 = contiguous
 #ifndef AWQ_ASSIGN_STRIDED
@@ -54,6 +62,7 @@ namespace awq {
 namespace {
 
 typedef short s2 __attribute__((ext_vector_type(2)));
+typedef unsigned short us2 __attribute__((ext_vector_type(2)));
 typedef float f2 __attribute__((ext_vector_type(2)));
 typedef __bf16 b2 __attribute__((ext_vector_type(2)));
 typedef uint32_t u4 __attribute__((ext_vector_type(4)));
@@ -64,7 +73,7 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* base, uint32_
                                              0x00020000);
 }
 
-__device__ __forceinline__ s2 key2(uint32_t u) {
+[[maybe_unused]] __device__ __forceinline__ s2 key2(uint32_t u) {
     s2 h = __builtin_bit_cast(s2, u);
     return h ^ ((h >> (s2)15) & (s2)0x7FFF);
 }
@@ -151,6 +160,20 @@ __device__ __forceinline__ GroupParams group_params(int mxk, int mnk) {
         p.z = z;
     }
     return p;
+}
+
+// Same from the raw-bits reductions: smax = signed max, umax = unsigned max, umin =
+// unsigned min (only valid when the group is single-signed).
+template <int BITS, bool SYM>
+__device__ __forceinline__ GroupParams group_params_raw(int smax, int umax, int umin) {
+    const int mx_bits = smax >= 0 ? smax : umin;          // all negative: smallest magnitude
+    const int mn_bits = umax >= 0x8000 ? umax : umin;     // none negative: smallest value
+    const bool nan = (smax > 0x7F80) || (umax > 0xFF80);
+    // keys of those bf16 values for group_params (order-preserving int16, sign-extended)
+    const int mxs = (int)(short)mx_bits, mns = (int)(short)mn_bits;
+    int mxk = mxs ^ ((mxs >> 15) & 0x7FFF), mnk = mns ^ ((mns >> 15) & 0x7FFF);
+    if (nan) mxk = 0x7FC0;                                 // any key beyond +inf
+    return group_params<BITS, SYM>(mxk, mnk);
 }
 
 // Quantize the 8 bf16 of one lane (awq.py:245-248) for a group with a finite scale and
@@ -245,22 +268,33 @@ struct TileCtx {
     uint32_t w0, nw;     // qzeros word range
     uint32_t G, WPR;     // geometry (see awq_internal.h)
     uint32_t r0, g0;     // row / group-in-row of the tile's first group
+    uint32_t bytes;      // byte tiles (qzeros written byte-wise) vs word tiles
 };
 
 template <int BITS>
 __device__ __forceinline__ TileCtx make_ctx(const awq_tensor_desc& d, uint32_t tile) {
     const TensorGeom g = fast_geom(d.rows, d.K, BITS);
     TileCtx c;
-    const uint32_t w0 = tile * g.WPT;
-    const uint32_t w1 = min(w0 + g.WPT, g.words);
-    const uint32_t r0 = w0 / g.WPR;
-    c.r0 = r0;
-    c.g0 = (w0 - r0 * g.WPR) * g.C;
-    c.start = r0 * g.G + c.g0;
-    const uint32_t end = (w1 == g.words) ? (uint32_t)d.rows * g.G : word_group(g, w1);
-    c.ng = end - c.start;
-    c.w0 = w0;
-    c.nw = w1 - w0;
+    c.bytes = g.bytes;
+    if (g.bytes) {
+        c.start = tile * kSlots;
+        c.ng = min((uint32_t)kSlots, (uint32_t)d.rows * g.G - c.start);
+        c.r0 = c.start / g.G;
+        c.g0 = c.start - c.r0 * g.G;
+        c.w0 = 0;
+        c.nw = 0;
+    } else {
+        const uint32_t w0 = tile * g.WPT;
+        const uint32_t w1 = min(w0 + g.WPT, g.words);
+        const uint32_t r0 = w0 / g.WPR;
+        c.r0 = r0;
+        c.g0 = (w0 - r0 * g.WPR) * g.C;
+        c.start = r0 * g.G + c.g0;
+        const uint32_t end = (w1 == g.words) ? (uint32_t)d.rows * g.G : word_group(g, w1);
+        c.ng = end - c.start;
+        c.w0 = w0;
+        c.nw = w1 - w0;
+    }
     c.G = g.G;
     c.WPR = g.WPR;
     c.wp = (const uint16_t*)d.w + (uint64_t)c.start * kGroup;
@@ -272,6 +306,22 @@ __device__ __forceinline__ TileCtx make_ctx(const awq_tensor_desc& d, uint32_t t
     return c;
 }
 
+// first flat group and group count of a tile (the input byte range it reads)
+template <int BITS>
+__device__ __forceinline__ void tile_src(int64_t rows, int64_t K, uint32_t tile, uint32_t& start, uint32_t& ng) {
+    const TensorGeom g = fast_geom(rows, K, BITS);
+    if (g.bytes) {
+        start = tile * kSlots;
+        ng = min((uint32_t)kSlots, (uint32_t)rows * g.G - start);
+        return;
+    }
+    const uint32_t w0 = tile * g.WPT;
+    const uint32_t w1 = min(w0 + g.WPT, g.words);
+    start = word_group(g, w0);
+    const uint32_t end = (w1 == g.words) ? (uint32_t)rows * g.G : word_group(g, w1);
+    ng = end - start;
+}
+
 // 4 x 16-B loads per lane: slot 4j + row, 16-B chunk c of the group.  Slots past the tile
 // end fall outside the descriptor's range and read as zero.
 __device__ __forceinline__ void load_tile(const TileCtx& c, u4 (&v)[4]) {
@@ -281,6 +331,18 @@ __device__ __forceinline__ void load_tile(const TileCtx& c, u4 (&v)[4]) {
 #pragma unroll
     for (int j = 0; j < 4; ++j)
         v[j] = __builtin_amdgcn_raw_buffer_load_b128(rw, (uint32_t)((4 * j + row) * 256 + ch * 16), 0, AWQ_LOAD_AUX);
+}
+
+// Same 4 KiB as load_tile, streamed into the wave's LDS slot by LDS-DMA: instruction j
+// writes 1 KiB contiguously (lane i -> slot + j*1024 + 16*i), i.e. the slot is a byte copy
+// of the tile and lane i later reads back exactly the 16 B load_tile would have given it.
+[[maybe_unused]] __device__ __forceinline__ void dma_tile(const uint16_t* wp, uint32_t ng, uint8_t* slot) {
+    const int lane = threadIdx.x & 63;
+    const __amdgpu_buffer_rsrc_t rw = rsrc(wp, ng * 256u);
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rw, (__attribute__((address_space(3))) void*)(slot + j * 1024), 16,
+                                                 (uint32_t)(j * 1024 + lane * 16), 0, 0, AWQ_LOAD_AUX);
 }
 
 template <int BITS, bool SYM>
@@ -315,6 +377,45 @@ __device__ __forceinline__ void compute_tile(const TileCtx& c, const u4 (&v)[4],
     // ---- 1. group min/max (awq.py:192-193) of the 4 groups this row holds: int16 keys,
     //         packed max/min over the lane's 8 values, then max and ~min (= max of ~key)
     //         reduced over the 16-lane row with DPP-fused v_max_i32 ----
+#if AWQ_RAW_MINMAX
+    // Raw bf16 bits, no key transform: the SIGNED int16 max is the float max whenever the
+    // group has a value with the sign bit clear, and the UNSIGNED max is the float min
+    // (most negative) whenever it has one with the sign bit set; NaNs land beyond 0x7F80 /
+    // 0xFF80.  Single-signed groups (rare in weights; LayerNorm gammas) take an extra
+    // unsigned-min reduction in a wave-uniform branch.
+    int smx[4], umx[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const s2 a = __builtin_bit_cast(s2, v[j].x), b = __builtin_bit_cast(s2, v[j].y);
+        const s2 c = __builtin_bit_cast(s2, v[j].z), e = __builtin_bit_cast(s2, v[j].w);
+        const s2 sm = __builtin_elementwise_max(__builtin_elementwise_max(a, b), __builtin_elementwise_max(c, e));
+        const us2 um = __builtin_elementwise_max(__builtin_elementwise_max(__builtin_bit_cast(us2, a), __builtin_bit_cast(us2, b)),
+                                                 __builtin_elementwise_max(__builtin_bit_cast(us2, c), __builtin_bit_cast(us2, e)));
+        smx[j] = row_max16<0>(max((int)sm.x, (int)sm.y));
+        umx[j] = row_max16<0>(max((int)um.x, (int)um.y));
+    }
+    int umn[4] = {0, 0, 0, 0};
+    bool one_signed = false;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) one_signed |= (smx[j] < 0) || (umx[j] < 0x8000);
+    if (__builtin_expect(__ballot(one_signed) != 0, 0)) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {   // unsigned min = 0xFFFF - max(0xFFFF - u)
+            const us2 ones = {0xFFFF, 0xFFFF};
+            const us2 a = ones - __builtin_bit_cast(us2, v[j].x), b = ones - __builtin_bit_cast(us2, v[j].y);
+            const us2 c = ones - __builtin_bit_cast(us2, v[j].z), e = ones - __builtin_bit_cast(us2, v[j].w);
+            const us2 m = __builtin_elementwise_max(__builtin_elementwise_max(a, b), __builtin_elementwise_max(c, e));
+            umn[j] = 0xFFFF - row_max16<0>(max((int)m.x, (int)m.y));
+        }
+    }
+    // ---- 2. scale / zero point: lane (row, ch) computes group 4*(ch&3) + row ----
+    const int jj = ch & 3;
+    int ssel = smx[0], usel = umx[0], nsel = umn[0];
+#pragma unroll
+    for (int j = 1; j < 4; ++j)
+        if (jj == j) { ssel = smx[j]; usel = umx[j]; nsel = umn[j]; }
+    const GroupParams p = group_params_raw<BITS, SYM>(ssel, usel, nsel);
+#else
     int kmax[4], knmin[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -331,56 +432,22 @@ __device__ __forceinline__ void compute_tile(const TileCtx& c, const u4 (&v)[4],
     for (int j = 1; j < 4; ++j)
         if (jj == j) { mxsel = kmax[j]; nmnsel = knmin[j]; }
     const GroupParams p = group_params<BITS, SYM>(mxsel, ~nmnsel);
+#endif
     const uint32_t my_slot = 4u * (uint32_t)jj + (uint32_t)row;
 
-    // ---- 3. per-group scalars out: lanes ch < 4 hold slots 0..15 (one store each) ----
-    if (ch < 4) {
-        if (c.scales) {
-            __amdgpu_buffer_rsrc_t rs = rsrc(c.scales + c.start, ng * 2u);
-            __builtin_amdgcn_raw_buffer_store_b16(f16_bits(p.s), rs, my_slot * 2u, 0, AWQ_STORE_AUX);
-        }
-        if (c.zeros) {
-            __amdgpu_buffer_rsrc_t rz = rsrc(c.zeros + c.start, ng * 4u);
-            int32_t zi = __builtin_isnan(p.z) ? INT32_MIN : (int32_t)p.z;
-            __builtin_amdgcn_raw_buffer_store_b32((uint32_t)zi, rz, my_slot * 4u, 0, AWQ_STORE_AUX);
-        }
-    }
-    // qzeros: each slot's field OR-ed into its word (wave-private LDS), then stored
-    if (c.qzeros) {
-        if (lane < 16) zw[lane] = 0u;
-        if (ch < 4 && my_slot < ng) {
-            uint32_t g = c.g0 + my_slot, r = c.r0;
-            if (g >= c.G) {                 // slot lies in a later row of the tile
-                const uint32_t k = g / c.G;
-                r += k;
-                g -= k * c.G;
-            }
-            const uint32_t wi = r * c.WPR + g / C;
-            const uint32_t pos = g % C;
-            uint32_t zn = __builtin_isnan(p.z) ? (uint32_t)(0u - (uint32_t)QMIN) : (uint32_t)((int)p.z - QMIN);
-            zn &= (1u << BITS) - 1u;
-            atomicOr(&zw[wi - c.w0], zn << (BITS * pos));
-        }
-        if ((uint32_t)lane < c.nw) {
-            __amdgpu_buffer_rsrc_t rz = rsrc(c.qzeros + c.w0, c.nw * 4u);
-            __builtin_amdgcn_raw_buffer_store_b32(zw[lane], rz, (uint32_t)lane * 4u, 0, AWQ_STORE_AUX);
-        }
-    }
     // ---- 4. quantize + pack the 4 groups of this row ----
-    float rj[4], zj[4];
-    rj[0] = row_bcast<0>(p.r); zj[0] = row_bcast<0>(p.z);
-    rj[1] = row_bcast<1>(p.r); zj[1] = row_bcast<1>(p.z);
-    rj[2] = row_bcast<2>(p.r); zj[2] = row_bcast<2>(p.z);
-    rj[3] = row_bcast<3>(p.r); zj[3] = row_bcast<3>(p.z);
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
         const int slot = 4 * j + row;
-        u2v word = quant8_fast<BITS, SYM>(v[j], rj[j], zj[j]);
-        const bool special = !(rj[j] > 0.0f);         // s = inf (r = 0) or NaN (r = NaN)
+        // this group's r, z from lane (row, j), broadcast just in time (short live ranges)
+        const float rj = j == 0 ? row_bcast<0>(p.r) : j == 1 ? row_bcast<1>(p.r) : j == 2 ? row_bcast<2>(p.r) : row_bcast<3>(p.r);
+        const float zj = SYM ? 0.0f : (j == 0 ? row_bcast<0>(p.z) : j == 1 ? row_bcast<1>(p.z) : j == 2 ? row_bcast<2>(p.z) : row_bcast<3>(p.z));
+        u2v word = quant8_fast<BITS, SYM>(v[j], rj, zj);
+        const bool special = !(rj > 0.0f);         // s = inf (r = 0) or NaN (r = NaN)
         int32_t q[8];
         if (__builtin_expect(special, 0)) {
             uint32_t nib[8];
-            quant8_special<BITS, SYM>(v[j], rj[j], zj[j], nib, q);
+            quant8_special<BITS, SYM>(v[j], rj, zj, nib, q);
             if (BITS == 4) {
                 uint32_t acc = 0;
 #pragma unroll
@@ -416,6 +483,68 @@ __device__ __forceinline__ void compute_tile(const TileCtx& c, const u4 (&v)[4],
             __builtin_amdgcn_raw_buffer_store_b128(hi, rt, (uint32_t)((slot * kGroup + 8 * ch) * 4 + 16), 0, AWQ_STORE_AUX);
         }
     }
+    // ---- 5. per-group scalars out (after the data registers are dead): lanes ch < 4 hold slots 0..15 (one store each) ----
+    if (ch < 4) {
+        if (c.scales) {
+            __amdgpu_buffer_rsrc_t rs = rsrc(c.scales + c.start, ng * 2u);
+            __builtin_amdgcn_raw_buffer_store_b16(f16_bits(p.s), rs, my_slot * 2u, 0, AWQ_STORE_AUX);
+        }
+        if (c.zeros) {
+            __amdgpu_buffer_rsrc_t rz = rsrc(c.zeros + c.start, ng * 4u);
+            int32_t zi = __builtin_isnan(p.z) ? INT32_MIN : (int32_t)p.z;
+            __builtin_amdgcn_raw_buffer_store_b32((uint32_t)zi, rz, my_slot * 4u, 0, AWQ_STORE_AUX);
+        }
+    }
+    // qzeros, byte tiles: each group's field OR-ed into its byte (wave-private LDS), then one
+    // lane per qzeros byte stores it (plus the zero pad bytes ending its row's last word)
+    if (c.qzeros && c.bytes) {
+        constexpr uint32_t GPB = BITS == 4 ? 2u : 1u;        // groups per byte
+        if (lane < 16) zw[lane] = 0u;
+        if (ch < 4 && my_slot < ng) {
+            uint32_t zn = __builtin_isnan(p.z) ? (uint32_t)(0u - (uint32_t)QMIN) : (uint32_t)((int)p.z - QMIN);
+            zn &= (1u << BITS) - 1u;
+            atomicOr(&zw[my_slot / GPB], zn << (BITS * (my_slot % GPB)));
+        }
+        const uint32_t nb = ng / GPB;                         // ng and the tile start are even
+        if ((uint32_t)lane < nb) {
+            uint32_t g = c.g0 + (uint32_t)lane * GPB, r = c.r0;
+            if (g >= c.G) {
+                const uint32_t k = g / c.G;
+                r += k;
+                g -= k * c.G;
+            }
+            const uint32_t row_bytes = c.WPR * 4u;
+            __amdgpu_buffer_rsrc_t rz = rsrc(c.qzeros, 0x7FFFFFFFu);
+            const uint32_t at = r * row_bytes + g / GPB;
+            __builtin_amdgcn_raw_buffer_store_b8((uint8_t)zw[lane], rz, at, 0, AWQ_STORE_AUX);
+            if (g + GPB >= c.G) {                               // row's last byte: zero the pad
+                for (uint32_t b = g / GPB + 1; b < row_bytes; ++b)
+                    __builtin_amdgcn_raw_buffer_store_b8((uint8_t)0, rz, r * row_bytes + b, 0, AWQ_STORE_AUX);
+            }
+        }
+    }
+    // qzeros, word tiles: each slot's field OR-ed into its word (wave-private LDS), then stored
+    if (c.qzeros && !c.bytes) {
+        if (lane < 16) zw[lane] = 0u;
+        if (ch < 4 && my_slot < ng) {
+            uint32_t g = c.g0 + my_slot, r = c.r0;
+            if (g >= c.G) {                 // slot lies in a later row of the tile
+                const uint32_t k = g / c.G;
+                r += k;
+                g -= k * c.G;
+            }
+            const uint32_t wi = r * c.WPR + g / C;
+            const uint32_t pos = g % C;
+            uint32_t zn = __builtin_isnan(p.z) ? (uint32_t)(0u - (uint32_t)QMIN) : (uint32_t)((int)p.z - QMIN);
+            zn &= (1u << BITS) - 1u;
+            atomicOr(&zw[wi - c.w0], zn << (BITS * pos));
+        }
+        if ((uint32_t)lane < c.nw) {
+            __amdgpu_buffer_rsrc_t rz = rsrc(c.qzeros + c.w0, c.nw * 4u);
+            __builtin_amdgcn_raw_buffer_store_b32(zw[lane], rz, (uint32_t)lane * 4u, 0, AWQ_STORE_AUX);
+        }
+    }
+
 }
 
 // Index of the tensor owning tile t, searching descs[base..n) (tile_begin ascending,
@@ -443,7 +572,7 @@ __device__ __forceinline__ int find_tensor(const awq_tensor_desc* __restrict__ d
 // tile's 4 loads are issued before the current tile is computed (register double buffer),
 // so every wave keeps 4 KiB of HBM reads in flight while it computes.
 template <int BITS, bool SYM>
-__global__ __launch_bounds__(256) void awq_fast_kernel(const awq_tensor_desc* __restrict__ descs,
+__global__ __launch_bounds__(256, AWQ_MIN_WAVES) void awq_fast_kernel(const awq_tensor_desc* __restrict__ descs,
                                                        awq_tensor_desc single, int n,
                                                        int64_t total_tiles) {
     __shared__ uint32_t zwords[kWavesPerBlock][kSlots];
@@ -473,7 +602,52 @@ __global__ __launch_bounds__(256) void awq_fast_kernel(const awq_tensor_desc* __
         d = descs[cur];
     }
     TileCtx ctx = make_ctx<BITS>(d, (uint32_t)(t - d.tile_begin));
-#if !AWQ_PREFETCH
+#if AWQ_PREFETCH == 2
+    // LDS-DMA pipeline: the next tile streams HBM -> LDS (buffer_load ... lds, no VGPRs)
+    // while this tile is computed; each wave owns one 4 KiB staging slot.  Only the next
+    // tile's source range is carried across the compute (few SGPRs): the full tile
+    // context is rebuilt right before it is used.
+    __shared__ __attribute__((aligned(16))) uint8_t stage[kWavesPerBlock][kSlots * 256];
+    uint8_t* slot = stage[wid];
+    const int lane = threadIdx.x & 63;
+    {
+        uint32_t st, ng;
+        tile_src<BITS>(d.rows, d.K, (uint32_t)(t - d.tile_begin), st, ng);
+        dma_tile((const uint16_t*)d.w + (uint64_t)st * kGroup, ng, slot);
+    }
+    for (; t < t_end; t += step) {
+        const int64_t tn = t + step;
+        const bool more = tn < t_end;
+        int nc = cur;
+        const uint16_t* nwp = nullptr;
+        uint32_t nng = 0;
+        if (more) {
+            if (descs != nullptr && cur + 1 < n && descs[cur + 1].tile_begin <= tn) {
+                nc = find_tensor(descs, n, cur + 1, tn);
+                const awq_tensor_desc* nd = descs + nc;
+                uint32_t st;
+                tile_src<BITS>(nd->rows, nd->K, (uint32_t)(tn - nd->tile_begin), st, nng);
+                nwp = (const uint16_t*)nd->w + (uint64_t)st * kGroup;
+            } else {
+                uint32_t st;
+                tile_src<BITS>(d.rows, d.K, (uint32_t)(tn - d.tile_begin), st, nng);
+                nwp = (const uint16_t*)d.w + (uint64_t)st * kGroup;
+            }
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");       // this tile has landed in LDS
+        u4 va[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) va[j] = *(const u4*)(slot + j * 1024 + lane * 16);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");     // slot read out: reusable
+        if (more) dma_tile(nwp, nng, slot);
+        compute_tile<BITS, SYM>(make_ctx<BITS>(d, (uint32_t)(t - d.tile_begin)), va, zw);
+        if (nc != cur) {
+            cur = nc;
+            d = descs[cur];
+        }
+    }
+    return;
+#elif !AWQ_PREFETCH
     // single-buffered: occupancy hides the latency (fewer VGPRs -> more waves)
     for (; t < t_end; t += step) {
         if (descs != nullptr && cur + 1 < n && descs[cur + 1].tile_begin <= t) {

@@ -13,10 +13,16 @@ namespace awq {
 //
 // A tensor [R, K] is a flat sequence of R*G groups of 128 bf16 (256 B).  qzeros packs
 // C = 32/bits consecutive groups of ONE row per word, so a row has WPR = ceil(G/C)
-// words.  A wave-tile is WPT consecutive words (<= 16 groups): every qzeros word is
-// produced inside one tile, and the groups of a tile are one contiguous byte range.
-//   WPR == 1 (G <= C): WPT = 16 / G whole rows per tile
-//   else            : WPT = 16 / C words (= 16 groups when every word is full)
+// words.  Two tilings (a wave-tile is <= 16 groups = one contiguous byte range):
+//   * byte tiles ("bytes" = 1): when a row's zero points fill whole BYTES of qzeros
+//     (8-bit, or 4-bit with G even), tiles are 16 consecutive flat groups and every
+//     tile writes the qzeros bytes of its own groups (byte stores, pad bytes of a row's
+//     last word written by the tile holding the row's last group) — full tiles for any
+//     such G (K = 768: 16 groups per tile, not 12);
+//   * word tiles (4-bit with G odd): a tile is WPT consecutive qzeros words, so every
+//     word is produced inside one tile:  WPR == 1 (G <= C): WPT = 16 / G whole rows,
+//     else WPT = 16 / C words (= 16 groups when every word is full).
+// When G % C == 0 both tilings coincide (16-group tiles of 2 or 4 whole words).
 // ---------------------------------------------------------------------------
 constexpr int kGroup = 128;          // elements per group on the fast path
 constexpr int kSlots = 16;           // group slots per wave-tile (4 loads x 4 lane-rows)
@@ -28,6 +34,7 @@ struct TensorGeom {
     uint32_t WPR;  // qzeros words per row
     uint32_t WPT;  // words per tile
     uint32_t words;  // R * WPR
+    uint32_t bytes;  // 1 = byte tiles (see above), 0 = word tiles
 };
 
 __host__ __device__ inline TensorGeom fast_geom(int64_t R, int64_t K, int bits) {
@@ -37,12 +44,14 @@ __host__ __device__ inline TensorGeom fast_geom(int64_t R, int64_t K, int bits) 
     g.WPR = (g.G + g.C - 1) / g.C;
     g.WPT = (g.WPR == 1) ? (kSlots / g.G) : (kSlots / g.C);
     g.words = (uint32_t)R * g.WPR;
+    g.bytes = (bits == 8 || (g.G % 2u) == 0u) ? 1u : 0u;
     return g;
 }
 
 __host__ __device__ inline int64_t fast_tiles(int64_t R, int64_t K, int bits) {
     if (R <= 0 || K <= 0) return 0;
     TensorGeom g = fast_geom(R, K, bits);
+    if (g.bytes) return (R * (int64_t)g.G + kSlots - 1) / kSlots;
     return ((int64_t)g.words + g.WPT - 1) / g.WPT;
 }
 

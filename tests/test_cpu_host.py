@@ -46,9 +46,14 @@ def test_host_helpers_without_gpu():
          _hip.TensorDesc(4096 * 32, 1, 768, 0, 0, 2 * 8192, 0, 0, 0, 0),
          _hip.TensorDesc(4096 * 48, 50, 768, 0, 0, 2 * 16384, 0, 0, 0, 0)]
     total = _hip.plan_ragged(d, 4)
-    # 1024 rows x G=32 -> 4 words/row -> 2048 tiles; G=6 -> 1 word/row, 2 rows/tile
-    assert d[0].tile_count == 2048 and d[1].tile_count == 1 and d[2].tile_count == 25
-    assert total == 2048 + 1 + 25 and d[2].tile_begin == 2049
+    # 1024 rows x G=32 -> 16-group tiles -> 2048; G=6 (even) -> byte tiles: 16 flat groups
+    assert d[0].tile_count == 2048 and d[1].tile_count == 1 and d[2].tile_count == 19
+    assert total == 2048 + 1 + 19 and d[2].tile_begin == 2049
+    # G odd at 4 bits -> word tiles: K=384 (G=3) -> 5 rows (15 groups) per tile
+    d = [_hip.TensorDesc(4096 * 16, 11, 384, 0, 0, 2 * 4096, 0, 0, 0, 0)]
+    assert _hip.plan_ragged(d, 4) == 3
+    d = [_hip.TensorDesc(4096 * 16, 11, 384, 0, 0, 2 * 4096, 0, 0, 0, 0)]
+    assert _hip.plan_ragged(d, 8) == 3   # 8-bit: byte tiles, 33 groups -> 3
     # validation errors come back with a message, nothing launched
     assert lib.awq_quantize_groups(None, 0, 4, 256, 128, 3, 0, None, None, None, None, None, None) != 0
     assert "bit width" in _hip.last_error()

@@ -83,7 +83,8 @@ def test_quantize_model_skip_semantics():
 
 # ---------------------------------------------------------------- oracle, random shapes
 FAST_SHAPES = [(1024, 4096), (4096, 768), (768,), (3072,), (7, 1792), (3, 1280), (5, 384), (9, 128),
-               (33, 11 * 128), (2, 8, 256), (64, 14336), (1, 65536)]
+               (33, 11 * 128), (2, 8, 256), (64, 14336), (1, 65536), (13, 1280), (6, 2560), (40, 256),
+               (7, 640), (5, 1152), (77, 768), (3, 896)]
 
 
 @pytest.mark.parametrize("bits", [4, 8])

@@ -227,7 +227,8 @@ def quantize_stream(loader, infos: List[TensorInfo], quantizer: AWQQuantizer, de
     `lookahead` ahead of the GPU; each tensor is quantized as soon as it is read and its
     results are copied back to host memory."""
     if device.startswith("cuda") and torch.cuda.is_available():
-        torch.cuda.set_device(torch.device(device))
+        dev = torch.device(device)
+        torch.cuda.set_device(dev.index if dev.index is not None else torch.cuda.current_device())
     pending = deque()
     it = iter(infos)
 

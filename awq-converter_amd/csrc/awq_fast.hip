@@ -73,6 +73,9 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* base, uint32_
                                              0x00020000);
 }
 
+__device__ __forceinline__ s2 as_s2(uint32_t u) { return __builtin_bit_cast(s2, u); }
+__device__ __forceinline__ us2 as_us2(uint32_t u) { return __builtin_bit_cast(us2, u); }
+
 [[maybe_unused]] __device__ __forceinline__ s2 key2(uint32_t u) {
     s2 h = __builtin_bit_cast(s2, u);
     return h ^ ((h >> (s2)15) & (s2)0x7FFF);
@@ -386,11 +389,13 @@ __device__ __forceinline__ void compute_tile(const TileCtx& c, const u4 (&v)[4],
     int smx[4], umx[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-        const s2 a = __builtin_bit_cast(s2, v[j].x), b = __builtin_bit_cast(s2, v[j].y);
-        const s2 c = __builtin_bit_cast(s2, v[j].z), e = __builtin_bit_cast(s2, v[j].w);
-        const s2 sm = __builtin_elementwise_max(__builtin_elementwise_max(a, b), __builtin_elementwise_max(c, e));
-        const us2 um = __builtin_elementwise_max(__builtin_elementwise_max(__builtin_bit_cast(us2, a), __builtin_bit_cast(us2, b)),
-                                                 __builtin_elementwise_max(__builtin_bit_cast(us2, c), __builtin_bit_cast(us2, e)));
+        // (the bit casts go through by-value helpers: hipcc 7.2 miscompiles
+        //  __builtin_bit_cast applied directly to an ext_vector element)
+        const uint32_t x0 = v[j].x, x1 = v[j].y, x2 = v[j].z, x3 = v[j].w;
+        const s2 sm = __builtin_elementwise_max(__builtin_elementwise_max(as_s2(x0), as_s2(x1)),
+                                                __builtin_elementwise_max(as_s2(x2), as_s2(x3)));
+        const us2 um = __builtin_elementwise_max(__builtin_elementwise_max(as_us2(x0), as_us2(x1)),
+                                                 __builtin_elementwise_max(as_us2(x2), as_us2(x3)));
         smx[j] = row_max16<0>(max((int)sm.x, (int)sm.y));
         umx[j] = row_max16<0>(max((int)um.x, (int)um.y));
     }
@@ -402,8 +407,9 @@ __device__ __forceinline__ void compute_tile(const TileCtx& c, const u4 (&v)[4],
 #pragma unroll
         for (int j = 0; j < 4; ++j) {   // unsigned min = 0xFFFF - max(0xFFFF - u)
             const us2 ones = {0xFFFF, 0xFFFF};
-            const us2 a = ones - __builtin_bit_cast(us2, v[j].x), b = ones - __builtin_bit_cast(us2, v[j].y);
-            const us2 c = ones - __builtin_bit_cast(us2, v[j].z), e = ones - __builtin_bit_cast(us2, v[j].w);
+            const uint32_t x0 = v[j].x, x1 = v[j].y, x2 = v[j].z, x3 = v[j].w;
+            const us2 a = ones - as_us2(x0), b = ones - as_us2(x1);
+            const us2 c = ones - as_us2(x2), e = ones - as_us2(x3);
             const us2 m = __builtin_elementwise_max(__builtin_elementwise_max(a, b), __builtin_elementwise_max(c, e));
             umn[j] = 0xFFFF - row_max16<0>(max((int)m.x, (int)m.y));
         }

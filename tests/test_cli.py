@@ -1,0 +1,129 @@
+"""The awq_quantizer CLI (drop-in for reference src/awq_quantizer/main.py).
+
+CPU tests: flag surface and defaults (reference main.py:22-159), tensor filter and order
+(main.py:241-259), LPT partition (main.py:395-427), output layout (main.py:430-512), exit
+codes.  GPU test: end-to-end run on a small safetensors model, every result equal to the
+oracle."""
+import json
+import os
+
+import pytest
+import torch
+from safetensors.torch import save_file
+
+
+def test_defaults_match_reference_cli():
+    from awq_quantizer.main import parse_args
+    a = parse_args(["--model_id", "m", "--output_dir", "o"])
+    assert (a.bits, a.group_size, a.symmetric, a.zero_point, a.percentile, a.scale_method, a.per_channel) == \
+        (4, 128, False, "minmax", 0.99, "mse", False)
+    assert (a.num_workers, a.max_memory, a.multi_gpu, a.batch_size, a.prefetch_factor, a.memory_efficient) == \
+        (4, 0.8, False, 10, 2, False)
+    assert (a.log_level, a.log_file, a.save_safetensors, a.chunk_size) == ("INFO", None, False, 10)
+    assert a.device == ("cuda" if torch.cuda.is_available() else "cpu")
+    with pytest.raises(SystemExit):
+        parse_args(["--model_id", "m", "--output_dir", "o", "--bits", "3"])
+    with pytest.raises(SystemExit):
+        parse_args(["--output_dir", "o"])
+
+
+def _model_dir(tmp_path, tensors, files=1):
+    d = tmp_path / "model"
+    d.mkdir()
+    names = list(tensors)
+    per = -(-len(names) // files)
+    for i in range(files):
+        part = {n: tensors[n] for n in names[i * per:(i + 1) * per]}
+        if part:
+            save_file(part, str(d / f"model-{i:05d}-of-{files:05d}.safetensors"))
+    return str(d)
+
+
+def _tensors():
+    g = torch.Generator().manual_seed(0)
+    r = lambda *s: (torch.randn(*s, generator=g) * 0.02).to(torch.bfloat16)
+    return {
+        "model.embed.weight": r(300, 256),
+        "model.layers.0.mlp.fc1.weight": r(256, 768),
+        "model.layers.0.mlp.fc1.bias": r(768),
+        "model.layers.0.ln.weight": torch.ones(256, dtype=torch.bfloat16),
+        "model.layers.0.attn.qkv.weight": r(96, 3, 64),
+        "model.layers.0.small": r(10, 10),
+        "model.layers.0.int": torch.arange(300, dtype=torch.int32),
+        "model.layers.0.fp16.weight": r(64, 256).to(torch.float16),
+    }
+
+
+def test_select_order_and_partition(tmp_path):
+    from awq_quantizer.main import partition_tensors, select_tensors
+    from awq_quantizer.model_loading import load_model_from_path
+    loader = load_model_from_path(_model_dir(tmp_path, _tensors(), files=2), logger_level="ERROR")
+    sel = select_tensors(loader.tensor_index())
+    names = [i.name for i in sel]
+    assert "model.layers.0.small" not in names and "model.layers.0.int" not in names   # numel<128, not float
+    sizes = [i.nbytes for i in sel]
+    assert sizes == sorted(sizes, reverse=True)
+    parts = partition_tensors(sel, 3)
+    assert sorted(i.name for p in parts for i in p) == sorted(names)
+    loads = [sum(i.nbytes for i in p) for p in parts]
+    assert max(loads) - min(loads) <= max(sizes)          # greedy LPT balance bound
+
+
+def test_save_layout(tmp_path):
+    from awq_quantizer.main import save_model_in_chunks
+    res = {f"t{i}": {"tensor_q": torch.zeros(4, 8, dtype=torch.int32), "scales": torch.ones(4, 1, dtype=torch.float16),
+                     "zero_points": torch.zeros(4, 1, dtype=torch.int32), "bits": torch.tensor(4, dtype=torch.int32),
+                     "group_size": torch.tensor(128, dtype=torch.int32), "symmetric": torch.tensor(False)}
+           for i in range(5)}
+    save_model_in_chunks(res, str(tmp_path / "pt"), chunk_size=2)
+    meta = json.load(open(tmp_path / "pt" / "metadata.json"))
+    assert meta["num_chunks"] == 3 and meta["num_tensors"] == 5 and meta["format"] == "pytorch"
+    assert meta["tensor_to_chunk"] == {"t0": 0, "t1": 0, "t2": 1, "t3": 1, "t4": 2}
+    assert meta["quantization_params"] == {"bits": 4, "group_size": 128, "symmetric": False}
+    chunk = torch.load(str(tmp_path / "pt" / "model_chunk_0001.pt"), weights_only=True)
+    assert set(chunk) == {"t2", "t3"} and torch.equal(chunk["t2"]["tensor_q"], res["t2"]["tensor_q"])
+    save_model_in_chunks(res, str(tmp_path / "st"), chunk_size=10, use_safetensors=True)   # works (reference: fails)
+    from safetensors.torch import load_file
+    flat = load_file(str(tmp_path / "st" / "model_chunk_0000.safetensors"))
+    assert "t4.tensor_q" in flat and json.load(open(tmp_path / "st" / "metadata.json"))["format"] == "safetensors"
+
+
+@pytest.mark.skipif(torch.cuda.is_available(), reason="checks the no-GPU exit code")
+def test_main_without_gpu_returns_1(tmp_path):
+    from awq_quantizer.main import main
+    d = _model_dir(tmp_path, _tensors())
+    assert main(["--model_id", d, "--output_dir", str(tmp_path / "out"), "--log_level", "CRITICAL"]) == 1
+
+
+def test_main_missing_model_returns_1(tmp_path):
+    from awq_quantizer.main import main
+    assert main(["--model_id", str(tmp_path / "nope"), "--output_dir", str(tmp_path / "out"),
+                 "--log_level", "CRITICAL"]) == 1
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not torch.cuda.is_available(), reason="needs the GPU")
+@pytest.mark.parametrize("fmt", ["reference", "packed"])
+def test_main_end_to_end_gpu(tmp_path, fmt):
+    from oracle import awq_oracle as orc
+    from awq_quantizer.main import main
+    tensors = _tensors()
+    d = _model_dir(tmp_path, tensors, files=2)
+    out = tmp_path / "out"
+    rc = main(["--model_id", d, "--output_dir", str(out), "--log_level", "ERROR", "--chunk_size", "3",
+               "--output_format", fmt])
+    assert rc == 0
+    meta = json.load(open(out / "metadata.json"))
+    assert meta["num_tensors"] == 6
+    for name, chunk_idx in meta["tensor_to_chunk"].items():
+        chunk = torch.load(str(out / f"model_chunk_{chunk_idx:04d}.pt"), weights_only=True)
+        res = chunk[name]
+        ref = orc.quantize(tensors[name], bits=4, group_size=128, symmetric=False, per_channel=False)
+        if fmt == "reference":
+            assert torch.equal(res["tensor_q"], ref["tensor_q"]), name
+            assert torch.equal(res["zero_points"], ref["zero_points"]), name
+            assert torch.equal(res["scales"].view(torch.int16), ref["scales"].view(torch.int16)), name
+        else:
+            rows = 1 if tensors[name].dim() <= 1 else tensors[name].shape[0]
+            assert torch.equal(res["qweight"], orc.pack_rows(ref["tensor_q"].reshape(rows, -1), 4, 0)), name
+            assert torch.equal(res["qzeros"], orc.pack_rows(ref["zero_points"], 4, 0)), name

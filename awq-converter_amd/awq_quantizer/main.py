@@ -222,7 +222,7 @@ def _to_cpu(d: Dict[str, torch.Tensor]) -> Dict[str, torch.Tensor]:
 
 def quantize_stream(loader, infos: List[TensorInfo], quantizer: AWQQuantizer, device: str, readers: int,
                     lookahead: int, packed: bool, out: Dict, lock: threading.Lock, logger,
-                    memory_efficient: bool = False) -> None:
+                    memory_efficient: bool = False, keep_on_device: bool = False) -> None:
     """Quantize `infos` on one device: `readers` threads read tensors from disk up to
     `lookahead` ahead of the GPU; each tensor is quantized as soon as it is read and its
     results are copied back to host memory."""
@@ -250,7 +250,8 @@ def quantize_stream(loader, infos: List[TensorInfo], quantizer: AWQQuantizer, de
                 if logger:
                     logger.info(f"Quantizing tensor: {info.name} on {device}")
                 res = quantizer.quantize_packed(t) if packed else quantizer.quantize(t)
-                res = _to_cpu(res)
+                if not keep_on_device:
+                    res = _to_cpu(res)
                 with lock:
                     out[info.name] = res
                 if logger:
@@ -303,6 +304,10 @@ def main(argv: Optional[List[str]] = None) -> int:
         logger.info("Preparing tensors for quantization")
         start = time.time()
         ordered = select_tensors(index, logger)
+        from . import distributed as D
+        rank, local, world = D.env_world()
+        if world > 1:   # torchrun: one process per GPU, LPT shard, RCCL gather to rank 0
+            return _main_distributed(args, loader, ordered, logger, start)
         parts = partition_tensors(ordered, len(devices))
         quantizers = {d: AWQQuantizer(bits=args.bits, group_size=args.group_size, symmetric=args.symmetric,
                                       zero_point=args.zero_point, percentile=args.percentile,
@@ -347,6 +352,76 @@ def main(argv: Optional[List[str]] = None) -> int:
         else:
             logger.error(f"Error during quantization: {e}")
         return 1
+
+
+_SCALARS = ("bits", "group_size", "symmetric", "shape")
+
+
+def _main_distributed(args, loader, ordered: List[TensorInfo], logger, start: float) -> int:
+    """torchrun mode: rank r quantizes the tensors an LPT partition by bytes assigns it
+    (identical on every rank, no exchange), keeps its results in HBM, then every result
+    is sent to rank 0 in one batched point-to-point round over RCCL (xGMI) and rank 0
+    writes the reference output layout.  Exit code agreed by all ranks."""
+    from . import distributed as D
+    import torch.distributed as dist
+    backend = os.environ.get("AWQ_DIST_BACKEND", "nccl")      # gloo: tests with 2 ranks on one GPU
+    if backend != "nccl":
+        D.init(backend)
+    rank, local, world = D.init("nccl") if backend == "nccl" else D.env_world()
+    device = f"cuda:{local % max(1, torch.cuda.device_count())}"
+    comm = torch.device(device) if backend == "nccl" else torch.device("cpu")
+    owner = dict(zip((i.name for i in ordered), D.shard([i.nbytes for i in ordered], world)))
+    mine = [i for i in ordered if owner[i.name] == rank]
+    q = AWQQuantizer(bits=args.bits, group_size=args.group_size, symmetric=args.symmetric, zero_point=args.zero_point,
+                     percentile=args.percentile, scale_method=args.scale_method, per_channel=args.per_channel,
+                     device=device, logger_name=f"awq_quantizer_{device}", logger_level=args.log_level,
+                     logger_to_file=args.log_file is not None, logger_file_path=args.log_file)
+    logger.info(f"rank {rank}/{world}: {len(mine)} of {len(ordered)} tensors on {device}")
+    results: Dict[str, Dict[str, torch.Tensor]] = {}
+    quantize_stream(loader, mine, q, device, args.num_workers, max(1, args.prefetch_factor * args.batch_size),
+                    args.output_format == "packed", results, threading.Lock(), logger, args.memory_efficient,
+                    keep_on_device=True)
+    # which tensors succeeded, and the shapes rank 0 must receive (tiny metadata)
+    meta = {n: {f: (tuple(t.shape), str(t.dtype)) for f, t in r.items() if f not in _SCALARS}
+            for n, r in results.items()}
+    all_meta = [None] * world
+    dist.all_gather_object(all_meta, meta)
+    ok_owner, shapes = {}, {}
+    for r, m in enumerate(all_meta):
+        for n, fields in m.items():
+            ok_owner[n] = r
+            shapes[n] = {f: (shp, getattr(torch, dt.split(".")[-1])) for f, (shp, dt) in fields.items()}
+    payload = {n: {f: t.to(comm) for f, t in r.items() if f not in _SCALARS} for n, r in results.items()}
+    merged = D.gather_to_rank0(payload, ok_owner, shapes, comm)
+    rc = 0
+    if rank == 0:
+        scal = {"bits": torch.tensor(args.bits, dtype=torch.int32),
+                "group_size": torch.tensor(args.group_size, dtype=torch.int32),
+                "symmetric": torch.tensor(args.symmetric, dtype=torch.bool)}
+        quantized = {}
+        for info in ordered:
+            if info.name in merged:
+                d = _to_cpu(merged[info.name])
+                d.update(scal)
+                if args.output_format == "packed":
+                    d["shape"] = torch.tensor(list(info.shape), dtype=torch.int64)
+                quantized[info.name] = d
+        if not quantized:
+            logger.error("No tensors were successfully quantized")
+            rc = 1
+        else:
+            logger.info(f"Successfully quantized {len(quantized)} tensors on {world} GPUs")
+            try:
+                save_model_in_chunks(quantized, args.output_dir, chunk_size=args.chunk_size,
+                                     use_safetensors=args.save_safetensors, logger=logger)
+                logger.info(f"Quantization complete in {time.time() - start:.2f} seconds")
+            except Exception as e:  # noqa: BLE001
+                logger.error(f"Failed to save quantized model: {e}")
+                rc = 1
+    flag = torch.tensor([rc], dtype=torch.int32, device=comm)
+    dist.broadcast(flag, 0)
+    dist.destroy_process_group()
+    return int(flag.item())
 
 
 if __name__ == "__main__":

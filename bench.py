@@ -70,6 +70,7 @@ def parse():
                     help="input replicas rotated across steps (0 = enough to exceed the 256 MiB Infinity Cache)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-seconds", type=float, default=15.0)
+    ap.add_argument("--events", default="step", choices=["step", "span"])
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     return ap.parse_args()
 
@@ -113,18 +114,12 @@ def cpu_baseline(shapes, budget_s):
 
 def main():
     args = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    from awq_quantizer import _hip
+    from awq_quantizer import distributed as D
+    from awq_quantizer.quantization.batch import PackedBatch
+    rank, local, world = D.init("nccl")          # RCCL; one process per GPU (torchrun)
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
-
-    from awq_quantizer import _hip
-    from awq_quantizer.quantization.batch import PackedBatch
     _hip.require_device(dev)
 
     shapes = shapes_of(args.workload)
@@ -139,35 +134,36 @@ def main():
     torch.cuda.synchronize()
     algo_bytes = batches[0].algorithmic_bytes()
 
-    def barrier():
-        if world > 1:
-            import torch.distributed as dist
-            dist.barrier()
-
+    barrier = D.barrier
     stream = torch.cuda.current_stream(dev)
     for i in range(args.warmup):
         batches[i % reps].run(stream)
     torch.cuda.synchronize()
 
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    # HIP events on the kernel's stream: around every launch ("step", default) or one
+    # pair around all K launches ("span": fewer markers in the queue, includes the gaps)
+    n_ev = args.steps if args.events == "step" else 1
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(n_ev)]
     barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for i in range(args.steps):
-        ev[i][0].record(stream)
-        batches[i % reps].run(stream)
-        ev[i][1].record(stream)
+    if args.events == "step":
+        for i in range(args.steps):
+            ev[i][0].record(stream)
+            batches[i % reps].run(stream)
+            ev[i][1].record(stream)
+    else:
+        ev[0][0].record(stream)
+        for i in range(args.steps):
+            batches[i % reps].run(stream)
+        ev[0][1].record(stream)
     torch.cuda.synchronize()
     barrier()
     elapsed = time.perf_counter() - t0
     kern_ms = [a.elapsed_time(b) for a, b in ev]
-    kern_avg_s = sum(kern_ms) / len(kern_ms) / 1e3
+    kern_avg_s = sum(kern_ms) / args.steps / 1e3
 
-    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-    if world > 1:
-        import torch.distributed as dist
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed = float(t.item())
+    elapsed = D.max_over_ranks(elapsed, dev)
 
     if rank != 0:
         if world > 1:
@@ -197,7 +193,7 @@ def main():
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                      "algorithmic_bytes_per_launch": algo_bytes,
-                     "kernel_avg_us": round(kern_avg_s * 1e6, 2)},
+                     "kernel_avg_us": round(kern_avg_s * 1e6, 2), "timing": f"hip events ({args.events})"},
     }
     if not args.no_cpu_baseline:
         gbs, secs, nbytes, nparts = cpu_baseline(shapes, args.cpu_sample_seconds)

@@ -127,3 +127,36 @@ def test_main_end_to_end_gpu(tmp_path, fmt):
             rows = 1 if tensors[name].dim() <= 1 else tensors[name].shape[0]
             assert torch.equal(res["qweight"], orc.pack_rows(ref["tensor_q"].reshape(rows, -1), 4, 0)), name
             assert torch.equal(res["qzeros"], orc.pack_rows(ref["zero_points"], 4, 0)), name
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not torch.cuda.is_available(), reason="needs the GPU")
+def test_main_torchrun_two_ranks_gpu(tmp_path):
+    """torchrun, 2 ranks sharing the box's GPU (gloo for the gather: RCCL refuses two ranks
+    on one device); rank 0 must write every tensor, equal to the oracle."""
+    import socket
+    import subprocess
+    import sys
+    from oracle import awq_oracle as orc
+    tensors = _tensors()
+    d = _model_dir(tmp_path, tensors, files=2)
+    out = tmp_path / "out"
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, AWQ_DIST_BACKEND="gloo",
+               PYTHONPATH=os.pathsep.join([os.path.join(root, "awq-converter_amd"), root]))
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", f"--master-port={port}", "-m", "awq_quantizer.main",
+           "--model_id", d, "--output_dir", str(out), "--log_level", "ERROR", "--output_format", "packed"]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    meta = json.load(open(out / "metadata.json"))
+    assert meta["num_tensors"] == 6
+    for name, ci in meta["tensor_to_chunk"].items():
+        res = torch.load(str(out / f"model_chunk_{ci:04d}.pt"), weights_only=True)[name]
+        ref = orc.quantize(tensors[name], bits=4, group_size=128, symmetric=False)
+        rows = 1 if tensors[name].dim() <= 1 else tensors[name].shape[0]
+        assert torch.equal(res["qweight"], orc.pack_rows(ref["tensor_q"].reshape(rows, -1), 4, 0)), name
+        assert torch.equal(res["scales"].view(torch.int16), ref["scales"].view(torch.int16)), name

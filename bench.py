@@ -70,7 +70,8 @@ def parse():
                     help="input replicas rotated across steps (0 = enough to exceed the 256 MiB Infinity Cache)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-seconds", type=float, default=15.0)
-    ap.add_argument("--events", default="step", choices=["step", "span"])
+    ap.add_argument("--events", default="span", choices=["step", "span"])
+    ap.add_argument("--no-copy-ceiling", action="store_true")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     return ap.parse_args()
 
@@ -82,6 +83,25 @@ def make_set(shapes, seed0, dev):
         g.manual_seed(seed0 + i)
         tensors[f"t{i:04d}"] = (torch.randn(*s, generator=g, device=dev, dtype=torch.float32) * 0.02).to(torch.bfloat16)
     return tensors
+
+
+def copy_ceiling(dev, stream, nbytes=1 << 30, iters=10):
+    """Device-to-device copy of `nbytes` (read + write counted) on the bench stream: the
+    measured HBM ceiling SURVEY.md §8(d) asks the kernel's rate to be quoted against."""
+    src = torch.empty(nbytes // 4, dtype=torch.int32, device=dev).fill_(1)
+    dst = torch.empty_like(src)
+    with torch.cuda.stream(stream):
+        for _ in range(3):
+            dst.copy_(src)
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(stream)
+        for _ in range(iters):
+            dst.copy_(src)
+        b.record(stream)
+    torch.cuda.synchronize()
+    gbs = 2 * nbytes * iters / (a.elapsed_time(b) / 1e3) / 1e9
+    del src, dst
+    return gbs
 
 
 def cpu_baseline(shapes, budget_s):
@@ -140,8 +160,10 @@ def main():
         batches[i % reps].run(stream)
     torch.cuda.synchronize()
 
-    # HIP events on the kernel's stream: around every launch ("step", default) or one
-    # pair around all K launches ("span": fewer markers in the queue, includes the gaps)
+    # HIP events on the kernel's stream.  "span" (default): one pair around the K back-to-back
+    # launches -> average launch duration incl. the sub-us dispatch gaps; it agrees with the
+    # rocprofv3 kernel average within ~1.5 % (profiles/r15_*).  "step": a pair around every
+    # launch; each marker adds ~4 us to the queue (r15: 70.5 us vs rocprof 67.8 us).
     n_ev = args.steps if args.events == "step" else 1
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(n_ev)]
     barrier()
@@ -162,6 +184,7 @@ def main():
     elapsed = time.perf_counter() - t0
     kern_ms = [a.elapsed_time(b) for a, b in ev]
     kern_avg_s = sum(kern_ms) / args.steps / 1e3
+    ceiling = None if args.no_copy_ceiling or rank != 0 else copy_ceiling(dev, stream)
 
     elapsed = D.max_over_ranks(elapsed, dev)
 
@@ -195,6 +218,9 @@ def main():
                      "algorithmic_bytes_per_launch": algo_bytes,
                      "kernel_avg_us": round(kern_avg_s * 1e6, 2), "timing": f"hip events ({args.events})"},
     }
+    if ceiling:
+        line["roofline"]["copy_ceiling"] = round(ceiling, 1)
+        line["roofline"]["frac_of_copy"] = round(achieved / ceiling, 4)
     if not args.no_cpu_baseline:
         gbs, secs, nbytes, nparts = cpu_baseline(shapes, args.cpu_sample_seconds)
         line["cpu_baseline"] = {"value": round(gbs, 5), "unit": "GB/s", "cores": 1, "kind": "port",

@@ -38,6 +38,7 @@ SIGNATURES = {
     "awq_last_error": (ctypes.c_char_p, []),
     "awq_device_check": (_I32, [ctypes.c_char_p, _I32]),
     "awq_quantize_groups": (_I32, [_P, _I32, _I64, _I64, _I64, _I32, _I32, _P, _P, _P, _P, _P, _P]),
+    "awq_quantize_search": (_I32, [_P, _I32, _I64, _I64, _I64, _I32, _I32, _I32, _I32, _P, _P, _P, _P, _P, _P]),
     "awq_ragged_eligible": (_I32, [_I32, _I64, _I64, _I64]),
     "awq_plan_ragged": (_I64, [ctypes.POINTER(TensorDesc), _I32, _I32]),
     "awq_quantize_ragged": (_I32, [_P, _I32, _I64, _I32, _I32, _P]),
@@ -120,6 +121,17 @@ def quantize_groups(x: torch.Tensor, rows: int, K: int, L: int, bits: int, symme
                                  ptr(qweight), ptr(qzeros), ptr(scales), ptr(tensor_q), ptr(zeros),
                                  ctypes.c_void_p(stream_ptr(x.device)))
     check(rc, "awq_quantize_groups")
+
+
+def quantize_search(x: torch.Tensor, rows: int, K: int, L: int, bits: int, symmetric: bool, n_grid: int,
+                    n_candidates: int, *, qweight=None, qzeros=None, scales=None, tensor_q=None,
+                    zeros=None) -> None:
+    """Launch awq_quantize_search (opt-in clip search, include/awq_hip.h)."""
+    lib = load_library()
+    rc = lib.awq_quantize_search(ptr(x), AWQ_DTYPE[x.dtype], rows, K, L, bits, int(bool(symmetric)),
+                                 int(n_grid), int(n_candidates), ptr(qweight), ptr(qzeros), ptr(scales),
+                                 ptr(tensor_q), ptr(zeros), ctypes.c_void_p(stream_ptr(x.device)))
+    check(rc, "awq_quantize_search")
 
 
 def ragged_eligible(dtype: torch.dtype, rows: int, K: int, L: int) -> bool:

@@ -51,8 +51,12 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--zero_point", type=str, default="minmax", choices=["none", "minmax", "percentile"],
                    help="Zero point calibration method")
     p.add_argument("--percentile", type=float, default=0.99, help="Percentile for zero point calibration")
-    p.add_argument("--scale_method", type=str, default="mse", choices=["minmax", "mse"],
-                   help="Scale calibration method")
+    p.add_argument("--scale_method", type=str, default="mse", choices=["minmax", "mse", "search"],
+                   help="Scale calibration method (minmax/mse: round-to-nearest as the reference; "
+                        "search: per-group clip search, opt-in extension)")
+    p.add_argument("--search_grid", type=int, default=20, help="scale_method=search: grid size")
+    p.add_argument("--search_max_shrink", type=float, default=0.5,
+                   help="scale_method=search: largest shrink of the group range tried")
     p.add_argument("--per_channel", action="store_true", help="Use per-channel quantization")
     p.add_argument("--device", type=str, default="cuda" if torch.cuda.is_available() else "cpu",
                    help="Device to use for quantization (cuda, cuda:0, cuda:1, cpu, or 'all' for all GPUs)")
@@ -312,6 +316,7 @@ def main(argv: Optional[List[str]] = None) -> int:
         quantizers = {d: AWQQuantizer(bits=args.bits, group_size=args.group_size, symmetric=args.symmetric,
                                       zero_point=args.zero_point, percentile=args.percentile,
                                       scale_method=args.scale_method, per_channel=args.per_channel, device=d,
+                                      search_grid=args.search_grid, search_max_shrink=args.search_max_shrink,
                                       logger_name=f"awq_quantizer_{d}", logger_level=args.log_level,
                                       logger_to_file=args.log_file is not None, logger_file_path=args.log_file)
                       for d in devices}
@@ -374,7 +379,8 @@ def _main_distributed(args, loader, ordered: List[TensorInfo], logger, start: fl
     mine = [i for i in ordered if owner[i.name] == rank]
     q = AWQQuantizer(bits=args.bits, group_size=args.group_size, symmetric=args.symmetric, zero_point=args.zero_point,
                      percentile=args.percentile, scale_method=args.scale_method, per_channel=args.per_channel,
-                     device=device, logger_name=f"awq_quantizer_{device}", logger_level=args.log_level,
+                     search_grid=args.search_grid, search_max_shrink=args.search_max_shrink, device=device,
+                     logger_name=f"awq_quantizer_{device}", logger_level=args.log_level,
                      logger_to_file=args.log_file is not None, logger_file_path=args.log_file)
     logger.info(f"rank {rank}/{world}: {len(mine)} of {len(ordered)} tensors on {device}")
     results: Dict[str, Dict[str, torch.Tensor]] = {}

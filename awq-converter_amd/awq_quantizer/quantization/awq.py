@@ -11,7 +11,9 @@ the reference CPU path (tests/test_gpu_parity.py against the oracle and the gold
 fixtures).
 
 Extensions (no reference counterpart): quantize_packed / quantize_model_packed keep the
-packed int4/int8 words (qweight/qzeros) and fp16 scales on the device for throughput.
+packed int4/int8 words (qweight/qzeros) and fp16 scales on the device for throughput;
+scale_method="search" (new value, opt-in) runs the per-group clip search of
+include/awq_hip.h awq_quantize_search instead of plain RTN ("mse"/"minmax" stay RTN).
 """
 
 import math
@@ -42,6 +44,8 @@ class AWQQuantizer:
         logger_level: str = "INFO",
         logger_to_file: bool = False,
         logger_file_path: Optional[str] = None,
+        search_grid: int = 20,
+        search_max_shrink: float = 0.5,
     ):
         self.bits = bits
         self.group_size = group_size
@@ -52,6 +56,10 @@ class AWQQuantizer:
         # reference's round-to-nearest scales (awq.py:66 stores it, nothing reads it)
         self.scale_method = scale_method
         self.per_channel = per_channel
+        # scale_method="search" only: candidates alpha = 1 - i/search_grid,
+        # i < int(search_max_shrink * search_grid) (alpha = 1 first: RTN wins ties)
+        self.search_grid = search_grid
+        self.search_max_shrink = search_max_shrink
 
         # device string semantics of awq.py:70-77
         if device is None:
@@ -79,8 +87,27 @@ class AWQQuantizer:
             raise ValueError(f"Unsupported zero point calibration method: {self.zero_point}")
         if self.zero_point == "percentile" and (self.percentile <= 0 or self.percentile >= 1):
             raise ValueError(f"Percentile must be in range (0, 1): {self.percentile}")
-        if self.scale_method not in ["minmax", "mse"]:
+        if self.scale_method not in ["minmax", "mse", "search"]:
             raise ValueError(f"Unsupported scale calibration method: {self.scale_method}")
+        if self.scale_method == "search":
+            if not isinstance(self.search_grid, int) or self.search_grid < 1:
+                raise ValueError(f"search_grid must be a positive integer: {self.search_grid}")
+            if not (0 < self.search_max_shrink <= 1):
+                raise ValueError(f"search_max_shrink must be in (0, 1]: {self.search_max_shrink}")
+
+    @property
+    def search_candidates(self) -> int:
+        """Number of clip candidates of scale_method="search" (0 = plain RTN)."""
+        if self.scale_method != "search":
+            return 0
+        return min(self.search_grid, max(1, int(self.search_max_shrink * self.search_grid)))
+
+    def _launch(self, x, rows, K, L, **outs) -> None:
+        if self.scale_method == "search":
+            _hip.quantize_search(x, rows, K, L, self.bits, self.symmetric, self.search_grid,
+                                 self.search_candidates, **outs)
+        else:
+            _hip.quantize_groups(x, rows, K, L, self.bits, self.symmetric, **outs)
 
     def _calculate_qmin_qmax(self) -> Tuple[int, int]:
         """awq.py:114-128."""
@@ -153,8 +180,7 @@ class AWQQuantizer:
         tensor_q = torch.empty(rows * K, dtype=torch.int32, device=dev)
         scales = torch.empty((rows, G), dtype=torch.float16, device=dev)
         zeros = torch.empty((rows, G), dtype=torch.int32, device=dev)
-        _hip.quantize_groups(x, rows, K, L, self.bits, self.symmetric, scales=scales, tensor_q=tensor_q,
-                             zeros=zeros)
+        self._launch(x, rows, K, L, scales=scales, tensor_q=tensor_q, zeros=zeros)
         if small == "tensor":
             scales, zeros = scales.reshape(()), zeros.reshape(())
         elif small == "row":
@@ -231,11 +257,11 @@ class AWQQuantizer:
         qzeros = torch.empty(sh["qzeros"], dtype=torch.int32, device=dev)
         scales = torch.empty(sh["scales"], dtype=torch.float16, device=dev)
         kw = {}
-        if not _hip.ragged_eligible(x.dtype, sh["rows"], sh["K"], self.group_size):
+        if self.search_candidates or not _hip.ragged_eligible(x.dtype, sh["rows"], sh["K"], self.group_size):
             kw = dict(tensor_q=torch.empty(sh["rows"] * sh["K"], dtype=torch.int32, device=dev),
                       zeros=torch.empty(sh["scales"], dtype=torch.int32, device=dev))
-        _hip.quantize_groups(x, sh["rows"], sh["K"], self.group_size, self.bits, self.symmetric,
-                             qweight=qweight, qzeros=qzeros, scales=scales, **kw)
+        self._launch(x, sh["rows"], sh["K"], self.group_size, qweight=qweight, qzeros=qzeros, scales=scales,
+                     **kw)
         return {"qweight": qweight, "qzeros": qzeros, "scales": scales,
                 "bits": torch.tensor(self.bits, dtype=torch.int32),
                 "group_size": torch.tensor(self.group_size, dtype=torch.int32),
@@ -259,7 +285,8 @@ class AWQQuantizer:
                 self.logger.error(f"Error quantizing tensor: {name}, error: numel < group_size")
                 continue
             rows = 1 if t.dim() <= 1 else t.shape[0]
-            if _hip.ragged_eligible(t.dtype, rows, t.numel() // rows, self.group_size):
+            if not self.search_candidates and _hip.ragged_eligible(t.dtype, rows, t.numel() // rows,
+                                                                   self.group_size):
                 eligible[name] = t
             else:
                 rest[name] = t

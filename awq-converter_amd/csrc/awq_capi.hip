@@ -110,6 +110,35 @@ int awq_quantize_groups(const void* w, int dtype, int64_t rows, int64_t K, int64
     return AWQ_OK;
 }
 
+int awq_quantize_search(const void* w, int dtype, int64_t rows, int64_t K, int64_t group_size, int bits,
+                        int symmetric, int n_grid, int n_candidates, int32_t* qweight, int32_t* qzeros,
+                        uint16_t* scales, int32_t* tensor_q, int32_t* zeros, void* stream) {
+    g_err.clear();
+    if (int rc = check_common(rows, K, group_size, bits)) return rc;
+    if (dtype < AWQ_DTYPE_BF16 || dtype > AWQ_DTYPE_F64) return fail(AWQ_EINVAL, "unknown dtype code %d", dtype);
+    if (n_grid < 1 || n_candidates < 1 || n_candidates > n_grid)
+        return fail(AWQ_EINVAL, "search grid needs 1 <= n_candidates (%d) <= n_grid (%d)", n_candidates, n_grid);
+    if (!qweight && !qzeros && !scales && !tensor_q && !zeros) return fail(AWQ_EINVAL, "no output requested");
+    if (rows * K == 0) return AWQ_OK;
+    if (!w) return fail(AWQ_EINVAL, "null input");
+    if ((qweight && !tensor_q) || (qzeros && !zeros))
+        return fail(AWQ_EINVAL, "packed outputs of the search kernel need the int32 tensor_q/zeros buffers "
+                                "as staging (pass them too)");
+    hipStream_t s = (hipStream_t)stream;
+    const int qmin = symmetric ? -(1 << (bits - 1)) : 0;
+    if (int rc = hip_status(awq::launch_generic(w, dtype, rows, K, group_size, bits, symmetric, tensor_q,
+                                                scales, zeros, s, n_grid, n_candidates), "awq search kernel"))
+        return rc;
+    const int64_t G = (K + group_size - 1) / group_size;
+    if (qweight)
+        if (int rc = hip_status(awq::launch_pack(tensor_q, rows, K, bits, qmin, qweight, s), "awq pack"))
+            return rc;
+    if (qzeros)
+        if (int rc = hip_status(awq::launch_pack(zeros, rows, G, bits, qmin, qzeros, s), "awq pack"))
+            return rc;
+    return AWQ_OK;
+}
+
 int64_t awq_plan_ragged(awq_tensor_desc* descs, int n, int bits) {
     g_err.clear();
     if (n < 0 || (n > 0 && !descs)) return fail(AWQ_EINVAL, "bad descriptor array"), -1;

@@ -113,10 +113,59 @@ template <typename C> __device__ __forceinline__ int32_t to_i32(C v) {         /
     return (v != v) ? INT32_MIN : (int32_t)v;
 }
 
+template <typename C> __device__ __forceinline__ C wave_sum(C v) {
+    // xor butterfly: lane l and lane l^o add the same two values, so every lane ends with
+    // the same, fixed-order tree sum (oracle_quantize_search restates this tree exactly)
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = v + __shfl_xor(v, o, 64);
+    return v;
+}
+
+// awq.py:196-213: scale and zero point of one group from its (NaN-propagated) min/max.
 template <int DT>
+__device__ __forceinline__ void group_params(typename Traits<DT>::C mn, typename Traits<DT>::C mx, int nan,
+                                             int qmin, int qmax, int sym, typename Traits<DT>::C& s_out,
+                                             typename Traits<DT>::C& z_out) {
+    typedef Traits<DT> T;
+    typedef typename T::C C;
+    if (sym) {                                   // awq.py:196-199 (Python max)
+        C amn = absv(mn), amx = absv(mx);   // torch.abs(-0) = +0
+        if (nan) { amn = mn; amx = mx; }
+        C a = (amx > amn) ? amx : amn;
+        mn = -a;
+        mx = a;
+    }
+    C s = T::rn(T::rn(mx - mn) / (C)(qmax - qmin));          // awq.py:202
+    if (!(s != s) && s < T::lo()) s = T::lo();                 // awq.py:205
+    C z = (C)0;
+    if (!sym) {                                                // awq.py:210-211
+        C y = T::rn(mn / s);
+        z = T::rn((C)qmin - y);
+        z = clampq(T::rn(rnd(z)), (C)qmin, (C)qmax);
+    }
+    s_out = s;
+    z_out = z;
+}
+
+template <int DT>
+__device__ __forceinline__ typename Traits<DT>::C quant1(typename Traits<DT>::C v, typename Traits<DT>::C s,
+                                                         typename Traits<DT>::C z, int qmin, int qmax) {
+    typedef Traits<DT> T;
+    typedef typename T::C C;
+    C t = T::rn(T::rn(v / s) + z);                     // awq.py:245
+    return clampq(T::rn(rnd(t)), (C)qmin, (C)qmax);    // awq.py:248
+}
+
+// SEARCH (opt-in scale_method="search"; no reference counterpart): before
+// the RTN parameters are taken, the group's [min, max] is shrunk by alpha_i = (n_grid-i)/n_grid,
+// i < n_cand, and the candidate whose dequantized group (the reference's dequantize:
+// fp16(fp16(q - z) * fp16(s)), awq.py:459-539) has the smallest squared error wins; ties and
+// NaN/inf groups keep i = 0, i.e. exactly the RTN result.
+template <int DT, bool SEARCH>
 __global__ __launch_bounds__(256) void awq_generic_kernel(const void* __restrict__ wv, int64_t rows,
                                                           int64_t K, int64_t L, int qmin, int qmax,
-                                                          int sym, int32_t* __restrict__ tensor_q,
+                                                          int sym, int n_grid, int n_cand,
+                                                          int32_t* __restrict__ tensor_q,
                                                           uint16_t* __restrict__ scales,
                                                           int32_t* __restrict__ zeros) {
     typedef Traits<DT> T;
@@ -146,32 +195,43 @@ __global__ __launch_bounds__(256) void awq_generic_kernel(const void* __restrict
         mx = wave_max(mx);
         nan = wave_or(nan);
         if (nan) { mn = (C)NAN; mx = (C)NAN; }
-        if (sym) {                                   // awq.py:196-199 (Python max)
-            C amn = absv(mn), amx = absv(mx);   // torch.abs(-0) = +0
-            if (nan) { amn = mn; amx = mx; }
-            C a = (amx > amn) ? amx : amn;
-            mn = -a;
-            mx = a;
+        if (SEARCH && !nan) {
+            if (sym) {
+                C a = (absv(mx) > absv(mn)) ? absv(mx) : absv(mn);
+                mn = -a;
+                mx = a;
+            }
+            C best = (C)INFINITY;
+            int bi = 0;
+            for (int i = 0; i < n_cand; ++i) {
+                const C al = (C)(n_grid - i) / (C)n_grid;
+                C cs, cz;
+                group_params<DT>(T::rn(mn * al), T::rn(mx * al), 0, qmin, qmax, sym, cs, cz);
+                const float sh = sw_f16_to_f32(canon_f16((float)cs));
+                C acc = (C)0;
+                for (int64_t k = k0 + lane; k < k1; k += 64) {
+                    const C v = T::load(w, base + k);
+                    const C q = quant1<DT>(v, cs, cz, qmin, qmax);
+                    const float h = sw_f16_to_f32(sw_f32_to_f16((float)(q - cz)));
+                    const C d = v - (C)sw_f16_to_f32(sw_f32_to_f16(h * sh));
+                    acc = acc + d * d;
+                }
+                acc = wave_sum(acc);
+                if (acc < best) { best = acc; bi = i; }
+            }
+            const C al = (C)(n_grid - bi) / (C)n_grid;
+            mn = T::rn(mn * al);
+            mx = T::rn(mx * al);
         }
-        C s = T::rn(T::rn(mx - mn) / (C)(qmax - qmin));          // awq.py:202
-        if (!(s != s) && s < T::lo()) s = T::lo();                 // awq.py:205
-        C z = (C)0;
-        if (!sym) {                                                // awq.py:210-211
-            C y = T::rn(mn / s);
-            z = T::rn((C)qmin - y);
-            z = clampq(T::rn(rnd(z)), (C)qmin, (C)qmax);
-        }
+        C s, z;
+        group_params<DT>(mn, mx, nan, qmin, qmax, sym, s, z);
         if (lane == 0) {
             if (scales) scales[gi] = canon_f16((float)s);         // fp64: via fp32 (awq.py:327)
             if (zeros) zeros[gi] = to_i32(z);
         }
         if (tensor_q) {
-            for (int64_t k = k0 + lane; k < k1; k += 64) {
-                C v = T::load(w, base + k);
-                C t = T::rn(T::rn(v / s) + z);                     // awq.py:245
-                t = clampq(T::rn(rnd(t)), (C)qmin, (C)qmax);   // awq.py:248
-                tensor_q[base + k] = to_i32(t);
-            }
+            for (int64_t k = k0 + lane; k < k1; k += 64)
+                tensor_q[base + k] = to_i32(quant1<DT>(T::load(w, base + k), s, z, qmin, qmax));
         }
     }
 }
@@ -235,14 +295,21 @@ inline unsigned grid_for(int64_t work, int64_t per_block, int64_t cap) {
 
 hipError_t launch_generic(const void* w, int dtype, int64_t rows, int64_t K, int64_t L, int bits,
                           int symmetric, int32_t* tensor_q, uint16_t* scales, int32_t* zeros,
-                          hipStream_t stream) {
+                          hipStream_t stream, int n_grid, int n_cand) {
     const int qmin = symmetric ? -(1 << (bits - 1)) : 0;
     const int qmax = symmetric ? (1 << (bits - 1)) - 1 : (1 << bits) - 1;
     const int64_t G = (K + L - 1) / L;
     const unsigned grid = grid_for(rows * G, 4, 256 * 16);
-#define AWQ_GEN(D) \
-    hipLaunchKernelGGL(awq_generic_kernel<D>, dim3(grid), dim3(256), 0, stream, w, rows, K, L, qmin, \
-                       qmax, symmetric, tensor_q, scales, zeros)
+    const bool search = n_cand > 0;
+#define AWQ_GEN(D)                                                                                   \
+    do {                                                                                             \
+        if (search)                                                                                  \
+            hipLaunchKernelGGL((awq_generic_kernel<D, true>), dim3(grid), dim3(256), 0, stream, w, rows, \
+                               K, L, qmin, qmax, symmetric, n_grid, n_cand, tensor_q, scales, zeros);  \
+        else                                                                                         \
+            hipLaunchKernelGGL((awq_generic_kernel<D, false>), dim3(grid), dim3(256), 0, stream, w,     \
+                               rows, K, L, qmin, qmax, symmetric, 1, 0, tensor_q, scales, zeros);      \
+    } while (0)
     switch (dtype) {
     case AWQ_DTYPE_BF16: AWQ_GEN(AWQ_DTYPE_BF16); break;
     case AWQ_DTYPE_F16: AWQ_GEN(AWQ_DTYPE_F16); break;

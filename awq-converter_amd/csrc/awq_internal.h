@@ -74,7 +74,7 @@ hipError_t launch_fast(const awq_tensor_desc* descs_dev, const awq_tensor_desc* 
                        int64_t total_tiles, int bits, int symmetric, hipStream_t stream);
 hipError_t launch_generic(const void* w, int dtype, int64_t rows, int64_t K, int64_t L, int bits,
                           int symmetric, int32_t* tensor_q, uint16_t* scales, int32_t* zeros,
-                          hipStream_t stream);
+                          hipStream_t stream, int n_grid = 1, int n_cand = 0);
 hipError_t launch_selftest(int which, unsigned long long* out, hipStream_t stream);
 hipError_t launch_pack(const int32_t* v, int64_t rows, int64_t n, int bits, int qmin,
                        int32_t* packed, hipStream_t stream);

@@ -83,6 +83,19 @@ int awq_quantize_groups(const void* w, int dtype, int64_t rows, int64_t K, int64
                         int bits, int symmetric, int32_t* qweight, int32_t* qzeros,
                         uint16_t* scales, int32_t* tensor_q, int32_t* zeros, void* stream);
 
+/* Opt-in per-group clip search (scale_method="search"; no reference counterpart: the
+ * reference stores scale_method but never uses it, awq.py:66,111-112 — SURVEY.md §8a).
+ * Same inputs/outputs as awq_quantize_groups.  For every group the min/max (after the
+ * symmetric abs-max, awq.py:196-199) are shrunk by alpha_i = (n_grid - i) / n_grid,
+ * i = 0 .. n_candidates-1, each candidate's scale/zero point taken exactly as RTN
+ * (awq.py:202-211), and the candidate with the smallest sum of squared errors between
+ * the group and its dequantization (awq.py:459-539 arithmetic) is kept; ties and NaN/inf
+ * groups keep i = 0, i.e. the RTN result bit-exactly.  1 <= n_candidates <= n_grid.
+ * Packed outputs need tensor_q / zeros as staging buffers. */
+int awq_quantize_search(const void* w, int dtype, int64_t rows, int64_t K, int64_t group_size, int bits,
+                        int symmetric, int n_grid, int n_candidates, int32_t* qweight, int32_t* qzeros,
+                        uint16_t* scales, int32_t* tensor_q, int32_t* zeros, void* stream);
+
 /* True (1) if a tensor of this dtype/shape is eligible for awq_quantize_ragged. */
 int awq_ragged_eligible(int dtype, int64_t rows, int64_t K, int64_t group_size);
 

@@ -189,6 +189,109 @@ int oracle_quantize(const void* x, int dtype, int64_t rows, int64_t K, int64_t L
     return 0;
 }
 
+/* Opt-in clip search (scale_method="search").  NOT in the reference (it stores
+ * scale_method, awq.py:66, validates it, :111-112, and never reads it again), so this
+ * restates the product's own definition (include/awq_hip.h, awq_quantize_search) — parity
+ * between it and the HIP kernel is checked, parity with the reference is unpinned except
+ * for candidate 0, which IS the RTN path above (golden-pinned).
+ *
+ * Per group: mn/mx as in oracle_quantize; sym -> (-a, a) with a = Python max(|mn|,|mx|);
+ * candidate i scales both ends by alpha_i = (n_grid - i) / n_grid (computed in the compute
+ * type, product rounded to D), takes (s, z) by awq.py:202-211, quantizes every element
+ * (awq.py:245-248) and dequantizes it the reference's way (awq.py:459-539:
+ * fp16(fp16(q - z) * fp16(s))).  err = sum (x - dq)^2 in the compute type, summed in the
+ * HIP kernel's fixed order: lane l (0..63) accumulates elements k0+l, k0+l+64, ... in
+ * sequence, then an xor butterfly t[l] = a[l] + a[l^o] for o = 32, 16, .., 1.  Smallest
+ * err wins, ties -> smaller i; NaN groups skip the search. */
+static double cadd(double a, double b, int f64) { return f64 ? a + b : (double)((float)a + (float)b); }
+static double cmul(double a, double b, int f64) { return f64 ? a * b : (double)((float)a * (float)b); }
+static double csub(double a, double b, int f64) { return f64 ? a - b : (double)((float)a - (float)b); }
+
+static double tree_sum64(double* a, int f64) {
+    double t[64];
+    for (int o = 32; o > 0; o >>= 1) {
+        for (int l = 0; l < 64; ++l) t[l] = cadd(a[l], a[l ^ o], f64);
+        memcpy(a, t, sizeof t);
+    }
+    return a[0];
+}
+
+int oracle_quantize_search(const void* x, int dtype, int64_t rows, int64_t K, int64_t L, int bits,
+                           int sym, int n_grid, int n_cand, int32_t* tensor_q, uint16_t* scales_f16,
+                           int32_t* zeros) {
+    if (!x || rows < 0 || K < 0 || L <= 0 || (bits != 4 && bits != 8)) return -1;
+    if (n_grid < 1 || n_cand < 1 || n_cand > n_grid) return -1;
+    int qmin = sym ? -(1 << (bits - 1)) : 0;
+    int qmax = sym ? (1 << (bits - 1)) - 1 : (1 << bits) - 1;
+    int f64 = dtype == AWQ_ORACLE_F64;
+    int64_t G = (K + L - 1) / L;
+    for (int64_t r = 0; r < rows; ++r) {
+        for (int64_t g = 0; g < G; ++g) {
+            int64_t k0 = g * L, k1 = k0 + L;
+            int padded = k1 > K;
+            if (k1 > K) k1 = K;
+            double mn = padded ? 0.0 : INFINITY, mx = padded ? 0.0 : -INFINITY;
+            int nan = 0;
+            for (int64_t k = k0; k < k1; ++k) {
+                double v = load_elem(x, dtype, r * K + k);
+                if (isnan(v)) nan = 1;
+                if (v < mn) mn = v;
+                if (v > mx) mx = v;
+            }
+            if (nan) { mn = NAN; mx = NAN; }
+            if (!nan) {
+                if (sym) {
+                    double a = (fabs(mx) > fabs(mn)) ? fabs(mx) : fabs(mn);
+                    mn = -a;
+                    mx = a;
+                }
+                double best = INFINITY;
+                int bi = 0;
+                for (int i = 0; i < n_cand; ++i) {
+                    double al = f64 ? (double)(n_grid - i) / (double)n_grid
+                                    : (double)((float)(n_grid - i) / (float)n_grid);
+                    double cs, cz;
+                    group_scale_zp(rn(cmul(mn, al, f64), dtype), rn(cmul(mx, al, f64), dtype), dtype, qmin,
+                                   qmax, sym, &cs, &cz);
+                    float sh = oracle_f16_to_f32(oracle_f32_to_f16((float)cs));
+                    double acc[64];
+                    for (int l = 0; l < 64; ++l) {
+                        acc[l] = 0.0;
+                        for (int64_t k = k0 + l; k < k1; k += 64) {
+                            double v = load_elem(x, dtype, r * K + k);
+                            double q = op_add(op_div(v, cs, dtype), cz, dtype);
+                            q = op_clamp(op_round(q, dtype), qmin, qmax);
+                            float h = oracle_f16_to_f32(oracle_f32_to_f16((float)(q - cz)));
+                            double dq = (double)oracle_f16_to_f32(oracle_f32_to_f16(h * sh));
+                            double d = csub(v, dq, f64);
+                            acc[l] = cadd(acc[l], cmul(d, d, f64), f64);
+                        }
+                    }
+                    double err = tree_sum64(acc, f64);
+                    if (err < best) { best = err; bi = i; }
+                }
+                double al = f64 ? (double)(n_grid - bi) / (double)n_grid
+                                : (double)((float)(n_grid - bi) / (float)n_grid);
+                mn = rn(cmul(mn, al, f64), dtype);
+                mx = rn(cmul(mx, al, f64), dtype);
+            }
+            double s, z;
+            group_scale_zp(mn, mx, dtype, qmin, qmax, sym, &s, &z);
+            if (scales_f16) scales_f16[r * G + g] = oracle_f32_to_f16((float)s);
+            if (zeros) zeros[r * G + g] = to_i32(z);
+            if (tensor_q) {
+                for (int64_t k = k0; k < k1; ++k) {
+                    double v = load_elem(x, dtype, r * K + k);
+                    double t = op_add(op_div(v, s, dtype), z, dtype);
+                    t = op_clamp(op_round(t, dtype), qmin, qmax);
+                    tensor_q[r * K + k] = to_i32(t);
+                }
+            }
+        }
+    }
+    return 0;
+}
+
 /* awq.py:459-539: dq = (q - z) [int32] * scale [fp16 0-d]  -> fp16 math -> stored fp32 */
 int oracle_dequantize(const int32_t* tensor_q, const uint16_t* scales_f16, const int32_t* zeros,
                       int64_t rows, int64_t K, int64_t L, float* out) {

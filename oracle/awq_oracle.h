@@ -12,6 +12,9 @@ enum { AWQ_ORACLE_BF16 = 0, AWQ_ORACLE_F16 = 1, AWQ_ORACLE_F32 = 2, AWQ_ORACLE_F
  * Outputs (any may be NULL): tensor_q int32 [rows, K], scales fp16 bits [rows, G], zeros int32 [rows, G]. */
 int oracle_quantize(const void* x, int dtype, int64_t rows, int64_t K, int64_t L, int bits, int sym,
                     int32_t* tensor_q, uint16_t* scales_f16, int32_t* zeros);
+/* opt-in clip search (product definition, include/awq_hip.h awq_quantize_search) */
+int oracle_quantize_search(const void* x, int dtype, int64_t rows, int64_t K, int64_t L, int bits, int sym,
+                           int n_grid, int n_cand, int32_t* tensor_q, uint16_t* scales_f16, int32_t* zeros);
 int oracle_dequantize(const int32_t* tensor_q, const uint16_t* scales_f16, const int32_t* zeros,
                       int64_t rows, int64_t K, int64_t L, float* out);
 int oracle_pack_rows(const int32_t* v, int64_t rows, int64_t n, int bits, int qmin, int32_t* packed);

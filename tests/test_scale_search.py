@@ -1,0 +1,156 @@
+"""Opt-in per-group clip search (scale_method="search", include/awq_hip.h awq_quantize_search).
+
+No reference counterpart (the reference stores scale_method and never reads it,
+awq.py:66,111-112; SURVEY.md §8a "parity unpinned"): the bar is
+  * candidate 0 alone (alpha = 1) reproduces the reference RTN result bit-exactly
+    (pinned through the golden fixtures),
+  * the search never increases a group's squared dequantization error over RTN,
+  * the HIP kernel equals oracle_quantize_search bit-for-bit (GPU tests).
+"""
+import pytest
+import torch
+
+import golden_io as gio
+from oracle import awq_oracle as orc
+
+
+def _group_err(x, res, gs):
+    """Per-group sum of squared errors of the reference dequantize, float64 [rows, G]."""
+    dq = orc.dequantize(res).double()
+    xd = x.double()
+    R = 1 if x.dim() <= 1 else x.shape[0]
+    K = x.numel() // R
+    G = -(-K // gs)
+    d = torch.zeros(R, G * gs, dtype=torch.float64)
+    d[:, :K] = ((xd - dq) ** 2).reshape(R, K)
+    return d.reshape(R, G, gs).sum(-1)
+
+
+# ---------------------------------------------------------------- CPU: oracle properties
+@pytest.mark.parametrize("case", [c for c in gio.ok_cases() if c["params"].get("group_size", 128) <= 256][::7],
+                         ids=lambda c: c["name"])
+def test_single_candidate_is_rtn_golden(case):
+    x = gio.case_input(case)
+    p = case["params"]
+    res = orc.quantize(x, bits=p.get("bits", 4), group_size=p.get("group_size", 128),
+                       symmetric=p.get("symmetric", True), per_channel=p.get("per_channel", True), search=(20, 1))
+    T = gio.tensors()
+    assert torch.equal(res["tensor_q"], T[case["name"] + ".tensor_q"])
+    assert torch.equal(res["zero_points"], T[case["name"] + ".zero_points"])
+    assert gio.same_bits_nan_eq(res["scales"], T[case["name"] + ".scales"])
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16, torch.float32])
+@pytest.mark.parametrize("sym", [False, True])
+@pytest.mark.parametrize("bits", [4, 8])
+def test_search_never_worse_than_rtn(dtype, sym, bits):
+    g = torch.Generator().manual_seed(5 + bits + sym)
+    x = (torch.randn(24, 640, generator=g) * 0.03).to(dtype)
+    x[3, :50] *= 40                                              # outliers: clipping pays off
+    rtn = orc.quantize(x, bits=bits, group_size=128, symmetric=sym)
+    srch = orc.quantize(x, bits=bits, group_size=128, symmetric=sym, search=(20, 10))
+    e0, e1 = _group_err(x, rtn, 128), _group_err(x, srch, 128)
+    # the search's own metric is an fp32 tree sum; allow its rounding, nothing more
+    assert bool((e1 <= e0 * (1 + 1e-5) + 1e-30).all())
+    if bits == 4:
+        assert e1.sum() < 0.97 * e0.sum()                        # and it does find better clips
+
+
+def test_search_nan_groups_keep_rtn():
+    x = (torch.randn(4, 256) * 0.1).to(torch.bfloat16)
+    x[1, 5] = float("nan")
+    x[2, 200] = float("inf")
+    rtn = orc.quantize(x, bits=4, group_size=128, symmetric=False)
+    srch = orc.quantize(x, bits=4, group_size=128, symmetric=False, search=(20, 10))
+    for r, g in [(1, 0), (2, 1)]:
+        assert gio.same_bits_nan_eq(srch["scales"][r, g], rtn["scales"][r, g])
+        assert torch.equal(srch["tensor_q"][r, g * 128:(g + 1) * 128], rtn["tensor_q"][r, g * 128:(g + 1) * 128])
+
+
+def test_search_validation():
+    from awq_quantizer.quantization import AWQQuantizer
+    q = AWQQuantizer(scale_method="search", logger_level="ERROR")
+    assert q.search_candidates == 10
+    assert AWQQuantizer(scale_method="mse", logger_level="ERROR").search_candidates == 0
+    assert AWQQuantizer(scale_method="search", search_grid=4, search_max_shrink=1.0,
+                        logger_level="ERROR").search_candidates == 4
+    with pytest.raises(ValueError, match="search_grid"):
+        AWQQuantizer(scale_method="search", search_grid=0, logger_level="ERROR")
+    with pytest.raises(ValueError, match="search_max_shrink"):
+        AWQQuantizer(scale_method="search", search_max_shrink=0.0, logger_level="ERROR")
+    with pytest.raises(ValueError, match="Unsupported scale calibration method"):
+        AWQQuantizer(scale_method="grid", logger_level="ERROR")
+
+
+def test_cli_accepts_search():
+    from awq_quantizer.main import parse_args
+    a = parse_args(["--model_id", "m", "--output_dir", "o", "--scale_method", "search", "--search_grid", "10"])
+    assert (a.scale_method, a.search_grid, a.search_max_shrink) == ("search", 10, 0.5)
+
+
+# ---------------------------------------------------------------- GPU: kernel vs oracle
+SEARCH_CASES = [(torch.bfloat16, (40, 1024), 128), (torch.bfloat16, (7, 300), 128), (torch.float16, (33, 300), 128),
+                (torch.float32, (17, 1000), 64), (torch.float64, (5, 777), 100), (torch.bfloat16, (3, 2, 50), 32),
+                (torch.bfloat16, (10, 10), 128), (torch.bfloat16, (60,), 128), (torch.float16, (4, 4096), 256)]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype,shape,gs", SEARCH_CASES, ids=str)
+@pytest.mark.parametrize("sym", [False, True])
+@pytest.mark.parametrize("bits", [4, 8])
+def test_search_gpu_vs_oracle(dtype, shape, gs, sym, bits):
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from awq_quantizer.quantization import AWQQuantizer
+    g = torch.Generator().manual_seed(17 + bits)
+    x = (torch.randn(*shape, generator=g) * 0.05).to(dtype)
+    if x.dim() == 2 and x.shape[1] > 64:
+        x[0, 3] = 2.0                                            # an outlier group
+    q = AWQQuantizer(bits=bits, group_size=gs, symmetric=sym, scale_method="search", device="cuda",
+                     logger_level="ERROR")
+    ref = orc.quantize(x, bits=bits, group_size=gs, symmetric=sym, search=(20, 10))
+    res = q.quantize(x)
+    assert torch.equal(res["tensor_q"], ref["tensor_q"])
+    assert torch.equal(res["zero_points"], ref["zero_points"])
+    assert gio.same_bits_nan_eq(res["scales"], ref["scales"])
+    if x.numel() >= gs:
+        pk = q.quantize_packed(x)
+        assert torch.equal(pk["qweight"].cpu(), orc.pack_rows(ref["tensor_q"], bits, q.qmin))
+        assert torch.equal(pk["qzeros"].cpu(), orc.pack_rows(ref["zero_points"], bits, q.qmin))
+
+
+@pytest.mark.gpu
+def test_search_gpu_special_values_and_rtn_identity():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from awq_quantizer.quantization import AWQQuantizer
+    from test_gpu_parity import special_tensor
+    x = special_tensor((32, 1024), 3)
+    for sym in (False, True):
+        ref = orc.quantize(x, bits=4, group_size=128, symmetric=sym, search=(16, 8))
+        q = AWQQuantizer(bits=4, symmetric=sym, scale_method="search", search_grid=16, device="cuda",
+                         logger_level="ERROR")
+        res = q.quantize(x)
+        assert torch.equal(res["tensor_q"], ref["tensor_q"])
+        assert gio.same_bits_nan_eq(res["scales"], ref["scales"])
+        one = AWQQuantizer(bits=4, symmetric=sym, scale_method="search", search_grid=16,
+                           search_max_shrink=1 / 16, device="cuda", logger_level="ERROR").quantize(x)
+        rtn = AWQQuantizer(bits=4, symmetric=sym, device="cuda", logger_level="ERROR").quantize(x)
+        assert torch.equal(one["tensor_q"], rtn["tensor_q"])
+        assert gio.same_bits_nan_eq(one["scales"], rtn["scales"])
+
+
+@pytest.mark.gpu
+def test_search_gpu_model_packed_routes_generic():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from awq_quantizer.quantization import AWQQuantizer
+    g = torch.Generator().manual_seed(2)
+    ts = {"a": (torch.randn(64, 512, generator=g) * 0.02).bfloat16(), "b": (torch.randn(768, generator=g)).bfloat16()}
+    q = AWQQuantizer(bits=4, symmetric=False, scale_method="search", device="cuda", logger_level="ERROR")
+    out = q.quantize_model_packed(ts)
+    for n, t in ts.items():
+        ref = orc.quantize(t, bits=4, group_size=128, symmetric=False, search=(20, 10))
+        rows = 1 if t.dim() == 1 else t.shape[0]
+        assert torch.equal(out[n]["qweight"].cpu(), orc.pack_rows(ref["tensor_q"].reshape(rows, -1), 4, 0))
+        assert gio.same_bits_nan_eq(out[n]["scales"].cpu(), ref["scales"])

@@ -63,6 +63,8 @@ def load_library(path: str = LIB_PATH):
     with _lock:
         if _lib is not None:
             return _lib
+        if path == LIB_PATH:   # tuning hook: run everything against another in-tree build
+            path = os.environ.get("AWQ_HIP_LIB", path)
         if not os.path.exists(path):
             raise HipUnavailable(
                 f"awq_quantizer: {path} is missing — build it with "

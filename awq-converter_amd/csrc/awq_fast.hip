@@ -45,6 +45,30 @@
 #ifndef AWQ_PREFETCH
 #define AWQ_PREFETCH 2
 #endif
+// cache policy of the small per-tile stores (scales, zeros, qzeros: 8-32 B per tile).
+// Default policy (0), not nt: the L2 then merges the partial lines neighbouring tiles
+// write (measured +2-5 % over nt, profiles/r19-r20)
+#ifndef AWQ_SMALL_AUX
+#define AWQ_SMALL_AUX 0
+#endif
+// tiles per assignment chunk (strided mode): a wave takes CH consecutive tiles, then jumps
+// CH * nwaves ahead — its per-tile scale/qzeros bytes then fill whole cache lines in ONE L2
+#ifndef AWQ_CHUNK
+#define AWQ_CHUNK 1
+#endif
+// per-wave driver: LDS-DMA from inline asm (1) or the builtin (0; compiler-inserted
+// vmcnt(0) waits).  The loader/consumer pipeline always uses the asm form.
+#ifndef AWQ_DMA_ASM
+#define AWQ_DMA_ASM 0
+#endif
+
+// XCD-aware block order: workgroups are dealt round-robin over the 8 XCDs (block b on XCD
+// b % 8); renumbering them so each XCD owns a contiguous run of logical blocks keeps the
+// tiles that share a cache line of scales / qzeros inside ONE L2 (no partial-line merges
+// across XCDs)
+#ifndef AWQ_XCD_REMAP
+#define AWQ_XCD_REMAP 0
+#endif
 // __launch_bounds__ minimum waves per SIMD (8 = 32 waves per CU: <= 64 VGPRs, <= 80 SGPRs)
 #ifndef AWQ_MIN_WAVES
 #define AWQ_MIN_WAVES 8
@@ -327,7 +351,7 @@ __device__ __forceinline__ void tile_src(int64_t rows, int64_t K, uint32_t tile,
 
 // 4 x 16-B loads per lane: slot 4j + row, 16-B chunk c of the group.  Slots past the tile
 // end fall outside the descriptor's range and read as zero.
-__device__ __forceinline__ void load_tile(const TileCtx& c, u4 (&v)[4]) {
+[[maybe_unused]] __device__ __forceinline__ void load_tile(const TileCtx& c, u4 (&v)[4]) {
     const int lane = threadIdx.x & 63;
     const int row = lane >> 4, ch = lane & 15;
     const __amdgpu_buffer_rsrc_t rw = rsrc(c.wp, c.ng * 256u);
@@ -339,13 +363,51 @@ __device__ __forceinline__ void load_tile(const TileCtx& c, u4 (&v)[4]) {
 // Same 4 KiB as load_tile, streamed into the wave's LDS slot by LDS-DMA: instruction j
 // writes 1 KiB contiguously (lane i -> slot + j*1024 + 16*i), i.e. the slot is a byte copy
 // of the tile and lane i later reads back exactly the 16 B load_tile would have given it.
+//
+// Two forms.  The builtin (default): the compiler then puts s_waitcnt vmcnt(0) in front
+// of every later LDS access of the wave (the qzeros ds_or, the slot read-out), which also
+// drains the tile's qweight stores.  The inline-asm form (AWQ_DMA_ASM=1) hides the DMA
+// from the compiler so the loop waits once, counted (vmcnt counts loads, stores and
+// LDS-DMA together, in issue order: MI355X_MICROARCH.md "s_waitcnt vmcnt(N)").  Measured
+// (profiles/r20_kbench.log): no gain — 0-4 % slower — so the store drains are not what
+// bounds this kernel.  A loader/consumer variant (one DMA wave per workgroup feeding a
+// ring of 4-16 slots) was also measured and was 8-50 % slower (r21_kbench.log).
+#if AWQ_LOAD_AUX == 2
+#define AWQ_DMA_POLICY " nt"
+#elif AWQ_LOAD_AUX == 0
+#define AWQ_DMA_POLICY ""
+#else
+#error "AWQ_LOAD_AUX must be 0 or 2 for the asm LDS-DMA"
+#endif
+[[maybe_unused]] __device__ __forceinline__ void dma_tile_asm(const uint16_t* wp, uint32_t ng, uint8_t* slot) {
+    const int lane = threadIdx.x & 63;
+    const uint64_t base = (uint64_t)wp;
+    const u4 desc = {(uint32_t)base, (uint32_t)(base >> 32) & 0xFFFFu, ng * 256u, 0x00020000u};
+    const uint32_t lds = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint8_t*)slot;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const uint32_t voff = (uint32_t)(j * 1024 + lane * 16);
+        uint32_t saved_m0;   // m0 is a compiler-reserved register: saved and restored here
+        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\t"
+                     "buffer_load_dwordx4 %2, %3, 0 offen" AWQ_DMA_POLICY " lds\n\ts_mov_b32 m0, %0"
+                     : "=&s"(saved_m0) : "s"(lds + (uint32_t)(j * 1024)), "v"(voff), "s"(desc) : "memory");
+    }
+}
+
+// builtin form: the compiler then waits vmcnt(0) before the wave's next LDS access —
+// measured no slower for the one-slot-per-wave driver (its only LDS accesses sit right
+// where it has to wait anyway)
 [[maybe_unused]] __device__ __forceinline__ void dma_tile(const uint16_t* wp, uint32_t ng, uint8_t* slot) {
+#if AWQ_DMA_ASM
+    dma_tile_asm(wp, ng, slot);
+#else
     const int lane = threadIdx.x & 63;
     const __amdgpu_buffer_rsrc_t rw = rsrc(wp, ng * 256u);
 #pragma unroll
     for (int j = 0; j < 4; ++j)
         __builtin_amdgcn_raw_ptr_buffer_load_lds(rw, (__attribute__((address_space(3))) void*)(slot + j * 1024), 16,
                                                  (uint32_t)(j * 1024 + lane * 16), 0, 0, AWQ_LOAD_AUX);
+#endif
 }
 
 template <int BITS, bool SYM>
@@ -366,14 +428,16 @@ __device__ __forceinline__ void compute_tile(const TileCtx& c, const u4 (&v)[4],
             __builtin_amdgcn_raw_buffer_store_b32(word, rq, (uint32_t)(((4 * j + row) * 16 + ch) * 4), 0, AWQ_STORE_AUX);
         }
     }
+#ifndef AWQ_TRIVIAL_NOSMALL
     if (ch < 4 && c.scales) {
         __amdgpu_buffer_rsrc_t rs = rsrc(c.scales + c.start, ng * 2u);
-        __builtin_amdgcn_raw_buffer_store_b16((uint16_t)v[0].x, rs, (4u * ch + row) * 2u, 0, AWQ_STORE_AUX);
+        __builtin_amdgcn_raw_buffer_store_b16((uint16_t)v[0].x, rs, (4u * ch + row) * 2u, 0, AWQ_SMALL_AUX);
     }
     if (c.qzeros && (uint32_t)lane < c.nw) {
         __amdgpu_buffer_rsrc_t rz = rsrc(c.qzeros + c.w0, c.nw * 4u);
-        __builtin_amdgcn_raw_buffer_store_b32(v[1].y, rz, (uint32_t)lane * 4u, 0, AWQ_STORE_AUX);
+        __builtin_amdgcn_raw_buffer_store_b32(v[1].y, rz, (uint32_t)lane * 4u, 0, AWQ_SMALL_AUX);
     }
+#endif
     return;
 #endif
 
@@ -493,12 +557,12 @@ __device__ __forceinline__ void compute_tile(const TileCtx& c, const u4 (&v)[4],
     if (ch < 4) {
         if (c.scales) {
             __amdgpu_buffer_rsrc_t rs = rsrc(c.scales + c.start, ng * 2u);
-            __builtin_amdgcn_raw_buffer_store_b16(f16_bits(p.s), rs, my_slot * 2u, 0, AWQ_STORE_AUX);
+            __builtin_amdgcn_raw_buffer_store_b16(f16_bits(p.s), rs, my_slot * 2u, 0, AWQ_SMALL_AUX);
         }
         if (c.zeros) {
             __amdgpu_buffer_rsrc_t rz = rsrc(c.zeros + c.start, ng * 4u);
             int32_t zi = __builtin_isnan(p.z) ? INT32_MIN : (int32_t)p.z;
-            __builtin_amdgcn_raw_buffer_store_b32((uint32_t)zi, rz, my_slot * 4u, 0, AWQ_STORE_AUX);
+            __builtin_amdgcn_raw_buffer_store_b32((uint32_t)zi, rz, my_slot * 4u, 0, AWQ_SMALL_AUX);
         }
     }
     // qzeros, byte tiles: each group's field OR-ed into its byte (wave-private LDS), then one
@@ -522,10 +586,10 @@ __device__ __forceinline__ void compute_tile(const TileCtx& c, const u4 (&v)[4],
             const uint32_t row_bytes = c.WPR * 4u;
             __amdgpu_buffer_rsrc_t rz = rsrc(c.qzeros, 0x7FFFFFFFu);
             const uint32_t at = r * row_bytes + g / GPB;
-            __builtin_amdgcn_raw_buffer_store_b8((uint8_t)zw[lane], rz, at, 0, AWQ_STORE_AUX);
+            __builtin_amdgcn_raw_buffer_store_b8((uint8_t)zw[lane], rz, at, 0, AWQ_SMALL_AUX);
             if (g + GPB >= c.G) {                               // row's last byte: zero the pad
                 for (uint32_t b = g / GPB + 1; b < row_bytes; ++b)
-                    __builtin_amdgcn_raw_buffer_store_b8((uint8_t)0, rz, r * row_bytes + b, 0, AWQ_STORE_AUX);
+                    __builtin_amdgcn_raw_buffer_store_b8((uint8_t)0, rz, r * row_bytes + b, 0, AWQ_SMALL_AUX);
             }
         }
     }
@@ -547,7 +611,7 @@ __device__ __forceinline__ void compute_tile(const TileCtx& c, const u4 (&v)[4],
         }
         if ((uint32_t)lane < c.nw) {
             __amdgpu_buffer_rsrc_t rz = rsrc(c.qzeros + c.w0, c.nw * 4u);
-            __builtin_amdgcn_raw_buffer_store_b32(zw[lane], rz, (uint32_t)lane * 4u, 0, AWQ_STORE_AUX);
+            __builtin_amdgcn_raw_buffer_store_b32(zw[lane], rz, (uint32_t)lane * 4u, 0, AWQ_SMALL_AUX);
         }
     }
 
@@ -558,7 +622,7 @@ __device__ __forceinline__ void compute_tile(const TileCtx& c, const u4 (&v)[4],
 // and a ballot narrows the range: one dependent load per round, 1 round for <= 64
 // candidates, 2 for <= 4096 — instead of a chain of scalar loads through every tiny
 // tensor (a model has ~100 1-tile bias tensors next to each other).
-__device__ __forceinline__ int find_tensor(const awq_tensor_desc* __restrict__ descs, int n, int base,
+[[maybe_unused]] __device__ __forceinline__ int find_tensor(const awq_tensor_desc* __restrict__ descs, int n, int base,
                                            int64_t t) {
     const int lane = threadIdx.x & 63;
     int span = n - base;
@@ -585,11 +649,17 @@ __global__ __launch_bounds__(256, AWQ_MIN_WAVES) void awq_fast_kernel(const awq_
     // wave index made provably uniform so tile/tensor bookkeeping and the buffer
     // descriptors live in SGPRs (no waterfall loops around the descriptors)
     const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+#if AWQ_XCD_REMAP
+    const uint32_t nb = gridDim.x;
+    const uint32_t lb = (nb % kXcds) ? blockIdx.x : (blockIdx.x % kXcds) * (nb / kXcds) + blockIdx.x / kXcds;
+    const int64_t wave = (int64_t)lb * kWavesPerBlock + wid;
+#else
     const int64_t wave = (int64_t)blockIdx.x * kWavesPerBlock + wid;
+#endif
     const int64_t nwaves = (int64_t)gridDim.x * kWavesPerBlock;
 #if AWQ_ASSIGN_STRIDED
     // interleaved: at any moment the waves of the chip read one compact window of memory
-    int64_t t = wave;
+    int64_t t = wave * AWQ_CHUNK;
     const int64_t step = nwaves;
     const int64_t t_end = total_tiles;
 #else
@@ -621,8 +691,13 @@ __global__ __launch_bounds__(256, AWQ_MIN_WAVES) void awq_fast_kernel(const awq_
         tile_src<BITS>(d.rows, d.K, (uint32_t)(t - d.tile_begin), st, ng);
         dma_tile((const uint16_t*)d.w + (uint64_t)st * kGroup, ng, slot);
     }
-    for (; t < t_end; t += step) {
+    bool prev_stores = false;
+    for (; t < t_end;) {
+#if AWQ_ASSIGN_STRIDED && AWQ_CHUNK > 1
+        const int64_t tn = ((t + 1) % AWQ_CHUNK) ? t + 1 : t + 1 + (step - 1) * AWQ_CHUNK;
+#else
         const int64_t tn = t + step;
+#endif
         const bool more = tn < t_end;
         int nc = cur;
         const uint16_t* nwp = nullptr;
@@ -640,17 +715,22 @@ __global__ __launch_bounds__(256, AWQ_MIN_WAVES) void awq_fast_kernel(const awq_
                 nwp = (const uint16_t*)d.w + (uint64_t)st * kGroup;
             }
         }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");       // this tile has landed in LDS
+        // this tile has landed in LDS: all but the youngest `prev_stores` vector-memory
+        // ops done — those are the previous tile's qweight stores, issued after this DMA
+        if (prev_stores && AWQ_DMA_ASM) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         u4 va[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) va[j] = *(const u4*)(slot + j * 1024 + lane * 16);
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");     // slot read out: reusable
         if (more) dma_tile(nwp, nng, slot);
         compute_tile<BITS, SYM>(make_ctx<BITS>(d, (uint32_t)(t - d.tile_begin)), va, zw);
+        prev_stores = d.qweight != nullptr;   // compute_tile issued 4 qweight stores after the DMA
         if (nc != cur) {
             cur = nc;
             d = descs[cur];
         }
+        t = tn;
     }
     return;
 #elif !AWQ_PREFETCH
@@ -735,7 +815,8 @@ hipError_t launch_fast(const awq_tensor_desc* descs_dev, const awq_tensor_desc* 
         long v = atol(e);
         if (v > 0) max_blocks = v;
     }
-    int64_t blocks = (total_tiles + kWavesPerBlock - 1) / kWavesPerBlock;
+    constexpr int64_t kTilesPerBlock = kWavesPerBlock * AWQ_CHUNK;
+    int64_t blocks = (total_tiles + kTilesPerBlock - 1) / kTilesPerBlock;
     if (blocks > max_blocks) blocks = max_blocks;
     awq_tensor_desc one{};
     if (single) one = *single;

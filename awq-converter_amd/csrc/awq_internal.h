@@ -27,6 +27,7 @@ namespace awq {
 constexpr int kGroup = 128;          // elements per group on the fast path
 constexpr int kSlots = 16;           // group slots per wave-tile (4 loads x 4 lane-rows)
 constexpr int kWavesPerBlock = 4;    // 256-thread workgroups
+constexpr uint32_t kXcds = 8;        // MI355X: 8 XCDs x 32 CUs, each XCD with its own L2
 
 struct TensorGeom {
     uint32_t G;    // groups per row

@@ -34,6 +34,10 @@
 #include <stdint.h>
 #include <string.h>
 
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
 #include "awq_oracle.h"
 
 /* ---------------- rounding helpers ---------------- */
@@ -158,6 +162,8 @@ int oracle_quantize(const void* x, int dtype, int64_t rows, int64_t K, int64_t L
     int qmin = sym ? -(1 << (bits - 1)) : 0;                                  /* awq.py:114-128 */
     int qmax = sym ? (1 << (bits - 1)) - 1 : (1 << bits) - 1;
     int64_t G = (K + L - 1) / L;
+    /* rows are independent: OpenMP over rows (results do not depend on the thread count) */
+#pragma omp parallel for schedule(static) if (rows * K >= (1 << 16))
     for (int64_t r = 0; r < rows; ++r) {
         for (int64_t g = 0; g < G; ++g) {
             int64_t k0 = g * L, k1 = k0 + L;
@@ -225,6 +231,7 @@ int oracle_quantize_search(const void* x, int dtype, int64_t rows, int64_t K, in
     int qmax = sym ? (1 << (bits - 1)) - 1 : (1 << bits) - 1;
     int f64 = dtype == AWQ_ORACLE_F64;
     int64_t G = (K + L - 1) / L;
+#pragma omp parallel for schedule(static) if (rows * K >= (1 << 14))
     for (int64_t r = 0; r < rows; ++r) {
         for (int64_t g = 0; g < G; ++g) {
             int64_t k0 = g * L, k1 = k0 + L;
@@ -290,6 +297,17 @@ int oracle_quantize_search(const void* x, int dtype, int64_t rows, int64_t K, in
         }
     }
     return 0;
+}
+
+/* threads used by the OpenMP row loops (bench.py's cpu_baseline reports this count) */
+int oracle_set_threads(int n) {
+#ifdef _OPENMP
+    if (n > 0) omp_set_num_threads(n);
+    return omp_get_max_threads();
+#else
+    (void)n;
+    return 1;
+#endif
 }
 
 /* awq.py:459-539: dq = (q - z) [int32] * scale [fp16 0-d]  -> fp16 math -> stored fp32 */

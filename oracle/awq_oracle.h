@@ -18,6 +18,7 @@ int oracle_quantize_search(const void* x, int dtype, int64_t rows, int64_t K, in
 int oracle_dequantize(const int32_t* tensor_q, const uint16_t* scales_f16, const int32_t* zeros,
                       int64_t rows, int64_t K, int64_t L, float* out);
 int oracle_pack_rows(const int32_t* v, int64_t rows, int64_t n, int bits, int qmin, int32_t* packed);
+int oracle_set_threads(int n);
 uint16_t oracle_f32_to_bf16(float f);
 float oracle_bf16_to_f32(uint16_t h);
 uint16_t oracle_f32_to_f16(float f);

@@ -9,12 +9,13 @@ from __future__ import annotations
 import ctypes
 import os
 import threading
+from typing import Optional
 
 import torch
 
 LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib")
 LIB_PATH = os.path.join(LIB_DIR, "libawq_hip.so")
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 AWQ_DTYPE = {torch.bfloat16: 0, torch.float16: 1, torch.float32: 2, torch.float64: 3}
 
@@ -41,7 +42,8 @@ SIGNATURES = {
     "awq_quantize_search": (_I32, [_P, _I32, _I64, _I64, _I64, _I32, _I32, _I32, _I32, _P, _P, _P, _P, _P, _P]),
     "awq_ragged_eligible": (_I32, [_I32, _I64, _I64, _I64]),
     "awq_plan_ragged": (_I64, [ctypes.POINTER(TensorDesc), _I32, _I32]),
-    "awq_quantize_ragged": (_I32, [_P, _I32, _I64, _I32, _I32, _P]),
+    "awq_plan_block_tensor": (_I64, [ctypes.POINTER(TensorDesc), _I32, _I64, _P, _I64]),
+    "awq_quantize_ragged": (_I32, [_P, _I32, _I64, _P, _I32, _I32, _P]),
     "awq_dequantize": (_I32, [_P, _P, _P, _I64, _I64, _I64, _P, _P]),
     "awq_dequantize_packed": (_I32, [_P, _P, _P, _I64, _I64, _I64, _I32, _I32, _P, _P]),
     "awq_pack_rows": (_I32, [_P, _I64, _I64, _I32, _I32, _P, _P]),
@@ -159,10 +161,23 @@ def descs_to_device(descs, device: torch.device) -> torch.Tensor:
     return host.to(device)
 
 
+def plan_block_tensor(descs, total_tiles: int, device: torch.device) -> torch.Tensor:
+    """awq_plan_block_tensor: the tensor of every workgroup's first tile, as a device int32
+    tensor (the kernel then skips the per-wave descriptor search)."""
+    lib = load_library()
+    arr = (TensorDesc * len(descs))(*descs)
+    nblk = -(-int(total_tiles) // 4)
+    host = torch.empty(max(nblk, 1), dtype=torch.int32)
+    rc = lib.awq_plan_block_tensor(arr, len(descs), total_tiles, ctypes.c_void_p(host.data_ptr()), host.numel())
+    if rc < 0:
+        raise RuntimeError(f"awq_plan_block_tensor failed: {last_error()}")
+    return host.to(device)
+
+
 def quantize_ragged(descs_dev: torch.Tensor, n: int, total_tiles: int, bits: int, symmetric: bool,
-                    stream: int) -> None:
-    rc = load_library().awq_quantize_ragged(ptr(descs_dev), n, total_tiles, bits, int(bool(symmetric)),
-                                            ctypes.c_void_p(stream))
+                    stream: int, block_tensor: Optional[torch.Tensor] = None) -> None:
+    rc = load_library().awq_quantize_ragged(ptr(descs_dev), n, total_tiles, ptr(block_tensor), bits,
+                                            int(bool(symmetric)), ctypes.c_void_p(stream))
     check(rc, "awq_quantize_ragged")
 
 

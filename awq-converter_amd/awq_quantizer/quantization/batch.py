@@ -20,10 +20,12 @@ class PackedBatch:
     inputs: name -> contiguous bf16 device tensor ([rows, ...] or 1-D), K % 128 == 0.
     parity=True additionally produces the reference's unpacked int32 tensor_q and
     zero_points (6.05 B/element of output traffic instead of 0.52).
+    use_block_table: upload the per-workgroup tensor table (awq_plan_block_tensor; 4 B per
+    4 tiles) so no wave has to search the descriptors.
     """
 
     def __init__(self, inputs: Dict[str, torch.Tensor], bits: int = 4, symmetric: bool = False,
-                 parity: bool = False, packed: bool = True):
+                 parity: bool = False, packed: bool = True, use_block_table: bool = True):
         if not inputs:
             raise ValueError("PackedBatch needs at least one tensor")
         self.bits, self.symmetric, self.parity = bits, bool(symmetric), parity
@@ -58,12 +60,13 @@ class PackedBatch:
         self.total_tiles = _hip.plan_ragged(descs, bits)
         self.descs = descs
         self.descs_dev = _hip.descs_to_device(descs, dev)
+        self.block_tensor = _hip.plan_block_tensor(descs, self.total_tiles, dev) if use_block_table else None
         self.elements = sum(inputs[n].numel() for n in self.names)
 
     def run(self, stream: Optional[torch.cuda.Stream] = None) -> None:
         s = stream if stream is not None else torch.cuda.current_stream(self.device)
         _hip.quantize_ragged(self.descs_dev, len(self.descs), self.total_tiles, self.bits, self.symmetric,
-                             s.cuda_stream)
+                             s.cuda_stream, self.block_tensor)
 
     def results(self) -> Dict[str, Dict[str, torch.Tensor]]:
         res = {}

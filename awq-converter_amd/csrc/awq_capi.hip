@@ -91,7 +91,8 @@ int awq_quantize_groups(const void* w, int dtype, int64_t rows, int64_t K, int64
         d.w = w; d.rows = rows; d.K = K; d.qweight = qweight; d.qzeros = qzeros; d.scales = scales;
         d.tensor_q = tensor_q; d.zeros = zeros; d.tile_begin = 0;
         d.tile_count = awq::fast_tiles(rows, K, bits);
-        return hip_status(awq::launch_fast(nullptr, &d, 1, d.tile_count, bits, symmetric, s), "awq fast kernel");
+        return hip_status(awq::launch_fast(nullptr, nullptr, &d, 1, d.tile_count, bits, symmetric, s),
+                          "awq fast kernel");
     }
     // generic path: per-group int32 values first, then packing (needs tensor_q / zeros buffers)
     if ((qweight && !tensor_q) || (qzeros && !zeros))
@@ -160,13 +161,28 @@ int64_t awq_plan_ragged(awq_tensor_desc* descs, int n, int bits) {
     return total;
 }
 
-int awq_quantize_ragged(const awq_tensor_desc* descs_device, int n, int64_t total_tiles, int bits,
-                        int symmetric, void* stream) {
+int64_t awq_plan_block_tensor(const awq_tensor_desc* descs, int n, int64_t total_tiles, int32_t* block_tensor,
+                              int64_t len) {
+    g_err.clear();
+    const int64_t need = (total_tiles + awq::kWavesPerBlock - 1) / awq::kWavesPerBlock;
+    if (!block_tensor || len < need) return fail(AWQ_EINVAL, "block table needs %lld entries", (long long)need), -1;
+    if (n <= 0 || !descs) return fail(AWQ_EINVAL, "bad descriptor array"), -1;
+    int cur = 0;
+    for (int64_t b = 0; b < need; ++b) {
+        const int64_t t = b * awq::kWavesPerBlock;
+        while (cur + 1 < n && descs[cur + 1].tile_begin <= t) ++cur;
+        block_tensor[b] = cur;
+    }
+    return need;
+}
+
+int awq_quantize_ragged(const awq_tensor_desc* descs_device, int n, int64_t total_tiles,
+                        const int32_t* block_tensor_device, int bits, int symmetric, void* stream) {
     g_err.clear();
     if (bits != 4 && bits != 8) return fail(AWQ_EINVAL, "Unsupported bit width: %d. Supported: 4, 8.", bits);
     if (n <= 0 || total_tiles <= 0) return AWQ_OK;
     if (!descs_device) return fail(AWQ_EINVAL, "null descriptor array");
-    return hip_status(awq::launch_fast(descs_device, nullptr, n, total_tiles, bits, symmetric,
+    return hip_status(awq::launch_fast(descs_device, block_tensor_device, nullptr, n, total_tiles, bits, symmetric,
                                        (hipStream_t)stream), "awq ragged kernel");
 }
 

@@ -7,16 +7,17 @@
 // tensor_q / zero_points).
 //
 // Mapping (HBM-bound, no MFMA):
-//   * one group = 128 bf16 = 256 B = 16 lanes x one 16-B buffer_load_dwordx4; a wave
-//     covers 4 groups per load and 4 loads (16 groups, 4 KiB) per tile; the next tile's
-//     loads are in flight while the current one is computed (register double buffer);
-//   * per-group min/max in the integer domain: bf16 bits -> order-preserving int16 key
-//     (v_pk_ashrrev_i16 + v_bitop3), v_pk_max_i16/v_pk_min_i16, then (max, ~min) packed in
-//     one dword and reduced across the 16-lane DPP row — no LDS; NaN is detected from the
-//     keys (a NaN key lies beyond +/-inf);
+//   * one wave = one tile = 16 group slots = 4 KiB of input: lane-row rho (16 lanes) holds
+//     groups 4j + rho, each lane one 16-B chunk per group (4 x buffer_load_dwordx4);
+//   * the grid has one wave per tile (non-persistent): the hardware dispatcher hands a
+//     finished wave's slot to the next workgroup, which balances the load across CUs.  A
+//     persistent grid (waves walking tiles) lost ~20 % to the dispatcher's age priority:
+//     the youngest workgroups of every CU ran last and alone (profiles/r24-r27);
+//   * per-group min/max from the raw bf16 bits (signed / unsigned int16 max), reduced over
+//     the 16-lane row with DPP-fused v_max_i32; NaN is detected from the bits;
 //   * the scale / zero point of the tile's 16 groups are computed ONCE, by 16 different
-//     lanes (lane (row, c) with c = j owns group 4j + row), with the reference's per-op
-//     bf16 rounding, then broadcast back to the group's 16 lanes with DPP row_newbcast;
+//     lanes (lane (row, c) owns group 4c + row), with the reference's per-op bf16 rounding,
+//     then broadcast back to the group's 16 lanes with DPP row_newbcast;
 //   * per element: RN_bf16(x * RN_f32(1/s)) == RN_bf16(x / s) for every bf16 x and every
 //     bf16 s >= RN_bf16(1e-10) (verified exhaustively: oracle/verify_recip.c), so one
 //     multiply replaces the division; RNE to bf16 is one v_cvt_pk_bf16_f32 with a zero
@@ -26,48 +27,25 @@
 //   * buffer descriptors are based at the tile start with the tile's byte length, so
 //     slots past the tile end read zeros and their stores are dropped by the hardware
 //     range check (no per-lane masks, no OOB access, tensors > 4 GB are fine).
-// Ragged launches: one grid over the tiles of many tensors (descriptor table in HBM);
-// each wave walks a contiguous tile range and advances a tensor cursor.
+// Ragged launches: one grid over the tiles of many tensors (descriptor table in HBM); a
+// wave finds its tensor with a 64-lane ballot search of the table.
 #include <cstdlib>
 
 #include "awq_internal.h"
 
-// cache-policy bits of the buffer loads/stores (aux operand; gfx950: 2 = nt).  Build-time
-// knobs for tuning (scripts/kbench.py compares variants); defaults measured best.
+// Build-time knobs (scripts/kbench.py compares variants; defaults measured best).
+// cache-policy bits of the input loads and the qweight / tensor_q stores (gfx950: 2 = nt)
 #ifndef AWQ_LOAD_AUX
 #define AWQ_LOAD_AUX 2
 #endif
 #ifndef AWQ_STORE_AUX
 #define AWQ_STORE_AUX 2
 #endif
-// next-tile prefetch: 2 = LDS-DMA staging slot per wave, 1 = register double buffer,
-// 0 = none (occupancy alone hides the latency)
-#ifndef AWQ_PREFETCH
-#define AWQ_PREFETCH 2
-#endif
 // cache policy of the small per-tile stores (scales, zeros, qzeros: 8-32 B per tile).
 // Default policy (0), not nt: the L2 then merges the partial lines neighbouring tiles
 // write (measured +2-5 % over nt, profiles/r19-r20)
 #ifndef AWQ_SMALL_AUX
 #define AWQ_SMALL_AUX 0
-#endif
-// tiles per assignment chunk (strided mode): a wave takes CH consecutive tiles, then jumps
-// CH * nwaves ahead — its per-tile scale/qzeros bytes then fill whole cache lines in ONE L2
-#ifndef AWQ_CHUNK
-#define AWQ_CHUNK 1
-#endif
-// per-wave driver: LDS-DMA from inline asm (1) or the builtin (0; compiler-inserted
-// vmcnt(0) waits).  The loader/consumer pipeline always uses the asm form.
-#ifndef AWQ_DMA_ASM
-#define AWQ_DMA_ASM 0
-#endif
-
-// XCD-aware block order: workgroups are dealt round-robin over the 8 XCDs (block b on XCD
-// b % 8); renumbering them so each XCD owns a contiguous run of logical blocks keeps the
-// tiles that share a cache line of scales / qzeros inside ONE L2 (no partial-line merges
-// across XCDs)
-#ifndef AWQ_XCD_REMAP
-#define AWQ_XCD_REMAP 0
 #endif
 // __launch_bounds__ minimum waves per SIMD (8 = 32 waves per CU: <= 64 VGPRs, <= 80 SGPRs)
 #ifndef AWQ_MIN_WAVES
@@ -76,10 +54,6 @@
 // group min/max from raw bf16 bits (1) or from order-preserving int16 keys (0)
 #ifndef AWQ_RAW_MINMAX
 #define AWQ_RAW_MINMAX 1
-#endif
-// tile -> wave assignment: 1 = interleaved (tile t on wave t mod nwaves), 0 = contiguous
-#ifndef AWQ_ASSIGN_STRIDED
-#define AWQ_ASSIGN_STRIDED 1
 #endif
 
 namespace awq {
@@ -351,63 +325,13 @@ __device__ __forceinline__ void tile_src(int64_t rows, int64_t K, uint32_t tile,
 
 // 4 x 16-B loads per lane: slot 4j + row, 16-B chunk c of the group.  Slots past the tile
 // end fall outside the descriptor's range and read as zero.
-[[maybe_unused]] __device__ __forceinline__ void load_tile(const TileCtx& c, u4 (&v)[4]) {
+__device__ __forceinline__ void load_tile(const TileCtx& c, u4 (&v)[4]) {
     const int lane = threadIdx.x & 63;
     const int row = lane >> 4, ch = lane & 15;
     const __amdgpu_buffer_rsrc_t rw = rsrc(c.wp, c.ng * 256u);
 #pragma unroll
     for (int j = 0; j < 4; ++j)
         v[j] = __builtin_amdgcn_raw_buffer_load_b128(rw, (uint32_t)((4 * j + row) * 256 + ch * 16), 0, AWQ_LOAD_AUX);
-}
-
-// Same 4 KiB as load_tile, streamed into the wave's LDS slot by LDS-DMA: instruction j
-// writes 1 KiB contiguously (lane i -> slot + j*1024 + 16*i), i.e. the slot is a byte copy
-// of the tile and lane i later reads back exactly the 16 B load_tile would have given it.
-//
-// Two forms.  The builtin (default): the compiler then puts s_waitcnt vmcnt(0) in front
-// of every later LDS access of the wave (the qzeros ds_or, the slot read-out), which also
-// drains the tile's qweight stores.  The inline-asm form (AWQ_DMA_ASM=1) hides the DMA
-// from the compiler so the loop waits once, counted (vmcnt counts loads, stores and
-// LDS-DMA together, in issue order: MI355X_MICROARCH.md "s_waitcnt vmcnt(N)").  Measured
-// (profiles/r20_kbench.log): no gain — 0-4 % slower — so the store drains are not what
-// bounds this kernel.  A loader/consumer variant (one DMA wave per workgroup feeding a
-// ring of 4-16 slots) was also measured and was 8-50 % slower (r21_kbench.log).
-#if AWQ_LOAD_AUX == 2
-#define AWQ_DMA_POLICY " nt"
-#elif AWQ_LOAD_AUX == 0
-#define AWQ_DMA_POLICY ""
-#else
-#error "AWQ_LOAD_AUX must be 0 or 2 for the asm LDS-DMA"
-#endif
-[[maybe_unused]] __device__ __forceinline__ void dma_tile_asm(const uint16_t* wp, uint32_t ng, uint8_t* slot) {
-    const int lane = threadIdx.x & 63;
-    const uint64_t base = (uint64_t)wp;
-    const u4 desc = {(uint32_t)base, (uint32_t)(base >> 32) & 0xFFFFu, ng * 256u, 0x00020000u};
-    const uint32_t lds = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint8_t*)slot;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const uint32_t voff = (uint32_t)(j * 1024 + lane * 16);
-        uint32_t saved_m0;   // m0 is a compiler-reserved register: saved and restored here
-        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\t"
-                     "buffer_load_dwordx4 %2, %3, 0 offen" AWQ_DMA_POLICY " lds\n\ts_mov_b32 m0, %0"
-                     : "=&s"(saved_m0) : "s"(lds + (uint32_t)(j * 1024)), "v"(voff), "s"(desc) : "memory");
-    }
-}
-
-// builtin form: the compiler then waits vmcnt(0) before the wave's next LDS access —
-// measured no slower for the one-slot-per-wave driver (its only LDS accesses sit right
-// where it has to wait anyway)
-[[maybe_unused]] __device__ __forceinline__ void dma_tile(const uint16_t* wp, uint32_t ng, uint8_t* slot) {
-#if AWQ_DMA_ASM
-    dma_tile_asm(wp, ng, slot);
-#else
-    const int lane = threadIdx.x & 63;
-    const __amdgpu_buffer_rsrc_t rw = rsrc(wp, ng * 256u);
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rw, (__attribute__((address_space(3))) void*)(slot + j * 1024), 16,
-                                                 (uint32_t)(j * 1024 + lane * 16), 0, 0, AWQ_LOAD_AUX);
-#endif
 }
 
 template <int BITS, bool SYM>
@@ -637,136 +561,67 @@ __device__ __forceinline__ void compute_tile(const TileCtx& c, const u4 (&v)[4],
     return __builtin_amdgcn_readfirstlane(base);
 }
 
-// Wave-level driver.  Each wave owns a contiguous range of tiles (consecutive tiles are
-// consecutive bytes of one tensor, crossing into the next tensor at its end); the next
-// tile's 4 loads are issued before the current tile is computed (register double buffer),
-// so every wave keeps 4 KiB of HBM reads in flight while it computes.
+#ifdef AWQ_TRACE
+__device__ uint64_t* g_trace = nullptr;
+#endif
+
+// One wave per tile.  The grid normally covers every tile once (launch_fast); a smaller
+// grid (AWQ_HIP_MAX_BLOCKS, tests) makes each wave walk tiles t, t + nwaves, ... with a
+// tensor cursor.
 template <int BITS, bool SYM>
 __global__ __launch_bounds__(256, AWQ_MIN_WAVES) void awq_fast_kernel(const awq_tensor_desc* __restrict__ descs,
+                                                       const int32_t* __restrict__ block_tensor,
                                                        awq_tensor_desc single, int n,
                                                        int64_t total_tiles) {
     __shared__ uint32_t zwords[kWavesPerBlock][kSlots];
     // wave index made provably uniform so tile/tensor bookkeeping and the buffer
     // descriptors live in SGPRs (no waterfall loops around the descriptors)
     const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-#if AWQ_XCD_REMAP
-    const uint32_t nb = gridDim.x;
-    const uint32_t lb = (nb % kXcds) ? blockIdx.x : (blockIdx.x % kXcds) * (nb / kXcds) + blockIdx.x / kXcds;
-    const int64_t wave = (int64_t)lb * kWavesPerBlock + wid;
-#else
     const int64_t wave = (int64_t)blockIdx.x * kWavesPerBlock + wid;
-#endif
     const int64_t nwaves = (int64_t)gridDim.x * kWavesPerBlock;
-#if AWQ_ASSIGN_STRIDED
-    // interleaved: at any moment the waves of the chip read one compact window of memory
-    int64_t t = wave * AWQ_CHUNK;
-    const int64_t step = nwaves;
-    const int64_t t_end = total_tiles;
-#else
-    const int64_t per = (total_tiles + nwaves - 1) / nwaves;
-    int64_t t = wave * per;
-    const int64_t step = 1;
-    const int64_t t_end = min(t + per, total_tiles);
-#endif
-    if (t >= t_end) return;
+    if (wave >= total_tiles) return;
     uint32_t* zw = zwords[wid];
-
+#ifdef AWQ_TRACE
+    // timing-only build: per wave (start, first tile done, end, tiles) in s_memrealtime
+    // ticks (100 MHz, chip-wide clock) -> scripts/trace_waves.py
+    const uint64_t tr0 = __builtin_amdgcn_s_memrealtime();
+    uint64_t tr1 = 0;
+    uint32_t trn = 0;
+#endif
     int cur = 0;
     awq_tensor_desc d = single;
     if (descs != nullptr) {
-        cur = find_tensor(descs, n, 0, t);
+        if (block_tensor != nullptr) {
+            // host-planned tensor of the block's first tile (awq_plan_block_tensor): one
+            // scalar load, then at most a few steps over 1-tile tensors
+            cur = __builtin_amdgcn_readfirstlane(block_tensor[blockIdx.x]);
+            while (cur + 1 < n && descs[cur + 1].tile_begin <= wave) ++cur;
+        } else {
+            cur = find_tensor(descs, n, 0, wave);
+        }
         d = descs[cur];
     }
-    TileCtx ctx = make_ctx<BITS>(d, (uint32_t)(t - d.tile_begin));
-#if AWQ_PREFETCH == 2
-    // LDS-DMA pipeline: the next tile streams HBM -> LDS (buffer_load ... lds, no VGPRs)
-    // while this tile is computed; each wave owns one 4 KiB staging slot.  Only the next
-    // tile's source range is carried across the compute (few SGPRs): the full tile
-    // context is rebuilt right before it is used.
-    __shared__ __attribute__((aligned(16))) uint8_t stage[kWavesPerBlock][kSlots * 256];
-    uint8_t* slot = stage[wid];
-    const int lane = threadIdx.x & 63;
-    {
-        uint32_t st, ng;
-        tile_src<BITS>(d.rows, d.K, (uint32_t)(t - d.tile_begin), st, ng);
-        dma_tile((const uint16_t*)d.w + (uint64_t)st * kGroup, ng, slot);
-    }
-    bool prev_stores = false;
-    for (; t < t_end;) {
-#if AWQ_ASSIGN_STRIDED && AWQ_CHUNK > 1
-        const int64_t tn = ((t + 1) % AWQ_CHUNK) ? t + 1 : t + 1 + (step - 1) * AWQ_CHUNK;
-#else
-        const int64_t tn = t + step;
-#endif
-        const bool more = tn < t_end;
-        int nc = cur;
-        const uint16_t* nwp = nullptr;
-        uint32_t nng = 0;
-        if (more) {
-            if (descs != nullptr && cur + 1 < n && descs[cur + 1].tile_begin <= tn) {
-                nc = find_tensor(descs, n, cur + 1, tn);
-                const awq_tensor_desc* nd = descs + nc;
-                uint32_t st;
-                tile_src<BITS>(nd->rows, nd->K, (uint32_t)(tn - nd->tile_begin), st, nng);
-                nwp = (const uint16_t*)nd->w + (uint64_t)st * kGroup;
-            } else {
-                uint32_t st;
-                tile_src<BITS>(d.rows, d.K, (uint32_t)(tn - d.tile_begin), st, nng);
-                nwp = (const uint16_t*)d.w + (uint64_t)st * kGroup;
-            }
-        }
-        // this tile has landed in LDS: all but the youngest `prev_stores` vector-memory
-        // ops done — those are the previous tile's qweight stores, issued after this DMA
-        if (prev_stores && AWQ_DMA_ASM) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        u4 va[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) va[j] = *(const u4*)(slot + j * 1024 + lane * 16);
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");     // slot read out: reusable
-        if (more) dma_tile(nwp, nng, slot);
-        compute_tile<BITS, SYM>(make_ctx<BITS>(d, (uint32_t)(t - d.tile_begin)), va, zw);
-        prev_stores = d.qweight != nullptr;   // compute_tile issued 4 qweight stores after the DMA
-        if (nc != cur) {
-            cur = nc;
-            d = descs[cur];
-        }
-        t = tn;
-    }
-    return;
-#elif !AWQ_PREFETCH
-    // single-buffered: occupancy hides the latency (fewer VGPRs -> more waves)
-    for (; t < t_end; t += step) {
+    for (int64_t t = wave; t < total_tiles; t += nwaves) {
         if (descs != nullptr && cur + 1 < n && descs[cur + 1].tile_begin <= t) {
             cur = find_tensor(descs, n, cur + 1, t);
             d = descs[cur];
         }
-        ctx = make_ctx<BITS>(d, (uint32_t)(t - d.tile_begin));
+        const TileCtx ctx = make_ctx<BITS>(d, (uint32_t)(t - d.tile_begin));
         u4 va[4];
         load_tile(ctx, va);
         compute_tile<BITS, SYM>(ctx, va, zw);
-    }
-    return;
+#ifdef AWQ_TRACE
+        if (trn++ == 0) tr1 = __builtin_amdgcn_s_memrealtime();
 #endif
-    u4 va[4];
-    load_tile(ctx, va);
-    for (; t < t_end; t += step) {
-        const int64_t tn = t + step;
-        const bool more = tn < t_end;
-        TileCtx nctx = ctx;
-        u4 vb[4] = {};
-        if (more) {
-            if (descs != nullptr && cur + 1 < n && descs[cur + 1].tile_begin <= tn) {
-                cur = find_tensor(descs, n, cur + 1, tn);
-                d = descs[cur];
-            }
-            nctx = make_ctx<BITS>(d, (uint32_t)(tn - d.tile_begin));
-            load_tile(nctx, vb);
-        }
-        compute_tile<BITS, SYM>(ctx, va, zw);
-        ctx = nctx;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) va[j] = vb[j];
     }
+#ifdef AWQ_TRACE
+    if (g_trace != nullptr && (threadIdx.x & 63) == 0) {
+        g_trace[wave * 4 + 0] = tr0;
+        g_trace[wave * 4 + 1] = tr1;
+        g_trace[wave * 4 + 2] = __builtin_amdgcn_s_memrealtime();
+        g_trace[wave * 4 + 3] = trn;
+    }
+#endif
 }
 
 // Exhaustive self-test of recip_bf16 over every non-negative bf16 bit pattern
@@ -783,47 +638,34 @@ __global__ void awq_selftest_recip_kernel(unsigned long long* mismatches) {
         atomicAdd(mismatches, 1ull);
 }
 
-int resident_blocks(const void* fn, int variant) {
-    // workgroups the device can hold at once for this kernel (grid = one full wave of
-    // workgroups; every wave then walks a contiguous tile range)
-    static int cache[64][4];
-    static bool init[64][4];
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 0;
-    if (!init[dev][variant]) {
-        int cus = 0, per_cu = 0;
-        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, 256, 0);
-        if (cus <= 0) cus = 256;
-        if (per_cu <= 0) per_cu = 4;
-        cache[dev][variant] = cus * per_cu;
-        init[dev][variant] = true;
-    }
-    return cache[dev][variant];
-}
-
 }  // namespace
 
-hipError_t launch_fast(const awq_tensor_desc* descs_dev, const awq_tensor_desc* single, int n,
-                       int64_t total_tiles, int bits, int symmetric, hipStream_t stream) {
+hipError_t launch_fast(const awq_tensor_desc* descs_dev, const int32_t* block_tensor,
+                       const awq_tensor_desc* single, int n, int64_t total_tiles, int bits, int symmetric,
+                       hipStream_t stream) {
     if (total_tiles <= 0) return hipSuccess;
-    const void* fns[4] = {(const void*)awq_fast_kernel<4, false>, (const void*)awq_fast_kernel<4, true>,
-                          (const void*)awq_fast_kernel<8, false>, (const void*)awq_fast_kernel<8, true>};
-    const int variant = (bits == 8 ? 2 : 0) + (symmetric ? 1 : 0);
-    int64_t max_blocks = resident_blocks(fns[variant], variant);
-    if (const char* e = getenv("AWQ_HIP_MAX_BLOCKS")) {   // testing / tuning: override the grid
-        long v = atol(e);
+    // one wave per tile (tuning / tests: AWQ_HIP_TILES_PER_WAVE = tiles per wave,
+    // AWQ_HIP_MAX_BLOCKS = grid cap; either makes waves walk several tiles)
+    int64_t tpw = 1, max_blocks = INT32_MAX;
+    if (const char* e = getenv("AWQ_HIP_TILES_PER_WAVE")) {
+        const long v = atol(e);
+        if (v > 0) tpw = v;
+    }
+    if (const char* e = getenv("AWQ_HIP_MAX_BLOCKS")) {
+        const long v = atol(e);
         if (v > 0) max_blocks = v;
     }
-    constexpr int64_t kTilesPerBlock = kWavesPerBlock * AWQ_CHUNK;
-    int64_t blocks = (total_tiles + kTilesPerBlock - 1) / kTilesPerBlock;
+    const int64_t per_block = kWavesPerBlock * tpw;
+    int64_t blocks = (total_tiles + per_block - 1) / per_block;
     if (blocks > max_blocks) blocks = max_blocks;
     awq_tensor_desc one{};
     if (single) one = *single;
-    dim3 grid((unsigned)blocks), block(256);
+    // the table describes the one-tile-per-wave grid only
+    const int32_t* bt = (tpw == 1 && blocks * per_block >= total_tiles) ? block_tensor : nullptr;
+    const dim3 grid((unsigned)blocks), block(256);
 #define AWQ_LAUNCH(B, S) \
-    hipLaunchKernelGGL((awq_fast_kernel<B, S>), grid, block, 0, stream, descs_dev, one, n, total_tiles)
-    switch (variant) {
+    hipLaunchKernelGGL((awq_fast_kernel<B, S>), grid, block, 0, stream, descs_dev, bt, one, n, total_tiles)
+    switch ((bits == 8 ? 2 : 0) + (symmetric ? 1 : 0)) {
     case 0: AWQ_LAUNCH(4, false); break;
     case 1: AWQ_LAUNCH(4, true); break;
     case 2: AWQ_LAUNCH(8, false); break;
@@ -832,6 +674,12 @@ hipError_t launch_fast(const awq_tensor_desc* descs_dev, const awq_tensor_desc* 
 #undef AWQ_LAUNCH
     return hipPeekAtLastError();
 }
+
+#ifdef AWQ_TRACE
+extern "C" int awq_debug_set_trace(void* buf) {
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_trace), &buf, sizeof(buf)) == hipSuccess ? 0 : 1;
+}
+#endif
 
 hipError_t launch_selftest(int which, unsigned long long* out, hipStream_t stream) {
     if (which != 0) return hipErrorInvalidValue;

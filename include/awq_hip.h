@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define AWQ_HIP_ABI_VERSION 1
+#define AWQ_HIP_ABI_VERSION 2
 
 /* dtype codes of the input weights (torch dtypes the reference accepts, awq.py:397) */
 enum { AWQ_DTYPE_BF16 = 0, AWQ_DTYPE_F16 = 1, AWQ_DTYPE_F32 = 2, AWQ_DTYPE_F64 = 3 };
@@ -103,10 +103,18 @@ int awq_ragged_eligible(int dtype, int64_t rows, int64_t K, int64_t group_size);
  * and returns the total tile count (< 0 on error).  All tensors must be eligible. */
 int64_t awq_plan_ragged(awq_tensor_desc* descs_host, int n, int bits);
 
-/* Quantize n eligible tensors in ONE launch.  descs_device: device copy of the array
- * planned by awq_plan_ragged (the caller uploads it; it can be reused across calls). */
+/* HOST helper: block_tensor[b] = index of the tensor holding tile 4*b (the first tile of
+ * workgroup b of the one-wave-per-tile grid), b < ceil(total_tiles / 4) = the return
+ * value (< 0 on error: len too small).  descs_host as planned by awq_plan_ragged. */
+int64_t awq_plan_block_tensor(const awq_tensor_desc* descs_host, int n, int64_t total_tiles,
+                              int32_t* block_tensor_host, int64_t len);
+
+/* Quantize n eligible tensors in ONE launch (replaces the CLI's per-tensor loop,
+ * main.py:353-392).  descs_device: device copy of the array planned by awq_plan_ragged
+ * (the caller uploads it; reusable across calls).  block_tensor_device: optional device
+ * copy of the awq_plan_block_tensor table (NULL: each wave searches the descriptors). */
 int awq_quantize_ragged(const awq_tensor_desc* descs_device, int n, int64_t total_tiles,
-                        int bits, int symmetric, void* stream);
+                        const int32_t* block_tensor_device, int bits, int symmetric, void* stream);
 
 /* Reference dequantize (awq.py:459-539): out fp32 [rows, K] =
  * fp16( fp16(tensor_q - zeros) * scales ) per element. */

@@ -22,6 +22,7 @@ SETS = dict(bench.WORKLOADS)
 SETS["llama3-8b-mlp"] = [((14336, 4096), 8), ((4096, 14336), 4)]      # 705 M elements
 SETS["c1x64"] = [((1024, 4096), 64)]
 SETS["k768"] = [((50272, 768), 4)]
+SETS.setdefault("c1", [((1024, 4096), 1)])
 
 
 def shapes_of(name):
@@ -95,17 +96,21 @@ def main():
         for sname, bl in batches.items():
             for lp, lib in handles.items():
                 for blk in args.blocks.split(","):
-                    if blk != "0":
+                    os.environ.pop("AWQ_HIP_MAX_BLOCKS", None)
+                    os.environ.pop("AWQ_HIP_TILES_PER_WAVE", None)
+                    if blk.startswith("t"):          # t<N>: non-persistent grid, N tiles per wave
+                        os.environ["AWQ_HIP_TILES_PER_WAVE"] = blk[1:]
+                    elif blk not in ("0", "nt"):     # nt: no per-block tensor table
                         os.environ["AWQ_HIP_MAX_BLOCKS"] = blk
-                    else:
-                        os.environ.pop("AWQ_HIP_MAX_BLOCKS", None)
                     evs = []
                     for it in range(args.iters + 3):
                         bt = bl[it % len(bl)]
                         s0, s1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                         s0.record(stream)
+                        table = None if blk == "nt" or bt.block_tensor is None else bt.block_tensor.data_ptr()
                         rc = lib.awq_quantize_ragged(ctypes.c_void_p(bt.descs_dev.data_ptr()), len(bt.descs),
-                                                     bt.total_tiles, bt.bits, int(bt.symmetric),
+                                                     bt.total_tiles, ctypes.c_void_p(table), bt.bits,
+                                                     int(bt.symmetric),
                                                      ctypes.c_void_p(stream.cuda_stream))
                         s1.record(stream)
                         assert rc == 0, lib.awq_last_error()
@@ -116,6 +121,7 @@ def main():
                     key = (sname, os.path.basename(lp), blk)
                     results.setdefault(key, []).append(statistics.median(us))
     os.environ.pop("AWQ_HIP_MAX_BLOCKS", None)
+    os.environ.pop("AWQ_HIP_TILES_PER_WAVE", None)
     print(f"{'set':16s} {'lib':28s} {'blocks':>6s} {'us':>9s} {'algoGB/s':>9s} {'inGB/s':>8s} {'frac8T':>6s}")
     for (sname, lname, blk), v in results.items():
         bt = batches[sname][0]

@@ -27,7 +27,7 @@ def test_library_exports_every_declared_symbol():
     for s in syms:
         assert hasattr(lib, s), s
     assert set(syms) == set(_hip.SIGNATURES), "python binding out of sync with include/awq_hip.h"
-    assert lib.awq_abi_version() == 1
+    assert lib.awq_abi_version() == _hip.ABI_VERSION == 2
 
 
 def test_library_is_gfx950_code_object():
@@ -49,6 +49,12 @@ def test_host_helpers_without_gpu():
     # 1024 rows x G=32 -> 16-group tiles -> 2048; G=6 (even) -> byte tiles: 16 flat groups
     assert d[0].tile_count == 2048 and d[1].tile_count == 1 and d[2].tile_count == 19
     assert total == 2048 + 1 + 19 and d[2].tile_begin == 2049
+    # per-workgroup tensor table: block b holds tiles 4b..4b+3
+    arr = (_hip.TensorDesc * 3)(*d)
+    tab = torch.full((517,), -7, dtype=torch.int32)
+    assert lib.awq_plan_block_tensor(arr, 3, total, ctypes.c_void_p(tab.data_ptr()), 517) == 517
+    assert tab[:512].eq(0).all() and tab[512].item() == 1 and tab[513:].eq(2).all()   # tile 2048 -> t1, 2052.. -> t2
+    assert lib.awq_plan_block_tensor(arr, 3, total, ctypes.c_void_p(tab.data_ptr()), 100) < 0
     # G odd at 4 bits -> word tiles: K=384 (G=3) -> 5 rows (15 groups) per tile
     d = [_hip.TensorDesc(4096 * 16, 11, 384, 0, 0, 2 * 4096, 0, 0, 0, 0)]
     assert _hip.plan_ragged(d, 4) == 3

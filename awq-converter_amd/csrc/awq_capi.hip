@@ -4,6 +4,7 @@
 // errors through a thread-local message.  No allocation, no synchronisation, no global
 // mutable state: one instance may be called from many host threads at once (the
 // reference's CLI shares one quantizer between its worker threads, main.py:609-621).
+#include <algorithm>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
@@ -171,7 +172,9 @@ int64_t awq_plan_block_tensor(const awq_tensor_desc* descs, int n, int64_t total
     for (int64_t b = 0; b < need; ++b) {
         const int64_t t = b * awq::kWavesPerBlock;
         while (cur + 1 < n && descs[cur + 1].tile_begin <= t) ++cur;
-        block_tensor[b] = cur;
+        const int64_t last = std::min(t + awq::kWavesPerBlock, total_tiles) - 1;
+        const bool spans = cur + 1 < n && descs[cur + 1].tile_begin <= last;
+        block_tensor[b] = (int32_t)((uint32_t)cur | (spans ? 0x80000000u : 0u));
     }
     return need;
 }

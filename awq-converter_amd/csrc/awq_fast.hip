@@ -325,10 +325,10 @@ __device__ __forceinline__ void tile_src(int64_t rows, int64_t K, uint32_t tile,
 
 // 4 x 16-B loads per lane: slot 4j + row, 16-B chunk c of the group.  Slots past the tile
 // end fall outside the descriptor's range and read as zero.
-__device__ __forceinline__ void load_tile(const TileCtx& c, u4 (&v)[4]) {
+__device__ __forceinline__ void load_tile(const uint16_t* wp, uint32_t ng, u4 (&v)[4]) {
     const int lane = threadIdx.x & 63;
     const int row = lane >> 4, ch = lane & 15;
-    const __amdgpu_buffer_rsrc_t rw = rsrc(c.wp, c.ng * 256u);
+    const __amdgpu_buffer_rsrc_t rw = rsrc(wp, ng * 256u);
 #pragma unroll
     for (int j = 0; j < 4; ++j)
         v[j] = __builtin_amdgcn_raw_buffer_load_b128(rw, (uint32_t)((4 * j + row) * 256 + ch * 16), 0, AWQ_LOAD_AUX);
@@ -593,9 +593,11 @@ __global__ __launch_bounds__(256, AWQ_MIN_WAVES) void awq_fast_kernel(const awq_
     if (descs != nullptr) {
         if (block_tensor != nullptr) {
             // host-planned tensor of the block's first tile (awq_plan_block_tensor): one
-            // scalar load, then at most a few steps over 1-tile tensors
-            cur = __builtin_amdgcn_readfirstlane(block_tensor[blockIdx.x]);
-            while (cur + 1 < n && descs[cur + 1].tile_begin <= wave) ++cur;
+            // scalar load; blocks spanning tensors (small tensors) take a few more steps
+            const int32_t e = __builtin_amdgcn_readfirstlane(block_tensor[blockIdx.x]);
+            cur = e & 0x7FFFFFFF;
+            if (e < 0)   // the block's tiles span tensors (bit 31): step to this wave's one
+                while (cur + 1 < n && descs[cur + 1].tile_begin <= wave) ++cur;
         } else {
             cur = find_tensor(descs, n, 0, wave);
         }
@@ -606,10 +608,14 @@ __global__ __launch_bounds__(256, AWQ_MIN_WAVES) void awq_fast_kernel(const awq_
             cur = find_tensor(descs, n, cur + 1, t);
             d = descs[cur];
         }
-        const TileCtx ctx = make_ctx<BITS>(d, (uint32_t)(t - d.tile_begin));
+        // the input range first (no division for byte tiles): the loads go out before the
+        // rest of the tile context (row / group divisions) is computed
+        const uint32_t tile = (uint32_t)(t - d.tile_begin);
+        uint32_t st, ng;
+        tile_src<BITS>(d.rows, d.K, tile, st, ng);
         u4 va[4];
-        load_tile(ctx, va);
-        compute_tile<BITS, SYM>(ctx, va, zw);
+        load_tile((const uint16_t*)d.w + (uint64_t)st * kGroup, ng, va);
+        compute_tile<BITS, SYM>(make_ctx<BITS>(d, tile), va, zw);
 #ifdef AWQ_TRACE
         if (trn++ == 0) tr1 = __builtin_amdgcn_s_memrealtime();
 #endif

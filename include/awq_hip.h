@@ -104,8 +104,9 @@ int awq_ragged_eligible(int dtype, int64_t rows, int64_t K, int64_t group_size);
 int64_t awq_plan_ragged(awq_tensor_desc* descs_host, int n, int bits);
 
 /* HOST helper: block_tensor[b] = index of the tensor holding tile 4*b (the first tile of
- * workgroup b of the one-wave-per-tile grid), b < ceil(total_tiles / 4) = the return
- * value (< 0 on error: len too small).  descs_host as planned by awq_plan_ragged. */
+ * workgroup b of the one-wave-per-tile grid), with bit 31 set when the workgroup's 4
+ * tiles span more than one tensor; b < ceil(total_tiles / 4) = the return value (< 0 on
+ * error: len too small).  descs_host as planned by awq_plan_ragged. */
 int64_t awq_plan_block_tensor(const awq_tensor_desc* descs_host, int n, int64_t total_tiles,
                               int32_t* block_tensor_host, int64_t len);
 

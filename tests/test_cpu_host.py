@@ -53,7 +53,8 @@ def test_host_helpers_without_gpu():
     arr = (_hip.TensorDesc * 3)(*d)
     tab = torch.full((517,), -7, dtype=torch.int32)
     assert lib.awq_plan_block_tensor(arr, 3, total, ctypes.c_void_p(tab.data_ptr()), 517) == 517
-    assert tab[:512].eq(0).all() and tab[512].item() == 1 and tab[513:].eq(2).all()   # tile 2048 -> t1, 2052.. -> t2
+    # block 512 = tiles 2048 (t1), 2049-2051 (t2): spans -> bit 31
+    assert tab[:512].eq(0).all() and tab[512].item() == (1 | -2**31) and tab[513:].eq(2).all()
     assert lib.awq_plan_block_tensor(arr, 3, total, ctypes.c_void_p(tab.data_ptr()), 100) < 0
     # G odd at 4 bits -> word tiles: K=384 (G=3) -> 5 rows (15 groups) per tile
     d = [_hip.TensorDesc(4096 * 16, 11, 384, 0, 0, 2 * 4096, 0, 0, 0, 0)]

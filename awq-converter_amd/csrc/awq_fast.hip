@@ -51,6 +51,11 @@
 #ifndef AWQ_MIN_WAVES
 #define AWQ_MIN_WAVES 8
 #endif
+// qweight stores: 1 = staged through LDS into one 16-B store per lane (4-bit: 1 store
+// instruction per tile instead of 4), 0 = one dword per lane per group row
+#ifndef AWQ_WIDE_STORE
+#define AWQ_WIDE_STORE 1
+#endif
 // group min/max from raw bf16 bits (1) or from order-preserving int16 keys (0)
 #ifndef AWQ_RAW_MINMAX
 #define AWQ_RAW_MINMAX 1
@@ -335,7 +340,7 @@ __device__ __forceinline__ void load_tile(const uint16_t* wp, uint32_t ng, u4 (&
 }
 
 template <int BITS, bool SYM>
-__device__ __forceinline__ void compute_tile(const TileCtx& c, const u4 (&v)[4], uint32_t* zw) {
+__device__ __forceinline__ void compute_tile(const TileCtx& c, const u4 (&v)[4], uint32_t* zw, uint32_t* qstage) {
     constexpr int QMIN = SYM ? -(1 << (BITS - 1)) : 0;
     constexpr uint32_t C = 32u / BITS;   // groups per qzeros word
     const int lane = threadIdx.x & 63;
@@ -453,6 +458,12 @@ __device__ __forceinline__ void compute_tile(const TileCtx& c, const u4 (&v)[4],
             }
         }
         if (c.qweight) {
+#if AWQ_WIDE_STORE
+            // staged in the wave's LDS block in output order (lanes of one j write 64
+            // consecutive words), stored below as one 16-B piece per lane
+            if (BITS == 4) qstage[slot * 16 + ch] = word.x;
+            else *(u2v*)(qstage + slot * 32 + 2 * ch) = word;
+#else
             if (BITS == 4) {
                 __amdgpu_buffer_rsrc_t rq = rsrc(c.qweight + (uint64_t)c.start * 16, ng * 64u);
                 __builtin_amdgcn_raw_buffer_store_b32(word.x, rq, (uint32_t)((slot * 16 + ch) * 4), 0, AWQ_STORE_AUX);
@@ -460,6 +471,7 @@ __device__ __forceinline__ void compute_tile(const TileCtx& c, const u4 (&v)[4],
                 __amdgpu_buffer_rsrc_t rq = rsrc(c.qweight + (uint64_t)c.start * 32, ng * 128u);
                 __builtin_amdgcn_raw_buffer_store_b64(word, rq, (uint32_t)((slot * 32 + 2 * ch) * 4), 0, AWQ_STORE_AUX);
             }
+#endif
         }
         if (c.tensor_q) {   // reference-layout int32 tensor_q (parity mode)
             if (!special) {
@@ -477,6 +489,17 @@ __device__ __forceinline__ void compute_tile(const TileCtx& c, const u4 (&v)[4],
             __builtin_amdgcn_raw_buffer_store_b128(hi, rt, (uint32_t)((slot * kGroup + 8 * ch) * 4 + 16), 0, AWQ_STORE_AUX);
         }
     }
+#if AWQ_WIDE_STORE
+    if (c.qweight) {   // 4-bit: 1 KiB per tile = one dwordx4 per lane; 8-bit: 2 KiB, two
+        const int lane_ = threadIdx.x & 63;
+        __amdgpu_buffer_rsrc_t rq = rsrc(c.qweight + (uint64_t)c.start * (BITS == 4 ? 16 : 32), ng * (BITS == 4 ? 64u : 128u));
+#pragma unroll
+        for (int h = 0; h < (BITS == 4 ? 1 : 2); ++h) {
+            const u4 w4 = *(const u4*)(qstage + h * 256 + lane_ * 4);
+            __builtin_amdgcn_raw_buffer_store_b128(w4, rq, (uint32_t)(h * 1024 + lane_ * 16), 0, AWQ_STORE_AUX);
+        }
+    }
+#endif
     // ---- 5. per-group scalars out (after the data registers are dead): lanes ch < 4 hold slots 0..15 (one store each) ----
     if (ch < 4) {
         if (c.scales) {
@@ -569,11 +592,14 @@ __device__ uint64_t* g_trace = nullptr;
 // grid (AWQ_HIP_MAX_BLOCKS, tests) makes each wave walk tiles t, t + nwaves, ... with a
 // tensor cursor.
 template <int BITS, bool SYM>
-__global__ __launch_bounds__(256, AWQ_MIN_WAVES) void awq_fast_kernel(const awq_tensor_desc* __restrict__ descs,
+__global__ __launch_bounds__(64 * kWavesPerBlock, AWQ_MIN_WAVES) void awq_fast_kernel(const awq_tensor_desc* __restrict__ descs,
                                                        const int32_t* __restrict__ block_tensor,
                                                        awq_tensor_desc single, int n,
                                                        int64_t total_tiles) {
     __shared__ uint32_t zwords[kWavesPerBlock][kSlots];
+#if AWQ_WIDE_STORE
+    __shared__ __attribute__((aligned(16))) uint32_t qstage_all[kWavesPerBlock][BITS == 4 ? 256 : 512];
+#endif
     // wave index made provably uniform so tile/tensor bookkeeping and the buffer
     // descriptors live in SGPRs (no waterfall loops around the descriptors)
     const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -581,12 +607,16 @@ __global__ __launch_bounds__(256, AWQ_MIN_WAVES) void awq_fast_kernel(const awq_
     const int64_t nwaves = (int64_t)gridDim.x * kWavesPerBlock;
     if (wave >= total_tiles) return;
     uint32_t* zw = zwords[wid];
+#if AWQ_WIDE_STORE
+    uint32_t* qs = qstage_all[wid];
+#else
+    uint32_t* qs = nullptr;
+#endif
 #ifdef AWQ_TRACE
-    // timing-only build: per wave (start, first tile done, end, tiles) in s_memrealtime
-    // ticks (100 MHz, chip-wide clock) -> scripts/trace_waves.py
+    // timing-only build: per wave (start, first tile's loads issued, landed, end) in
+    // s_memrealtime ticks (100 MHz, chip-wide clock) -> scripts/trace_waves.py
     const uint64_t tr0 = __builtin_amdgcn_s_memrealtime();
-    uint64_t tr1 = 0;
-    uint32_t trn = 0;
+    uint64_t tr1 = 0, tr2 = 0;
 #endif
     int cur = 0;
     awq_tensor_desc d = single;
@@ -615,17 +645,21 @@ __global__ __launch_bounds__(256, AWQ_MIN_WAVES) void awq_fast_kernel(const awq_
         tile_src<BITS>(d.rows, d.K, tile, st, ng);
         u4 va[4];
         load_tile((const uint16_t*)d.w + (uint64_t)st * kGroup, ng, va);
-        compute_tile<BITS, SYM>(make_ctx<BITS>(d, tile), va, zw);
 #ifdef AWQ_TRACE
-        if (trn++ == 0) tr1 = __builtin_amdgcn_s_memrealtime();
+        if (tr1 == 0) {
+            tr1 = __builtin_amdgcn_s_memrealtime();
+            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+            tr2 = __builtin_amdgcn_s_memrealtime();
+        }
 #endif
+        compute_tile<BITS, SYM>(make_ctx<BITS>(d, tile), va, zw, qs);
     }
 #ifdef AWQ_TRACE
     if (g_trace != nullptr && (threadIdx.x & 63) == 0) {
         g_trace[wave * 4 + 0] = tr0;
         g_trace[wave * 4 + 1] = tr1;
-        g_trace[wave * 4 + 2] = __builtin_amdgcn_s_memrealtime();
-        g_trace[wave * 4 + 3] = trn;
+        g_trace[wave * 4 + 2] = tr2;
+        g_trace[wave * 4 + 3] = __builtin_amdgcn_s_memrealtime();
     }
 #endif
 }
@@ -668,7 +702,7 @@ hipError_t launch_fast(const awq_tensor_desc* descs_dev, const int32_t* block_te
     if (single) one = *single;
     // the table describes the one-tile-per-wave grid only
     const int32_t* bt = (tpw == 1 && blocks * per_block >= total_tiles) ? block_tensor : nullptr;
-    const dim3 grid((unsigned)blocks), block(256);
+    const dim3 grid((unsigned)blocks), block(64 * kWavesPerBlock);
 #define AWQ_LAUNCH(B, S) \
     hipLaunchKernelGGL((awq_fast_kernel<B, S>), grid, block, 0, stream, descs_dev, bt, one, n, total_tiles)
     switch ((bits == 8 ? 2 : 0) + (symmetric ? 1 : 0)) {

@@ -26,8 +26,11 @@ namespace awq {
 // ---------------------------------------------------------------------------
 constexpr int kGroup = 128;          // elements per group on the fast path
 constexpr int kSlots = 16;           // group slots per wave-tile (4 loads x 4 lane-rows)
-constexpr int kWavesPerBlock = 4;    // 256-thread workgroups
-constexpr uint32_t kXcds = 8;        // MI355X: 8 XCDs x 32 CUs, each XCD with its own L2
+#ifndef AWQ_WPB
+#define AWQ_WPB AWQ_BLOCK_TILES   // include/awq_hip.h (tuning builds may override)
+#endif
+constexpr int kWavesPerBlock = AWQ_WPB;   // waves (= tiles) per workgroup: 8 = 512 threads (halves the
+                                          // workgroup dispatch rate the one-wave-per-tile grid needs)
 
 struct TensorGeom {
     uint32_t G;    // groups per row

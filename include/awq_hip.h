@@ -103,10 +103,13 @@ int awq_ragged_eligible(int dtype, int64_t rows, int64_t K, int64_t group_size);
  * and returns the total tile count (< 0 on error).  All tensors must be eligible. */
 int64_t awq_plan_ragged(awq_tensor_desc* descs_host, int n, int bits);
 
-/* HOST helper: block_tensor[b] = index of the tensor holding tile 4*b (the first tile of
- * workgroup b of the one-wave-per-tile grid), with bit 31 set when the workgroup's 4
- * tiles span more than one tensor; b < ceil(total_tiles / 4) = the return value (< 0 on
- * error: len too small).  descs_host as planned by awq_plan_ragged. */
+/* Tiles (= waves) per workgroup of the ragged kernel's one-wave-per-tile grid. */
+#define AWQ_BLOCK_TILES 8
+
+/* HOST helper: block_tensor[b] = index of the tensor holding tile AWQ_BLOCK_TILES * b (the
+ * first tile of workgroup b), with bit 31 set when the workgroup's tiles span more than
+ * one tensor; b < ceil(total_tiles / AWQ_BLOCK_TILES) = the return value (< 0 on error:
+ * len too small).  descs_host as planned by awq_plan_ragged. */
 int64_t awq_plan_block_tensor(const awq_tensor_desc* descs_host, int n, int64_t total_tiles,
                               int32_t* block_tensor_host, int64_t len);
 

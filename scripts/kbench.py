@@ -91,6 +91,19 @@ def main():
     torch.cuda.synchronize()
 
     stream = torch.cuda.current_stream(dev)
+    tables = {}
+
+    def block_table(lp, lib, bt):
+        """the per-workgroup tensor table planned by THIS library (its own workgroup size)"""
+        key = (lp, id(bt))
+        if key not in tables:
+            arr = (_hip.TensorDesc * len(bt.descs))(*bt.descs)
+            host = torch.empty(-(-bt.total_tiles // 4), dtype=torch.int32)
+            rc = lib.awq_plan_block_tensor(arr, len(bt.descs), bt.total_tiles, ctypes.c_void_p(host.data_ptr()),
+                                           host.numel())
+            assert rc > 0, lib.awq_last_error()
+            tables[key] = host.to(dev)
+        return tables[key]
     results = {}
     for rnd in range(args.rounds):
         for sname, bl in batches.items():
@@ -107,7 +120,7 @@ def main():
                         bt = bl[it % len(bl)]
                         s0, s1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                         s0.record(stream)
-                        table = None if blk == "nt" or bt.block_tensor is None else bt.block_tensor.data_ptr()
+                        table = None if blk == "nt" else block_table(lp, lib, bt).data_ptr()
                         rc = lib.awq_quantize_ragged(ctypes.c_void_p(bt.descs_dev.data_ptr()), len(bt.descs),
                                                      bt.total_tiles, ctypes.c_void_p(table), bt.bits,
                                                      int(bt.symmetric),

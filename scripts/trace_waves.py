@@ -1,12 +1,15 @@
 #!/usr/bin/env python3
 """Per-wave timeline of one ragged launch (build variant AWQ_TRACE: every wave records
-s_memrealtime at start, after its first tile, at the end, and its tile count).
+s_memrealtime at start, when its tile's loads are issued, when they have landed, and at
+the end).
 
   make -C awq-converter_amd/csrc variant-trace VFLAGS=-DAWQ_TRACE
   python scripts/trace_waves.py --set opt-125m
 
-Prints the launch span and how the waves fill it: start ramp, first-tile latency, the
-end-time distribution (the tail), and the busy fraction sum(end - start) / (waves x span).
+Prints the launch span, the median wave lifetime split into setup (start -> loads
+issued: kernel arguments, tensor table / descriptor loads, tile geometry), load wait
+(issued -> landed) and compute + store issue (landed -> end), and the mean number of
+live waves (sum of lifetimes / span; 8192 = every slot of the chip busy).
 The kernel must run its default one-wave-per-tile grid (no AWQ_HIP_* overrides): the
 trace buffer holds exactly one record per wave of that grid.
 """
@@ -22,7 +25,7 @@ import torch  # noqa: E402
 
 import kbench  # noqa: E402  (tensor-set manifests)
 
-TICK_NS = 10.0   # s_memrealtime: 100 MHz
+TICK_US = 0.01   # s_memrealtime: 100 MHz
 
 
 def main():
@@ -31,10 +34,12 @@ def main():
     ap.add_argument("--lib", default=os.path.join(ROOT, "awq-converter_amd/awq_quantizer/_lib/variants/libawq_hip_trace.so"))
     ap.add_argument("--reps", type=int, default=5)
     args = ap.parse_args()
+    for k in ("AWQ_HIP_MAX_BLOCKS", "AWQ_HIP_TILES_PER_WAVE"):
+        os.environ.pop(k, None)
     os.environ["AWQ_HIP_LIB"] = args.lib
     from awq_quantizer import _hip
     from awq_quantizer.quantization.batch import PackedBatch
-    lib = _hip.load_library()
+    _hip.load_library()
     raw = ctypes.CDLL(args.lib)
     dev = torch.device("cuda", 0)
     _hip.require_device(dev)
@@ -51,54 +56,27 @@ def main():
     nwaves = -(-max(b.total_tiles for b in batches) // 4) * 4
     buf = torch.zeros(nwaves * 4, dtype=torch.int64, device=dev)
     assert raw.awq_debug_set_trace(ctypes.c_void_p(buf.data_ptr())) == 0
-    out = []
     for it in range(3 * args.reps):
         buf.zero_()
-        batches[it % args.reps].run()
+        b = batches[it % args.reps]
+        b.run()
         torch.cuda.synchronize()
-        if it >= args.reps:
-            out.append(buf.view(nwaves, 4).cpu())
-    assert lib is not None
-    res = []
-    for tr in out:
-        act = tr[:, 3] > 0
-        t = tr[act].double()
-        t0 = t[:, 0].min()
-        start, first, end, n = (t[:, 0] - t0) * TICK_NS / 1e3, (t[:, 1] - t0) * TICK_NS / 1e3, \
-            (t[:, 2] - t0) * TICK_NS / 1e3, t[:, 3]
+        if it < args.reps:
+            continue
+        tr = buf.view(nwaves, 4)[: b.total_tiles].cpu().double()
+        t0 = tr[:, 0].min()
+        start, issued, landed, end = [(tr[:, i] - t0) * TICK_US for i in range(4)]
         span = float(end.max())
-        q = lambda v, p: float(torch.quantile(v, p))
-        busy = float((end - start).sum()) / (len(end) * span)
-        res.append({"waves": int(act.sum()), "span_us": round(span, 2),
-                    "start_us_p50_p99_max": [round(q(start, .5), 2), round(q(start, .99), 2), round(float(start.max()), 2)],
-                    "first_tile_done_us_p10_p50_p90": [round(q(first, .1), 2), round(q(first, .5), 2), round(q(first, .9), 2)],
-                    "end_us_p10_p50_p90_p99": [round(q(end, .1), 2), round(q(end, .5), 2), round(q(end, .9), 2), round(q(end, .99), 2)],
-                    "tiles_min_max": [int(n.min()), int(n.max())], "busy_fraction": round(busy, 3),
-                    "per_tile_us_median": round(q((end - first) / (n - 1).clamp(min=1), .5), 3)})
-    for r in res:
-        print(json.dumps({"set": args.set, **r}))
-    # where the slow waves are: wave w = 4 * block + wid; block b runs on XCD b % 8
-    tr = out[-1]
-    act = tr[:, 3] > 0
-    t = tr.double()
-    t0 = t[act, 0].min()
-    end = (t[:, 2] - t0) * TICK_NS / 1e3
-    w = torch.arange(nwaves)
-    blk = w // 4
-    xcd = blk % 8
-    per_xcd = {int(x): round(float(end[act & (xcd == x)].median()), 1) for x in range(8)}
-    slot = (blk // 8) % 256       # block's position within its XCD (~ CU after 8 blocks/CU)
-    print(json.dumps({"end_median_by_xcd_us": per_xcd}))
-    print(json.dumps({"end_median_by_wid_us": {int(i): round(float(end[act & (w % 4 == i)].median()), 1) for i in range(4)}}))
-    # block-level spread inside one XCD and between the 4 waves of a block
-    e = end.view(-1, 4)
-    print(json.dumps({"within_block_range_us_median": round(float((e.max(1).values - e.min(1).values).median()), 2),
-                      "block_end_p10_p50_p90_us": [round(float(torch.quantile(e.max(1).values, q)), 1) for q in (.1, .5, .9)]}))
-    bend = e.max(1).values
-    order = torch.argsort(bend)
-    print(json.dumps({"fastest_blocks": order[:8].tolist(), "slowest_blocks": order[-8:].tolist(),
-                      "blocks_per_xcd_in_fastest_quarter": torch.bincount((order[:512] % 8), minlength=8).tolist()}))
-    del slot
+        q = lambda v, p: round(float(torch.quantile(v, p)), 2)
+        life = end - start
+        print(json.dumps({
+            "set": args.set, "waves": int(b.total_tiles), "span_us": round(span, 2),
+            "lifetime_us_p10_p50_p90": [q(life, .1), q(life, .5), q(life, .9)],
+            "setup_us_p50_p90": [q(issued - start, .5), q(issued - start, .9)],
+            "load_wait_us_p50_p90": [q(landed - issued, .5), q(landed - issued, .9)],
+            "compute_us_p50_p90": [q(end - landed, .5), q(end - landed, .9)],
+            "mean_live_waves": round(float(life.sum()) / span, 1),
+            "first_wave_end_us": q(end, 0.0), "start_of_last_wave_us": round(float(start.max()), 2)}))
 
 
 if __name__ == "__main__":

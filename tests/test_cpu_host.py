@@ -49,12 +49,13 @@ def test_host_helpers_without_gpu():
     # 1024 rows x G=32 -> 16-group tiles -> 2048; G=6 (even) -> byte tiles: 16 flat groups
     assert d[0].tile_count == 2048 and d[1].tile_count == 1 and d[2].tile_count == 19
     assert total == 2048 + 1 + 19 and d[2].tile_begin == 2049
-    # per-workgroup tensor table: block b holds tiles 4b..4b+3
+    # per-workgroup tensor table: workgroup b holds tiles 8b..8b+7 (AWQ_BLOCK_TILES)
     arr = (_hip.TensorDesc * 3)(*d)
-    tab = torch.full((517,), -7, dtype=torch.int32)
-    assert lib.awq_plan_block_tensor(arr, 3, total, ctypes.c_void_p(tab.data_ptr()), 517) == 517
-    # block 512 = tiles 2048 (t1), 2049-2051 (t2): spans -> bit 31
-    assert tab[:512].eq(0).all() and tab[512].item() == (1 | -2**31) and tab[513:].eq(2).all()
+    tab = torch.full((300,), -7, dtype=torch.int32)
+    assert lib.awq_plan_block_tensor(arr, 3, total, ctypes.c_void_p(tab.data_ptr()), 300) == 259
+    # block 256 = tiles 2048 (t1), 2049-2055 (t2): spans -> bit 31
+    assert tab[:256].eq(0).all() and tab[256].item() == (1 | -2**31) and tab[257:259].eq(2).all()
+    assert tab[259:].eq(-7).all()
     assert lib.awq_plan_block_tensor(arr, 3, total, ctypes.c_void_p(tab.data_ptr()), 100) < 0
     # G odd at 4 bits -> word tiles: K=384 (G=3) -> 5 rows (15 groups) per tile
     d = [_hip.TensorDesc(4096 * 16, 11, 384, 0, 0, 2 * 4096, 0, 0, 0, 0)]

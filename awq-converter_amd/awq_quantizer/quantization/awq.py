@@ -269,9 +269,9 @@ class AWQQuantizer:
                 "shape": torch.tensor(list(tensor.shape), dtype=torch.int64)}
 
     def quantize_model_packed(self, tensors: Dict[str, torch.Tensor]) -> Dict[str, Dict[str, torch.Tensor]]:
-        """Packed quantization of many tensors: every fast-path-eligible tensor (bf16,
-        group_size 128, K % 128 == 0) goes into ONE ragged launch; the rest are quantized
-        one by one.  Outputs stay on the device.  Failures are logged and skipped."""
+        """Packed quantization of many tensors: the fast-path-eligible tensors (bf16 or fp16,
+        group_size 128, K % 128 == 0) go into one ragged launch per dtype; the rest are
+        quantized one by one.  Outputs stay on the device.  Failures are logged and skipped."""
         from .batch import PackedBatch
         self._check_mode()
         eligible, rest = {}, {}
@@ -293,10 +293,12 @@ class AWQQuantizer:
         out = {}
         if eligible:
             dev = self.compute_device()
-            batch = PackedBatch({k: v.detach().to(dev).contiguous() for k, v in eligible.items()},
-                                bits=self.bits, symmetric=self.symmetric)
-            batch.run()
-            out.update(batch.results())
+            for dt in (torch.bfloat16, torch.float16):   # one ragged launch per input dtype
+                part = {k: v.detach().to(dev).contiguous() for k, v in eligible.items() if v.dtype == dt}
+                if part:
+                    batch = PackedBatch(part, bits=self.bits, symmetric=self.symmetric)
+                    batch.run()
+                    out.update(batch.results())
         for name, t in rest.items():
             try:
                 out[name] = self.quantize_packed(t)

@@ -17,7 +17,8 @@ from .. import _hip
 class PackedBatch:
     """Device-resident inputs + packed outputs of one ragged launch.
 
-    inputs: name -> contiguous bf16 device tensor ([rows, ...] or 1-D), K % 128 == 0.
+    inputs: name -> contiguous device tensor ([rows, ...] or 1-D), K % 128 == 0, all bf16 or
+    all fp16.
     parity=True additionally produces the reference's unpacked int32 tensor_q and
     zero_points (6.05 B/element of output traffic instead of 0.52).
     use_block_table: upload the per-workgroup tensor table (awq_plan_block_tensor; 4 B per
@@ -30,7 +31,10 @@ class PackedBatch:
             raise ValueError("PackedBatch needs at least one tensor")
         self.bits, self.symmetric, self.parity = bits, bool(symmetric), parity
         self.names = list(inputs)
-        dev = next(iter(inputs.values())).device
+        first = next(iter(inputs.values()))
+        dev, self.dtype = first.device, first.dtype
+        if self.dtype not in (torch.bfloat16, torch.float16):
+            raise ValueError(f"PackedBatch takes bf16 or fp16 tensors, got {self.dtype}")
         _hip.require_device(dev)
         self.device = dev
         self.inputs = inputs
@@ -39,8 +43,9 @@ class PackedBatch:
         descs = []
         for name in self.names:
             x = inputs[name]
-            if x.device != dev or x.dtype != torch.bfloat16 or not x.is_contiguous():
-                raise ValueError(f"{name}: inputs must be contiguous bf16 tensors on {dev}")
+            if x.device != dev or x.dtype != self.dtype or not x.is_contiguous():
+                raise ValueError(f"{name}: inputs must be contiguous {self.dtype} tensors on {dev} (one dtype "
+                                 f"per batch)")
             rows = 1 if x.dim() <= 1 else x.shape[0]
             K = x.numel() // rows
             if not _hip.ragged_eligible(x.dtype, rows, K, 128):
@@ -66,7 +71,7 @@ class PackedBatch:
     def run(self, stream: Optional[torch.cuda.Stream] = None) -> None:
         s = stream if stream is not None else torch.cuda.current_stream(self.device)
         _hip.quantize_ragged(self.descs_dev, len(self.descs), self.total_tiles, self.bits, self.symmetric,
-                             s.cuda_stream, self.block_tensor)
+                             s.cuda_stream, self.block_tensor, self.dtype)
 
     def results(self) -> Dict[str, Dict[str, torch.Tensor]]:
         res = {}
@@ -83,7 +88,7 @@ class PackedBatch:
         """HBM bytes one launch must move: bf16 in + packed out (+ parity outputs)."""
         b = 0
         for name in self.names:
-            b += self.inputs[name].numel() * 2
+            b += self.inputs[name].numel() * self.inputs[name].element_size()
             for t in self.out[name].values():
                 b += t.numel() * t.element_size()
         return b

@@ -42,7 +42,8 @@ int check_common(int64_t rows, int64_t K, int64_t group_size, int bits) {
 }
 
 bool fast_eligible(int dtype, int64_t rows, int64_t K, int64_t group_size) {
-    return dtype == AWQ_DTYPE_BF16 && group_size == awq::kGroup && awq::fast_shape_ok(rows, K);
+    return (dtype == AWQ_DTYPE_BF16 || dtype == AWQ_DTYPE_F16) && group_size == awq::kGroup &&
+           awq::fast_shape_ok(rows, K);
 }
 
 }  // namespace
@@ -92,7 +93,7 @@ int awq_quantize_groups(const void* w, int dtype, int64_t rows, int64_t K, int64
         d.w = w; d.rows = rows; d.K = K; d.qweight = qweight; d.qzeros = qzeros; d.scales = scales;
         d.tensor_q = tensor_q; d.zeros = zeros; d.tile_begin = 0;
         d.tile_count = awq::fast_tiles(rows, K, bits);
-        return hip_status(awq::launch_fast(nullptr, nullptr, &d, 1, d.tile_count, bits, symmetric, s),
+        return hip_status(awq::launch_fast(nullptr, nullptr, &d, 1, d.tile_count, dtype, bits, symmetric, s),
                           "awq fast kernel");
     }
     // generic path: per-group int32 values first, then packing (needs tensor_q / zeros buffers)
@@ -180,13 +181,15 @@ int64_t awq_plan_block_tensor(const awq_tensor_desc* descs, int n, int64_t total
 }
 
 int awq_quantize_ragged(const awq_tensor_desc* descs_device, int n, int64_t total_tiles,
-                        const int32_t* block_tensor_device, int bits, int symmetric, void* stream) {
+                        const int32_t* block_tensor_device, int dtype, int bits, int symmetric, void* stream) {
     g_err.clear();
     if (bits != 4 && bits != 8) return fail(AWQ_EINVAL, "Unsupported bit width: %d. Supported: 4, 8.", bits);
+    if (dtype != AWQ_DTYPE_BF16 && dtype != AWQ_DTYPE_F16)
+        return fail(AWQ_EINVAL, "ragged launches take bf16 or fp16 tensors (dtype code %d)", dtype);
     if (n <= 0 || total_tiles <= 0) return AWQ_OK;
     if (!descs_device) return fail(AWQ_EINVAL, "null descriptor array");
-    return hip_status(awq::launch_fast(descs_device, block_tensor_device, nullptr, n, total_tiles, bits, symmetric,
-                                       (hipStream_t)stream), "awq ragged kernel");
+    return hip_status(awq::launch_fast(descs_device, block_tensor_device, nullptr, n, total_tiles, dtype, bits,
+                                       symmetric, (hipStream_t)stream), "awq ragged kernel");
 }
 
 int awq_dequantize(const int32_t* tensor_q, const uint16_t* scales, const int32_t* zeros, int64_t rows,

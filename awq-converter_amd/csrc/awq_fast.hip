@@ -56,10 +56,6 @@
 #ifndef AWQ_WIDE_STORE
 #define AWQ_WIDE_STORE 1
 #endif
-// group min/max from raw bf16 bits (1) or from order-preserving int16 keys (0)
-#ifndef AWQ_RAW_MINMAX
-#define AWQ_RAW_MINMAX 1
-#endif
 
 namespace awq {
 namespace {
@@ -78,17 +74,6 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* base, uint32_
 
 __device__ __forceinline__ s2 as_s2(uint32_t u) { return __builtin_bit_cast(s2, u); }
 __device__ __forceinline__ us2 as_us2(uint32_t u) { return __builtin_bit_cast(us2, u); }
-
-[[maybe_unused]] __device__ __forceinline__ s2 key2(uint32_t u) {
-    s2 h = __builtin_bit_cast(s2, u);
-    return h ^ ((h >> (s2)15) & (s2)0x7FFF);
-}
-
-__device__ __forceinline__ float key_to_f32(int key16) {
-    // key16: sign-extended int16 key; the same involution maps it back to bf16 bits
-    uint32_t h = (uint32_t)(key16 ^ ((key16 >> 15) & 0x7FFF)) & 0xFFFFu;
-    return __uint_as_float(h << 16);
-}
 
 // RN_bf16 of an fp32 value, returned as fp32: v_cvt_pk_bf16_f32 dst, 0, a puts
 // bf16(a) in the high half and zero in the low half — which is bf16(a) as an fp32.
@@ -130,20 +115,92 @@ __device__ __forceinline__ float recip_bf16(float s) {
     return __builtin_fmaf(r0, e, r0);
 }
 
-struct GroupParams {
-    float r;   // RN_f32(1 / s); 0 or NaN <=> s not finite ("special" group)
-    float z;   // zero point (integral float; NaN only in special groups)
-    float s;   // scale (bf16 value)
+// ---- input formats ----------------------------------------------------------------
+// Both are 16-bit sign-magnitude floats, so the raw-bits min/max below works for both.
+// They differ in decoding, NaN thresholds, the rounding applied after every op (torch
+// computes a bf16/fp16 op in fp32 and rounds to the dtype, awq.py's per-op semantics) and
+// in how x / s is formed exactly.
+struct FmtBF16 {
+    static constexpr int kNanS = 0x7F80, kNanU = 0xFF80;   // bits beyond +inf / -inf
+    __device__ static float dec(uint32_t h) { return __uint_as_float(h << 16); }
+    __device__ static float lo(uint32_t w) { return __uint_as_float(w << 16); }
+    __device__ static float hi(uint32_t w) { return __uint_as_float(w & 0xFFFF0000u); }
+    __device__ static float rn(float a) { return rn_bf16(a); }
+    __device__ static float as_fmt(float z) { return z; }
+    // RN(x / s) for a finite s: RN_bf16(x * RN_f32(1/s)) is exact (oracle/verify_recip.c)
+    __device__ static float quot(float x, float s, float r) {
+        (void)s;
+        return rn_bf16(x * r);
+    }
+    // awq.py:202 before the clamp: RN(RN(mx - mn) / QR); / QR == * RN(1/QR), same identity
+    __device__ static float scale(float d, float qr) { return rn_bf16(rn_bf16(d) * (1.0f / qr)); }
+    __device__ static float lo_clamp() { return __uint_as_float(0x2EDC0000u); }   // RN_bf16(1e-10)
+    __device__ static float recip(float s) { return recip_bf16(s); }
+    // awq.py:210 RN(mn / s) for the zero point, any s (r = 0 for s = inf, NaN for NaN)
+    __device__ static float quot_any(float x, float s, float r) { return quot(x, s, r); }
+    // the per-element fast path needs a finite scale (s >= 1e-10 always)
+    __device__ static bool fast(float r) { return r > 0.0f; }
 };
 
-// awq.py:192-211 on one group, from the row-reduced keys.  QR = qmax - qmin.
-template <int BITS, bool SYM>
-__device__ __forceinline__ GroupParams group_params(int mxk, int mnk) {
+// An f32 value the optimizer cannot see through: keeps `RN_f16(a / b)` an f32 IEEE division
+// followed by one v_cvt_f16_f32, instead of being narrowed to an f16 division (whose
+// rcp-based lowering we do not rely on for exactness).
+__device__ __forceinline__ float opaque(float a) {
+    asm volatile("" : "+v"(a));
+    return a;
+}
+
+// same for a wave-uniform constant kept in an SGPR (usable as a VOP3P operand in place)
+__device__ __forceinline__ float opaque_s(float a) {
+    asm("" : "+s"(a));   // not volatile: one copy per kernel, hoisted
+    return a;
+}
+
+struct FmtF16 {
+    static constexpr int kNanS = 0x7C00, kNanU = 0xFC00;
+    __device__ static float dec(uint32_t h) { return (float)__builtin_bit_cast(_Float16, (uint16_t)h); }
+    __device__ static float lo(uint32_t w) { return dec(w & 0xFFFFu); }
+    __device__ static float hi(uint32_t w) { return dec(w >> 16); }
+    __device__ static float rn(float a) { return (float)(_Float16)a; }   // v_cvt_f16_f32: RNE
+    // z as an fp16 round trip (exact: an integer <= 255): RN(t + z) of two fp16 values is
+    // then narrowed by the compiler to one v_add_f16 (exact: a single RNE fp16 add)
+    __device__ static float as_fmt(float z) { return (float)(_Float16)z; }
+    // RN(x / s) for a positive finite s: Markstein-corrected quotient, exact for all fp16
+    // pairs (oracle/verify_recip.c f16m; the plain x * RN(1/s) misses 2 990 pairs)
+    __device__ static float quot(float x, float s, float r) {
+        // x * r written as fma(x, r, -0) (bitwise the same product, signed zeros included)
+        // so that both uses of x fold the fp16 -> f32 conversion into v_fma_mix_f32
+        const float q0 = __builtin_fmaf(x, r, opaque_s(-0.0f));
+        const float e = __builtin_fmaf(-s, q0, x);
+        // RN_f32 first, as verified: a fused fma -> f16 (v_fma_mixlo_f16) rounds once
+        return rn(opaque(__builtin_fmaf(e, r, q0)));
+    }
+    __device__ static float scale(float d, float qr) { return rn(opaque(rn(d)) / qr); }   // IEEE division
+    __device__ static float lo_clamp() { return 0.0f; }                            // RN_f16(1e-10) = 0
+    __device__ static float recip(float s) { return 1.0f / s; }
+    __device__ static float quot_any(float x, float s, float r) {
+        (void)r;
+        return rn(opaque(x) / s);
+    }
+    // s = 0 (constant group: the fp16 clamp min is 0), inf or NaN -> exact special path
+    __device__ static bool fast(float r) { return r > 0.0f && r < __builtin_inff(); }
+};
+
+struct GroupParams {
+    float r;   // RN_f32(1 / s)
+    float z;   // zero point (integral float; NaN only in special groups)
+    float s;   // scale (a value of the input dtype)
+};
+
+// awq.py:192-211 on one group from the raw-bits row reductions: smax = signed-int16 max,
+// umax = unsigned max, umin = unsigned min (only valid when the group is single-signed).
+template <typename F, int BITS, bool SYM>
+__device__ __forceinline__ GroupParams group_params(int smax, int umax, int umin) {
     constexpr float QR = (float)((1 << BITS) - 1);
-    constexpr float INV_QR = 1.0f / QR;               // RN_f32(1/15), RN_f32(1/255)
-    const float LO = __uint_as_float(0x2EDC0000u);    // RN_bf16(1e-10) = 1.0004442e-10
-    const bool nan = (mxk > 0x7F80) || (mnk < -32641);   // keys beyond +inf / -inf
-    float mx = key_to_f32(mxk), mn = key_to_f32(mnk);
+    const int mx_bits = smax >= 0 ? smax : umin;          // all negative: smallest magnitude
+    const int mn_bits = umax >= 0x8000 ? umax : umin;     // none negative: smallest value
+    const bool nan = (smax > F::kNanS) || (umax > F::kNanU);
+    float mx = F::dec((uint32_t)mx_bits), mn = F::dec((uint32_t)mn_bits);
     if (nan) { mx = __builtin_nanf(""); mn = mx; }   // torch min/max both propagate NaN
     if (SYM) {                                        // awq.py:196-199
         float a = __builtin_fmaxf(__builtin_fabsf(mn), __builtin_fabsf(mx));
@@ -151,16 +208,15 @@ __device__ __forceinline__ GroupParams group_params(int mxk, int mnk) {
         mn = -a;
         mx = a;
     }
-    // awq.py:202: bf16 subtract, bf16 / (qmax-qmin) (== * RN(1/QR), same identity)
-    float s = rn_bf16(rn_bf16(mx - mn) * INV_QR);
-    if (!__builtin_isnan(s)) s = __builtin_fmaxf(s, LO);   // awq.py:205 clamp(min=1e-10)
+    float s = F::scale(mx - mn, QR);                  // awq.py:202
+    if (!__builtin_isnan(s)) s = __builtin_fmaxf(s, F::lo_clamp());   // awq.py:205
     GroupParams p;
     p.s = s;
-    p.r = recip_bf16(s);
+    p.r = F::recip(s);
     if (SYM) {
         p.z = 0.0f;                                   // awq.py:208
     } else {
-        const float y = rn_bf16(mn * p.r);            // == RN_bf16(mn / s)
+        const float y = F::quot_any(mn, s, p.r);      // RN(mn / s)
         float z = __builtin_rintf(-y);                // awq.py:210-211 (qmin = 0)
         if (!__builtin_isnan(z)) z = __builtin_fminf(__builtin_fmaxf(z, 0.0f), QR);
         p.z = z;
@@ -168,39 +224,25 @@ __device__ __forceinline__ GroupParams group_params(int mxk, int mnk) {
     return p;
 }
 
-// Same from the raw-bits reductions: smax = signed max, umax = unsigned max, umin =
-// unsigned min (only valid when the group is single-signed).
-template <int BITS, bool SYM>
-__device__ __forceinline__ GroupParams group_params_raw(int smax, int umax, int umin) {
-    const int mx_bits = smax >= 0 ? smax : umin;          // all negative: smallest magnitude
-    const int mn_bits = umax >= 0x8000 ? umax : umin;     // none negative: smallest value
-    const bool nan = (smax > 0x7F80) || (umax > 0xFF80);
-    // keys of those bf16 values for group_params (order-preserving int16, sign-extended)
-    const int mxs = (int)(short)mx_bits, mns = (int)(short)mn_bits;
-    int mxk = mxs ^ ((mxs >> 15) & 0x7FFF), mnk = mns ^ ((mns >> 15) & 0x7FFF);
-    if (nan) mxk = 0x7FC0;                                 // any key beyond +inf
-    return group_params<BITS, SYM>(mxk, mnk);
-}
-
-// Quantize the 8 bf16 of one lane (awq.py:245-248) for a group with a finite scale and
-// pack them: 4-bit -> w.x, 8-bit -> (w.x, w.y).  Field value = q - qmin.
-template <int BITS, bool SYM>
-__device__ __forceinline__ u2v quant8_fast(const u4 v, float r, float z) {
+// Quantize the 8 values of one lane (awq.py:245-248) for a group with a positive finite
+// scale and pack them: 4-bit -> w.x, 8-bit -> (w.x, w.y).  Field value = q - qmin.
+template <typename F, int BITS, bool SYM>
+__device__ __forceinline__ u2v quant8_fast(const u4 v, float r, float z, float s) {
     constexpr float QR = (float)((1 << BITS) - 1);
     constexpr float HALF = (float)(1 << (BITS - 1));
     const uint32_t src[4] = {v.x, v.y, v.z, v.w};
+    const float zf = F::as_fmt(z);
     float q[8];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-        const float x0 = __uint_as_float(src[i] << 16), x1 = __uint_as_float(src[i] & 0xFFFF0000u);
-        float t0 = rn_bf16(x0 * r), t1 = rn_bf16(x1 * r);            // RN_bf16(x / s)
+        const float t0 = F::quot(F::lo(src[i]), s, r), t1 = F::quot(F::hi(src[i]), s, r);   // RN(x / s)
         float u0, u1;
         if (SYM) {
             u0 = t0 + HALF;                                          // rint(t)+8 == rint(t+8)
             u1 = t1 + HALF;
         } else {
-            u0 = rn_bf16(t0 + z);                                    // RN_bf16(x/s + z)
-            u1 = rn_bf16(t1 + z);
+            u0 = F::rn(t0 + zf);                                     // RN(x/s + z)
+            u1 = F::rn(t1 + zf);
         }
         q[2 * i] = __builtin_fminf(__builtin_fmaxf(__builtin_rintf(u0), 0.0f), QR);
         q[2 * i + 1] = __builtin_fminf(__builtin_fmaxf(__builtin_rintf(u1), 0.0f), QR);
@@ -226,9 +268,10 @@ __device__ __forceinline__ u2v quant8_fast(const u4 v, float r, float z) {
     return w;
 }
 
-// Same with the reference's NaN/inf semantics (groups whose scale is inf or NaN).
-template <int BITS, bool SYM>
-__device__ __forceinline__ void quant8_special(const u4 v, float r, float z, uint32_t (&nib)[8],
+// Same with the reference's NaN/inf semantics (groups whose scale is 0, inf or NaN), with
+// a true IEEE division per element.
+template <typename F, int BITS, bool SYM>
+__device__ __forceinline__ void quant8_special(const u4 v, float z, float s, uint32_t (&nib)[8],
                                                int32_t (&q)[8]) {
     constexpr int QMIN = SYM ? -(1 << (BITS - 1)) : 0;
     constexpr int QMAX = SYM ? (1 << (BITS - 1)) - 1 : (1 << BITS) - 1;
@@ -236,10 +279,9 @@ __device__ __forceinline__ void quant8_special(const u4 v, float r, float z, uin
     const uint32_t src[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-        uint32_t bits = (i & 1) ? (src[i >> 1] & 0xFFFF0000u) : (src[i >> 1] << 16);
-        float x = __uint_as_float(bits);
-        float t = rn_bf16(x * r);
-        float u = SYM ? t : rn_bf16(t + z);
+        const float x = (i & 1) ? F::hi(src[i >> 1]) : F::lo(src[i >> 1]);
+        const float t = F::rn(opaque(x) / s);
+        const float u = SYM ? t : F::rn(t + z);
         float rr = __builtin_rintf(u);
         int32_t qi;
         if (__builtin_isnan(rr)) {
@@ -339,7 +381,7 @@ __device__ __forceinline__ void load_tile(const uint16_t* wp, uint32_t ng, u4 (&
         v[j] = __builtin_amdgcn_raw_buffer_load_b128(rw, (uint32_t)((4 * j + row) * 256 + ch * 16), 0, AWQ_LOAD_AUX);
 }
 
-template <int BITS, bool SYM>
+template <typename F, int BITS, bool SYM>
 __device__ __forceinline__ void compute_tile(const TileCtx& c, const u4 (&v)[4], uint32_t* zw, uint32_t* qstage) {
     constexpr int QMIN = SYM ? -(1 << (BITS - 1)) : 0;
     constexpr uint32_t C = 32u / BITS;   // groups per qzeros word
@@ -370,15 +412,13 @@ __device__ __forceinline__ void compute_tile(const TileCtx& c, const u4 (&v)[4],
     return;
 #endif
 
-    // ---- 1. group min/max (awq.py:192-193) of the 4 groups this row holds: int16 keys,
-    //         packed max/min over the lane's 8 values, then max and ~min (= max of ~key)
-    //         reduced over the 16-lane row with DPP-fused v_max_i32 ----
-#if AWQ_RAW_MINMAX
-    // Raw bf16 bits, no key transform: the SIGNED int16 max is the float max whenever the
-    // group has a value with the sign bit clear, and the UNSIGNED max is the float min
-    // (most negative) whenever it has one with the sign bit set; NaNs land beyond 0x7F80 /
-    // 0xFF80.  Single-signed groups (rare in weights; LayerNorm gammas) take an extra
-    // unsigned-min reduction in a wave-uniform branch.
+    // ---- 1. group min/max (awq.py:192-193) of the 4 groups this row holds, from the raw
+    //         16-bit patterns: the SIGNED int16 max is the float max whenever the group has
+    //         a value with the sign bit clear, and the UNSIGNED max is the float min (most
+    //         negative) whenever it has one with the sign bit set; NaNs land beyond F::kNanS /
+    //         F::kNanU.  Single-signed groups (rare in weights; LayerNorm gammas) take an
+    //         extra unsigned-min reduction in a wave-uniform branch.  Row reductions: DPP-
+    //         fused v_max_i32 over the 16 lanes of the group ----
     int smx[4], umx[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -413,25 +453,7 @@ __device__ __forceinline__ void compute_tile(const TileCtx& c, const u4 (&v)[4],
 #pragma unroll
     for (int j = 1; j < 4; ++j)
         if (jj == j) { ssel = smx[j]; usel = umx[j]; nsel = umn[j]; }
-    const GroupParams p = group_params_raw<BITS, SYM>(ssel, usel, nsel);
-#else
-    int kmax[4], knmin[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        s2 k0 = key2(v[j].x), k1 = key2(v[j].y), k2 = key2(v[j].z), k3 = key2(v[j].w);
-        s2 mx = __builtin_elementwise_max(__builtin_elementwise_max(k0, k1), __builtin_elementwise_max(k2, k3));
-        s2 mn = __builtin_elementwise_min(__builtin_elementwise_min(k0, k1), __builtin_elementwise_min(k2, k3));
-        kmax[j] = row_max16<0>(max((int)mx.x, (int)mx.y));
-        knmin[j] = row_max16<0>(~min((int)mn.x, (int)mn.y));
-    }
-    // ---- 2. scale / zero point: lane (row, ch) computes group 4*(ch&3) + row ----
-    const int jj = ch & 3;
-    int mxsel = kmax[0], nmnsel = knmin[0];
-#pragma unroll
-    for (int j = 1; j < 4; ++j)
-        if (jj == j) { mxsel = kmax[j]; nmnsel = knmin[j]; }
-    const GroupParams p = group_params<BITS, SYM>(mxsel, ~nmnsel);
-#endif
+    const GroupParams p = group_params<F, BITS, SYM>(ssel, usel, nsel);
     const uint32_t my_slot = 4u * (uint32_t)jj + (uint32_t)row;
 
     // ---- 4. quantize + pack the 4 groups of this row ----
@@ -441,12 +463,13 @@ __device__ __forceinline__ void compute_tile(const TileCtx& c, const u4 (&v)[4],
         // this group's r, z from lane (row, j), broadcast just in time (short live ranges)
         const float rj = j == 0 ? row_bcast<0>(p.r) : j == 1 ? row_bcast<1>(p.r) : j == 2 ? row_bcast<2>(p.r) : row_bcast<3>(p.r);
         const float zj = SYM ? 0.0f : (j == 0 ? row_bcast<0>(p.z) : j == 1 ? row_bcast<1>(p.z) : j == 2 ? row_bcast<2>(p.z) : row_bcast<3>(p.z));
-        u2v word = quant8_fast<BITS, SYM>(v[j], rj, zj);
-        const bool special = !(rj > 0.0f);         // s = inf (r = 0) or NaN (r = NaN)
+        const float sj = j == 0 ? row_bcast<0>(p.s) : j == 1 ? row_bcast<1>(p.s) : j == 2 ? row_bcast<2>(p.s) : row_bcast<3>(p.s);
+        u2v word = quant8_fast<F, BITS, SYM>(v[j], rj, zj, sj);
+        const bool special = !F::fast(rj);         // scale 0 / inf / NaN
         int32_t q[8];
         if (__builtin_expect(special, 0)) {
             uint32_t nib[8];
-            quant8_special<BITS, SYM>(v[j], rj, zj, nib, q);
+            quant8_special<F, BITS, SYM>(v[j], zj, sj, nib, q);
             if (BITS == 4) {
                 uint32_t acc = 0;
 #pragma unroll
@@ -591,7 +614,7 @@ __device__ uint64_t* g_trace = nullptr;
 // One wave per tile.  The grid normally covers every tile once (launch_fast); a smaller
 // grid (AWQ_HIP_MAX_BLOCKS, tests) makes each wave walk tiles t, t + nwaves, ... with a
 // tensor cursor.
-template <int BITS, bool SYM>
+template <typename F, int BITS, bool SYM>
 __global__ __launch_bounds__(64 * kWavesPerBlock, AWQ_MIN_WAVES) void awq_fast_kernel(const awq_tensor_desc* __restrict__ descs,
                                                        const int32_t* __restrict__ block_tensor,
                                                        awq_tensor_desc single, int n,
@@ -652,7 +675,7 @@ __global__ __launch_bounds__(64 * kWavesPerBlock, AWQ_MIN_WAVES) void awq_fast_k
             tr2 = __builtin_amdgcn_s_memrealtime();
         }
 #endif
-        compute_tile<BITS, SYM>(make_ctx<BITS>(d, tile), va, zw, qs);
+        compute_tile<F, BITS, SYM>(make_ctx<BITS>(d, tile), va, zw, qs);
     }
 #ifdef AWQ_TRACE
     if (g_trace != nullptr && (threadIdx.x & 63) == 0) {
@@ -681,8 +704,8 @@ __global__ void awq_selftest_recip_kernel(unsigned long long* mismatches) {
 }  // namespace
 
 hipError_t launch_fast(const awq_tensor_desc* descs_dev, const int32_t* block_tensor,
-                       const awq_tensor_desc* single, int n, int64_t total_tiles, int bits, int symmetric,
-                       hipStream_t stream) {
+                       const awq_tensor_desc* single, int n, int64_t total_tiles, int dtype, int bits,
+                       int symmetric, hipStream_t stream) {
     if (total_tiles <= 0) return hipSuccess;
     // one wave per tile (tuning / tests: AWQ_HIP_TILES_PER_WAVE = tiles per wave,
     // AWQ_HIP_MAX_BLOCKS = grid cap; either makes waves walk several tiles)
@@ -703,14 +726,21 @@ hipError_t launch_fast(const awq_tensor_desc* descs_dev, const int32_t* block_te
     // the table describes the one-tile-per-wave grid only
     const int32_t* bt = (tpw == 1 && blocks * per_block >= total_tiles) ? block_tensor : nullptr;
     const dim3 grid((unsigned)blocks), block(64 * kWavesPerBlock);
-#define AWQ_LAUNCH(B, S) \
-    hipLaunchKernelGGL((awq_fast_kernel<B, S>), grid, block, 0, stream, descs_dev, bt, one, n, total_tiles)
-    switch ((bits == 8 ? 2 : 0) + (symmetric ? 1 : 0)) {
-    case 0: AWQ_LAUNCH(4, false); break;
-    case 1: AWQ_LAUNCH(4, true); break;
-    case 2: AWQ_LAUNCH(8, false); break;
-    default: AWQ_LAUNCH(8, true); break;
+#define AWQ_LAUNCH(Fm, B, S) \
+    hipLaunchKernelGGL((awq_fast_kernel<Fm, B, S>), grid, block, 0, stream, descs_dev, bt, one, n, total_tiles)
+#define AWQ_LAUNCH_FMT(Fm)                          \
+    switch ((bits == 8 ? 2 : 0) + (symmetric ? 1 : 0)) { \
+    case 0: AWQ_LAUNCH(Fm, 4, false); break;        \
+    case 1: AWQ_LAUNCH(Fm, 4, true); break;         \
+    case 2: AWQ_LAUNCH(Fm, 8, false); break;        \
+    default: AWQ_LAUNCH(Fm, 8, true); break;        \
     }
+    if (dtype == AWQ_DTYPE_F16) {
+        AWQ_LAUNCH_FMT(FmtF16)
+    } else {
+        AWQ_LAUNCH_FMT(FmtBF16)
+    }
+#undef AWQ_LAUNCH_FMT
 #undef AWQ_LAUNCH
     return hipPeekAtLastError();
 }

@@ -8,7 +8,8 @@
  * reproduces awq.py:245's `tensor / scale` (torch bf16 divide = fp32 divide + RNE)
  * and awq.py:210's `t_min / scale` bit for bit.  Also reports the fp16 analogue
  * (expected to FAIL, which is why fp16 inputs use a true division).
- * Usage: verify_recip [bf16|f16]   -> prints mismatches, exit 0 iff none (bf16). */
+ * Usage: verify_recip [bf16|f16|f16m] -> prints mismatches, exit 0 iff none (bf16, f16m:
+ * the fp16 Markstein-corrected quotient below). */
 #include <math.h>
 #include <stdio.h>
 #include <stdint.h>
@@ -21,7 +22,36 @@ static int finite16(uint16_t h, int bf) {
 static float dec(uint16_t h, int bf) { return bf ? oracle_bf16_to_f32(h) : oracle_f16_to_f32(h); }
 static uint16_t enc(float f, int bf) { return bf ? oracle_f32_to_bf16(f) : oracle_f32_to_f16(f); }
 
+/* fp16 fast path (csrc/awq_fast.hip, Fmt<F16>::div): r = RN_f32(1/s), q0 = RN_f32(x*r),
+ * e = fma(-s, q0, x) (exact residual), q1 = fma(e, r, q0) — must give RN_f16(x / s) for
+ * every finite fp16 x and every positive finite fp16 s (scale clamp min RN_f16(1e-10) = 0,
+ * s = 0 takes the IEEE-division special path).  Zeros compare by value (-0 == +0: the
+ * quantized integer does not depend on the sign of a zero quotient). */
+static int check_f16_markstein(void) {
+    long long mismatches = 0, pairs = 0;
+#pragma omp parallel for reduction(+ : mismatches, pairs) schedule(dynamic, 64)
+    for (int si = 1; si < 0x7C00; ++si) {
+        float s = oracle_f16_to_f32((uint16_t)si);
+        volatile float one = 1.0f;
+        float r = one / s;
+        for (int xi = 0; xi < 65536; ++xi) {
+            uint16_t xh = (uint16_t)xi;
+            if ((xh & 0x7C00u) == 0x7C00u) continue;
+            float x = oracle_f16_to_f32(xh);
+            float q0 = x * r;
+            float e = fmaf(-s, q0, x);
+            float q1 = fmaf(e, r, q0);
+            float a = oracle_f16_to_f32(oracle_f32_to_f16(q1)), b = oracle_f16_to_f32(oracle_f32_to_f16(x / s));
+            pairs++;
+            if (!(a == b)) mismatches++;
+        }
+    }
+    printf("f16 markstein: pairs=%lld mismatches=%lld\n", pairs, mismatches);
+    return mismatches == 0 ? 0 : 1;
+}
+
 int main(int argc, char** argv) {
+    if (argc > 1 && strcmp(argv[1], "f16m") == 0) return check_f16_markstein();
     int bf = !(argc > 1 && strcmp(argv[1], "f16") == 0);
     float lo = dec(enc(1e-10f, bf), bf);
     long long mismatches = 0, pairs = 0;

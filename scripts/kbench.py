@@ -42,6 +42,7 @@ def main():
     ap.add_argument("--bits", type=int, default=4)
     ap.add_argument("--symmetric", action="store_true")
     ap.add_argument("--parity", action="store_true")
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "f16"])
     args = ap.parse_args()
     from awq_quantizer import _hip
     from awq_quantizer.quantization.batch import PackedBatch
@@ -85,7 +86,8 @@ def main():
             inputs = {}
             for i, s in enumerate(shapes):
                 g.manual_seed(r * 1000 + i)
-                inputs[f"t{i}"] = (torch.randn(*s, generator=g, device=dev) * 0.02).to(torch.bfloat16)
+                inputs[f"t{i}"] = (torch.randn(*s, generator=g, device=dev) * 0.02).to(
+                    torch.float16 if args.dtype == "f16" else torch.bfloat16)
             bl.append(PackedBatch(inputs, bits=args.bits, symmetric=args.symmetric, parity=args.parity))
         batches[sname] = bl
     torch.cuda.synchronize()
@@ -122,8 +124,8 @@ def main():
                         s0.record(stream)
                         table = None if blk == "nt" else block_table(lp, lib, bt).data_ptr()
                         rc = lib.awq_quantize_ragged(ctypes.c_void_p(bt.descs_dev.data_ptr()), len(bt.descs),
-                                                     bt.total_tiles, ctypes.c_void_p(table), bt.bits,
-                                                     int(bt.symmetric),
+                                                     bt.total_tiles, ctypes.c_void_p(table),
+                                                     _hip.AWQ_DTYPE[bt.dtype], bt.bits, int(bt.symmetric),
                                                      ctypes.c_void_p(stream.cuda_stream))
                         s1.record(stream)
                         assert rc == 0, lib.awq_last_error()

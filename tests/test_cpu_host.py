@@ -27,7 +27,7 @@ def test_library_exports_every_declared_symbol():
     for s in syms:
         assert hasattr(lib, s), s
     assert set(syms) == set(_hip.SIGNATURES), "python binding out of sync with include/awq_hip.h"
-    assert lib.awq_abi_version() == _hip.ABI_VERSION == 2
+    assert lib.awq_abi_version() == _hip.ABI_VERSION == 3
 
 
 def test_library_is_gfx950_code_object():
@@ -41,7 +41,8 @@ def test_host_helpers_without_gpu():
     lib = _hip.load_library()
     assert lib.awq_ragged_eligible(0, 1024, 4096, 128) == 1
     assert lib.awq_ragged_eligible(0, 1024, 4000, 128) == 0
-    assert lib.awq_ragged_eligible(1, 1024, 4096, 128) == 0
+    assert lib.awq_ragged_eligible(1, 1024, 4096, 128) == 1     # fp16 streams too
+    assert lib.awq_ragged_eligible(2, 1024, 4096, 128) == 0     # fp32 -> generic kernel
     d = [_hip.TensorDesc(4096 * 16, 1024, 4096, 0, 0, 2 * 4096, 0, 0, 0, 0),
          _hip.TensorDesc(4096 * 32, 1, 768, 0, 0, 2 * 8192, 0, 0, 0, 0),
          _hip.TensorDesc(4096 * 48, 50, 768, 0, 0, 2 * 16384, 0, 0, 0, 0)]

@@ -55,3 +55,15 @@ def test_exhaustive_bf16_reciprocal_identity():
                          capture_output=True, text=True, timeout=600)
     assert out.returncode == 0, out.stdout + out.stderr
     assert "mismatches=0" in out.stdout
+
+
+def test_f16_markstein_division_exhaustive():
+    """The fp16 fast path's corrected quotient fma(fma(-s, x*r, x), r, x*r) == RN(x/s) after
+    fp16 rounding, over all 2.0e9 (x, positive finite s) pairs."""
+    import os
+    import subprocess
+    subprocess.run(["make", "-s", "-C", os.path.dirname(orc.__file__), "verify_recip"], check=True)
+    out = subprocess.run([os.path.join(os.path.dirname(orc.__file__), "verify_recip"), "f16m"],
+                         capture_output=True, text=True, timeout=600)
+    assert out.returncode == 0, out.stdout + out.stderr
+    assert "mismatches=0" in out.stdout

@@ -8,10 +8,11 @@ dicts + metadata.json, main.py:430-512) and exit codes (0 ok; 1 on load failure,
 tensor quantized, or save failure).
 
 What changes underneath, MI355X-first:
-  * weights are streamed: headers are read first, then one tensor at a time is read
-    from its (memory-mapped) file by a prefetch thread while the GPU quantizes the
-    previous one (the reference loads every file whole, then copies every tensor to
-    the device eagerly, main.py:296-307);
+  * weights are streamed: headers are read first, then batches of tensors are read by
+    reader threads into pinned host memory, copied to the GPU on a copy stream while the
+    previous batch is quantized (one ragged launch per batch), and the results copied
+    back asynchronously (the reference loads every file whole, then copies every tensor
+    to the device eagerly, main.py:296-307, and quantizes tensor by tensor);
   * --multi_gpu / --device all really shards: the tensor list is LPT-partitioned over
     the GPUs (the reference's own partition_tensors, main.py:395-427, which it never
     calls; instead every device re-quantizes every tensor, main.py:596-606), one host
@@ -224,47 +225,143 @@ def _to_cpu(d: Dict[str, torch.Tensor]) -> Dict[str, torch.Tensor]:
     return {k: (v.cpu() if isinstance(v, torch.Tensor) else v) for k, v in d.items()}
 
 
+def _batches(infos: List[TensorInfo], budget: int) -> List[List[TensorInfo]]:
+    """Consecutive runs of tensors (processing order kept) of at most `budget` input bytes
+    (a larger tensor forms a batch of its own)."""
+    out, cur, size = [], [], 0
+    for info in infos:
+        if cur and size + info.nbytes > budget:
+            out.append(cur)
+            cur, size = [], 0
+        cur.append(info)
+        size += info.nbytes
+    if cur:
+        out.append(cur)
+    return out
+
+
+def _pinned_copy(t: torch.Tensor) -> torch.Tensor:
+    """Host copy in page-locked memory (torch's caching host allocator), so the H2D / D2H
+    copies run asynchronously on the copy stream."""
+    p = torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
+    p.copy_(t)
+    return p
+
+
 def quantize_stream(loader, infos: List[TensorInfo], quantizer: AWQQuantizer, device: str, readers: int,
                     lookahead: int, packed: bool, out: Dict, lock: threading.Lock, logger,
-                    memory_efficient: bool = False, keep_on_device: bool = False) -> None:
-    """Quantize `infos` on one device: `readers` threads read tensors from disk up to
-    `lookahead` ahead of the GPU; each tensor is quantized as soon as it is read and its
-    results are copied back to host memory."""
-    if device.startswith("cuda") and torch.cuda.is_available():
-        dev = torch.device(device)
-        torch.cuda.set_device(dev.index if dev.index is not None else torch.cuda.current_device())
-    pending = deque()
-    it = iter(infos)
+                    memory_efficient: bool = False, keep_on_device: bool = False,
+                    batch_bytes: int = 1 << 30) -> None:
+    """Quantize `infos` on one GPU as a pipeline over batches of tensors (<= batch_bytes of
+    input each):
+
+      reader threads: safetensors read -> pinned host copy      (batch k+1 .. k+lookahead)
+      copy stream:    H2D of batch k                            (overlaps batch k-1's kernels)
+      compute stream: one ragged launch per dtype for batch k   (awq_quantize_ragged)
+      copy stream:    D2H of batch k's results into pinned host memory
+
+    The reference instead loads every file whole and copies every tensor to the device
+    eagerly (main.py:296-307), then quantizes tensor by tensor.  Per-tensor failures are
+    logged and skipped (main.py:387-390)."""
+    if not (device.startswith("cuda") and torch.cuda.is_available()):
+        quantizer.compute_device()   # raises HipUnavailable: no CPU path
+    dev = torch.device(device)
+    if dev.index is None:
+        dev = torch.device("cuda", torch.cuda.current_device())
+    torch.cuda.set_device(dev)
+    copy_stream = torch.cuda.Stream(dev)
+    compute = torch.cuda.current_stream(dev)
+    batches = _batches(infos, batch_bytes)
+    depth = max(1, lookahead // max(1, max(len(b) for b in batches) if batches else 1))
 
     def read(info):
-        return loader.read(info)
+        return _pinned_copy(loader.read(info))
+
+    inflight = deque()
+
+    def finish(entry):
+        results, ev, _keep = entry
+        ev.synchronize()
+        with lock:
+            out.update(results)
+        if logger:
+            for name in results:
+                logger.info(f"Successfully quantized tensor: {name} on {device}")
 
     with ThreadPoolExecutor(max_workers=max(1, readers)) as pool:
-        for info in it:
-            pending.append((info, pool.submit(read, info)))
-            if len(pending) >= max(1, lookahead):
-                break
-        while pending:
-            info, fut = pending.popleft()
-            nxt = next(it, None)
-            if nxt is not None:
-                pending.append((nxt, pool.submit(read, nxt)))
-            try:
-                t = fut.result()
-                if logger:
-                    logger.info(f"Quantizing tensor: {info.name} on {device}")
-                res = quantizer.quantize_packed(t) if packed else quantizer.quantize(t)
-                if not keep_on_device:
-                    res = _to_cpu(res)
+        futs = {}
+
+        def submit(k):
+            if k < len(batches) and k not in futs:
+                futs[k] = [(info, pool.submit(read, info)) for info in batches[k]]
+
+        for k in range(min(len(batches), depth + 1)):
+            submit(k)
+        for k in range(len(batches)):
+            submit(k + depth)
+            host = {}
+            for info, fut in futs.pop(k):
+                try:
+                    host[info.name] = fut.result()
+                except Exception as e:  # noqa: BLE001
+                    if logger:
+                        logger.error(f"Failed to quantize tensor {info.name} on {device}: {e}")
+            if not host:
+                continue
+            if logger:
+                for name in host:
+                    logger.info(f"Quantizing tensor: {name} on {device}")
+            with torch.cuda.stream(copy_stream):
+                dev_in = {n: t.to(dev, non_blocking=True) for n, t in host.items()}
+                ev_in = torch.cuda.Event()
+                ev_in.record(copy_stream)
+            compute.wait_event(ev_in)
+            with torch.cuda.stream(compute):
+                res = quantizer.quantize_model_device(dev_in, packed=packed)
+                ev_k = torch.cuda.Event()
+                ev_k.record(compute)
+            for name in host:
+                if name not in res and logger:
+                    logger.error(f"Failed to quantize tensor {name} on {device}")
+            if keep_on_device:
+                ev_k.synchronize()
                 with lock:
-                    out[info.name] = res
-                if logger:
-                    logger.info(f"Successfully quantized tensor: {info.name} on {device}")
-            except Exception as e:  # reference: log and continue (main.py:387-390)
-                if logger:
-                    logger.error(f"Failed to quantize tensor {info.name} on {device}: {e}")
-            if memory_efficient and device.startswith("cuda"):
+                    out.update(res)
+                continue
+            copy_stream.wait_event(ev_k)
+            with torch.cuda.stream(copy_stream):
+                host_res = {}
+                for name, r in res.items():
+                    hr = {}
+                    for f, v in r.items():
+                        if isinstance(v, torch.Tensor) and v.is_cuda:
+                            h = torch.empty(v.shape, dtype=v.dtype, pin_memory=True)
+                            h.copy_(v, non_blocking=True)
+                            hr[f] = h
+                        else:
+                            hr[f] = v
+                    host_res[name] = hr
+                ev_out = torch.cuda.Event()
+                ev_out.record(copy_stream)
+            # inputs and device results stay referenced until their copies are done
+            inflight.append((host_res, ev_out, (host, dev_in, res)))
+            while len(inflight) > 1:
+                finish(inflight.popleft())
+            if memory_efficient:
                 torch.cuda.empty_cache()
+        while inflight:
+            finish(inflight.popleft())
+
+
+def _device_worker(*args) -> None:
+    """Thread body of one device: a failure of the whole device (no GPU, no library) is
+    logged; its tensors then count as not quantized."""
+    logger, device = args[9], args[3]
+    try:
+        quantize_stream(*args)
+    except Exception as e:  # noqa: BLE001
+        if logger:
+            logger.error(f"Quantization on {device} failed: {e}")
 
 
 def main(argv: Optional[List[str]] = None) -> int:
@@ -327,9 +424,9 @@ def main(argv: Optional[List[str]] = None) -> int:
         threads = []
         for d, part in zip(devices, parts):
             logger.info(f"Processing {len(part)} tensors on {d}")
-            th = threading.Thread(target=quantize_stream, args=(loader, part, quantizers[d], d, args.num_workers,
-                                                                lookahead, packed, results, lock, logger,
-                                                                args.memory_efficient))
+            th = threading.Thread(target=_device_worker, args=(loader, part, quantizers[d], d, args.num_workers,
+                                                               lookahead, packed, results, lock, logger,
+                                                               args.memory_efficient))
             th.start()
             threads.append(th)
         for th in threads:

@@ -171,6 +171,10 @@ class AWQQuantizer:
         [rows, groups]; 0-d or [rows] for tensors smaller than one group), zero_points
         (int32, same shape as scales), bits / group_size (int32 0-d), symmetric (bool 0-d).
         """
+        return {k: (v.cpu() if isinstance(v, torch.Tensor) else v) for k, v in self._quantize_device(tensor).items()}
+
+    def _quantize_device(self, tensor: torch.Tensor) -> Dict[str, torch.Tensor]:
+        """quantize() with the result tensors left on the device."""
         self._check_input(tensor)
         rows, K, L, small = self._layout(tensor)
         self._check_mode()
@@ -186,9 +190,9 @@ class AWQQuantizer:
         elif small == "row":
             scales, zeros = scales.reshape(rows), zeros.reshape(rows)
         return {
-            "tensor_q": tensor_q.reshape(tensor.shape).cpu(),
-            "scales": scales.cpu(),
-            "zero_points": zeros.cpu(),
+            "tensor_q": tensor_q.reshape(tensor.shape),
+            "scales": scales,
+            "zero_points": zeros,
             "bits": torch.tensor(self.bits, dtype=torch.int32),
             "group_size": torch.tensor(self.group_size, dtype=torch.int32),
             "symmetric": torch.tensor(self.symmetric, dtype=torch.bool),
@@ -304,6 +308,45 @@ class AWQQuantizer:
                 out[name] = self.quantize_packed(t)
             except Exception as e:
                 self.logger.error(f"Error quantizing tensor: {name}, error: {e}")
+        return {k: out[k] for k in tensors if k in out}
+
+    def quantize_model_device(self, tensors: Dict[str, torch.Tensor], packed: bool = True
+                              ) -> Dict[str, Dict[str, torch.Tensor]]:
+        """Many tensors at once, results left on the device: packed outputs
+        (quantize_model_packed) or the reference's result dicts (quantize(), unpacked int32),
+        the latter also from one ragged launch per dtype for the streaming-eligible tensors.
+        Failures are logged and skipped (awq.py:453-455)."""
+        if packed:
+            return self.quantize_model_packed(tensors)
+        from .batch import PackedBatch
+        out, eligible = {}, {}
+        for name, t in tensors.items():
+            try:
+                self._check_input(t)
+                self._check_mode()
+            except Exception as e:  # reference semantics: skip and continue
+                self.logger.error(f"Error quantizing tensor: {name}, error: {e}")
+                continue
+            rows = 1 if t.dim() <= 1 else t.shape[0]
+            if (not self.search_candidates and t.numel() >= self.group_size
+                    and _hip.ragged_eligible(t.dtype, rows, t.numel() // rows, self.group_size)):
+                eligible[name] = t
+            else:
+                try:
+                    out[name] = self._quantize_device(t)
+                except Exception as e:
+                    self.logger.error(f"Error quantizing tensor: {name}, error: {e}")
+        if eligible:
+            dev = self.compute_device()
+            for dt in (torch.bfloat16, torch.float16):
+                part = {k: v.detach().to(dev).contiguous() for k, v in eligible.items() if v.dtype == dt}
+                if part:
+                    batch = PackedBatch(part, bits=self.bits, symmetric=self.symmetric, parity=True, packed=False)
+                    batch.run()
+                    for name, r in batch.results().items():
+                        out[name] = {"tensor_q": r["tensor_q"], "scales": r["scales"],
+                                     "zero_points": r["zero_points"], "bits": r["bits"],
+                                     "group_size": r["group_size"], "symmetric": r["symmetric"]}
         return {k: out[k] for k in tensors if k in out}
 
     def dequantize_packed(self, packed: Dict[str, torch.Tensor], dtype: torch.dtype = torch.float32) -> torch.Tensor:

@@ -64,6 +64,8 @@ def max_over_ranks(value: float, device: torch.device) -> float:
     """Max of a per-rank float over all ranks (the bench's wall time)."""
     if not (dist.is_initialized() and dist.get_world_size() > 1):
         return float(value)
+    if dist.get_backend() != "nccl":
+        device = torch.device("cpu")
     t = torch.tensor([float(value)], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())

@@ -151,8 +151,10 @@ def main():
     from awq_quantizer import _hip
     from awq_quantizer import distributed as D
     from awq_quantizer.quantization.batch import PackedBatch
-    rank, local, world = D.init("nccl")          # RCCL; one process per GPU (torchrun)
-    dev = torch.device("cuda", local)
+    # RCCL, one process per GPU (torchrun).  AWQ_DIST_BACKEND=gloo only to rehearse the
+    # N>1 path with several ranks on one GPU (RCCL refuses two ranks on one device).
+    rank, local, world = D.init(os.environ.get("AWQ_DIST_BACKEND", "nccl"))
+    dev = torch.device("cuda", local % max(1, torch.cuda.device_count()))
     torch.cuda.set_device(dev)
     _hip.require_device(dev)
 

@@ -42,6 +42,7 @@ SIGNATURES = {
     "awq_quantize_search": (_I32, [_P, _I32, _I64, _I64, _I64, _I32, _I32, _I32, _I32, _P, _P, _P, _P, _P, _P]),
     "awq_ragged_eligible": (_I32, [_I32, _I64, _I64, _I64]),
     "awq_plan_ragged": (_I64, [ctypes.POINTER(TensorDesc), _I32, _I32]),
+    "awq_export_autoawq_gemm": (_I32, [_P, _P, _P, _I64, _I64, _I64, _I32, _P, _P, _P, _P]),
     "awq_plan_block_tensor": (_I64, [ctypes.POINTER(TensorDesc), _I32, _I64, _P, _I64]),
     "awq_quantize_ragged": (_I32, [_P, _I32, _I64, _P, _I32, _I32, _I32, _P]),
     "awq_dequantize": (_I32, [_P, _P, _P, _I64, _I64, _I64, _P, _P]),
@@ -180,6 +181,14 @@ def quantize_ragged(descs_dev: torch.Tensor, n: int, total_tiles: int, bits: int
     rc = load_library().awq_quantize_ragged(ptr(descs_dev), n, total_tiles, ptr(block_tensor), AWQ_DTYPE[dtype],
                                             bits, int(bool(symmetric)), ctypes.c_void_p(stream))
     check(rc, "awq_quantize_ragged")
+
+
+def export_autoawq_gemm(qweight, qzeros, scales, N: int, K: int, L: int, bits: int, qweight_t, qzeros_t,
+                        scales_t) -> None:
+    rc = load_library().awq_export_autoawq_gemm(ptr(qweight), ptr(qzeros), ptr(scales), N, K, L, bits,
+                                                ptr(qweight_t), ptr(qzeros_t), ptr(scales_t),
+                                                ctypes.c_void_p(stream_ptr(qweight.device)))
+    check(rc, "awq_export_autoawq_gemm")
 
 
 def dequantize(tensor_q, scales, zeros, rows, K, L, out) -> None:

@@ -77,9 +77,11 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--save_safetensors", action="store_true", help="Save in safetensors format instead of pytorch format")
     p.add_argument("--chunk_size", type=int, default=10, help="Number of tensors to save in each chunk (for large models)")
     # extension (not in the reference)
-    p.add_argument("--output_format", type=str, default="reference", choices=["reference", "packed"],
+    p.add_argument("--output_format", type=str, default="reference", choices=["reference", "packed", "autoawq"],
                    help="reference: int32 tensor_q/zero_points + fp16 scales per tensor (reference layout); "
-                        "packed: int32 qweight/qzeros (bits-packed) + fp16 scales")
+                        "packed: int32 qweight/qzeros (bits-packed) + fp16 scales; "
+                        "autoawq: a 4-bit checkpoint in AutoAWQ's GEMM layout (linear weights quantized, "
+                        "everything else copied) + quant_config.json")
     return p
 
 
@@ -225,6 +227,50 @@ def _to_cpu(d: Dict[str, torch.Tensor]) -> Dict[str, torch.Tensor]:
     return {k: (v.cpu() if isinstance(v, torch.Tensor) else v) for k, v in d.items()}
 
 
+_NOT_LINEAR = ("embed", "lm_head", "norm", "wte", "wpe", "ln_")
+
+
+def is_linear_weight(info: TensorInfo, group_size: int) -> bool:
+    """The tensors an AutoAWQ checkpoint quantizes: 2-D `*.weight` of linear layers (not
+    embeddings, the LM head or norms) whose shape the GEMM layout can hold."""
+    if len(info.shape) != 2 or not info.name.endswith(".weight") or not info.dtype.is_floating_point:
+        return False
+    if any(s in info.name for s in _NOT_LINEAR):
+        return False
+    n, k = info.shape
+    return n % 8 == 0 and k % group_size == 0
+
+
+def save_autoawq(quantized: Dict[str, Dict[str, torch.Tensor]], loader, passthrough: List[TensorInfo],
+                 output_dir: str, args, logger=None) -> None:
+    """model.safetensors with `<layer>.qweight/.qzeros/.scales` for every quantized linear
+    weight and every other tensor copied unchanged, quant_config.json (AutoAWQ) and, when
+    the source has one, config.json with a transformers `quantization_config`."""
+    from safetensors.torch import save_file
+    tensors = {}
+    for name, r in quantized.items():
+        prefix = name[: -len(".weight")]
+        for f in ("qweight", "qzeros", "scales"):
+            tensors[f"{prefix}.{f}"] = r[f].contiguous()
+    for info in passthrough:
+        tensors[info.name] = loader.read(info).contiguous()
+    save_file(tensors, os.path.join(output_dir, "model.safetensors"), metadata={"format": "pt"})
+    qcfg = {"zero_point": not args.symmetric, "q_group_size": args.group_size, "w_bit": 4, "version": "GEMM"}
+    with open(os.path.join(output_dir, "quant_config.json"), "w") as f:
+        json.dump(qcfg, f, indent=2)
+    src = os.path.join(getattr(loader, "model_path", "") or "", "config.json")
+    if os.path.isfile(src):
+        with open(src) as f:
+            cfg = json.load(f)
+        cfg["quantization_config"] = {"quant_method": "awq", "bits": 4, "group_size": args.group_size,
+                                      "zero_point": not args.symmetric, "version": "gemm"}
+        with open(os.path.join(output_dir, "config.json"), "w") as f:
+            json.dump(cfg, f, indent=2)
+    if logger:
+        logger.info(f"Saved AutoAWQ checkpoint: {len(quantized)} quantized linear weights, "
+                    f"{len(passthrough)} tensors copied")
+
+
 def _batches(infos: List[TensorInfo], budget: int) -> List[List[TensorInfo]]:
     """Consecutive runs of tensors (processing order kept) of at most `budget` input bytes
     (a larger tensor forms a batch of its own)."""
@@ -251,7 +297,7 @@ def _pinned_copy(t: torch.Tensor) -> torch.Tensor:
 def quantize_stream(loader, infos: List[TensorInfo], quantizer: AWQQuantizer, device: str, readers: int,
                     lookahead: int, packed: bool, out: Dict, lock: threading.Lock, logger,
                     memory_efficient: bool = False, keep_on_device: bool = False,
-                    batch_bytes: int = 1 << 30) -> None:
+                    batch_bytes: int = 1 << 30, export_autoawq: bool = False) -> None:
     """Quantize `infos` on one GPU as a pipeline over batches of tensors (<= batch_bytes of
     input each):
 
@@ -318,6 +364,8 @@ def quantize_stream(loader, infos: List[TensorInfo], quantizer: AWQQuantizer, de
             compute.wait_event(ev_in)
             with torch.cuda.stream(compute):
                 res = quantizer.quantize_model_device(dev_in, packed=packed)
+                if export_autoawq:
+                    res = {n: quantizer.export_autoawq(r) for n, r in res.items()}
                 ev_k = torch.cuda.Event()
                 ev_k.record(compute)
             for name in host:
@@ -405,10 +453,20 @@ def main(argv: Optional[List[str]] = None) -> int:
         logger.info("Preparing tensors for quantization")
         start = time.time()
         ordered = select_tensors(index, logger)
+        autoawq = args.output_format == "autoawq"
+        passthrough: List[TensorInfo] = []
+        if autoawq:
+            if args.bits != 4:
+                logger.error("--output_format autoawq writes 4-bit checkpoints (AutoAWQ GEMM layout)")
+                return 1
+            linear = {i.name for i in ordered if is_linear_weight(i, args.group_size)}
+            passthrough = [i for i in index if i.name not in linear]
+            ordered = [i for i in ordered if i.name in linear]
+            logger.info(f"AutoAWQ export: {len(ordered)} linear weights quantized, {len(passthrough)} copied")
         from . import distributed as D
         rank, local, world = D.env_world()
         if world > 1:   # torchrun: one process per GPU, LPT shard, RCCL gather to rank 0
-            return _main_distributed(args, loader, ordered, logger, start)
+            return _main_distributed(args, loader, ordered, logger, start, passthrough)
         parts = partition_tensors(ordered, len(devices))
         quantizers = {d: AWQQuantizer(bits=args.bits, group_size=args.group_size, symmetric=args.symmetric,
                                       zero_point=args.zero_point, percentile=args.percentile,
@@ -420,13 +478,13 @@ def main(argv: Optional[List[str]] = None) -> int:
         results: Dict[str, Dict[str, torch.Tensor]] = {}
         lock = threading.Lock()
         lookahead = max(1, args.prefetch_factor * args.batch_size)
-        packed = args.output_format == "packed"
+        packed = args.output_format in ("packed", "autoawq")
         threads = []
         for d, part in zip(devices, parts):
             logger.info(f"Processing {len(part)} tensors on {d}")
             th = threading.Thread(target=_device_worker, args=(loader, part, quantizers[d], d, args.num_workers,
                                                                lookahead, packed, results, lock, logger,
-                                                               args.memory_efficient))
+                                                               args.memory_efficient, False, 1 << 30, autoawq))
             th.start()
             threads.append(th)
         for th in threads:
@@ -439,8 +497,11 @@ def main(argv: Optional[List[str]] = None) -> int:
         logger.info(f"Successfully quantized {len(quantized)} tensors")
         logger.info(f"Saving quantized model to {args.output_dir}")
         try:
-            save_model_in_chunks(quantized, args.output_dir, chunk_size=args.chunk_size,
-                                 use_safetensors=args.save_safetensors, logger=logger)
+            if autoawq:
+                save_autoawq(quantized, loader, passthrough, args.output_dir, args, logger)
+            else:
+                save_model_in_chunks(quantized, args.output_dir, chunk_size=args.chunk_size,
+                                     use_safetensors=args.save_safetensors, logger=logger)
         except Exception as e:  # noqa: BLE001
             logger.error(f"Failed to save quantized model: {e}")
             return 1
@@ -459,7 +520,8 @@ def main(argv: Optional[List[str]] = None) -> int:
 _SCALARS = ("bits", "group_size", "symmetric", "shape")
 
 
-def _main_distributed(args, loader, ordered: List[TensorInfo], logger, start: float) -> int:
+def _main_distributed(args, loader, ordered: List[TensorInfo], logger, start: float,
+                      passthrough: Optional[List[TensorInfo]] = None) -> int:
     """torchrun mode: rank r quantizes the tensors an LPT partition by bytes assigns it
     (identical on every rank, no exchange), keeps its results in HBM, then every result
     is sent to rank 0 in one batched point-to-point round over RCCL (xGMI) and rank 0
@@ -481,9 +543,10 @@ def _main_distributed(args, loader, ordered: List[TensorInfo], logger, start: fl
                      logger_to_file=args.log_file is not None, logger_file_path=args.log_file)
     logger.info(f"rank {rank}/{world}: {len(mine)} of {len(ordered)} tensors on {device}")
     results: Dict[str, Dict[str, torch.Tensor]] = {}
+    autoawq = args.output_format == "autoawq"
     quantize_stream(loader, mine, q, device, args.num_workers, max(1, args.prefetch_factor * args.batch_size),
-                    args.output_format == "packed", results, threading.Lock(), logger, args.memory_efficient,
-                    keep_on_device=True)
+                    args.output_format in ("packed", "autoawq"), results, threading.Lock(), logger,
+                    args.memory_efficient, keep_on_device=True, export_autoawq=autoawq)
     # which tensors succeeded, and the shapes rank 0 must receive (tiny metadata)
     meta = {n: {f: (tuple(t.shape), str(t.dtype)) for f, t in r.items() if f not in _SCALARS}
             for n, r in results.items()}
@@ -505,7 +568,8 @@ def _main_distributed(args, loader, ordered: List[TensorInfo], logger, start: fl
         for info in ordered:
             if info.name in merged:
                 d = _to_cpu(merged[info.name])
-                d.update(scal)
+                if not autoawq:
+                    d.update(scal)
                 if args.output_format == "packed":
                     d["shape"] = torch.tensor(list(info.shape), dtype=torch.int64)
                 quantized[info.name] = d
@@ -515,8 +579,11 @@ def _main_distributed(args, loader, ordered: List[TensorInfo], logger, start: fl
         else:
             logger.info(f"Successfully quantized {len(quantized)} tensors on {world} GPUs")
             try:
-                save_model_in_chunks(quantized, args.output_dir, chunk_size=args.chunk_size,
-                                     use_safetensors=args.save_safetensors, logger=logger)
+                if autoawq:
+                    save_autoawq(quantized, loader, passthrough or [], args.output_dir, args, logger)
+                else:
+                    save_model_in_chunks(quantized, args.output_dir, chunk_size=args.chunk_size,
+                                         use_safetensors=args.save_safetensors, logger=logger)
                 logger.info(f"Quantization complete in {time.time() - start:.2f} seconds")
             except Exception as e:  # noqa: BLE001
                 logger.error(f"Failed to save quantized model: {e}")

@@ -349,6 +349,27 @@ class AWQQuantizer:
                                      "group_size": r["group_size"], "symmetric": r["symmetric"]}
         return {k: out[k] for k in tensors if k in out}
 
+    def export_autoawq(self, packed: Dict[str, torch.Tensor]) -> Dict[str, torch.Tensor]:
+        """A quantize_packed() result of a 2-D [out_features, in_features] weight in the
+        AutoAWQ "GEMM" layout (include/awq_hip.h awq_export_autoawq_gemm): qweight int32
+        [in, out/8], qzeros int32 [in/group_size, out/8], scales fp16 [in/group_size, out],
+        packed along out_features with AWQ_ORDER.  Device tensors; 4-bit only."""
+        shape = tuple(int(v) for v in packed["shape"].tolist())
+        if len(shape) != 2:
+            raise ValueError(f"AutoAWQ GEMM layout is for 2-D linear weights, got shape {shape}")
+        N, K = shape
+        L = int(packed["group_size"].item())
+        bits = int(packed["bits"].item())
+        dev = packed["qweight"].device
+        G = K // L
+        out = {"qweight": torch.empty((K, N // 8), dtype=torch.int32, device=dev),
+               "qzeros": torch.empty((G, N // 8), dtype=torch.int32, device=dev),
+               "scales": torch.empty((G, N), dtype=torch.float16, device=dev)}
+        _hip.export_autoawq_gemm(packed["qweight"].contiguous(), packed["qzeros"].contiguous(),
+                                 packed["scales"].contiguous(), N, K, L, bits, out["qweight"], out["qzeros"],
+                                 out["scales"])
+        return out
+
     def dequantize_packed(self, packed: Dict[str, torch.Tensor], dtype: torch.dtype = torch.float32) -> torch.Tensor:
         """Inverse of quantize_packed with the reference's dequantize arithmetic (fp16 math)."""
         shape = tuple(int(v) for v in packed["shape"].tolist())

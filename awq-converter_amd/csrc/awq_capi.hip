@@ -221,6 +221,20 @@ int awq_pack_rows(const int32_t* v, int64_t rows, int64_t n, int bits, int qmin,
     return hip_status(awq::launch_pack(v, rows, n, bits, qmin, packed, (hipStream_t)stream), "awq pack");
 }
 
+int awq_export_autoawq_gemm(const int32_t* qweight, const int32_t* qzeros, const uint16_t* scales, int64_t N,
+                            int64_t K, int64_t group_size, int bits, int32_t* qweight_t, int32_t* qzeros_t,
+                            uint16_t* scales_t, void* stream) {
+    g_err.clear();
+    if (bits != 4) return fail(AWQ_EUNSUPPORTED, "the AutoAWQ GEMM layout is 4-bit only (bits=%d)", bits);
+    if (group_size <= 0) return fail(AWQ_EINVAL, "Group size must be a positive integer: %lld", (long long)group_size);
+    if (N <= 0 || K <= 0 || N % 8 != 0 || K % 8 != 0 || K % group_size != 0)
+        return fail(AWQ_EINVAL, "AutoAWQ GEMM layout needs out_features %% 8 == 0 and in_features %% group_size == 0 "
+                                "(N=%lld, K=%lld, group_size=%lld)", (long long)N, (long long)K, (long long)group_size);
+    if (!qweight || !qzeros || !scales || !qweight_t || !qzeros_t || !scales_t) return fail(AWQ_EINVAL, "null argument");
+    return hip_status(awq::launch_export_gemm(qweight, qzeros, scales, N, K, group_size, qweight_t, qzeros_t, scales_t,
+                                              (hipStream_t)stream), "awq export kernel");
+}
+
 int awq_selftest(int which, unsigned long long* result, void* stream) {
     g_err.clear();
     if (!result) return fail(AWQ_EINVAL, "null result pointer");

@@ -120,6 +120,16 @@ int64_t awq_plan_block_tensor(const awq_tensor_desc* descs_host, int n, int64_t 
 int awq_quantize_ragged(const awq_tensor_desc* descs_device, int n, int64_t total_tiles,
                         const int32_t* block_tensor_device, int dtype, int bits, int symmetric, void* stream);
 
+/* AutoAWQ "GEMM" layout (the reference has no packed format): from
+ * this library's row-major packed 4-bit results of an [N = out_features, K = in_features]
+ * weight (qweight [N, K/8], qzeros [N, ceil(G/8)], scales fp16 [N, G], G = K / group_size)
+ * to qweight_t int32 [K, N/8], qzeros_t int32 [G, N/8], scales_t fp16 [G, N], packed along
+ * N with AWQ_ORDER {0,2,4,6,1,3,5,7} (nibble i of word c = column 8c + AWQ_ORDER[i]).
+ * bits must be 4; N % 8 == 0; K % group_size == 0. */
+int awq_export_autoawq_gemm(const int32_t* qweight, const int32_t* qzeros, const uint16_t* scales, int64_t N,
+                            int64_t K, int64_t group_size, int bits, int32_t* qweight_t, int32_t* qzeros_t,
+                            uint16_t* scales_t, void* stream);
+
 /* Reference dequantize (awq.py:459-539): out fp32 [rows, K] =
  * fp16( fp16(tensor_q - zeros) * scales ) per element. */
 int awq_dequantize(const int32_t* tensor_q, const uint16_t* scales, const int32_t* zeros,

@@ -160,3 +160,48 @@ def test_main_torchrun_two_ranks_gpu(tmp_path):
         rows = 1 if tensors[name].dim() <= 1 else tensors[name].shape[0]
         assert torch.equal(res["qweight"], orc.pack_rows(ref["tensor_q"].reshape(rows, -1), 4, 0)), name
         assert torch.equal(res["scales"].view(torch.int16), ref["scales"].view(torch.int16)), name
+
+
+def test_linear_selection_for_autoawq():
+    from awq_quantizer.main import is_linear_weight
+    from awq_quantizer.model_loading import TensorInfo
+    mk = lambda n, s, dt=torch.bfloat16: TensorInfo(n, "f", dt, s)
+    assert is_linear_weight(mk("model.layers.0.mlp.fc1.weight", (256, 768)), 128)
+    assert not is_linear_weight(mk("model.embed_tokens.weight", (512, 256)), 128)
+    assert not is_linear_weight(mk("lm_head.weight", (512, 256)), 128)
+    assert not is_linear_weight(mk("model.layers.0.ln.weight", (256,)), 128)
+    assert not is_linear_weight(mk("model.layers.0.x.weight", (250, 256)), 128)      # out % 8
+    assert not is_linear_weight(mk("model.layers.0.x.weight", (256, 200)), 128)      # in % group
+    assert not is_linear_weight(mk("model.layers.0.x.bias", (256, 256)), 128)
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not torch.cuda.is_available(), reason="needs the GPU")
+def test_main_autoawq_output_gpu(tmp_path):
+    from safetensors.torch import load_file
+    from oracle import awq_oracle as orc
+    from awq_quantizer.main import main
+    tensors = _tensors()
+    d = _model_dir(tmp_path, tensors, files=2)
+    with open(os.path.join(d, "config.json"), "w") as f:
+        json.dump({"model_type": "opt", "hidden_size": 256}, f)
+    out = tmp_path / "out"
+    assert main(["--model_id", d, "--output_dir", str(out), "--log_level", "ERROR", "--output_format", "autoawq"]) == 0
+    st = load_file(str(out / "model.safetensors"))
+    for name in ("model.layers.0.mlp.fc1.weight", "model.layers.0.fp16.weight"):
+        prefix = name[: -len(".weight")]
+        ref = orc.quantize(tensors[name], bits=4, group_size=128, symmetric=False)
+        qw, qz, sc = orc.autoawq_pack(ref["tensor_q"].to(torch.int64), ref["zero_points"].to(torch.int64),
+                                      ref["scales"])
+        assert torch.equal(st[prefix + ".qweight"], qw) and torch.equal(st[prefix + ".qzeros"], qz), name
+        assert torch.equal(st[prefix + ".scales"], sc), name
+        assert name not in st
+    for name in ("model.embed.weight", "model.layers.0.mlp.fc1.bias", "model.layers.0.ln.weight",
+                 "model.layers.0.attn.qkv.weight", "model.layers.0.small", "model.layers.0.int"):
+        assert torch.equal(st[name], tensors[name]), name
+    qc = json.load(open(out / "quant_config.json"))
+    assert qc == {"zero_point": True, "q_group_size": 128, "w_bit": 4, "version": "GEMM"}
+    cfg = json.load(open(out / "config.json"))
+    assert cfg["quantization_config"]["quant_method"] == "awq" and cfg["model_type"] == "opt"
+    assert main(["--model_id", d, "--output_dir", str(tmp_path / "o8"), "--log_level", "CRITICAL", "--bits", "8",
+                 "--output_format", "autoawq"]) == 1

@@ -121,14 +121,26 @@ int awq_quantize_search(const void* w, int dtype, int64_t rows, int64_t K, int64
     if (dtype < AWQ_DTYPE_BF16 || dtype > AWQ_DTYPE_F64) return fail(AWQ_EINVAL, "unknown dtype code %d", dtype);
     if (n_grid < 1 || n_candidates < 1 || n_candidates > n_grid)
         return fail(AWQ_EINVAL, "search grid needs 1 <= n_candidates (%d) <= n_grid (%d)", n_candidates, n_grid);
+    if (group_size > 512 && K > 512)   // (the small-tensor path uses group = K < group_size)
+        return fail(AWQ_EUNSUPPORTED, "scale search supports group_size <= 512 (got %lld)", (long long)group_size);
     if (!qweight && !qzeros && !scales && !tensor_q && !zeros) return fail(AWQ_EINVAL, "no output requested");
     if (rows * K == 0) return AWQ_OK;
     if (!w) return fail(AWQ_EINVAL, "null input");
-    if ((qweight && !tensor_q) || (qzeros && !zeros))
-        return fail(AWQ_EINVAL, "packed outputs of the search kernel need the int32 tensor_q/zeros buffers "
-                                "as staging (pass them too)");
     hipStream_t s = (hipStream_t)stream;
     const int qmin = symmetric ? -(1 << (bits - 1)) : 0;
+    if (fast_eligible(dtype, rows, K, group_size) && aligned(w, 16) && (!qweight || aligned(qweight, 8)) &&
+        (!tensor_q || aligned(tensor_q, 16)) && (!zeros || aligned(zeros, 4)) && (!qzeros || aligned(qzeros, 4)) &&
+        (!scales || aligned(scales, 2))) {
+        awq_tensor_desc d{};
+        d.w = w; d.rows = rows; d.K = K; d.qweight = qweight; d.qzeros = qzeros; d.scales = scales;
+        d.tensor_q = tensor_q; d.zeros = zeros; d.tile_begin = 0;
+        d.tile_count = awq::fast_tiles(rows, K, bits);
+        return hip_status(awq::launch_fast(nullptr, nullptr, &d, 1, d.tile_count, dtype, bits, symmetric, s, n_grid,
+                                           n_candidates), "awq fast search kernel");
+    }
+    if ((qweight && !tensor_q) || (qzeros && !zeros))
+        return fail(AWQ_EINVAL, "packed outputs of the generic search kernel need the int32 tensor_q/zeros "
+                                "buffers as staging (pass them too)");
     if (int rc = hip_status(awq::launch_generic(w, dtype, rows, K, group_size, bits, symmetric, tensor_q,
                                                 scales, zeros, s, n_grid, n_candidates), "awq search kernel"))
         return rc;

@@ -127,6 +127,8 @@ struct FmtBF16 {
     __device__ static float hi(uint32_t w) { return __uint_as_float(w & 0xFFFF0000u); }
     __device__ static float rn(float a) { return rn_bf16(a); }
     __device__ static float as_fmt(float z) { return z; }
+    // fp16 value of the scale the reference's dequantize multiplies by (awq.py:411, 459-539)
+    __device__ static float dq_scale(float s) { return (float)(_Float16)s; }
     // RN(x / s) for a finite s: RN_bf16(x * RN_f32(1/s)) is exact (oracle/verify_recip.c)
     __device__ static float quot(float x, float s, float r) {
         (void)s;
@@ -165,6 +167,7 @@ struct FmtF16 {
     // z as an fp16 round trip (exact: an integer <= 255): RN(t + z) of two fp16 values is
     // then narrowed by the compiler to one v_add_f16 (exact: a single RNE fp16 add)
     __device__ static float as_fmt(float z) { return (float)(_Float16)z; }
+    __device__ static float dq_scale(float s) { return s; }   // already an fp16 value
     // RN(x / s) for a positive finite s: Markstein-corrected quotient, exact for all fp16
     // pairs (oracle/verify_recip.c f16m; the plain x * RN(1/s) misses 2 990 pairs)
     __device__ static float quot(float x, float s, float r) {
@@ -192,11 +195,12 @@ struct GroupParams {
     float s;   // scale (a value of the input dtype)
 };
 
-// awq.py:192-211 on one group from the raw-bits row reductions: smax = signed-int16 max,
+// awq.py:192-199 on one group from the raw-bits row reductions: smax = signed-int16 max,
 // umax = unsigned max, umin = unsigned min (only valid when the group is single-signed).
-template <typename F, int BITS, bool SYM>
-__device__ __forceinline__ GroupParams group_params(int smax, int umax, int umin) {
-    constexpr float QR = (float)((1 << BITS) - 1);
+// Returns the (NaN-propagated, symmetric-folded) [mn, mx] the scale is taken from.
+template <typename F, bool SYM>
+__device__ __forceinline__ void group_range(int smax, int umax, int umin, float& mn_out, float& mx_out,
+                                            bool& nan_out) {
     const int mx_bits = smax >= 0 ? smax : umin;          // all negative: smallest magnitude
     const int mn_bits = umax >= 0x8000 ? umax : umin;     // none negative: smallest value
     const bool nan = (smax > F::kNanS) || (umax > F::kNanU);
@@ -208,6 +212,15 @@ __device__ __forceinline__ GroupParams group_params(int smax, int umax, int umin
         mn = -a;
         mx = a;
     }
+    mn_out = mn;
+    mx_out = mx;
+    nan_out = nan;
+}
+
+// awq.py:202-211: scale, reciprocal and zero point from the group's [mn, mx].
+template <typename F, int BITS, bool SYM>
+__device__ __forceinline__ GroupParams params_from_range(float mn, float mx) {
+    constexpr float QR = (float)((1 << BITS) - 1);
     float s = F::scale(mx - mn, QR);                  // awq.py:202
     if (!__builtin_isnan(s)) s = __builtin_fmaxf(s, F::lo_clamp());   // awq.py:205
     GroupParams p;
@@ -381,8 +394,99 @@ __device__ __forceinline__ void load_tile(const uint16_t* wp, uint32_t ng, u4 (&
         v[j] = __builtin_amdgcn_raw_buffer_load_b128(rw, (uint32_t)((4 * j + row) * 256 + ch * 16), 0, AWQ_LOAD_AUX);
 }
 
+// sum over the 16 lanes of a row, pairwise over adjacent lanes (xor 1, xor 2, then the
+// half-row and row mirrors pair adjacent blocks): every lane ends with the same value, the
+// tree include/awq_hip.h (awq_quantize_search) defines for the clip-search error
+template <int CTRL>
+__device__ __forceinline__ float dpp_add(float v) {
+    return v + __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), CTRL, 0xF, 0xF, true));
+}
+__device__ __forceinline__ float row_sum16(float v) {
+    v = dpp_add<0xB1>(v);    // quad_perm [1,0,3,2]
+    v = dpp_add<0x4E>(v);    // quad_perm [2,3,0,1]
+    v = dpp_add<0x141>(v);   // row_half_mirror
+    return dpp_add<0x140>(v);   // row_mirror
+}
+
+// Squared error of this lane's 8-element chunk of a group for one candidate (r, z, s) —
+// quantize (awq.py:245-248), dequantize the reference's way (fp16(fp16(q - z) * fp16(s)),
+// awq.py:459-539), (x - dq)^2 summed in element order.  `special`: the candidate's scale
+// is 0 / inf / NaN (exact division, NaN-propagating clamp).
 template <typename F, int BITS, bool SYM>
-__device__ __forceinline__ void compute_tile(const TileCtx& c, const u4 (&v)[4], uint32_t* zw, uint32_t* qstage) {
+__device__ __forceinline__ float chunk_err(const u4 v, float r, float z, float s, float sh, bool special) {
+    constexpr float QMIN = SYM ? -(float)(1 << (BITS - 1)) : 0.0f;
+    constexpr float QMAX = SYM ? (float)((1 << (BITS - 1)) - 1) : (float)((1 << BITS) - 1);
+    const uint32_t src[4] = {v.x, v.y, v.z, v.w};
+    const float zf = F::as_fmt(z);
+    float acc = 0.0f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const float x = (i & 1) ? F::hi(src[i >> 1]) : F::lo(src[i >> 1]);
+        float q;
+        if (__builtin_expect(special, 0)) {
+            const float t = F::rn(opaque(x) / s);
+            const float rr = __builtin_rintf(SYM ? t : F::rn(t + zf));
+            q = __builtin_isnan(rr) ? rr : __builtin_fminf(__builtin_fmaxf(rr, QMIN), QMAX);
+        } else {
+            const float t = F::quot(x, s, r);
+            q = __builtin_fminf(__builtin_fmaxf(__builtin_rintf(SYM ? t : F::rn(t + zf)), QMIN), QMAX);
+        }
+        const float dq = (float)(_Float16)((q - zf) * sh);
+        const float d = x - dq;
+        acc = acc + d * d;
+    }
+    return acc;
+}
+
+// Opt-in clip search (include/awq_hip.h awq_quantize_search) inside the streaming kernel:
+// candidates alpha_i = (n_grid - i) / n_grid shrink [mn, mx]; lane (row, ch) evaluates the
+// candidate's parameters for its parameter group 4(ch&3) + row, the 16 lanes of the row
+// score each of the row's 4 groups (8 elements per lane, row_sum16), and the smallest
+// error (ties: the earlier candidate; NaN never wins) picks the group's final [mn, mx].
+// RN(v * alpha) as torch evaluates it (fp32 product, then one rounding to the dtype); the
+// barrier stops the fp16 product from becoming a single-rounding v_mad_mixlo_f16
+template <typename F>
+__device__ __forceinline__ float shrink(float v, float al) {
+    return F::rn(opaque(v * al));
+}
+
+template <typename F, int BITS, bool SYM>
+__device__ __forceinline__ void search_range(const u4 (&v)[4], float& gmn, float& gmx, bool gnan, int n_grid,
+                                          int n_cand) {
+    const int jj = threadIdx.x & 3;
+    float best = __builtin_inff();
+    int bi = 0;
+    for (int i = 0; i < n_cand; ++i) {
+        const float al = (float)(n_grid - i) / (float)n_grid;
+        const GroupParams cp = params_from_range<F, BITS, SYM>(shrink<F>(gmn, al), shrink<F>(gmx, al));
+        const float csh = F::dq_scale(cp.s);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const float rj = j == 0 ? row_bcast<0>(cp.r) : j == 1 ? row_bcast<1>(cp.r) : j == 2 ? row_bcast<2>(cp.r) : row_bcast<3>(cp.r);
+            const float zj = SYM ? 0.0f : (j == 0 ? row_bcast<0>(cp.z) : j == 1 ? row_bcast<1>(cp.z) : j == 2 ? row_bcast<2>(cp.z) : row_bcast<3>(cp.z));
+            const float sj = j == 0 ? row_bcast<0>(cp.s) : j == 1 ? row_bcast<1>(cp.s) : j == 2 ? row_bcast<2>(cp.s) : row_bcast<3>(cp.s);
+            const float hj = j == 0 ? row_bcast<0>(csh) : j == 1 ? row_bcast<1>(csh) : j == 2 ? row_bcast<2>(csh) : row_bcast<3>(csh);
+            const bool special = !F::fast(rj);
+            float e;
+            if (__builtin_expect(__ballot(special) != 0, 0)) e = chunk_err<F, BITS, SYM>(v[j], rj, zj, sj, hj, special);
+            else e = chunk_err<F, BITS, SYM>(v[j], rj, zj, sj, hj, false);
+            e = row_sum16(e);
+            if (j == jj && e < best) {
+                best = e;
+                bi = i;
+            }
+        }
+    }
+    if (!gnan && bi != 0) {
+        const float al = (float)(n_grid - bi) / (float)n_grid;
+        gmn = shrink<F>(gmn, al);
+        gmx = shrink<F>(gmx, al);
+    }
+}
+
+template <typename F, int BITS, bool SYM, bool SEARCH>
+__device__ __forceinline__ void compute_tile(const TileCtx& c, const u4 (&v)[4], uint32_t* zw, uint32_t* qstage,
+                                             int n_grid, int n_cand) {
     constexpr int QMIN = SYM ? -(1 << (BITS - 1)) : 0;
     constexpr uint32_t C = 32u / BITS;   // groups per qzeros word
     const int lane = threadIdx.x & 63;
@@ -453,7 +557,11 @@ __device__ __forceinline__ void compute_tile(const TileCtx& c, const u4 (&v)[4],
 #pragma unroll
     for (int j = 1; j < 4; ++j)
         if (jj == j) { ssel = smx[j]; usel = umx[j]; nsel = umn[j]; }
-    const GroupParams p = group_params<F, BITS, SYM>(ssel, usel, nsel);
+    float gmn, gmx;
+    bool gnan;
+    group_range<F, SYM>(ssel, usel, nsel, gmn, gmx, gnan);
+    if (SEARCH && n_cand > 1) search_range<F, BITS, SYM>(v, gmn, gmx, gnan, n_grid, n_cand);
+    const GroupParams p = params_from_range<F, BITS, SYM>(gmn, gmx);
     const uint32_t my_slot = 4u * (uint32_t)jj + (uint32_t)row;
 
     // ---- 4. quantize + pack the 4 groups of this row ----
@@ -614,11 +722,10 @@ __device__ uint64_t* g_trace = nullptr;
 // One wave per tile.  The grid normally covers every tile once (launch_fast); a smaller
 // grid (AWQ_HIP_MAX_BLOCKS, tests) makes each wave walk tiles t, t + nwaves, ... with a
 // tensor cursor.
-template <typename F, int BITS, bool SYM>
-__global__ __launch_bounds__(64 * kWavesPerBlock, AWQ_MIN_WAVES) void awq_fast_kernel(const awq_tensor_desc* __restrict__ descs,
-                                                       const int32_t* __restrict__ block_tensor,
-                                                       awq_tensor_desc single, int n,
-                                                       int64_t total_tiles) {
+template <typename F, int BITS, bool SYM, bool SEARCH>
+__global__ __launch_bounds__(64 * kWavesPerBlock, SEARCH ? 4 : AWQ_MIN_WAVES) void awq_fast_kernel(
+    const awq_tensor_desc* __restrict__ descs, const int32_t* __restrict__ block_tensor, awq_tensor_desc single,
+    int n, int64_t total_tiles, int n_grid, int n_cand) {
     __shared__ uint32_t zwords[kWavesPerBlock][kSlots];
 #if AWQ_WIDE_STORE
     __shared__ __attribute__((aligned(16))) uint32_t qstage_all[kWavesPerBlock][BITS == 4 ? 256 : 512];
@@ -675,7 +782,7 @@ __global__ __launch_bounds__(64 * kWavesPerBlock, AWQ_MIN_WAVES) void awq_fast_k
             tr2 = __builtin_amdgcn_s_memrealtime();
         }
 #endif
-        compute_tile<F, BITS, SYM>(make_ctx<BITS>(d, tile), va, zw, qs);
+        compute_tile<F, BITS, SYM, SEARCH>(make_ctx<BITS>(d, tile), va, zw, qs, n_grid, n_cand);
     }
 #ifdef AWQ_TRACE
     if (g_trace != nullptr && (threadIdx.x & 63) == 0) {
@@ -705,7 +812,7 @@ __global__ void awq_selftest_recip_kernel(unsigned long long* mismatches) {
 
 hipError_t launch_fast(const awq_tensor_desc* descs_dev, const int32_t* block_tensor,
                        const awq_tensor_desc* single, int n, int64_t total_tiles, int dtype, int bits,
-                       int symmetric, hipStream_t stream) {
+                       int symmetric, hipStream_t stream, int n_grid, int n_cand) {
     if (total_tiles <= 0) return hipSuccess;
     // one wave per tile (tuning / tests: AWQ_HIP_TILES_PER_WAVE = tiles per wave,
     // AWQ_HIP_MAX_BLOCKS = grid cap; either makes waves walk several tiles)
@@ -726,8 +833,15 @@ hipError_t launch_fast(const awq_tensor_desc* descs_dev, const int32_t* block_te
     // the table describes the one-tile-per-wave grid only
     const int32_t* bt = (tpw == 1 && blocks * per_block >= total_tiles) ? block_tensor : nullptr;
     const dim3 grid((unsigned)blocks), block(64 * kWavesPerBlock);
-#define AWQ_LAUNCH(Fm, B, S) \
-    hipLaunchKernelGGL((awq_fast_kernel<Fm, B, S>), grid, block, 0, stream, descs_dev, bt, one, n, total_tiles)
+#define AWQ_LAUNCH(Fm, B, S)                                                                               \
+    do {                                                                                                   \
+        if (n_cand > 1)                                                                                    \
+            hipLaunchKernelGGL((awq_fast_kernel<Fm, B, S, true>), grid, block, 0, stream, descs_dev, bt, one, n, \
+                               total_tiles, n_grid, n_cand);                                               \
+        else                                                                                               \
+            hipLaunchKernelGGL((awq_fast_kernel<Fm, B, S, false>), grid, block, 0, stream, descs_dev, bt, one, \
+                               n, total_tiles, 1, 0);                                                      \
+    } while (0)
 #define AWQ_LAUNCH_FMT(Fm)                          \
     switch ((bits == 8 ? 2 : 0) + (symmetric ? 1 : 0)) { \
     case 0: AWQ_LAUNCH(Fm, 4, false); break;        \

@@ -114,10 +114,12 @@ template <typename C> __device__ __forceinline__ int32_t to_i32(C v) {         /
 }
 
 template <typename C> __device__ __forceinline__ C wave_sum(C v) {
-    // xor butterfly: lane l and lane l^o add the same two values, so every lane ends with
-    // the same, fixed-order tree sum (oracle_quantize_search restates this tree exactly)
+    // xor butterfly with growing offsets = the pairwise tree over adjacent lanes: lanes l
+    // and l^o add the same two values, so every lane ends with the same sum
+    // (oracle_quantize_search restates this tree; the streaming kernel's 16-lane DPP
+    // reduction is the same tree's first four levels)
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = v + __shfl_xor(v, o, 64);
+    for (int o = 1; o < 64; o <<= 1) v = v + __shfl_xor(v, o, 64);
     return v;
 }
 
@@ -160,7 +162,8 @@ __device__ __forceinline__ typename Traits<DT>::C quant1(typename Traits<DT>::C 
 // the RTN parameters are taken, the group's [min, max] is shrunk by alpha_i = (n_grid-i)/n_grid,
 // i < n_cand, and the candidate whose dequantized group (the reference's dequantize:
 // fp16(fp16(q - z) * fp16(s)), awq.py:459-539) has the smallest squared error wins; ties and
-// NaN/inf groups keep i = 0, i.e. exactly the RTN result.
+// NaN/inf groups keep i = 0, i.e. exactly the RTN result.  Group size <= 512 (one 8-element
+// chunk per lane).
 template <int DT, bool SEARCH>
 __global__ __launch_bounds__(256) void awq_generic_kernel(const void* __restrict__ wv, int64_t rows,
                                                           int64_t K, int64_t L, int qmin, int qmax,
@@ -208,8 +211,11 @@ __global__ __launch_bounds__(256) void awq_generic_kernel(const void* __restrict
                 C cs, cz;
                 group_params<DT>(T::rn(mn * al), T::rn(mx * al), 0, qmin, qmax, sym, cs, cz);
                 const float sh = sw_f16_to_f32(canon_f16((float)cs));
+                // canonical error sum (include/awq_hip.h): lane l sums chunk l = elements
+                // 8l .. 8l+7 of the group in order, then the pairwise tree over the lanes
                 C acc = (C)0;
-                for (int64_t k = k0 + lane; k < k1; k += 64) {
+                const int64_t c0 = k0 + 8 * lane, c1 = (c0 + 8 < k1) ? c0 + 8 : k1;
+                for (int64_t k = c0; k < c1; ++k) {
                     const C v = T::load(w, base + k);
                     const C q = quant1<DT>(v, cs, cz, qmin, qmax);
                     const float h = sw_f16_to_f32(sw_f32_to_f16((float)(q - cz)));

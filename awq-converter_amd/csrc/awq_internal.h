@@ -76,7 +76,7 @@ __host__ __device__ inline bool fast_shape_ok(int64_t R, int64_t K) {
 // launchers (awq_fast.hip / awq_generic.hip)
 hipError_t launch_fast(const awq_tensor_desc* descs_dev, const int32_t* block_tensor,
                        const awq_tensor_desc* single, int n, int64_t total_tiles, int dtype, int bits,
-                       int symmetric, hipStream_t stream);
+                       int symmetric, hipStream_t stream, int n_grid = 1, int n_cand = 0);
 hipError_t launch_generic(const void* w, int dtype, int64_t rows, int64_t K, int64_t L, int bits,
                           int symmetric, int32_t* tensor_q, uint16_t* scales, int32_t* zeros,
                           hipStream_t stream, int n_grid = 1, int n_cand = 0);

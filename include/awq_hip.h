@@ -91,6 +91,10 @@ int awq_quantize_groups(const void* w, int dtype, int64_t rows, int64_t K, int64
  * (awq.py:202-211), and the candidate with the smallest sum of squared errors between
  * the group and its dequantization (awq.py:459-539 arithmetic) is kept; ties and NaN/inf
  * groups keep i = 0, i.e. the RTN result bit-exactly.  1 <= n_candidates <= n_grid.
+ * The squared error is summed in fp32 (fp64 for fp64 input) in one canonical order, so
+ * every kernel gets the same bits: chunk c = the group's elements 8c .. 8c+7 summed in
+ * order, then a pairwise tree over 64 chunk slots, adjacent pairs first (empty slots = 0):
+ * group_size <= 512.
  * Packed outputs need tensor_q / zeros as staging buffers. */
 int awq_quantize_search(const void* w, int dtype, int64_t rows, int64_t K, int64_t group_size, int bits,
                         int symmetric, int n_grid, int n_candidates, int32_t* qweight, int32_t* qzeros,

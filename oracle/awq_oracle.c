@@ -206,16 +206,18 @@ int oracle_quantize(const void* x, int dtype, int64_t rows, int64_t K, int64_t L
  * type, product rounded to D), takes (s, z) by awq.py:202-211, quantizes every element
  * (awq.py:245-248) and dequantizes it the reference's way (awq.py:459-539:
  * fp16(fp16(q - z) * fp16(s))).  err = sum (x - dq)^2 in the compute type, summed in the
- * HIP kernel's fixed order: lane l (0..63) accumulates elements k0+l, k0+l+64, ... in
- * sequence, then an xor butterfly t[l] = a[l] + a[l^o] for o = 32, 16, .., 1.  Smallest
- * err wins, ties -> smaller i; NaN groups skip the search. */
+ * product's canonical order: chunk l (0..63) = elements k0+8l .. k0+8l+7 accumulated in
+ * sequence, then the pairwise tree over the 64 chunks, adjacent pairs first (written as an
+ * xor butterfly t[l] = a[l] + a[l^o], o = 1, 2, .., 32, which every lane of the GPU's wave
+ * reproduces).
+ * Smallest err wins, ties -> smaller i; NaN groups skip the search.  L <= 512. */
 static double cadd(double a, double b, int f64) { return f64 ? a + b : (double)((float)a + (float)b); }
 static double cmul(double a, double b, int f64) { return f64 ? a * b : (double)((float)a * (float)b); }
 static double csub(double a, double b, int f64) { return f64 ? a - b : (double)((float)a - (float)b); }
 
 static double tree_sum64(double* a, int f64) {
     double t[64];
-    for (int o = 32; o > 0; o >>= 1) {
+    for (int o = 1; o < 64; o <<= 1) {   /* pairwise tree over adjacent chunks */
         for (int l = 0; l < 64; ++l) t[l] = cadd(a[l], a[l ^ o], f64);
         memcpy(a, t, sizeof t);
     }
@@ -227,6 +229,7 @@ int oracle_quantize_search(const void* x, int dtype, int64_t rows, int64_t K, in
                            int32_t* zeros) {
     if (!x || rows < 0 || K < 0 || L <= 0 || (bits != 4 && bits != 8)) return -1;
     if (n_grid < 1 || n_cand < 1 || n_cand > n_grid) return -1;
+    if (L > 512 && K > 512) return -1;   /* one 8-element chunk per slot, 64 slots */
     int qmin = sym ? -(1 << (bits - 1)) : 0;
     int qmax = sym ? (1 << (bits - 1)) - 1 : (1 << bits) - 1;
     int f64 = dtype == AWQ_ORACLE_F64;
@@ -264,7 +267,8 @@ int oracle_quantize_search(const void* x, int dtype, int64_t rows, int64_t K, in
                     double acc[64];
                     for (int l = 0; l < 64; ++l) {
                         acc[l] = 0.0;
-                        for (int64_t k = k0 + l; k < k1; k += 64) {
+                        int64_t c0 = k0 + 8 * l, c1 = c0 + 8 < k1 ? c0 + 8 : k1;
+                        for (int64_t k = c0; k < c1; ++k) {
                             double v = load_elem(x, dtype, r * K + k);
                             double q = op_add(op_div(v, cs, dtype), cz, dtype);
                             q = op_clamp(op_round(q, dtype), qmin, qmax);

@@ -7,6 +7,8 @@ awq.py:66,111-112; SURVEY.md §8a "parity unpinned"): the bar is
   * the search never increases a group's squared dequantization error over RTN,
   * the HIP kernel equals oracle_quantize_search bit-for-bit (GPU tests).
 """
+import ctypes
+
 import pytest
 import torch
 
@@ -89,7 +91,9 @@ def test_cli_accepts_search():
 
 
 # ---------------------------------------------------------------- GPU: kernel vs oracle
-SEARCH_CASES = [(torch.bfloat16, (40, 1024), 128), (torch.bfloat16, (7, 300), 128), (torch.float16, (33, 300), 128),
+SEARCH_CASES = [(torch.bfloat16, (40, 1024), 128), (torch.float16, (32, 1024), 128), (torch.bfloat16, (50, 768), 128),
+                (torch.float16, (77, 768), 128), (torch.bfloat16, (3, 1280), 128), (torch.bfloat16, (768,), 128),
+                (torch.bfloat16, (7, 300), 128), (torch.float16, (33, 300), 128),
                 (torch.float32, (17, 1000), 64), (torch.float64, (5, 777), 100), (torch.bfloat16, (3, 2, 50), 32),
                 (torch.bfloat16, (10, 10), 128), (torch.bfloat16, (60,), 128), (torch.float16, (4, 4096), 256)]
 
@@ -117,6 +121,42 @@ def test_search_gpu_vs_oracle(dtype, shape, gs, sym, bits):
         pk = q.quantize_packed(x)
         assert torch.equal(pk["qweight"].cpu(), orc.pack_rows(ref["tensor_q"], bits, q.qmin))
         assert torch.equal(pk["qzeros"].cpu(), orc.pack_rows(ref["zero_points"], bits, q.qmin))
+
+
+def test_search_group_size_limit():
+    """One 8-element chunk per error slot, 64 slots: group_size <= 512."""
+    from awq_quantizer import _hip
+    lib = _hip.load_library()
+    assert lib.awq_quantize_search(ctypes.c_void_p(16), 0, 4, 2048, 1024, 4, 0, 20, 10, None, None,
+                                   ctypes.c_void_p(16), None, None, None) != 0
+    assert "group_size <= 512" in _hip.last_error()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+def test_search_gpu_fast_path_special_groups(dtype):
+    """The streaming kernel's search on NaN / inf / constant / near-constant groups (fp16:
+    a shrunk candidate of a near-constant group can hit the scale clamp min 0)."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from awq_quantizer.quantization import AWQQuantizer
+    g = torch.Generator().manual_seed(8)
+    x = (torch.randn(32, 1024, generator=g) * 0.05)
+    x[0, 5] = float("nan")
+    x[1, 200] = float("inf")
+    x[2, :128] = 0.25
+    x[3, 128:256] = 0.25
+    x[3, 130] = 0.2502                     # near-constant: shrunk candidates collapse
+    x[4, 256:384] = torch.linspace(-6e-5, 6e-5, 128)
+    x[5, :128] = -3.0
+    x = x.to(dtype)
+    for sym in (False, True):
+        q = AWQQuantizer(bits=4, symmetric=sym, scale_method="search", device="cuda", logger_level="ERROR")
+        ref = orc.quantize(x, bits=4, group_size=128, symmetric=sym, search=(20, 10))
+        res = q.quantize(x)
+        assert torch.equal(res["tensor_q"], ref["tensor_q"])
+        assert torch.equal(res["zero_points"], ref["zero_points"])
+        assert gio.same_bits_nan_eq(res["scales"], ref["scales"])
 
 
 @pytest.mark.gpu

@@ -42,6 +42,7 @@ SIGNATURES = {
     "awq_quantize_search": (_I32, [_P, _I32, _I64, _I64, _I64, _I32, _I32, _I32, _I32, _P, _P, _P, _P, _P, _P]),
     "awq_ragged_eligible": (_I32, [_I32, _I64, _I64, _I64]),
     "awq_plan_ragged": (_I64, [ctypes.POINTER(TensorDesc), _I32, _I32]),
+    "awq_stream_copy": (_I32, [_P, _P, _I64, _P]),
     "awq_export_autoawq_gemm": (_I32, [_P, _P, _P, _I64, _I64, _I64, _I32, _P, _P, _P, _P]),
     "awq_plan_block_tensor": (_I64, [ctypes.POINTER(TensorDesc), _I32, _I64, _P, _I64]),
     "awq_quantize_ragged": (_I32, [_P, _I32, _I64, _P, _I32, _I32, _I32, _P]),
@@ -181,6 +182,11 @@ def quantize_ragged(descs_dev: torch.Tensor, n: int, total_tiles: int, bits: int
     rc = load_library().awq_quantize_ragged(ptr(descs_dev), n, total_tiles, ptr(block_tensor), AWQ_DTYPE[dtype],
                                             bits, int(bool(symmetric)), ctypes.c_void_p(stream))
     check(rc, "awq_quantize_ragged")
+
+
+def stream_copy(src: torch.Tensor, dst: torch.Tensor, stream: int) -> None:
+    rc = load_library().awq_stream_copy(ptr(src), ptr(dst), src.numel() * src.element_size(), ctypes.c_void_p(stream))
+    check(rc, "awq_stream_copy")
 
 
 def export_autoawq_gemm(qweight, qzeros, scales, N: int, K: int, L: int, bits: int, qweight_t, qzeros_t,

@@ -247,6 +247,14 @@ int awq_export_autoawq_gemm(const int32_t* qweight, const int32_t* qzeros, const
                                               (hipStream_t)stream), "awq export kernel");
 }
 
+int awq_stream_copy(const void* src, void* dst, int64_t bytes, void* stream) {
+    g_err.clear();
+    if (bytes < 0 || bytes % 16 != 0) return fail(AWQ_EINVAL, "bytes must be a non-negative multiple of 16");
+    if (bytes > 0 && (!src || !dst || !aligned(src, 16) || !aligned(dst, 16)))
+        return fail(AWQ_EINVAL, "null or misaligned buffer");
+    return hip_status(awq::launch_stream_copy(src, dst, bytes, (hipStream_t)stream), "awq stream copy");
+}
+
 int awq_selftest(int which, unsigned long long* result, void* stream) {
     g_err.clear();
     if (!result) return fail(AWQ_EINVAL, "null result pointer");

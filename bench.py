@@ -86,18 +86,19 @@ def make_set(shapes, seed0, dev):
 
 
 def copy_ceiling(dev, stream, nbytes=1 << 30, iters=10):
-    """Device-to-device copy of `nbytes` (read + write counted) on the bench stream: the
-    measured HBM ceiling SURVEY.md §8(d) asks the kernel's rate to be quoted against."""
+    """HBM copy of `nbytes` (read + write counted) by the library's stream-copy kernel, which
+    has the quantizer's memory structure (one wave per 4 KiB, 16-B nt accesses): the
+    achievable-bandwidth reference SURVEY.md §8(d) asks the kernel to be quoted against."""
+    from awq_quantizer import _hip
     src = torch.empty(nbytes // 4, dtype=torch.int32, device=dev).fill_(1)
     dst = torch.empty_like(src)
-    with torch.cuda.stream(stream):
-        for _ in range(3):
-            dst.copy_(src)
-        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        a.record(stream)
-        for _ in range(iters):
-            dst.copy_(src)
-        b.record(stream)
+    for _ in range(3):
+        _hip.stream_copy(src, dst, stream.cuda_stream)
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record(stream)
+    for _ in range(iters):
+        _hip.stream_copy(src, dst, stream.cuda_stream)
+    b.record(stream)
     torch.cuda.synchronize()
     gbs = 2 * nbytes * iters / (a.elapsed_time(b) / 1e3) / 1e9
     del src, dst

@@ -134,6 +134,11 @@ int awq_export_autoawq_gemm(const int32_t* qweight, const int32_t* qzeros, const
                             int64_t K, int64_t group_size, int bits, int32_t* qweight_t, int32_t* qzeros_t,
                             uint16_t* scales_t, void* stream);
 
+/* Measurement helper: copy `bytes` (multiple of 16, 16-B aligned buffers) with the
+ * quantizer's memory structure (one wave per 4 KiB, 16-B nt loads/stores); bench.py
+ * quotes the kernel against this copy's rate. */
+int awq_stream_copy(const void* src, void* dst, int64_t bytes, void* stream);
+
 /* Reference dequantize (awq.py:459-539): out fp32 [rows, K] =
  * fp16( fp16(tensor_q - zeros) * scales ) per element. */
 int awq_dequantize(const int32_t* tensor_q, const uint16_t* scales, const int32_t* zeros,

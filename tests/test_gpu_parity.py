@@ -254,3 +254,15 @@ def test_selftest_fast_reciprocal_exhaustive():
     """recip_bf16 (v_rcp + Newton) == IEEE 1/s for every bf16 scale value."""
     from awq_quantizer import _hip
     assert _hip.selftest(0, torch.device(DEV, 0)) == 0
+
+
+def test_stream_copy_helper_copies_exactly():
+    """bench.py's copy-ceiling kernel (awq_stream_copy) is a faithful copy, tail included."""
+    from awq_quantizer import _hip
+    dev = torch.device(DEV, 0)
+    for n in (16, 4096, 4096 * 8 * 3 + 48):
+        src = torch.randint(-2 ** 31, 2 ** 31 - 1, (n // 4,), dtype=torch.int32, device=dev)
+        dst = torch.zeros_like(src)
+        _hip.stream_copy(src, dst, torch.cuda.current_stream(dev).cuda_stream)
+        torch.cuda.synchronize()
+        assert torch.equal(src, dst)

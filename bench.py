@@ -72,6 +72,7 @@ def parse():
     ap.add_argument("--cpu-sample-seconds", type=float, default=15.0)
     ap.add_argument("--events", default="span", choices=["step", "span"])
     ap.add_argument("--no-copy-ceiling", action="store_true")
+    ap.add_argument("--no-gather", action="store_true", help="N>1: skip the (untimed) gather-to-rank-0 leg")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     return ap.parse_args()
 
@@ -147,6 +148,35 @@ def cpu_baseline(shapes, budget_s):
     return done_bytes / t_total / 1e9, t_total, done_bytes, parts, threads
 
 
+def gather_leg(batch, rank, world, dev, backend, iters=3):
+    """N>1 only, after the timed region: the CLI's exchange step (distributed.gather_to_rank0,
+    one coalesced message per peer) on every rank's packed outputs of one replica.  Reported
+    beside `value`, never inside it (the gather is a separate line)."""
+    from awq_quantizer import distributed as D
+    comm = dev if backend == "nccl" else torch.device("cpu")
+    fields = ("qweight", "qzeros", "scales")
+    owner, shapes = {}, {}
+    for r in range(world):
+        for n in batch.names:
+            owner[f"{r}/{n}"] = r
+            shapes[f"{r}/{n}"] = {f: (tuple(batch.out[n][f].shape), batch.out[n][f].dtype) for f in fields}
+    local = {f"{rank}/{n}": {f: batch.out[n][f].to(comm) for f in fields} for n in batch.names}
+    per_rank = sum(batch.out[n][f].numel() * batch.out[n][f].element_size() for n in batch.names for f in fields)
+    D.gather_to_rank0(local, owner, shapes, comm)                     # warmup (connects the P2P channels)
+    torch.cuda.synchronize(dev)
+    D.barrier()
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        D.gather_to_rank0(local, owner, shapes, comm)
+    torch.cuda.synchronize(dev)
+    D.barrier()
+    t = D.max_over_ranks((time.perf_counter() - t0) / iters, dev)
+    moved = per_rank * (world - 1)
+    return {"what": "gather of every rank's packed outputs (one replica) to rank 0, one P2P message per peer "
+                    f"({backend}); outside the timed region", "bytes_to_rank0": moved,
+            "ms": round(t * 1e3, 3), "GBs_into_rank0": round(moved / t / 1e9, 2)}
+
+
 def main():
     args = parse()
     from awq_quantizer import _hip
@@ -154,7 +184,8 @@ def main():
     from awq_quantizer.quantization.batch import PackedBatch
     # RCCL, one process per GPU (torchrun).  AWQ_DIST_BACKEND=gloo only to rehearse the
     # N>1 path with several ranks on one GPU (RCCL refuses two ranks on one device).
-    rank, local, world = D.init(os.environ.get("AWQ_DIST_BACKEND", "nccl"))
+    backend = os.environ.get("AWQ_DIST_BACKEND", "nccl")
+    rank, local, world = D.init(backend)
     dev = torch.device("cuda", local % max(1, torch.cuda.device_count()))
     torch.cuda.set_device(dev)
     _hip.require_device(dev)
@@ -204,6 +235,7 @@ def main():
     ceiling = None if args.no_copy_ceiling or rank != 0 else copy_ceiling(dev, stream)
 
     elapsed = D.max_over_ranks(elapsed, dev)
+    gather = gather_leg(batches[0], rank, world, dev, backend) if world > 1 and not args.no_gather else None
 
     if rank != 0:
         if world > 1:
@@ -235,6 +267,8 @@ def main():
                      "algorithmic_bytes_per_launch": algo_bytes,
                      "kernel_avg_us": round(kern_avg_s * 1e6, 2), "timing": f"hip events ({args.events})"},
     }
+    if gather:
+        line["exchange"] = gather
     if ceiling:
         line["roofline"]["copy_ceiling"] = round(ceiling, 1)
         line["roofline"]["frac_of_copy"] = round(achieved / ceiling, 4)

@@ -205,3 +205,29 @@ def test_main_autoawq_output_gpu(tmp_path):
     assert cfg["quantization_config"]["quant_method"] == "awq" and cfg["model_type"] == "opt"
     assert main(["--model_id", d, "--output_dir", str(tmp_path / "o8"), "--log_level", "CRITICAL", "--bits", "8",
                  "--output_format", "autoawq"]) == 1
+
+
+@pytest.mark.gpu
+def test_bench_two_ranks_gpu():
+    """bench.py's N>1 path (max-over-ranks timing, the gather leg) with 2 ranks on the box's
+    one GPU over gloo; the driver runs it over RCCL, one rank per GPU."""
+    import socket
+    import subprocess
+    import sys
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, AWQ_DIST_BACKEND="gloo")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.join(root, "bench.py"), "--gpus", "2",
+           "--steps", "3", "--warmup", "1", "--workload", "c1", "--no-cpu-baseline", "--no-copy-ceiling"]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300, cwd=root)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert line["n_gpus"] == 2 and line["value"] > 0
+    # one peer's packed outputs of the 1024x4096 tensor: qweight 2 MiB + qzeros 16 KiB + scales 64 KiB
+    assert line["exchange"]["bytes_to_rank0"] == 1024 * 512 * 4 + 1024 * 4 * 4 + 1024 * 32 * 2
+    assert line["exchange"]["ms"] > 0

@@ -41,8 +41,8 @@ def _worker(rank, world, port, q):
         r, _, w = D.init("gloo")
         assert (r, w) == (rank, world)
         dev = torch.device("cpu")
-        names = [f"t{i}" for i in range(7)]
-        sizes = [64, 8, 32, 16, 16, 4, 2]
+        names = [f"t{i}" for i in range(8)]
+        sizes = [64, 8, 32, 16, 16, 3, 1, 0]   # odd byte counts: 16-B aligned slots; an empty tensor
         owner = dict(zip(names, D.shard(sizes, world)))
         shapes = {n: {"qweight": ((s, 2), torch.int32), "scales": ((s,), torch.float16)} for n, s in zip(names, sizes)}
         local = {n: {"qweight": torch.full((s, 2), 1000 * i + s, dtype=torch.int32),
@@ -56,6 +56,8 @@ def _worker(rank, world, port, q):
             for i, (n, s) in enumerate(zip(names, sizes)):
                 ok &= bool(torch.equal(merged[n]["qweight"], torch.full((s, 2), 1000 * i + s, dtype=torch.int32)))
                 ok &= bool(torch.equal(merged[n]["scales"], torch.full((s,), float(i), dtype=torch.float16)))
+            import io
+            torch.save(merged, io.BytesIO())   # results own their storage (the CLI saves them)
             q.put(("ok" if ok else "mismatch", sorted(merged)))
         dist.destroy_process_group()
     except Exception as e:  # surface to the parent
@@ -64,11 +66,12 @@ def _worker(rank, world, port, q):
 
 
 @pytest.mark.timeout(180)
-def test_gloo_world2_gather_and_timing():
+@pytest.mark.parametrize("world", [2, 3])
+def test_gloo_gather_and_timing(world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
     res = q.get(timeout=150)

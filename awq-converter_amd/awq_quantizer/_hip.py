@@ -15,7 +15,7 @@ import torch
 
 LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib")
 LIB_PATH = os.path.join(LIB_DIR, "libawq_hip.so")
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 AWQ_DTYPE = {torch.bfloat16: 0, torch.float16: 1, torch.float32: 2, torch.float64: 3}
 
@@ -50,6 +50,13 @@ SIGNATURES = {
     "awq_dequantize_packed": (_I32, [_P, _P, _P, _I64, _I64, _I64, _I32, _I32, _P, _P]),
     "awq_pack_rows": (_I32, [_P, _I64, _I64, _I32, _I32, _P, _P]),
     "awq_selftest": (_I32, [_I32, _P, _P]),
+    "awq_act_stats": (_I32, [_P, _I32, _I64, _I64, _P, _P, _P, _P]),
+    "awq_weight_colsum": (_I32, [_P, _I32, _I64, _I64, _I64, _P, _P, _P]),
+    "awq_column_mean": (_I32, [_P, _I64, _I64, ctypes.c_double, _P, _P]),
+    "awq_act_scale_table": (_I32, [_P, _P, _I64, _I32, _P, _P]),
+    "awq_act_search_losses": (_I32, [_P, _I32, _I64, _I64, _I64, _I32, _I32, _P, _I32, _P, _P, _I64, _P]),
+    "awq_act_search_select": (_I32, [_P, _I32, _I64, _P, _I64, _P, _P, _P, _P, _P]),
+    "awq_apply_input_scale": (_I32, [_P, _I32, _I64, _I64, _P, _P, _P]),
 }
 
 _lib = None
@@ -221,3 +228,90 @@ def selftest(which: int, device: torch.device) -> int:
     out = torch.zeros(1, dtype=torch.int64, device=device)
     check(load_library().awq_selftest(which, ptr(out), ctypes.c_void_p(stream_ptr(device))), "awq_selftest")
     return int(out.item())
+
+
+# ---- activation-aware scale search (include/awq_hip.h awq_act_*) ----
+ACT_ROW_BLOCK = 256      # canonical fp64 column-sum block (rows / tokens)
+ACT_GROUP_BLOCK = 1024   # canonical fp64 loss block (groups)
+ACT_MAX_GRID = 256
+
+
+def _stream(t: torch.Tensor) -> ctypes.c_void_p:
+    return ctypes.c_void_p(stream_ptr(t.device))
+
+
+def act_stats(x: torch.Tensor):
+    """x [tokens, K] on the device -> (x_mean, x_sq) fp32 [K]."""
+    T, K = x.shape
+    work = torch.empty(2 * (-(-T // ACT_ROW_BLOCK)) * K, dtype=torch.float64, device=x.device)
+    xm = torch.empty(K, dtype=torch.float32, device=x.device)
+    xs = torch.empty(K, dtype=torch.float32, device=x.device)
+    check(load_library().awq_act_stats(ptr(x), AWQ_DTYPE[x.dtype], T, K, ptr(work), ptr(xm), ptr(xs), _stream(x)),
+          "awq_act_stats")
+    return xm, xs
+
+
+def weight_mean(weights, group_size: int) -> torch.Tensor:
+    """Duo-scaling w_mean [K] of linears sharing an input (rows concatenated in list order)."""
+    lib = load_library()
+    K = weights[0].shape[1]
+    dev = weights[0].device
+    nblk = [-(-w.shape[0] // ACT_ROW_BLOCK) for w in weights]
+    part = torch.empty((sum(nblk), K), dtype=torch.float64, device=dev)
+    b0 = 0
+    for w, nb in zip(weights, nblk):
+        gmax = torch.empty(w.shape[0] * (K // group_size), dtype=torch.float32, device=dev)
+        check(lib.awq_weight_colsum(ptr(w), AWQ_DTYPE[w.dtype], w.shape[0], K, group_size, ptr(gmax),
+                                    ctypes.c_void_p(part[b0].data_ptr()), _stream(w)), "awq_weight_colsum")
+        b0 += nb
+    out = torch.empty(K, dtype=torch.float32, device=dev)
+    check(lib.awq_column_mean(ptr(part), part.shape[0], K, float(sum(w.shape[0] for w in weights)), ptr(out),
+                              _stream(out)), "awq_column_mean")
+    return out
+
+
+def act_scale_table(x_mean: torch.Tensor, w_mean: Optional[torch.Tensor], n_grid: int) -> torch.Tensor:
+    K = x_mean.numel()
+    table = torch.empty((n_grid, K), dtype=torch.float32, device=x_mean.device)
+    check(load_library().awq_act_scale_table(ptr(x_mean), ptr(w_mean), K, n_grid, ptr(table), _stream(table)),
+          "awq_act_scale_table")
+    return table
+
+
+def act_search_losses(weights, x_sq: torch.Tensor, table: torch.Tensor, group_size: int, bits: int,
+                      symmetric: bool) -> torch.Tensor:
+    """Per-group losses of every candidate: part fp32 [n_grid, total groups of all linears]."""
+    lib = load_library()
+    n_grid, K = table.shape
+    groups = [w.shape[0] * (K // group_size) for w in weights]
+    stride = sum(groups)
+    part = torch.empty((n_grid, stride), dtype=torch.float32, device=table.device)
+    off = 0
+    for w, g in zip(weights, groups):
+        check(lib.awq_act_search_losses(ptr(w), AWQ_DTYPE[w.dtype], w.shape[0], K, group_size, bits,
+                                        int(bool(symmetric)), ptr(table), n_grid, ptr(x_sq),
+                                        ctypes.c_void_p(part.data_ptr() + 4 * off), stride, _stream(w)),
+              "awq_act_search_losses")
+        off += g
+    return part
+
+
+def act_search_select(part: torch.Tensor, table: torch.Tensor):
+    """-> (losses fp64 [n_grid], best int32 [1], s_best fp32 [K]) on the device."""
+    n_grid, stride = part.shape
+    K = table.shape[1]
+    dev = part.device
+    work = torch.empty(n_grid * (-(-stride // ACT_GROUP_BLOCK)), dtype=torch.float64, device=dev)
+    losses = torch.empty(n_grid, dtype=torch.float64, device=dev)
+    best = torch.empty(1, dtype=torch.int32, device=dev)
+    s_best = torch.empty(K, dtype=torch.float32, device=dev)
+    check(load_library().awq_act_search_select(ptr(part), n_grid, stride, ptr(table), K, ptr(work), ptr(losses),
+                                               ptr(best), ptr(s_best), _stream(part)), "awq_act_search_select")
+    return losses, best, s_best
+
+
+def apply_input_scale(w: torch.Tensor, s: torch.Tensor) -> torch.Tensor:
+    out = torch.empty_like(w)
+    check(load_library().awq_apply_input_scale(ptr(w), AWQ_DTYPE[w.dtype], w.shape[0], w.shape[1], ptr(s), ptr(out),
+                                               _stream(w)), "awq_apply_input_scale")
+    return out

@@ -13,7 +13,9 @@ fixtures).
 Extensions (no reference counterpart): quantize_packed / quantize_model_packed keep the
 packed int4/int8 words (qweight/qzeros) and fp16 scales on the device for throughput;
 scale_method="search" (new value, opt-in) runs the per-group clip search of
-include/awq_hip.h awq_quantize_search instead of plain RTN ("mse"/"minmax" stay RTN).
+include/awq_hip.h awq_quantize_search instead of plain RTN ("mse"/"minmax" stay RTN);
+scale_method="awq" (new value, opt-in) adds quantize_layer_group, the activation-aware
+per-input-channel scale search of include/awq_hip.h awq_act_* (act_search.py).
 """
 
 import math
@@ -46,6 +48,7 @@ class AWQQuantizer:
         logger_file_path: Optional[str] = None,
         search_grid: int = 20,
         search_max_shrink: float = 0.5,
+        duo_scaling: bool = True,
     ):
         self.bits = bits
         self.group_size = group_size
@@ -60,6 +63,9 @@ class AWQQuantizer:
         # i < int(search_max_shrink * search_grid) (alpha = 1 first: RTN wins ties)
         self.search_grid = search_grid
         self.search_max_shrink = search_max_shrink
+        # scale_method="awq" only (quantize_layer_group): search_grid ratios r = i/search_grid,
+        # channel scales x_mean^r [/ w_mean^(1-r)] (duo_scaling, AutoAWQ's default)
+        self.duo_scaling = duo_scaling
 
         # device string semantics of awq.py:70-77
         if device is None:
@@ -75,6 +81,9 @@ class AWQQuantizer:
         self.qmin, self.qmax = self._calculate_qmin_qmax()
         self.logger.info(f"Initialized AWQ Quantizer with bits={bits}, group_size={group_size}, symmetric={symmetric}")
         self.logger.info(f"Quantization range: [{self.qmin}, {self.qmax}]")
+        if self.scale_method == "awq":
+            self.logger.info("scale_method='awq': the activation-aware search runs in quantize_layer_group(); "
+                             "tensors quantized without activations (quantize, quantize_model) are RTN")
 
     # ------------------------------------------------------------------ validation
     def _validate_parameters(self) -> None:
@@ -87,11 +96,14 @@ class AWQQuantizer:
             raise ValueError(f"Unsupported zero point calibration method: {self.zero_point}")
         if self.zero_point == "percentile" and (self.percentile <= 0 or self.percentile >= 1):
             raise ValueError(f"Percentile must be in range (0, 1): {self.percentile}")
-        if self.scale_method not in ["minmax", "mse", "search"]:
+        if self.scale_method not in ["minmax", "mse", "search", "awq"]:
             raise ValueError(f"Unsupported scale calibration method: {self.scale_method}")
-        if self.scale_method == "search":
+        if self.scale_method in ("search", "awq"):
             if not isinstance(self.search_grid, int) or self.search_grid < 1:
                 raise ValueError(f"search_grid must be a positive integer: {self.search_grid}")
+        if self.scale_method == "awq" and self.search_grid > _hip.ACT_MAX_GRID:
+            raise ValueError(f"search_grid must be <= {_hip.ACT_MAX_GRID} for scale_method='awq': {self.search_grid}")
+        if self.scale_method == "search":
             if not (0 < self.search_max_shrink <= 1):
                 raise ValueError(f"search_max_shrink must be in (0, 1]: {self.search_max_shrink}")
 
@@ -348,6 +360,38 @@ class AWQQuantizer:
                                      "zero_points": r["zero_points"], "bits": r["bits"],
                                      "group_size": r["group_size"], "symmetric": r["symmetric"]}
         return {k: out[k] for k in tensors if k in out}
+
+    def quantize_layer_group(self, weights: Dict[str, torch.Tensor], activations: Optional[torch.Tensor] = None,
+                             *, x_mean: Optional[torch.Tensor] = None, x_sq: Optional[torch.Tensor] = None,
+                             packed: bool = True, table: Optional[torch.Tensor] = None) -> dict:
+        """Activation-aware scale search + quantization of linears that read one input
+        (scale_method="awq"; include/awq_hip.h awq_act_*, act_search.py).
+
+        weights: name -> [out_features, in_features] (one dtype: bf16 / fp16 / fp32);
+        activations: calibration inputs [tokens, in_features], or the per-channel statistics
+        x_mean = mean |x|, x_sq = mean x^2 directly.  Each weight is quantized as
+        W * diag(input_scale) (quantize_packed() result dicts if packed, else quantize()'s,
+        device tensors, each with "input_scale"); the caller folds 1 / input_scale into the
+        op producing x.  Returns {"results", "input_scale" fp32 [in], "ratio", "best",
+        "losses" fp64 [search_grid] (the candidates' diagonal-MSE losses)}."""
+        from .act_search import _check_group, search_layer_group
+        if self.scale_method != "awq":
+            raise ValueError("quantize_layer_group needs scale_method='awq'")
+        _check_group(weights, self.group_size)
+        self._check_mode()
+        dev = self.compute_device()
+        sr = search_layer_group(weights, dev, group_size=self.group_size, bits=self.bits, symmetric=self.symmetric,
+                                n_grid=self.search_grid, duo_scaling=self.duo_scaling, activations=activations,
+                                x_mean=x_mean, x_sq=x_sq, table=table)
+        results = {}
+        for name, sw in sr["scaled"].items():
+            r = self.quantize_packed(sw) if packed else self._quantize_device(sw)   # RTN of W * diag(s)
+            r["input_scale"] = sr["input_scale"]
+            results[name] = r
+        best = int(sr["best"].item())
+        self.logger.info(f"awq search over {list(weights)}: ratio {best}/{self.search_grid}")
+        return {"results": results, "input_scale": sr["input_scale"], "best": best,
+                "ratio": best / self.search_grid, "losses": sr["losses"], "table": sr["table"]}
 
     def export_autoawq(self, packed: Dict[str, torch.Tensor]) -> Dict[str, torch.Tensor]:
         """A quantize_packed() result of a 2-D [out_features, in_features] weight in the

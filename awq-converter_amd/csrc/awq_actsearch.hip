@@ -1,0 +1,396 @@
+// awq_actsearch.hip — activation-aware per-input-channel scale search (scale_method="awq").
+//
+// No reference counterpart: the reference stores scale_method and never reads it
+// (awq.py:66,111-112) and collects no activations (SURVEY.md §1, §8a "parity unpinned").
+// This is the search AutoAWQ publishes (per input channel k, s_k = x_mean_k^r, optionally
+// divided by w_mean_k^(1-r) ("duo scaling"), normalised, r = i / n_grid; quantize W·diag(s),
+// undo s, keep the r with the smallest error), with its output-MSE loss
+// ||X (Ŵ - W)^T||² replaced by the diagonal form Σ_k E[x_k²] Σ_n (Ŵ_nk - W_nk)² — exact
+// for uncorrelated input channels, computable per element, so the whole search is one
+// streaming pass over W (all candidates evaluated from registers) instead of n_grid GEMMs.
+// Definition, canonical summation orders and ABI: include/awq_hip.h (awq_act_*); CPU
+// restatement: oracle/awq_oracle.c (oracle_act_*).
+//
+// Every element-wise op follows the reference recipe for the weight dtype D (refmath:
+// fp32 math, RNE to D after each op); the scale table is computed in fp64.
+#include "awq_refmath.h"
+
+namespace awq {
+namespace {
+
+using namespace refmath;
+
+constexpr int kRowBlock = 256;     // rows per canonical fp64 column-sum block
+constexpr int kGroupBlock = 1024;  // groups per canonical fp64 loss block
+
+// 8 consecutive elements as fp32 (compute type of bf16 / fp16 / fp32 inputs)
+template <int DT>
+__device__ __forceinline__ void load8(const void* base, int64_t i, float (&v)[8]) {
+    if (DT == AWQ_DTYPE_F32) {
+        const float4* p = (const float4*)((const float*)base + i);
+        const float4 a = p[0], b = p[1];
+        v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+        v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+    } else {
+        const uint4 u = *(const uint4*)((const uint16_t*)base + i);
+        const uint32_t h[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint16_t lo = (uint16_t)(h[j] & 0xFFFFu), hi = (uint16_t)(h[j] >> 16);
+            if (DT == AWQ_DTYPE_BF16) {
+                v[2 * j] = __uint_as_float((uint32_t)lo << 16);
+                v[2 * j + 1] = __uint_as_float((uint32_t)hi << 16);
+            } else {
+                v[2 * j] = sw_f16_to_f32(lo);
+                v[2 * j + 1] = sw_f16_to_f32(hi);
+            }
+        }
+    }
+}
+
+// ---- column sums (canonical: rows ascending inside a 256-row block, fp64) ----
+// MODE 0, activations x [T, K]:  part0[b][k] = sum |x|,  part1[b][k] = sum x*x
+// MODE 1, weights w [R, K]:      part0[b][k] = sum fp32(|w| / fp32(gmax[r, k/L] + 1e-6f))
+template <int DT, int MODE>
+__global__ __launch_bounds__(256) void colsum_kernel(const void* __restrict__ src, int64_t rows, int64_t K,
+                                                     int64_t L, const float* __restrict__ gmax,
+                                                     double* __restrict__ part0, double* __restrict__ part1) {
+    typedef Traits<DT> T;
+    const int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (k >= K) return;
+    const int64_t b = blockIdx.y;
+    const int64_t r0 = b * kRowBlock;
+    const int64_t r1 = (r0 + kRowBlock < rows) ? r0 + kRowBlock : rows;
+    const typename T::S* p = (const typename T::S*)src;
+    const int64_t G = K / L;
+    double s0 = 0.0, s1 = 0.0;
+    for (int64_t r = r0; r < r1; ++r) {
+        const float v = T::load(p, r * K + k);
+        if (MODE == 0) {
+            const double d = (double)v;     // |x| and x*x are exact in fp64
+            s0 += __builtin_fabs(d);
+            s1 += d * d;
+        } else {
+            const float den = gmax[r * G + k / L] + 1e-6f;
+            s0 += (double)(__builtin_fabsf(v) / den);
+        }
+    }
+    part0[b * K + k] = s0;
+    if (MODE == 0) part1[b * K + k] = s1;
+}
+
+// out[k] = fp32(sum over blocks, ascending, fp64 / divisor)
+__global__ __launch_bounds__(256) void colmean_kernel(const double* __restrict__ part, int64_t nblk, int64_t K,
+                                                      double divisor, float* __restrict__ out) {
+    const int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (k >= K) return;
+    double s = 0.0;
+    for (int64_t b = 0; b < nblk; ++b) s += part[b * K + k];
+    out[k] = (float)(s / divisor);
+}
+
+// Lane layout shared by the group kernels: LPG = L / 8 lanes per group (8 consecutive
+// elements per lane), GPW = 64 / LPG groups per wave, the wave's groups are GPW
+// consecutive ROWS of one group column g (the same k range: table / x_sq loads are shared).
+struct GroupLane {
+    int64_t r, g, k0;
+    bool valid;
+};
+
+__device__ __forceinline__ bool group_lane(int64_t item, int64_t R, int64_t G, int lpg, GroupLane& gl) {
+    const int lane = threadIdx.x & 63;
+    const int gpw = 64 / lpg;
+    const int64_t nrb = (R + gpw - 1) / gpw;
+    if (item >= nrb * G) return false;
+    gl.g = item / nrb;
+    const int64_t rb = item - gl.g * nrb;
+    gl.r = rb * gpw + lane / lpg;
+    gl.valid = gl.r < R;
+    gl.k0 = gl.g * (int64_t)(8 * lpg) + 8 * (lane % lpg);
+    return true;
+}
+
+// NaN-propagating max |w| of every group (awq_weight_mean's normaliser)
+template <int DT>
+__global__ __launch_bounds__(256) void group_absmax_kernel(const void* __restrict__ w, int64_t R, int64_t K,
+                                                           int lpg, float* __restrict__ gmax) {
+    const int64_t G = K / (8 * lpg);
+    const int64_t nw = (int64_t)gridDim.x * 4;
+    for (int64_t item = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);; item += nw) {
+        GroupLane gl;
+        if (!group_lane(item, R, G, lpg, gl)) break;
+        float v[8];
+        if (gl.valid) load8<DT>(w, gl.r * K + gl.k0, v);
+        else for (int j = 0; j < 8; ++j) v[j] = 0.0f;
+        float m = 0.0f;
+        int nan = 0;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const float a = __builtin_fabsf(v[j]);
+            nan |= a != a;
+            m = a > m ? a : m;
+        }
+        for (int o = 1; o < lpg; o <<= 1) {
+            const float t = __shfl_xor(m, o, 64);
+            m = t > m ? t : m;
+            nan |= __shfl_xor(nan, o, 64);
+        }
+        if (gl.valid && (threadIdx.x & 63) % lpg == 0) gmax[gl.r * G + gl.g] = nan ? __builtin_nanf("") : m;
+    }
+}
+
+// candidate i's raw scale of channel k (fp64): x_mean^r [/ (w_mean^(1-r) + 1e-4)], >= 1e-4
+__device__ __forceinline__ double raw_scale(const float* x_mean, const float* w_mean, int64_t k, double r) {
+    double s = pow((double)x_mean[k], r);
+    if (w_mean) s = s / (pow((double)w_mean[k], 1.0 - r) + 1e-4);
+    return s < 1e-4 ? 1e-4 : s;   // NaN stays NaN
+}
+
+// table[i][k] = fp32(raw / sqrt(max_k raw * min_k raw)), inf / NaN -> 1; one workgroup per
+// candidate; max / min propagate NaN (order-independent, so any reduction order is exact)
+__global__ __launch_bounds__(256) void scale_table_kernel(const float* __restrict__ x_mean,
+                                                          const float* __restrict__ w_mean, int64_t K, int n_grid,
+                                                          float* __restrict__ table) {
+    __shared__ double smx[256], smn[256];
+    __shared__ int snan[256];
+    const int i = blockIdx.x, tid = threadIdx.x;
+    const double r = (double)i / (double)n_grid;
+    double mx = -__builtin_inf(), mn = __builtin_inf();
+    int nan = 0;
+    for (int64_t k = tid; k < K; k += 256) {
+        const double s = raw_scale(x_mean, w_mean, k, r);
+        if (s != s) nan = 1;
+        mx = s > mx ? s : mx;
+        mn = s < mn ? s : mn;
+    }
+    smx[tid] = mx;
+    smn[tid] = mn;
+    snan[tid] = nan;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+        if (tid < o) {
+            smx[tid] = smx[tid + o] > smx[tid] ? smx[tid + o] : smx[tid];
+            smn[tid] = smn[tid + o] < smn[tid] ? smn[tid + o] : smn[tid];
+            snan[tid] |= snan[tid + o];
+        }
+        __syncthreads();
+    }
+    const double norm = snan[0] ? __builtin_nan("") : sqrt(smx[0] * smn[0]);
+    for (int64_t k = tid; k < K; k += 256) {
+        double s = raw_scale(x_mean, w_mean, k, r) / norm;
+        if (s != s || __builtin_isinf(s)) s = 1.0;
+        table[(int64_t)i * K + k] = (float)s;
+    }
+}
+
+// Per group and candidate i: w' = RN(w * s_i), RTN parameters of w' (awq.py:173-213),
+// q (awq.py:245-248), the reference's dequantize dq = fp16(fp16(q - z) * fp16(scale))
+// (awq.py:459-539), ŵ = dq / s_i (fp32), e = ŵ - w, loss = sum x_sq[k] * (e * e): each
+// lane sums its 8 elements in order, then the xor-butterfly (pairwise) tree over the
+// group's LPG lanes; part[i * stride + r * G + g] (fp32).
+template <int DT>
+__global__ __launch_bounds__(256) void act_loss_kernel(const void* __restrict__ w, int64_t R, int64_t K, int lpg,
+                                                       int qmin, int qmax, int sym, const float* __restrict__ table,
+                                                       int n_grid, const float* __restrict__ x_sq,
+                                                       float* __restrict__ part, int64_t stride) {
+    typedef Traits<DT> T;
+    const int64_t G = K / (8 * lpg);
+    const int64_t nw = (int64_t)gridDim.x * 4;
+    const bool leader = (threadIdx.x & 63) % lpg == 0;
+    for (int64_t item = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);; item += nw) {
+        GroupLane gl;
+        if (!group_lane(item, R, G, lpg, gl)) break;
+        float v[8], h[8];
+        if (gl.valid) load8<DT>(w, gl.r * K + gl.k0, v);
+        else for (int j = 0; j < 8; ++j) v[j] = 0.0f;
+        load8<AWQ_DTYPE_F32>(x_sq, gl.k0, h);
+        for (int i = 0; i < n_grid; ++i) {
+            float s[8], ws[8];
+            load8<AWQ_DTYPE_F32>(table, (int64_t)i * K + gl.k0, s);
+            float mn = __builtin_inff(), mx = -__builtin_inff();
+            int nan = 0;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                ws[j] = T::rn(v[j] * s[j]);
+                nan |= ws[j] != ws[j];
+                mn = ws[j] < mn ? ws[j] : mn;
+                mx = ws[j] > mx ? ws[j] : mx;
+            }
+            for (int o = 1; o < lpg; o <<= 1) {
+                const float a = __shfl_xor(mn, o, 64), b = __shfl_xor(mx, o, 64);
+                mn = a < mn ? a : mn;
+                mx = b > mx ? b : mx;
+                nan |= __shfl_xor(nan, o, 64);
+            }
+            if (nan) { mn = __builtin_nanf(""); mx = __builtin_nanf(""); }
+            float cs, cz;
+            group_params<DT>(mn, mx, nan, qmin, qmax, sym, cs, cz);
+            const float sh = sw_f16_to_f32(canon_f16(cs));
+            float acc = 0.0f;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const float q = quant1<DT>(ws[j], cs, cz, qmin, qmax);
+                const float hq = sw_f16_to_f32(sw_f32_to_f16(q - cz));
+                const float dq = sw_f16_to_f32(sw_f32_to_f16(hq * sh));
+                const float e = dq / s[j] - v[j];
+                acc = acc + h[j] * (e * e);
+            }
+            for (int o = 1; o < lpg; o <<= 1) acc = acc + __shfl_xor(acc, o, 64);
+            if (gl.valid && leader) part[(int64_t)i * stride + gl.r * G + gl.g] = acc;
+        }
+    }
+}
+
+// work[i * nblk + b] = sum of part[i][b*1024 .. +1024) ascending, fp64
+__global__ __launch_bounds__(256) void loss_block_kernel(const float* __restrict__ part, int n_grid, int64_t stride,
+                                                         int64_t nblk, double* __restrict__ work) {
+    const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (idx >= (int64_t)n_grid * nblk) return;
+    const int64_t i = idx / nblk, b = idx - i * nblk;
+    const int64_t g0 = b * kGroupBlock, g1 = (g0 + kGroupBlock < stride) ? g0 + kGroupBlock : stride;
+    const float* p = part + i * stride;
+    double s = 0.0;
+    for (int64_t g = g0; g < g1; ++g) s += (double)p[g];
+    work[idx] = s;
+}
+
+// losses[i] = blocks ascending (fp64); best = first minimum (NaN never wins; all NaN -> 0);
+// s_best = table[best]
+__global__ __launch_bounds__(256) void select_kernel(const double* __restrict__ work, int n_grid, int64_t nblk,
+                                                     const float* __restrict__ table, int64_t K,
+                                                     double* __restrict__ losses, int32_t* __restrict__ best,
+                                                     float* __restrict__ s_best) {
+    __shared__ double sl[256];
+    __shared__ int sb;
+    const int tid = threadIdx.x;
+    if (tid < n_grid) {
+        double s = 0.0;
+        for (int64_t b = 0; b < nblk; ++b) s += work[(int64_t)tid * nblk + b];
+        sl[tid] = s;
+        if (losses) losses[tid] = s;
+    }
+    __syncthreads();
+    if (tid == 0) {
+        double bv = __builtin_inf();
+        int bi = 0;
+        for (int i = 0; i < n_grid; ++i)
+            if (sl[i] < bv) { bv = sl[i]; bi = i; }
+        sb = bi;
+        if (best) best[0] = bi;
+    }
+    __syncthreads();
+    if (s_best)
+        for (int64_t k = tid; k < K; k += 256) s_best[k] = table[(int64_t)sb * K + k];
+}
+
+// out = RN_D(w * s[k]) (torch: W.mul_(scales) on a D tensor with an fp32 scale vector)
+template <int DT>
+__global__ __launch_bounds__(256) void apply_scale_kernel(const void* __restrict__ w, int64_t R, int64_t K,
+                                                          const float* __restrict__ s, void* __restrict__ out) {
+    typedef Traits<DT> T;
+    const typename T::S* p = (const typename T::S*)w;
+    const int64_t total = R * K;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+        const float y = T::rn(T::load(p, i) * s[i % K]);
+        if (DT == AWQ_DTYPE_BF16) ((uint16_t*)out)[i] = (uint16_t)(__float_as_uint(y) >> 16);
+        else if (DT == AWQ_DTYPE_F16) ((uint16_t*)out)[i] = sw_f32_to_f16(y);
+        else ((float*)out)[i] = y;
+    }
+}
+
+inline unsigned blocks_for(int64_t work, int64_t per_block, int64_t cap) {
+    int64_t b = (work + per_block - 1) / per_block;
+    if (b < 1) b = 1;
+    if (b > cap) b = cap;
+    return (unsigned)b;
+}
+
+}  // namespace
+
+#define AWQ_DT_SWITCH(dtype, KERNEL_CALL)                            \
+    switch (dtype) {                                                 \
+    case AWQ_DTYPE_BF16: { constexpr int D = AWQ_DTYPE_BF16; KERNEL_CALL; } break; \
+    case AWQ_DTYPE_F16: { constexpr int D = AWQ_DTYPE_F16; KERNEL_CALL; } break;   \
+    case AWQ_DTYPE_F32: { constexpr int D = AWQ_DTYPE_F32; KERNEL_CALL; } break;   \
+    default: return hipErrorInvalidValue;                            \
+    }
+
+hipError_t launch_act_stats(const void* x, int dtype, int64_t T, int64_t K, double* work, float* x_mean,
+                            float* x_sq, hipStream_t stream) {
+    const int64_t nblk = (T + kRowBlock - 1) / kRowBlock;
+    double* p0 = work;
+    double* p1 = work + nblk * K;
+    const dim3 grid((unsigned)((K + 255) / 256), (unsigned)nblk);
+    AWQ_DT_SWITCH(dtype, hipLaunchKernelGGL((colsum_kernel<D, 0>), grid, dim3(256), 0, stream, x, T, K, K,
+                                            nullptr, p0, p1))
+    if (hipError_t e = hipPeekAtLastError()) return e;
+    const dim3 g1((unsigned)((K + 255) / 256));
+    hipLaunchKernelGGL(colmean_kernel, g1, dim3(256), 0, stream, p0, nblk, K, (double)T, x_mean);
+    hipLaunchKernelGGL(colmean_kernel, g1, dim3(256), 0, stream, p1, nblk, K, (double)T, x_sq);
+    return hipPeekAtLastError();
+}
+
+hipError_t launch_weight_colsum(const void* w, int dtype, int64_t R, int64_t K, int64_t L, float* gmax,
+                                double* part, hipStream_t stream) {
+    const int lpg = (int)(L / 8);
+    const int64_t G = K / L;
+    const int64_t items = ((R + (64 / lpg) - 1) / (64 / lpg)) * G;
+    AWQ_DT_SWITCH(dtype, hipLaunchKernelGGL((group_absmax_kernel<D>), dim3(blocks_for(items, 4, 256 * 64)),
+                                            dim3(256), 0, stream, w, R, K, lpg, gmax))
+    if (hipError_t e = hipPeekAtLastError()) return e;
+    const int64_t nblk = (R + kRowBlock - 1) / kRowBlock;
+    const dim3 grid((unsigned)((K + 255) / 256), (unsigned)nblk);
+    AWQ_DT_SWITCH(dtype, hipLaunchKernelGGL((colsum_kernel<D, 1>), grid, dim3(256), 0, stream, w, R, K, L, gmax,
+                                            part, nullptr))
+    return hipPeekAtLastError();
+}
+
+hipError_t launch_colmean(const double* part, int64_t nblk, int64_t K, double divisor, float* out,
+                          hipStream_t stream) {
+    hipLaunchKernelGGL(colmean_kernel, dim3((unsigned)((K + 255) / 256)), dim3(256), 0, stream, part, nblk, K,
+                       divisor, out);
+    return hipPeekAtLastError();
+}
+
+hipError_t launch_scale_table(const float* x_mean, const float* w_mean, int64_t K, int n_grid, float* table,
+                              hipStream_t stream) {
+    hipLaunchKernelGGL(scale_table_kernel, dim3((unsigned)n_grid), dim3(256), 0, stream, x_mean, w_mean, K, n_grid,
+                       table);
+    return hipPeekAtLastError();
+}
+
+hipError_t launch_act_losses(const void* w, int dtype, int64_t R, int64_t K, int64_t L, int bits, int symmetric,
+                             const float* table, int n_grid, const float* x_sq, float* part, int64_t stride,
+                             hipStream_t stream) {
+    const int qmin = symmetric ? -(1 << (bits - 1)) : 0;
+    const int qmax = symmetric ? (1 << (bits - 1)) - 1 : (1 << bits) - 1;
+    const int lpg = (int)(L / 8);
+    const int64_t items = ((R + (64 / lpg) - 1) / (64 / lpg)) * (K / L);
+    const unsigned grid = blocks_for(items, 4, 256 * 32);
+    AWQ_DT_SWITCH(dtype, hipLaunchKernelGGL((act_loss_kernel<D>), dim3(grid), dim3(256), 0, stream, w, R, K, lpg,
+                                            qmin, qmax, symmetric, table, n_grid, x_sq, part, stride))
+    return hipPeekAtLastError();
+}
+
+hipError_t launch_act_select(const float* part, int n_grid, int64_t stride, const float* table, int64_t K,
+                             double* work, double* losses, int32_t* best, float* s_best, hipStream_t stream) {
+    const int64_t nblk = (stride + kGroupBlock - 1) / kGroupBlock;
+    hipLaunchKernelGGL(loss_block_kernel, dim3(blocks_for((int64_t)n_grid * nblk, 256, INT32_MAX)), dim3(256), 0,
+                       stream, part, n_grid, stride, nblk, work);
+    if (hipError_t e = hipPeekAtLastError()) return e;
+    hipLaunchKernelGGL(select_kernel, dim3(1), dim3(256), 0, stream, work, n_grid, nblk, table, K, losses, best,
+                       s_best);
+    return hipPeekAtLastError();
+}
+
+hipError_t launch_apply_scale(const void* w, int dtype, int64_t R, int64_t K, const float* s, void* out,
+                              hipStream_t stream) {
+    const unsigned grid = blocks_for(R * K, 256, 256 * 64);
+    AWQ_DT_SWITCH(dtype, hipLaunchKernelGGL((apply_scale_kernel<D>), dim3(grid), dim3(256), 0, stream, w, R, K, s,
+                                            out))
+    return hipPeekAtLastError();
+}
+
+#undef AWQ_DT_SWITCH
+
+}  // namespace awq

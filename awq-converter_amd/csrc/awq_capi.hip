@@ -255,6 +255,99 @@ int awq_stream_copy(const void* src, void* dst, int64_t bytes, void* stream) {
     return hip_status(awq::launch_stream_copy(src, dst, bytes, (hipStream_t)stream), "awq stream copy");
 }
 
+// ---- activation-aware scale search (include/awq_hip.h awq_act_*) ----
+namespace {
+int check_act_shape(int dtype, int64_t rows, int64_t K, int64_t group_size) {
+    if (dtype != AWQ_DTYPE_BF16 && dtype != AWQ_DTYPE_F16 && dtype != AWQ_DTYPE_F32)
+        return fail(AWQ_EUNSUPPORTED, "activation-aware search takes bf16 / fp16 / fp32 weights (dtype code %d)", dtype);
+    if (group_size < 8 || group_size > 512 || (group_size & (group_size - 1)) != 0)
+        return fail(AWQ_EUNSUPPORTED, "activation-aware search needs a power-of-two group_size in [8, 512] (got %lld)",
+                    (long long)group_size);
+    if (rows <= 0 || K <= 0 || K % group_size != 0)
+        return fail(AWQ_EINVAL, "activation-aware search needs a 2-D [rows, K] weight with K %% group_size == 0 "
+                                "(rows=%lld, K=%lld, group_size=%lld)", (long long)rows, (long long)K,
+                    (long long)group_size);
+    return AWQ_OK;
+}
+}  // namespace
+
+int awq_act_stats(const void* x, int dtype, int64_t tokens, int64_t K, double* work, float* x_mean, float* x_sq,
+                  void* stream) {
+    g_err.clear();
+    if (dtype != AWQ_DTYPE_BF16 && dtype != AWQ_DTYPE_F16 && dtype != AWQ_DTYPE_F32)
+        return fail(AWQ_EUNSUPPORTED, "activations must be bf16 / fp16 / fp32 (dtype code %d)", dtype);
+    if (tokens <= 0 || K <= 0) return fail(AWQ_EINVAL, "activations must be a non-empty [tokens, K] matrix");
+    if (!x || !work || !x_mean || !x_sq) return fail(AWQ_EINVAL, "null argument");
+    return hip_status(awq::launch_act_stats(x, dtype, tokens, K, work, x_mean, x_sq, (hipStream_t)stream),
+                      "awq act stats");
+}
+
+int awq_weight_colsum(const void* w, int dtype, int64_t rows, int64_t K, int64_t group_size, float* gmax_work,
+                      double* partial, void* stream) {
+    g_err.clear();
+    if (int rc = check_act_shape(dtype, rows, K, group_size)) return rc;
+    if (!w || !gmax_work || !partial) return fail(AWQ_EINVAL, "null argument");
+    if (!aligned(w, 16)) return fail(AWQ_EINVAL, "weights must be 16-B aligned");
+    return hip_status(awq::launch_weight_colsum(w, dtype, rows, K, group_size, gmax_work, partial,
+                                                (hipStream_t)stream), "awq weight colsum");
+}
+
+int awq_column_mean(const double* partial, int64_t nblk, int64_t K, double divisor, float* out, void* stream) {
+    g_err.clear();
+    if (nblk <= 0 || K <= 0 || !(divisor > 0)) return fail(AWQ_EINVAL, "empty column sum");
+    if (!partial || !out) return fail(AWQ_EINVAL, "null argument");
+    return hip_status(awq::launch_colmean(partial, nblk, K, divisor, out, (hipStream_t)stream), "awq column mean");
+}
+
+int awq_act_scale_table(const float* x_mean, const float* w_mean, int64_t K, int n_grid, float* table,
+                        void* stream) {
+    g_err.clear();
+    if (n_grid < 1 || n_grid > AWQ_ACT_MAX_GRID)
+        return fail(AWQ_EINVAL, "n_grid must be in [1, %d] (got %d)", AWQ_ACT_MAX_GRID, n_grid);
+    if (K <= 0) return fail(AWQ_EINVAL, "K must be positive");
+    if (!x_mean || !table) return fail(AWQ_EINVAL, "null argument");
+    return hip_status(awq::launch_scale_table(x_mean, w_mean, K, n_grid, table, (hipStream_t)stream),
+                      "awq scale table");
+}
+
+int awq_act_search_losses(const void* w, int dtype, int64_t rows, int64_t K, int64_t group_size, int bits,
+                          int symmetric, const float* table, int n_grid, const float* x_sq, float* part,
+                          int64_t part_stride, void* stream) {
+    g_err.clear();
+    if (bits != 4 && bits != 8) return fail(AWQ_EINVAL, "Unsupported bit width: %d. Supported: 4, 8.", bits);
+    if (int rc = check_act_shape(dtype, rows, K, group_size)) return rc;
+    if (n_grid < 1 || n_grid > AWQ_ACT_MAX_GRID)
+        return fail(AWQ_EINVAL, "n_grid must be in [1, %d] (got %d)", AWQ_ACT_MAX_GRID, n_grid);
+    if (part_stride < rows * (K / group_size)) return fail(AWQ_EINVAL, "part_stride smaller than the group count");
+    if (!w || !table || !x_sq || !part) return fail(AWQ_EINVAL, "null argument");
+    if (!aligned(w, 16) || !aligned(table, 16) || !aligned(x_sq, 16) || !aligned(part, 4))
+        return fail(AWQ_EINVAL, "weights, table and x_sq must be 16-B aligned");
+    return hip_status(awq::launch_act_losses(w, dtype, rows, K, group_size, bits, symmetric, table, n_grid, x_sq,
+                                             part, part_stride, (hipStream_t)stream), "awq act losses");
+}
+
+int awq_act_search_select(const float* part, int n_grid, int64_t part_stride, const float* table, int64_t K,
+                          double* work, double* losses, int32_t* best, float* s_best, void* stream) {
+    g_err.clear();
+    if (n_grid < 1 || n_grid > AWQ_ACT_MAX_GRID)
+        return fail(AWQ_EINVAL, "n_grid must be in [1, %d] (got %d)", AWQ_ACT_MAX_GRID, n_grid);
+    if (part_stride <= 0 || K <= 0) return fail(AWQ_EINVAL, "empty search");
+    if (!part || !table || !work) return fail(AWQ_EINVAL, "null argument");
+    return hip_status(awq::launch_act_select(part, n_grid, part_stride, table, K, work, losses, best, s_best,
+                                             (hipStream_t)stream), "awq act select");
+}
+
+int awq_apply_input_scale(const void* w, int dtype, int64_t rows, int64_t K, const float* s, void* out,
+                          void* stream) {
+    g_err.clear();
+    if (dtype != AWQ_DTYPE_BF16 && dtype != AWQ_DTYPE_F16 && dtype != AWQ_DTYPE_F32)
+        return fail(AWQ_EUNSUPPORTED, "input scaling takes bf16 / fp16 / fp32 weights (dtype code %d)", dtype);
+    if (rows < 0 || K < 0) return fail(AWQ_EINVAL, "negative shape");
+    if (rows * K == 0) return AWQ_OK;
+    if (!w || !s || !out) return fail(AWQ_EINVAL, "null argument");
+    return hip_status(awq::launch_apply_scale(w, dtype, rows, K, s, out, (hipStream_t)stream), "awq apply scale");
+}
+
 int awq_selftest(int which, unsigned long long* result, void* stream) {
     g_err.clear();
     if (!result) return fail(AWQ_EINVAL, "null result pointer");

@@ -91,4 +91,21 @@ hipError_t launch_dequant(const int32_t* tensor_q, const int32_t* qweight, const
                           const int32_t* zeros, const int32_t* qzeros, int64_t rows, int64_t K,
                           int64_t L, int bits, int qmin, float* out, hipStream_t stream);
 
+// activation-aware scale search (awq_actsearch.hip)
+hipError_t launch_act_stats(const void* x, int dtype, int64_t T, int64_t K, double* work, float* x_mean,
+                            float* x_sq, hipStream_t stream);
+hipError_t launch_weight_colsum(const void* w, int dtype, int64_t R, int64_t K, int64_t L, float* gmax,
+                                double* part, hipStream_t stream);
+hipError_t launch_colmean(const double* part, int64_t nblk, int64_t K, double divisor, float* out,
+                          hipStream_t stream);
+hipError_t launch_scale_table(const float* x_mean, const float* w_mean, int64_t K, int n_grid, float* table,
+                              hipStream_t stream);
+hipError_t launch_act_losses(const void* w, int dtype, int64_t R, int64_t K, int64_t L, int bits, int symmetric,
+                             const float* table, int n_grid, const float* x_sq, float* part, int64_t stride,
+                             hipStream_t stream);
+hipError_t launch_act_select(const float* part, int n_grid, int64_t stride, const float* table, int64_t K,
+                             double* work, double* losses, int32_t* best, float* s_best, hipStream_t stream);
+hipError_t launch_apply_scale(const void* w, int dtype, int64_t R, int64_t K, const float* s, void* out,
+                              hipStream_t stream);
+
 }  // namespace awq

@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define AWQ_HIP_ABI_VERSION 3
+#define AWQ_HIP_ABI_VERSION 4
 
 /* dtype codes of the input weights (torch dtypes the reference accepts, awq.py:397) */
 enum { AWQ_DTYPE_BF16 = 0, AWQ_DTYPE_F16 = 1, AWQ_DTYPE_F32 = 2, AWQ_DTYPE_F64 = 3 };
@@ -152,6 +152,64 @@ int awq_dequantize_packed(const int32_t* qweight, const int32_t* qzeros, const u
 /* Pack int32 values [rows, n] into [rows, ceil(n*bits/32)] words ((v - qmin) & mask). */
 int awq_pack_rows(const int32_t* v, int64_t rows, int64_t n, int bits, int qmin, int32_t* packed,
                   void* stream);
+
+/* ---- Activation-aware per-input-channel scale search (scale_method="awq") ----------
+ * Not in the reference (it stores scale_method, awq.py:66, and collects no activations;
+ * parity unpinned).  AutoAWQ's published search (third-party,
+ * not vendored in the reference) restated with a per-element loss, for one "layer group"
+ * of n >= 1 linears W_j [R_j, K] that read the same input x [tokens, K]:
+ *
+ *   x_mean[k] = fp32(sum_t |x[t,k]| / T),  x_sq[k] = fp32(sum_t x[t,k]^2 / T)
+ *       (awq_act_stats; sums in fp64, t ascending inside 256-token blocks, then the
+ *        blocks ascending)
+ *   w_mean[k] = fp32(sum_{j,r} fp32(|W_j[r,k]| / fp32(gmax_j[r, k/gs] + 1e-6f)) / sum_j R_j)
+ *       (duo scaling only; gmax = max |W| of the group; same fp64 block order, the
+ *        linears' blocks in list order; awq_weight_colsum per linear + awq_column_mean)
+ *   candidate i = 0 .. n_grid-1, r = i / n_grid (fp64):
+ *       raw_k = max(x_mean_k^r [/ (w_mean_k^(1-r) + 1e-4)], 1e-4)
+ *       s_i[k] = fp32(raw_k / sqrt(max_k raw * min_k raw)), inf / NaN -> 1
+ *       (awq_act_scale_table, fp64 pow / sqrt: the only step not bit-reproducible across
+ *        math libraries; callers check it to 1 fp32 ulp and feed the table downstream)
+ *   per element of every group, in the weight dtype D's per-op rounding:
+ *       w' = RN_D(w * s_i[k]); RTN scale/zero of w' (awq.py:173-213); q (awq.py:245-248);
+ *       dq = fp16(fp16(q - z) * fp16(scale)) (awq.py:459-539); e = fp32(dq / s_i[k]) - w;
+ *       c = x_sq[k] * (e * e)
+ *   group loss: each 8-element chunk summed in order, then the pairwise tree over the
+ *       group's gs/8 chunks (fp32) -> part[i * part_stride + group]
+ *       (awq_act_search_losses, per linear at its offset in one group list)
+ *   loss_i = sum over 1024-group blocks (ascending, fp64) of the blocks' ascending fp64
+ *       sums; best = first minimum (NaN never wins; all NaN -> 0) (awq_act_search_select)
+ *   result: every W_j quantized as W_j * diag(s_best) (awq_apply_input_scale, then
+ *       awq_quantize_groups); s_best is returned to be folded into the op producing x
+ *       (x / s_best, e.g. the preceding norm's weight).
+ * The loss is the diagonal (uncorrelated-channel) form of AutoAWQ's output MSE
+ * ||x (W' - W)^T||^2.  Weights: bf16 / fp16 / fp32, 2-D, K % gs == 0, gs a power of two in
+ * [8, 512]; weights / table / x_sq 16-B aligned.  Sizes of the caller's workspaces:
+ *   awq_act_stats      work    fp64 [2 * ceil(T/256) * K]
+ *   awq_weight_colsum  gmax_work fp32 [R * K/gs]; partial fp64 [ceil(R/256) * K] (this
+ *                      linear's slice of the group's [sum_j ceil(R_j/256), K] array)
+ *   awq_act_search_select work fp64 [n_grid * ceil(part_stride / 1024)]
+ * n_grid <= AWQ_ACT_MAX_GRID. */
+#define AWQ_ACT_MAX_GRID 256
+
+int awq_act_stats(const void* x, int dtype, int64_t tokens, int64_t K, double* work, float* x_mean, float* x_sq,
+                  void* stream);
+int awq_weight_colsum(const void* w, int dtype, int64_t rows, int64_t K, int64_t group_size, float* gmax_work,
+                      double* partial, void* stream);
+/* out[k] = fp32(sum_{b < nblk, ascending} partial[b * K + k] / divisor) (fp64 sum) */
+int awq_column_mean(const double* partial, int64_t nblk, int64_t K, double divisor, float* out, void* stream);
+/* table fp32 [n_grid, K]; w_mean NULL = no duo scaling */
+int awq_act_scale_table(const float* x_mean, const float* w_mean, int64_t K, int n_grid, float* table,
+                        void* stream);
+int awq_act_search_losses(const void* w, int dtype, int64_t rows, int64_t K, int64_t group_size, int bits,
+                          int symmetric, const float* table, int n_grid, const float* x_sq, float* part,
+                          int64_t part_stride, void* stream);
+/* losses fp64 [n_grid], best int32 [1], s_best fp32 [K] (any may be NULL) */
+int awq_act_search_select(const float* part, int n_grid, int64_t part_stride, const float* table, int64_t K,
+                          double* work, double* losses, int32_t* best, float* s_best, void* stream);
+/* out [rows, K] (dtype D) = RN_D(w * s[k]) */
+int awq_apply_input_scale(const void* w, int dtype, int64_t rows, int64_t K, const float* s, void* out,
+                          void* stream);
 
 /* Device self-test (diagnostics).  which = 0: the fast reciprocal used by the streaming
  * kernel against IEEE 1/s over every bf16 s >= RN_bf16(1e-10); adds the number of

@@ -32,6 +32,7 @@
  */
 #include <math.h>
 #include <stdint.h>
+#include <stdlib.h>
 #include <string.h>
 
 #ifdef _OPENMP
@@ -348,6 +349,197 @@ int oracle_pack_rows(const int32_t* v, int64_t rows, int64_t n, int bits, int qm
             }
             packed[r * words + c] = (int32_t)w;
         }
+    }
+    return 0;
+}
+
+/* ---------------- activation-aware scale search (scale_method="awq") ----------------
+ * NOT in the reference (awq.py:66 stores scale_method; no activations are collected):
+ * restates the product's definition (include/awq_hip.h, awq_act_*), itself AutoAWQ's
+ * published per-input-channel search (third-party; not vendored in the reference, not
+ * installed here) with the output-MSE loss in its diagonal per-element form.  Parity with
+ * the HIP kernels is checked bit for bit given the same scale table (the table's fp64
+ * pow differs between math libraries by <= 1 fp32 ulp, checked separately); parity with
+ * AutoAWQ is unpinned. */
+#define ACT_ROW_BLOCK 256
+#define ACT_GROUP_BLOCK 1024
+
+static inline float load_f(const void* x, int dtype, int64_t i) { return (float)load_elem(x, dtype, i); }
+
+int oracle_act_stats(const void* x, int dtype, int64_t T, int64_t K, float* x_mean, float* x_sq) {
+    if (!x || T <= 0 || K <= 0 || dtype == AWQ_ORACLE_F64) return -1;
+    int64_t nblk = (T + ACT_ROW_BLOCK - 1) / ACT_ROW_BLOCK;
+#pragma omp parallel for schedule(static) if (T * K >= (1 << 16))
+    for (int64_t k = 0; k < K; ++k) {
+        double a = 0.0, q = 0.0;
+        for (int64_t b = 0; b < nblk; ++b) {   /* fp64, tokens ascending inside a block */
+            double pa = 0.0, pq = 0.0;
+            int64_t t1 = (b + 1) * ACT_ROW_BLOCK < T ? (b + 1) * ACT_ROW_BLOCK : T;
+            for (int64_t t = b * ACT_ROW_BLOCK; t < t1; ++t) {
+                double v = (double)load_f(x, dtype, t * K + k);
+                pa += fabs(v);
+                pq += v * v;
+            }
+            a += pa;
+            q += pq;
+        }
+        x_mean[k] = (float)(a / (double)T);
+        x_sq[k] = (float)(q / (double)T);
+    }
+    return 0;
+}
+
+/* partial[b][k] for this linear's ceil(R/256) row blocks: sum fp32(|w| / fp32(gmax + 1e-6f)) */
+int oracle_weight_colsum(const void* w, int dtype, int64_t R, int64_t K, int64_t L, double* partial) {
+    if (!w || R <= 0 || K <= 0 || L <= 0 || K % L || dtype == AWQ_ORACLE_F64) return -1;
+    int64_t G = K / L, nblk = (R + ACT_ROW_BLOCK - 1) / ACT_ROW_BLOCK;
+    float* gmax = (float*)malloc(sizeof(float) * (size_t)(R * G));
+    if (!gmax) return -1;
+    for (int64_t r = 0; r < R; ++r)
+        for (int64_t g = 0; g < G; ++g) {
+            float m = 0.0f;
+            int nan = 0;
+            for (int64_t k = g * L; k < (g + 1) * L; ++k) {
+                float a = fabsf(load_f(w, dtype, r * K + k));
+                if (isnan(a)) nan = 1;
+                if (a > m) m = a;
+            }
+            gmax[r * G + g] = nan ? NAN : m;
+        }
+    for (int64_t b = 0; b < nblk; ++b)
+        for (int64_t k = 0; k < K; ++k) {
+            double s = 0.0;
+            int64_t r1 = (b + 1) * ACT_ROW_BLOCK < R ? (b + 1) * ACT_ROW_BLOCK : R;
+            for (int64_t r = b * ACT_ROW_BLOCK; r < r1; ++r) {
+                float den = gmax[r * G + k / L] + 1e-6f;
+                s += (double)(fabsf(load_f(w, dtype, r * K + k)) / den);
+            }
+            partial[b * K + k] = s;
+        }
+    free(gmax);
+    return 0;
+}
+
+int oracle_column_mean(const double* partial, int64_t nblk, int64_t K, double divisor, float* out) {
+    if (!partial || !out || nblk <= 0 || K <= 0) return -1;
+    for (int64_t k = 0; k < K; ++k) {
+        double s = 0.0;
+        for (int64_t b = 0; b < nblk; ++b) s += partial[b * K + k];
+        out[k] = (float)(s / divisor);
+    }
+    return 0;
+}
+
+static double act_raw(const float* x_mean, const float* w_mean, int64_t k, double r) {
+    double s = pow((double)x_mean[k], r);
+    if (w_mean) s = s / (pow((double)w_mean[k], 1.0 - r) + 1e-4);
+    return s < 1e-4 ? 1e-4 : s;   /* NaN stays NaN */
+}
+
+int oracle_act_scale_table(const float* x_mean, const float* w_mean, int64_t K, int n_grid, float* table) {
+    if (!x_mean || !table || K <= 0 || n_grid < 1) return -1;
+    for (int i = 0; i < n_grid; ++i) {
+        double r = (double)i / (double)n_grid, mx = -INFINITY, mn = INFINITY;
+        int nan = 0;
+        for (int64_t k = 0; k < K; ++k) {
+            double s = act_raw(x_mean, w_mean, k, r);
+            if (isnan(s)) nan = 1;
+            if (s > mx) mx = s;
+            if (s < mn) mn = s;
+        }
+        double norm = nan ? NAN : sqrt(mx * mn);
+        for (int64_t k = 0; k < K; ++k) {
+            double s = act_raw(x_mean, w_mean, k, r) / norm;
+            if (isnan(s) || isinf(s)) s = 1.0;
+            table[(int64_t)i * K + k] = (float)s;
+        }
+    }
+    return 0;
+}
+
+int oracle_act_search_losses(const void* w, int dtype, int64_t R, int64_t K, int64_t L, int bits, int sym,
+                             const float* table, int n_grid, const float* x_sq, float* part, int64_t stride) {
+    if (!w || !table || !x_sq || !part || R <= 0 || K <= 0 || L < 8 || L > 512 || (L & (L - 1)) || K % L ||
+        (bits != 4 && bits != 8) || dtype == AWQ_ORACLE_F64)
+        return -1;
+    int qmin = sym ? -(1 << (bits - 1)) : 0;
+    int qmax = sym ? (1 << (bits - 1)) - 1 : (1 << bits) - 1;
+    int64_t G = K / L;
+    int lpg = (int)(L / 8);
+#pragma omp parallel for schedule(static) if (R * K >= (1 << 12))
+    for (int64_t r = 0; r < R; ++r) {
+        float v[512], ws[512];
+        for (int64_t g = 0; g < G; ++g) {
+            int64_t k0 = g * L;
+            for (int64_t e = 0; e < L; ++e) v[e] = load_f(w, dtype, r * K + k0 + e);
+            for (int i = 0; i < n_grid; ++i) {
+                const float* s = table + (int64_t)i * K + k0;
+                double mn = INFINITY, mx = -INFINITY;
+                int nan = 0;
+                for (int64_t e = 0; e < L; ++e) {
+                    ws[e] = (float)rn((double)(v[e] * s[e]), dtype);
+                    if (isnan(ws[e])) nan = 1;
+                    if (ws[e] < mn) mn = ws[e];
+                    if (ws[e] > mx) mx = ws[e];
+                }
+                if (nan) { mn = NAN; mx = NAN; }
+                double cs, cz;
+                group_scale_zp(mn, mx, dtype, qmin, qmax, sym, &cs, &cz);
+                float sh = oracle_f16_to_f32(oracle_f32_to_f16((float)cs));
+                double acc[64];
+                for (int l = 0; l < lpg; ++l) {   /* chunk l: elements 8l .. 8l+7 in order */
+                    float a = 0.0f;
+                    for (int j = 0; j < 8; ++j) {
+                        int64_t e = 8 * l + j;
+                        double q = op_add(op_div(ws[e], cs, dtype), cz, dtype);
+                        q = op_clamp(op_round(q, dtype), qmin, qmax);
+                        float hq = oracle_f16_to_f32(oracle_f32_to_f16((float)(q - cz)));
+                        float dq = oracle_f16_to_f32(oracle_f32_to_f16(hq * sh));
+                        float d = dq / s[e] - v[e];
+                        a = a + x_sq[k0 + e] * (d * d);
+                    }
+                    acc[l] = a;
+                }
+                for (int o = 1; o < lpg; o <<= 1) {   /* pairwise tree, adjacent chunks first */
+                    double t[64];
+                    for (int l = 0; l < lpg; ++l) t[l] = (double)((float)acc[l] + (float)acc[l ^ o]);
+                    memcpy(acc, t, sizeof(double) * (size_t)lpg);
+                }
+                part[(int64_t)i * stride + r * G + g] = (float)acc[0];
+            }
+        }
+    }
+    return 0;
+}
+
+int oracle_act_search_select(const float* part, int n_grid, int64_t stride, double* losses, int32_t* best) {
+    if (!part || n_grid < 1 || stride <= 0) return -1;
+    int64_t nblk = (stride + ACT_GROUP_BLOCK - 1) / ACT_GROUP_BLOCK;
+    double bv = INFINITY;
+    int bi = 0;
+    for (int i = 0; i < n_grid; ++i) {
+        double tot = 0.0;
+        for (int64_t b = 0; b < nblk; ++b) {
+            double s = 0.0;
+            int64_t g1 = (b + 1) * ACT_GROUP_BLOCK < stride ? (b + 1) * ACT_GROUP_BLOCK : stride;
+            for (int64_t g = b * ACT_GROUP_BLOCK; g < g1; ++g) s += (double)part[(int64_t)i * stride + g];
+            tot += s;
+        }
+        if (losses) losses[i] = tot;
+        if (tot < bv) { bv = tot; bi = i; }
+    }
+    if (best) *best = bi;
+    return 0;
+}
+
+/* out = RN_D(w * s[k]) in the weight dtype (bits of bf16 / fp16, or fp32) */
+int oracle_apply_input_scale(const void* w, int dtype, int64_t R, int64_t K, const float* s, void* out) {
+    if (!w || !s || !out || dtype == AWQ_ORACLE_F64) return -1;
+    for (int64_t i = 0; i < R * K; ++i) {
+        float y = load_f(w, dtype, i) * s[i % K];
+        if (dtype == AWQ_ORACLE_BF16) ((uint16_t*)out)[i] = oracle_f32_to_bf16(y);
+        else if (dtype == AWQ_ORACLE_F16) ((uint16_t*)out)[i] = oracle_f32_to_f16(y);
+        else ((float*)out)[i] = y;
     }
     return 0;
 }

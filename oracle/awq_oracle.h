@@ -19,6 +19,15 @@ int oracle_dequantize(const int32_t* tensor_q, const uint16_t* scales_f16, const
                       int64_t rows, int64_t K, int64_t L, float* out);
 int oracle_pack_rows(const int32_t* v, int64_t rows, int64_t n, int bits, int qmin, int32_t* packed);
 int oracle_set_threads(int n);
+/* activation-aware scale search (product definition, include/awq_hip.h awq_act_*) */
+int oracle_act_stats(const void* x, int dtype, int64_t T, int64_t K, float* x_mean, float* x_sq);
+int oracle_weight_colsum(const void* w, int dtype, int64_t R, int64_t K, int64_t L, double* partial);
+int oracle_column_mean(const double* partial, int64_t nblk, int64_t K, double divisor, float* out);
+int oracle_act_scale_table(const float* x_mean, const float* w_mean, int64_t K, int n_grid, float* table);
+int oracle_act_search_losses(const void* w, int dtype, int64_t R, int64_t K, int64_t L, int bits, int sym,
+                             const float* table, int n_grid, const float* x_sq, float* part, int64_t stride);
+int oracle_act_search_select(const float* part, int n_grid, int64_t stride, double* losses, int32_t* best);
+int oracle_apply_input_scale(const void* w, int dtype, int64_t R, int64_t K, const float* s, void* out);
 uint16_t oracle_f32_to_bf16(float f);
 float oracle_bf16_to_f32(uint16_t h);
 uint16_t oracle_f32_to_f16(float f);

@@ -1,0 +1,275 @@
+"""Activation-aware per-input-channel scale search (scale_method="awq"; include/awq_hip.h
+awq_act_*).
+
+No reference counterpart (the reference collects no activations, awq.py:66 stores
+scale_method and never reads it) and AutoAWQ is not installed: parity with either is
+unpinned.  The bar here:
+  * the HIP kernels equal oracle_act_* bit for bit (statistics, w_mean, per-group losses,
+    loss totals, the chosen candidate, the scaled weight and its quantization) given the
+    same fp64 scale table; the table itself (pow / sqrt in fp64) within 1 fp32 ulp;
+  * properties: without duo scaling candidate 0 is the identity scaling, i.e. exactly the
+    reference RTN result; the chosen candidate's loss is the minimum; on activations with
+    outlier channels the search beats RTN on the weighted error.
+"""
+import ctypes
+
+import pytest
+import torch
+
+from oracle import awq_oracle as orc
+
+
+def _layer(seed, rows=(96, 40), K=512, dtype=torch.bfloat16, outliers=True):
+    g = torch.Generator().manual_seed(seed)
+    ws = {f"w{i}": (torch.randn(r, K, generator=g) * 0.02).to(dtype) for i, r in enumerate(rows)}
+    amp = torch.ones(K)
+    if outliers:
+        amp[torch.randperm(K, generator=g)[: K // 32]] = 30.0          # salient channels
+    x = (torch.randn(300, K, generator=g) * amp).to(dtype)
+    return ws, x
+
+
+def _ulp_diff(a, b):
+    ia = a.contiguous().view(torch.int32).to(torch.int64)
+    ib = b.contiguous().view(torch.int32).to(torch.int64)
+    return (ia - ib).abs()
+
+
+# ---------------------------------------------------------------- CPU: oracle properties
+def test_oracle_stats_match_fp64():
+    ws, x = _layer(0, dtype=torch.bfloat16)
+    xm, xs = orc.act_stats(x)
+    xd = x.double()
+    assert int(_ulp_diff(xm, (xd.abs().sum(0) / x.shape[0]).float()).max()) <= 1
+    assert int(_ulp_diff(xs, ((xd * xd).sum(0) / x.shape[0]).float()).max()) <= 1
+
+
+def test_oracle_table_formula():
+    ws, x = _layer(1)
+    xm, _ = orc.act_stats(x)
+    wm = orc.weight_mean(list(ws.values()), 128)
+    for duo in (False, True):
+        t = orc.act_scale_table(xm, wm if duo else None, 10)
+        for i in (0, 3, 9):
+            r = i / 10
+            raw = xm.double() ** r
+            if duo:
+                raw = raw / (wm.double() ** (1 - r) + 1e-4)
+            raw = raw.clamp(min=1e-4)
+            want = (raw / (raw.max() * raw.min()).sqrt()).float()
+            assert int(_ulp_diff(t[i], want).max()) <= 1
+    assert torch.equal(orc.act_scale_table(xm, None, 10)[0], torch.ones_like(xm))    # r = 0: identity
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16, torch.float32])
+def test_ratio0_without_duo_is_rtn(dtype):
+    ws, x = _layer(2, dtype=dtype)
+    r = orc.awq_search(list(ws.values()), x, n_grid=8, duo_scaling=False)
+    for w in ws.values():
+        s0 = orc.apply_input_scale(w, r["table"][0])
+        assert torch.equal(s0.view(torch.uint8), w.contiguous().view(torch.uint8))
+    # the weighted error of candidate 0 is the RTN error
+    assert r["losses"][r["best"]] <= r["losses"][0]
+
+
+def test_search_beats_rtn_on_salient_channels():
+    ws, x = _layer(3, rows=(128,), K=1024)
+    r = orc.awq_search(list(ws.values()), x, n_grid=20, duo_scaling=False)
+    assert r["best"] > 0
+    assert r["losses"][r["best"]] < 0.9 * r["losses"][0]
+    # the diagonal loss IS the expected output error for independent channels: check it
+    # against the true output MSE on the calibration set, best candidate vs RTN
+    w = next(iter(ws.values()))
+    xs = x.double()
+    def out_err(res, s):
+        dq = orc.dequantize(res).double() / s.double()
+        return ((xs @ (dq - w.double()).t()) ** 2).mean()
+    rtn = orc.quantize(w, bits=4, group_size=128, symmetric=False)
+    assert out_err(r["results"][0], r["input_scale"]) < out_err(rtn, torch.ones(w.shape[1]))
+
+
+def test_nan_weight_keeps_candidate_0():
+    ws, x = _layer(4)
+    w = next(iter(ws.values())).clone()
+    w[3, 17] = float("nan")
+    r = orc.awq_search([w], x, n_grid=6, duo_scaling=False)
+    assert r["best"] == 0 and bool(torch.isnan(r["losses"]).all())
+
+
+def test_quantizer_validation_without_gpu():
+    from awq_quantizer.quantization import AWQQuantizer
+    q = AWQQuantizer(scale_method="awq", logger_level="ERROR")
+    assert q.duo_scaling and q.search_grid == 20
+    with pytest.raises(ValueError, match="search_grid"):
+        AWQQuantizer(scale_method="awq", search_grid=300, logger_level="ERROR")
+    with pytest.raises(ValueError, match="2-D"):
+        q.quantize_layer_group({"a": torch.zeros(128)})
+    with pytest.raises(ValueError, match="share in_features"):
+        q.quantize_layer_group({"a": torch.zeros(8, 128), "b": torch.zeros(8, 256)})
+    with pytest.raises(ValueError, match="power-of-two"):
+        AWQQuantizer(scale_method="awq", group_size=96, logger_level="ERROR").quantize_layer_group(
+            {"a": torch.zeros(8, 192)})
+    with pytest.raises(ValueError, match="scale_method='awq'"):
+        AWQQuantizer(logger_level="ERROR").quantize_layer_group({"a": torch.zeros(8, 128)})
+
+
+def test_capi_validation_without_gpu():
+    from awq_quantizer import _hip
+    lib = _hip.load_library()
+    P = ctypes.c_void_p(16)
+    assert lib.awq_act_scale_table(P, None, 128, 0, P, None) != 0
+    assert "n_grid" in _hip.last_error()
+    assert lib.awq_act_search_losses(P, 0, 8, 384, 96, 4, 0, P, 4, P, P, 24, None) != 0
+    assert "power-of-two" in _hip.last_error()
+    assert lib.awq_act_search_losses(P, 3, 8, 256, 128, 4, 0, P, 4, P, P, 16, None) != 0
+    assert "bf16 / fp16 / fp32" in _hip.last_error()
+    assert lib.awq_act_search_losses(P, 0, 8, 256, 128, 4, 0, P, 4, P, P, 15, None) != 0
+    assert "part_stride" in _hip.last_error()
+    assert lib.awq_act_stats(P, 0, 0, 128, P, P, P, None) != 0
+
+
+# ---------------------------------------------------------------- GPU: kernels vs oracle
+def _gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return torch.device("cuda", 0)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16, torch.float32])
+@pytest.mark.parametrize("T", [1, 255, 300, 1024])
+def test_gpu_stats_bit_exact(dtype, T):
+    dev = _gpu()
+    from awq_quantizer import _hip
+    g = torch.Generator().manual_seed(T)
+    x = (torch.randn(T, 777, generator=g) * 3).to(dtype)
+    x[0, 5] = float("inf")
+    xm, xs = _hip.act_stats(x.to(dev))
+    om, os_ = orc.act_stats(x)
+    assert torch.equal(xm.cpu().view(torch.int32), om.view(torch.int32))
+    assert torch.equal(xs.cpu().view(torch.int32), os_.view(torch.int32))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16, torch.float32])
+@pytest.mark.parametrize("gs", [8, 64, 128, 512])
+def test_gpu_weight_mean_bit_exact(dtype, gs):
+    dev = _gpu()
+    from awq_quantizer import _hip
+    g = torch.Generator().manual_seed(gs)
+    ws = [(torch.randn(r, 1024, generator=g) * 0.05).to(dtype) for r in (300, 1, 17)]
+    ws[1][0, :gs] = 0.0                                            # an all-zero group
+    got = _hip.weight_mean([w.to(dev) for w in ws], gs).cpu()
+    assert torch.equal(got.view(torch.int32), orc.weight_mean(ws, gs).view(torch.int32))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("duo", [False, True])
+def test_gpu_table_within_one_ulp(duo):
+    dev = _gpu()
+    from awq_quantizer import _hip
+    ws, x = _layer(5, K=2048)
+    xm, _ = orc.act_stats(x)
+    wm = orc.weight_mean(list(ws.values()), 128) if duo else None
+    t = _hip.act_scale_table(xm.to(dev), None if wm is None else wm.to(dev), 20).cpu()
+    o = orc.act_scale_table(xm, wm, 20)
+    d = _ulp_diff(t, o)
+    assert int(d.max()) <= 1 and float((d == 0).float().mean()) > 0.999
+
+
+LOSS_CASES = [(torch.bfloat16, 128, 4, False), (torch.bfloat16, 128, 4, True), (torch.bfloat16, 128, 8, False),
+              (torch.float16, 128, 4, False), (torch.float16, 64, 4, True), (torch.float32, 128, 4, False),
+              (torch.bfloat16, 32, 4, False), (torch.bfloat16, 512, 4, False), (torch.bfloat16, 8, 8, True),
+              (torch.float16, 256, 8, False)]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype,gs,bits,sym", LOSS_CASES, ids=str)
+def test_gpu_losses_bit_exact(dtype, gs, bits, sym):
+    dev = _gpu()
+    from awq_quantizer import _hip
+    ws, x = _layer(6 + gs + bits, rows=(70, 5, 33), K=1024, dtype=dtype)
+    wl = list(ws.values())
+    xm, xs = orc.act_stats(x)
+    table = _hip.act_scale_table(xm.to(dev), _hip.weight_mean([w.to(dev) for w in wl], gs), 12)
+    part = _hip.act_search_losses([w.to(dev) for w in wl], xs.to(dev), table, gs, bits, sym)
+    losses, best, s_best = _hip.act_search_select(part, table)
+    ol, ob, opart = orc.act_search_losses(wl, xs, table.cpu(), gs, bits, sym)
+    assert torch.equal(part.cpu().view(torch.int32), opart.view(torch.int32))
+    assert torch.equal(losses.cpu().view(torch.int64), ol.view(torch.int64))
+    assert int(best.item()) == ob
+    assert torch.equal(s_best.cpu(), table.cpu()[ob])
+
+
+@pytest.mark.gpu
+def test_gpu_losses_special_values():
+    dev = _gpu()
+    from awq_quantizer import _hip
+    ws, x = _layer(9, rows=(40,), K=512)
+    w = ws["w0"].clone()
+    w[1, :128] = 0.0                     # all-zero group
+    w[2, 128:256] = 1e-30                # constant tiny group (bf16 subnormal range)
+    w[3, 5] = 3e38                       # overflows once scaled
+    xm, xs = orc.act_stats(x)
+    table = _hip.act_scale_table(xm.to(dev), None, 8)
+    part = _hip.act_search_losses([w.to(dev)], xs.to(dev), table, 128, 4, False)
+    _, _, opart = orc.act_search_losses([w], xs, table.cpu(), 128, 4, False)
+    a, b = part.cpu(), opart
+    assert torch.equal(torch.isnan(a), torch.isnan(b))
+    assert torch.equal(torch.where(torch.isnan(a), 0, a).view(torch.int32), torch.where(torch.isnan(b), 0, b).view(torch.int32))
+    w[7, 9] = float("nan")
+    part = _hip.act_search_losses([w.to(dev)], xs.to(dev), table, 128, 4, False)
+    losses, best, _ = _hip.act_search_select(part, table)
+    assert int(best.item()) == 0 and bool(torch.isnan(losses.cpu()).all())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16, torch.float32])
+def test_gpu_apply_input_scale_bit_exact(dtype):
+    dev = _gpu()
+    from awq_quantizer import _hip
+    ws, x = _layer(10, rows=(33,), K=640, dtype=dtype)
+    w = ws["w0"]
+    s = torch.rand(640) * 4 + 0.01
+    got = _hip.apply_input_scale(w.to(dev), s.to(dev)).cpu()
+    assert torch.equal(got.view(torch.uint8), orc.apply_input_scale(w, s).view(torch.uint8))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("duo", [False, True])
+@pytest.mark.parametrize("dtype,sym", [(torch.bfloat16, False), (torch.float16, True), (torch.float32, False)])
+def test_gpu_quantize_layer_group_end_to_end(dtype, sym, duo):
+    dev = _gpu()
+    from awq_quantizer.quantization import AWQQuantizer
+    ws, x = _layer(11, rows=(128, 64, 64), K=1024, dtype=dtype)
+    q = AWQQuantizer(bits=4, group_size=128, symmetric=sym, scale_method="awq", duo_scaling=duo, device="cuda",
+                     logger_level="ERROR")
+    out = q.quantize_layer_group(ws, x.to(dev))
+    ref = orc.awq_search(list(ws.values()), x, n_grid=20, symmetric=sym, duo_scaling=duo, table=out["table"].cpu())
+    assert out["best"] == ref["best"]
+    assert torch.equal(out["losses"].cpu().view(torch.int64), ref["losses"].view(torch.int64))
+    assert torch.equal(out["input_scale"].cpu(), ref["input_scale"])
+    for (name, r), rr in zip(out["results"].items(), ref["results"]):
+        rows = ws[name].shape[0]
+        assert torch.equal(r["qweight"].cpu(), orc.pack_rows(rr["tensor_q"].reshape(rows, -1), 4, q.qmin)), name
+        assert torch.equal(r["qzeros"].cpu(), orc.pack_rows(rr["zero_points"], 4, q.qmin)), name
+        assert torch.equal(r["scales"].cpu().view(torch.int16), rr["scales"].view(torch.int16)), name
+        assert r["input_scale"] is out["input_scale"]
+    # unpacked (reference-format) results of the same search
+    out2 = q.quantize_layer_group(ws, x_mean=ref["x_mean"], x_sq=ref["x_sq"], packed=False)
+    for (name, r), rr in zip(out2["results"].items(), ref["results"]):
+        assert torch.equal(r["tensor_q"].cpu(), rr["tensor_q"]), name
+
+
+@pytest.mark.gpu
+def test_gpu_ratio0_is_rtn():
+    dev = _gpu()
+    from awq_quantizer.quantization import AWQQuantizer
+    ws, x = _layer(12, rows=(64,), K=512)
+    q = AWQQuantizer(bits=4, symmetric=False, scale_method="awq", search_grid=1, duo_scaling=False, device="cuda",
+                     logger_level="ERROR")
+    out = q.quantize_layer_group(ws, x.to(dev))
+    rtn = AWQQuantizer(bits=4, symmetric=False, device="cuda", logger_level="ERROR").quantize_packed(ws["w0"])
+    assert out["best"] == 0
+    assert torch.equal(out["results"]["w0"]["qweight"], rtn["qweight"])
+    assert torch.equal(out["input_scale"].cpu(), torch.ones(512))

@@ -52,10 +52,16 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--zero_point", type=str, default="minmax", choices=["none", "minmax", "percentile"],
                    help="Zero point calibration method")
     p.add_argument("--percentile", type=float, default=0.99, help="Percentile for zero point calibration")
-    p.add_argument("--scale_method", type=str, default="mse", choices=["minmax", "mse", "search"],
+    p.add_argument("--scale_method", type=str, default="mse", choices=["minmax", "mse", "search", "awq"],
                    help="Scale calibration method (minmax/mse: round-to-nearest as the reference; "
                         "search: per-group clip search, opt-in extension)")
-    p.add_argument("--search_grid", type=int, default=20, help="scale_method=search: grid size")
+    p.add_argument("--search_grid", type=int, default=20, help="scale_method=search / awq: grid size")
+    p.add_argument("--act_stats", type=str, default=None,
+                   help="scale_method=awq: safetensors file of per-input-channel activation statistics, "
+                        "'<weight name>.x_mean' (mean |x|) and '<weight name>.x_sq' (mean x^2), fp32 [in_features]; "
+                        "weights without statistics are quantized RTN")
+    p.add_argument("--no_duo_scaling", action="store_true",
+                   help="scale_method=awq: channel scales x_mean^r instead of x_mean^r / w_mean^(1-r)")
     p.add_argument("--search_max_shrink", type=float, default=0.5,
                    help="scale_method=search: largest shrink of the group range tried")
     p.add_argument("--per_channel", action="store_true", help="Use per-channel quantization")
@@ -297,7 +303,8 @@ def _pinned_copy(t: torch.Tensor) -> torch.Tensor:
 def quantize_stream(loader, infos: List[TensorInfo], quantizer: AWQQuantizer, device: str, readers: int,
                     lookahead: int, packed: bool, out: Dict, lock: threading.Lock, logger,
                     memory_efficient: bool = False, keep_on_device: bool = False,
-                    batch_bytes: int = 1 << 30, export_autoawq: bool = False) -> None:
+                    batch_bytes: int = 1 << 30, export_autoawq: bool = False,
+                    act_stats: Optional[Dict[str, Tuple[torch.Tensor, torch.Tensor]]] = None) -> None:
     """Quantize `infos` on one GPU as a pipeline over batches of tensors (<= batch_bytes of
     input each):
 
@@ -308,7 +315,11 @@ def quantize_stream(loader, infos: List[TensorInfo], quantizer: AWQQuantizer, de
 
     The reference instead loads every file whole and copies every tensor to the device
     eagerly (main.py:296-307), then quantizes tensor by tensor.  Per-tensor failures are
-    logged and skipped (main.py:387-390)."""
+    logged and skipped (main.py:387-390).
+
+    act_stats (scale_method="awq"): name -> (x_mean, x_sq); those weights take the
+    activation-aware search (AWQQuantizer.quantize_layer_group, one weight per layer group)
+    and carry its "input_scale" in their results."""
     if not (device.startswith("cuda") and torch.cuda.is_available()):
         quantizer.compute_device()   # raises HipUnavailable: no CPU path
     dev = torch.device(device)
@@ -363,9 +374,20 @@ def quantize_stream(loader, infos: List[TensorInfo], quantizer: AWQQuantizer, de
                 ev_in.record(copy_stream)
             compute.wait_event(ev_in)
             with torch.cuda.stream(compute):
-                res = quantizer.quantize_model_device(dev_in, packed=packed)
+                searched = {}
+                for name in [n for n in dev_in if act_stats and n in act_stats]:
+                    try:
+                        xm, xs = act_stats[name]
+                        searched[name] = quantizer.quantize_layer_group(
+                            {name: dev_in[name]}, x_mean=xm, x_sq=xs, packed=packed)["results"][name]
+                    except Exception as e:  # noqa: BLE001  (reference semantics: skip and continue)
+                        if logger:
+                            logger.error(f"Error quantizing tensor: {name}, error: {e}")
+                res = quantizer.quantize_model_device({n: t for n, t in dev_in.items()
+                                                       if not (act_stats and n in act_stats)}, packed=packed)
+                res.update(searched)
                 if export_autoawq:
-                    res = {n: quantizer.export_autoawq(r) for n, r in res.items()}
+                    res = {n: _with_input_scale(quantizer.export_autoawq(r), r) for n, r in res.items()}
                 ev_k = torch.cuda.Event()
                 ev_k.record(compute)
             for name in host:
@@ -401,12 +423,35 @@ def quantize_stream(loader, infos: List[TensorInfo], quantizer: AWQQuantizer, de
             finish(inflight.popleft())
 
 
-def _device_worker(*args) -> None:
+def _with_input_scale(exported: Dict[str, torch.Tensor], packed: Dict[str, torch.Tensor]) -> Dict[str, torch.Tensor]:
+    if "input_scale" in packed:
+        exported["input_scale"] = packed["input_scale"]
+    return exported
+
+
+def load_act_stats(path: str, logger=None) -> Dict[str, Tuple[torch.Tensor, torch.Tensor]]:
+    """--act_stats: '<weight name>.x_mean' / '<weight name>.x_sq' fp32 vectors (safetensors)."""
+    from safetensors.torch import load_file
+    flat = load_file(path)
+    out = {}
+    for key, t in flat.items():
+        if key.endswith(".x_mean"):
+            name = key[: -len(".x_mean")]
+            sq = flat.get(name + ".x_sq")
+            if sq is None:
+                raise ValueError(f"--act_stats: {key} has no matching {name}.x_sq")
+            out[name] = (t.float().reshape(-1), sq.float().reshape(-1))
+    if logger:
+        logger.info(f"Loaded activation statistics for {len(out)} weights from {path}")
+    return out
+
+
+def _device_worker(*args, **kwargs) -> None:
     """Thread body of one device: a failure of the whole device (no GPU, no library) is
     logged; its tensors then count as not quantized."""
     logger, device = args[9], args[3]
     try:
-        quantize_stream(*args)
+        quantize_stream(*args, **kwargs)
     except Exception as e:  # noqa: BLE001
         if logger:
             logger.error(f"Quantization on {device} failed: {e}")
@@ -463,16 +508,29 @@ def main(argv: Optional[List[str]] = None) -> int:
             passthrough = [i for i in index if i.name not in linear]
             ordered = [i for i in ordered if i.name in linear]
             logger.info(f"AutoAWQ export: {len(ordered)} linear weights quantized, {len(passthrough)} copied")
+        act_stats = None
+        if args.act_stats:
+            if args.scale_method != "awq":
+                logger.error("--act_stats needs --scale_method awq")
+                return 1
+            if autoawq:
+                logger.error("--act_stats with --output_format autoawq: the searched input scales must be folded "
+                             "into the ops producing each input first; use --output_format packed or reference "
+                             "(results carry 'input_scale')")
+                return 1
+            act_stats = load_act_stats(args.act_stats, logger)
+        elif args.scale_method == "awq":
+            logger.warning("--scale_method awq without --act_stats: every weight is quantized RTN")
         from . import distributed as D
         rank, local, world = D.env_world()
         if world > 1:   # torchrun: one process per GPU, LPT shard, RCCL gather to rank 0
-            return _main_distributed(args, loader, ordered, logger, start, passthrough)
+            return _main_distributed(args, loader, ordered, logger, start, passthrough, act_stats)
         parts = partition_tensors(ordered, len(devices))
         quantizers = {d: AWQQuantizer(bits=args.bits, group_size=args.group_size, symmetric=args.symmetric,
                                       zero_point=args.zero_point, percentile=args.percentile,
                                       scale_method=args.scale_method, per_channel=args.per_channel, device=d,
                                       search_grid=args.search_grid, search_max_shrink=args.search_max_shrink,
-                                      logger_name=f"awq_quantizer_{d}", logger_level=args.log_level,
+                                      duo_scaling=not args.no_duo_scaling, logger_name=f"awq_quantizer_{d}", logger_level=args.log_level,
                                       logger_to_file=args.log_file is not None, logger_file_path=args.log_file)
                       for d in devices}
         results: Dict[str, Dict[str, torch.Tensor]] = {}
@@ -484,7 +542,8 @@ def main(argv: Optional[List[str]] = None) -> int:
             logger.info(f"Processing {len(part)} tensors on {d}")
             th = threading.Thread(target=_device_worker, args=(loader, part, quantizers[d], d, args.num_workers,
                                                                lookahead, packed, results, lock, logger,
-                                                               args.memory_efficient, False, 1 << 30, autoawq))
+                                                               args.memory_efficient, False, 1 << 30, autoawq),
+                                  kwargs={"act_stats": act_stats})
             th.start()
             threads.append(th)
         for th in threads:
@@ -521,7 +580,7 @@ _SCALARS = ("bits", "group_size", "symmetric", "shape")
 
 
 def _main_distributed(args, loader, ordered: List[TensorInfo], logger, start: float,
-                      passthrough: Optional[List[TensorInfo]] = None) -> int:
+                      passthrough: Optional[List[TensorInfo]] = None, act_stats=None) -> int:
     """torchrun mode: rank r quantizes the tensors an LPT partition by bytes assigns it
     (identical on every rank, no exchange), keeps its results in HBM, then every result
     is sent to rank 0 in one batched point-to-point round over RCCL (xGMI) and rank 0
@@ -538,7 +597,8 @@ def _main_distributed(args, loader, ordered: List[TensorInfo], logger, start: fl
     mine = [i for i in ordered if owner[i.name] == rank]
     q = AWQQuantizer(bits=args.bits, group_size=args.group_size, symmetric=args.symmetric, zero_point=args.zero_point,
                      percentile=args.percentile, scale_method=args.scale_method, per_channel=args.per_channel,
-                     search_grid=args.search_grid, search_max_shrink=args.search_max_shrink, device=device,
+                     search_grid=args.search_grid, search_max_shrink=args.search_max_shrink,
+                     duo_scaling=not args.no_duo_scaling, device=device,
                      logger_name=f"awq_quantizer_{device}", logger_level=args.log_level,
                      logger_to_file=args.log_file is not None, logger_file_path=args.log_file)
     logger.info(f"rank {rank}/{world}: {len(mine)} of {len(ordered)} tensors on {device}")
@@ -546,7 +606,7 @@ def _main_distributed(args, loader, ordered: List[TensorInfo], logger, start: fl
     autoawq = args.output_format == "autoawq"
     quantize_stream(loader, mine, q, device, args.num_workers, max(1, args.prefetch_factor * args.batch_size),
                     args.output_format in ("packed", "autoawq"), results, threading.Lock(), logger,
-                    args.memory_efficient, keep_on_device=True, export_autoawq=autoawq)
+                    args.memory_efficient, keep_on_device=True, export_autoawq=autoawq, act_stats=act_stats)
     # which tensors succeeded, and the shapes rank 0 must receive (tiny metadata)
     meta = {n: {f: (tuple(t.shape), str(t.dtype)) for f, t in r.items() if f not in _SCALARS}
             for n, r in results.items()}

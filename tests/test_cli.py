@@ -231,3 +231,62 @@ def test_bench_two_ranks_gpu():
     # one peer's packed outputs of the 1024x4096 tensor: qweight 2 MiB + qzeros 16 KiB + scales 64 KiB
     assert line["exchange"]["bytes_to_rank0"] == 1024 * 512 * 4 + 1024 * 4 * 4 + 1024 * 32 * 2
     assert line["exchange"]["ms"] > 0
+
+
+def test_act_stats_file_and_flags(tmp_path):
+    from awq_quantizer.main import load_act_stats, main, parse_args
+    a = parse_args(["--model_id", "m", "--output_dir", "o", "--scale_method", "awq", "--act_stats", "s.st",
+                    "--no_duo_scaling"])
+    assert (a.scale_method, a.act_stats, a.no_duo_scaling) == ("awq", "s.st", True)
+    p = str(tmp_path / "stats.safetensors")
+    save_file({"a.weight.x_mean": torch.ones(4), "a.weight.x_sq": torch.full((4,), 2.0),
+               "b.weight.x_mean": torch.ones(4)}, p)
+    with pytest.raises(ValueError, match="x_sq"):
+        load_act_stats(p)
+    save_file({"a.weight.x_mean": torch.ones(4), "a.weight.x_sq": torch.full((4,), 2.0)}, p)
+    st = load_act_stats(p)
+    assert list(st) == ["a.weight"] and torch.equal(st["a.weight"][1], torch.full((4,), 2.0))
+    d = _model_dir(tmp_path, _tensors())
+    # statistics need scale_method awq; awq input scales cannot go into an AutoAWQ checkpoint unfolded
+    assert main(["--model_id", d, "--output_dir", str(tmp_path / "o1"), "--act_stats", p, "--log_level",
+                 "CRITICAL"]) == 1
+    assert main(["--model_id", d, "--output_dir", str(tmp_path / "o2"), "--act_stats", p, "--scale_method", "awq",
+                 "--output_format", "autoawq", "--log_level", "CRITICAL"]) == 1
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not torch.cuda.is_available(), reason="needs the GPU")
+@pytest.mark.parametrize("fmt", ["packed", "reference"])
+def test_main_act_stats_gpu(tmp_path, fmt):
+    """--scale_method awq --act_stats: weights with statistics take the activation-aware
+    search (equal to the oracle's, given the GPU's scale table) and carry input_scale; the
+    others are RTN."""
+    from awq_quantizer import _hip
+    from awq_quantizer.main import main
+    from oracle import awq_oracle as orc
+    tensors = _tensors()
+    d = _model_dir(tmp_path, tensors)
+    g = torch.Generator().manual_seed(3)
+    x = (torch.randn(200, 768, generator=g) * (1 + 20 * (torch.rand(768, generator=g) < 0.05))).bfloat16()
+    xm, xs = orc.act_stats(x)
+    name = "model.layers.0.mlp.fc1.weight"
+    p = str(tmp_path / "stats.safetensors")
+    save_file({name + ".x_mean": xm, name + ".x_sq": xs}, p)
+    out = tmp_path / "out"
+    assert main(["--model_id", d, "--output_dir", str(out), "--scale_method", "awq", "--act_stats", p,
+                 "--output_format", fmt, "--log_level", "ERROR"]) == 0
+    meta = json.load(open(out / "metadata.json"))
+    res = torch.load(str(out / f"model_chunk_{meta['tensor_to_chunk'][name]:04d}.pt"), weights_only=True)[name]
+    w = tensors[name]
+    dev = torch.device("cuda", 0)
+    table = _hip.act_scale_table(xm.to(dev), _hip.weight_mean([w.to(dev)], 128), 20).cpu()
+    ref = orc.awq_search([w], x_mean=xm, x_sq=xs, n_grid=20, symmetric=False, table=table)
+    assert torch.equal(res["input_scale"], ref["input_scale"])
+    rr = ref["results"][0]
+    if fmt == "packed":
+        assert torch.equal(res["qweight"], orc.pack_rows(rr["tensor_q"], 4, 0))
+    else:
+        assert torch.equal(res["tensor_q"], rr["tensor_q"])
+    other = torch.load(str(out / f"model_chunk_{meta['tensor_to_chunk']['model.embed.weight']:04d}.pt"),
+                       weights_only=True)["model.embed.weight"]
+    assert "input_scale" not in other

@@ -20,6 +20,42 @@ namespace {
 
 using namespace refmath;
 
+typedef float f2 __attribute__((ext_vector_type(2)));
+typedef __bf16 b2 __attribute__((ext_vector_type(2)));
+
+// ---- hardware-conversion arithmetic for bf16 / fp16 weights (the streaming kernel's
+// verified identities, awq_fast.hip): same results as refmath, ~4x fewer VALU ----
+__device__ __forceinline__ float opq(float a) {   // value barrier: no f16 narrowing / mixlo fusion
+    asm volatile("" : "+v"(a));
+    return a;
+}
+__device__ __forceinline__ float hw_rn_bf16(float a) {   // v_cvt_pk_bf16_f32: RNE, NaN stays NaN
+    b2 h = __builtin_convertvector((f2){0.0f, a}, b2);
+    return __builtin_bit_cast(float, h);
+}
+__device__ __forceinline__ float hw_rn_f16(float a) { return (float)(_Float16)opq(a); }   // v_cvt_f16_f32: RNE
+
+template <int DT> struct HwFmt;
+template <> struct HwFmt<AWQ_DTYPE_BF16> {
+    __device__ static float rn(float a) { return hw_rn_bf16(a); }
+    // RN(x / s) = RN_bf16(x * RN_f32(1/s)) for bf16 x and bf16 s >= RN_bf16(1e-10)
+    // (exhaustive, oracle/verify_recip.c)
+    __device__ static float quot(float x, float s, float r) {
+        (void)s;
+        return hw_rn_bf16(x * r);
+    }
+};
+template <> struct HwFmt<AWQ_DTYPE_F16> {
+    __device__ static float rn(float a) { return hw_rn_f16(a); }
+    // Markstein-corrected quotient, exact for every fp16 x and positive finite fp16 s
+    // (oracle/verify_recip.c f16m)
+    __device__ static float quot(float x, float s, float r) {
+        const float q0 = x * r;
+        const float e = __builtin_fmaf(-s, q0, x);
+        return hw_rn_f16(__builtin_fmaf(e, r, q0));
+    }
+};
+
 constexpr int kRowBlock = 256;     // rows per canonical fp64 column-sum block
 constexpr int kGroupBlock = 1024;  // groups per canonical fp64 loss block
 
@@ -41,8 +77,8 @@ __device__ __forceinline__ void load8(const void* base, int64_t i, float (&v)[8]
                 v[2 * j] = __uint_as_float((uint32_t)lo << 16);
                 v[2 * j + 1] = __uint_as_float((uint32_t)hi << 16);
             } else {
-                v[2 * j] = sw_f16_to_f32(lo);
-                v[2 * j + 1] = sw_f16_to_f32(hi);
+                v[2 * j] = (float)__builtin_bit_cast(_Float16, lo);      // exact
+                v[2 * j + 1] = (float)__builtin_bit_cast(_Float16, hi);
             }
         }
     }
@@ -193,7 +229,6 @@ __global__ __launch_bounds__(256) void act_loss_kernel(const void* __restrict__ 
                                                        int qmin, int qmax, int sym, const float* __restrict__ table,
                                                        int n_grid, const float* __restrict__ x_sq,
                                                        float* __restrict__ part, int64_t stride) {
-    typedef Traits<DT> T;
     const int64_t G = K / (8 * lpg);
     const int64_t nw = (int64_t)gridDim.x * 4;
     const bool leader = (threadIdx.x & 63) % lpg == 0;
@@ -211,7 +246,8 @@ __global__ __launch_bounds__(256) void act_loss_kernel(const void* __restrict__ 
             int nan = 0;
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
-                ws[j] = T::rn(v[j] * s[j]);
+                if (DT == AWQ_DTYPE_F32) ws[j] = v[j] * s[j];
+                else ws[j] = HwFmt<DT == AWQ_DTYPE_F32 ? AWQ_DTYPE_BF16 : DT>::rn(v[j] * s[j]);
                 nan |= ws[j] != ws[j];
                 mn = ws[j] < mn ? ws[j] : mn;
                 mx = ws[j] > mx ? ws[j] : mx;
@@ -225,15 +261,33 @@ __global__ __launch_bounds__(256) void act_loss_kernel(const void* __restrict__ 
             if (nan) { mn = __builtin_nanf(""); mx = __builtin_nanf(""); }
             float cs, cz;
             group_params<DT>(mn, mx, nan, qmin, qmax, sym, cs, cz);
-            const float sh = sw_f16_to_f32(canon_f16(cs));
             float acc = 0.0f;
+            if (DT != AWQ_DTYPE_F32 && cs > 0.0f && cs < __builtin_inff()) {
+                // finite positive scale (every group but constant fp16 / inf / NaN ones):
+                // RN(w'/s) from the group's reciprocal, hardware RNE conversions; q - z is an
+                // integer |.| <= 510, exact in fp16, so only the product is rounded
+                typedef HwFmt<DT == AWQ_DTYPE_F32 ? AWQ_DTYPE_BF16 : DT> H;
+                const float r = 1.0f / cs;
+                const float sh = (float)(_Float16)cs;
 #pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                const float q = quant1<DT>(ws[j], cs, cz, qmin, qmax);
-                const float hq = sw_f16_to_f32(sw_f32_to_f16(q - cz));
-                const float dq = sw_f16_to_f32(sw_f32_to_f16(hq * sh));
-                const float e = dq / s[j] - v[j];
-                acc = acc + h[j] * (e * e);
+                for (int j = 0; j < 8; ++j) {
+                    const float t = H::quot(ws[j], cs, r);
+                    const float u = sym ? t : H::rn(t + cz);
+                    const float q = __builtin_amdgcn_fmed3f(__builtin_rintf(u), (float)qmin, (float)qmax);
+                    const float dq = hw_rn_f16((q - cz) * sh);
+                    const float e = dq / s[j] - v[j];
+                    acc = acc + h[j] * (e * e);
+                }
+            } else {
+                const float sh = sw_f16_to_f32(canon_f16(cs));
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const float q = quant1<DT>(ws[j], cs, cz, qmin, qmax);
+                    const float hq = sw_f16_to_f32(sw_f32_to_f16(q - cz));
+                    const float dq = sw_f16_to_f32(sw_f32_to_f16(hq * sh));
+                    const float e = dq / s[j] - v[j];
+                    acc = acc + h[j] * (e * e);
+                }
             }
             for (int o = 1; o < lpg; o <<= 1) acc = acc + __shfl_xor(acc, o, 64);
             if (gl.valid && leader) part[(int64_t)i * stride + gl.r * G + gl.g] = acc;

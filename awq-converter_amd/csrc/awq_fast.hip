@@ -57,6 +57,10 @@
 #define AWQ_WIDE_STORE 1
 #endif
 
+#ifndef AWQ_F16_PLAIN
+#define AWQ_F16_PLAIN 1
+#endif
+
 namespace awq {
 namespace {
 
@@ -142,6 +146,10 @@ struct FmtBF16 {
     __device__ static float quot_any(float x, float s, float r) { return quot(x, s, r); }
     // the per-element fast path needs a finite scale (s >= 1e-10 always)
     __device__ static bool fast(float r) { return r > 0.0f; }
+    // quot() is already the plain product
+    static constexpr bool kHasPlain = false;
+    __device__ static bool plain_ok(float s) { (void)s; return false; }
+    __device__ static float quot_plain(float x, float r) { return rn_bf16(x * r); }
 };
 
 // An f32 value the optimizer cannot see through: keeps `RN_f16(a / b)` an f32 IEEE division
@@ -187,6 +195,15 @@ struct FmtF16 {
     }
     // s = 0 (constant group: the fp16 clamp min is 0), inf or NaN -> exact special path
     __device__ static bool fast(float r) { return r > 0.0f && r < __builtin_inff(); }
+    // The plain RN_f16(RN_f32(x * RN_f32(1/s))) misses RN_f16(x / s) only for scales
+    // s >= 14 (302 of the 31 743 positive finite fp16 values, all >= 14; exhaustive,
+    // oracle/verify_recip.c f16s): a tile whose 16 scales are all < 14 (every realistic
+    // weight group: 4-bit s = range/15) takes one multiply per element instead of the
+    // Markstein quotient.  The barrier keeps the product rounded to f32 first (a fused
+    // v_mad_mixlo_f16 would round once).
+    static constexpr bool kHasPlain = AWQ_F16_PLAIN;   // tuning builds: -DAWQ_F16_PLAIN=0
+    __device__ static bool plain_ok(float s) { return s < 14.0f; }
+    __device__ static float quot_plain(float x, float r) { return rn(opaque(x * r)); }
 };
 
 struct GroupParams {
@@ -239,7 +256,7 @@ __device__ __forceinline__ GroupParams params_from_range(float mn, float mx) {
 
 // Quantize the 8 values of one lane (awq.py:245-248) for a group with a positive finite
 // scale and pack them: 4-bit -> w.x, 8-bit -> (w.x, w.y).  Field value = q - qmin.
-template <typename F, int BITS, bool SYM>
+template <typename F, int BITS, bool SYM, bool PLAIN = false>
 __device__ __forceinline__ u2v quant8_fast(const u4 v, float r, float z, float s) {
     constexpr float QR = (float)((1 << BITS) - 1);
     constexpr float HALF = (float)(1 << (BITS - 1));
@@ -248,7 +265,9 @@ __device__ __forceinline__ u2v quant8_fast(const u4 v, float r, float z, float s
     float q[8];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-        const float t0 = F::quot(F::lo(src[i]), s, r), t1 = F::quot(F::hi(src[i]), s, r);   // RN(x / s)
+        // RN(x / s)
+        const float t0 = PLAIN ? F::quot_plain(F::lo(src[i]), r) : F::quot(F::lo(src[i]), s, r);
+        const float t1 = PLAIN ? F::quot_plain(F::hi(src[i]), r) : F::quot(F::hi(src[i]), s, r);
         float u0, u1;
         if (SYM) {
             u0 = t0 + HALF;                                          // rint(t)+8 == rint(t+8)
@@ -563,6 +582,8 @@ __device__ __forceinline__ void compute_tile(const TileCtx& c, const u4 (&v)[4],
     if (SEARCH && n_cand > 1) search_range<F, BITS, SYM>(v, gmn, gmx, gnan, n_grid, n_cand);
     const GroupParams p = params_from_range<F, BITS, SYM>(gmn, gmx);
     const uint32_t my_slot = 4u * (uint32_t)jj + (uint32_t)row;
+    // wave-uniform: every group of the tile admits the plain quotient (F::plain_ok)
+    const bool plain = F::kHasPlain && __builtin_amdgcn_ballot_w64(!F::plain_ok(p.s)) == 0;
 
     // ---- 4. quantize + pack the 4 groups of this row ----
 #pragma unroll
@@ -572,7 +593,8 @@ __device__ __forceinline__ void compute_tile(const TileCtx& c, const u4 (&v)[4],
         const float rj = j == 0 ? row_bcast<0>(p.r) : j == 1 ? row_bcast<1>(p.r) : j == 2 ? row_bcast<2>(p.r) : row_bcast<3>(p.r);
         const float zj = SYM ? 0.0f : (j == 0 ? row_bcast<0>(p.z) : j == 1 ? row_bcast<1>(p.z) : j == 2 ? row_bcast<2>(p.z) : row_bcast<3>(p.z));
         const float sj = j == 0 ? row_bcast<0>(p.s) : j == 1 ? row_bcast<1>(p.s) : j == 2 ? row_bcast<2>(p.s) : row_bcast<3>(p.s);
-        u2v word = quant8_fast<F, BITS, SYM>(v[j], rj, zj, sj);
+        u2v word = plain ? quant8_fast<F, BITS, SYM, true>(v[j], rj, zj, sj)
+                         : quant8_fast<F, BITS, SYM, false>(v[j], rj, zj, sj);
         const bool special = !F::fast(rj);         // scale 0 / inf / NaN
         int32_t q[8];
         if (__builtin_expect(special, 0)) {

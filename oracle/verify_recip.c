@@ -8,8 +8,8 @@
  * reproduces awq.py:245's `tensor / scale` (torch bf16 divide = fp32 divide + RNE)
  * and awq.py:210's `t_min / scale` bit for bit.  Also reports the fp16 analogue
  * (expected to FAIL, which is why fp16 inputs use a true division).
- * Usage: verify_recip [bf16|f16|f16m] -> prints mismatches, exit 0 iff none (bf16, f16m:
- * the fp16 Markstein-corrected quotient below). */
+ * Usage: verify_recip [bf16|f16|f16m|f16s] -> prints mismatches, exit 0 iff none (bf16;
+ * f16m: the fp16 Markstein-corrected quotient; f16s: the fp16 plain product for s < 14). */
 #include <math.h>
 #include <stdio.h>
 #include <stdint.h>
@@ -50,8 +50,37 @@ static int check_f16_markstein(void) {
     return mismatches == 0 ? 0 : 1;
 }
 
+/* fp16 plain product for small scales (csrc/awq_fast.hip FmtF16::quot_plain): for every
+ * finite fp16 x and every positive fp16 s < 14, RN_f16(RN_f32(x * RN_f32(1/s))) equals
+ * RN_f16(x / s).  Also reports the smallest scale for which the plain product fails. */
+static int check_f16_small(void) {
+    long long mismatches = 0, pairs = 0;
+    int first_bad = 0x7C00;
+#pragma omp parallel for reduction(+ : mismatches, pairs) reduction(min : first_bad) schedule(dynamic, 64)
+    for (int si = 1; si < 0x7C00; ++si) {
+        float s = oracle_f16_to_f32((uint16_t)si);
+        volatile float one = 1.0f;
+        float r = one / s;
+        for (int xi = 0; xi < 65536; ++xi) {
+            uint16_t xh = (uint16_t)xi;
+            if ((xh & 0x7C00u) == 0x7C00u) continue;
+            float x = oracle_f16_to_f32(xh);
+            float a = oracle_f16_to_f32(oracle_f32_to_f16(x * r)), b = oracle_f16_to_f32(oracle_f32_to_f16(x / s));
+            if (s < 14.0f) pairs++;
+            if (!(a == b)) {
+                if (s < 14.0f) mismatches++;
+                if (si < first_bad) first_bad = si;
+            }
+        }
+    }
+    printf("f16 small-scale plain product: pairs=%lld mismatches=%lld first_failing_scale=%g\n", pairs,
+           mismatches, oracle_f16_to_f32((uint16_t)first_bad));
+    return mismatches == 0 ? 0 : 1;
+}
+
 int main(int argc, char** argv) {
     if (argc > 1 && strcmp(argv[1], "f16m") == 0) return check_f16_markstein();
+    if (argc > 1 && strcmp(argv[1], "f16s") == 0) return check_f16_small();
     int bf = !(argc > 1 && strcmp(argv[1], "f16") == 0);
     float lo = dec(enc(1e-10f, bf), bf);
     long long mismatches = 0, pairs = 0;

@@ -1,8 +1,10 @@
 """fp16 inputs on the streaming kernel (FmtF16 in csrc/awq_fast.hip) against the oracle.
 
 The reference computes an fp16 tensor's ops in fp16 (torch CPU: fp32 math, RNE to fp16
-per op).  The kernel forms x / s with a Markstein-corrected quotient (exhaustively exact
-over all fp16 pairs: tests/test_oracle_golden.py::test_f16_markstein_division_exhaustive),
+per op).  The kernel forms x / s as the plain x * RN(1/s) in tiles whose scales are all
+< 14 (exhaustively exact there: test_oracle_golden.py::
+test_f16_plain_product_small_scales_exhaustive) and with a Markstein-corrected quotient
+otherwise (exact over all fp16 pairs: test_f16_markstein_division_exhaustive),
 the scale and zero point with IEEE divisions, and routes groups whose scale is 0 (the fp16
 clamp min RN_f16(1e-10) is 0: constant groups), inf or NaN through an exact per-element
 division.  Bar: bit-exact int32 values, fp16 scales, packed words.
@@ -116,3 +118,25 @@ def test_f16_ragged_and_model_packed():
         assert torch.equal(out[name]["qweight"].cpu(), orc.pack_rows(ref["tensor_q"].reshape(rows, -1), 4, 0)), name
     with pytest.raises(ValueError, match="one dtype"):
         PackedBatch({"a": mixed["a"].to(dev), "b": mixed["b"].to(dev)})
+
+
+@pytest.mark.parametrize("bits", [4, 8])
+@pytest.mark.parametrize("sym", [False, True])
+@pytest.mark.parametrize("bound", [100.0, 1.0, 1e-3])
+def test_f16_plain_quotient_tiles_random_bits(bits, sym, bound):
+    """Every fp16 bit pattern of magnitude < bound (subnormals, zeros of both signs): all
+    scales < 14, so every tile takes the plain-product quotient."""
+    g = torch.Generator().manual_seed(int(bound * 1000) + bits)
+    bitsv = torch.randint(0, 0x7C00, (512 * 128,), generator=g, dtype=torch.int32)
+    sign = torch.randint(0, 2, bitsv.shape, generator=g, dtype=torch.int32) << 15
+    x = (bitsv | sign).to(torch.int16).view(torch.float16).reshape(512, 128)
+    x = torch.where(x.abs() < bound, x, x * 0)
+    check(x, bits, sym)
+
+
+@pytest.mark.parametrize("bits", [4, 8])
+def test_f16_mixed_plain_and_markstein_tiles(bits):
+    """Large-range groups (scale >= 14) next to ordinary ones: tiles of both kinds."""
+    x = rand16((256, 1024), 11, 0.05).float()
+    x[::7, :128] *= 30000.0 / x[::7, :128].abs().max()
+    check(x.to(torch.float16), bits, False)

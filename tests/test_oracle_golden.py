@@ -67,3 +67,15 @@ def test_f16_markstein_division_exhaustive():
                          capture_output=True, text=True, timeout=600)
     assert out.returncode == 0, out.stdout + out.stderr
     assert "mismatches=0" in out.stdout
+
+
+def test_f16_plain_product_small_scales_exhaustive():
+    """The fp16 fast path's plain quotient RN(x * RN(1/s)) == RN(x/s) for every fp16 x and
+    every positive fp16 scale s < 14 (1.2e9 pairs); 14 is the first scale where it fails."""
+    import os
+    import subprocess
+    subprocess.run(["make", "-s", "-C", os.path.dirname(orc.__file__), "verify_recip"], check=True)
+    out = subprocess.run([os.path.join(os.path.dirname(orc.__file__), "verify_recip"), "f16s"],
+                         capture_output=True, text=True, timeout=600)
+    assert out.returncode == 0, out.stdout + out.stderr
+    assert "mismatches=0" in out.stdout and "first_failing_scale=14" in out.stdout

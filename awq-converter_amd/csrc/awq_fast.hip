@@ -596,10 +596,12 @@ __device__ __forceinline__ void compute_tile(const TileCtx& c, const u4 (&v)[4],
         u2v word = plain ? quant8_fast<F, BITS, SYM, true>(v[j], rj, zj, sj)
                          : quant8_fast<F, BITS, SYM, false>(v[j], rj, zj, sj);
         const bool special = !F::fast(rj);         // scale 0 / inf / NaN
-        int32_t q[8];
         if (__builtin_expect(special, 0)) {
+            // (q values stay local to the rare branches: a q array live across them made
+            // the compiler zero-initialise 8 registers per j on the common path)
             uint32_t nib[8];
-            quant8_special<F, BITS, SYM>(v[j], zj, sj, nib, q);
+            int32_t qs[8];
+            quant8_special<F, BITS, SYM>(v[j], zj, sj, nib, qs);
             if (BITS == 4) {
                 uint32_t acc = 0;
 #pragma unroll
@@ -627,7 +629,11 @@ __device__ __forceinline__ void compute_tile(const TileCtx& c, const u4 (&v)[4],
 #endif
         }
         if (c.tensor_q) {   // reference-layout int32 tensor_q (parity mode)
-            if (!special) {
+            int32_t q[8];
+            if (__builtin_expect(special, 0)) {
+                uint32_t nib[8];
+                quant8_special<F, BITS, SYM>(v[j], zj, sj, nib, q);
+            } else {
 #pragma unroll
                 for (int i = 0; i < 8; ++i) {
                     const uint32_t wd = (BITS == 4) ? word.x : (i < 4 ? word.x : word.y);

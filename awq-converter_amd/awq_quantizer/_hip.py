@@ -15,7 +15,7 @@ import torch
 
 LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib")
 LIB_PATH = os.path.join(LIB_DIR, "libawq_hip.so")
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 AWQ_DTYPE = {torch.bfloat16: 0, torch.float16: 1, torch.float32: 2, torch.float64: 3}
 
@@ -41,11 +41,11 @@ SIGNATURES = {
     "awq_quantize_groups": (_I32, [_P, _I32, _I64, _I64, _I64, _I32, _I32, _P, _P, _P, _P, _P, _P]),
     "awq_quantize_search": (_I32, [_P, _I32, _I64, _I64, _I64, _I32, _I32, _I32, _I32, _P, _P, _P, _P, _P, _P]),
     "awq_ragged_eligible": (_I32, [_I32, _I64, _I64, _I64]),
-    "awq_plan_ragged": (_I64, [ctypes.POINTER(TensorDesc), _I32, _I32]),
+    "awq_plan_ragged": (_I64, [ctypes.POINTER(TensorDesc), _I32, _I32, _I64]),
     "awq_stream_copy": (_I32, [_P, _P, _I64, _P]),
     "awq_export_autoawq_gemm": (_I32, [_P, _P, _P, _I64, _I64, _I64, _I32, _P, _P, _P, _P]),
     "awq_plan_block_tensor": (_I64, [ctypes.POINTER(TensorDesc), _I32, _I64, _P, _I64]),
-    "awq_quantize_ragged": (_I32, [_P, _I32, _I64, _P, _I32, _I32, _I32, _P]),
+    "awq_quantize_ragged": (_I32, [_P, _I32, _I64, _P, _I32, _I32, _I32, _I64, _P]),
     "awq_dequantize": (_I32, [_P, _P, _P, _I64, _I64, _I64, _P, _P]),
     "awq_dequantize_packed": (_I32, [_P, _P, _P, _I64, _I64, _I64, _I32, _I32, _P, _P]),
     "awq_pack_rows": (_I32, [_P, _I64, _I64, _I32, _I32, _P, _P]),
@@ -153,10 +153,10 @@ def ragged_eligible(dtype: torch.dtype, rows: int, K: int, L: int) -> bool:
     return bool(load_library().awq_ragged_eligible(AWQ_DTYPE[dtype], rows, K, L))
 
 
-def plan_ragged(descs, bits: int) -> int:
+def plan_ragged(descs, bits: int, group_size: int = 128) -> int:
     lib = load_library()
     arr = (TensorDesc * len(descs))(*descs)
-    total = lib.awq_plan_ragged(arr, len(descs), bits)
+    total = lib.awq_plan_ragged(arr, len(descs), bits, group_size)
     if total < 0:
         raise RuntimeError(f"awq_plan_ragged failed: {last_error()}")
     for i in range(len(descs)):
@@ -185,9 +185,9 @@ def plan_block_tensor(descs, total_tiles: int, device: torch.device) -> torch.Te
 
 def quantize_ragged(descs_dev: torch.Tensor, n: int, total_tiles: int, bits: int, symmetric: bool,
                     stream: int, block_tensor: Optional[torch.Tensor] = None,
-                    dtype: torch.dtype = torch.bfloat16) -> None:
+                    dtype: torch.dtype = torch.bfloat16, group_size: int = 128) -> None:
     rc = load_library().awq_quantize_ragged(ptr(descs_dev), n, total_tiles, ptr(block_tensor), AWQ_DTYPE[dtype],
-                                            bits, int(bool(symmetric)), ctypes.c_void_p(stream))
+                                            bits, int(bool(symmetric)), group_size, ctypes.c_void_p(stream))
     check(rc, "awq_quantize_ragged")
 
 

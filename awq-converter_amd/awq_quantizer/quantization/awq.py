@@ -286,7 +286,7 @@ class AWQQuantizer:
 
     def quantize_model_packed(self, tensors: Dict[str, torch.Tensor]) -> Dict[str, Dict[str, torch.Tensor]]:
         """Packed quantization of many tensors: the fast-path-eligible tensors (bf16 or fp16,
-        group_size 128, K % 128 == 0) go into one ragged launch per dtype; the rest are
+        group_size 32/64/128/256, K % group_size == 0) go into one ragged launch per dtype; the rest are
         quantized one by one.  Outputs stay on the device.  Failures are logged and skipped."""
         from .batch import PackedBatch
         self._check_mode()
@@ -312,7 +312,7 @@ class AWQQuantizer:
             for dt in (torch.bfloat16, torch.float16):   # one ragged launch per input dtype
                 part = {k: v.detach().to(dev).contiguous() for k, v in eligible.items() if v.dtype == dt}
                 if part:
-                    batch = PackedBatch(part, bits=self.bits, symmetric=self.symmetric)
+                    batch = PackedBatch(part, bits=self.bits, symmetric=self.symmetric, group_size=self.group_size)
                     batch.run()
                     out.update(batch.results())
         for name, t in rest.items():
@@ -353,7 +353,8 @@ class AWQQuantizer:
             for dt in (torch.bfloat16, torch.float16):
                 part = {k: v.detach().to(dev).contiguous() for k, v in eligible.items() if v.dtype == dt}
                 if part:
-                    batch = PackedBatch(part, bits=self.bits, symmetric=self.symmetric, parity=True, packed=False)
+                    batch = PackedBatch(part, bits=self.bits, symmetric=self.symmetric, parity=True, packed=False,
+                                        group_size=self.group_size)
                     batch.run()
                     for name, r in batch.results().items():
                         out[name] = {"tensor_q": r["tensor_q"], "scales": r["scales"],

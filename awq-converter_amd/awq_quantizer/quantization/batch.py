@@ -17,8 +17,8 @@ from .. import _hip
 class PackedBatch:
     """Device-resident inputs + packed outputs of one ragged launch.
 
-    inputs: name -> contiguous device tensor ([rows, ...] or 1-D), K % 128 == 0, all bf16 or
-    all fp16.
+    inputs: name -> contiguous device tensor ([rows, ...] or 1-D), K % group_size == 0, all
+    bf16 or all fp16; group_size 32, 64, 128 or 256 (one per batch).
     parity=True additionally produces the reference's unpacked int32 tensor_q and
     zero_points (6.05 B/element of output traffic instead of 0.52).
     use_block_table: upload the per-workgroup tensor table (awq_plan_block_tensor; 4 B per
@@ -26,10 +26,11 @@ class PackedBatch:
     """
 
     def __init__(self, inputs: Dict[str, torch.Tensor], bits: int = 4, symmetric: bool = False,
-                 parity: bool = False, packed: bool = True, use_block_table: bool = True):
+                 parity: bool = False, packed: bool = True, use_block_table: bool = True, group_size: int = 128):
         if not inputs:
             raise ValueError("PackedBatch needs at least one tensor")
         self.bits, self.symmetric, self.parity = bits, bool(symmetric), parity
+        self.group_size = gs = int(group_size)
         self.names = list(inputs)
         first = next(iter(inputs.values()))
         dev, self.dtype = first.device, first.dtype
@@ -48,9 +49,10 @@ class PackedBatch:
                                  f"per batch)")
             rows = 1 if x.dim() <= 1 else x.shape[0]
             K = x.numel() // rows
-            if not _hip.ragged_eligible(x.dtype, rows, K, 128):
-                raise ValueError(f"{name}: shape {tuple(x.shape)} is not eligible for a ragged launch")
-            G = K // 128
+            if not _hip.ragged_eligible(x.dtype, rows, K, gs):
+                raise ValueError(f"{name}: shape {tuple(x.shape)} is not eligible for a ragged launch "
+                                 f"(group_size {gs})")
+            G = K // gs
             o = {"scales": torch.empty((rows, G), dtype=torch.float16, device=dev)}
             if packed:
                 o["qweight"] = torch.empty((rows, -(-K // per)), dtype=torch.int32, device=dev)
@@ -62,7 +64,7 @@ class PackedBatch:
             p = lambda k: o[k].data_ptr() if k in o else None
             descs.append(_hip.TensorDesc(x.data_ptr(), rows, K, p("qweight"), p("qzeros"), p("scales"),
                                          p("tensor_q"), p("zero_points"), 0, 0))
-        self.total_tiles = _hip.plan_ragged(descs, bits)
+        self.total_tiles = _hip.plan_ragged(descs, bits, gs)
         self.descs = descs
         self.descs_dev = _hip.descs_to_device(descs, dev)
         self.block_tensor = _hip.plan_block_tensor(descs, self.total_tiles, dev) if use_block_table else None
@@ -71,14 +73,14 @@ class PackedBatch:
     def run(self, stream: Optional[torch.cuda.Stream] = None) -> None:
         s = stream if stream is not None else torch.cuda.current_stream(self.device)
         _hip.quantize_ragged(self.descs_dev, len(self.descs), self.total_tiles, self.bits, self.symmetric,
-                             s.cuda_stream, self.block_tensor, self.dtype)
+                             s.cuda_stream, self.block_tensor, self.dtype, self.group_size)
 
     def results(self) -> Dict[str, Dict[str, torch.Tensor]]:
         res = {}
         for name in self.names:
             o = dict(self.out[name])
             o["bits"] = torch.tensor(self.bits, dtype=torch.int32)
-            o["group_size"] = torch.tensor(128, dtype=torch.int32)
+            o["group_size"] = torch.tensor(self.group_size, dtype=torch.int32)
             o["symmetric"] = torch.tensor(self.symmetric, dtype=torch.bool)
             o["shape"] = torch.tensor(list(self.inputs[name].shape), dtype=torch.int64)
             res[name] = o

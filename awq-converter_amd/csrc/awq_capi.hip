@@ -42,8 +42,7 @@ int check_common(int64_t rows, int64_t K, int64_t group_size, int bits) {
 }
 
 bool fast_eligible(int dtype, int64_t rows, int64_t K, int64_t group_size) {
-    return (dtype == AWQ_DTYPE_BF16 || dtype == AWQ_DTYPE_F16) && group_size == awq::kGroup &&
-           awq::fast_shape_ok(rows, K);
+    return (dtype == AWQ_DTYPE_BF16 || dtype == AWQ_DTYPE_F16) && awq::fast_shape_ok(rows, K, group_size);
 }
 
 }  // namespace
@@ -92,9 +91,9 @@ int awq_quantize_groups(const void* w, int dtype, int64_t rows, int64_t K, int64
         awq_tensor_desc d{};
         d.w = w; d.rows = rows; d.K = K; d.qweight = qweight; d.qzeros = qzeros; d.scales = scales;
         d.tensor_q = tensor_q; d.zeros = zeros; d.tile_begin = 0;
-        d.tile_count = awq::fast_tiles(rows, K, bits);
-        return hip_status(awq::launch_fast(nullptr, nullptr, &d, 1, d.tile_count, dtype, bits, symmetric, s),
-                          "awq fast kernel");
+        d.tile_count = awq::fast_tiles(rows, K, bits, (int)group_size);
+        return hip_status(awq::launch_fast(nullptr, nullptr, &d, 1, d.tile_count, dtype, bits, symmetric,
+                                           (int)group_size, s), "awq fast kernel");
     }
     // generic path: per-group int32 values first, then packing (needs tensor_q / zeros buffers)
     if ((qweight && !tensor_q) || (qzeros && !zeros))
@@ -134,9 +133,9 @@ int awq_quantize_search(const void* w, int dtype, int64_t rows, int64_t K, int64
         awq_tensor_desc d{};
         d.w = w; d.rows = rows; d.K = K; d.qweight = qweight; d.qzeros = qzeros; d.scales = scales;
         d.tensor_q = tensor_q; d.zeros = zeros; d.tile_begin = 0;
-        d.tile_count = awq::fast_tiles(rows, K, bits);
-        return hip_status(awq::launch_fast(nullptr, nullptr, &d, 1, d.tile_count, dtype, bits, symmetric, s, n_grid,
-                                           n_candidates), "awq fast search kernel");
+        d.tile_count = awq::fast_tiles(rows, K, bits, (int)group_size);
+        return hip_status(awq::launch_fast(nullptr, nullptr, &d, 1, d.tile_count, dtype, bits, symmetric,
+                                           (int)group_size, s, n_grid, n_candidates), "awq fast search kernel");
     }
     if ((qweight && !tensor_q) || (qzeros && !zeros))
         return fail(AWQ_EINVAL, "packed outputs of the generic search kernel need the int32 tensor_q/zeros "
@@ -154,14 +153,17 @@ int awq_quantize_search(const void* w, int dtype, int64_t rows, int64_t K, int64
     return AWQ_OK;
 }
 
-int64_t awq_plan_ragged(awq_tensor_desc* descs, int n, int bits) {
+int64_t awq_plan_ragged(awq_tensor_desc* descs, int n, int bits, int64_t group_size) {
     g_err.clear();
     if (n < 0 || (n > 0 && !descs)) return fail(AWQ_EINVAL, "bad descriptor array"), -1;
     if (bits != 4 && bits != 8) return fail(AWQ_EINVAL, "Unsupported bit width: %d. Supported: 4, 8.", bits), -1;
+    if (!awq::fast_group_size(group_size))
+        return fail(AWQ_EUNSUPPORTED, "ragged launches take group_size 32, 64, 128 or 256 (got %lld)",
+                    (long long)group_size), -1;
     int64_t total = 0;
     for (int i = 0; i < n; ++i) {
         awq_tensor_desc& d = descs[i];
-        if (!fast_eligible(AWQ_DTYPE_BF16, d.rows, d.K, awq::kGroup))
+        if (!fast_eligible(AWQ_DTYPE_BF16, d.rows, d.K, group_size))
             return fail(AWQ_EINVAL, "tensor %d (%lld x %lld) is not eligible for a ragged launch", i,
                         (long long)d.rows, (long long)d.K), -1;
         if (!d.w || !aligned(d.w, 16) || (d.qweight && !aligned(d.qweight, 8)) ||
@@ -169,7 +171,7 @@ int64_t awq_plan_ragged(awq_tensor_desc* descs, int n, int bits) {
             (d.qzeros && !aligned(d.qzeros, 4)) || (d.scales && !aligned(d.scales, 2)))
             return fail(AWQ_EINVAL, "tensor %d: null or misaligned pointer", i), -1;
         d.tile_begin = total;
-        d.tile_count = awq::fast_tiles(d.rows, d.K, bits);
+        d.tile_count = awq::fast_tiles(d.rows, d.K, bits, (int)group_size);
         total += d.tile_count;
     }
     return total;
@@ -193,15 +195,19 @@ int64_t awq_plan_block_tensor(const awq_tensor_desc* descs, int n, int64_t total
 }
 
 int awq_quantize_ragged(const awq_tensor_desc* descs_device, int n, int64_t total_tiles,
-                        const int32_t* block_tensor_device, int dtype, int bits, int symmetric, void* stream) {
+                        const int32_t* block_tensor_device, int dtype, int bits, int symmetric, int64_t group_size,
+                        void* stream) {
     g_err.clear();
     if (bits != 4 && bits != 8) return fail(AWQ_EINVAL, "Unsupported bit width: %d. Supported: 4, 8.", bits);
+    if (!awq::fast_group_size(group_size))
+        return fail(AWQ_EUNSUPPORTED, "ragged launches take group_size 32, 64, 128 or 256 (got %lld)",
+                    (long long)group_size);
     if (dtype != AWQ_DTYPE_BF16 && dtype != AWQ_DTYPE_F16)
         return fail(AWQ_EINVAL, "ragged launches take bf16 or fp16 tensors (dtype code %d)", dtype);
     if (n <= 0 || total_tiles <= 0) return AWQ_OK;
     if (!descs_device) return fail(AWQ_EINVAL, "null descriptor array");
     return hip_status(awq::launch_fast(descs_device, block_tensor_device, nullptr, n, total_tiles, dtype, bits,
-                                       symmetric, (hipStream_t)stream), "awq ragged kernel");
+                                       symmetric, (int)group_size, (hipStream_t)stream), "awq ragged kernel");
 }
 
 int awq_dequantize(const int32_t* tensor_q, const uint16_t* scales, const int32_t* zeros, int64_t rows,

@@ -94,19 +94,33 @@ __device__ __forceinline__ int dpp_max(int v) {
     return max(v, __builtin_amdgcn_mov_dpp(v, CTRL, 0xF, 0xF, true));
 }
 
-template <int CTRL>
-__device__ __forceinline__ int row_max16(int v) {   // all 16 lanes of the row get the max
-    (void)CTRL;
-    v = dpp_max<0xB1>(v);    // quad_perm [1,0,3,2]
-    v = dpp_max<0x4E>(v);    // quad_perm [2,3,0,1]
-    v = dpp_max<0x141>(v);   // row_half_mirror
-    return dpp_max<0x140>(v);   // row_mirror
+// max over the L = GS/8 consecutive lanes of a group; every lane of the group gets it.
+// L <= 16: DPP steps inside a row (each folds into one v_max_i32_dpp); L = 32: the group
+// spans two rows, paired by one v_permlane16_swap (gfx950).
+template <int L>
+__device__ __forceinline__ int grp_max(int v) {
+    static_assert(L == 4 || L == 8 || L == 16 || L == 32, "lanes per group");
+    v = dpp_max<0xB1>(v);                  // quad_perm [1,0,3,2]
+    v = dpp_max<0x4E>(v);                  // quad_perm [2,3,0,1]
+    if (L >= 8) v = dpp_max<0x141>(v);     // row_half_mirror
+    if (L >= 16) v = dpp_max<0x140>(v);    // row_mirror
+    if (L >= 32) {                         // rows 0<->1, 2<->3
+        const auto p = __builtin_amdgcn_permlane16_swap((unsigned)v, (unsigned)v, false, false);
+        v = max((int)p[0], (int)p[1]);
+    }
+    return v;
 }
 
-// value of lane (row, J) broadcast to the 16 lanes of each row (DPP row_newbcast:J)
+// value of lane J of each quad broadcast to its quad (DPP quad_perm [J,J,J,J]).  Every lane
+// c of a group with c & 3 == J holds the parameters of the group in load J, so this one
+// DPP hands them to all the group's lanes for any GS.
 template <int J>
-__device__ __forceinline__ float row_bcast(float v) {
-    return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x150 + J, 0xF, 0xF, true));
+__device__ __forceinline__ float quad_bcast(float v) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), J * 0x55, 0xF, 0xF, true));
+}
+
+__device__ __forceinline__ float bcast_j(int j, float v) {   // j is a compile-time constant at every use
+    return j == 0 ? quad_bcast<0>(v) : j == 1 ? quad_bcast<1>(v) : j == 2 ? quad_bcast<2>(v) : quad_bcast<3>(v);
 }
 
 // RN_f32(1/s) for a bf16-valued s: v_rcp_f32 + one Newton step with fma is correctly
@@ -344,21 +358,22 @@ struct TileCtx {
     int32_t* tensor_q;
     int32_t* zeros;
     uint32_t start;      // flat group index of the tile's first group
-    uint32_t ng;         // groups in the tile (<= 16)
+    uint32_t ng;         // groups in the tile (<= S = 2048 / GS)
     uint32_t w0, nw;     // qzeros word range
     uint32_t G, WPR;     // geometry (see awq_internal.h)
     uint32_t r0, g0;     // row / group-in-row of the tile's first group
     uint32_t bytes;      // byte tiles (qzeros written byte-wise) vs word tiles
 };
 
-template <int BITS>
+template <int BITS, int GS>
 __device__ __forceinline__ TileCtx make_ctx(const awq_tensor_desc& d, uint32_t tile) {
-    const TensorGeom g = fast_geom(d.rows, d.K, BITS);
+    constexpr uint32_t S = kTileElems / GS;
+    const TensorGeom g = fast_geom(d.rows, d.K, BITS, GS);
     TileCtx c;
     c.bytes = g.bytes;
     if (g.bytes) {
-        c.start = tile * kSlots;
-        c.ng = min((uint32_t)kSlots, (uint32_t)d.rows * g.G - c.start);
+        c.start = tile * S;
+        c.ng = min(S, (uint32_t)d.rows * g.G - c.start);
         c.r0 = c.start / g.G;
         c.g0 = c.start - c.r0 * g.G;
         c.w0 = 0;
@@ -377,7 +392,7 @@ __device__ __forceinline__ TileCtx make_ctx(const awq_tensor_desc& d, uint32_t t
     }
     c.G = g.G;
     c.WPR = g.WPR;
-    c.wp = (const uint16_t*)d.w + (uint64_t)c.start * kGroup;
+    c.wp = (const uint16_t*)d.w + (uint64_t)c.start * GS;
     c.qweight = d.qweight;
     c.qzeros = d.qzeros;
     c.scales = d.scales;
@@ -387,12 +402,13 @@ __device__ __forceinline__ TileCtx make_ctx(const awq_tensor_desc& d, uint32_t t
 }
 
 // first flat group and group count of a tile (the input byte range it reads)
-template <int BITS>
+template <int BITS, int GS>
 __device__ __forceinline__ void tile_src(int64_t rows, int64_t K, uint32_t tile, uint32_t& start, uint32_t& ng) {
-    const TensorGeom g = fast_geom(rows, K, BITS);
+    constexpr uint32_t S = kTileElems / GS;
+    const TensorGeom g = fast_geom(rows, K, BITS, GS);
     if (g.bytes) {
-        start = tile * kSlots;
-        ng = min((uint32_t)kSlots, (uint32_t)rows * g.G - start);
+        start = tile * S;
+        ng = min(S, (uint32_t)rows * g.G - start);
         return;
     }
     const uint32_t w0 = tile * g.WPT;
@@ -402,29 +418,39 @@ __device__ __forceinline__ void tile_src(int64_t rows, int64_t K, uint32_t tile,
     ng = end - start;
 }
 
-// 4 x 16-B loads per lane: slot 4j + row, 16-B chunk c of the group.  Slots past the tile
-// end fall outside the descriptor's range and read as zero.
+// 4 x 16-B loads per lane: load j covers the tile's bytes [1 KiB j, 1 KiB (j+1)), lane l
+// its 16 B at 16 l — group slot j * (64 / L) + l / L, chunk l % L of that group
+// (L = GS / 8).  Slots past the tile end fall outside the descriptor's range and read as
+// zero.
+template <int GS>
 __device__ __forceinline__ void load_tile(const uint16_t* wp, uint32_t ng, u4 (&v)[4]) {
     const int lane = threadIdx.x & 63;
-    const int row = lane >> 4, ch = lane & 15;
-    const __amdgpu_buffer_rsrc_t rw = rsrc(wp, ng * 256u);
+    const __amdgpu_buffer_rsrc_t rw = rsrc(wp, ng * (2u * GS));
 #pragma unroll
     for (int j = 0; j < 4; ++j)
-        v[j] = __builtin_amdgcn_raw_buffer_load_b128(rw, (uint32_t)((4 * j + row) * 256 + ch * 16), 0, AWQ_LOAD_AUX);
+        v[j] = __builtin_amdgcn_raw_buffer_load_b128(rw, (uint32_t)(j * 1024 + lane * 16), 0, AWQ_LOAD_AUX);
 }
 
-// sum over the 16 lanes of a row, pairwise over adjacent lanes (xor 1, xor 2, then the
-// half-row and row mirrors pair adjacent blocks): every lane ends with the same value, the
-// tree include/awq_hip.h (awq_quantize_search) defines for the clip-search error
+// sum over the L lanes of a group, pairwise over adjacent lanes (xor 1, xor 2, then the
+// half-row and row mirrors and the row swap pair adjacent blocks): every lane ends with the
+// same value, the tree include/awq_hip.h (awq_quantize_search) defines for the clip-search
+// error
 template <int CTRL>
 __device__ __forceinline__ float dpp_add(float v) {
     return v + __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), CTRL, 0xF, 0xF, true));
 }
-__device__ __forceinline__ float row_sum16(float v) {
-    v = dpp_add<0xB1>(v);    // quad_perm [1,0,3,2]
-    v = dpp_add<0x4E>(v);    // quad_perm [2,3,0,1]
-    v = dpp_add<0x141>(v);   // row_half_mirror
-    return dpp_add<0x140>(v);   // row_mirror
+template <int L>
+__device__ __forceinline__ float grp_sum(float v) {
+    v = dpp_add<0xB1>(v);                  // quad_perm [1,0,3,2]
+    v = dpp_add<0x4E>(v);                  // quad_perm [2,3,0,1]
+    if (L >= 8) v = dpp_add<0x141>(v);     // row_half_mirror
+    if (L >= 16) v = dpp_add<0x140>(v);    // row_mirror
+    if (L >= 32) {                         // (row 2k) + (row 2k+1) on both rows
+        const auto p = __builtin_amdgcn_permlane16_swap(__builtin_bit_cast(unsigned, v), __builtin_bit_cast(unsigned, v),
+                                                        false, false);
+        v = __builtin_bit_cast(float, (unsigned)p[0]) + __builtin_bit_cast(float, (unsigned)p[1]);
+    }
+    return v;
 }
 
 // Squared error of this lane's 8-element chunk of a group for one candidate (r, z, s) —
@@ -458,9 +484,9 @@ __device__ __forceinline__ float chunk_err(const u4 v, float r, float z, float s
 }
 
 // Opt-in clip search (include/awq_hip.h awq_quantize_search) inside the streaming kernel:
-// candidates alpha_i = (n_grid - i) / n_grid shrink [mn, mx]; lane (row, ch) evaluates the
-// candidate's parameters for its parameter group 4(ch&3) + row, the 16 lanes of the row
-// score each of the row's 4 groups (8 elements per lane, row_sum16), and the smallest
+// candidates alpha_i = (n_grid - i) / n_grid shrink [mn, mx]; lane (grp, ch) evaluates the
+// candidate's parameters for its parameter group (the one in load ch & 3), the L lanes of a
+// group score each of its 4 loads' groups (8 elements per lane, grp_sum), and the smallest
 // error (ties: the earlier candidate; NaN never wins) picks the group's final [mn, mx].
 // RN(v * alpha) as torch evaluates it (fp32 product, then one rounding to the dtype); the
 // barrier stops the fp16 product from becoming a single-rounding v_mad_mixlo_f16
@@ -469,7 +495,7 @@ __device__ __forceinline__ float shrink(float v, float al) {
     return F::rn(opaque(v * al));
 }
 
-template <typename F, int BITS, bool SYM>
+template <typename F, int BITS, bool SYM, int GS>
 __device__ __forceinline__ void search_range(const u4 (&v)[4], float& gmn, float& gmx, bool gnan, int n_grid,
                                           int n_cand) {
     const int jj = threadIdx.x & 3;
@@ -481,15 +507,15 @@ __device__ __forceinline__ void search_range(const u4 (&v)[4], float& gmn, float
         const float csh = F::dq_scale(cp.s);
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            const float rj = j == 0 ? row_bcast<0>(cp.r) : j == 1 ? row_bcast<1>(cp.r) : j == 2 ? row_bcast<2>(cp.r) : row_bcast<3>(cp.r);
-            const float zj = SYM ? 0.0f : (j == 0 ? row_bcast<0>(cp.z) : j == 1 ? row_bcast<1>(cp.z) : j == 2 ? row_bcast<2>(cp.z) : row_bcast<3>(cp.z));
-            const float sj = j == 0 ? row_bcast<0>(cp.s) : j == 1 ? row_bcast<1>(cp.s) : j == 2 ? row_bcast<2>(cp.s) : row_bcast<3>(cp.s);
-            const float hj = j == 0 ? row_bcast<0>(csh) : j == 1 ? row_bcast<1>(csh) : j == 2 ? row_bcast<2>(csh) : row_bcast<3>(csh);
+            const float rj = bcast_j(j, cp.r);
+            const float zj = SYM ? 0.0f : bcast_j(j, cp.z);
+            const float sj = bcast_j(j, cp.s);
+            const float hj = bcast_j(j, csh);
             const bool special = !F::fast(rj);
             float e;
             if (__builtin_expect(__ballot(special) != 0, 0)) e = chunk_err<F, BITS, SYM>(v[j], rj, zj, sj, hj, special);
             else e = chunk_err<F, BITS, SYM>(v[j], rj, zj, sj, hj, false);
-            e = row_sum16(e);
+            e = grp_sum<GS / 8>(e);
             if (j == jj && e < best) {
                 best = e;
                 bi = i;
@@ -503,14 +529,18 @@ __device__ __forceinline__ void search_range(const u4 (&v)[4], float& gmn, float
     }
 }
 
-template <typename F, int BITS, bool SYM, bool SEARCH>
+template <typename F, int BITS, bool SYM, bool SEARCH, int GS>
 __device__ __forceinline__ void compute_tile(const TileCtx& c, const u4 (&v)[4], uint32_t* zw, uint32_t* qstage,
                                              int n_grid, int n_cand) {
     constexpr int QMIN = SYM ? -(1 << (BITS - 1)) : 0;
     constexpr uint32_t C = 32u / BITS;   // groups per qzeros word
+    constexpr int L = GS / 8;            // lanes per group (8 elements = 16 B per lane)
+    constexpr int GPJ = 64 / L;          // groups per load instruction
+    constexpr uint32_t S = 4 * GPJ;      // group slots per tile
+    constexpr uint32_t WPG = GS * BITS / 32;   // qweight words per group
     const int lane = threadIdx.x & 63;
-    const int row = lane >> 4;           // lane-row: 16 lanes = one group
-    const int ch = lane & 15;            // 16-B chunk of the group
+    const int grp = lane / L;            // group of this lane inside each load
+    const int ch = lane % L;             // 16-B chunk of the group
     const uint32_t ng = c.ng;
 #ifdef AWQ_TRIVIAL_COMPUTE
     // timing-only build (scripts/kbench.py): same loads and stores, no arithmetic
@@ -518,14 +548,14 @@ __device__ __forceinline__ void compute_tile(const TileCtx& c, const u4 (&v)[4],
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             const uint32_t word = v[j].x ^ v[j].y ^ v[j].z ^ v[j].w;
-            __amdgpu_buffer_rsrc_t rq = rsrc(c.qweight + (uint64_t)c.start * 16, ng * 64u);
-            __builtin_amdgcn_raw_buffer_store_b32(word, rq, (uint32_t)(((4 * j + row) * 16 + ch) * 4), 0, AWQ_STORE_AUX);
+            __amdgpu_buffer_rsrc_t rq = rsrc(c.qweight + (uint64_t)c.start * WPG, ng * WPG * 4u);
+            __builtin_amdgcn_raw_buffer_store_b32(word, rq, (uint32_t)((64 * j + lane) * 4), 0, AWQ_STORE_AUX);
         }
     }
 #ifndef AWQ_TRIVIAL_NOSMALL
     if (ch < 4 && c.scales) {
         __amdgpu_buffer_rsrc_t rs = rsrc(c.scales + c.start, ng * 2u);
-        __builtin_amdgcn_raw_buffer_store_b16((uint16_t)v[0].x, rs, (4u * ch + row) * 2u, 0, AWQ_SMALL_AUX);
+        __builtin_amdgcn_raw_buffer_store_b16((uint16_t)v[0].x, rs, (GPJ * ch + grp) * 2u, 0, AWQ_SMALL_AUX);
     }
     if (c.qzeros && (uint32_t)lane < c.nw) {
         __amdgpu_buffer_rsrc_t rz = rsrc(c.qzeros + c.w0, c.nw * 4u);
@@ -535,13 +565,13 @@ __device__ __forceinline__ void compute_tile(const TileCtx& c, const u4 (&v)[4],
     return;
 #endif
 
-    // ---- 1. group min/max (awq.py:192-193) of the 4 groups this row holds, from the raw
-    //         16-bit patterns: the SIGNED int16 max is the float max whenever the group has
-    //         a value with the sign bit clear, and the UNSIGNED max is the float min (most
-    //         negative) whenever it has one with the sign bit set; NaNs land beyond F::kNanS /
-    //         F::kNanU.  Single-signed groups (rare in weights; LayerNorm gammas) take an
-    //         extra unsigned-min reduction in a wave-uniform branch.  Row reductions: DPP-
-    //         fused v_max_i32 over the 16 lanes of the group ----
+    // ---- 1. group min/max (awq.py:192-193) of the 4 groups this lane's group-lanes hold,
+    //         from the raw 16-bit patterns: the SIGNED int16 max is the float max whenever
+    //         the group has a value with the sign bit clear, and the UNSIGNED max is the
+    //         float min (most negative) whenever it has one with the sign bit set; NaNs land
+    //         beyond F::kNanS / F::kNanU.  Single-signed groups (rare in weights; LayerNorm
+    //         gammas) take an extra unsigned-min reduction in a wave-uniform branch.
+    //         Reductions over the group's L lanes: DPP-fused v_max_i32 (grp_max) ----
     int smx[4], umx[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -552,8 +582,8 @@ __device__ __forceinline__ void compute_tile(const TileCtx& c, const u4 (&v)[4],
                                                 __builtin_elementwise_max(as_s2(x2), as_s2(x3)));
         const us2 um = __builtin_elementwise_max(__builtin_elementwise_max(as_us2(x0), as_us2(x1)),
                                                  __builtin_elementwise_max(as_us2(x2), as_us2(x3)));
-        smx[j] = row_max16<0>(max((int)sm.x, (int)sm.y));
-        umx[j] = row_max16<0>(max((int)um.x, (int)um.y));
+        smx[j] = grp_max<L>(max((int)sm.x, (int)sm.y));
+        umx[j] = grp_max<L>(max((int)um.x, (int)um.y));
     }
     int umn[4] = {0, 0, 0, 0};
     bool one_signed = false;
@@ -567,10 +597,12 @@ __device__ __forceinline__ void compute_tile(const TileCtx& c, const u4 (&v)[4],
             const us2 a = ones - as_us2(x0), b = ones - as_us2(x1);
             const us2 c = ones - as_us2(x2), e = ones - as_us2(x3);
             const us2 m = __builtin_elementwise_max(__builtin_elementwise_max(a, b), __builtin_elementwise_max(c, e));
-            umn[j] = 0xFFFF - row_max16<0>(max((int)m.x, (int)m.y));
+            umn[j] = 0xFFFF - grp_max<L>(max((int)m.x, (int)m.y));
         }
     }
-    // ---- 2. scale / zero point: lane (row, ch) computes group 4*(ch&3) + row ----
+    // ---- 2. scale / zero point: lane (grp, ch) computes the group of load ch & 3, i.e.
+    //         slot GPJ * (ch & 3) + grp (the L / 4 lanes of a group with equal ch & 3 do the
+    //         same work; for GS 32 every lane owns exactly one of the 64 slots) ----
     const int jj = ch & 3;
     int ssel = smx[0], usel = umx[0], nsel = umn[0];
 #pragma unroll
@@ -579,20 +611,20 @@ __device__ __forceinline__ void compute_tile(const TileCtx& c, const u4 (&v)[4],
     float gmn, gmx;
     bool gnan;
     group_range<F, SYM>(ssel, usel, nsel, gmn, gmx, gnan);
-    if (SEARCH && n_cand > 1) search_range<F, BITS, SYM>(v, gmn, gmx, gnan, n_grid, n_cand);
+    if (SEARCH && n_cand > 1) search_range<F, BITS, SYM, GS>(v, gmn, gmx, gnan, n_grid, n_cand);
     const GroupParams p = params_from_range<F, BITS, SYM>(gmn, gmx);
-    const uint32_t my_slot = 4u * (uint32_t)jj + (uint32_t)row;
+    const uint32_t my_slot = GPJ * (uint32_t)jj + (uint32_t)grp;
     // wave-uniform: every group of the tile admits the plain quotient (F::plain_ok)
     const bool plain = F::kHasPlain && __builtin_amdgcn_ballot_w64(!F::plain_ok(p.s)) == 0;
 
-    // ---- 4. quantize + pack the 4 groups of this row ----
+    // ---- 4. quantize + pack the 4 groups of this lane ----
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-        const int slot = 4 * j + row;
-        // this group's r, z from lane (row, j), broadcast just in time (short live ranges)
-        const float rj = j == 0 ? row_bcast<0>(p.r) : j == 1 ? row_bcast<1>(p.r) : j == 2 ? row_bcast<2>(p.r) : row_bcast<3>(p.r);
-        const float zj = SYM ? 0.0f : (j == 0 ? row_bcast<0>(p.z) : j == 1 ? row_bcast<1>(p.z) : j == 2 ? row_bcast<2>(p.z) : row_bcast<3>(p.z));
-        const float sj = j == 0 ? row_bcast<0>(p.s) : j == 1 ? row_bcast<1>(p.s) : j == 2 ? row_bcast<2>(p.s) : row_bcast<3>(p.s);
+        // this group's r, z, s from the quad lane with ch & 3 == j, broadcast just in time
+        // (short live ranges)
+        const float rj = bcast_j(j, p.r);
+        const float zj = SYM ? 0.0f : bcast_j(j, p.z);
+        const float sj = bcast_j(j, p.s);
         u2v word = plain ? quant8_fast<F, BITS, SYM, true>(v[j], rj, zj, sj)
                          : quant8_fast<F, BITS, SYM, false>(v[j], rj, zj, sj);
         const bool special = !F::fast(rj);         // scale 0 / inf / NaN
@@ -612,20 +644,19 @@ __device__ __forceinline__ void compute_tile(const TileCtx& c, const u4 (&v)[4],
                 word.y = nib[4] | (nib[5] << 8) | (nib[6] << 16) | (nib[7] << 24);
             }
         }
+        // this lane's 8 elements are tile elements 512 j + 8 lane: packed word 64 j + lane
         if (c.qweight) {
 #if AWQ_WIDE_STORE
-            // staged in the wave's LDS block in output order (lanes of one j write 64
+            // staged in the wave's LDS block in output order (the lanes of one j write 64
             // consecutive words), stored below as one 16-B piece per lane
-            if (BITS == 4) qstage[slot * 16 + ch] = word.x;
-            else *(u2v*)(qstage + slot * 32 + 2 * ch) = word;
+            if (BITS == 4) qstage[64 * j + lane] = word.x;
+            else *(u2v*)(qstage + 128 * j + 2 * lane) = word;
 #else
-            if (BITS == 4) {
-                __amdgpu_buffer_rsrc_t rq = rsrc(c.qweight + (uint64_t)c.start * 16, ng * 64u);
-                __builtin_amdgcn_raw_buffer_store_b32(word.x, rq, (uint32_t)((slot * 16 + ch) * 4), 0, AWQ_STORE_AUX);
-            } else {
-                __amdgpu_buffer_rsrc_t rq = rsrc(c.qweight + (uint64_t)c.start * 32, ng * 128u);
-                __builtin_amdgcn_raw_buffer_store_b64(word, rq, (uint32_t)((slot * 32 + 2 * ch) * 4), 0, AWQ_STORE_AUX);
-            }
+            __amdgpu_buffer_rsrc_t rq = rsrc(c.qweight + (uint64_t)c.start * WPG, ng * WPG * 4u);
+            if (BITS == 4)
+                __builtin_amdgcn_raw_buffer_store_b32(word.x, rq, (uint32_t)((64 * j + lane) * 4), 0, AWQ_STORE_AUX);
+            else
+                __builtin_amdgcn_raw_buffer_store_b64(word, rq, (uint32_t)((64 * j + lane) * 8), 0, AWQ_STORE_AUX);
 #endif
         }
         if (c.tensor_q) {   // reference-layout int32 tensor_q (parity mode)
@@ -641,25 +672,25 @@ __device__ __forceinline__ void compute_tile(const TileCtx& c, const u4 (&v)[4],
                     q[i] = (int32_t)((wd >> sh) & ((1u << BITS) - 1u)) + QMIN;
                 }
             }
-            __amdgpu_buffer_rsrc_t rt = rsrc(c.tensor_q + (uint64_t)c.start * kGroup, ng * 512u);
+            __amdgpu_buffer_rsrc_t rt = rsrc(c.tensor_q + (uint64_t)c.start * GS, ng * (GS * 4u));
             u4 lo = {(uint32_t)q[0], (uint32_t)q[1], (uint32_t)q[2], (uint32_t)q[3]};
             u4 hi = {(uint32_t)q[4], (uint32_t)q[5], (uint32_t)q[6], (uint32_t)q[7]};
-            __builtin_amdgcn_raw_buffer_store_b128(lo, rt, (uint32_t)((slot * kGroup + 8 * ch) * 4), 0, AWQ_STORE_AUX);
-            __builtin_amdgcn_raw_buffer_store_b128(hi, rt, (uint32_t)((slot * kGroup + 8 * ch) * 4 + 16), 0, AWQ_STORE_AUX);
+            __builtin_amdgcn_raw_buffer_store_b128(lo, rt, (uint32_t)((512 * j + 8 * lane) * 4), 0, AWQ_STORE_AUX);
+            __builtin_amdgcn_raw_buffer_store_b128(hi, rt, (uint32_t)((512 * j + 8 * lane) * 4 + 16), 0, AWQ_STORE_AUX);
         }
     }
 #if AWQ_WIDE_STORE
     if (c.qweight) {   // 4-bit: 1 KiB per tile = one dwordx4 per lane; 8-bit: 2 KiB, two
-        const int lane_ = threadIdx.x & 63;
-        __amdgpu_buffer_rsrc_t rq = rsrc(c.qweight + (uint64_t)c.start * (BITS == 4 ? 16 : 32), ng * (BITS == 4 ? 64u : 128u));
+        __amdgpu_buffer_rsrc_t rq = rsrc(c.qweight + (uint64_t)c.start * WPG, ng * WPG * 4u);
 #pragma unroll
         for (int h = 0; h < (BITS == 4 ? 1 : 2); ++h) {
-            const u4 w4 = *(const u4*)(qstage + h * 256 + lane_ * 4);
-            __builtin_amdgcn_raw_buffer_store_b128(w4, rq, (uint32_t)(h * 1024 + lane_ * 16), 0, AWQ_STORE_AUX);
+            const u4 w4 = *(const u4*)(qstage + h * 256 + lane * 4);
+            __builtin_amdgcn_raw_buffer_store_b128(w4, rq, (uint32_t)(h * 1024 + lane * 16), 0, AWQ_STORE_AUX);
         }
     }
 #endif
-    // ---- 5. per-group scalars out (after the data registers are dead): lanes ch < 4 hold slots 0..15 (one store each) ----
+    // ---- 5. per-group scalars out (after the data registers are dead): lanes ch < 4 hold
+    //         the S slots (one store each) ----
     if (ch < 4) {
         if (c.scales) {
             __amdgpu_buffer_rsrc_t rs = rsrc(c.scales + c.start, ng * 2u);
@@ -675,7 +706,7 @@ __device__ __forceinline__ void compute_tile(const TileCtx& c, const u4 (&v)[4],
     // lane per qzeros byte stores it (plus the zero pad bytes ending its row's last word)
     if (c.qzeros && c.bytes) {
         constexpr uint32_t GPB = BITS == 4 ? 2u : 1u;        // groups per byte
-        if (lane < 16) zw[lane] = 0u;
+        if ((uint32_t)lane < S) zw[lane] = 0u;
         if (ch < 4 && my_slot < ng) {
             uint32_t zn = __builtin_isnan(p.z) ? (uint32_t)(0u - (uint32_t)QMIN) : (uint32_t)((int)p.z - QMIN);
             zn &= (1u << BITS) - 1u;
@@ -701,7 +732,7 @@ __device__ __forceinline__ void compute_tile(const TileCtx& c, const u4 (&v)[4],
     }
     // qzeros, word tiles: each slot's field OR-ed into its word (wave-private LDS), then stored
     if (c.qzeros && !c.bytes) {
-        if (lane < 16) zw[lane] = 0u;
+        if ((uint32_t)lane < S) zw[lane] = 0u;
         if (ch < 4 && my_slot < ng) {
             uint32_t g = c.g0 + my_slot, r = c.r0;
             if (g >= c.G) {                 // slot lies in a later row of the tile
@@ -750,11 +781,11 @@ __device__ uint64_t* g_trace = nullptr;
 // One wave per tile.  The grid normally covers every tile once (launch_fast); a smaller
 // grid (AWQ_HIP_MAX_BLOCKS, tests) makes each wave walk tiles t, t + nwaves, ... with a
 // tensor cursor.
-template <typename F, int BITS, bool SYM, bool SEARCH>
+template <typename F, int BITS, bool SYM, bool SEARCH, int GS>
 __global__ __launch_bounds__(64 * kWavesPerBlock, SEARCH ? 4 : AWQ_MIN_WAVES) void awq_fast_kernel(
     const awq_tensor_desc* __restrict__ descs, const int32_t* __restrict__ block_tensor, awq_tensor_desc single,
     int n, int64_t total_tiles, int n_grid, int n_cand) {
-    __shared__ uint32_t zwords[kWavesPerBlock][kSlots];
+    __shared__ uint32_t zwords[kWavesPerBlock][kTileElems / GS];
 #if AWQ_WIDE_STORE
     __shared__ __attribute__((aligned(16))) uint32_t qstage_all[kWavesPerBlock][BITS == 4 ? 256 : 512];
 #endif
@@ -800,9 +831,9 @@ __global__ __launch_bounds__(64 * kWavesPerBlock, SEARCH ? 4 : AWQ_MIN_WAVES) vo
         // rest of the tile context (row / group divisions) is computed
         const uint32_t tile = (uint32_t)(t - d.tile_begin);
         uint32_t st, ng;
-        tile_src<BITS>(d.rows, d.K, tile, st, ng);
+        tile_src<BITS, GS>(d.rows, d.K, tile, st, ng);
         u4 va[4];
-        load_tile((const uint16_t*)d.w + (uint64_t)st * kGroup, ng, va);
+        load_tile<GS>((const uint16_t*)d.w + (uint64_t)st * GS, ng, va);
 #ifdef AWQ_TRACE
         if (tr1 == 0) {
             tr1 = __builtin_amdgcn_s_memrealtime();
@@ -810,7 +841,7 @@ __global__ __launch_bounds__(64 * kWavesPerBlock, SEARCH ? 4 : AWQ_MIN_WAVES) vo
             tr2 = __builtin_amdgcn_s_memrealtime();
         }
 #endif
-        compute_tile<F, BITS, SYM, SEARCH>(make_ctx<BITS>(d, tile), va, zw, qs, n_grid, n_cand);
+        compute_tile<F, BITS, SYM, SEARCH, GS>(make_ctx<BITS, GS>(d, tile), va, zw, qs, n_grid, n_cand);
     }
 #ifdef AWQ_TRACE
     if (g_trace != nullptr && (threadIdx.x & 63) == 0) {
@@ -840,7 +871,7 @@ __global__ void awq_selftest_recip_kernel(unsigned long long* mismatches) {
 
 hipError_t launch_fast(const awq_tensor_desc* descs_dev, const int32_t* block_tensor,
                        const awq_tensor_desc* single, int n, int64_t total_tiles, int dtype, int bits,
-                       int symmetric, hipStream_t stream, int n_grid, int n_cand) {
+                       int symmetric, int group_size, hipStream_t stream, int n_grid, int n_cand) {
     if (total_tiles <= 0) return hipSuccess;
     // one wave per tile (tuning / tests: AWQ_HIP_TILES_PER_WAVE = tiles per wave,
     // AWQ_HIP_MAX_BLOCKS = grid cap; either makes waves walk several tiles)
@@ -861,15 +892,22 @@ hipError_t launch_fast(const awq_tensor_desc* descs_dev, const int32_t* block_te
     // the table describes the one-tile-per-wave grid only
     const int32_t* bt = (tpw == 1 && blocks * per_block >= total_tiles) ? block_tensor : nullptr;
     const dim3 grid((unsigned)blocks), block(64 * kWavesPerBlock);
-#define AWQ_LAUNCH(Fm, B, S)                                                                               \
+#define AWQ_LAUNCH_GS(Fm, B, S, G)                                                                         \
     do {                                                                                                   \
         if (n_cand > 1)                                                                                    \
-            hipLaunchKernelGGL((awq_fast_kernel<Fm, B, S, true>), grid, block, 0, stream, descs_dev, bt, one, n, \
-                               total_tiles, n_grid, n_cand);                                               \
+            hipLaunchKernelGGL((awq_fast_kernel<Fm, B, S, true, G>), grid, block, 0, stream, descs_dev, bt, one, \
+                               n, total_tiles, n_grid, n_cand);                                            \
         else                                                                                               \
-            hipLaunchKernelGGL((awq_fast_kernel<Fm, B, S, false>), grid, block, 0, stream, descs_dev, bt, one, \
-                               n, total_tiles, 1, 0);                                                      \
+            hipLaunchKernelGGL((awq_fast_kernel<Fm, B, S, false, G>), grid, block, 0, stream, descs_dev, bt,    \
+                               one, n, total_tiles, 1, 0);                                                 \
     } while (0)
+#define AWQ_LAUNCH(Fm, B, S)                                   \
+    switch (group_size) {                                      \
+    case 32: AWQ_LAUNCH_GS(Fm, B, S, 32); break;               \
+    case 64: AWQ_LAUNCH_GS(Fm, B, S, 64); break;               \
+    case 256: AWQ_LAUNCH_GS(Fm, B, S, 256); break;             \
+    default: AWQ_LAUNCH_GS(Fm, B, S, 128); break;              \
+    }
 #define AWQ_LAUNCH_FMT(Fm)                          \
     switch ((bits == 8 ? 2 : 0) + (symmetric ? 1 : 0)) { \
     case 0: AWQ_LAUNCH(Fm, 4, false); break;        \
@@ -877,6 +915,7 @@ hipError_t launch_fast(const awq_tensor_desc* descs_dev, const int32_t* block_te
     case 2: AWQ_LAUNCH(Fm, 8, false); break;        \
     default: AWQ_LAUNCH(Fm, 8, true); break;        \
     }
+    if (!fast_group_size(group_size)) return hipErrorInvalidValue;
     if (dtype == AWQ_DTYPE_F16) {
         AWQ_LAUNCH_FMT(FmtF16)
     } else {
@@ -884,6 +923,7 @@ hipError_t launch_fast(const awq_tensor_desc* descs_dev, const int32_t* block_te
     }
 #undef AWQ_LAUNCH_FMT
 #undef AWQ_LAUNCH
+#undef AWQ_LAUNCH_GS
     return hipPeekAtLastError();
 }
 

@@ -9,28 +9,37 @@
 namespace awq {
 
 // ---------------------------------------------------------------------------
-// Fast-kernel tile geometry (bf16, group_size 128, K % 128 == 0).
+// Fast-kernel tile geometry (bf16 / fp16, group_size GS in {32, 64, 128, 256}, K % GS == 0).
 //
-// A tensor [R, K] is a flat sequence of R*G groups of 128 bf16 (256 B).  qzeros packs
-// C = 32/bits consecutive groups of ONE row per word, so a row has WPR = ceil(G/C)
-// words.  Two tilings (a wave-tile is <= 16 groups = one contiguous byte range):
+// A tensor [R, K] is a flat sequence of R*G groups of GS elements (G = K / GS).  A
+// wave-tile is 2048 elements = 4 KiB of input = S = 2048 / GS group slots (64, 32, 16, 8).
+// qzeros packs C = 32/bits consecutive groups of ONE row per word, so a row has
+// WPR = ceil(G/C) words.  Two tilings (a wave-tile is <= S groups = one contiguous byte
+// range):
 //   * byte tiles ("bytes" = 1): when a row's zero points fill whole BYTES of qzeros
-//     (8-bit, or 4-bit with G even), tiles are 16 consecutive flat groups and every
+//     (8-bit, or 4-bit with G even), tiles are S consecutive flat groups and every
 //     tile writes the qzeros bytes of its own groups (byte stores, pad bytes of a row's
 //     last word written by the tile holding the row's last group) — full tiles for any
-//     such G (K = 768: 16 groups per tile, not 12);
+//     such G (GS 128, K = 768: 16 groups per tile, not 12);
 //   * word tiles (4-bit with G odd): a tile is WPT consecutive qzeros words, so every
-//     word is produced inside one tile:  WPR == 1 (G <= C): WPT = 16 / G whole rows,
-//     else WPT = 16 / C words (= 16 groups when every word is full).
-// When G % C == 0 both tilings coincide (16-group tiles of 2 or 4 whole words).
+//     word is produced inside one tile:  WPR == 1 (G <= C): WPT = S / G whole rows,
+//     else WPT = S / C words (= S groups when every word is full).  S >= C always.
+// When G % C == 0 both tilings coincide (S-group tiles of whole words).
 // ---------------------------------------------------------------------------
-constexpr int kGroup = 128;          // elements per group on the fast path
-constexpr int kSlots = 16;           // group slots per wave-tile (4 loads x 4 lane-rows)
+constexpr int kTileElems = 2048;     // elements per wave-tile (4 loads x 64 lanes x 8)
+constexpr int kGroup = 128;          // the benchmark's group size (BASELINE.json)
 #ifndef AWQ_WPB
 #define AWQ_WPB AWQ_BLOCK_TILES   // include/awq_hip.h (tuning builds may override)
 #endif
 constexpr int kWavesPerBlock = AWQ_WPB;   // waves (= tiles) per workgroup: 8 = 512 threads (halves the
                                           // workgroup dispatch rate the one-wave-per-tile grid needs)
+
+// group sizes the streaming kernel is instantiated for (8 elements per lane: GS / 8 lanes
+// per group, a power of two between 4 and 32 so the group reductions stay inside DPP rows
+// or one permlane16 swap)
+__host__ __device__ inline bool fast_group_size(int64_t gs) {
+    return gs == 32 || gs == 64 || gs == 128 || gs == 256;
+}
 
 struct TensorGeom {
     uint32_t G;    // groups per row
@@ -39,23 +48,25 @@ struct TensorGeom {
     uint32_t WPT;  // words per tile
     uint32_t words;  // R * WPR
     uint32_t bytes;  // 1 = byte tiles (see above), 0 = word tiles
+    uint32_t S;      // group slots per tile
 };
 
-__host__ __device__ inline TensorGeom fast_geom(int64_t R, int64_t K, int bits) {
+__host__ __device__ inline TensorGeom fast_geom(int64_t R, int64_t K, int bits, int gs) {
     TensorGeom g;
-    g.G = (uint32_t)(K / kGroup);
+    g.S = (uint32_t)(kTileElems / gs);
+    g.G = (uint32_t)(K / gs);
     g.C = 32u / (uint32_t)bits;
     g.WPR = (g.G + g.C - 1) / g.C;
-    g.WPT = (g.WPR == 1) ? (kSlots / g.G) : (kSlots / g.C);
+    g.WPT = (g.WPR == 1) ? (g.S / g.G) : (g.S / g.C);
     g.words = (uint32_t)R * g.WPR;
     g.bytes = (bits == 8 || (g.G % 2u) == 0u) ? 1u : 0u;
     return g;
 }
 
-__host__ __device__ inline int64_t fast_tiles(int64_t R, int64_t K, int bits) {
+__host__ __device__ inline int64_t fast_tiles(int64_t R, int64_t K, int bits, int gs) {
     if (R <= 0 || K <= 0) return 0;
-    TensorGeom g = fast_geom(R, K, bits);
-    if (g.bytes) return (R * (int64_t)g.G + kSlots - 1) / kSlots;
+    TensorGeom g = fast_geom(R, K, bits, gs);
+    if (g.bytes) return (R * (int64_t)g.G + g.S - 1) / g.S;
     return ((int64_t)g.words + g.WPT - 1) / g.WPT;
 }
 
@@ -67,16 +78,16 @@ __host__ __device__ inline uint32_t word_group(const TensorGeom& g, uint32_t w) 
 }
 
 // Limits of the fast path: flat group indices must fit 32 bits.
-__host__ __device__ inline bool fast_shape_ok(int64_t R, int64_t K) {
-    if (R <= 0 || K <= 0 || (K % kGroup) != 0) return false;
-    int64_t G = K / kGroup;
+__host__ __device__ inline bool fast_shape_ok(int64_t R, int64_t K, int64_t gs) {
+    if (!fast_group_size(gs) || R <= 0 || K <= 0 || (K % gs) != 0) return false;
+    int64_t G = K / gs;
     return R * G < (int64_t)0x7FFFFFFF && R * (G + 1) < (int64_t)0x7FFFFFFF;
 }
 
 // launchers (awq_fast.hip / awq_generic.hip)
 hipError_t launch_fast(const awq_tensor_desc* descs_dev, const int32_t* block_tensor,
                        const awq_tensor_desc* single, int n, int64_t total_tiles, int dtype, int bits,
-                       int symmetric, hipStream_t stream, int n_grid = 1, int n_cand = 0);
+                       int symmetric, int group_size, hipStream_t stream, int n_grid = 1, int n_cand = 0);
 hipError_t launch_generic(const void* w, int dtype, int64_t rows, int64_t K, int64_t L, int bits,
                           int symmetric, int32_t* tensor_q, uint16_t* scales, int32_t* zeros,
                           hipStream_t stream, int n_grid = 1, int n_cand = 0);

@@ -65,6 +65,8 @@ def parse():
     ap.add_argument("--workload", default="opt-125m", choices=sorted(WORKLOADS))
     ap.add_argument("--bits", type=int, default=4, choices=[4, 8])
     ap.add_argument("--symmetric", action="store_true")
+    ap.add_argument("--group-size", type=int, default=128, choices=[32, 64, 128, 256],
+                    help="128 = the BASELINE metric; other sizes are extra lines (metric names the size)")
     ap.add_argument("--parity", action="store_true", help="also write unpacked int32 tensor_q/zero_points")
     ap.add_argument("--replicas", type=int, default=0,
                     help="input replicas rotated across steps (0 = enough to exceed the 256 MiB Infinity Cache)")
@@ -115,7 +117,7 @@ def cpu_threads():
     return len(os.sched_getaffinity(0))
 
 
-def cpu_baseline(shapes, budget_s):
+def cpu_baseline(shapes, budget_s, group_size=128):
     """The oracle (oracle/awq_oracle.c, OpenMP over rows) on a bounded sample of the SAME
     workload: the tensor set in processing order, pass after pass, until about budget_s of
     CPU work (the last tensor may be cut to a row block).  Returns (GB/s of bf16 input,
@@ -141,7 +143,7 @@ def cpu_baseline(shapes, budget_s):
                 cache[key] = (torch.randn(take, K, generator=g) * 0.02).to(torch.bfloat16)
             x = cache[key]
             t0 = time.perf_counter()
-            orc.quantize_groups(x, take, K, 128, 4, False)
+            orc.quantize_groups(x, take, K, group_size, 4, False)
             t_total += time.perf_counter() - t0
             done_bytes += x.numel() * 2
             parts += 1
@@ -198,7 +200,8 @@ def main():
     for r in range(reps):
         seed0 = (rank * 64 + r) * 100003
         inputs = make_set(shapes, seed0, dev)
-        batches.append(PackedBatch(inputs, bits=args.bits, symmetric=args.symmetric, parity=args.parity))
+        batches.append(PackedBatch(inputs, bits=args.bits, symmetric=args.symmetric, parity=args.parity,
+                                   group_size=args.group_size))
     torch.cuda.synchronize()
     algo_bytes = batches[0].algorithmic_bytes()
 
@@ -250,15 +253,17 @@ def main():
         with open(args.traffic_json) as f:
             tj = json.load(f)
         key = f"{args.workload}.b{args.bits}.{'sym' if args.symmetric else 'asym'}.{'parity' if args.parity else 'packed'}"
+        if args.group_size != 128:
+            key += f".gs{args.group_size}"
         traffic = tj.get(key, {}).get("hbm_bytes_per_launch")
     except (OSError, ValueError):
         pass
     line = {
-        "metric": METRIC, "value": round(value, 3), "unit": "GB/s", "n_gpus": world, "steps": args.steps,
+        "metric": METRIC.replace("group_size=128", f"group_size={args.group_size}"), "value": round(value, 3), "unit": "GB/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "bf16", "data": "synthetic",
         "config": {"workload": f"{args.workload}: {DESCR[args.workload]}", "tensors": len(shapes),
-                   "elements": elems, "group_size": 128, "bits": args.bits, "symmetric": args.symmetric,
+                   "elements": elems, "group_size": args.group_size, "bits": args.bits, "symmetric": args.symmetric,
                    "outputs": "qweight+qzeros+fp16 scales" + (" + int32 tensor_q/zero_points" if args.parity else ""),
                    "launches_per_step": 1, "input_replicas_rotated": reps,
                    "parallelism": f"dp{world} (each rank quantizes its own replica of the tensor set)"},
@@ -273,7 +278,7 @@ def main():
         line["roofline"]["copy_ceiling"] = round(ceiling, 1)
         line["roofline"]["frac_of_copy"] = round(achieved / ceiling, 4)
     if not args.no_cpu_baseline:
-        gbs, secs, nbytes, nparts, threads = cpu_baseline(shapes, args.cpu_sample_seconds)
+        gbs, secs, nbytes, nparts, threads = cpu_baseline(shapes, args.cpu_sample_seconds, args.group_size)
         line["cpu_baseline"] = {"value": round(gbs, 5), "unit": "GB/s", "cores": threads, "kind": "port",
                                 "sample": f"oracle/awq_oracle.c (OpenMP over rows, {threads} threads) on "
                                           f"{nbytes / 1e6:.1f} MB of the {args.workload} set ({nparts} tensors/row-"

@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define AWQ_HIP_ABI_VERSION 4
+#define AWQ_HIP_ABI_VERSION 5
 
 /* dtype codes of the input weights (torch dtypes the reference accepts, awq.py:397) */
 enum { AWQ_DTYPE_BF16 = 0, AWQ_DTYPE_F16 = 1, AWQ_DTYPE_F32 = 2, AWQ_DTYPE_F64 = 3 };
@@ -77,8 +77,8 @@ int awq_device_check(char* arch, int len);
 /* Quantize one [rows, K] tensor (replaces awq.py:286-374 incl. the small-tensor
  * path awq.py:130-171, which a caller expresses as group_size = K).
  * bits in {4, 8}; symmetric selects qmin/qmax per awq.py:114-128.
- * bf16 / fp16 with group_size == 128 and K % 128 == 0 take the streaming fast kernel; every
- * other shape/dtype takes the generic kernel (same results). */
+ * bf16 / fp16 with group_size in {32, 64, 128, 256} and K % group_size == 0 take the
+ * streaming fast kernel; every other shape/dtype takes the generic kernel (same results). */
 int awq_quantize_groups(const void* w, int dtype, int64_t rows, int64_t K, int64_t group_size,
                         int bits, int symmetric, int32_t* qweight, int32_t* qzeros,
                         uint16_t* scales, int32_t* tensor_q, int32_t* zeros, void* stream);
@@ -104,8 +104,9 @@ int awq_quantize_search(const void* w, int dtype, int64_t rows, int64_t K, int64
 int awq_ragged_eligible(int dtype, int64_t rows, int64_t K, int64_t group_size);
 
 /* HOST helper: fills descs[i].tile_begin / tile_count (host array) for a ragged launch
- * and returns the total tile count (< 0 on error).  All tensors must be eligible. */
-int64_t awq_plan_ragged(awq_tensor_desc* descs_host, int n, int bits);
+ * and returns the total tile count (< 0 on error).  All tensors must be eligible for this
+ * group_size (32, 64, 128 or 256; a tile is 2048 elements = 2048 / group_size groups). */
+int64_t awq_plan_ragged(awq_tensor_desc* descs_host, int n, int bits, int64_t group_size);
 
 /* Tiles (= waves) per workgroup of the ragged kernel's one-wave-per-tile grid. */
 #define AWQ_BLOCK_TILES 8
@@ -118,11 +119,13 @@ int64_t awq_plan_block_tensor(const awq_tensor_desc* descs_host, int n, int64_t 
                               int32_t* block_tensor_host, int64_t len);
 
 /* Quantize n eligible tensors of one dtype (AWQ_DTYPE_BF16 or AWQ_DTYPE_F16) in ONE
- * launch (replaces the CLI's per-tensor loop, main.py:353-392).  descs_device: device copy of the array planned by awq_plan_ragged
- * (the caller uploads it; reusable across calls).  block_tensor_device: optional device
- * copy of the awq_plan_block_tensor table (NULL: each wave searches the descriptors). */
+ * launch (replaces the CLI's per-tensor loop, main.py:353-392).  descs_device: device copy
+ * of the array planned by awq_plan_ragged with the same bits and group_size (the caller
+ * uploads it; reusable across calls).  block_tensor_device: optional device copy of the
+ * awq_plan_block_tensor table (NULL: each wave searches the descriptors). */
 int awq_quantize_ragged(const awq_tensor_desc* descs_device, int n, int64_t total_tiles,
-                        const int32_t* block_tensor_device, int dtype, int bits, int symmetric, void* stream);
+                        const int32_t* block_tensor_device, int dtype, int bits, int symmetric, int64_t group_size,
+                        void* stream);
 
 /* AutoAWQ "GEMM" layout (the reference has no packed format): from
  * this library's row-major packed 4-bit results of an [N = out_features, K = in_features]

@@ -43,6 +43,7 @@ def main():
     ap.add_argument("--symmetric", action="store_true")
     ap.add_argument("--parity", action="store_true")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "f16"])
+    ap.add_argument("--group-size", type=int, default=128)
     args = ap.parse_args()
     from awq_quantizer import _hip
     from awq_quantizer.quantization.batch import PackedBatch
@@ -56,6 +57,8 @@ def main():
             if fn is not None:
                 fn.restype = res
                 fn.argtypes = argt
+        if lib.awq_abi_version() < 5:   # older builds: no group_size argument (gs 128 only)
+            lib.awq_quantize_ragged.argtypes = _hip.SIGNATURES["awq_quantize_ragged"][1][:-2] + [ctypes.c_void_p]
         handles[p] = lib
     _hip.load_library()
     _hip.require_device(dev)
@@ -88,7 +91,8 @@ def main():
                 g.manual_seed(r * 1000 + i)
                 inputs[f"t{i}"] = (torch.randn(*s, generator=g, device=dev) * 0.02).to(
                     torch.float16 if args.dtype == "f16" else torch.bfloat16)
-            bl.append(PackedBatch(inputs, bits=args.bits, symmetric=args.symmetric, parity=args.parity))
+            bl.append(PackedBatch(inputs, bits=args.bits, symmetric=args.symmetric, parity=args.parity,
+                                  group_size=args.group_size))
         batches[sname] = bl
     torch.cuda.synchronize()
 
@@ -123,10 +127,11 @@ def main():
                         s0, s1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                         s0.record(stream)
                         table = None if blk == "nt" else block_table(lp, lib, bt).data_ptr()
+                        gsa = (bt.group_size,) if lib.awq_abi_version() >= 5 else ()
                         rc = lib.awq_quantize_ragged(ctypes.c_void_p(bt.descs_dev.data_ptr()), len(bt.descs),
                                                      bt.total_tiles, ctypes.c_void_p(table),
                                                      _hip.AWQ_DTYPE[bt.dtype], bt.bits, int(bt.symmetric),
-                                                     ctypes.c_void_p(stream.cuda_stream))
+                                                     *gsa, ctypes.c_void_p(stream.cuda_stream))
                         s1.record(stream)
                         assert rc == 0, lib.awq_last_error()
                         if it >= 3:

@@ -27,7 +27,7 @@ def test_library_exports_every_declared_symbol():
     for s in syms:
         assert hasattr(lib, s), s
     assert set(syms) == set(_hip.SIGNATURES), "python binding out of sync with include/awq_hip.h"
-    assert lib.awq_abi_version() == _hip.ABI_VERSION == 4
+    assert lib.awq_abi_version() == _hip.ABI_VERSION == 5
 
 
 def test_library_is_gfx950_code_object():
@@ -63,6 +63,23 @@ def test_host_helpers_without_gpu():
     assert _hip.plan_ragged(d, 4) == 3
     d = [_hip.TensorDesc(4096 * 16, 11, 384, 0, 0, 2 * 4096, 0, 0, 0, 0)]
     assert _hip.plan_ragged(d, 8) == 3   # 8-bit: byte tiles, 33 groups -> 3
+    # other group sizes: a tile is 2048 elements = 2048 / gs group slots
+    for gs in (32, 64, 128, 256):
+        assert lib.awq_ragged_eligible(0, 1024, 4096, gs) == 1
+        assert lib.awq_ragged_eligible(1, 7, 3 * gs, gs) == 1
+        assert lib.awq_ragged_eligible(0, 7, 3 * gs + 8, gs) == 0   # K % gs != 0 -> generic
+    for gs in (16, 100, 512):
+        assert lib.awq_ragged_eligible(0, 1024, 4096, gs) == 0
+    d = [_hip.TensorDesc(4096 * 16, 1024, 4096, 0, 0, 2 * 4096, 0, 0, 0, 0)]
+    assert _hip.plan_ragged(d, 4, 32) == 1024 * 4096 // 2048        # byte tiles, 64 groups each
+    d = [_hip.TensorDesc(4096 * 16, 11, 96, 0, 0, 2 * 4096, 0, 0, 0, 0)]
+    assert _hip.plan_ragged(d, 4, 32) == 1   # G=3 odd -> word tiles of 21 whole rows (63 groups)
+    d = [_hip.TensorDesc(4096 * 16, 11, 768, 0, 0, 2 * 4096, 0, 0, 0, 0)]
+    assert _hip.plan_ragged(d, 4, 256) == 6   # gs 256: 8 slots; G=3 odd, WPR=1 -> 2 whole rows per tile
+    d = [_hip.TensorDesc(4096 * 16, 11, 768, 0, 0, 2 * 4096, 0, 0, 0, 0)]
+    assert _hip.plan_ragged(d, 8, 256) == 5   # 8-bit: byte tiles, 33 groups / 8 -> 5
+    with pytest.raises(RuntimeError, match="group_size"):
+        _hip.plan_ragged(d, 4, 100)
     # validation errors come back with a message, nothing launched
     assert lib.awq_quantize_groups(None, 0, 4, 256, 128, 3, 0, None, None, None, None, None, None) != 0
     assert "bit width" in _hip.last_error()

@@ -285,7 +285,7 @@ class AWQQuantizer:
                 "shape": torch.tensor(list(tensor.shape), dtype=torch.int64)}
 
     def quantize_model_packed(self, tensors: Dict[str, torch.Tensor]) -> Dict[str, Dict[str, torch.Tensor]]:
-        """Packed quantization of many tensors: the fast-path-eligible tensors (bf16 or fp16,
+        """Packed quantization of many tensors: the fast-path-eligible tensors (bf16, fp16 or fp32,
         group_size 32/64/128/256, K % group_size == 0) go into one ragged launch per dtype; the rest are
         quantized one by one.  Outputs stay on the device.  Failures are logged and skipped."""
         from .batch import PackedBatch
@@ -309,7 +309,7 @@ class AWQQuantizer:
         out = {}
         if eligible:
             dev = self.compute_device()
-            for dt in (torch.bfloat16, torch.float16):   # one ragged launch per input dtype
+            for dt in (torch.bfloat16, torch.float16, torch.float32):   # one ragged launch per input dtype
                 part = {k: v.detach().to(dev).contiguous() for k, v in eligible.items() if v.dtype == dt}
                 if part:
                     batch = PackedBatch(part, bits=self.bits, symmetric=self.symmetric, group_size=self.group_size)
@@ -350,7 +350,7 @@ class AWQQuantizer:
                     self.logger.error(f"Error quantizing tensor: {name}, error: {e}")
         if eligible:
             dev = self.compute_device()
-            for dt in (torch.bfloat16, torch.float16):
+            for dt in (torch.bfloat16, torch.float16, torch.float32):
                 part = {k: v.detach().to(dev).contiguous() for k, v in eligible.items() if v.dtype == dt}
                 if part:
                     batch = PackedBatch(part, bits=self.bits, symmetric=self.symmetric, parity=True, packed=False,

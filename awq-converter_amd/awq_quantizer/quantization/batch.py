@@ -18,7 +18,7 @@ class PackedBatch:
     """Device-resident inputs + packed outputs of one ragged launch.
 
     inputs: name -> contiguous device tensor ([rows, ...] or 1-D), K % group_size == 0, all
-    bf16 or all fp16; group_size 32, 64, 128 or 256 (one per batch).
+    bf16, all fp16 or all fp32; group_size 32, 64, 128 or 256 (one per batch).
     parity=True additionally produces the reference's unpacked int32 tensor_q and
     zero_points (6.05 B/element of output traffic instead of 0.52).
     use_block_table: upload the per-workgroup tensor table (awq_plan_block_tensor; 4 B per
@@ -34,8 +34,8 @@ class PackedBatch:
         self.names = list(inputs)
         first = next(iter(inputs.values()))
         dev, self.dtype = first.device, first.dtype
-        if self.dtype not in (torch.bfloat16, torch.float16):
-            raise ValueError(f"PackedBatch takes bf16 or fp16 tensors, got {self.dtype}")
+        if self.dtype not in (torch.bfloat16, torch.float16, torch.float32):
+            raise ValueError(f"PackedBatch takes bf16, fp16 or fp32 tensors, got {self.dtype}")
         _hip.require_device(dev)
         self.device = dev
         self.inputs = inputs

@@ -42,7 +42,8 @@ int check_common(int64_t rows, int64_t K, int64_t group_size, int bits) {
 }
 
 bool fast_eligible(int dtype, int64_t rows, int64_t K, int64_t group_size) {
-    return (dtype == AWQ_DTYPE_BF16 || dtype == AWQ_DTYPE_F16) && awq::fast_shape_ok(rows, K, group_size);
+    return (dtype == AWQ_DTYPE_BF16 || dtype == AWQ_DTYPE_F16 || dtype == AWQ_DTYPE_F32) &&
+           awq::fast_shape_ok(rows, K, group_size);
 }
 
 }  // namespace
@@ -202,8 +203,8 @@ int awq_quantize_ragged(const awq_tensor_desc* descs_device, int n, int64_t tota
     if (!awq::fast_group_size(group_size))
         return fail(AWQ_EUNSUPPORTED, "ragged launches take group_size 32, 64, 128 or 256 (got %lld)",
                     (long long)group_size);
-    if (dtype != AWQ_DTYPE_BF16 && dtype != AWQ_DTYPE_F16)
-        return fail(AWQ_EINVAL, "ragged launches take bf16 or fp16 tensors (dtype code %d)", dtype);
+    if (dtype != AWQ_DTYPE_BF16 && dtype != AWQ_DTYPE_F16 && dtype != AWQ_DTYPE_F32)
+        return fail(AWQ_EINVAL, "ragged launches take bf16, fp16 or fp32 tensors (dtype code %d)", dtype);
     if (n <= 0 || total_tiles <= 0) return AWQ_OK;
     if (!descs_device) return fail(AWQ_EINVAL, "null descriptor array");
     return hip_status(awq::launch_fast(descs_device, block_tensor_device, nullptr, n, total_tiles, dtype, bits,

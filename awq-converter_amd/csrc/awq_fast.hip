@@ -51,6 +51,10 @@
 #ifndef AWQ_MIN_WAVES
 #define AWQ_MIN_WAVES 8
 #endif
+// same for fp32 inputs (32 data VGPRs per lane instead of 16)
+#ifndef AWQ_MIN_WAVES_WIDE
+#define AWQ_MIN_WAVES_WIDE 6
+#endif
 // qweight stores: 1 = staged through LDS into one 16-B store per lane (4-bit: 1 store
 // instruction per tile instead of 4), 0 = one dword per lane per group row
 #ifndef AWQ_WIDE_STORE
@@ -89,16 +93,16 @@ __device__ __forceinline__ float rn_bf16(float a) {
 
 // one step of a 16-lane row reduction: max with a DPP-permuted copy (full row/bank masks,
 // every source lane valid) — LLVM folds the mov into v_max_i32_dpp (one instruction)
-template <int CTRL>
-__device__ __forceinline__ int dpp_max(int v) {
-    return max(v, __builtin_amdgcn_mov_dpp(v, CTRL, 0xF, 0xF, true));
+template <int CTRL, typename T>
+__device__ __forceinline__ T dpp_max(T v) {   // T = int (signed max) or uint32_t (unsigned)
+    return max(v, (T)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xF, 0xF, true));
 }
 
 // max over the L = GS/8 consecutive lanes of a group; every lane of the group gets it.
 // L <= 16: DPP steps inside a row (each folds into one v_max_i32_dpp); L = 32: the group
 // spans two rows, paired by one v_permlane16_swap (gfx950).
-template <int L>
-__device__ __forceinline__ int grp_max(int v) {
+template <int L, typename T>
+__device__ __forceinline__ T grp_max(T v) {
     static_assert(L == 4 || L == 8 || L == 16 || L == 32, "lanes per group");
     v = dpp_max<0xB1>(v);                  // quad_perm [1,0,3,2]
     v = dpp_max<0x4E>(v);                  // quad_perm [2,3,0,1]
@@ -106,7 +110,7 @@ __device__ __forceinline__ int grp_max(int v) {
     if (L >= 16) v = dpp_max<0x140>(v);    // row_mirror
     if (L >= 32) {                         // rows 0<->1, 2<->3
         const auto p = __builtin_amdgcn_permlane16_swap((unsigned)v, (unsigned)v, false, false);
-        v = max((int)p[0], (int)p[1]);
+        v = max((T)p[0], (T)p[1]);
     }
     return v;
 }
@@ -134,12 +138,45 @@ __device__ __forceinline__ float recip_bf16(float s) {
 }
 
 // ---- input formats ----------------------------------------------------------------
-// Both are 16-bit sign-magnitude floats, so the raw-bits min/max below works for both.
-// They differ in decoding, NaN thresholds, the rounding applied after every op (torch
-// computes a bf16/fp16 op in fp32 and rounds to the dtype, awq.py's per-op semantics) and
-// in how x / s is formed exactly.
+// All are sign-magnitude floats, so the raw-bits min/max below works for each.  They
+// differ in width (a lane's 8 consecutive elements of a group are one 16-B load for the
+// 16-bit formats, two for fp32), decoding, NaN thresholds, the rounding applied after
+// every op (torch computes a bf16/fp16 op in fp32 and rounds to the dtype, awq.py's per-op
+// semantics) and in how x / s is formed exactly.
+template <int NW>
+struct Chunk {
+    u4 w[NW];
+};
+
+// raw-bits lane maxima of 8 packed 16-bit values: signed (sign-extended) and unsigned
+__device__ __forceinline__ void lane_max16(const u4 v, int& smax, uint32_t& umax) {
+    // (the bit casts go through by-value helpers: hipcc 7.2 miscompiles
+    //  __builtin_bit_cast applied directly to an ext_vector element)
+    const uint32_t x0 = v.x, x1 = v.y, x2 = v.z, x3 = v.w;
+    const s2 sm = __builtin_elementwise_max(__builtin_elementwise_max(as_s2(x0), as_s2(x1)),
+                                            __builtin_elementwise_max(as_s2(x2), as_s2(x3)));
+    const us2 um = __builtin_elementwise_max(__builtin_elementwise_max(as_us2(x0), as_us2(x1)),
+                                             __builtin_elementwise_max(as_us2(x2), as_us2(x3)));
+    smax = max((int)sm.x, (int)sm.y);
+    umax = (uint32_t)max((int)um.x, (int)um.y);
+}
+// max of the complements 0xFFFF - u (unsigned min = 0xFFFF - that)
+__device__ __forceinline__ uint32_t lane_cmax16(const u4 v) {
+    const us2 ones = {0xFFFF, 0xFFFF};
+    const uint32_t x0 = v.x, x1 = v.y, x2 = v.z, x3 = v.w;
+    const us2 a = ones - as_us2(x0), b = ones - as_us2(x1);
+    const us2 c = ones - as_us2(x2), e = ones - as_us2(x3);
+    const us2 m = __builtin_elementwise_max(__builtin_elementwise_max(a, b), __builtin_elementwise_max(c, e));
+    return (uint32_t)max((int)m.x, (int)m.y);
+}
+
 struct FmtBF16 {
-    static constexpr int kNanS = 0x7F80, kNanU = 0xFF80;   // bits beyond +inf / -inf
+    static constexpr int NW = 1, kBytes = 2;
+    static constexpr bool kWide = false;
+    static constexpr int kNanS = 0x7F80;                   // bits beyond +inf / -inf
+    static constexpr uint32_t kNanU = 0xFF80u, kSign = 0x8000u, kOnes = 0xFFFFu;
+    __device__ static void lane_max(const Chunk<1>& c, int& smax, uint32_t& umax) { lane_max16(c.w[0], smax, umax); }
+    __device__ static uint32_t lane_cmax(const Chunk<1>& c) { return lane_cmax16(c.w[0]); }
     __device__ static float dec(uint32_t h) { return __uint_as_float(h << 16); }
     __device__ static float lo(uint32_t w) { return __uint_as_float(w << 16); }
     __device__ static float hi(uint32_t w) { return __uint_as_float(w & 0xFFFF0000u); }
@@ -164,6 +201,10 @@ struct FmtBF16 {
     static constexpr bool kHasPlain = false;
     __device__ static bool plain_ok(float s) { (void)s; return false; }
     __device__ static float quot_plain(float x, float r) { return rn_bf16(x * r); }
+    __device__ static float elem(const Chunk<1>& c, int i) {
+        const uint32_t w = c.w[0][i >> 1];
+        return (i & 1) ? hi(w) : lo(w);
+    }
 };
 
 // An f32 value the optimizer cannot see through: keeps `RN_f16(a / b)` an f32 IEEE division
@@ -181,7 +222,12 @@ __device__ __forceinline__ float opaque_s(float a) {
 }
 
 struct FmtF16 {
-    static constexpr int kNanS = 0x7C00, kNanU = 0xFC00;
+    static constexpr int NW = 1, kBytes = 2;
+    static constexpr bool kWide = false;
+    static constexpr int kNanS = 0x7C00;
+    static constexpr uint32_t kNanU = 0xFC00u, kSign = 0x8000u, kOnes = 0xFFFFu;
+    __device__ static void lane_max(const Chunk<1>& c, int& smax, uint32_t& umax) { lane_max16(c.w[0], smax, umax); }
+    __device__ static uint32_t lane_cmax(const Chunk<1>& c) { return lane_cmax16(c.w[0]); }
     __device__ static float dec(uint32_t h) { return (float)__builtin_bit_cast(_Float16, (uint16_t)h); }
     __device__ static float lo(uint32_t w) { return dec(w & 0xFFFFu); }
     __device__ static float hi(uint32_t w) { return dec(w >> 16); }
@@ -218,6 +264,59 @@ struct FmtF16 {
     static constexpr bool kHasPlain = AWQ_F16_PLAIN;   // tuning builds: -DAWQ_F16_PLAIN=0
     __device__ static bool plain_ok(float s) { return s < 14.0f; }
     __device__ static float quot_plain(float x, float r) { return rn(opaque(x * r)); }
+    __device__ static float elem(const Chunk<1>& c, int i) {
+        const uint32_t w = c.w[0][i >> 1];
+        return (i & 1) ? hi(w) : lo(w);
+    }
+};
+
+// fp32 weights: every op is the IEEE fp32 op (no rounding to a narrower dtype), x / s is
+// the IEEE division itself (the kernel stays memory-bound: 4 B per element against the
+// 16-bit formats' 2), min/max on the raw 32-bit patterns.
+struct FmtF32 {
+    static constexpr int NW = 2, kBytes = 4;
+    static constexpr bool kWide = true;    // t + 8 is not exact in fp32: sym shifts after rint
+    static constexpr int kNanS = 0x7F800000;
+    static constexpr uint32_t kNanU = 0xFF800000u, kSign = 0x80000000u, kOnes = 0xFFFFFFFFu;
+    __device__ static void lane_max(const Chunk<2>& c, int& smax, uint32_t& umax) {
+        int sm = (int)c.w[0].x;
+        uint32_t um = c.w[0].x;
+#pragma unroll
+        for (int i = 1; i < 8; ++i) {
+            const uint32_t w = c.w[i >> 2][i & 3];
+            sm = max(sm, (int)w);
+            um = max(um, w);
+        }
+        smax = sm;
+        umax = um;
+    }
+    __device__ static uint32_t lane_cmax(const Chunk<2>& c) {
+        uint32_t m = ~c.w[0].x;
+#pragma unroll
+        for (int i = 1; i < 8; ++i) m = max(m, ~(uint32_t)c.w[i >> 2][i & 3]);
+        return m;
+    }
+    __device__ static float dec(uint32_t h) { return __uint_as_float(h); }
+    __device__ static float rn(float a) { return a; }
+    __device__ static float as_fmt(float z) { return z; }
+    __device__ static float dq_scale(float s) { return (float)(_Float16)s; }
+    __device__ static float quot(float x, float s, float r) {
+        (void)r;
+        return x / s;                                   // IEEE (-fhip-fp32-correctly-rounded-divide-sqrt)
+    }
+    __device__ static float scale(float d, float qr) { return d / qr; }
+    __device__ static float lo_clamp() { return 1e-10f; }                            // RN_f32(1e-10)
+    __device__ static float recip(float s) { return 1.0f / s; }
+    __device__ static float quot_any(float x, float s, float r) { return quot(x, s, r); }
+    // s = inf (r = 0) or NaN -> exact special path; every finite s >= 1e-10 is fast
+    __device__ static bool fast(float r) { return r > 0.0f && r < __builtin_inff(); }
+    static constexpr bool kHasPlain = false;
+    __device__ static bool plain_ok(float s) { (void)s; return false; }
+    __device__ static float quot_plain(float x, float r) { return x * r; }
+    __device__ static float elem(const Chunk<2>& c, int i) {
+        const uint32_t w = c.w[i >> 2][i & 3];
+        return __uint_as_float(w);
+    }
 };
 
 struct GroupParams {
@@ -226,16 +325,17 @@ struct GroupParams {
     float s;   // scale (a value of the input dtype)
 };
 
-// awq.py:192-199 on one group from the raw-bits row reductions: smax = signed-int16 max,
-// umax = unsigned max, umin = unsigned min (only valid when the group is single-signed).
-// Returns the (NaN-propagated, symmetric-folded) [mn, mx] the scale is taken from.
+// awq.py:192-199 on one group from the raw-bits reductions: smax = signed max of the bit
+// patterns (sign-extended), umax = unsigned max, umin = unsigned min (only valid when the
+// group is single-signed).  Returns the (NaN-propagated, symmetric-folded) [mn, mx] the
+// scale is taken from.
 template <typename F, bool SYM>
-__device__ __forceinline__ void group_range(int smax, int umax, int umin, float& mn_out, float& mx_out,
+__device__ __forceinline__ void group_range(int smax, uint32_t umax, uint32_t umin, float& mn_out, float& mx_out,
                                             bool& nan_out) {
-    const int mx_bits = smax >= 0 ? smax : umin;          // all negative: smallest magnitude
-    const int mn_bits = umax >= 0x8000 ? umax : umin;     // none negative: smallest value
+    const uint32_t mx_bits = smax >= 0 ? (uint32_t)smax : umin;   // all negative: smallest magnitude
+    const uint32_t mn_bits = umax >= F::kSign ? umax : umin;      // none negative: smallest value
     const bool nan = (smax > F::kNanS) || (umax > F::kNanU);
-    float mx = F::dec((uint32_t)mx_bits), mn = F::dec((uint32_t)mn_bits);
+    float mx = F::dec(mx_bits), mn = F::dec(mn_bits);
     if (nan) { mx = __builtin_nanf(""); mn = mx; }   // torch min/max both propagate NaN
     if (SYM) {                                        // awq.py:196-199
         float a = __builtin_fmaxf(__builtin_fabsf(mn), __builtin_fabsf(mx));
@@ -271,21 +371,24 @@ __device__ __forceinline__ GroupParams params_from_range(float mn, float mx) {
 // Quantize the 8 values of one lane (awq.py:245-248) for a group with a positive finite
 // scale and pack them: 4-bit -> w.x, 8-bit -> (w.x, w.y).  Field value = q - qmin.
 template <typename F, int BITS, bool SYM, bool PLAIN = false>
-__device__ __forceinline__ u2v quant8_fast(const u4 v, float r, float z, float s) {
+__device__ __forceinline__ u2v quant8_fast(const Chunk<F::NW>& v, float r, float z, float s) {
     constexpr float QR = (float)((1 << BITS) - 1);
     constexpr float HALF = (float)(1 << (BITS - 1));
-    const uint32_t src[4] = {v.x, v.y, v.z, v.w};
     const float zf = F::as_fmt(z);
     float q[8];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         // RN(x / s)
-        const float t0 = PLAIN ? F::quot_plain(F::lo(src[i]), r) : F::quot(F::lo(src[i]), s, r);
-        const float t1 = PLAIN ? F::quot_plain(F::hi(src[i]), r) : F::quot(F::hi(src[i]), s, r);
+        const float x0 = F::elem(v, 2 * i), x1 = F::elem(v, 2 * i + 1);
+        const float t0 = PLAIN ? F::quot_plain(x0, r) : F::quot(x0, s, r);
+        const float t1 = PLAIN ? F::quot_plain(x1, r) : F::quot(x1, s, r);
         float u0, u1;
-        if (SYM) {
+        if (SYM && F::kWide) {
+            u0 = __builtin_rintf(t0) + HALF;                         // exact: an integer + 8
+            u1 = __builtin_rintf(t1) + HALF;
+        } else if (SYM) {
             u0 = t0 + HALF;                                          // rint(t)+8 == rint(t+8)
-            u1 = t1 + HALF;
+            u1 = t1 + HALF;                                          // (exact for 16-bit t)
         } else {
             u0 = F::rn(t0 + zf);                                     // RN(x/s + z)
             u1 = F::rn(t1 + zf);
@@ -317,15 +420,14 @@ __device__ __forceinline__ u2v quant8_fast(const u4 v, float r, float z, float s
 // Same with the reference's NaN/inf semantics (groups whose scale is 0, inf or NaN), with
 // a true IEEE division per element.
 template <typename F, int BITS, bool SYM>
-__device__ __forceinline__ void quant8_special(const u4 v, float z, float s, uint32_t (&nib)[8],
+__device__ __forceinline__ void quant8_special(const Chunk<F::NW>& v, float z, float s, uint32_t (&nib)[8],
                                                int32_t (&q)[8]) {
     constexpr int QMIN = SYM ? -(1 << (BITS - 1)) : 0;
     constexpr int QMAX = SYM ? (1 << (BITS - 1)) - 1 : (1 << BITS) - 1;
     constexpr uint32_t MASK = (1u << BITS) - 1u;
-    const uint32_t src[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-        const float x = (i & 1) ? F::hi(src[i >> 1]) : F::lo(src[i >> 1]);
+        const float x = F::elem(v, i);
         const float t = F::rn(opaque(x) / s);
         const float u = SYM ? t : F::rn(t + z);
         float rr = __builtin_rintf(u);
@@ -351,7 +453,6 @@ __device__ __forceinline__ uint16_t f16_bits(float s) {
 // Tile context: everything a wave needs about one tile, all wave-uniform (SGPRs).
 // ---------------------------------------------------------------------------------------
 struct TileCtx {
-    const uint16_t* wp;  // first input element of the tile
     int32_t* qweight;    // tensor bases of the outputs (nullptr = not wanted)
     int32_t* qzeros;
     uint16_t* scales;
@@ -392,7 +493,6 @@ __device__ __forceinline__ TileCtx make_ctx(const awq_tensor_desc& d, uint32_t t
     }
     c.G = g.G;
     c.WPR = g.WPR;
-    c.wp = (const uint16_t*)d.w + (uint64_t)c.start * GS;
     c.qweight = d.qweight;
     c.qzeros = d.qzeros;
     c.scales = d.scales;
@@ -422,13 +522,18 @@ __device__ __forceinline__ void tile_src(int64_t rows, int64_t K, uint32_t tile,
 // its 16 B at 16 l — group slot j * (64 / L) + l / L, chunk l % L of that group
 // (L = GS / 8).  Slots past the tile end fall outside the descriptor's range and read as
 // zero.
-template <int GS>
-__device__ __forceinline__ void load_tile(const uint16_t* wp, uint32_t ng, u4 (&v)[4]) {
+// fp32: the same element mapping, each lane's 32 B as two 16-B loads (a pair of
+// instructions covers 2 KiB contiguously).
+template <typename F, int GS>
+__device__ __forceinline__ void load_tile(const char* wp, uint32_t ng, Chunk<F::NW> (&v)[4]) {
     const int lane = threadIdx.x & 63;
-    const __amdgpu_buffer_rsrc_t rw = rsrc(wp, ng * (2u * GS));
+    const __amdgpu_buffer_rsrc_t rw = rsrc(wp, ng * (uint32_t)(F::kBytes * GS));
 #pragma unroll
     for (int j = 0; j < 4; ++j)
-        v[j] = __builtin_amdgcn_raw_buffer_load_b128(rw, (uint32_t)(j * 1024 + lane * 16), 0, AWQ_LOAD_AUX);
+#pragma unroll
+        for (int h = 0; h < F::NW; ++h)
+            v[j].w[h] = __builtin_amdgcn_raw_buffer_load_b128(
+                rw, (uint32_t)(j * 512 * F::kBytes + lane * 8 * F::kBytes + 16 * h), 0, AWQ_LOAD_AUX);
 }
 
 // sum over the L lanes of a group, pairwise over adjacent lanes (xor 1, xor 2, then the
@@ -458,15 +563,14 @@ __device__ __forceinline__ float grp_sum(float v) {
 // awq.py:459-539), (x - dq)^2 summed in element order.  `special`: the candidate's scale
 // is 0 / inf / NaN (exact division, NaN-propagating clamp).
 template <typename F, int BITS, bool SYM>
-__device__ __forceinline__ float chunk_err(const u4 v, float r, float z, float s, float sh, bool special) {
+__device__ __forceinline__ float chunk_err(const Chunk<F::NW>& v, float r, float z, float s, float sh, bool special) {
     constexpr float QMIN = SYM ? -(float)(1 << (BITS - 1)) : 0.0f;
     constexpr float QMAX = SYM ? (float)((1 << (BITS - 1)) - 1) : (float)((1 << BITS) - 1);
-    const uint32_t src[4] = {v.x, v.y, v.z, v.w};
     const float zf = F::as_fmt(z);
     float acc = 0.0f;
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-        const float x = (i & 1) ? F::hi(src[i >> 1]) : F::lo(src[i >> 1]);
+        const float x = F::elem(v, i);
         float q;
         if (__builtin_expect(special, 0)) {
             const float t = F::rn(opaque(x) / s);
@@ -496,7 +600,7 @@ __device__ __forceinline__ float shrink(float v, float al) {
 }
 
 template <typename F, int BITS, bool SYM, int GS>
-__device__ __forceinline__ void search_range(const u4 (&v)[4], float& gmn, float& gmx, bool gnan, int n_grid,
+__device__ __forceinline__ void search_range(const Chunk<F::NW> (&v)[4], float& gmn, float& gmx, bool gnan, int n_grid,
                                           int n_cand) {
     const int jj = threadIdx.x & 3;
     float best = __builtin_inff();
@@ -530,7 +634,7 @@ __device__ __forceinline__ void search_range(const u4 (&v)[4], float& gmn, float
 }
 
 template <typename F, int BITS, bool SYM, bool SEARCH, int GS>
-__device__ __forceinline__ void compute_tile(const TileCtx& c, const u4 (&v)[4], uint32_t* zw, uint32_t* qstage,
+__device__ __forceinline__ void compute_tile(const TileCtx& c, const Chunk<F::NW> (&v)[4], uint32_t* zw, uint32_t* qstage,
                                              int n_grid, int n_cand) {
     constexpr int QMIN = SYM ? -(1 << (BITS - 1)) : 0;
     constexpr uint32_t C = 32u / BITS;   // groups per qzeros word
@@ -547,7 +651,7 @@ __device__ __forceinline__ void compute_tile(const TileCtx& c, const u4 (&v)[4],
     if (c.qweight) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            const uint32_t word = v[j].x ^ v[j].y ^ v[j].z ^ v[j].w;
+            const uint32_t word = v[j].w[0].x ^ v[j].w[0].y ^ v[j].w[0].z ^ v[j].w[F::NW - 1].w;
             __amdgpu_buffer_rsrc_t rq = rsrc(c.qweight + (uint64_t)c.start * WPG, ng * WPG * 4u);
             __builtin_amdgcn_raw_buffer_store_b32(word, rq, (uint32_t)((64 * j + lane) * 4), 0, AWQ_STORE_AUX);
         }
@@ -555,11 +659,11 @@ __device__ __forceinline__ void compute_tile(const TileCtx& c, const u4 (&v)[4],
 #ifndef AWQ_TRIVIAL_NOSMALL
     if (ch < 4 && c.scales) {
         __amdgpu_buffer_rsrc_t rs = rsrc(c.scales + c.start, ng * 2u);
-        __builtin_amdgcn_raw_buffer_store_b16((uint16_t)v[0].x, rs, (GPJ * ch + grp) * 2u, 0, AWQ_SMALL_AUX);
+        __builtin_amdgcn_raw_buffer_store_b16((uint16_t)v[0].w[0].x, rs, (GPJ * ch + grp) * 2u, 0, AWQ_SMALL_AUX);
     }
     if (c.qzeros && (uint32_t)lane < c.nw) {
         __amdgpu_buffer_rsrc_t rz = rsrc(c.qzeros + c.w0, c.nw * 4u);
-        __builtin_amdgcn_raw_buffer_store_b32(v[1].y, rz, (uint32_t)lane * 4u, 0, AWQ_SMALL_AUX);
+        __builtin_amdgcn_raw_buffer_store_b32(v[1].w[0].y, rz, (uint32_t)lane * 4u, 0, AWQ_SMALL_AUX);
     }
 #endif
     return;
@@ -572,39 +676,30 @@ __device__ __forceinline__ void compute_tile(const TileCtx& c, const u4 (&v)[4],
     //         beyond F::kNanS / F::kNanU.  Single-signed groups (rare in weights; LayerNorm
     //         gammas) take an extra unsigned-min reduction in a wave-uniform branch.
     //         Reductions over the group's L lanes: DPP-fused v_max_i32 (grp_max) ----
-    int smx[4], umx[4];
+    int smx[4];
+    uint32_t umx[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-        // (the bit casts go through by-value helpers: hipcc 7.2 miscompiles
-        //  __builtin_bit_cast applied directly to an ext_vector element)
-        const uint32_t x0 = v[j].x, x1 = v[j].y, x2 = v[j].z, x3 = v[j].w;
-        const s2 sm = __builtin_elementwise_max(__builtin_elementwise_max(as_s2(x0), as_s2(x1)),
-                                                __builtin_elementwise_max(as_s2(x2), as_s2(x3)));
-        const us2 um = __builtin_elementwise_max(__builtin_elementwise_max(as_us2(x0), as_us2(x1)),
-                                                 __builtin_elementwise_max(as_us2(x2), as_us2(x3)));
-        smx[j] = grp_max<L>(max((int)sm.x, (int)sm.y));
-        umx[j] = grp_max<L>(max((int)um.x, (int)um.y));
+        int sm;
+        uint32_t um;
+        F::lane_max(v[j], sm, um);
+        smx[j] = grp_max<L>(sm);
+        umx[j] = grp_max<L>(um);
     }
-    int umn[4] = {0, 0, 0, 0};
+    uint32_t umn[4] = {0, 0, 0, 0};
     bool one_signed = false;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) one_signed |= (smx[j] < 0) || (umx[j] < 0x8000);
+    for (int j = 0; j < 4; ++j) one_signed |= (smx[j] < 0) || (umx[j] < F::kSign);
     if (__builtin_expect(__ballot(one_signed) != 0, 0)) {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {   // unsigned min = 0xFFFF - max(0xFFFF - u)
-            const us2 ones = {0xFFFF, 0xFFFF};
-            const uint32_t x0 = v[j].x, x1 = v[j].y, x2 = v[j].z, x3 = v[j].w;
-            const us2 a = ones - as_us2(x0), b = ones - as_us2(x1);
-            const us2 c = ones - as_us2(x2), e = ones - as_us2(x3);
-            const us2 m = __builtin_elementwise_max(__builtin_elementwise_max(a, b), __builtin_elementwise_max(c, e));
-            umn[j] = 0xFFFF - grp_max<L>(max((int)m.x, (int)m.y));
-        }
+        for (int j = 0; j < 4; ++j) umn[j] = F::kOnes - grp_max<L>(F::lane_cmax(v[j]));   // unsigned min
     }
     // ---- 2. scale / zero point: lane (grp, ch) computes the group of load ch & 3, i.e.
     //         slot GPJ * (ch & 3) + grp (the L / 4 lanes of a group with equal ch & 3 do the
     //         same work; for GS 32 every lane owns exactly one of the 64 slots) ----
     const int jj = ch & 3;
-    int ssel = smx[0], usel = umx[0], nsel = umn[0];
+    int ssel = smx[0];
+    uint32_t usel = umx[0], nsel = umn[0];
 #pragma unroll
     for (int j = 1; j < 4; ++j)
         if (jj == j) { ssel = smx[j]; usel = umx[j]; nsel = umn[j]; }
@@ -782,7 +877,8 @@ __device__ uint64_t* g_trace = nullptr;
 // grid (AWQ_HIP_MAX_BLOCKS, tests) makes each wave walk tiles t, t + nwaves, ... with a
 // tensor cursor.
 template <typename F, int BITS, bool SYM, bool SEARCH, int GS>
-__global__ __launch_bounds__(64 * kWavesPerBlock, SEARCH ? 4 : AWQ_MIN_WAVES) void awq_fast_kernel(
+__global__ __launch_bounds__(64 * kWavesPerBlock, SEARCH ? 4 : (F::kWide ? AWQ_MIN_WAVES_WIDE : AWQ_MIN_WAVES))
+void awq_fast_kernel(
     const awq_tensor_desc* __restrict__ descs, const int32_t* __restrict__ block_tensor, awq_tensor_desc single,
     int n, int64_t total_tiles, int n_grid, int n_cand) {
     __shared__ uint32_t zwords[kWavesPerBlock][kTileElems / GS];
@@ -832,8 +928,8 @@ __global__ __launch_bounds__(64 * kWavesPerBlock, SEARCH ? 4 : AWQ_MIN_WAVES) vo
         const uint32_t tile = (uint32_t)(t - d.tile_begin);
         uint32_t st, ng;
         tile_src<BITS, GS>(d.rows, d.K, tile, st, ng);
-        u4 va[4];
-        load_tile<GS>((const uint16_t*)d.w + (uint64_t)st * GS, ng, va);
+        Chunk<F::NW> va[4];
+        load_tile<F, GS>((const char*)d.w + (uint64_t)st * GS * F::kBytes, ng, va);
 #ifdef AWQ_TRACE
         if (tr1 == 0) {
             tr1 = __builtin_amdgcn_s_memrealtime();
@@ -918,6 +1014,8 @@ hipError_t launch_fast(const awq_tensor_desc* descs_dev, const int32_t* block_te
     if (!fast_group_size(group_size)) return hipErrorInvalidValue;
     if (dtype == AWQ_DTYPE_F16) {
         AWQ_LAUNCH_FMT(FmtF16)
+    } else if (dtype == AWQ_DTYPE_F32) {
+        AWQ_LAUNCH_FMT(FmtF32)
     } else {
         AWQ_LAUNCH_FMT(FmtBF16)
     }

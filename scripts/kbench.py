@@ -42,7 +42,7 @@ def main():
     ap.add_argument("--bits", type=int, default=4)
     ap.add_argument("--symmetric", action="store_true")
     ap.add_argument("--parity", action="store_true")
-    ap.add_argument("--dtype", default="bf16", choices=["bf16", "f16"])
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "f16", "f32"])
     ap.add_argument("--group-size", type=int, default=128)
     args = ap.parse_args()
     from awq_quantizer import _hip
@@ -81,7 +81,7 @@ def main():
     batches = {}
     for sname in args.sets.split(","):
         shapes = shapes_of(sname)
-        nbytes = sum(int(torch.Size(s).numel()) * 2 for s in shapes)
+        nbytes = sum(int(torch.Size(s).numel()) * (4 if args.dtype == "f32" else 2) for s in shapes)
         reps = max(1, -(-(1 << 30) // nbytes))
         bl = []
         for r in range(reps):
@@ -90,7 +90,7 @@ def main():
             for i, s in enumerate(shapes):
                 g.manual_seed(r * 1000 + i)
                 inputs[f"t{i}"] = (torch.randn(*s, generator=g, device=dev) * 0.02).to(
-                    torch.float16 if args.dtype == "f16" else torch.bfloat16)
+                    {"f16": torch.float16, "f32": torch.float32}.get(args.dtype, torch.bfloat16))
             bl.append(PackedBatch(inputs, bits=args.bits, symmetric=args.symmetric, parity=args.parity,
                                   group_size=args.group_size))
         batches[sname] = bl
@@ -147,7 +147,7 @@ def main():
         bt = batches[sname][0]
         us = min(v)
         algo = bt.algorithmic_bytes() / (us / 1e6) / 1e9
-        inp = bt.elements * 2 / (us / 1e6) / 1e9
+        inp = bt.elements * bt.inputs[bt.names[0]].element_size() / (us / 1e6) / 1e9
         print(f"{sname:16s} {lname:28s} {blk:>6s} {us:9.1f} {algo:9.1f} {inp:8.1f} {algo / 8000:6.3f}")
         print(json.dumps({"set": sname, "lib": lname, "blocks": blk, "us": round(us, 2), "algo_GBs": round(algo, 1),
                           "in_GBs": round(inp, 1), "rounds_us": [round(x, 1) for x in v]}))

@@ -42,7 +42,8 @@ def test_host_helpers_without_gpu():
     assert lib.awq_ragged_eligible(0, 1024, 4096, 128) == 1
     assert lib.awq_ragged_eligible(0, 1024, 4000, 128) == 0
     assert lib.awq_ragged_eligible(1, 1024, 4096, 128) == 1     # fp16 streams too
-    assert lib.awq_ragged_eligible(2, 1024, 4096, 128) == 0     # fp32 -> generic kernel
+    assert lib.awq_ragged_eligible(2, 1024, 4096, 128) == 1     # fp32 streams too
+    assert lib.awq_ragged_eligible(3, 1024, 4096, 128) == 0     # fp64 -> generic kernel
     d = [_hip.TensorDesc(4096 * 16, 1024, 4096, 0, 0, 2 * 4096, 0, 0, 0, 0),
          _hip.TensorDesc(4096 * 32, 1, 768, 0, 0, 2 * 8192, 0, 0, 0, 0),
          _hip.TensorDesc(4096 * 48, 50, 768, 0, 0, 2 * 16384, 0, 0, 0, 0)]

@@ -55,7 +55,7 @@ def check(x, bits, sym):
 def test_f16_takes_the_streaming_kernel():
     from awq_quantizer import _hip
     assert _hip.ragged_eligible(torch.float16, 1024, 4096, 128)
-    assert not _hip.ragged_eligible(torch.float32, 1024, 4096, 128)
+    assert not _hip.ragged_eligible(torch.float64, 1024, 4096, 128)
 
 
 @pytest.mark.parametrize("bits", [4, 8])

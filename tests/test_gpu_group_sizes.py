@@ -65,7 +65,8 @@ def test_group_sizes_take_the_streaming_kernel():
     for gs in GROUP_SIZES + [128]:
         assert _hip.ragged_eligible(torch.bfloat16, 7, 3 * gs, gs)
         assert _hip.ragged_eligible(torch.float16, 7, 3 * gs, gs)
-        assert not _hip.ragged_eligible(torch.float32, 7, 3 * gs, gs)
+        assert _hip.ragged_eligible(torch.float32, 7, 3 * gs, gs)
+        assert not _hip.ragged_eligible(torch.float64, 7, 3 * gs, gs)
 
 
 @pytest.mark.parametrize("bits", [4, 8])

@@ -1,34 +1,41 @@
-// awq_fast.hip — streaming group quantizer for bf16 weights, group_size 128 (gfx950).
+// awq_fast.hip — streaming group quantizer for bf16 / fp16 / fp32 weights, group_size
+// 32, 64, 128 or 256 (gfx950).
 //
 // Replaces the per-group Python double loop of the reference
 // (src/awq_quantizer/quantization/awq.py:286-374 -> _compute_scale_zp_for_group :173-213
-// -> _quantize_tensor :215-250) with one HBM pass: read bf16 once, write packed
+// -> _quantize_tensor :215-250) with one HBM pass: read the weights once, write packed
 // qweight/qzeros + fp16 scales (and, in parity mode, the reference's unpacked int32
 // tensor_q / zero_points).
 //
-// Mapping (HBM-bound, no MFMA):
-//   * one wave = one tile = 16 group slots = 4 KiB of input: lane-row rho (16 lanes) holds
-//     groups 4j + rho, each lane one 16-B chunk per group (4 x buffer_load_dwordx4);
+// Mapping (HBM-bound, no MFMA; described for bf16, GS 128 — the benchmark — with the
+// general rule in brackets):
+//   * one wave = one tile = 2048 elements = 4 KiB of bf16 [2048 / GS group slots]; lane l
+//     holds elements 512 j + 8 l .. + 7 of load j, one 16-B buffer_load_dwordx4 [two for
+//     fp32], so a group spans 16 lanes [L = GS / 8] and lane-row rho holds groups 4j + rho;
 //   * the grid has one wave per tile (non-persistent): the hardware dispatcher hands a
 //     finished wave's slot to the next workgroup, which balances the load across CUs.  A
 //     persistent grid (waves walking tiles) lost ~20 % to the dispatcher's age priority:
 //     the youngest workgroups of every CU ran last and alone (profiles/r24-r27);
-//   * per-group min/max from the raw bf16 bits (signed / unsigned int16 max), reduced over
-//     the 16-lane row with DPP-fused v_max_i32; NaN is detected from the bits;
-//   * the scale / zero point of the tile's 16 groups are computed ONCE, by 16 different
-//     lanes (lane (row, c) owns group 4c + row), with the reference's per-op bf16 rounding,
-//     then broadcast back to the group's 16 lanes with DPP row_newbcast;
+//   * per-group min/max from the raw bits (signed / unsigned integer max), reduced over
+//     the group's lanes with DPP-fused v_max [plus one v_permlane16_swap at GS 256]; NaN
+//     is detected from the bits;
+//   * the scale / zero point of the tile's groups are computed ONCE per lane set (lane c of
+//     a group owns the group of load c & 3), with the reference's per-op rounding, then
+//     broadcast to the group's lanes with one DPP quad_perm per parameter;
 //   * per element: RN_bf16(x * RN_f32(1/s)) == RN_bf16(x / s) for every bf16 x and every
 //     bf16 s >= RN_bf16(1e-10) (verified exhaustively: oracle/verify_recip.c), so one
 //     multiply replaces the division; RNE to bf16 is one v_cvt_pk_bf16_f32 with a zero
 //     low half (the dword IS the rounded f32); + z, round-half-even, clamp, and
-//     v_cvt_pk_u8_f32 packs nibble pairs / bytes;
-//   * each lane emits exactly one packed int32 (4-bit): 256 B contiguous per store;
+//     v_cvt_pk_u8_f32 packs nibble pairs / bytes [fp16: plain or Markstein quotient;
+//     fp32: the IEEE division];
+//   * each lane emits one packed int32 per load (4-bit), staged in LDS into one 16-B store
+//     per lane;
 //   * buffer descriptors are based at the tile start with the tile's byte length, so
 //     slots past the tile end read zeros and their stores are dropped by the hardware
 //     range check (no per-lane masks, no OOB access, tensors > 4 GB are fine).
 // Ragged launches: one grid over the tiles of many tensors (descriptor table in HBM); a
-// wave finds its tensor with a 64-lane ballot search of the table.
+// wave finds its tensor from a host-planned per-workgroup table (or, without it, a
+// 64-lane ballot search of the descriptors).
 #include <cstdlib>
 
 #include "awq_internal.h"

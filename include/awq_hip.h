@@ -77,8 +77,9 @@ int awq_device_check(char* arch, int len);
 /* Quantize one [rows, K] tensor (replaces awq.py:286-374 incl. the small-tensor
  * path awq.py:130-171, which a caller expresses as group_size = K).
  * bits in {4, 8}; symmetric selects qmin/qmax per awq.py:114-128.
- * bf16 / fp16 with group_size in {32, 64, 128, 256} and K % group_size == 0 take the
- * streaming fast kernel; every other shape/dtype takes the generic kernel (same results). */
+ * bf16 / fp16 / fp32 with group_size in {32, 64, 128, 256} and K % group_size == 0 take
+ * the streaming fast kernel; every other shape/dtype (fp64, other group sizes, padded
+ * tails) takes the generic kernel (same results). */
 int awq_quantize_groups(const void* w, int dtype, int64_t rows, int64_t K, int64_t group_size,
                         int bits, int symmetric, int32_t* qweight, int32_t* qzeros,
                         uint16_t* scales, int32_t* tensor_q, int32_t* zeros, void* stream);
@@ -118,7 +119,7 @@ int64_t awq_plan_ragged(awq_tensor_desc* descs_host, int n, int bits, int64_t gr
 int64_t awq_plan_block_tensor(const awq_tensor_desc* descs_host, int n, int64_t total_tiles,
                               int32_t* block_tensor_host, int64_t len);
 
-/* Quantize n eligible tensors of one dtype (AWQ_DTYPE_BF16 or AWQ_DTYPE_F16) in ONE
+/* Quantize n eligible tensors of one dtype (AWQ_DTYPE_BF16, _F16 or _F32) in ONE
  * launch (replaces the CLI's per-tensor loop, main.py:353-392).  descs_device: device copy
  * of the array planned by awq_plan_ragged with the same bits and group_size (the caller
  * uploads it; reusable across calls).  block_tensor_device: optional device copy of the

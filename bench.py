@@ -60,11 +60,18 @@ def shapes_of(workload):
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
+    # Defaults measure the sustained rate: the chip's clocks settle only after ~20-30 ms of
+    # back-to-back launches (scripts/sustain_probe.py, profiles/r60: opt-125m launches run
+    # 54-66 us during the first ~300, then a steady 53.9 us), so 500 warmup launches
+    # (~28 ms) precede 1000 timed ones (~54 ms; the ~35 us launch / sync edge of the timed
+    # region is then < 0.1 %).
+    ap.add_argument("--steps", type=int, default=1000)
+    ap.add_argument("--warmup", type=int, default=500)
     ap.add_argument("--workload", default="opt-125m", choices=sorted(WORKLOADS))
     ap.add_argument("--bits", type=int, default=4, choices=[4, 8])
     ap.add_argument("--symmetric", action="store_true")
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "f16", "f32"],
+                    help="bf16 = the BASELINE metric; f16 / f32 are extra lines (metric names the dtype)")
     ap.add_argument("--group-size", type=int, default=128, choices=[32, 64, 128, 256],
                     help="128 = the BASELINE metric; other sizes are extra lines (metric names the size)")
     ap.add_argument("--parity", action="store_true", help="also write unpacked int32 tensor_q/zero_points")
@@ -79,12 +86,15 @@ def parse():
     return ap.parse_args()
 
 
-def make_set(shapes, seed0, dev):
+DTYPES = {"bf16": torch.bfloat16, "f16": torch.float16, "f32": torch.float32}
+
+
+def make_set(shapes, seed0, dev, dtype=torch.bfloat16):
     g = torch.Generator(device=dev)
     tensors = {}
     for i, s in enumerate(shapes):
         g.manual_seed(seed0 + i)
-        tensors[f"t{i:04d}"] = (torch.randn(*s, generator=g, device=dev, dtype=torch.float32) * 0.02).to(torch.bfloat16)
+        tensors[f"t{i:04d}"] = (torch.randn(*s, generator=g, device=dev, dtype=torch.float32) * 0.02).to(dtype)
     return tensors
 
 
@@ -117,10 +127,10 @@ def cpu_threads():
     return len(os.sched_getaffinity(0))
 
 
-def cpu_baseline(shapes, budget_s, group_size=128):
+def cpu_baseline(shapes, budget_s, group_size=128, dtype=torch.bfloat16):
     """The oracle (oracle/awq_oracle.c, OpenMP over rows) on a bounded sample of the SAME
     workload: the tensor set in processing order, pass after pass, until about budget_s of
-    CPU work (the last tensor may be cut to a row block).  Returns (GB/s of bf16 input,
+    CPU work (the last tensor may be cut to a row block).  Returns (GB/s of input,
     seconds, bytes, tensors, threads)."""
     from oracle import awq_oracle as orc
     threads = orc.set_threads(cpu_threads())
@@ -140,12 +150,12 @@ def cpu_baseline(shapes, budget_s, group_size=128):
                 take = max(1, int(rows * remaining / est))
             key = (take, K)
             if key not in cache:
-                cache[key] = (torch.randn(take, K, generator=g) * 0.02).to(torch.bfloat16)
+                cache[key] = (torch.randn(take, K, generator=g) * 0.02).to(dtype)
             x = cache[key]
             t0 = time.perf_counter()
             orc.quantize_groups(x, take, K, group_size, 4, False)
             t_total += time.perf_counter() - t0
-            done_bytes += x.numel() * 2
+            done_bytes += x.numel() * x.element_size()
             parts += 1
     return done_bytes / t_total / 1e9, t_total, done_bytes, parts, threads
 
@@ -194,12 +204,13 @@ def main():
 
     shapes = shapes_of(args.workload)
     elems = sum(int(torch.Size(s).numel()) for s in shapes)
-    in_bytes = elems * 2
+    dtype = DTYPES[args.dtype]
+    in_bytes = elems * torch.empty((), dtype=dtype).element_size()
     reps = args.replicas or max(1, -(-(1 << 30) // in_bytes))   # >= 1 GiB of inputs in rotation
     batches = []
     for r in range(reps):
         seed0 = (rank * 64 + r) * 100003
-        inputs = make_set(shapes, seed0, dev)
+        inputs = make_set(shapes, seed0, dev, dtype)
         batches.append(PackedBatch(inputs, bits=args.bits, symmetric=args.symmetric, parity=args.parity,
                                    group_size=args.group_size))
     torch.cuda.synchronize()
@@ -255,13 +266,16 @@ def main():
         key = f"{args.workload}.b{args.bits}.{'sym' if args.symmetric else 'asym'}.{'parity' if args.parity else 'packed'}"
         if args.group_size != 128:
             key += f".gs{args.group_size}"
+        if args.dtype != "bf16":
+            key += f".{args.dtype}"
         traffic = tj.get(key, {}).get("hbm_bytes_per_launch")
     except (OSError, ValueError):
         pass
     line = {
-        "metric": METRIC.replace("group_size=128", f"group_size={args.group_size}"), "value": round(value, 3), "unit": "GB/s", "n_gpus": world, "steps": args.steps,
+        "metric": METRIC.replace("group_size=128", f"group_size={args.group_size}").replace("bf16", args.dtype),
+        "value": round(value, 3), "unit": "GB/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
-        "scaling": "weak", "vs_baseline": None, "dtype": "bf16", "data": "synthetic",
+        "scaling": "weak", "vs_baseline": None, "dtype": args.dtype, "data": "synthetic",
         "config": {"workload": f"{args.workload}: {DESCR[args.workload]}", "tensors": len(shapes),
                    "elements": elems, "group_size": args.group_size, "bits": args.bits, "symmetric": args.symmetric,
                    "outputs": "qweight+qzeros+fp16 scales" + (" + int32 tensor_q/zero_points" if args.parity else ""),
@@ -278,7 +292,7 @@ def main():
         line["roofline"]["copy_ceiling"] = round(ceiling, 1)
         line["roofline"]["frac_of_copy"] = round(achieved / ceiling, 4)
     if not args.no_cpu_baseline:
-        gbs, secs, nbytes, nparts, threads = cpu_baseline(shapes, args.cpu_sample_seconds, args.group_size)
+        gbs, secs, nbytes, nparts, threads = cpu_baseline(shapes, args.cpu_sample_seconds, args.group_size, dtype)
         line["cpu_baseline"] = {"value": round(gbs, 5), "unit": "GB/s", "cores": threads, "kind": "port",
                                 "sample": f"oracle/awq_oracle.c (OpenMP over rows, {threads} threads) on "
                                           f"{nbytes / 1e6:.1f} MB of the {args.workload} set ({nparts} tensors/row-"

@@ -22,12 +22,12 @@ run() {  # run <name> <seconds> <cmd...>
 }
 run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || exit 1
 run pytest_gpu 1200 python -m pytest tests -m gpu -q --maxfail=30 -p no:cacheprovider
-run bench 600 python bench.py --steps 20 --warmup 5
+run bench 600 python bench.py
 for WL in ${BENCH_EXTRA:-}; do
   run bench_$WL 900 python bench.py --workload $WL --steps 10 --warmup 3 --no-cpu-baseline
 done
 if [ "${PROFILE:-1}" = 1 ]; then
   run rocprof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- \
-      python bench.py --steps 20 --warmup 5 --no-cpu-baseline
+      python bench.py --no-cpu-baseline
 fi
 echo done

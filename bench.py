@@ -10,6 +10,8 @@ asymmetric (the CLI default, reference main.py:59-63), outputs = packed qweight/
 fp16 scales, inputs resident in HBM.  Multi-GPU: one process per GPU (torchrun); every
 rank quantizes its own replica of the tensor set (weak scaling, no data-path collective:
 tensors are independent).  value = all ranks' input bytes / max-over-ranks time.
+--shard: strong scaling instead — one copy of the set, its tensor list LPT-sharded over the
+ranks (the CLI's torchrun mode), value = the set's bytes / max-over-ranks time.
 
 Usage: python bench.py [--gpus N --steps K --warmup W --workload opt-125m]
        N>1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
@@ -75,6 +77,10 @@ def parse():
     ap.add_argument("--group-size", type=int, default=128, choices=[32, 64, 128, 256],
                     help="128 = the BASELINE metric; other sizes are extra lines (metric names the size)")
     ap.add_argument("--parity", action="store_true", help="also write unpacked int32 tensor_q/zero_points")
+    ap.add_argument("--shard", action="store_true",
+                    help="strong scaling: ONE copy of the tensor set, its tensor list LPT-sharded across the "
+                         "ranks (distributed.shard, the CLI's torchrun mode; SURVEY 8e) instead of a replica "
+                         "per rank")
     ap.add_argument("--replicas", type=int, default=0,
                     help="input replicas rotated across steps (0 = enough to exceed the 256 MiB Infinity Cache)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -89,10 +95,14 @@ def parse():
 DTYPES = {"bf16": torch.bfloat16, "f16": torch.float16, "f32": torch.float32}
 
 
-def make_set(shapes, seed0, dev, dtype=torch.bfloat16):
+def make_set(shapes, seed0, dev, dtype=torch.bfloat16, only=None):
+    """Synthetic N(0, 0.02) tensors, tensor i seeded by seed0 + i; `only`: the indices to
+    materialise (a rank's shard)."""
     g = torch.Generator(device=dev)
     tensors = {}
     for i, s in enumerate(shapes):
+        if only is not None and i not in only:
+            continue
         g.manual_seed(seed0 + i)
         tensors[f"t{i:04d}"] = (torch.randn(*s, generator=g, device=dev, dtype=torch.float32) * 0.02).to(dtype)
     return tensors
@@ -160,19 +170,35 @@ def cpu_baseline(shapes, budget_s, group_size=128, dtype=torch.bfloat16):
     return done_bytes / t_total / 1e9, t_total, done_bytes, parts, threads
 
 
-def gather_leg(batch, rank, world, dev, backend, iters=3):
+def packed_out_shapes(shape, bits, gs):
+    """qweight / qzeros / scales shapes and dtypes of one tensor's packed outputs (PackedBatch)."""
+    rows = 1 if len(shape) <= 1 else shape[0]
+    K = int(torch.Size(shape).numel()) // rows
+    G, per = K // gs, 32 // bits
+    return {"qweight": ((rows, -(-K // per)), torch.int32), "qzeros": ((rows, -(-G // per)), torch.int32),
+            "scales": ((rows, G), torch.float16)}
+
+
+def gather_leg(batch, rank, world, dev, backend, iters=3, shard_owner=None, all_shapes=None, bits=4, gs=128):
     """N>1 only, after the timed region: the CLI's exchange step (distributed.gather_to_rank0,
-    one coalesced message per peer) on every rank's packed outputs of one replica.  Reported
-    beside `value`, never inside it (the gather is a separate line)."""
+    one coalesced message per peer) on every rank's packed outputs of one replica (or, with
+    --shard, of its shard: the real exchange of the CLI's torchrun mode).  Reported beside
+    `value`, never inside it (the gather is a separate line)."""
     from awq_quantizer import distributed as D
     comm = dev if backend == "nccl" else torch.device("cpu")
     fields = ("qweight", "qzeros", "scales")
     owner, shapes = {}, {}
-    for r in range(world):
-        for n in batch.names:
-            owner[f"{r}/{n}"] = r
-            shapes[f"{r}/{n}"] = {f: (tuple(batch.out[n][f].shape), batch.out[n][f].dtype) for f in fields}
-    local = {f"{rank}/{n}": {f: batch.out[n][f].to(comm) for f in fields} for n in batch.names}
+    if shard_owner is None:
+        for r in range(world):
+            for n in batch.names:
+                owner[f"{r}/{n}"] = r
+                shapes[f"{r}/{n}"] = {f: (tuple(batch.out[n][f].shape), batch.out[n][f].dtype) for f in fields}
+        local = {f"{rank}/{n}": {f: batch.out[n][f].to(comm) for f in fields} for n in batch.names}
+    else:
+        for i, r in enumerate(shard_owner):
+            owner[f"t{i:04d}"] = r
+            shapes[f"t{i:04d}"] = packed_out_shapes(all_shapes[i], bits, gs)
+        local = {n: {f: batch.out[n][f].to(comm) for f in fields} for n in batch.names}
     per_rank = sum(batch.out[n][f].numel() * batch.out[n][f].element_size() for n in batch.names for f in fields)
     D.gather_to_rank0(local, owner, shapes, comm)                     # warmup (connects the P2P channels)
     torch.cuda.synchronize(dev)
@@ -183,10 +209,15 @@ def gather_leg(batch, rank, world, dev, backend, iters=3):
     torch.cuda.synchronize(dev)
     D.barrier()
     t = D.max_over_ranks((time.perf_counter() - t0) / iters, dev)
-    moved = per_rank * (world - 1)
-    return {"what": "gather of every rank's packed outputs (one replica) to rank 0, one P2P message per peer "
-                    f"({backend}); outside the timed region", "bytes_to_rank0": moved,
-            "ms": round(t * 1e3, 3), "GBs_into_rank0": round(moved / t / 1e9, 2)}
+    if shard_owner is None:
+        moved = per_rank * (world - 1)
+    else:
+        moved = sum(int(torch.Size(sh).numel()) * torch.empty((), dtype=dt).element_size()
+                    for i, r in enumerate(shard_owner) if r != 0 for sh, dt in shapes[f"t{i:04d}"].values())
+    what = ("gather of the other ranks' packed shards to rank 0" if shard_owner is not None else
+            "gather of every rank's packed outputs (one replica) to rank 0")
+    return {"what": what + f", one P2P message per peer ({backend}); outside the timed region",
+            "bytes_to_rank0": moved, "ms": round(t * 1e3, 3), "GBs_into_rank0": round(moved / t / 1e9, 2)}
 
 
 def main():
@@ -202,15 +233,29 @@ def main():
     torch.cuda.set_device(dev)
     _hip.require_device(dev)
 
-    shapes = shapes_of(args.workload)
-    elems = sum(int(torch.Size(s).numel()) for s in shapes)
+    all_shapes = shapes_of(args.workload)
     dtype = DTYPES[args.dtype]
-    in_bytes = elems * torch.empty((), dtype=dtype).element_size()
-    reps = args.replicas or max(1, -(-(1 << 30) // in_bytes))   # >= 1 GiB of inputs in rotation
+    esize = torch.empty((), dtype=dtype).element_size()
+    if args.shard:
+        # strong scaling: rank r quantizes the tensors LPT assigns it (tensor i is seeded by
+        # its index, so the data do not depend on the world size)
+        owner = D.shard([int(torch.Size(s).numel()) for s in all_shapes], world)
+        mine = [i for i in range(len(all_shapes)) if owner[i] == rank]
+    else:
+        mine = list(range(len(all_shapes)))
+    shapes = [all_shapes[i] for i in mine]
+    elems = sum(int(torch.Size(s).numel()) for s in shapes)
+    total_elems = sum(int(torch.Size(s).numel()) for s in all_shapes)
+    in_bytes = elems * esize
+    # bytes all ranks quantize per step: the whole set once (shard) or one replica per rank
+    step_bytes = total_elems * esize if args.shard else in_bytes * world
+    reps = args.replicas or max(1, -(-(1 << 30) // max(1, in_bytes)))   # >= 1 GiB of inputs in rotation
     batches = []
     for r in range(reps):
-        seed0 = (rank * 64 + r) * 100003
-        inputs = make_set(shapes, seed0, dev, dtype)
+        if args.shard:
+            inputs = make_set(all_shapes, r * 100003, dev, dtype, only=set(mine))
+        else:
+            inputs = make_set(shapes, (rank * 64 + r) * 100003, dev, dtype)
         batches.append(PackedBatch(inputs, bits=args.bits, symmetric=args.symmetric, parity=args.parity,
                                    group_size=args.group_size))
     torch.cuda.synchronize()
@@ -249,7 +294,9 @@ def main():
     ceiling = None if args.no_copy_ceiling or rank != 0 else copy_ceiling(dev, stream)
 
     elapsed = D.max_over_ranks(elapsed, dev)
-    gather = gather_leg(batches[0], rank, world, dev, backend) if world > 1 and not args.no_gather else None
+    gather = (gather_leg(batches[0], rank, world, dev, backend, shard_owner=owner if args.shard else None,
+                         all_shapes=all_shapes, bits=args.bits, gs=args.group_size)
+              if world > 1 and not args.no_gather else None)
 
     if rank != 0:
         if world > 1:
@@ -257,7 +304,7 @@ def main():
             dist.destroy_process_group()
         return
 
-    value = in_bytes * world * args.steps / elapsed / 1e9
+    value = step_bytes * args.steps / elapsed / 1e9
     achieved = algo_bytes / kern_avg_s / 1e9
     traffic = None
     try:
@@ -275,12 +322,14 @@ def main():
         "metric": METRIC.replace("group_size=128", f"group_size={args.group_size}").replace("bf16", args.dtype),
         "value": round(value, 3), "unit": "GB/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
-        "scaling": "weak", "vs_baseline": None, "dtype": args.dtype, "data": "synthetic",
-        "config": {"workload": f"{args.workload}: {DESCR[args.workload]}", "tensors": len(shapes),
-                   "elements": elems, "group_size": args.group_size, "bits": args.bits, "symmetric": args.symmetric,
+        "scaling": "strong" if args.shard else "weak", "vs_baseline": None, "dtype": args.dtype, "data": "synthetic",
+        "config": {"workload": f"{args.workload}: {DESCR[args.workload]}", "tensors": len(all_shapes),
+                   "elements": total_elems, "group_size": args.group_size, "bits": args.bits, "symmetric": args.symmetric,
                    "outputs": "qweight+qzeros+fp16 scales" + (" + int32 tensor_q/zero_points" if args.parity else ""),
                    "launches_per_step": 1, "input_replicas_rotated": reps,
-                   "parallelism": f"dp{world} (each rank quantizes its own replica of the tensor set)"},
+                   "parallelism": (f"shard{world} (tensor list LPT-sharded over the ranks; rank 0 holds "
+                                   f"{len(shapes)} tensors, {elems} elements)") if args.shard else
+                                  f"dp{world} (each rank quantizes its own replica of the tensor set)"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                      "algorithmic_bytes_per_launch": algo_bytes,

@@ -233,6 +233,43 @@ def test_bench_two_ranks_gpu():
     assert line["exchange"]["ms"] > 0
 
 
+@pytest.mark.gpu
+def test_bench_two_ranks_shard_gpu():
+    """bench.py --shard (strong scaling: the opt-125m tensor list LPT-sharded over 2 ranks,
+    gloo on the box's one GPU): value counts the set once, the gather moves exactly the peer's
+    packed shard (derived here from distributed.shard and the packed output shapes)."""
+    import socket
+    import subprocess
+    import sys
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    import bench
+    from awq_quantizer import distributed as D
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    env = dict(os.environ, AWQ_DIST_BACKEND="gloo")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.join(root, "bench.py"), "--gpus", "2",
+           "--steps", "3", "--warmup", "1", "--workload", "opt-125m", "--shard", "--replicas", "1",
+           "--no-cpu-baseline", "--no-copy-ceiling"]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300, cwd=root)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert line["n_gpus"] == 2 and line["scaling"] == "strong" and line["value"] > 0
+    assert line["config"]["elements"] == 125239296 and line["config"]["parallelism"].startswith("shard2")
+    shapes = bench.shapes_of("opt-125m")
+    owner = D.shard([int(torch.Size(s).numel()) for s in shapes], 2)
+    want = 0
+    for i, sh in enumerate(shapes):
+        if owner[i] == 1:
+            for (dims, dt) in bench.packed_out_shapes(sh, 4, 128).values():
+                want += int(torch.Size(dims).numel()) * torch.empty((), dtype=dt).element_size()
+    assert line["exchange"]["bytes_to_rank0"] == want
+
+
 def test_act_stats_file_and_flags(tmp_path):
     from awq_quantizer.main import load_act_stats, main, parse_args
     a = parse_args(["--model_id", "m", "--output_dir", "o", "--scale_method", "awq", "--act_stats", "s.st",

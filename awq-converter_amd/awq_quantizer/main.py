@@ -33,7 +33,7 @@ import threading
 import time
 from collections import deque
 from concurrent.futures import ThreadPoolExecutor
-from typing import Dict, List, Optional, Tuple
+from typing import Callable, Dict, List, Optional, Tuple
 
 import torch
 
@@ -207,26 +207,97 @@ def save_model_in_chunks(tensors: Dict[str, Dict[str, torch.Tensor]], output_dir
     tensor_to_chunk = {}
     for c in range(num_chunks):
         chunk_names = names[c * chunk_size:(c + 1) * chunk_size]
-        chunk = {n: tensors[n] for n in chunk_names}
         for n in chunk_names:
             tensor_to_chunk[n] = c
-        path = os.path.join(output_dir, f"model_chunk_{c:04d}")
-        if use_safetensors:
-            from safetensors.torch import save_file
-            save_file(_flatten(chunk), path + ".safetensors")
-            if logger:
-                logger.info(f"Saved chunk {c + 1}/{num_chunks} with {len(chunk)} tensors in safetensors format")
-        else:
-            torch.save(chunk, path + ".pt")
-            if logger:
-                logger.info(f"Saved chunk {c + 1}/{num_chunks} with {len(chunk)} tensors in PyTorch format")
+        _write_chunk({n: tensors[n] for n in chunk_names}, output_dir, c, use_safetensors, logger,
+                     f"{c + 1}/{num_chunks}")
+    _write_metadata(output_dir, num_chunks, chunk_size, tensor_to_chunk, use_safetensors, len(names), qparams,
+                    logger)
+
+
+def _write_chunk(chunk: Dict[str, Dict[str, torch.Tensor]], output_dir: str, c: int, use_safetensors: bool,
+                 logger=None, label: str = "") -> None:
+    path = os.path.join(output_dir, f"model_chunk_{c:04d}")
+    if use_safetensors:
+        from safetensors.torch import save_file
+        save_file(_flatten(chunk), path + ".safetensors")
+        if logger:
+            logger.info(f"Saved chunk {label or c + 1} with {len(chunk)} tensors in safetensors format")
+    else:
+        torch.save(chunk, path + ".pt")
+        if logger:
+            logger.info(f"Saved chunk {label or c + 1} with {len(chunk)} tensors in PyTorch format")
+
+
+def _write_metadata(output_dir, num_chunks, chunk_size, tensor_to_chunk, use_safetensors, num_tensors, qparams,
+                    logger=None) -> None:
     meta = {"num_chunks": num_chunks, "chunk_size": chunk_size, "tensor_to_chunk": tensor_to_chunk,
-            "format": "safetensors" if use_safetensors else "pytorch", "num_tensors": len(names),
+            "format": "safetensors" if use_safetensors else "pytorch", "num_tensors": num_tensors,
             "quantization_params": qparams}
     with open(os.path.join(output_dir, "metadata.json"), "w") as f:
         json.dump(meta, f, indent=2)
     if logger:
         logger.info("Saved metadata file with tensor mapping")
+
+
+class ChunkWriter:
+    """save_model_in_chunks while the GPU pipeline is still running: a writer thread walks the
+    tensors in processing order (bytes descending, main.py:259) and writes chunk c as soon as
+    its chunk_size successful tensors are on the host, so disk writes overlap the reads and
+    kernels of later batches.  Output files and metadata.json are identical to
+    save_model_in_chunks on the finished dict (failed tensors are skipped in the same order;
+    chunk numbers are only known once every earlier tensor has finished)."""
+
+    def __init__(self, order: List[str], output_dir: str, chunk_size: int, use_safetensors: bool, logger=None):
+        self.order, self.dir, self.size, self.st, self.logger = order, output_dir, chunk_size, use_safetensors, logger
+        self.status: Dict[str, Optional[Dict[str, torch.Tensor]]] = {}
+        self.closed = False
+        self.error: Optional[BaseException] = None
+        self.cv = threading.Condition()
+        os.makedirs(output_dir, exist_ok=True)
+        self.thread = threading.Thread(target=self._run, daemon=True)
+        self.thread.start()
+
+    def done(self, name: str, result: Optional[Dict[str, torch.Tensor]]) -> None:
+        """A tensor finished: its host result dict, or None if it failed."""
+        with self.cv:
+            self.status[name] = result
+            self.cv.notify()
+
+    def _run(self) -> None:
+        try:
+            chunk, c, t2c, qparams, n_ok = {}, 0, {}, None, 0
+            for name in self.order:
+                with self.cv:
+                    while name not in self.status and not self.closed:
+                        self.cv.wait()
+                    res = self.status.pop(name, None)
+                if res is None:
+                    continue
+                if qparams is None:
+                    qparams = {k: (res[k].item() if k in res else None) for k in ("bits", "group_size", "symmetric")}
+                chunk[name] = res
+                t2c[name] = c
+                n_ok += 1
+                if len(chunk) == self.size:
+                    _write_chunk(chunk, self.dir, c, self.st, self.logger)
+                    chunk, c = {}, c + 1
+            if chunk:
+                _write_chunk(chunk, self.dir, c, self.st, self.logger)
+                c += 1
+            if n_ok:
+                _write_metadata(self.dir, c, self.size, t2c, self.st, n_ok, qparams, self.logger)
+        except BaseException as e:  # noqa: BLE001  (reported by close())
+            self.error = e
+
+    def close(self) -> None:
+        """Every producer has finished: unfinished tensors count as failed; wait for the writes."""
+        with self.cv:
+            self.closed = True
+            self.cv.notify()
+        self.thread.join()
+        if self.error is not None:
+            raise self.error
 
 
 def _to_cpu(d: Dict[str, torch.Tensor]) -> Dict[str, torch.Tensor]:
@@ -304,7 +375,8 @@ def quantize_stream(loader, infos: List[TensorInfo], quantizer: AWQQuantizer, de
                     lookahead: int, packed: bool, out: Dict, lock: threading.Lock, logger,
                     memory_efficient: bool = False, keep_on_device: bool = False,
                     batch_bytes: int = 1 << 30, export_autoawq: bool = False,
-                    act_stats: Optional[Dict[str, Tuple[torch.Tensor, torch.Tensor]]] = None) -> None:
+                    act_stats: Optional[Dict[str, Tuple[torch.Tensor, torch.Tensor]]] = None,
+                    on_done: Optional[Callable[[str, Optional[Dict[str, torch.Tensor]]], None]] = None) -> None:
     """Quantize `infos` on one GPU as a pipeline over batches of tensors (<= batch_bytes of
     input each):
 
@@ -341,9 +413,11 @@ def quantize_stream(loader, infos: List[TensorInfo], quantizer: AWQQuantizer, de
         ev.synchronize()
         with lock:
             out.update(results)
-        if logger:
-            for name in results:
+        for name in results:
+            if logger:
                 logger.info(f"Successfully quantized tensor: {name} on {device}")
+            if on_done:
+                on_done(name, results[name])
 
     with ThreadPoolExecutor(max_workers=max(1, readers)) as pool:
         futs = {}
@@ -363,6 +437,8 @@ def quantize_stream(loader, infos: List[TensorInfo], quantizer: AWQQuantizer, de
                 except Exception as e:  # noqa: BLE001
                     if logger:
                         logger.error(f"Failed to quantize tensor {info.name} on {device}: {e}")
+                    if on_done:
+                        on_done(info.name, None)
             if not host:
                 continue
             if logger:
@@ -391,8 +467,11 @@ def quantize_stream(loader, infos: List[TensorInfo], quantizer: AWQQuantizer, de
                 ev_k = torch.cuda.Event()
                 ev_k.record(compute)
             for name in host:
-                if name not in res and logger:
-                    logger.error(f"Failed to quantize tensor {name} on {device}")
+                if name not in res:
+                    if logger:
+                        logger.error(f"Failed to quantize tensor {name} on {device}")
+                    if on_done:
+                        on_done(name, None)
             if keep_on_device:
                 ev_k.synchronize()
                 with lock:
@@ -537,20 +616,29 @@ def main(argv: Optional[List[str]] = None) -> int:
         lock = threading.Lock()
         lookahead = max(1, args.prefetch_factor * args.batch_size)
         packed = args.output_format in ("packed", "autoawq")
+        # chunked output written while later batches are still being read and quantized
+        # (AWQ_CLI_SERIAL_SAVE=1: after everything, like the reference)
+        writer = None
+        if not autoawq and os.environ.get("AWQ_CLI_SERIAL_SAVE", "0") != "1":
+            writer = ChunkWriter([i.name for i in ordered], args.output_dir, args.chunk_size, args.save_safetensors,
+                                 logger)
         threads = []
         for d, part in zip(devices, parts):
             logger.info(f"Processing {len(part)} tensors on {d}")
             th = threading.Thread(target=_device_worker, args=(loader, part, quantizers[d], d, args.num_workers,
                                                                lookahead, packed, results, lock, logger,
                                                                args.memory_efficient, False, 1 << 30, autoawq),
-                                  kwargs={"act_stats": act_stats})
+                                  kwargs={"act_stats": act_stats, "on_done": writer.done if writer else None})
             th.start()
             threads.append(th)
         for th in threads:
             th.join()
+        TIMINGS["quantize_s"] = time.time() - start
 
         quantized = {i.name: results[i.name] for i in ordered if i.name in results}   # size-descending
         if not quantized:
+            if writer is not None:
+                writer.close()
             logger.error("No tensors were successfully quantized")
             return 1
         logger.info(f"Successfully quantized {len(quantized)} tensors")
@@ -558,12 +646,15 @@ def main(argv: Optional[List[str]] = None) -> int:
         try:
             if autoawq:
                 save_autoawq(quantized, loader, passthrough, args.output_dir, args, logger)
+            elif writer is not None:
+                writer.close()
             else:
                 save_model_in_chunks(quantized, args.output_dir, chunk_size=args.chunk_size,
                                      use_safetensors=args.save_safetensors, logger=logger)
         except Exception as e:  # noqa: BLE001
             logger.error(f"Failed to save quantized model: {e}")
             return 1
+        TIMINGS["total_s"] = time.time() - start
         logger.info(f"Quantization complete in {time.time() - start:.2f} seconds")
         return 0
     except SystemExit:
@@ -577,6 +668,7 @@ def main(argv: Optional[List[str]] = None) -> int:
 
 
 _SCALARS = ("bits", "group_size", "symmetric", "shape")
+TIMINGS: Dict[str, float] = {}   # phase times of the last main() call (scripts/cli_bench.py)
 
 
 def _main_distributed(args, loader, ordered: List[TensorInfo], logger, start: float,

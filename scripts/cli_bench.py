@@ -24,6 +24,8 @@ import bench  # noqa: E402
 
 def build_model(path, workload, shards):
     shapes = bench.shapes_of(workload)
+    if os.path.exists(os.path.join(path, "complete")):    # reuse a model built by an earlier run (--workdir)
+        return sum(int(torch.Size(s).numel()) * 2 for s in shapes)
     g = torch.Generator().manual_seed(0)
     names = [f"model.layers.{i // 8}.t{i}.weight" for i in range(len(shapes))]
     per = -(-len(shapes) // shards)
@@ -35,6 +37,7 @@ def build_model(path, workload, shards):
             nbytes += part[n].numel() * 2
         if part:
             save_file(part, os.path.join(path, f"model-{sh:05d}-of-{shards:05d}.safetensors"))
+    open(os.path.join(path, "complete"), "w").close()
     return nbytes
 
 
@@ -46,7 +49,8 @@ def main():
     ap.add_argument("--workdir", default=None)
     ap.add_argument("--repeat", type=int, default=2)
     args = ap.parse_args()
-    from awq_quantizer.main import main as cli
+    from awq_quantizer import main as cli_mod
+    cli = cli_mod.main
     work = args.workdir or tempfile.mkdtemp(prefix="awq_cli_")
     model = os.path.join(work, "model")
     os.makedirs(model, exist_ok=True)
@@ -62,7 +66,9 @@ def main():
         out_bytes = sum(os.path.getsize(os.path.join(out, f)) for f in os.listdir(out))
         print(json.dumps({"workload": args.workload, "format": args.format, "run": r, "input_GB": round(nbytes / 1e9, 3),
                           "output_GB": round(out_bytes / 1e9, 3), "wall_s": round(wall, 3),
-                          "input_GBs": round(nbytes / wall / 1e9, 3), "model_build_s": round(build_s, 1)}), flush=True)
+                          "input_GBs": round(nbytes / wall / 1e9, 3), "model_build_s": round(build_s, 1),
+                          "serial_save": os.environ.get("AWQ_CLI_SERIAL_SAVE", "0") == "1",
+                          "phases_s": {k: round(v, 3) for k, v in cli_mod.TIMINGS.items()}}), flush=True)
         shutil.rmtree(out, ignore_errors=True)
     if args.workdir is None:
         shutil.rmtree(work, ignore_errors=True)

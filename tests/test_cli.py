@@ -89,6 +89,53 @@ def test_save_layout(tmp_path):
 
 
 @pytest.mark.skipif(torch.cuda.is_available(), reason="checks the no-GPU exit code")
+@pytest.mark.parametrize("use_st", [False, True])
+def test_chunk_writer_matches_serial_save(tmp_path, use_st):
+    """ChunkWriter (chunks written while the pipeline runs, out-of-order completions from
+    several threads, some tensors failing) produces exactly save_model_in_chunks' files."""
+    import random
+    import threading
+    from safetensors.torch import load_file
+    from awq_quantizer.main import ChunkWriter, save_model_in_chunks
+    order = [f"layer.{i}.weight" for i in range(23)]
+    failed = {order[3], order[10], order[11]}
+    res = {n: {"qweight": torch.full((4, 2), i, dtype=torch.int32), "scales": torch.full((4, 1), i, dtype=torch.float16),
+               "bits": torch.tensor(4, dtype=torch.int32), "group_size": torch.tensor(128, dtype=torch.int32),
+               "symmetric": torch.tensor(False)} for i, n in enumerate(order)}
+    w = ChunkWriter(order, str(tmp_path / "a"), 5, use_st, writers=3)
+    names = order[:]
+    random.Random(0).shuffle(names)
+    ths = [threading.Thread(target=lambda part: [w.done(n, None if n in failed else res[n]) for n in part],
+                            args=(names[k::3],)) for k in range(3)]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join()
+    w.close()
+    ok = {n: res[n] for n in order if n not in failed}
+    save_model_in_chunks(ok, str(tmp_path / "b"), chunk_size=5, use_safetensors=use_st)
+    a_files, b_files = sorted(os.listdir(tmp_path / "a")), sorted(os.listdir(tmp_path / "b"))
+    assert a_files == b_files and len(a_files) == 5          # 20 tensors -> 4 chunks + metadata
+    assert json.load(open(tmp_path / "a" / "metadata.json")) == json.load(open(tmp_path / "b" / "metadata.json"))
+    for f in a_files:
+        if f.endswith(".pt"):
+            x, y = torch.load(tmp_path / "a" / f, weights_only=True), torch.load(tmp_path / "b" / f, weights_only=True)
+            assert list(x) == list(y) and all(torch.equal(x[n][k], y[n][k]) for n in x for k in x[n])
+        elif f.endswith(".safetensors"):
+            x, y = load_file(str(tmp_path / "a" / f)), load_file(str(tmp_path / "b" / f))
+            assert list(x) == list(y) and all(torch.equal(x[k], y[k]) for k in x)
+
+
+def test_chunk_writer_close_marks_unfinished_failed(tmp_path):
+    from awq_quantizer.main import ChunkWriter
+    order = ["a", "b", "c"]
+    w = ChunkWriter(order, str(tmp_path), 2, False, writers=1)
+    w.done("a", {"q": torch.zeros(1), "bits": torch.tensor(4)})
+    w.close()                      # "b", "c" never reported (a device worker died): skipped
+    meta = json.load(open(tmp_path / "metadata.json"))
+    assert meta["num_tensors"] == 1 and meta["tensor_to_chunk"] == {"a": 0}
+
+
 def test_main_without_gpu_returns_1(tmp_path):
     from awq_quantizer.main import main
     d = _model_dir(tmp_path, _tensors())

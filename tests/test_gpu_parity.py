@@ -227,20 +227,22 @@ def test_full_size_properties(shape):
     assert torch.equal(pk["scales"][rows].cpu(), ref["scales"])
 
 
-@pytest.mark.parametrize("blocks", ["1", "3", "8"])
-def test_grid_stride_loop(blocks, monkeypatch):
+@pytest.mark.parametrize("blocks,gs,dtype", [("1", 128, torch.bfloat16), ("3", 128, torch.bfloat16),
+                                             ("8", 128, torch.bfloat16), ("3", 32, torch.bfloat16),
+                                             ("5", 256, torch.float16), ("3", 64, torch.float32)], ids=str)
+def test_grid_stride_loop(blocks, gs, dtype, monkeypatch):
     """Force a tiny grid (AWQ_HIP_MAX_BLOCKS) so every wave walks many tiles/tensors."""
     from awq_quantizer.quantization.batch import PackedBatch
     monkeypatch.setenv("AWQ_HIP_MAX_BLOCKS", blocks)
     dev = torch.device(DEV, 0)
-    shapes = [(300, 4096), (768,), (50, 768), (7, 1792), (4096,), (33, 384)]
-    inputs = {f"t{i}": rand_bf16(s, 400 + i, 0.02).to(dev) for i, s in enumerate(shapes)}
-    b = PackedBatch(inputs, bits=4, symmetric=False, parity=True)
+    shapes = [s for s in [(300, 4096), (768,), (50, 768), (7, 1792), (4096,), (33, 384)] if s[-1] % gs == 0]
+    inputs = {f"t{i}": rand_bf16(s, 400 + i, 0.02, dtype).to(dev) for i, s in enumerate(shapes)}
+    b = PackedBatch(inputs, bits=4, symmetric=False, parity=True, group_size=gs)
     b.run()
     torch.cuda.synchronize()
-    q = Q(bits=4, symmetric=False)
+    q = Q(bits=4, symmetric=False, group_size=gs)
     for name, x in inputs.items():
-        ref = orc.quantize(x.cpu(), bits=4, group_size=128, symmetric=False)
+        ref = orc.quantize(x.cpu(), bits=4, group_size=gs, symmetric=False)
         o = b.out[name]
         assert torch.equal(o["tensor_q"].cpu(), ref["tensor_q"]), name
         assert torch.equal(o["qweight"].cpu(), orc.pack_rows(ref["tensor_q"], 4, 0)), name

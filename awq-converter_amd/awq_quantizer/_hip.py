@@ -15,7 +15,7 @@ import torch
 
 LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib")
 LIB_PATH = os.path.join(LIB_DIR, "libawq_hip.so")
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 AWQ_DTYPE = {torch.bfloat16: 0, torch.float16: 1, torch.float32: 2, torch.float64: 3}
 
@@ -54,7 +54,8 @@ SIGNATURES = {
     "awq_weight_colsum": (_I32, [_P, _I32, _I64, _I64, _I64, _P, _P, _P]),
     "awq_column_mean": (_I32, [_P, _I64, _I64, ctypes.c_double, _P, _P]),
     "awq_act_scale_table": (_I32, [_P, _P, _I64, _I32, _P, _P]),
-    "awq_act_search_losses": (_I32, [_P, _I32, _I64, _I64, _I64, _I32, _I32, _P, _I32, _P, _P, _I64, _P]),
+    "awq_act_recip_table": (_I32, [_P, _I32, _I64, _P, _P]),
+    "awq_act_search_losses": (_I32, [_P, _I32, _I64, _I64, _I64, _I32, _I32, _P, _P, _I32, _P, _P, _I64, _P]),
     "awq_act_search_select": (_I32, [_P, _I32, _I64, _P, _I64, _P, _P, _P, _P, _P]),
     "awq_apply_input_scale": (_I32, [_P, _I32, _I64, _I64, _P, _P, _P]),
 }
@@ -278,18 +279,33 @@ def act_scale_table(x_mean: torch.Tensor, w_mean: Optional[torch.Tensor], n_grid
     return table
 
 
+def act_recip_table(table: torch.Tensor) -> torch.Tensor:
+    """RN(1 / table) where the loss kernel's Markstein quotient is proven exact, else 0."""
+    n_grid, K = table.shape
+    rtable = torch.empty_like(table)
+    check(load_library().awq_act_recip_table(ptr(table), n_grid, K, ptr(rtable), _stream(table)),
+          "awq_act_recip_table")
+    return rtable
+
+
 def act_search_losses(weights, x_sq: torch.Tensor, table: torch.Tensor, group_size: int, bits: int,
-                      symmetric: bool) -> torch.Tensor:
-    """Per-group losses of every candidate: part fp32 [n_grid, total groups of all linears]."""
+                      symmetric: bool, rtable: Optional[torch.Tensor] = None, use_rtable: bool = True) -> torch.Tensor:
+    """Per-group losses of every candidate: part fp32 [n_grid, total groups of all linears].
+    rtable: act_recip_table(table) (computed here unless given; use_rtable=False: IEEE
+    divisions, same results)."""
     lib = load_library()
     n_grid, K = table.shape
+    if use_rtable and rtable is None:
+        rtable = act_recip_table(table)
+    if not use_rtable:
+        rtable = None
     groups = [w.shape[0] * (K // group_size) for w in weights]
     stride = sum(groups)
     part = torch.empty((n_grid, stride), dtype=torch.float32, device=table.device)
     off = 0
     for w, g in zip(weights, groups):
         check(lib.awq_act_search_losses(ptr(w), AWQ_DTYPE[w.dtype], w.shape[0], K, group_size, bits,
-                                        int(bool(symmetric)), ptr(table), n_grid, ptr(x_sq),
+                                        int(bool(symmetric)), ptr(table), ptr(rtable), n_grid, ptr(x_sq),
                                         ctypes.c_void_p(part.data_ptr() + 4 * off), stride, _stream(w)),
               "awq_act_search_losses")
         off += g

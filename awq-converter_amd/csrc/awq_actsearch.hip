@@ -35,8 +35,29 @@ __device__ __forceinline__ float hw_rn_bf16(float a) {   // v_cvt_pk_bf16_f32: R
 }
 __device__ __forceinline__ float hw_rn_f16(float a) { return (float)(_Float16)opq(a); }   // v_cvt_f16_f32: RNE
 
+// RN_f32(1/s) for a bf16-valued s: v_rcp_f32 + one Newton step, correctly rounded for every
+// bf16 s < 2^126 (awq_selftest checks all of them against IEEE 1/s); IEEE division beyond
+__device__ __forceinline__ float recip_bf16(float s) {
+    if (__builtin_expect(!(s < 0x1p126f), 0)) return 1.0f / s;
+    const float r0 = __builtin_amdgcn_rcpf(s);
+    const float e = __builtin_fmaf(-s, r0, 1.0f);
+    return __builtin_fmaf(r0, e, r0);
+}
+
 template <int DT> struct HwFmt;
 template <> struct HwFmt<AWQ_DTYPE_BF16> {
+    __device__ static float lo() { return __uint_as_float(0x2EDC0000u); }   // RN_bf16(1e-10)
+    // RN(d / qr) for bf16 d, qr in {15, 255}: d * RN(1/qr) (the same exhaustive identity)
+    __device__ static float scale(float d, float qr, float rq) {
+        (void)qr;
+        return hw_rn_bf16(d * rq);
+    }
+    __device__ static float recip(float s) { return recip_bf16(s); }
+    // RN(x / s) for any s >= RN(1e-10) incl. inf / NaN (r = 0 / NaN carries them)
+    __device__ static float quot_any(float x, float s, float r) {
+        (void)s;
+        return hw_rn_bf16(x * r);
+    }
     __device__ static float rn(float a) { return hw_rn_bf16(a); }
     // RN(x / s) = RN_bf16(x * RN_f32(1/s)) for bf16 x and bf16 s >= RN_bf16(1e-10)
     // (exhaustive, oracle/verify_recip.c)
@@ -46,6 +67,16 @@ template <> struct HwFmt<AWQ_DTYPE_BF16> {
     }
 };
 template <> struct HwFmt<AWQ_DTYPE_F16> {
+    __device__ static float lo() { return 0.0f; }                           // RN_f16(1e-10) = 0
+    __device__ static float scale(float d, float qr, float rq) {   // IEEE: d may be inf (Markstein would NaN)
+        (void)rq;
+        return hw_rn_f16(opq(d) / qr);
+    }
+    __device__ static float recip(float s) { return 1.0f / s; }
+    __device__ static float quot_any(float x, float s, float r) {          // IEEE: s may be 0 / inf / NaN
+        (void)r;
+        return hw_rn_f16(opq(x) / s);
+    }
     __device__ static float rn(float a) { return hw_rn_f16(a); }
     // Markstein-corrected quotient, exact for every fp16 x and positive finite fp16 s
     // (oracle/verify_recip.c f16m)
@@ -55,6 +86,111 @@ template <> struct HwFmt<AWQ_DTYPE_F16> {
         return hw_rn_f16(__builtin_fmaf(e, r, q0));
     }
 };
+// fp32 weights: every op is the fp32 op itself, x / s the IEEE division
+template <> struct HwFmt<AWQ_DTYPE_F32> {
+    __device__ static float lo() { return 1e-10f; }
+    __device__ static float scale(float d, float qr, float rq) {
+        (void)rq;
+        return d / qr;
+    }
+    __device__ static float recip(float s) { return 1.0f / s; }
+    __device__ static float quot_any(float x, float s, float r) {
+        (void)r;
+        return x / s;
+    }
+    __device__ static float rn(float a) { return a; }
+    __device__ static float quot(float x, float s, float r) {
+        (void)r;
+        return x / s;
+    }
+};
+
+// awq.py:196-213 with the hardware identities above (same results as refmath::group_params:
+// qmin = 0 whenever the zero point is used, so RN(qmin - y) is exact, and rint of a value of
+// the dtype is again a value of the dtype); also returns r = RN_f32(1 / s) for the element
+// path.
+template <int DT>
+__device__ __forceinline__ void hw_group_params(float mn, float mx, int nan, int qmin, int qmax, int sym, float rq,
+                                                float& s_out, float& z_out, float& r_out) {
+    typedef HwFmt<DT> H;
+    if (sym) {                                                // awq.py:196-199
+        float amn = __builtin_fabsf(mn), amx = __builtin_fabsf(mx);
+        if (nan) { amn = mn; amx = mx; }
+        const float a = (amx > amn) ? amx : amn;
+        mn = -a;
+        mx = a;
+    }
+    float s = H::scale(H::rn(mx - mn), (float)(qmax - qmin), rq);   // awq.py:202
+    if (!(s != s) && s < H::lo()) s = H::lo();                        // awq.py:205
+    const float r = H::recip(s);
+    float z = 0.0f;
+    if (!sym)                                                 // awq.py:210-211
+        z = clampq(__builtin_rintf((float)qmin - H::quot_any(mn, s, r)), (float)qmin, (float)qmax);
+    s_out = s;
+    z_out = z;
+    r_out = r;
+}
+
+// Reductions over the lpg consecutive lanes of a group (lpg a power of two <= 64), every
+// lane getting the result: DPP inside 16-lane rows (quad perms, half-row / row mirrors —
+// after the earlier steps these pair exactly the lanes an xor butterfly pairs), permlane
+// swaps across rows.  fmin/fmax skip NaN (NaN is tracked separately); the sum adds
+// own + partner at every level like the xor butterfly (the canonical tree, include/awq_hip.h).
+template <int CTRL>
+__device__ __forceinline__ float dppf(float v) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), CTRL, 0xF, 0xF, true));
+}
+template <int CTRL>
+__device__ __forceinline__ int dppi(int v) {
+    return __builtin_amdgcn_mov_dpp(v, CTRL, 0xF, 0xF, true);
+}
+// the two 16-lane rows (or 32-lane halves) of a pair, swapped: lane l sees {its pair's
+// first half, its pair's second half} whichever half it is in, so combining p.x and p.y
+// symmetrically (min, max, or, +) gives every lane f(own, partner) exactly
+__device__ __forceinline__ void swap16(unsigned u, unsigned& a, unsigned& b) {
+    const auto p = __builtin_amdgcn_permlane16_swap(u, u, false, false);
+    a = p[0];
+    b = p[1];
+}
+__device__ __forceinline__ void swap32(unsigned u, unsigned& a, unsigned& b) {
+    const auto p = __builtin_amdgcn_permlane32_swap(u, u, false, false);
+    a = p[0];
+    b = p[1];
+}
+__device__ __forceinline__ float fbits(unsigned u) { return __builtin_bit_cast(float, u); }
+__device__ __forceinline__ unsigned ubits(float f) { return __builtin_bit_cast(unsigned, f); }
+
+template <bool ROW32>
+__device__ __forceinline__ void minmax_cross(float& mn, float& mx, int& nan) {
+    unsigned a, b;
+    if (ROW32) swap32(ubits(mn), a, b); else swap16(ubits(mn), a, b);
+    mn = __builtin_fminf(fbits(a), fbits(b));
+    if (ROW32) swap32(ubits(mx), a, b); else swap16(ubits(mx), a, b);
+    mx = __builtin_fmaxf(fbits(a), fbits(b));
+    if (ROW32) swap32((unsigned)nan, a, b); else swap16((unsigned)nan, a, b);
+    nan = (int)(a | b);
+}
+
+__device__ __forceinline__ void grp_minmax(float& mn, float& mx, int& nan, int lpg) {
+    if (lpg >= 2) { mn = __builtin_fminf(mn, dppf<0xB1>(mn)); mx = __builtin_fmaxf(mx, dppf<0xB1>(mx)); nan |= dppi<0xB1>(nan); }
+    if (lpg >= 4) { mn = __builtin_fminf(mn, dppf<0x4E>(mn)); mx = __builtin_fmaxf(mx, dppf<0x4E>(mx)); nan |= dppi<0x4E>(nan); }
+    if (lpg >= 8) { mn = __builtin_fminf(mn, dppf<0x141>(mn)); mx = __builtin_fmaxf(mx, dppf<0x141>(mx)); nan |= dppi<0x141>(nan); }
+    if (lpg >= 16) { mn = __builtin_fminf(mn, dppf<0x140>(mn)); mx = __builtin_fmaxf(mx, dppf<0x140>(mx)); nan |= dppi<0x140>(nan); }
+    if (lpg >= 32) minmax_cross<false>(mn, mx, nan);
+    if (lpg >= 64) minmax_cross<true>(mn, mx, nan);
+}
+
+__device__ __forceinline__ float grp_sum(float v, int lpg) {
+    if (lpg >= 2) v = v + dppf<0xB1>(v);
+    if (lpg >= 4) v = v + dppf<0x4E>(v);
+    if (lpg >= 8) v = v + dppf<0x141>(v);
+    if (lpg >= 16) v = v + dppf<0x140>(v);
+    unsigned x, y;
+    if (lpg >= 32) { swap16(ubits(v), x, y); v = fbits(x) + fbits(y); }   // own + partner, either order
+    if (lpg >= 64) { swap32(ubits(v), x, y); v = fbits(x) + fbits(y); }
+    return v;
+}
+
 
 constexpr int kRowBlock = 256;     // rows per canonical fp64 column-sum block
 constexpr int kGroupBlock = 1024;  // groups per canonical fp64 loss block
@@ -224,14 +360,27 @@ __global__ __launch_bounds__(256) void scale_table_kernel(const float* __restric
 // (awq.py:459-539), ŵ = dq / s_i (fp32), e = ŵ - w, loss = sum x_sq[k] * (e * e): each
 // lane sums its 8 elements in order, then the xor-butterfly (pairwise) tree over the
 // group's LPG lanes; part[i * stride + r * G + g] (fp32).
+// ŵ = RN_f32(dq / s) from rs = RN_f32(1 / s) with one Markstein correction: exact for every
+// fp16-valued dq and every s in [2^-60, 2^60] (awq_selftest 1: all 2^23 mantissas of s x
+// every positive finite fp16 dq, 2.7e11 pairs, against the IEEE division; the steps are
+// scale-invariant while no intermediate leaves the normal range, which this s range keeps)
+__device__ __forceinline__ float mquot(float a, float s, float rs) {
+    const float q0 = a * rs;
+    const float r = __builtin_fmaf(-s, q0, a);
+    return __builtin_fmaf(r, rs, q0);
+}
+
 template <int DT>
 __global__ __launch_bounds__(256) void act_loss_kernel(const void* __restrict__ w, int64_t R, int64_t K, int lpg,
                                                        int qmin, int qmax, int sym, const float* __restrict__ table,
-                                                       int n_grid, const float* __restrict__ x_sq,
-                                                       float* __restrict__ part, int64_t stride) {
+                                                       const float* __restrict__ rtable, int n_grid,
+                                                       const float* __restrict__ x_sq, float* __restrict__ part,
+                                                       int64_t stride) {
+    typedef HwFmt<DT> H;
     const int64_t G = K / (8 * lpg);
     const int64_t nw = (int64_t)gridDim.x * 4;
     const bool leader = (threadIdx.x & 63) % lpg == 0;
+    const float rq = 1.0f / (float)(qmax - qmin);   // RN_f32(1 / 15) or RN_f32(1 / 255)
     for (int64_t item = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);; item += nw) {
         GroupLane gl;
         if (!group_lane(item, R, G, lpg, gl)) break;
@@ -242,41 +391,58 @@ __global__ __launch_bounds__(256) void act_loss_kernel(const void* __restrict__ 
         for (int i = 0; i < n_grid; ++i) {
             float s[8], ws[8];
             load8<AWQ_DTYPE_F32>(table, (int64_t)i * K + gl.k0, s);
+            // min / max skipping NaN (fmin / fmax; the signs of zero extrema cannot change the
+            // scale or zero point) with NaN tracked on the side: torch's NaN-propagating
+            // min / max once combined
             float mn = __builtin_inff(), mx = -__builtin_inff();
             int nan = 0;
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
-                if (DT == AWQ_DTYPE_F32) ws[j] = v[j] * s[j];
-                else ws[j] = HwFmt<DT == AWQ_DTYPE_F32 ? AWQ_DTYPE_BF16 : DT>::rn(v[j] * s[j]);
+                ws[j] = H::rn(v[j] * s[j]);
                 nan |= ws[j] != ws[j];
-                mn = ws[j] < mn ? ws[j] : mn;
-                mx = ws[j] > mx ? ws[j] : mx;
+                mn = __builtin_fminf(mn, ws[j]);
+                mx = __builtin_fmaxf(mx, ws[j]);
             }
-            for (int o = 1; o < lpg; o <<= 1) {
-                const float a = __shfl_xor(mn, o, 64), b = __shfl_xor(mx, o, 64);
-                mn = a < mn ? a : mn;
-                mx = b > mx ? b : mx;
-                nan |= __shfl_xor(nan, o, 64);
-            }
+            grp_minmax(mn, mx, nan, lpg);
             if (nan) { mn = __builtin_nanf(""); mx = __builtin_nanf(""); }
-            float cs, cz;
-            group_params<DT>(mn, mx, nan, qmin, qmax, sym, cs, cz);
+            float cs, cz, r;
+            hw_group_params<DT>(mn, mx, nan, qmin, qmax, sym, rq, cs, cz, r);
             float acc = 0.0f;
-            if (DT != AWQ_DTYPE_F32 && cs > 0.0f && cs < __builtin_inff()) {
+            // channel reciprocals for ŵ = dq / s (0 = outside the proven range: IEEE division)
+            float rs[8];
+            bool mq = false;
+            if (rtable != nullptr) {
+                load8<AWQ_DTYPE_F32>(rtable, (int64_t)i * K + gl.k0, rs);
+                float m = rs[0];
+#pragma unroll
+                for (int j = 1; j < 8; ++j) m = __builtin_fminf(m, rs[j]);
+                mq = __builtin_amdgcn_ballot_w64(!(m > 0.0f)) == 0;   // wave-uniform
+            }
+            if (cs > 0.0f && cs < __builtin_inff()) {
                 // finite positive scale (every group but constant fp16 / inf / NaN ones):
                 // RN(w'/s) from the group's reciprocal, hardware RNE conversions; q - z is an
                 // integer |.| <= 510, exact in fp16, so only the product is rounded
-                typedef HwFmt<DT == AWQ_DTYPE_F32 ? AWQ_DTYPE_BF16 : DT> H;
-                const float r = 1.0f / cs;
                 const float sh = (float)(_Float16)cs;
+                float dq[8];
 #pragma unroll
                 for (int j = 0; j < 8; ++j) {
                     const float t = H::quot(ws[j], cs, r);
                     const float u = sym ? t : H::rn(t + cz);
                     const float q = __builtin_amdgcn_fmed3f(__builtin_rintf(u), (float)qmin, (float)qmax);
-                    const float dq = hw_rn_f16((q - cz) * sh);
-                    const float e = dq / s[j] - v[j];
-                    acc = acc + h[j] * (e * e);
+                    dq[j] = hw_rn_f16((q - cz) * sh);
+                }
+                if (mq) {
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) {
+                        const float e = mquot(dq[j], s[j], rs[j]) - v[j];
+                        acc = acc + h[j] * (e * e);
+                    }
+                } else {
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) {
+                        const float e = dq[j] / s[j] - v[j];
+                        acc = acc + h[j] * (e * e);
+                    }
                 }
             } else {
                 const float sh = sw_f16_to_f32(canon_f16(cs));
@@ -289,7 +455,7 @@ __global__ __launch_bounds__(256) void act_loss_kernel(const void* __restrict__ 
                     acc = acc + h[j] * (e * e);
                 }
             }
-            for (int o = 1; o < lpg; o <<= 1) acc = acc + __shfl_xor(acc, o, 64);
+            acc = grp_sum(acc, lpg);
             if (gl.valid && leader) part[(int64_t)i * stride + gl.r * G + gl.g] = acc;
         }
     }
@@ -413,16 +579,51 @@ hipError_t launch_scale_table(const float* x_mean, const float* w_mean, int64_t 
     return hipPeekAtLastError();
 }
 
+// rtable[i] = RN_f32(1 / table[i]) inside [2^-60, 2^60] (mquot's proven range), else 0
+__global__ __launch_bounds__(256) void recip_table_kernel(const float* __restrict__ table, int64_t n,
+                                                          float* __restrict__ rtable) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const float s = table[i];
+    rtable[i] = (s >= 0x1p-60f && s <= 0x1p60f) ? 1.0f / s : 0.0f;
+}
+
+// awq_selftest 1: mquot == IEEE division for every s in [1, 2) (all 2^23 mantissas) and every
+// positive finite fp16 a; counts mismatches
+__global__ __launch_bounds__(256) void selftest_mquot_kernel(unsigned long long* mismatches) {
+    const uint32_t m = blockIdx.x * 256 + threadIdx.x;
+    if (m >= (1u << 23)) return;
+    const float s = __uint_as_float(0x3F800000u | m);
+    const float rs = 1.0f / s;
+    unsigned long long bad = 0;
+    for (uint32_t h = 1; h < 0x7C00u; ++h) {
+        const float a = (float)__builtin_bit_cast(_Float16, (uint16_t)h);
+        bad += __float_as_uint(mquot(a, s, rs)) != __float_as_uint(a / s);
+    }
+    if (bad) atomicAdd(mismatches, bad);
+}
+
+hipError_t launch_recip_table(const float* table, int64_t n, float* rtable, hipStream_t stream) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(recip_table_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, table, n, rtable);
+    return hipPeekAtLastError();
+}
+
+hipError_t launch_selftest_mquot(unsigned long long* out, hipStream_t stream) {
+    hipLaunchKernelGGL(selftest_mquot_kernel, dim3((1u << 23) / 256), dim3(256), 0, stream, out);
+    return hipPeekAtLastError();
+}
+
 hipError_t launch_act_losses(const void* w, int dtype, int64_t R, int64_t K, int64_t L, int bits, int symmetric,
-                             const float* table, int n_grid, const float* x_sq, float* part, int64_t stride,
-                             hipStream_t stream) {
+                             const float* table, const float* rtable, int n_grid, const float* x_sq, float* part,
+                             int64_t stride, hipStream_t stream) {
     const int qmin = symmetric ? -(1 << (bits - 1)) : 0;
     const int qmax = symmetric ? (1 << (bits - 1)) - 1 : (1 << bits) - 1;
     const int lpg = (int)(L / 8);
     const int64_t items = ((R + (64 / lpg) - 1) / (64 / lpg)) * (K / L);
     const unsigned grid = blocks_for(items, 4, 256 * 32);
     AWQ_DT_SWITCH(dtype, hipLaunchKernelGGL((act_loss_kernel<D>), dim3(grid), dim3(256), 0, stream, w, R, K, lpg,
-                                            qmin, qmax, symmetric, table, n_grid, x_sq, part, stride))
+                                            qmin, qmax, symmetric, table, rtable, n_grid, x_sq, part, stride))
     return hipPeekAtLastError();
 }
 

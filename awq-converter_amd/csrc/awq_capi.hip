@@ -317,9 +317,19 @@ int awq_act_scale_table(const float* x_mean, const float* w_mean, int64_t K, int
                       "awq scale table");
 }
 
+int awq_act_recip_table(const float* table, int n_grid, int64_t K, float* rtable, void* stream) {
+    g_err.clear();
+    if (n_grid < 1 || n_grid > AWQ_ACT_MAX_GRID)
+        return fail(AWQ_EINVAL, "n_grid must be in [1, %d] (got %d)", AWQ_ACT_MAX_GRID, n_grid);
+    if (K <= 0) return fail(AWQ_EINVAL, "K must be positive");
+    if (!table || !rtable) return fail(AWQ_EINVAL, "null argument");
+    return hip_status(awq::launch_recip_table(table, (int64_t)n_grid * K, rtable, (hipStream_t)stream),
+                      "awq recip table");
+}
+
 int awq_act_search_losses(const void* w, int dtype, int64_t rows, int64_t K, int64_t group_size, int bits,
-                          int symmetric, const float* table, int n_grid, const float* x_sq, float* part,
-                          int64_t part_stride, void* stream) {
+                          int symmetric, const float* table, const float* rtable, int n_grid, const float* x_sq,
+                          float* part, int64_t part_stride, void* stream) {
     g_err.clear();
     if (bits != 4 && bits != 8) return fail(AWQ_EINVAL, "Unsupported bit width: %d. Supported: 4, 8.", bits);
     if (int rc = check_act_shape(dtype, rows, K, group_size)) return rc;
@@ -327,10 +337,11 @@ int awq_act_search_losses(const void* w, int dtype, int64_t rows, int64_t K, int
         return fail(AWQ_EINVAL, "n_grid must be in [1, %d] (got %d)", AWQ_ACT_MAX_GRID, n_grid);
     if (part_stride < rows * (K / group_size)) return fail(AWQ_EINVAL, "part_stride smaller than the group count");
     if (!w || !table || !x_sq || !part) return fail(AWQ_EINVAL, "null argument");
-    if (!aligned(w, 16) || !aligned(table, 16) || !aligned(x_sq, 16) || !aligned(part, 4))
-        return fail(AWQ_EINVAL, "weights, table and x_sq must be 16-B aligned");
-    return hip_status(awq::launch_act_losses(w, dtype, rows, K, group_size, bits, symmetric, table, n_grid, x_sq,
-                                             part, part_stride, (hipStream_t)stream), "awq act losses");
+    if (!aligned(w, 16) || !aligned(table, 16) || !aligned(x_sq, 16) || !aligned(part, 4) ||
+        (rtable && !aligned(rtable, 16)))
+        return fail(AWQ_EINVAL, "weights, table, rtable and x_sq must be 16-B aligned");
+    return hip_status(awq::launch_act_losses(w, dtype, rows, K, group_size, bits, symmetric, table, rtable, n_grid,
+                                             x_sq, part, part_stride, (hipStream_t)stream), "awq act losses");
 }
 
 int awq_act_search_select(const float* part, int n_grid, int64_t part_stride, const float* table, int64_t K,
@@ -358,6 +369,7 @@ int awq_apply_input_scale(const void* w, int dtype, int64_t rows, int64_t K, con
 int awq_selftest(int which, unsigned long long* result, void* stream) {
     g_err.clear();
     if (!result) return fail(AWQ_EINVAL, "null result pointer");
+    if (which == 1) return hip_status(awq::launch_selftest_mquot(result, (hipStream_t)stream), "awq selftest");
     if (which != 0) return fail(AWQ_EINVAL, "unknown self-test %d", which);
     return hip_status(awq::launch_selftest(which, result, (hipStream_t)stream), "awq selftest");
 }

@@ -112,8 +112,10 @@ hipError_t launch_colmean(const double* part, int64_t nblk, int64_t K, double di
 hipError_t launch_scale_table(const float* x_mean, const float* w_mean, int64_t K, int n_grid, float* table,
                               hipStream_t stream);
 hipError_t launch_act_losses(const void* w, int dtype, int64_t R, int64_t K, int64_t L, int bits, int symmetric,
-                             const float* table, int n_grid, const float* x_sq, float* part, int64_t stride,
-                             hipStream_t stream);
+                             const float* table, const float* rtable, int n_grid, const float* x_sq, float* part,
+                             int64_t stride, hipStream_t stream);
+hipError_t launch_recip_table(const float* table, int64_t n, float* rtable, hipStream_t stream);
+hipError_t launch_selftest_mquot(unsigned long long* out, hipStream_t stream);
 hipError_t launch_act_select(const float* part, int n_grid, int64_t stride, const float* table, int64_t K,
                              double* work, double* losses, int32_t* best, float* s_best, hipStream_t stream);
 hipError_t launch_apply_scale(const void* w, int dtype, int64_t R, int64_t K, const float* s, void* out,

@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define AWQ_HIP_ABI_VERSION 5
+#define AWQ_HIP_ABI_VERSION 6
 
 /* dtype codes of the input weights (torch dtypes the reference accepts, awq.py:397) */
 enum { AWQ_DTYPE_BF16 = 0, AWQ_DTYPE_F16 = 1, AWQ_DTYPE_F32 = 2, AWQ_DTYPE_F64 = 3 };
@@ -205,9 +205,14 @@ int awq_column_mean(const double* partial, int64_t nblk, int64_t K, double divis
 /* table fp32 [n_grid, K]; w_mean NULL = no duo scaling */
 int awq_act_scale_table(const float* x_mean, const float* w_mean, int64_t K, int n_grid, float* table,
                         void* stream);
+/* rtable [n_grid, K] = RN_f32(1 / table) where table is in [2^-60, 2^60], else 0: lets the
+ * loss kernel form fp32(dq / s) as one Markstein-corrected product (exact there: awq_selftest
+ * 1), falling back to the IEEE division for a wave whose channels leave that range. */
+int awq_act_recip_table(const float* table, int n_grid, int64_t K, float* rtable, void* stream);
+/* rtable: awq_act_recip_table's output for the same table, or NULL (IEEE divisions) */
 int awq_act_search_losses(const void* w, int dtype, int64_t rows, int64_t K, int64_t group_size, int bits,
-                          int symmetric, const float* table, int n_grid, const float* x_sq, float* part,
-                          int64_t part_stride, void* stream);
+                          int symmetric, const float* table, const float* rtable, int n_grid, const float* x_sq,
+                          float* part, int64_t part_stride, void* stream);
 /* losses fp64 [n_grid], best int32 [1], s_best fp32 [K] (any may be NULL) */
 int awq_act_search_select(const float* part, int n_grid, int64_t part_stride, const float* table, int64_t K,
                           double* work, double* losses, int32_t* best, float* s_best, void* stream);
@@ -216,8 +221,10 @@ int awq_apply_input_scale(const void* w, int dtype, int64_t rows, int64_t K, con
                           void* stream);
 
 /* Device self-test (diagnostics).  which = 0: the fast reciprocal used by the streaming
- * kernel against IEEE 1/s over every bf16 s >= RN_bf16(1e-10); adds the number of
- * mismatches to *result (device unsigned long long, caller-zeroed). */
+ * kernel against IEEE 1/s over every bf16 s >= RN_bf16(1e-10); which = 1: the loss kernel's
+ * Markstein quotient against the IEEE division for every s in [1, 2) and every positive
+ * finite fp16 dividend; adds the number of mismatches to *result (device unsigned long
+ * long, caller-zeroed). */
 int awq_selftest(int which, unsigned long long* result, void* stream);
 
 #ifdef __cplusplus

@@ -119,13 +119,14 @@ def test_capi_validation_without_gpu():
     P = ctypes.c_void_p(16)
     assert lib.awq_act_scale_table(P, None, 128, 0, P, None) != 0
     assert "n_grid" in _hip.last_error()
-    assert lib.awq_act_search_losses(P, 0, 8, 384, 96, 4, 0, P, 4, P, P, 24, None) != 0
+    assert lib.awq_act_search_losses(P, 0, 8, 384, 96, 4, 0, P, None, 4, P, P, 24, None) != 0
     assert "power-of-two" in _hip.last_error()
-    assert lib.awq_act_search_losses(P, 3, 8, 256, 128, 4, 0, P, 4, P, P, 16, None) != 0
+    assert lib.awq_act_search_losses(P, 3, 8, 256, 128, 4, 0, P, None, 4, P, P, 16, None) != 0
     assert "bf16 / fp16 / fp32" in _hip.last_error()
-    assert lib.awq_act_search_losses(P, 0, 8, 256, 128, 4, 0, P, 4, P, P, 15, None) != 0
+    assert lib.awq_act_search_losses(P, 0, 8, 256, 128, 4, 0, P, None, 4, P, P, 15, None) != 0
     assert "part_stride" in _hip.last_error()
     assert lib.awq_act_stats(P, 0, 0, 128, P, P, P, None) != 0
+    assert lib.awq_act_recip_table(P, 0, 128, P, None) != 0 and "n_grid" in _hip.last_error()
 
 
 # ---------------------------------------------------------------- GPU: kernels vs oracle
@@ -199,6 +200,38 @@ def test_gpu_losses_bit_exact(dtype, gs, bits, sym):
     assert torch.equal(losses.cpu().view(torch.int64), ol.view(torch.int64))
     assert int(best.item()) == ob
     assert torch.equal(s_best.cpu(), table.cpu()[ob])
+
+
+@pytest.mark.gpu
+def test_selftest_markstein_quotient_exhaustive():
+    """The loss kernel's fp32(dq / s) from RN(1/s) + one Markstein correction == the IEEE
+    division for every s in [1, 2) and every positive finite fp16 dq (2.7e11 pairs; by scale
+    invariance this covers the whole range awq_act_recip_table enables)."""
+    from awq_quantizer import _hip
+    assert _hip.selftest(1, _gpu()) == 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16, torch.float32], ids=str)
+def test_gpu_losses_rtable_paths_agree(dtype):
+    """Markstein path (rtable) == IEEE path (no rtable) bit for bit, including a table whose
+    channels leave the proven range for part of the candidates (those waves fall back)."""
+    dev = _gpu()
+    from awq_quantizer import _hip
+    ws, x = _layer(21, rows=(64, 33), K=1024, dtype=dtype)
+    wl = [w.to(dev) for w in ws.values()]
+    xm, xs = orc.act_stats(x)
+    table = _hip.act_scale_table(xm.to(dev), None, 10)
+    table[3, 100] = 2.0 ** -70                 # outside [2^-60, 2^60]: IEEE fallback for those waves
+    table[7, 900] = 2.0 ** 70
+    rt = _hip.act_recip_table(table)
+    assert float(rt[3, 100]) == 0.0 and float(rt[7, 900]) == 0.0
+    assert torch.equal(rt.cpu()[:3], torch.ones(()) / table.cpu()[:3])      # IEEE fp32 1/s (CPU)
+    a = _hip.act_search_losses(wl, xs.to(dev), table, 128, 4, False, rtable=rt)
+    b = _hip.act_search_losses(wl, xs.to(dev), table, 128, 4, False, use_rtable=False)
+    assert torch.equal(a.view(torch.int32), b.view(torch.int32))
+    _, _, opart = orc.act_search_losses([w.cpu() for w in wl], xs, table.cpu(), 128, 4, False)
+    assert torch.equal(a.cpu().view(torch.int32), opart.view(torch.int32))
 
 
 @pytest.mark.gpu

@@ -231,7 +231,12 @@ def test_gpu_losses_rtable_paths_agree(dtype):
     b = _hip.act_search_losses(wl, xs.to(dev), table, 128, 4, False, use_rtable=False)
     assert torch.equal(a.view(torch.int32), b.view(torch.int32))
     _, _, opart = orc.act_search_losses([w.cpu() for w in wl], xs, table.cpu(), 128, 4, False)
-    assert torch.equal(a.cpu().view(torch.int32), opart.view(torch.int32))
+    # (fp16: the 2^70 channel overflows to inf, its groups' losses are NaN; NaN payloads are
+    # not part of the definition, so NaN positions are compared and the rest bit for bit)
+    a = a.cpu()
+    assert torch.equal(torch.isnan(a), torch.isnan(opart))
+    assert torch.equal(torch.where(torch.isnan(a), 0, a).view(torch.int32),
+                       torch.where(torch.isnan(opart), 0, opart).view(torch.int32))
 
 
 @pytest.mark.gpu

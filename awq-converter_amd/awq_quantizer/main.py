@@ -205,12 +205,17 @@ def save_model_in_chunks(tensors: Dict[str, Dict[str, torch.Tensor]], output_dir
     first = next(iter(tensors.values()))
     qparams = {k: (first[k].item() if k in first else None) for k in ("bits", "group_size", "symmetric")}
     tensor_to_chunk = {}
-    for c in range(num_chunks):
-        chunk_names = names[c * chunk_size:(c + 1) * chunk_size]
-        for n in chunk_names:
-            tensor_to_chunk[n] = c
-        _write_chunk({n: tensors[n] for n in chunk_names}, output_dir, c, use_safetensors, logger,
-                     f"{c + 1}/{num_chunks}")
+    # chunk files are independent: written by a small thread pool (torch.save releases the GIL)
+    with ThreadPoolExecutor(max_workers=min(8, max(2, (os.cpu_count() or 4) // 2))) as pool:
+        futs = []
+        for c in range(num_chunks):
+            chunk_names = names[c * chunk_size:(c + 1) * chunk_size]
+            for n in chunk_names:
+                tensor_to_chunk[n] = c
+            futs.append(pool.submit(_write_chunk, {n: tensors[n] for n in chunk_names}, output_dir, c,
+                                    use_safetensors, logger, f"{c + 1}/{num_chunks}"))
+        for f in futs:
+            f.result()
     _write_metadata(output_dir, num_chunks, chunk_size, tensor_to_chunk, use_safetensors, len(names), qparams,
                     logger)
 

@@ -416,8 +416,12 @@ def quantize_stream(loader, infos: List[TensorInfo], quantizer: AWQQuantizer, de
     batches = _batches(infos, batch_bytes)
     depth = max(1, lookahead // max(1, max(len(b) for b in batches) if batches else 1))
 
+    direct = hasattr(loader, "read_pinned") and os.environ.get("AWQ_CLI_MMAP_READ", "0") != "1"
+
     def read(info):
-        return _pinned_copy(loader.read(info))
+        # straight from the file into pinned memory (one copy); AWQ_CLI_MMAP_READ=1: the
+        # safetensors mmap read + a pinned copy (two)
+        return loader.read_pinned(info) if direct else _pinned_copy(loader.read(info))
 
     inflight = deque()
 

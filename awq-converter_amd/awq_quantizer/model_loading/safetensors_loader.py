@@ -7,9 +7,14 @@ and load_tensors() contract, and adds what the MI355X path needs:
 
   * tensor_index(): names / dtypes / shapes / sizes from the file headers only;
   * read(name): one tensor at a time (memory-mapped slice of its file), so the CLI can
-    stream weights host -> HBM while the previous tensor is being quantized.
+    stream weights host -> HBM while the previous tensor is being quantized;
+  * read_pinned(name): the same bytes read straight from the file into page-locked host
+    memory (one pread per tensor at the offset the file header gives; the GIL is released
+    during the read, so reader threads run in parallel), ready for an async H2D copy.
 """
+import json
 import os
+import struct
 import threading
 from typing import Dict, Iterator, List, Optional, Tuple
 
@@ -61,6 +66,9 @@ class SafetensorsLoader:
         self.tensors: Dict[str, torch.Tensor] = {}
         self._index: Optional[List[TensorInfo]] = None
         self._handles = {}
+        self._layouts: Dict[str, Tuple[int, Dict[str, Tuple[int, int]]]] = {}
+        self._fds: Dict[str, int] = {}
+        self._lock = threading.Lock()
 
     # ---- header-only index (file order, key order of safe_open) ----
     def tensor_index(self) -> List[TensorInfo]:
@@ -88,6 +96,52 @@ class SafetensorsLoader:
             h = safe_open(info.file, framework="pt")
             self._handles[key] = h
         return h.get_tensor(info.name)
+
+    def _layout(self, path: str) -> Tuple[int, Dict[str, Tuple[int, int]]]:
+        """(data start, name -> (begin, end) byte offsets) from a safetensors header:
+        8-byte little-endian header length, JSON header, then the data block."""
+        with self._lock:
+            lay = self._layouts.get(path)
+            if lay is None:
+                with open(path, "rb") as f:
+                    n = struct.unpack("<Q", f.read(8))[0]
+                    hdr = json.loads(f.read(n))
+                lay = (8 + n, {k: tuple(v["data_offsets"]) for k, v in hdr.items() if k != "__metadata__"})
+                self._layouts[path] = lay
+                self._fds[path] = os.open(path, os.O_RDONLY)
+            return lay
+
+    def read_pinned(self, info: TensorInfo) -> torch.Tensor:
+        """Read one tensor into page-locked host memory."""
+        if info.dtype is None:
+            raise ValueError(f"{info.name}: unsupported dtype")
+        return self.read_into(info, torch.empty(info.shape, dtype=info.dtype, pin_memory=True))
+
+    def read_into(self, info: TensorInfo, out: torch.Tensor) -> torch.Tensor:
+        """Read one tensor's bytes from its file into `out` (contiguous CPU tensor of the
+        tensor's dtype and shape) with pread at the header's offsets."""
+        start, offs = self._layout(info.file)
+        begin, end = offs[info.name]
+        nbytes = end - begin
+        if not out.is_contiguous() or nbytes != out.numel() * out.element_size():
+            raise ValueError(f"{info.name}: header size {nbytes} B does not match the destination "
+                             f"{tuple(out.shape)} {out.dtype}")
+        if nbytes:
+            view = memoryview(out.view(-1).view(torch.uint8).numpy())
+            fd, pos, done = self._fds[info.file], start + begin, 0
+            while done < nbytes:
+                got = os.preadv(fd, [view[done:]], pos + done)
+                if got <= 0:
+                    raise IOError(f"{info.name}: short read at byte {done} of {nbytes}")
+                done += got
+        return out
+
+    def close(self) -> None:
+        with self._lock:
+            for fd in self._fds.values():
+                os.close(fd)
+            self._fds.clear()
+            self._layouts.clear()
 
     def iter_tensors(self) -> Iterator[Tuple[str, torch.Tensor]]:
         for info in self.tensor_index():

@@ -136,6 +136,23 @@ def test_chunk_writer_close_marks_unfinished_failed(tmp_path):
     assert meta["num_tensors"] == 1 and meta["tensor_to_chunk"] == {"a": 0}
 
 
+def test_loader_read_into_matches_safetensors(tmp_path):
+    """read_into (pread at the header offsets, the CLI's pinned-read path) == safetensors'
+    own read for every dtype, empty tensors and several files."""
+    from awq_quantizer.model_loading import load_model_from_path
+    t = {"a": torch.randn(37, 129).to(torch.bfloat16), "b": torch.arange(10, dtype=torch.int32),
+         "c": torch.randn(5).half(), "d": torch.randn(3, 4, 5), "e": torch.zeros(0, 3), "f": torch.randn(7).double()}
+    loader = load_model_from_path(_model_dir(tmp_path, t, files=2), logger_level="ERROR")
+    for info in loader.tensor_index():
+        out = torch.empty(info.shape, dtype=info.dtype)
+        assert torch.equal(loader.read_into(info, out), t[info.name]), info.name
+        assert torch.equal(out, loader.read(info)), info.name
+    with pytest.raises(ValueError, match="header size"):
+        info = [i for i in loader.tensor_index() if i.name == "a"][0]
+        loader.read_into(info, torch.empty(36, 129, dtype=torch.bfloat16))
+    loader.close()
+
+
 def test_main_without_gpu_returns_1(tmp_path):
     from awq_quantizer.main import main
     d = _model_dir(tmp_path, _tensors())

@@ -52,7 +52,7 @@ class PackedBatch:
             if not _hip.ragged_eligible(x.dtype, rows, K, gs):
                 raise ValueError(f"{name}: shape {tuple(x.shape)} is not eligible for a ragged launch "
                                  f"(group_size {gs})")
-            G = K // gs
+            G = -(-K // gs)          # padded rows: the tail group counts (awq.py:337-339)
             o = {"scales": torch.empty((rows, G), dtype=torch.float16, device=dev)}
             if packed:
                 o["qweight"] = torch.empty((rows, -(-K // per)), dtype=torch.int32, device=dev)

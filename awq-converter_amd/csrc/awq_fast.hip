@@ -471,15 +471,32 @@ struct TileCtx {
     uint32_t G, WPR;     // geometry (see awq_internal.h)
     uint32_t r0, g0;     // row / group-in-row of the tile's first group
     uint32_t bytes;      // byte tiles (qzeros written byte-wise) vs word tiles
+    uint64_t el_off;     // first input / tensor_q element of the tile
+    uint32_t valid;      // elements of the tile inside the tensor (padded rows: inside the row)
+    uint64_t qw_off;     // first qweight word of the tile
+    uint32_t qw_n;       // qweight words of the tile
 };
 
 template <int BITS, int GS>
 __device__ __forceinline__ TileCtx make_ctx(const awq_tensor_desc& d, uint32_t tile) {
     constexpr uint32_t S = kTileElems / GS;
     const TensorGeom g = fast_geom(d.rows, d.K, BITS, GS);
+    constexpr uint32_t WPG = GS * BITS / 32;   // qweight words per group
     TileCtx c;
     c.bytes = g.bytes;
-    if (g.bytes) {
+    if (g.TR) {                                // padded rows: row tiles
+        const uint32_t r = tile / g.TR;
+        c.r0 = r;
+        c.g0 = (tile - r * g.TR) * S;
+        c.ng = min(S, g.G - c.g0);
+        c.start = r * g.G + c.g0;
+        c.w0 = r * g.WPR + c.g0 / g.C;
+        c.nw = (c.ng + g.C - 1) / g.C;
+        c.el_off = (uint64_t)r * (uint64_t)d.K + (uint64_t)c.g0 * GS;
+        c.valid = (uint32_t)min((int64_t)c.ng * GS, d.K - (int64_t)c.g0 * GS);
+        c.qw_off = (uint64_t)r * (uint64_t)(d.K * BITS / 32) + (uint64_t)c.g0 * WPG;
+        c.qw_n = c.valid * BITS / 32;
+    } else if (g.bytes) {
         c.start = tile * S;
         c.ng = min(S, (uint32_t)d.rows * g.G - c.start);
         c.r0 = c.start / g.G;
@@ -498,6 +515,12 @@ __device__ __forceinline__ TileCtx make_ctx(const awq_tensor_desc& d, uint32_t t
         c.w0 = w0;
         c.nw = w1 - w0;
     }
+    if (!g.TR) {
+        c.el_off = (uint64_t)c.start * GS;
+        c.valid = c.ng * GS;
+        c.qw_off = (uint64_t)c.start * WPG;
+        c.qw_n = c.ng * WPG;
+    }
     c.G = g.G;
     c.WPR = g.WPR;
     c.qweight = d.qweight;
@@ -508,21 +531,32 @@ __device__ __forceinline__ TileCtx make_ctx(const awq_tensor_desc& d, uint32_t t
     return c;
 }
 
-// first flat group and group count of a tile (the input byte range it reads)
+// first element and element count of a tile (the input range it reads; padded rows stop at
+// the row end, the range check supplies the zero padding)
 template <int BITS, int GS>
-__device__ __forceinline__ void tile_src(int64_t rows, int64_t K, uint32_t tile, uint32_t& start, uint32_t& ng) {
+__device__ __forceinline__ void tile_src(int64_t rows, int64_t K, uint32_t tile, uint64_t& el_off, uint32_t& valid) {
     constexpr uint32_t S = kTileElems / GS;
     const TensorGeom g = fast_geom(rows, K, BITS, GS);
+    if (g.TR) {
+        const uint32_t r = tile / g.TR;
+        const uint32_t g0 = (tile - r * g.TR) * S;
+        el_off = (uint64_t)r * (uint64_t)K + (uint64_t)g0 * GS;
+        valid = (uint32_t)min((int64_t)S * GS, K - (int64_t)g0 * GS);
+        return;
+    }
+    uint32_t start, ng;
     if (g.bytes) {
         start = tile * S;
         ng = min(S, (uint32_t)rows * g.G - start);
-        return;
+    } else {
+        const uint32_t w0 = tile * g.WPT;
+        const uint32_t w1 = min(w0 + g.WPT, g.words);
+        start = word_group(g, w0);
+        const uint32_t end = (w1 == g.words) ? (uint32_t)rows * g.G : word_group(g, w1);
+        ng = end - start;
     }
-    const uint32_t w0 = tile * g.WPT;
-    const uint32_t w1 = min(w0 + g.WPT, g.words);
-    start = word_group(g, w0);
-    const uint32_t end = (w1 == g.words) ? (uint32_t)rows * g.G : word_group(g, w1);
-    ng = end - start;
+    el_off = (uint64_t)start * GS;
+    valid = ng * GS;
 }
 
 // 4 x 16-B loads per lane: load j covers the tile's bytes [1 KiB j, 1 KiB (j+1)), lane l
@@ -532,9 +566,9 @@ __device__ __forceinline__ void tile_src(int64_t rows, int64_t K, uint32_t tile,
 // fp32: the same element mapping, each lane's 32 B as two 16-B loads (a pair of
 // instructions covers 2 KiB contiguously).
 template <typename F, int GS>
-__device__ __forceinline__ void load_tile(const char* wp, uint32_t ng, Chunk<F::NW> (&v)[4]) {
+__device__ __forceinline__ void load_tile(const char* wp, uint32_t valid, Chunk<F::NW> (&v)[4]) {
     const int lane = threadIdx.x & 63;
-    const __amdgpu_buffer_rsrc_t rw = rsrc(wp, ng * (uint32_t)(F::kBytes * GS));
+    const __amdgpu_buffer_rsrc_t rw = rsrc(wp, valid * (uint32_t)F::kBytes);
 #pragma unroll
     for (int j = 0; j < 4; ++j)
 #pragma unroll
@@ -648,7 +682,6 @@ __device__ __forceinline__ void compute_tile(const TileCtx& c, const Chunk<F::NW
     constexpr int L = GS / 8;            // lanes per group (8 elements = 16 B per lane)
     constexpr int GPJ = 64 / L;          // groups per load instruction
     constexpr uint32_t S = 4 * GPJ;      // group slots per tile
-    constexpr uint32_t WPG = GS * BITS / 32;   // qweight words per group
     const int lane = threadIdx.x & 63;
     const int grp = lane / L;            // group of this lane inside each load
     const int ch = lane % L;             // 16-B chunk of the group
@@ -659,7 +692,7 @@ __device__ __forceinline__ void compute_tile(const TileCtx& c, const Chunk<F::NW
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             const uint32_t word = v[j].w[0].x ^ v[j].w[0].y ^ v[j].w[0].z ^ v[j].w[F::NW - 1].w;
-            __amdgpu_buffer_rsrc_t rq = rsrc(c.qweight + (uint64_t)c.start * WPG, ng * WPG * 4u);
+            __amdgpu_buffer_rsrc_t rq = rsrc(c.qweight + c.qw_off, c.qw_n * 4u);
             __builtin_amdgcn_raw_buffer_store_b32(word, rq, (uint32_t)((64 * j + lane) * 4), 0, AWQ_STORE_AUX);
         }
     }
@@ -754,7 +787,7 @@ __device__ __forceinline__ void compute_tile(const TileCtx& c, const Chunk<F::NW
             if (BITS == 4) qstage[64 * j + lane] = word.x;
             else *(u2v*)(qstage + 128 * j + 2 * lane) = word;
 #else
-            __amdgpu_buffer_rsrc_t rq = rsrc(c.qweight + (uint64_t)c.start * WPG, ng * WPG * 4u);
+            __amdgpu_buffer_rsrc_t rq = rsrc(c.qweight + c.qw_off, c.qw_n * 4u);
             if (BITS == 4)
                 __builtin_amdgcn_raw_buffer_store_b32(word.x, rq, (uint32_t)((64 * j + lane) * 4), 0, AWQ_STORE_AUX);
             else
@@ -774,7 +807,7 @@ __device__ __forceinline__ void compute_tile(const TileCtx& c, const Chunk<F::NW
                     q[i] = (int32_t)((wd >> sh) & ((1u << BITS) - 1u)) + QMIN;
                 }
             }
-            __amdgpu_buffer_rsrc_t rt = rsrc(c.tensor_q + (uint64_t)c.start * GS, ng * (GS * 4u));
+            __amdgpu_buffer_rsrc_t rt = rsrc(c.tensor_q + c.el_off, c.valid * 4u);
             u4 lo = {(uint32_t)q[0], (uint32_t)q[1], (uint32_t)q[2], (uint32_t)q[3]};
             u4 hi = {(uint32_t)q[4], (uint32_t)q[5], (uint32_t)q[6], (uint32_t)q[7]};
             __builtin_amdgcn_raw_buffer_store_b128(lo, rt, (uint32_t)((512 * j + 8 * lane) * 4), 0, AWQ_STORE_AUX);
@@ -783,7 +816,7 @@ __device__ __forceinline__ void compute_tile(const TileCtx& c, const Chunk<F::NW
     }
 #if AWQ_WIDE_STORE
     if (c.qweight) {   // 4-bit: 1 KiB per tile = one dwordx4 per lane; 8-bit: 2 KiB, two
-        __amdgpu_buffer_rsrc_t rq = rsrc(c.qweight + (uint64_t)c.start * WPG, ng * WPG * 4u);
+        __amdgpu_buffer_rsrc_t rq = rsrc(c.qweight + c.qw_off, c.qw_n * 4u);
 #pragma unroll
         for (int h = 0; h < (BITS == 4 ? 1 : 2); ++h) {
             const u4 w4 = *(const u4*)(qstage + h * 256 + lane * 4);
@@ -933,10 +966,11 @@ void awq_fast_kernel(
         // the input range first (no division for byte tiles): the loads go out before the
         // rest of the tile context (row / group divisions) is computed
         const uint32_t tile = (uint32_t)(t - d.tile_begin);
-        uint32_t st, ng;
-        tile_src<BITS, GS>(d.rows, d.K, tile, st, ng);
+        uint64_t el_off;
+        uint32_t valid;
+        tile_src<BITS, GS>(d.rows, d.K, tile, el_off, valid);
         Chunk<F::NW> va[4];
-        load_tile<F, GS>((const char*)d.w + (uint64_t)st * GS * F::kBytes, ng, va);
+        load_tile<F, GS>((const char*)d.w + el_off * F::kBytes, valid, va);
 #ifdef AWQ_TRACE
         if (tr1 == 0) {
             tr1 = __builtin_amdgcn_s_memrealtime();

@@ -25,6 +25,12 @@ namespace awq {
 //     word is produced inside one tile:  WPR == 1 (G <= C): WPT = S / G whole rows,
 //     else WPT = S / C words (= S groups when every word is full).  S >= C always.
 // When G % C == 0 both tilings coincide (S-group tiles of whole words).
+// Padded rows (K % gs != 0, K % 8 == 0; the reference zero-pads each row's tail group,
+// awq.py:337-339): row tiles — a tile never leaves its row (tiles per row TR = ceil(G / S));
+// the loads stop at the row end (the buffer range check returns the padding zeros) and
+// every tile owns whole qzeros words (S is a multiple of C).  K % 8 == 0 keeps every
+// 8-element lane chunk, packed word and tensor_q store either wholly inside or wholly
+// outside the row.
 // ---------------------------------------------------------------------------
 constexpr int kTileElems = 2048;     // elements per wave-tile (4 loads x 64 lanes x 8)
 constexpr int kGroup = 128;          // the benchmark's group size (BASELINE.json)
@@ -49,23 +55,26 @@ struct TensorGeom {
     uint32_t words;  // R * WPR
     uint32_t bytes;  // 1 = byte tiles (see above), 0 = word tiles
     uint32_t S;      // group slots per tile
+    uint32_t TR;     // padded rows: tiles per row (0 = flat tiling)
 };
 
 __host__ __device__ inline TensorGeom fast_geom(int64_t R, int64_t K, int bits, int gs) {
     TensorGeom g;
     g.S = (uint32_t)(kTileElems / gs);
-    g.G = (uint32_t)(K / gs);
+    g.G = (uint32_t)((K + gs - 1) / gs);
     g.C = 32u / (uint32_t)bits;
     g.WPR = (g.G + g.C - 1) / g.C;
     g.WPT = (g.WPR == 1) ? (g.S / g.G) : (g.S / g.C);
     g.words = (uint32_t)R * g.WPR;
-    g.bytes = (bits == 8 || (g.G % 2u) == 0u) ? 1u : 0u;
+    g.TR = (K % gs) ? (g.G + g.S - 1) / g.S : 0u;
+    g.bytes = (!g.TR && (bits == 8 || (g.G % 2u) == 0u)) ? 1u : 0u;
     return g;
 }
 
 __host__ __device__ inline int64_t fast_tiles(int64_t R, int64_t K, int bits, int gs) {
     if (R <= 0 || K <= 0) return 0;
     TensorGeom g = fast_geom(R, K, bits, gs);
+    if (g.TR) return R * (int64_t)g.TR;
     if (g.bytes) return (R * (int64_t)g.G + g.S - 1) / g.S;
     return ((int64_t)g.words + g.WPT - 1) / g.WPT;
 }
@@ -77,10 +86,11 @@ __host__ __device__ inline uint32_t word_group(const TensorGeom& g, uint32_t w) 
     return row * g.G + wi * g.C;
 }
 
-// Limits of the fast path: flat group indices must fit 32 bits.
+// Limits of the fast path: whole groups, or padded rows with K % 8 == 0; flat group
+// indices must fit 32 bits.
 __host__ __device__ inline bool fast_shape_ok(int64_t R, int64_t K, int64_t gs) {
-    if (!fast_group_size(gs) || R <= 0 || K <= 0 || (K % gs) != 0) return false;
-    int64_t G = K / gs;
+    if (!fast_group_size(gs) || R <= 0 || K <= 0 || ((K % gs) != 0 && (K % 8) != 0)) return false;
+    int64_t G = (K + gs - 1) / gs;
     return R * G < (int64_t)0x7FFFFFFF && R * (G + 1) < (int64_t)0x7FFFFFFF;
 }
 

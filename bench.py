@@ -174,7 +174,7 @@ def packed_out_shapes(shape, bits, gs):
     """qweight / qzeros / scales shapes and dtypes of one tensor's packed outputs (PackedBatch)."""
     rows = 1 if len(shape) <= 1 else shape[0]
     K = int(torch.Size(shape).numel()) // rows
-    G, per = K // gs, 32 // bits
+    G, per = -(-K // gs), 32 // bits
     return {"qweight": ((rows, -(-K // per)), torch.int32), "qzeros": ((rows, -(-G // per)), torch.int32),
             "scales": ((rows, G), torch.float16)}
 

@@ -22,6 +22,7 @@ SETS = dict(bench.WORKLOADS)
 SETS["llama3-8b-mlp"] = [((14336, 4096), 8), ((4096, 14336), 4)]      # 705 M elements
 SETS["c1x64"] = [((1024, 4096), 64)]
 SETS["k768"] = [((50272, 768), 4)]
+SETS["falcon7b-mlp"] = [((18176, 4544), 8), ((4544, 18176), 4)]   # K = 4544: padded rows at gs 128
 SETS.setdefault("c1", [((1024, 4096), 1)])
 
 

@@ -40,7 +40,8 @@ def test_host_helpers_without_gpu():
     from awq_quantizer import _hip
     lib = _hip.load_library()
     assert lib.awq_ragged_eligible(0, 1024, 4096, 128) == 1
-    assert lib.awq_ragged_eligible(0, 1024, 4000, 128) == 0
+    assert lib.awq_ragged_eligible(0, 1024, 4000, 128) == 1     # padded rows: 4000 % 8 == 0
+    assert lib.awq_ragged_eligible(0, 1024, 4001, 128) == 0
     assert lib.awq_ragged_eligible(1, 1024, 4096, 128) == 1     # fp16 streams too
     assert lib.awq_ragged_eligible(2, 1024, 4096, 128) == 1     # fp32 streams too
     assert lib.awq_ragged_eligible(3, 1024, 4096, 128) == 0     # fp64 -> generic kernel
@@ -68,7 +69,8 @@ def test_host_helpers_without_gpu():
     for gs in (32, 64, 128, 256):
         assert lib.awq_ragged_eligible(0, 1024, 4096, gs) == 1
         assert lib.awq_ragged_eligible(1, 7, 3 * gs, gs) == 1
-        assert lib.awq_ragged_eligible(0, 7, 3 * gs + 8, gs) == 0   # K % gs != 0 -> generic
+        assert lib.awq_ragged_eligible(0, 7, 3 * gs + 8, gs) == 1   # padded rows (K % 8 == 0) stream too
+        assert lib.awq_ragged_eligible(0, 7, 3 * gs + 4, gs) == 0   # K % 8 != 0 -> generic
     for gs in (16, 100, 512):
         assert lib.awq_ragged_eligible(0, 1024, 4096, gs) == 0
     d = [_hip.TensorDesc(4096 * 16, 1024, 4096, 0, 0, 2 * 4096, 0, 0, 0, 0)]
@@ -81,6 +83,11 @@ def test_host_helpers_without_gpu():
     assert _hip.plan_ragged(d, 8, 256) == 5   # 8-bit: byte tiles, 33 groups / 8 -> 5
     with pytest.raises(RuntimeError, match="group_size"):
         _hip.plan_ragged(d, 4, 100)
+    # padded rows: row tiles, ceil(G / S) per row (K = 4544, gs 128: G = 36 -> 3 tiles per row)
+    d = [_hip.TensorDesc(4096 * 16, 11, 4544, 0, 0, 2 * 4096, 0, 0, 0, 0)]
+    assert _hip.plan_ragged(d, 4, 128) == 33
+    d = [_hip.TensorDesc(4096 * 16, 1, 5000, 0, 0, 2 * 4096, 0, 0, 0, 0)]
+    assert _hip.plan_ragged(d, 4, 256) == 3          # G = 20, 8 slots per tile
     # validation errors come back with a message, nothing launched
     assert lib.awq_quantize_groups(None, 0, 4, 256, 128, 3, 0, None, None, None, None, None, None) != 0
     assert "bit width" in _hip.last_error()

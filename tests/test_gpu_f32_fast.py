@@ -55,7 +55,8 @@ def test_f32_takes_the_streaming_kernel():
     from awq_quantizer import _hip
     for gs in (32, 64, 128, 256):
         assert _hip.ragged_eligible(torch.float32, 1024, 16 * gs, gs)
-    assert not _hip.ragged_eligible(torch.float32, 1024, 4000, 128)   # K % gs != 0: generic
+    assert _hip.ragged_eligible(torch.float32, 1024, 4000, 128)       # padded rows (K % 8 == 0)
+    assert not _hip.ragged_eligible(torch.float32, 1024, 4001, 128)   # K % 8 != 0: generic
 
 
 @pytest.mark.parametrize("bits", [4, 8])

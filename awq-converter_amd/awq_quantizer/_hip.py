@@ -15,7 +15,7 @@ import torch
 
 LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib")
 LIB_PATH = os.path.join(LIB_DIR, "libawq_hip.so")
-ABI_VERSION = 6
+ABI_VERSION = 7
 
 AWQ_DTYPE = {torch.bfloat16: 0, torch.float16: 1, torch.float32: 2, torch.float64: 3}
 
@@ -45,7 +45,8 @@ SIGNATURES = {
     "awq_stream_copy": (_I32, [_P, _P, _I64, _P]),
     "awq_export_autoawq_gemm": (_I32, [_P, _P, _P, _I64, _I64, _I64, _I32, _P, _P, _P, _P]),
     "awq_plan_block_tensor": (_I64, [ctypes.POINTER(TensorDesc), _I32, _I64, _P, _I64]),
-    "awq_quantize_ragged": (_I32, [_P, _I32, _I64, _P, _I32, _I32, _I32, _I64, _P]),
+    "awq_ragged_flags": (_I32, [ctypes.POINTER(TensorDesc), _I32, _I64]),
+    "awq_quantize_ragged": (_I32, [_P, _I32, _I64, _P, _I32, _I32, _I32, _I64, _I32, _P]),
     "awq_dequantize": (_I32, [_P, _P, _P, _I64, _I64, _I64, _P, _P]),
     "awq_dequantize_packed": (_I32, [_P, _P, _P, _I64, _I64, _I64, _I32, _I32, _P, _P]),
     "awq_pack_rows": (_I32, [_P, _I64, _I64, _I32, _I32, _P, _P]),
@@ -154,6 +155,11 @@ def ragged_eligible(dtype: torch.dtype, rows: int, K: int, L: int) -> bool:
     return bool(load_library().awq_ragged_eligible(AWQ_DTYPE[dtype], rows, K, L))
 
 
+def ragged_flags(descs, group_size: int = 128) -> int:
+    arr = (TensorDesc * len(descs))(*descs)
+    return int(load_library().awq_ragged_flags(arr, len(descs), group_size))
+
+
 def plan_ragged(descs, bits: int, group_size: int = 128) -> int:
     lib = load_library()
     arr = (TensorDesc * len(descs))(*descs)
@@ -186,9 +192,9 @@ def plan_block_tensor(descs, total_tiles: int, device: torch.device) -> torch.Te
 
 def quantize_ragged(descs_dev: torch.Tensor, n: int, total_tiles: int, bits: int, symmetric: bool,
                     stream: int, block_tensor: Optional[torch.Tensor] = None,
-                    dtype: torch.dtype = torch.bfloat16, group_size: int = 128) -> None:
+                    dtype: torch.dtype = torch.bfloat16, group_size: int = 128, flags: int = 0) -> None:
     rc = load_library().awq_quantize_ragged(ptr(descs_dev), n, total_tiles, ptr(block_tensor), AWQ_DTYPE[dtype],
-                                            bits, int(bool(symmetric)), group_size, ctypes.c_void_p(stream))
+                                            bits, int(bool(symmetric)), group_size, flags, ctypes.c_void_p(stream))
     check(rc, "awq_quantize_ragged")
 
 

@@ -65,6 +65,7 @@ class PackedBatch:
             descs.append(_hip.TensorDesc(x.data_ptr(), rows, K, p("qweight"), p("qzeros"), p("scales"),
                                          p("tensor_q"), p("zero_points"), 0, 0))
         self.total_tiles = _hip.plan_ragged(descs, bits, gs)
+        self.flags = _hip.ragged_flags(descs, gs)       # padded rows -> the row-tile kernel instance
         self.descs = descs
         self.descs_dev = _hip.descs_to_device(descs, dev)
         self.block_tensor = _hip.plan_block_tensor(descs, self.total_tiles, dev) if use_block_table else None
@@ -73,7 +74,7 @@ class PackedBatch:
     def run(self, stream: Optional[torch.cuda.Stream] = None) -> None:
         s = stream if stream is not None else torch.cuda.current_stream(self.device)
         _hip.quantize_ragged(self.descs_dev, len(self.descs), self.total_tiles, self.bits, self.symmetric,
-                             s.cuda_stream, self.block_tensor, self.dtype, self.group_size)
+                             s.cuda_stream, self.block_tensor, self.dtype, self.group_size, self.flags)
 
     def results(self) -> Dict[str, Dict[str, torch.Tensor]]:
         res = {}

@@ -94,7 +94,7 @@ int awq_quantize_groups(const void* w, int dtype, int64_t rows, int64_t K, int64
         d.tensor_q = tensor_q; d.zeros = zeros; d.tile_begin = 0;
         d.tile_count = awq::fast_tiles(rows, K, bits, (int)group_size);
         return hip_status(awq::launch_fast(nullptr, nullptr, &d, 1, d.tile_count, dtype, bits, symmetric,
-                                           (int)group_size, s), "awq fast kernel");
+                                           (int)group_size, (K % group_size) != 0, s), "awq fast kernel");
     }
     // generic path: per-group int32 values first, then packing (needs tensor_q / zeros buffers)
     if ((qweight && !tensor_q) || (qzeros && !zeros))
@@ -136,7 +136,8 @@ int awq_quantize_search(const void* w, int dtype, int64_t rows, int64_t K, int64
         d.tensor_q = tensor_q; d.zeros = zeros; d.tile_begin = 0;
         d.tile_count = awq::fast_tiles(rows, K, bits, (int)group_size);
         return hip_status(awq::launch_fast(nullptr, nullptr, &d, 1, d.tile_count, dtype, bits, symmetric,
-                                           (int)group_size, s, n_grid, n_candidates), "awq fast search kernel");
+                                           (int)group_size, (K % group_size) != 0, s, n_grid, n_candidates),
+                          "awq fast search kernel");
     }
     if ((qweight && !tensor_q) || (qzeros && !zeros))
         return fail(AWQ_EINVAL, "packed outputs of the generic search kernel need the int32 tensor_q/zeros "
@@ -195,9 +196,16 @@ int64_t awq_plan_block_tensor(const awq_tensor_desc* descs, int n, int64_t total
     return need;
 }
 
+int awq_ragged_flags(const awq_tensor_desc* descs, int n, int64_t group_size) {
+    int flags = 0;
+    for (int i = 0; descs && i < n; ++i)
+        if (group_size > 0 && descs[i].K % group_size) flags |= AWQ_RAGGED_PADDED;
+    return flags;
+}
+
 int awq_quantize_ragged(const awq_tensor_desc* descs_device, int n, int64_t total_tiles,
                         const int32_t* block_tensor_device, int dtype, int bits, int symmetric, int64_t group_size,
-                        void* stream) {
+                        int flags, void* stream) {
     g_err.clear();
     if (bits != 4 && bits != 8) return fail(AWQ_EINVAL, "Unsupported bit width: %d. Supported: 4, 8.", bits);
     if (!awq::fast_group_size(group_size))
@@ -205,10 +213,12 @@ int awq_quantize_ragged(const awq_tensor_desc* descs_device, int n, int64_t tota
                     (long long)group_size);
     if (dtype != AWQ_DTYPE_BF16 && dtype != AWQ_DTYPE_F16 && dtype != AWQ_DTYPE_F32)
         return fail(AWQ_EINVAL, "ragged launches take bf16, fp16 or fp32 tensors (dtype code %d)", dtype);
+    if (flags & ~AWQ_RAGGED_PADDED) return fail(AWQ_EINVAL, "unknown ragged flags 0x%x", flags);
     if (n <= 0 || total_tiles <= 0) return AWQ_OK;
     if (!descs_device) return fail(AWQ_EINVAL, "null descriptor array");
     return hip_status(awq::launch_fast(descs_device, block_tensor_device, nullptr, n, total_tiles, dtype, bits,
-                                       symmetric, (int)group_size, (hipStream_t)stream), "awq ragged kernel");
+                                       symmetric, (int)group_size, (flags & AWQ_RAGGED_PADDED) != 0,
+                                       (hipStream_t)stream), "awq ragged kernel");
 }
 
 int awq_dequantize(const int32_t* tensor_q, const uint16_t* scales, const int32_t* zeros, int64_t rows,

@@ -477,10 +477,10 @@ struct TileCtx {
     uint32_t qw_n;       // qweight words of the tile
 };
 
-template <int BITS, int GS>
+template <int BITS, int GS, bool PAD>
 __device__ __forceinline__ TileCtx make_ctx(const awq_tensor_desc& d, uint32_t tile) {
     constexpr uint32_t S = kTileElems / GS;
-    const TensorGeom g = fast_geom(d.rows, d.K, BITS, GS);
+    const TensorGeom g = fast_geom(d.rows, d.K, BITS, GS, PAD);
     constexpr uint32_t WPG = GS * BITS / 32;   // qweight words per group
     TileCtx c;
     c.bytes = g.bytes;
@@ -533,10 +533,10 @@ __device__ __forceinline__ TileCtx make_ctx(const awq_tensor_desc& d, uint32_t t
 
 // first element and element count of a tile (the input range it reads; padded rows stop at
 // the row end, the range check supplies the zero padding)
-template <int BITS, int GS>
+template <int BITS, int GS, bool PAD>
 __device__ __forceinline__ void tile_src(int64_t rows, int64_t K, uint32_t tile, uint64_t& el_off, uint32_t& valid) {
     constexpr uint32_t S = kTileElems / GS;
-    const TensorGeom g = fast_geom(rows, K, BITS, GS);
+    const TensorGeom g = fast_geom(rows, K, BITS, GS, PAD);
     if (g.TR) {
         const uint32_t r = tile / g.TR;
         const uint32_t g0 = (tile - r * g.TR) * S;
@@ -916,7 +916,7 @@ __device__ uint64_t* g_trace = nullptr;
 // One wave per tile.  The grid normally covers every tile once (launch_fast); a smaller
 // grid (AWQ_HIP_MAX_BLOCKS, tests) makes each wave walk tiles t, t + nwaves, ... with a
 // tensor cursor.
-template <typename F, int BITS, bool SYM, bool SEARCH, int GS>
+template <typename F, int BITS, bool SYM, bool SEARCH, int GS, bool PAD>
 __global__ __launch_bounds__(64 * kWavesPerBlock, SEARCH ? 4 : (F::kWide ? AWQ_MIN_WAVES_WIDE : AWQ_MIN_WAVES))
 void awq_fast_kernel(
     const awq_tensor_desc* __restrict__ descs, const int32_t* __restrict__ block_tensor, awq_tensor_desc single,
@@ -968,7 +968,7 @@ void awq_fast_kernel(
         const uint32_t tile = (uint32_t)(t - d.tile_begin);
         uint64_t el_off;
         uint32_t valid;
-        tile_src<BITS, GS>(d.rows, d.K, tile, el_off, valid);
+        tile_src<BITS, GS, PAD>(d.rows, d.K, tile, el_off, valid);
         Chunk<F::NW> va[4];
         load_tile<F, GS>((const char*)d.w + el_off * F::kBytes, valid, va);
 #ifdef AWQ_TRACE
@@ -978,7 +978,7 @@ void awq_fast_kernel(
             tr2 = __builtin_amdgcn_s_memrealtime();
         }
 #endif
-        compute_tile<F, BITS, SYM, SEARCH, GS>(make_ctx<BITS, GS>(d, tile), va, zw, qs, n_grid, n_cand);
+        compute_tile<F, BITS, SYM, SEARCH, GS>(make_ctx<BITS, GS, PAD>(d, tile), va, zw, qs, n_grid, n_cand);
     }
 #ifdef AWQ_TRACE
     if (g_trace != nullptr && (threadIdx.x & 63) == 0) {
@@ -1008,7 +1008,7 @@ __global__ void awq_selftest_recip_kernel(unsigned long long* mismatches) {
 
 hipError_t launch_fast(const awq_tensor_desc* descs_dev, const int32_t* block_tensor,
                        const awq_tensor_desc* single, int n, int64_t total_tiles, int dtype, int bits,
-                       int symmetric, int group_size, hipStream_t stream, int n_grid, int n_cand) {
+                       int symmetric, int group_size, bool padded, hipStream_t stream, int n_grid, int n_cand) {
     if (total_tiles <= 0) return hipSuccess;
     // one wave per tile (tuning / tests: AWQ_HIP_TILES_PER_WAVE = tiles per wave,
     // AWQ_HIP_MAX_BLOCKS = grid cap; either makes waves walk several tiles)
@@ -1031,12 +1031,18 @@ hipError_t launch_fast(const awq_tensor_desc* descs_dev, const int32_t* block_te
     const dim3 grid((unsigned)blocks), block(64 * kWavesPerBlock);
 #define AWQ_LAUNCH_GS(Fm, B, S, G)                                                                         \
     do {                                                                                                   \
-        if (n_cand > 1)                                                                                    \
-            hipLaunchKernelGGL((awq_fast_kernel<Fm, B, S, true, G>), grid, block, 0, stream, descs_dev, bt, one, \
-                               n, total_tiles, n_grid, n_cand);                                            \
+        if (n_cand > 1 && padded)                                                                          \
+            hipLaunchKernelGGL((awq_fast_kernel<Fm, B, S, true, G, true>), grid, block, 0, stream, descs_dev, bt, \
+                               one, n, total_tiles, n_grid, n_cand);                                       \
+        else if (n_cand > 1)                                                                               \
+            hipLaunchKernelGGL((awq_fast_kernel<Fm, B, S, true, G, false>), grid, block, 0, stream, descs_dev, \
+                               bt, one, n, total_tiles, n_grid, n_cand);                                   \
+        else if (padded)                                                                                   \
+            hipLaunchKernelGGL((awq_fast_kernel<Fm, B, S, false, G, true>), grid, block, 0, stream, descs_dev,  \
+                               bt, one, n, total_tiles, 1, 0);                                             \
         else                                                                                               \
-            hipLaunchKernelGGL((awq_fast_kernel<Fm, B, S, false, G>), grid, block, 0, stream, descs_dev, bt,    \
-                               one, n, total_tiles, 1, 0);                                                 \
+            hipLaunchKernelGGL((awq_fast_kernel<Fm, B, S, false, G, false>), grid, block, 0, stream, descs_dev, \
+                               bt, one, n, total_tiles, 1, 0);                                             \
     } while (0)
 #define AWQ_LAUNCH(Fm, B, S)                                   \
     switch (group_size) {                                      \

@@ -58,15 +58,16 @@ struct TensorGeom {
     uint32_t TR;     // padded rows: tiles per row (0 = flat tiling)
 };
 
-__host__ __device__ inline TensorGeom fast_geom(int64_t R, int64_t K, int bits, int gs) {
+// pad = false: the caller guarantees K % gs == 0 (kernels built without the row-tile path)
+__host__ __device__ inline TensorGeom fast_geom(int64_t R, int64_t K, int bits, int gs, bool pad = true) {
     TensorGeom g;
     g.S = (uint32_t)(kTileElems / gs);
-    g.G = (uint32_t)((K + gs - 1) / gs);
+    g.G = (uint32_t)(pad ? (K + gs - 1) / gs : K / gs);
     g.C = 32u / (uint32_t)bits;
     g.WPR = (g.G + g.C - 1) / g.C;
     g.WPT = (g.WPR == 1) ? (g.S / g.G) : (g.S / g.C);
     g.words = (uint32_t)R * g.WPR;
-    g.TR = (K % gs) ? (g.G + g.S - 1) / g.S : 0u;
+    g.TR = (pad && (K % gs)) ? (g.G + g.S - 1) / g.S : 0u;
     g.bytes = (!g.TR && (bits == 8 || (g.G % 2u) == 0u)) ? 1u : 0u;
     return g;
 }
@@ -97,7 +98,8 @@ __host__ __device__ inline bool fast_shape_ok(int64_t R, int64_t K, int64_t gs) 
 // launchers (awq_fast.hip / awq_generic.hip)
 hipError_t launch_fast(const awq_tensor_desc* descs_dev, const int32_t* block_tensor,
                        const awq_tensor_desc* single, int n, int64_t total_tiles, int dtype, int bits,
-                       int symmetric, int group_size, hipStream_t stream, int n_grid = 1, int n_cand = 0);
+                       int symmetric, int group_size, bool padded, hipStream_t stream, int n_grid = 1,
+                       int n_cand = 0);
 hipError_t launch_generic(const void* w, int dtype, int64_t rows, int64_t K, int64_t L, int bits,
                           int symmetric, int32_t* tensor_q, uint16_t* scales, int32_t* zeros,
                           hipStream_t stream, int n_grid = 1, int n_cand = 0);

@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define AWQ_HIP_ABI_VERSION 6
+#define AWQ_HIP_ABI_VERSION 7
 
 /* dtype codes of the input weights (torch dtypes the reference accepts, awq.py:397) */
 enum { AWQ_DTYPE_BF16 = 0, AWQ_DTYPE_F16 = 1, AWQ_DTYPE_F32 = 2, AWQ_DTYPE_F64 = 3 };
@@ -77,9 +77,10 @@ int awq_device_check(char* arch, int len);
 /* Quantize one [rows, K] tensor (replaces awq.py:286-374 incl. the small-tensor
  * path awq.py:130-171, which a caller expresses as group_size = K).
  * bits in {4, 8}; symmetric selects qmin/qmax per awq.py:114-128.
- * bf16 / fp16 / fp32 with group_size in {32, 64, 128, 256} and K % group_size == 0 take
- * the streaming fast kernel; every other shape/dtype (fp64, other group sizes, padded
- * tails) takes the generic kernel (same results). */
+ * bf16 / fp16 / fp32 with group_size in {32, 64, 128, 256} and K % group_size == 0, or
+ * K % 8 == 0 (padded rows, awq.py:337-339), take the streaming fast kernel; every other
+ * shape/dtype (fp64, other group sizes, K % 8 != 0 tails) takes the generic kernel (same
+ * results). */
 int awq_quantize_groups(const void* w, int dtype, int64_t rows, int64_t K, int64_t group_size,
                         int bits, int symmetric, int32_t* qweight, int32_t* qzeros,
                         uint16_t* scales, int32_t* tensor_q, int32_t* zeros, void* stream);
@@ -119,6 +120,13 @@ int64_t awq_plan_ragged(awq_tensor_desc* descs_host, int n, int bits, int64_t gr
 int64_t awq_plan_block_tensor(const awq_tensor_desc* descs_host, int n, int64_t total_tiles,
                               int32_t* block_tensor_host, int64_t len);
 
+/* flags of awq_quantize_ragged: some tensor has K % group_size != 0 (padded rows: the
+ * kernel instance with the row-tile path; the others are built without it) */
+#define AWQ_RAGGED_PADDED 1
+
+/* HOST helper: the awq_quantize_ragged flags a descriptor array needs. */
+int awq_ragged_flags(const awq_tensor_desc* descs_host, int n, int64_t group_size);
+
 /* Quantize n eligible tensors of one dtype (AWQ_DTYPE_BF16, _F16 or _F32) in ONE
  * launch (replaces the CLI's per-tensor loop, main.py:353-392).  descs_device: device copy
  * of the array planned by awq_plan_ragged with the same bits and group_size (the caller
@@ -126,7 +134,7 @@ int64_t awq_plan_block_tensor(const awq_tensor_desc* descs_host, int n, int64_t 
  * awq_plan_block_tensor table (NULL: each wave searches the descriptors). */
 int awq_quantize_ragged(const awq_tensor_desc* descs_device, int n, int64_t total_tiles,
                         const int32_t* block_tensor_device, int dtype, int bits, int symmetric, int64_t group_size,
-                        void* stream);
+                        int flags, void* stream);
 
 /* AutoAWQ "GEMM" layout (the reference has no packed format): from
  * this library's row-major packed 4-bit results of an [N = out_features, K = in_features]

@@ -59,6 +59,8 @@ def main():
                 fn.restype = res
                 fn.argtypes = argt
         if lib.awq_abi_version() < 5:   # older builds: no group_size argument (gs 128 only)
+            lib.awq_quantize_ragged.argtypes = _hip.SIGNATURES["awq_quantize_ragged"][1][:-3] + [ctypes.c_void_p]
+        elif lib.awq_abi_version() < 7:   # no flags argument
             lib.awq_quantize_ragged.argtypes = _hip.SIGNATURES["awq_quantize_ragged"][1][:-2] + [ctypes.c_void_p]
         handles[p] = lib
     _hip.load_library()
@@ -128,7 +130,8 @@ def main():
                         s0, s1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                         s0.record(stream)
                         table = None if blk == "nt" else block_table(lp, lib, bt).data_ptr()
-                        gsa = (bt.group_size,) if lib.awq_abi_version() >= 5 else ()
+                        abi = lib.awq_abi_version()
+                        gsa = ((bt.group_size,) if abi >= 5 else ()) + ((bt.flags,) if abi >= 7 else ())
                         rc = lib.awq_quantize_ragged(ctypes.c_void_p(bt.descs_dev.data_ptr()), len(bt.descs),
                                                      bt.total_tiles, ctypes.c_void_p(table),
                                                      _hip.AWQ_DTYPE[bt.dtype], bt.bits, int(bt.symmetric),

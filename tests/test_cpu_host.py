@@ -27,7 +27,7 @@ def test_library_exports_every_declared_symbol():
     for s in syms:
         assert hasattr(lib, s), s
     assert set(syms) == set(_hip.SIGNATURES), "python binding out of sync with include/awq_hip.h"
-    assert lib.awq_abi_version() == _hip.ABI_VERSION == 6
+    assert lib.awq_abi_version() == _hip.ABI_VERSION == 7
 
 
 def test_library_is_gfx950_code_object():
@@ -86,6 +86,7 @@ def test_host_helpers_without_gpu():
     # padded rows: row tiles, ceil(G / S) per row (K = 4544, gs 128: G = 36 -> 3 tiles per row)
     d = [_hip.TensorDesc(4096 * 16, 11, 4544, 0, 0, 2 * 4096, 0, 0, 0, 0)]
     assert _hip.plan_ragged(d, 4, 128) == 33
+    assert _hip.ragged_flags(d, 128) == 1 and _hip.ragged_flags(d, 64) == 0   # 4544 = 71 x 64
     d = [_hip.TensorDesc(4096 * 16, 1, 5000, 0, 0, 2 * 4096, 0, 0, 0, 0)]
     assert _hip.plan_ragged(d, 4, 256) == 3          # G = 20, 8 slots per tile
     # validation errors come back with a message, nothing launched

@@ -919,8 +919,11 @@ __device__ uint64_t* g_trace = nullptr;
 template <typename F, int BITS, bool SYM, bool SEARCH, int GS, bool PAD>
 __global__ __launch_bounds__(64 * kWavesPerBlock, SEARCH ? 4 : (F::kWide ? AWQ_MIN_WAVES_WIDE : AWQ_MIN_WAVES))
 void awq_fast_kernel(
-    const awq_tensor_desc* __restrict__ descs, const int32_t* __restrict__ block_tensor, awq_tensor_desc single,
-    int n, int64_t total_tiles, int n_grid, int n_cand) {
+    // the scalars every wave needs first lead the argument block (they fit the kernarg
+    // preload window of a -mllvm -amdgpu-kernarg-preload-count build); the 80-B single-
+    // tensor descriptor goes last
+    const int32_t* __restrict__ block_tensor, const awq_tensor_desc* __restrict__ descs, int64_t total_tiles,
+    int n, int n_grid, int n_cand, awq_tensor_desc single) {
     __shared__ uint32_t zwords[kWavesPerBlock][kTileElems / GS];
 #if AWQ_WIDE_STORE
     __shared__ __attribute__((aligned(16))) uint32_t qstage_all[kWavesPerBlock][BITS == 4 ? 256 : 512];
@@ -1029,20 +1032,20 @@ hipError_t launch_fast(const awq_tensor_desc* descs_dev, const int32_t* block_te
     // the table describes the one-tile-per-wave grid only
     const int32_t* bt = (tpw == 1 && blocks * per_block >= total_tiles) ? block_tensor : nullptr;
     const dim3 grid((unsigned)blocks), block(64 * kWavesPerBlock);
-#define AWQ_LAUNCH_GS(Fm, B, S, G)                                                                         \
-    do {                                                                                                   \
-        if (n_cand > 1 && padded)                                                                          \
-            hipLaunchKernelGGL((awq_fast_kernel<Fm, B, S, true, G, true>), grid, block, 0, stream, descs_dev, bt, \
-                               one, n, total_tiles, n_grid, n_cand);                                       \
-        else if (n_cand > 1)                                                                               \
-            hipLaunchKernelGGL((awq_fast_kernel<Fm, B, S, true, G, false>), grid, block, 0, stream, descs_dev, \
-                               bt, one, n, total_tiles, n_grid, n_cand);                                   \
-        else if (padded)                                                                                   \
-            hipLaunchKernelGGL((awq_fast_kernel<Fm, B, S, false, G, true>), grid, block, 0, stream, descs_dev,  \
-                               bt, one, n, total_tiles, 1, 0);                                             \
-        else                                                                                               \
-            hipLaunchKernelGGL((awq_fast_kernel<Fm, B, S, false, G, false>), grid, block, 0, stream, descs_dev, \
-                               bt, one, n, total_tiles, 1, 0);                                             \
+#define AWQ_LAUNCH_GS(Fm, B, S, G)                                                                                  \
+    do {                                                                                                            \
+        if (n_cand > 1 && padded)                                                                                   \
+            hipLaunchKernelGGL((awq_fast_kernel<Fm, B, S, true, G, true>), grid, block, 0, stream, bt, descs_dev,   \
+                               total_tiles, n, n_grid, n_cand, one);                                                \
+        else if (n_cand > 1)                                                                                        \
+            hipLaunchKernelGGL((awq_fast_kernel<Fm, B, S, true, G, false>), grid, block, 0, stream, bt, descs_dev,  \
+                               total_tiles, n, n_grid, n_cand, one);                                                \
+        else if (padded)                                                                                            \
+            hipLaunchKernelGGL((awq_fast_kernel<Fm, B, S, false, G, true>), grid, block, 0, stream, bt, descs_dev,  \
+                               total_tiles, n, 1, 0, one);                                                          \
+        else                                                                                                        \
+            hipLaunchKernelGGL((awq_fast_kernel<Fm, B, S, false, G, false>), grid, block, 0, stream, bt, descs_dev, \
+                               total_tiles, n, 1, 0, one);                                                          \
     } while (0)
 #define AWQ_LAUNCH(Fm, B, S)                                   \
     switch (group_size) {                                      \

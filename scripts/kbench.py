@@ -23,6 +23,7 @@ SETS["llama3-8b-mlp"] = [((14336, 4096), 8), ((4096, 14336), 4)]      # 705 M el
 SETS["c1x64"] = [((1024, 4096), 64)]
 SETS["k768"] = [((50272, 768), 4)]
 SETS["falcon7b-mlp"] = [((18176, 4544), 8), ((4544, 18176), 4)]   # K = 4544: padded rows at gs 128
+SETS["qwen05-odd"] = [((4864, 896), 8), ((151936, 896), 1)]   # K = 896: 7 groups (odd) at gs 128 -> word tiles (2 rows per tile)
 SETS.setdefault("c1", [((1024, 4096), 1)])
 
 

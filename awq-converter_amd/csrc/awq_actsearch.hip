@@ -164,18 +164,24 @@ template <bool ROW32>
 __device__ __forceinline__ void minmax_cross(float& mn, float& mx, int& nan) {
     unsigned a, b;
     if (ROW32) swap32(ubits(mn), a, b); else swap16(ubits(mn), a, b);
-    mn = __builtin_fminf(fbits(a), fbits(b));
+    mn = __builtin_amdgcn_fmed3f(fbits(a), fbits(b), -__builtin_inff());
     if (ROW32) swap32(ubits(mx), a, b); else swap16(ubits(mx), a, b);
-    mx = __builtin_fmaxf(fbits(a), fbits(b));
+    mx = __builtin_amdgcn_fmed3f(fbits(a), fbits(b), __builtin_inff());
     if (ROW32) swap32((unsigned)nan, a, b); else swap16((unsigned)nan, a, b);
     nan = (int)(a | b);
 }
 
+// min(a, b) / max(a, b) as v_med3 against -inf / +inf: no NaN-quieting of the DPP-moved
+// operand (fminf / fmaxf need it in IEEE mode); NaN is tracked on the side, so no operand is
+// NaN whenever the result is used
+__device__ __forceinline__ float min2(float a, float b) { return __builtin_amdgcn_fmed3f(a, b, -__builtin_inff()); }
+__device__ __forceinline__ float max2(float a, float b) { return __builtin_amdgcn_fmed3f(a, b, __builtin_inff()); }
+
 __device__ __forceinline__ void grp_minmax(float& mn, float& mx, int& nan, int lpg) {
-    if (lpg >= 2) { mn = __builtin_fminf(mn, dppf<0xB1>(mn)); mx = __builtin_fmaxf(mx, dppf<0xB1>(mx)); nan |= dppi<0xB1>(nan); }
-    if (lpg >= 4) { mn = __builtin_fminf(mn, dppf<0x4E>(mn)); mx = __builtin_fmaxf(mx, dppf<0x4E>(mx)); nan |= dppi<0x4E>(nan); }
-    if (lpg >= 8) { mn = __builtin_fminf(mn, dppf<0x141>(mn)); mx = __builtin_fmaxf(mx, dppf<0x141>(mx)); nan |= dppi<0x141>(nan); }
-    if (lpg >= 16) { mn = __builtin_fminf(mn, dppf<0x140>(mn)); mx = __builtin_fmaxf(mx, dppf<0x140>(mx)); nan |= dppi<0x140>(nan); }
+    if (lpg >= 2) { mn = min2(mn, dppf<0xB1>(mn)); mx = max2(mx, dppf<0xB1>(mx)); nan |= dppi<0xB1>(nan); }
+    if (lpg >= 4) { mn = min2(mn, dppf<0x4E>(mn)); mx = max2(mx, dppf<0x4E>(mx)); nan |= dppi<0x4E>(nan); }
+    if (lpg >= 8) { mn = min2(mn, dppf<0x141>(mn)); mx = max2(mx, dppf<0x141>(mx)); nan |= dppi<0x141>(nan); }
+    if (lpg >= 16) { mn = min2(mn, dppf<0x140>(mn)); mx = max2(mx, dppf<0x140>(mx)); nan |= dppi<0x140>(nan); }
     if (lpg >= 32) minmax_cross<false>(mn, mx, nan);
     if (lpg >= 64) minmax_cross<true>(mn, mx, nan);
 }
@@ -223,6 +229,11 @@ __device__ __forceinline__ void load8(const void* base, int64_t i, float (&v)[8]
 // ---- column sums (canonical: rows ascending inside a 256-row block, fp64) ----
 // MODE 0, activations x [T, K]:  part0[b][k] = sum |x|,  part1[b][k] = sum x*x
 // MODE 1, weights w [R, K]:      part0[b][k] = sum fp32(|w| / fp32(gmax[r, k/L] + 1e-6f))
+// One lane per column and block; the sum is a dependent fp64 chain, so the loads go out
+// kColBatch rows ahead of it (a lane's loads are independent of its sums): the chain
+// order is unchanged, only the memory latency overlaps.
+constexpr int kColBatch = 16;
+
 template <int DT, int MODE>
 __global__ __launch_bounds__(256) void colsum_kernel(const void* __restrict__ src, int64_t rows, int64_t K,
                                                      int64_t L, const float* __restrict__ gmax,
@@ -234,17 +245,27 @@ __global__ __launch_bounds__(256) void colsum_kernel(const void* __restrict__ sr
     const int64_t r0 = b * kRowBlock;
     const int64_t r1 = (r0 + kRowBlock < rows) ? r0 + kRowBlock : rows;
     const typename T::S* p = (const typename T::S*)src;
-    const int64_t G = K / L;
+    const int64_t G = K / L, gk = k / L;
     double s0 = 0.0, s1 = 0.0;
-    for (int64_t r = r0; r < r1; ++r) {
-        const float v = T::load(p, r * K + k);
-        if (MODE == 0) {
-            const double d = (double)v;     // |x| and x*x are exact in fp64
-            s0 += __builtin_fabs(d);
-            s1 += d * d;
-        } else {
-            const float den = gmax[r * G + k / L] + 1e-6f;
-            s0 += (double)(__builtin_fabsf(v) / den);
+    for (int64_t r = r0; r < r1; r += kColBatch) {
+        float v[kColBatch], den[kColBatch];
+#pragma unroll
+        for (int j = 0; j < kColBatch; ++j) {
+            const int64_t rr = (r + j < r1) ? r + j : r1 - 1;   // in range; the tail is skipped below
+            v[j] = T::load(p, rr * K + k);
+            if (MODE == 1) den[j] = gmax[rr * G + gk] + 1e-6f;
+        }
+#pragma unroll
+        for (int j = 0; j < kColBatch; ++j) {
+            if (r + j < r1) {
+                if (MODE == 0) {
+                    const double d = (double)v[j];     // |x| and x*x are exact in fp64
+                    s0 += __builtin_fabs(d);
+                    s1 += d * d;
+                } else {
+                    s0 += (double)(__builtin_fabsf(v[j]) / den[j]);
+                }
+            }
         }
     }
     part0[b * K + k] = s0;
@@ -257,8 +278,80 @@ __global__ __launch_bounds__(256) void colmean_kernel(const double* __restrict__
     const int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (k >= K) return;
     double s = 0.0;
-    for (int64_t b = 0; b < nblk; ++b) s += part[b * K + k];
+    for (int64_t b = 0; b < nblk; b += kColBatch) {
+        double v[kColBatch];
+#pragma unroll
+        for (int j = 0; j < kColBatch; ++j) v[j] = part[((b + j < nblk) ? b + j : nblk - 1) * K + k];
+#pragma unroll
+        for (int j = 0; j < kColBatch; ++j)
+            if (b + j < nblk) s += v[j];
+    }
     out[k] = (float)(s / divisor);
+}
+
+// Same sums, staged through LDS: a workgroup takes one 256-row block x 64 columns; every
+// thread loads 8 rows x 8 columns (16-B loads, all in flight at once) and stores the fp32
+// terms (MODE 1: the quotient, computed at load time) in LDS; then 64 lanes run the 64
+// column chains (rows ascending, fp64) from LDS.  Needs K % 8 == 0 and a 16-B aligned src.
+constexpr int kColTile = 64;
+template <int DT, int MODE>
+__global__ __launch_bounds__(256) void colsum_tile_kernel(const void* __restrict__ src, int64_t rows, int64_t K,
+                                                          int64_t L, const float* __restrict__ gmax,
+                                                          double* __restrict__ part0, double* __restrict__ part1) {
+    __shared__ __attribute__((aligned(16))) float sv[kRowBlock][kColTile];
+    const int tid = threadIdx.x;
+    const int64_t kt = (int64_t)blockIdx.x * kColTile;
+    const int64_t b = blockIdx.y, r0 = b * kRowBlock;
+    const int nr = (int)((r0 + kRowBlock < rows) ? kRowBlock : rows - r0);
+    const int oc = tid & 7, rl = tid >> 3;             // column octet, first row
+    const int64_t k0 = kt + 8 * oc;
+    const bool kin = k0 < K;
+    constexpr int NI = kRowBlock / 32;
+    float v[NI][8];
+    float den[NI];
+#pragma unroll
+    for (int it = 0; it < NI; ++it) {
+        const int rr = rl + 32 * it;
+        if (kin && rr < nr) {
+            load8<DT>(src, (r0 + rr) * K + k0, v[it]);
+            if (MODE == 1) den[it] = gmax[(r0 + rr) * (K / L) + k0 / L] + 1e-6f;
+        } else {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) v[it][j] = 0.0f;
+            if (MODE == 1) den[it] = 1.0f;
+        }
+    }
+#pragma unroll
+    for (int it = 0; it < NI; ++it) {
+        const int rr = rl + 32 * it;
+        if (MODE == 1)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) v[it][j] = __builtin_fabsf(v[it][j]) / den[it];
+        *(float4*)&sv[rr][8 * oc] = make_float4(v[it][0], v[it][1], v[it][2], v[it][3]);
+        *(float4*)&sv[rr][8 * oc + 4] = make_float4(v[it][4], v[it][5], v[it][6], v[it][7]);
+    }
+    __syncthreads();
+    if (tid >= kColTile || kt + tid >= K) return;
+    double s0 = 0.0, s1 = 0.0;
+    for (int r = 0; r < nr; r += 16) {
+        float t[16];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) t[j] = sv[(r + j < nr) ? r + j : nr - 1][tid];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            if (r + j < nr) {
+                const double d = (double)t[j];
+                if (MODE == 0) {
+                    s0 += __builtin_fabs(d);
+                    s1 += d * d;
+                } else {
+                    s0 += d;
+                }
+            }
+        }
+    }
+    part0[b * K + kt + tid] = s0;
+    if (MODE == 0) part1[b * K + kt + tid] = s1;
 }
 
 // Lane layout shared by the group kernels: LPG = L / 8 lanes per group (8 consecutive
@@ -320,16 +413,18 @@ __device__ __forceinline__ double raw_scale(const float* x_mean, const float* w_
 
 // table[i][k] = fp32(raw / sqrt(max_k raw * min_k raw)), inf / NaN -> 1; one workgroup per
 // candidate; max / min propagate NaN (order-independent, so any reduction order is exact)
-__global__ __launch_bounds__(256) void scale_table_kernel(const float* __restrict__ x_mean,
+// (16 waves per workgroup: the fp64 pow chains are latency-bound, one workgroup per CU)
+constexpr int kTableThreads = 1024;
+__global__ __launch_bounds__(kTableThreads) void scale_table_kernel(const float* __restrict__ x_mean,
                                                           const float* __restrict__ w_mean, int64_t K, int n_grid,
                                                           float* __restrict__ table) {
-    __shared__ double smx[256], smn[256];
-    __shared__ int snan[256];
+    __shared__ double smx[kTableThreads], smn[kTableThreads];
+    __shared__ int snan[kTableThreads];
     const int i = blockIdx.x, tid = threadIdx.x;
     const double r = (double)i / (double)n_grid;
     double mx = -__builtin_inf(), mn = __builtin_inf();
     int nan = 0;
-    for (int64_t k = tid; k < K; k += 256) {
+    for (int64_t k = tid; k < K; k += kTableThreads) {
         const double s = raw_scale(x_mean, w_mean, k, r);
         if (s != s) nan = 1;
         mx = s > mx ? s : mx;
@@ -339,7 +434,7 @@ __global__ __launch_bounds__(256) void scale_table_kernel(const float* __restric
     smn[tid] = mn;
     snan[tid] = nan;
     __syncthreads();
-    for (int o = 128; o > 0; o >>= 1) {
+    for (int o = kTableThreads / 2; o > 0; o >>= 1) {
         if (tid < o) {
             smx[tid] = smx[tid + o] > smx[tid] ? smx[tid + o] : smx[tid];
             smn[tid] = smn[tid + o] < smn[tid] ? smn[tid + o] : smn[tid];
@@ -348,7 +443,7 @@ __global__ __launch_bounds__(256) void scale_table_kernel(const float* __restric
         __syncthreads();
     }
     const double norm = snan[0] ? __builtin_nan("") : sqrt(smx[0] * smn[0]);
-    for (int64_t k = tid; k < K; k += 256) {
+    for (int64_t k = tid; k < K; k += kTableThreads) {
         double s = raw_scale(x_mean, w_mean, k, r) / norm;
         if (s != s || __builtin_isinf(s)) s = 1.0;
         table[(int64_t)i * K + k] = (float)s;
@@ -370,13 +465,16 @@ __device__ __forceinline__ float mquot(float a, float s, float rs) {
     return __builtin_fmaf(r, rs, q0);
 }
 
-template <int DT>
-__global__ __launch_bounds__(256) void act_loss_kernel(const void* __restrict__ w, int64_t R, int64_t K, int lpg,
-                                                       int qmin, int qmax, int sym, const float* __restrict__ table,
+// LPG: lanes per group as a constant (0 = the run-time lpg argument); SYM: symmetric
+template <int DT, int LPG, bool SYM>
+__global__ __launch_bounds__(256) void act_loss_kernel(const void* __restrict__ w, int64_t R, int64_t K, int lpg_rt,
+                                                       int qmin, int qmax, const float* __restrict__ table,
                                                        const float* __restrict__ rtable, int n_grid,
                                                        const float* __restrict__ x_sq, float* __restrict__ part,
                                                        int64_t stride) {
     typedef HwFmt<DT> H;
+    const int lpg = LPG ? LPG : lpg_rt;
+    constexpr int sym = SYM ? 1 : 0;
     const int64_t G = K / (8 * lpg);
     const int64_t nw = (int64_t)gridDim.x * 4;
     const bool leader = (threadIdx.x & 63) % lpg == 0;
@@ -461,31 +559,80 @@ __global__ __launch_bounds__(256) void act_loss_kernel(const void* __restrict__ 
     }
 }
 
-// work[i * nblk + b] = sum of part[i][b*1024 .. +1024) ascending, fp64
+// work[i * nblk + b] = sum of part[i][b*1024 .. +1024) ascending, fp64.  A workgroup takes
+// kLossChains consecutive (i, b) chains: their floats come in through LDS with coalesced
+// loads (all in flight at once), then one lane per chain runs its fp64 chain from LDS.
+constexpr int kLossChains = 16;
 __global__ __launch_bounds__(256) void loss_block_kernel(const float* __restrict__ part, int n_grid, int64_t stride,
                                                          int64_t nblk, double* __restrict__ work) {
-    const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (idx >= (int64_t)n_grid * nblk) return;
+    __shared__ __attribute__((aligned(16))) float sp[kLossChains][kGroupBlock];
+    const int tid = threadIdx.x;
+    const int64_t c0 = (int64_t)blockIdx.x * kLossChains;
+    const int64_t nch = (int64_t)n_grid * nblk;
+#pragma unroll 4
+    for (int c = 0; c < kLossChains; ++c) {
+        const int64_t idx = c0 + c;
+        if (idx >= nch) break;
+        const int64_t i = idx / nblk, b = idx - i * nblk;
+        const int64_t g0 = b * kGroupBlock;
+        const int64_t n = (g0 + kGroupBlock < stride) ? kGroupBlock : stride - g0;
+        const float* p = part + i * stride + g0;
+#pragma unroll
+        for (int e = 0; e < kGroupBlock / 256; ++e)
+            if (e * 256 + tid < n) sp[c][e * 256 + tid] = p[e * 256 + tid];
+    }
+    __syncthreads();
+    const int64_t idx = c0 + tid;
+    if (tid >= kLossChains || idx >= nch) return;
     const int64_t i = idx / nblk, b = idx - i * nblk;
-    const int64_t g0 = b * kGroupBlock, g1 = (g0 + kGroupBlock < stride) ? g0 + kGroupBlock : stride;
-    const float* p = part + i * stride;
+    const int64_t g0 = b * kGroupBlock;
+    const int n = (int)((g0 + kGroupBlock < stride) ? kGroupBlock : stride - g0);
+    const float* q = sp[tid];
     double s = 0.0;
-    for (int64_t g = g0; g < g1; ++g) s += (double)p[g];
+    for (int g = 0; g < n; g += 16) {                    // 16 LDS values ahead of the chain
+        float t[16];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) *(float4*)&t[4 * j] = *(const float4*)&q[g + 4 * j];
+#pragma unroll
+        for (int j = 0; j < 16; ++j)
+            if (g + j < n) s += (double)t[j];
+    }
     work[idx] = s;
 }
 
 // losses[i] = blocks ascending (fp64); best = first minimum (NaN never wins; all NaN -> 0);
-// s_best = table[best]
+// s_best = table[best].  The [n_grid, nblk] block sums come through LDS in column chunks
+// (coalesced loads), each candidate's chain continuing over the chunks in block order.
 __global__ __launch_bounds__(256) void select_kernel(const double* __restrict__ work, int n_grid, int64_t nblk,
                                                      const float* __restrict__ table, int64_t K,
                                                      double* __restrict__ losses, int32_t* __restrict__ best,
                                                      float* __restrict__ s_best) {
+    constexpr int kChunkElems = 4096;                  // 32 KiB of fp64
+    __shared__ double sw[kChunkElems];
     __shared__ double sl[256];
     __shared__ int sb;
     const int tid = threadIdx.x;
+    const int64_t cb = (kChunkElems / n_grid < nblk) ? kChunkElems / n_grid : nblk;   // blocks per chunk
+    double s = 0.0;
+    for (int64_t b0 = 0; b0 < nblk; b0 += cb) {
+        const int64_t nb = (b0 + cb < nblk) ? cb : nblk - b0;
+        __syncthreads();
+        for (int64_t e = tid; e < (int64_t)n_grid * nb; e += 256) {
+            const int64_t i = e / nb, j = e - i * nb;
+            sw[i * nb + j] = work[i * nblk + b0 + j];
+        }
+        __syncthreads();
+        if (tid < n_grid)
+            for (int64_t j = 0; j < nb; j += 8) {          // 8 LDS values ahead of the chain
+                double t[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) t[u] = sw[tid * nb + ((j + u < nb) ? j + u : nb - 1)];
+#pragma unroll
+                for (int u = 0; u < 8; ++u)
+                    if (j + u < nb) s += t[u];
+            }
+    }
     if (tid < n_grid) {
-        double s = 0.0;
-        for (int64_t b = 0; b < nblk; ++b) s += work[(int64_t)tid * nblk + b];
         sl[tid] = s;
         if (losses) losses[tid] = s;
     }
@@ -503,10 +650,41 @@ __global__ __launch_bounds__(256) void select_kernel(const double* __restrict__ 
         for (int64_t k = tid; k < K; k += 256) s_best[k] = table[(int64_t)sb * K + k];
 }
 
-// out = RN_D(w * s[k]) (torch: W.mul_(scales) on a D tensor with an fp32 scale vector)
+// out = RN_D(w * s[k]) (torch: W.mul_(scales) on a D tensor with an fp32 scale vector);
+// 8 consecutive elements of one row per lane (K % 8 == 0), vector loads / stores
 template <int DT>
 __global__ __launch_bounds__(256) void apply_scale_kernel(const void* __restrict__ w, int64_t R, int64_t K,
                                                           const float* __restrict__ s, void* __restrict__ out) {
+    typedef Traits<DT> T;
+    const int64_t n8 = R * K / 8;
+    for (int64_t o = (int64_t)blockIdx.x * 256 + threadIdx.x; o < n8; o += (int64_t)gridDim.x * 256) {
+        const int64_t i = o * 8;
+        const int64_t k = i % K;
+        float v[8], y[8];
+        load8<DT>(w, i, v);
+        const float4 sa = *(const float4*)(s + k), sb = *(const float4*)(s + k + 4);
+        const float sv[8] = {sa.x, sa.y, sa.z, sa.w, sb.x, sb.y, sb.z, sb.w};
+#pragma unroll
+        for (int j = 0; j < 8; ++j) y[j] = T::rn(v[j] * sv[j]);
+        if (DT == AWQ_DTYPE_F32) {
+            float4* q = (float4*)((float*)out + i);
+            q[0] = make_float4(y[0], y[1], y[2], y[3]);
+            q[1] = make_float4(y[4], y[5], y[6], y[7]);
+        } else {
+            uint32_t h[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+                h[j] = (DT == AWQ_DTYPE_BF16) ? (__float_as_uint(y[j]) >> 16) : (uint32_t)sw_f32_to_f16(y[j]);
+            *(uint4*)((uint16_t*)out + i) = make_uint4(h[0] | (h[1] << 16), h[2] | (h[3] << 16), h[4] | (h[5] << 16),
+                                                       h[6] | (h[7] << 16));
+        }
+    }
+}
+
+// any shape / alignment: one element per lane
+template <int DT>
+__global__ __launch_bounds__(256) void apply_scale_any_kernel(const void* __restrict__ w, int64_t R, int64_t K,
+                                                              const float* __restrict__ s, void* __restrict__ out) {
     typedef Traits<DT> T;
     const typename T::S* p = (const typename T::S*)w;
     const int64_t total = R * K;
@@ -540,9 +718,15 @@ hipError_t launch_act_stats(const void* x, int dtype, int64_t T, int64_t K, doub
     const int64_t nblk = (T + kRowBlock - 1) / kRowBlock;
     double* p0 = work;
     double* p1 = work + nblk * K;
-    const dim3 grid((unsigned)((K + 255) / 256), (unsigned)nblk);
-    AWQ_DT_SWITCH(dtype, hipLaunchKernelGGL((colsum_kernel<D, 0>), grid, dim3(256), 0, stream, x, T, K, K,
-                                            nullptr, p0, p1))
+    if (K % 8 == 0 && (uintptr_t)x % 16 == 0) {
+        const dim3 gt((unsigned)((K + kColTile - 1) / kColTile), (unsigned)nblk);
+        AWQ_DT_SWITCH(dtype, hipLaunchKernelGGL((colsum_tile_kernel<D, 0>), gt, dim3(256), 0, stream, x, T, K, K,
+                                                nullptr, p0, p1))
+    } else {
+        const dim3 grid((unsigned)((K + 255) / 256), (unsigned)nblk);
+        AWQ_DT_SWITCH(dtype, hipLaunchKernelGGL((colsum_kernel<D, 0>), grid, dim3(256), 0, stream, x, T, K, K,
+                                                nullptr, p0, p1))
+    }
     if (hipError_t e = hipPeekAtLastError()) return e;
     const dim3 g1((unsigned)((K + 255) / 256));
     hipLaunchKernelGGL(colmean_kernel, g1, dim3(256), 0, stream, p0, nblk, K, (double)T, x_mean);
@@ -559,9 +743,15 @@ hipError_t launch_weight_colsum(const void* w, int dtype, int64_t R, int64_t K, 
                                             dim3(256), 0, stream, w, R, K, lpg, gmax))
     if (hipError_t e = hipPeekAtLastError()) return e;
     const int64_t nblk = (R + kRowBlock - 1) / kRowBlock;
-    const dim3 grid((unsigned)((K + 255) / 256), (unsigned)nblk);
-    AWQ_DT_SWITCH(dtype, hipLaunchKernelGGL((colsum_kernel<D, 1>), grid, dim3(256), 0, stream, w, R, K, L, gmax,
-                                            part, nullptr))
+    if (K % 8 == 0 && L % 8 == 0 && (uintptr_t)w % 16 == 0) {
+        const dim3 gt((unsigned)((K + kColTile - 1) / kColTile), (unsigned)nblk);
+        AWQ_DT_SWITCH(dtype, hipLaunchKernelGGL((colsum_tile_kernel<D, 1>), gt, dim3(256), 0, stream, w, R, K, L,
+                                                gmax, part, nullptr))
+    } else {
+        const dim3 grid((unsigned)((K + 255) / 256), (unsigned)nblk);
+        AWQ_DT_SWITCH(dtype, hipLaunchKernelGGL((colsum_kernel<D, 1>), grid, dim3(256), 0, stream, w, R, K, L, gmax,
+                                                part, nullptr))
+    }
     return hipPeekAtLastError();
 }
 
@@ -574,8 +764,8 @@ hipError_t launch_colmean(const double* part, int64_t nblk, int64_t K, double di
 
 hipError_t launch_scale_table(const float* x_mean, const float* w_mean, int64_t K, int n_grid, float* table,
                               hipStream_t stream) {
-    hipLaunchKernelGGL(scale_table_kernel, dim3((unsigned)n_grid), dim3(256), 0, stream, x_mean, w_mean, K, n_grid,
-                       table);
+    hipLaunchKernelGGL(scale_table_kernel, dim3((unsigned)n_grid), dim3(kTableThreads), 0, stream, x_mean, w_mean, K,
+                       n_grid, table);
     return hipPeekAtLastError();
 }
 
@@ -622,16 +812,28 @@ hipError_t launch_act_losses(const void* w, int dtype, int64_t R, int64_t K, int
     const int lpg = (int)(L / 8);
     const int64_t items = ((R + (64 / lpg) - 1) / (64 / lpg)) * (K / L);
     const unsigned grid = blocks_for(items, 4, 256 * 32);
-    AWQ_DT_SWITCH(dtype, hipLaunchKernelGGL((act_loss_kernel<D>), dim3(grid), dim3(256), 0, stream, w, R, K, lpg,
-                                            qmin, qmax, symmetric, table, rtable, n_grid, x_sq, part, stride))
+#define AWQ_LOSS_LAUNCH(LP, SY)                                                                                    \
+    AWQ_DT_SWITCH(dtype, hipLaunchKernelGGL((act_loss_kernel<D, LP, SY>), dim3(grid), dim3(256), 0, stream, w, R, K, \
+                                            lpg, qmin, qmax, table, rtable, n_grid, x_sq, part, stride))
+#define AWQ_LOSS_SYM(LP)                 \
+    if (symmetric) { AWQ_LOSS_LAUNCH(LP, true) } else { AWQ_LOSS_LAUNCH(LP, false) }
+    switch (lpg) {   // the streaming group sizes 32 / 64 / 128 / 256 as constants
+    case 4: AWQ_LOSS_SYM(4) break;
+    case 8: AWQ_LOSS_SYM(8) break;
+    case 16: AWQ_LOSS_SYM(16) break;
+    case 32: AWQ_LOSS_SYM(32) break;
+    default: AWQ_LOSS_SYM(0) break;
+    }
+#undef AWQ_LOSS_SYM
+#undef AWQ_LOSS_LAUNCH
     return hipPeekAtLastError();
 }
 
 hipError_t launch_act_select(const float* part, int n_grid, int64_t stride, const float* table, int64_t K,
                              double* work, double* losses, int32_t* best, float* s_best, hipStream_t stream) {
     const int64_t nblk = (stride + kGroupBlock - 1) / kGroupBlock;
-    hipLaunchKernelGGL(loss_block_kernel, dim3(blocks_for((int64_t)n_grid * nblk, 256, INT32_MAX)), dim3(256), 0,
-                       stream, part, n_grid, stride, nblk, work);
+    hipLaunchKernelGGL(loss_block_kernel, dim3(blocks_for((int64_t)n_grid * nblk, kLossChains, INT32_MAX)), dim3(256),
+                       0, stream, part, n_grid, stride, nblk, work);
     if (hipError_t e = hipPeekAtLastError()) return e;
     hipLaunchKernelGGL(select_kernel, dim3(1), dim3(256), 0, stream, work, n_grid, nblk, table, K, losses, best,
                        s_best);
@@ -640,7 +842,14 @@ hipError_t launch_act_select(const float* part, int n_grid, int64_t stride, cons
 
 hipError_t launch_apply_scale(const void* w, int dtype, int64_t R, int64_t K, const float* s, void* out,
                               hipStream_t stream) {
-    const unsigned grid = blocks_for(R * K, 256, 256 * 64);
+    const bool vec = K % 8 == 0 && ((uintptr_t)w | (uintptr_t)s | (uintptr_t)out) % 16 == 0;
+    if (!vec) {
+        const unsigned g1 = blocks_for(R * K, 256, 256 * 64);
+        AWQ_DT_SWITCH(dtype, hipLaunchKernelGGL((apply_scale_any_kernel<D>), dim3(g1), dim3(256), 0, stream, w, R, K,
+                                                s, out))
+        return hipPeekAtLastError();
+    }
+    const unsigned grid = blocks_for(R * K / 8, 256, 256 * 64);
     AWQ_DT_SWITCH(dtype, hipLaunchKernelGGL((apply_scale_kernel<D>), dim3(grid), dim3(256), 0, stream, w, R, K, s,
                                             out))
     return hipPeekAtLastError();

@@ -362,6 +362,8 @@ struct GroupLane {
     bool valid;
 };
 
+// (EPL elements per lane: 8, or 16 = two consecutive 8-element chunks)
+template <int EPL = 8>
 __device__ __forceinline__ bool group_lane(int64_t item, int64_t R, int64_t G, int lpg, GroupLane& gl) {
     const int lane = threadIdx.x & 63;
     const int gpw = 64 / lpg;
@@ -371,7 +373,7 @@ __device__ __forceinline__ bool group_lane(int64_t item, int64_t R, int64_t G, i
     const int64_t rb = item - gl.g * nrb;
     gl.r = rb * gpw + lane / lpg;
     gl.valid = gl.r < R;
-    gl.k0 = gl.g * (int64_t)(8 * lpg) + 8 * (lane % lpg);
+    gl.k0 = gl.g * (int64_t)(EPL * lpg) + EPL * (lane % lpg);
     return true;
 }
 
@@ -465,8 +467,12 @@ __device__ __forceinline__ float mquot(float a, float s, float rs) {
     return __builtin_fmaf(r, rs, q0);
 }
 
-// LPG: lanes per group as a constant (0 = the run-time lpg argument); SYM: symmetric
-template <int DT, int LPG, bool SYM>
+// LPG: lanes per group as a constant (0 = the run-time lpg argument); SYM: symmetric;
+// EPL: elements per lane — 16 (two consecutive 8-element chunks, LPG = gs / 16 lanes per
+// group) halves the per-candidate group work per element (reductions, RTN parameters, table
+// checks).  The loss tree is unchanged: each chunk is summed in order, the lane adds its two
+// chunks (the tree's first pairwise level; + is commutative), grp_sum does the rest.
+template <int DT, int LPG, bool SYM, int EPL>
 __global__ __launch_bounds__(256) void act_loss_kernel(const void* __restrict__ w, int64_t R, int64_t K, int lpg_rt,
                                                        int qmin, int qmax, const float* __restrict__ table,
                                                        const float* __restrict__ rtable, int n_grid,
@@ -475,27 +481,31 @@ __global__ __launch_bounds__(256) void act_loss_kernel(const void* __restrict__ 
     typedef HwFmt<DT> H;
     const int lpg = LPG ? LPG : lpg_rt;
     constexpr int sym = SYM ? 1 : 0;
-    const int64_t G = K / (8 * lpg);
+    const int64_t G = K / (EPL * lpg);
     const int64_t nw = (int64_t)gridDim.x * 4;
     const bool leader = (threadIdx.x & 63) % lpg == 0;
     const float rq = 1.0f / (float)(qmax - qmin);   // RN_f32(1 / 15) or RN_f32(1 / 255)
     for (int64_t item = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);; item += nw) {
         GroupLane gl;
-        if (!group_lane(item, R, G, lpg, gl)) break;
-        float v[8], h[8];
-        if (gl.valid) load8<DT>(w, gl.r * K + gl.k0, v);
-        else for (int j = 0; j < 8; ++j) v[j] = 0.0f;
-        load8<AWQ_DTYPE_F32>(x_sq, gl.k0, h);
+        if (!group_lane<EPL>(item, R, G, lpg, gl)) break;
+        float v[EPL], h[EPL];
+#pragma unroll
+        for (int c = 0; c < EPL; c += 8) {
+            if (gl.valid) load8<DT>(w, gl.r * K + gl.k0 + c, *(float(*)[8]) & v[c]);
+            else for (int j = 0; j < 8; ++j) v[c + j] = 0.0f;
+            load8<AWQ_DTYPE_F32>(x_sq, gl.k0 + c, *(float(*)[8]) & h[c]);
+        }
         for (int i = 0; i < n_grid; ++i) {
-            float s[8], ws[8];
-            load8<AWQ_DTYPE_F32>(table, (int64_t)i * K + gl.k0, s);
+            float s[EPL], ws[EPL];
+#pragma unroll
+            for (int c = 0; c < EPL; c += 8) load8<AWQ_DTYPE_F32>(table, (int64_t)i * K + gl.k0 + c, *(float(*)[8]) & s[c]);
             // min / max skipping NaN (fmin / fmax; the signs of zero extrema cannot change the
             // scale or zero point) with NaN tracked on the side: torch's NaN-propagating
             // min / max once combined
             float mn = __builtin_inff(), mx = -__builtin_inff();
             int nan = 0;
 #pragma unroll
-            for (int j = 0; j < 8; ++j) {
+            for (int j = 0; j < EPL; ++j) {
                 ws[j] = H::rn(v[j] * s[j]);
                 nan |= ws[j] != ws[j];
                 mn = __builtin_fminf(mn, ws[j]);
@@ -505,15 +515,19 @@ __global__ __launch_bounds__(256) void act_loss_kernel(const void* __restrict__ 
             if (nan) { mn = __builtin_nanf(""); mx = __builtin_nanf(""); }
             float cs, cz, r;
             hw_group_params<DT>(mn, mx, nan, qmin, qmax, sym, rq, cs, cz, r);
-            float acc = 0.0f;
+            float acc[EPL / 8];
+#pragma unroll
+            for (int c = 0; c < EPL / 8; ++c) acc[c] = 0.0f;
             // channel reciprocals for ŵ = dq / s (0 = outside the proven range: IEEE division)
-            float rs[8];
+            float rs[EPL];
             bool mq = false;
             if (rtable != nullptr) {
-                load8<AWQ_DTYPE_F32>(rtable, (int64_t)i * K + gl.k0, rs);
+#pragma unroll
+                for (int c = 0; c < EPL; c += 8)
+                    load8<AWQ_DTYPE_F32>(rtable, (int64_t)i * K + gl.k0 + c, *(float(*)[8]) & rs[c]);
                 float m = rs[0];
 #pragma unroll
-                for (int j = 1; j < 8; ++j) m = __builtin_fminf(m, rs[j]);
+                for (int j = 1; j < EPL; ++j) m = __builtin_fminf(m, rs[j]);
                 mq = __builtin_amdgcn_ballot_w64(!(m > 0.0f)) == 0;   // wave-uniform
             }
             if (cs > 0.0f && cs < __builtin_inff()) {
@@ -521,9 +535,9 @@ __global__ __launch_bounds__(256) void act_loss_kernel(const void* __restrict__ 
                 // RN(w'/s) from the group's reciprocal, hardware RNE conversions; q - z is an
                 // integer |.| <= 510, exact in fp16, so only the product is rounded
                 const float sh = (float)(_Float16)cs;
-                float dq[8];
+                float dq[EPL];
 #pragma unroll
-                for (int j = 0; j < 8; ++j) {
+                for (int j = 0; j < EPL; ++j) {
                     const float t = H::quot(ws[j], cs, r);
                     const float u = sym ? t : H::rn(t + cz);
                     const float q = __builtin_amdgcn_fmed3f(__builtin_rintf(u), (float)qmin, (float)qmax);
@@ -531,30 +545,32 @@ __global__ __launch_bounds__(256) void act_loss_kernel(const void* __restrict__ 
                 }
                 if (mq) {
 #pragma unroll
-                    for (int j = 0; j < 8; ++j) {
+                    for (int j = 0; j < EPL; ++j) {
                         const float e = mquot(dq[j], s[j], rs[j]) - v[j];
-                        acc = acc + h[j] * (e * e);
+                        acc[j / 8] = acc[j / 8] + h[j] * (e * e);
                     }
                 } else {
 #pragma unroll
-                    for (int j = 0; j < 8; ++j) {
+                    for (int j = 0; j < EPL; ++j) {
                         const float e = dq[j] / s[j] - v[j];
-                        acc = acc + h[j] * (e * e);
+                        acc[j / 8] = acc[j / 8] + h[j] * (e * e);
                     }
                 }
             } else {
                 const float sh = sw_f16_to_f32(canon_f16(cs));
 #pragma unroll
-                for (int j = 0; j < 8; ++j) {
+                for (int j = 0; j < EPL; ++j) {
                     const float q = quant1<DT>(ws[j], cs, cz, qmin, qmax);
                     const float hq = sw_f16_to_f32(sw_f32_to_f16(q - cz));
                     const float dq = sw_f16_to_f32(sw_f32_to_f16(hq * sh));
                     const float e = dq / s[j] - v[j];
-                    acc = acc + h[j] * (e * e);
+                    acc[j / 8] = acc[j / 8] + h[j] * (e * e);
                 }
             }
-            acc = grp_sum(acc, lpg);
-            if (gl.valid && leader) part[(int64_t)i * stride + gl.r * G + gl.g] = acc;
+            float a = acc[0];
+            if (EPL == 16) a = acc[0] + acc[EPL / 8 - 1];
+            a = grp_sum(a, lpg);
+            if (gl.valid && leader) part[(int64_t)i * stride + gl.r * G + gl.g] = a;
         }
     }
 }
@@ -812,17 +828,20 @@ hipError_t launch_act_losses(const void* w, int dtype, int64_t R, int64_t K, int
     const int lpg = (int)(L / 8);
     const int64_t items = ((R + (64 / lpg) - 1) / (64 / lpg)) * (K / L);
     const unsigned grid = blocks_for(items, 4, 256 * 32);
-#define AWQ_LOSS_LAUNCH(LP, SY)                                                                                    \
-    AWQ_DT_SWITCH(dtype, hipLaunchKernelGGL((act_loss_kernel<D, LP, SY>), dim3(grid), dim3(256), 0, stream, w, R, K, \
-                                            lpg, qmin, qmax, table, rtable, n_grid, x_sq, part, stride))
-#define AWQ_LOSS_SYM(LP)                 \
-    if (symmetric) { AWQ_LOSS_LAUNCH(LP, true) } else { AWQ_LOSS_LAUNCH(LP, false) }
-    switch (lpg) {   // the streaming group sizes 32 / 64 / 128 / 256 as constants
-    case 4: AWQ_LOSS_SYM(4) break;
-    case 8: AWQ_LOSS_SYM(8) break;
-    case 16: AWQ_LOSS_SYM(16) break;
-    case 32: AWQ_LOSS_SYM(32) break;
-    default: AWQ_LOSS_SYM(0) break;
+#define AWQ_LOSS_LAUNCH(LP, SY, EP, LPA)                                                                       \
+    AWQ_DT_SWITCH(dtype, hipLaunchKernelGGL((act_loss_kernel<D, LP, SY, EP>), dim3(g2), dim3(256), 0, stream, w, R, \
+                                            K, LPA, qmin, qmax, table, rtable, n_grid, x_sq, part, stride))
+#define AWQ_LOSS_SYM(LP, EP, LPA)                                                   \
+    if (symmetric) { AWQ_LOSS_LAUNCH(LP, true, EP, LPA) } else { AWQ_LOSS_LAUNCH(LP, false, EP, LPA) }
+    // the streaming group sizes 32 / 64 / 128 / 256: 16 elements per lane, gs / 16 lanes per
+    // group as a constant (twice the groups per wave: half the items)
+    const unsigned g2 = (lpg >= 4 && lpg <= 32) ? blocks_for((items + 1) / 2, 4, 256 * 32) : grid;
+    switch (lpg) {
+    case 4: AWQ_LOSS_SYM(2, 16, 2) break;
+    case 8: AWQ_LOSS_SYM(4, 16, 4) break;
+    case 16: AWQ_LOSS_SYM(8, 16, 8) break;
+    case 32: AWQ_LOSS_SYM(16, 16, 16) break;
+    default: AWQ_LOSS_SYM(0, 8, lpg) break;
     }
 #undef AWQ_LOSS_SYM
 #undef AWQ_LOSS_LAUNCH

@@ -181,7 +181,9 @@ def test_gpu_table_within_one_ulp(duo):
 LOSS_CASES = [(torch.bfloat16, 128, 4, False), (torch.bfloat16, 128, 4, True), (torch.bfloat16, 128, 8, False),
               (torch.float16, 128, 4, False), (torch.float16, 64, 4, True), (torch.float32, 128, 4, False),
               (torch.bfloat16, 32, 4, False), (torch.bfloat16, 512, 4, False), (torch.bfloat16, 8, 8, True),
-              (torch.float16, 256, 8, False)]
+              (torch.float16, 256, 8, False), (torch.float32, 32, 8, True), (torch.float16, 32, 4, False),
+              (torch.bfloat16, 256, 4, True), (torch.float32, 64, 4, True), (torch.bfloat16, 16, 4, False),
+              (torch.float32, 256, 4, False)]
 
 
 @pytest.mark.gpu

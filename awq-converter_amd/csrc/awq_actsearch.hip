@@ -354,6 +354,84 @@ __global__ __launch_bounds__(256) void colsum_tile_kernel(const void* __restrict
     if (MODE == 0) part1[b * K + kt + tid] = s1;
 }
 
+// 16-bit inputs (bf16 / fp16): the same chains over a 256-row x 128-column tile kept in LDS
+// as the raw 16-bit values (64 KiB) plus, for MODE 1, the tile's per-row group normalisers;
+// every thread's 16 loads are in flight at once; 128 lanes then run the column chains,
+// forming each term (MODE 1: fp32(|w| / den)) from LDS exactly as colsum_kernel does.
+constexpr int kColTileW = 128;
+template <int DT, int MODE>
+__global__ __launch_bounds__(256) void colsum_wide_kernel(const void* __restrict__ src, int64_t rows, int64_t K,
+                                                          int64_t L, const float* __restrict__ gmax,
+                                                          double* __restrict__ part0, double* __restrict__ part1) {
+    typedef Traits<DT> T;
+    constexpr int OPR = kColTileW / 8;                  // 16-B octets per row
+    constexpr int NI = kRowBlock * OPR / 256;           // loads per thread
+    constexpr int ND = MODE == 1 ? kRowBlock * OPR / 256 : 1;   // normalisers per thread
+    __shared__ __attribute__((aligned(16))) uint16_t sv[kRowBlock][kColTileW];
+    __shared__ float sden[MODE == 1 ? kRowBlock : 1][MODE == 1 ? OPR : 1];
+    const int tid = threadIdx.x;
+    const int64_t kt = (int64_t)blockIdx.x * kColTileW;
+    const int64_t b = blockIdx.y, r0 = b * kRowBlock;
+    const int nr = (int)((r0 + kRowBlock < rows) ? kRowBlock : rows - r0);
+    const int oc = tid % OPR, rl = tid / OPR;
+    const int64_t k0 = kt + 8 * oc;
+    const uint16_t* p = (const uint16_t*)src;
+    uint4 v[NI];
+#pragma unroll
+    for (int it = 0; it < NI; ++it) {
+        const int rr = rl + (256 / OPR) * it;
+        v[it] = (k0 < K && rr < nr) ? *(const uint4*)(p + (r0 + rr) * K + k0) : make_uint4(0, 0, 0, 0);
+    }
+    const int64_t G = K / L;
+    const int64_t g0 = kt / L;                           // the tile's first group
+    const int64_t kend = (kt + kColTileW < K) ? kt + kColTileW : K;
+    const int ngt = (int)((kend - 1) / L - g0 + 1);     // groups in the tile (<= OPR: L >= 8)
+    float dn[ND];
+    if (MODE == 1) {
+#pragma unroll
+        for (int u = 0; u < ND; ++u) {
+            const int e = tid + 256 * u, rr = e / OPR, gi = e % OPR;
+            dn[u] = (rr < nr && gi < ngt) ? gmax[(r0 + rr) * G + g0 + gi] + 1e-6f : 1.0f;
+        }
+    }
+#pragma unroll
+    for (int it = 0; it < NI; ++it) *(uint4*)&sv[rl + (256 / OPR) * it][8 * oc] = v[it];
+    if (MODE == 1) {
+#pragma unroll
+        for (int u = 0; u < ND; ++u) {
+            const int e = tid + 256 * u;
+            sden[e / OPR][e % OPR] = dn[u];
+        }
+    }
+    __syncthreads();
+    if (tid >= kColTileW || kt + tid >= K) return;
+    const int gi = (int)((kt + tid) / L - g0);
+    double s0 = 0.0, s1 = 0.0;
+    for (int r = 0; r < nr; r += 16) {
+        float t[16];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            const int rr = (r + j < nr) ? r + j : nr - 1;
+            t[j] = T::load(&sv[rr][tid], 0);
+            if (MODE == 1) t[j] = __builtin_fabsf(t[j]) / sden[rr][gi];
+        }
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            if (r + j < nr) {
+                const double d = (double)t[j];
+                if (MODE == 0) {
+                    s0 += __builtin_fabs(d);
+                    s1 += d * d;
+                } else {
+                    s0 += d;
+                }
+            }
+        }
+    }
+    part0[b * K + kt + tid] = s0;
+    if (MODE == 0) part1[b * K + kt + tid] = s1;
+}
+
 // Lane layout shared by the group kernels: LPG = L / 8 lanes per group (8 consecutive
 // elements per lane), GPW = 64 / LPG groups per wave, the wave's groups are GPW
 // consecutive ROWS of one group column g (the same k range: table / x_sq loads are shared).
@@ -585,18 +663,24 @@ __global__ __launch_bounds__(256) void loss_block_kernel(const float* __restrict
     const int tid = threadIdx.x;
     const int64_t c0 = (int64_t)blockIdx.x * kLossChains;
     const int64_t nch = (int64_t)n_grid * nblk;
-#pragma unroll 4
+    // every load first (64 per thread in flight), then the LDS stores: a load -> store loop
+    // would wait out one memory round trip per element
+    constexpr int NE = kGroupBlock / 256;
+    float t[kLossChains][NE];
+#pragma unroll
     for (int c = 0; c < kLossChains; ++c) {
-        const int64_t idx = c0 + c;
-        if (idx >= nch) break;
+        const int64_t idx = (c0 + c < nch) ? c0 + c : nch - 1;
         const int64_t i = idx / nblk, b = idx - i * nblk;
         const int64_t g0 = b * kGroupBlock;
         const int64_t n = (g0 + kGroupBlock < stride) ? kGroupBlock : stride - g0;
         const float* p = part + i * stride + g0;
 #pragma unroll
-        for (int e = 0; e < kGroupBlock / 256; ++e)
-            if (e * 256 + tid < n) sp[c][e * 256 + tid] = p[e * 256 + tid];
+        for (int e = 0; e < NE; ++e) t[c][e] = (e * 256 + tid < n) ? p[e * 256 + tid] : 0.0f;
     }
+#pragma unroll
+    for (int c = 0; c < kLossChains; ++c)
+#pragma unroll
+        for (int e = 0; e < NE; ++e) sp[c][e * 256 + tid] = t[c][e];
     __syncthreads();
     const int64_t idx = c0 + tid;
     if (tid >= kLossChains || idx >= nch) return;
@@ -633,10 +717,17 @@ __global__ __launch_bounds__(256) void select_kernel(const double* __restrict__ 
     for (int64_t b0 = 0; b0 < nblk; b0 += cb) {
         const int64_t nb = (b0 + cb < nblk) ? cb : nblk - b0;
         __syncthreads();
-        for (int64_t e = tid; e < (int64_t)n_grid * nb; e += 256) {
+        double t[kChunkElems / 256];                   // all loads in flight, then the stores
+        const int64_t ne = (int64_t)n_grid * nb;
+#pragma unroll
+        for (int u = 0; u < kChunkElems / 256; ++u) {
+            const int64_t e = tid + 256 * u;
             const int64_t i = e / nb, j = e - i * nb;
-            sw[i * nb + j] = work[i * nblk + b0 + j];
+            t[u] = (e < ne) ? work[i * nblk + b0 + j] : 0.0;
         }
+#pragma unroll
+        for (int u = 0; u < kChunkElems / 256; ++u)
+            if (tid + 256 * u < ne) sw[tid + 256 * u] = t[u];
         __syncthreads();
         if (tid < n_grid)
             for (int64_t j = 0; j < nb; j += 8) {          // 8 LDS values ahead of the chain
@@ -734,7 +825,15 @@ hipError_t launch_act_stats(const void* x, int dtype, int64_t T, int64_t K, doub
     const int64_t nblk = (T + kRowBlock - 1) / kRowBlock;
     double* p0 = work;
     double* p1 = work + nblk * K;
-    if (K % 8 == 0 && (uintptr_t)x % 16 == 0) {
+    if (K % 8 == 0 && (uintptr_t)x % 16 == 0 && dtype != AWQ_DTYPE_F32) {
+        const dim3 gw((unsigned)((K + kColTileW - 1) / kColTileW), (unsigned)nblk);
+        if (dtype == AWQ_DTYPE_BF16)
+            hipLaunchKernelGGL((colsum_wide_kernel<AWQ_DTYPE_BF16, 0>), gw, dim3(256), 0, stream, x, T, K, K, nullptr,
+                               p0, p1);
+        else
+            hipLaunchKernelGGL((colsum_wide_kernel<AWQ_DTYPE_F16, 0>), gw, dim3(256), 0, stream, x, T, K, K, nullptr,
+                               p0, p1);
+    } else if (K % 8 == 0 && (uintptr_t)x % 16 == 0) {
         const dim3 gt((unsigned)((K + kColTile - 1) / kColTile), (unsigned)nblk);
         AWQ_DT_SWITCH(dtype, hipLaunchKernelGGL((colsum_tile_kernel<D, 0>), gt, dim3(256), 0, stream, x, T, K, K,
                                                 nullptr, p0, p1))
@@ -759,7 +858,15 @@ hipError_t launch_weight_colsum(const void* w, int dtype, int64_t R, int64_t K, 
                                             dim3(256), 0, stream, w, R, K, lpg, gmax))
     if (hipError_t e = hipPeekAtLastError()) return e;
     const int64_t nblk = (R + kRowBlock - 1) / kRowBlock;
-    if (K % 8 == 0 && L % 8 == 0 && (uintptr_t)w % 16 == 0) {
+    if (K % 8 == 0 && L % 8 == 0 && (uintptr_t)w % 16 == 0 && dtype != AWQ_DTYPE_F32) {
+        const dim3 gw((unsigned)((K + kColTileW - 1) / kColTileW), (unsigned)nblk);
+        if (dtype == AWQ_DTYPE_BF16)
+            hipLaunchKernelGGL((colsum_wide_kernel<AWQ_DTYPE_BF16, 1>), gw, dim3(256), 0, stream, w, R, K, L, gmax, part,
+                               nullptr);
+        else
+            hipLaunchKernelGGL((colsum_wide_kernel<AWQ_DTYPE_F16, 1>), gw, dim3(256), 0, stream, w, R, K, L, gmax, part,
+                               nullptr);
+    } else if (K % 8 == 0 && L % 8 == 0 && (uintptr_t)w % 16 == 0) {
         const dim3 gt((unsigned)((K + kColTile - 1) / kColTile), (unsigned)nblk);
         AWQ_DT_SWITCH(dtype, hipLaunchKernelGGL((colsum_tile_kernel<D, 1>), gt, dim3(256), 0, stream, w, R, K, L,
                                                 gmax, part, nullptr))

@@ -405,6 +405,7 @@ def quantize_stream(loader, infos: List[TensorInfo], quantizer: AWQQuantizer, de
     act_stats (scale_method="awq"): name -> (x_mean, x_sq); those weights take the
     activation-aware search (AWQQuantizer.quantize_layer_group, one weight per layer group)
     and carry its "input_scale" in their results."""
+    t_enter = time.perf_counter()
     if not (device.startswith("cuda") and torch.cuda.is_available()):
         quantizer.compute_device()   # raises HipUnavailable: no CPU path
     dev = torch.device(device)
@@ -413,21 +414,49 @@ def quantize_stream(loader, infos: List[TensorInfo], quantizer: AWQQuantizer, de
     torch.cuda.set_device(dev)
     copy_stream = torch.cuda.Stream(dev)
     compute = torch.cuda.current_stream(dev)
-    batches = _batches(infos, batch_bytes)
+    # batches small enough that a small model still pipelines (read / H2D / kernel / D2H of
+    # neighbouring batches overlap): about 8 batches per device, 32 MiB .. batch_bytes each
+    total = sum(i.nbytes for i in infos)
+    budget = int(os.environ.get("AWQ_CLI_BATCH_MB", "0")) << 20 or max(32 << 20, min(batch_bytes, total // 8))
+    batches = _batches(infos, budget)
     depth = max(1, lookahead // max(1, max(len(b) for b in batches) if batches else 1))
+    clock = time.perf_counter
+    t_read = t_submit = t_finish = 0.0
 
     direct = hasattr(loader, "read_pinned") and os.environ.get("AWQ_CLI_MMAP_READ", "0") != "1"
 
-    def read(info):
-        # straight from the file into pinned memory (one copy); AWQ_CLI_MMAP_READ=1: the
-        # safetensors mmap read + a pinned copy (two)
+    def read(info, dst=None):
+        # straight from the file into pinned memory (one copy) — into the batch's staging
+        # buffer when one is given; AWQ_CLI_MMAP_READ=1: the safetensors mmap read + a pinned
+        # copy (two)
+        if dst is not None:
+            return loader.read_into(info, dst)
         return loader.read_pinned(info) if direct else _pinned_copy(loader.read(info))
+
+    staging = {}   # batch -> (pinned uint8 buffer, name -> byte offset): one H2D per batch
+
+    def stage(k):
+        offs, pos = {}, 0
+        for info in batches[k]:
+            if info.dtype is None:
+                continue
+            offs[info.name] = pos
+            pos += (info.nbytes + 255) // 256 * 256      # 256-B aligned slices (16-B vector loads)
+        buf = torch.empty(max(pos, 1), dtype=torch.uint8, pin_memory=True)
+        staging[k] = (buf, offs)
+        return buf, offs
+
+    def view(buf, off, info):
+        return buf[off:off + info.nbytes].view(info.dtype).view(info.shape)
 
     inflight = deque()
 
     def finish(entry):
+        nonlocal t_finish
         results, ev, _keep = entry
+        t0 = clock()
         ev.synchronize()
+        t_finish += clock() - t0
         with lock:
             out.update(results)
         for name in results:
@@ -441,13 +470,19 @@ def quantize_stream(loader, infos: List[TensorInfo], quantizer: AWQQuantizer, de
 
         def submit(k):
             if k < len(batches) and k not in futs:
-                futs[k] = [(info, pool.submit(read, info)) for info in batches[k]]
+                if direct:
+                    buf, offs = stage(k)
+                    futs[k] = [(info, pool.submit(read, info, view(buf, offs[info.name], info) if info.name in offs
+                                                  else None)) for info in batches[k]]
+                else:
+                    futs[k] = [(info, pool.submit(read, info)) for info in batches[k]]
 
         for k in range(min(len(batches), depth + 1)):
             submit(k)
         for k in range(len(batches)):
             submit(k + depth)
             host = {}
+            t0 = clock()
             for info, fut in futs.pop(k):
                 try:
                     host[info.name] = fut.result()
@@ -456,13 +491,24 @@ def quantize_stream(loader, infos: List[TensorInfo], quantizer: AWQQuantizer, de
                         logger.error(f"Failed to quantize tensor {info.name} on {device}: {e}")
                     if on_done:
                         on_done(info.name, None)
+            t1 = clock()
+            t_read += t1 - t0
             if not host:
                 continue
             if logger:
                 for name in host:
                     logger.info(f"Quantizing tensor: {name} on {device}")
+            staged = None
             with torch.cuda.stream(copy_stream):
-                dev_in = {n: t.to(dev, non_blocking=True) for n, t in host.items()}
+                if k in staging:     # the whole staging buffer in one copy; device views of it
+                    buf, offs = staging.pop(k)
+                    dbuf = torch.empty(buf.numel(), dtype=torch.uint8, device=dev)
+                    dbuf.copy_(buf, non_blocking=True)
+                    by_name = {i.name: i for i in batches[k]}
+                    dev_in = {n: view(dbuf, offs[n], by_name[n]) for n in host}
+                    staged = buf                      # kept alive until the copy is done
+                else:
+                    dev_in = {n: t.to(dev, non_blocking=True) for n, t in host.items()}
                 ev_in = torch.cuda.Event()
                 ev_in.record(copy_stream)
             compute.wait_event(ev_in)
@@ -509,14 +555,20 @@ def quantize_stream(loader, infos: List[TensorInfo], quantizer: AWQQuantizer, de
                     host_res[name] = hr
                 ev_out = torch.cuda.Event()
                 ev_out.record(copy_stream)
+            t_submit += clock() - t1
             # inputs and device results stay referenced until their copies are done
-            inflight.append((host_res, ev_out, (host, dev_in, res)))
+            inflight.append((host_res, ev_out, (host, dev_in, res, staged)))
             while len(inflight) > 1:
                 finish(inflight.popleft())
             if memory_efficient:
                 torch.cuda.empty_cache()
         while inflight:
             finish(inflight.popleft())
+    # host-side phase times of this device's pipeline (scripts/cli_bench.py prints them)
+    TIMINGS.update({f"stream_{device}": {"wall_s": round(time.perf_counter() - t_enter, 4),
+                                          "batches": len(batches), "batch_MB": budget >> 20,
+                                          "read_wait_s": round(t_read, 4), "submit_s": round(t_submit, 4),
+                                          "finish_wait_s": round(t_finish, 4)}})
 
 
 def _with_input_scale(exported: Dict[str, torch.Tensor], packed: Dict[str, torch.Tensor]) -> Dict[str, torch.Tensor]:
@@ -547,7 +599,12 @@ def _device_worker(*args, **kwargs) -> None:
     logged; its tensors then count as not quantized."""
     logger, device = args[9], args[3]
     try:
-        quantize_stream(*args, **kwargs)
+        prof_path = os.environ.get("AWQ_CLI_PROFILE")   # diagnostics: cProfile of this thread
+        if prof_path:
+            import cProfile
+            cProfile.runctx("quantize_stream(*args, **kwargs)", globals(), locals(), prof_path)
+        else:
+            quantize_stream(*args, **kwargs)
     except Exception as e:  # noqa: BLE001
         if logger:
             logger.error(f"Quantization on {device} failed: {e}")

@@ -310,7 +310,8 @@ class AWQQuantizer:
         if eligible:
             dev = self.compute_device()
             for dt in (torch.bfloat16, torch.float16, torch.float32):   # one ragged launch per input dtype
-                part = {k: v.detach().to(dev).contiguous() for k, v in eligible.items() if v.dtype == dt}
+                part = {k: (v if v.device == dev and v.is_contiguous() else v.detach().to(dev).contiguous())
+                        for k, v in eligible.items() if v.dtype == dt}
                 if part:
                     batch = PackedBatch(part, bits=self.bits, symmetric=self.symmetric, group_size=self.group_size)
                     batch.run()
@@ -351,7 +352,8 @@ class AWQQuantizer:
         if eligible:
             dev = self.compute_device()
             for dt in (torch.bfloat16, torch.float16, torch.float32):
-                part = {k: v.detach().to(dev).contiguous() for k, v in eligible.items() if v.dtype == dt}
+                part = {k: (v if v.device == dev and v.is_contiguous() else v.detach().to(dev).contiguous())
+                        for k, v in eligible.items() if v.dtype == dt}
                 if part:
                     batch = PackedBatch(part, bits=self.bits, symmetric=self.symmetric, parity=True, packed=False,
                                         group_size=self.group_size)

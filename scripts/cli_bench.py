@@ -68,7 +68,7 @@ def main():
                           "output_GB": round(out_bytes / 1e9, 3), "wall_s": round(wall, 3),
                           "input_GBs": round(nbytes / wall / 1e9, 3), "model_build_s": round(build_s, 1),
                           "serial_save": os.environ.get("AWQ_CLI_SERIAL_SAVE", "0") == "1",
-                          "phases_s": {k: round(v, 3) for k, v in cli_mod.TIMINGS.items()}}), flush=True)
+                          "phases_s": {k: (round(v, 3) if isinstance(v, float) else v) for k, v in cli_mod.TIMINGS.items()}}), flush=True)
         shutil.rmtree(out, ignore_errors=True)
     if args.workdir is None:
         shutil.rmtree(work, ignore_errors=True)

@@ -289,11 +289,14 @@ __global__ __launch_bounds__(256) void colmean_kernel(const double* __restrict__
     out[k] = (float)(s / divisor);
 }
 
-// Same sums, staged through LDS: a workgroup takes one 256-row block x 64 columns; every
-// thread loads 8 rows x 8 columns (16-B loads, all in flight at once) and stores the fp32
-// terms (MODE 1: the quotient, computed at load time) in LDS; then 64 lanes run the 64
-// column chains (rows ascending, fp64) from LDS.  Needs K % 8 == 0 and a 16-B aligned src.
-constexpr int kColTile = 64;
+// Same sums, staged through LDS: a workgroup takes one 256-row block x kColTile columns;
+// every thread loads 8-column octets of several rows (16-B loads, all in flight at once) and
+// stores the fp32 terms (MODE 1: the quotient, computed at load time) in LDS; then
+// kColTile lanes run the column chains (rows ascending, fp64) from LDS.  Needs K % 8 == 0
+// and a 16-B aligned src.
+// 32 columns: 32 KiB of LDS, several workgroups per CU overlap one another's load and chain
+// phases (r90: 64 columns or a 128-column tile of raw 16-bit values were 5-25 % slower)
+constexpr int kColTile = 32;
 template <int DT, int MODE>
 __global__ __launch_bounds__(256) void colsum_tile_kernel(const void* __restrict__ src, int64_t rows, int64_t K,
                                                           int64_t L, const float* __restrict__ gmax,
@@ -303,15 +306,16 @@ __global__ __launch_bounds__(256) void colsum_tile_kernel(const void* __restrict
     const int64_t kt = (int64_t)blockIdx.x * kColTile;
     const int64_t b = blockIdx.y, r0 = b * kRowBlock;
     const int nr = (int)((r0 + kRowBlock < rows) ? kRowBlock : rows - r0);
-    const int oc = tid & 7, rl = tid >> 3;             // column octet, first row
+    constexpr int OPR = kColTile / 8, RPP = 256 / OPR;   // octets per row, rows per pass
+    const int oc = tid % OPR, rl = tid / OPR;           // column octet, first row
     const int64_t k0 = kt + 8 * oc;
     const bool kin = k0 < K;
-    constexpr int NI = kRowBlock / 32;
+    constexpr int NI = kRowBlock / RPP;
     float v[NI][8];
     float den[NI];
 #pragma unroll
     for (int it = 0; it < NI; ++it) {
-        const int rr = rl + 32 * it;
+        const int rr = rl + RPP * it;
         if (kin && rr < nr) {
             load8<DT>(src, (r0 + rr) * K + k0, v[it]);
             if (MODE == 1) den[it] = gmax[(r0 + rr) * (K / L) + k0 / L] + 1e-6f;
@@ -323,7 +327,7 @@ __global__ __launch_bounds__(256) void colsum_tile_kernel(const void* __restrict
     }
 #pragma unroll
     for (int it = 0; it < NI; ++it) {
-        const int rr = rl + 32 * it;
+        const int rr = rl + RPP * it;
         if (MODE == 1)
 #pragma unroll
             for (int j = 0; j < 8; ++j) v[it][j] = __builtin_fabsf(v[it][j]) / den[it];
@@ -337,84 +341,6 @@ __global__ __launch_bounds__(256) void colsum_tile_kernel(const void* __restrict
         float t[16];
 #pragma unroll
         for (int j = 0; j < 16; ++j) t[j] = sv[(r + j < nr) ? r + j : nr - 1][tid];
-#pragma unroll
-        for (int j = 0; j < 16; ++j) {
-            if (r + j < nr) {
-                const double d = (double)t[j];
-                if (MODE == 0) {
-                    s0 += __builtin_fabs(d);
-                    s1 += d * d;
-                } else {
-                    s0 += d;
-                }
-            }
-        }
-    }
-    part0[b * K + kt + tid] = s0;
-    if (MODE == 0) part1[b * K + kt + tid] = s1;
-}
-
-// 16-bit inputs (bf16 / fp16): the same chains over a 256-row x 128-column tile kept in LDS
-// as the raw 16-bit values (64 KiB) plus, for MODE 1, the tile's per-row group normalisers;
-// every thread's 16 loads are in flight at once; 128 lanes then run the column chains,
-// forming each term (MODE 1: fp32(|w| / den)) from LDS exactly as colsum_kernel does.
-constexpr int kColTileW = 128;
-template <int DT, int MODE>
-__global__ __launch_bounds__(256) void colsum_wide_kernel(const void* __restrict__ src, int64_t rows, int64_t K,
-                                                          int64_t L, const float* __restrict__ gmax,
-                                                          double* __restrict__ part0, double* __restrict__ part1) {
-    typedef Traits<DT> T;
-    constexpr int OPR = kColTileW / 8;                  // 16-B octets per row
-    constexpr int NI = kRowBlock * OPR / 256;           // loads per thread
-    constexpr int ND = MODE == 1 ? kRowBlock * OPR / 256 : 1;   // normalisers per thread
-    __shared__ __attribute__((aligned(16))) uint16_t sv[kRowBlock][kColTileW];
-    __shared__ float sden[MODE == 1 ? kRowBlock : 1][MODE == 1 ? OPR : 1];
-    const int tid = threadIdx.x;
-    const int64_t kt = (int64_t)blockIdx.x * kColTileW;
-    const int64_t b = blockIdx.y, r0 = b * kRowBlock;
-    const int nr = (int)((r0 + kRowBlock < rows) ? kRowBlock : rows - r0);
-    const int oc = tid % OPR, rl = tid / OPR;
-    const int64_t k0 = kt + 8 * oc;
-    const uint16_t* p = (const uint16_t*)src;
-    uint4 v[NI];
-#pragma unroll
-    for (int it = 0; it < NI; ++it) {
-        const int rr = rl + (256 / OPR) * it;
-        v[it] = (k0 < K && rr < nr) ? *(const uint4*)(p + (r0 + rr) * K + k0) : make_uint4(0, 0, 0, 0);
-    }
-    const int64_t G = K / L;
-    const int64_t g0 = kt / L;                           // the tile's first group
-    const int64_t kend = (kt + kColTileW < K) ? kt + kColTileW : K;
-    const int ngt = (int)((kend - 1) / L - g0 + 1);     // groups in the tile (<= OPR: L >= 8)
-    float dn[ND];
-    if (MODE == 1) {
-#pragma unroll
-        for (int u = 0; u < ND; ++u) {
-            const int e = tid + 256 * u, rr = e / OPR, gi = e % OPR;
-            dn[u] = (rr < nr && gi < ngt) ? gmax[(r0 + rr) * G + g0 + gi] + 1e-6f : 1.0f;
-        }
-    }
-#pragma unroll
-    for (int it = 0; it < NI; ++it) *(uint4*)&sv[rl + (256 / OPR) * it][8 * oc] = v[it];
-    if (MODE == 1) {
-#pragma unroll
-        for (int u = 0; u < ND; ++u) {
-            const int e = tid + 256 * u;
-            sden[e / OPR][e % OPR] = dn[u];
-        }
-    }
-    __syncthreads();
-    if (tid >= kColTileW || kt + tid >= K) return;
-    const int gi = (int)((kt + tid) / L - g0);
-    double s0 = 0.0, s1 = 0.0;
-    for (int r = 0; r < nr; r += 16) {
-        float t[16];
-#pragma unroll
-        for (int j = 0; j < 16; ++j) {
-            const int rr = (r + j < nr) ? r + j : nr - 1;
-            t[j] = T::load(&sv[rr][tid], 0);
-            if (MODE == 1) t[j] = __builtin_fabsf(t[j]) / sden[rr][gi];
-        }
 #pragma unroll
         for (int j = 0; j < 16; ++j) {
             if (r + j < nr) {
@@ -825,15 +751,7 @@ hipError_t launch_act_stats(const void* x, int dtype, int64_t T, int64_t K, doub
     const int64_t nblk = (T + kRowBlock - 1) / kRowBlock;
     double* p0 = work;
     double* p1 = work + nblk * K;
-    if (K % 8 == 0 && (uintptr_t)x % 16 == 0 && dtype != AWQ_DTYPE_F32) {
-        const dim3 gw((unsigned)((K + kColTileW - 1) / kColTileW), (unsigned)nblk);
-        if (dtype == AWQ_DTYPE_BF16)
-            hipLaunchKernelGGL((colsum_wide_kernel<AWQ_DTYPE_BF16, 0>), gw, dim3(256), 0, stream, x, T, K, K, nullptr,
-                               p0, p1);
-        else
-            hipLaunchKernelGGL((colsum_wide_kernel<AWQ_DTYPE_F16, 0>), gw, dim3(256), 0, stream, x, T, K, K, nullptr,
-                               p0, p1);
-    } else if (K % 8 == 0 && (uintptr_t)x % 16 == 0) {
+    if (K % 8 == 0 && (uintptr_t)x % 16 == 0) {
         const dim3 gt((unsigned)((K + kColTile - 1) / kColTile), (unsigned)nblk);
         AWQ_DT_SWITCH(dtype, hipLaunchKernelGGL((colsum_tile_kernel<D, 0>), gt, dim3(256), 0, stream, x, T, K, K,
                                                 nullptr, p0, p1))
@@ -858,15 +776,7 @@ hipError_t launch_weight_colsum(const void* w, int dtype, int64_t R, int64_t K, 
                                             dim3(256), 0, stream, w, R, K, lpg, gmax))
     if (hipError_t e = hipPeekAtLastError()) return e;
     const int64_t nblk = (R + kRowBlock - 1) / kRowBlock;
-    if (K % 8 == 0 && L % 8 == 0 && (uintptr_t)w % 16 == 0 && dtype != AWQ_DTYPE_F32) {
-        const dim3 gw((unsigned)((K + kColTileW - 1) / kColTileW), (unsigned)nblk);
-        if (dtype == AWQ_DTYPE_BF16)
-            hipLaunchKernelGGL((colsum_wide_kernel<AWQ_DTYPE_BF16, 1>), gw, dim3(256), 0, stream, w, R, K, L, gmax, part,
-                               nullptr);
-        else
-            hipLaunchKernelGGL((colsum_wide_kernel<AWQ_DTYPE_F16, 1>), gw, dim3(256), 0, stream, w, R, K, L, gmax, part,
-                               nullptr);
-    } else if (K % 8 == 0 && L % 8 == 0 && (uintptr_t)w % 16 == 0) {
+    if (K % 8 == 0 && L % 8 == 0 && (uintptr_t)w % 16 == 0) {
         const dim3 gt((unsigned)((K + kColTile - 1) / kColTile), (unsigned)nblk);
         AWQ_DT_SWITCH(dtype, hipLaunchKernelGGL((colsum_tile_kernel<D, 1>), gt, dim3(256), 0, stream, w, R, K, L,
                                                 gmax, part, nullptr))

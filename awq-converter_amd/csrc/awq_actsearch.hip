@@ -582,7 +582,7 @@ __global__ __launch_bounds__(256) void act_loss_kernel(const void* __restrict__ 
 // work[i * nblk + b] = sum of part[i][b*1024 .. +1024) ascending, fp64.  A workgroup takes
 // kLossChains consecutive (i, b) chains: their floats come in through LDS with coalesced
 // loads (all in flight at once), then one lane per chain runs its fp64 chain from LDS.
-constexpr int kLossChains = 16;
+constexpr int kLossChains = 16;   // r92: 8 or 4 chains per workgroup were 5-30 % slower
 __global__ __launch_bounds__(256) void loss_block_kernel(const float* __restrict__ part, int n_grid, int64_t stride,
                                                          int64_t nblk, double* __restrict__ work) {
     __shared__ __attribute__((aligned(16))) float sp[kLossChains][kGroupBlock];

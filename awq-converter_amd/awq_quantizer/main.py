@@ -376,6 +376,14 @@ def _batches(infos: List[TensorInfo], budget: int) -> List[List[TensorInfo]]:
     return out
 
 
+def _batch_budget(total: int, batch_bytes: int) -> int:
+    """Input bytes per batch: small enough that a small model still pipelines (read / H2D /
+    kernel / D2H of neighbouring batches overlap) — about 8 batches per device, 32 MiB ..
+    batch_bytes each; AWQ_CLI_BATCH_MB overrides."""
+    forced = int(os.environ.get("AWQ_CLI_BATCH_MB", "0")) << 20
+    return forced or max(32 << 20, min(batch_bytes, total // 8))
+
+
 def _pinned_copy(t: torch.Tensor) -> torch.Tensor:
     """Host copy in page-locked memory (torch's caching host allocator), so the H2D / D2H
     copies run asynchronously on the copy stream."""
@@ -414,10 +422,7 @@ def quantize_stream(loader, infos: List[TensorInfo], quantizer: AWQQuantizer, de
     torch.cuda.set_device(dev)
     copy_stream = torch.cuda.Stream(dev)
     compute = torch.cuda.current_stream(dev)
-    # batches small enough that a small model still pipelines (read / H2D / kernel / D2H of
-    # neighbouring batches overlap): about 8 batches per device, 32 MiB .. batch_bytes each
-    total = sum(i.nbytes for i in infos)
-    budget = int(os.environ.get("AWQ_CLI_BATCH_MB", "0")) << 20 or max(32 << 20, min(batch_bytes, total // 8))
+    budget = _batch_budget(sum(i.nbytes for i in infos), batch_bytes)
     batches = _batches(infos, budget)
     depth = max(1, lookahead // max(1, max(len(b) for b in batches) if batches else 1))
     clock = time.perf_counter

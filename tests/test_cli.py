@@ -69,6 +69,23 @@ def test_select_order_and_partition(tmp_path):
     assert max(loads) - min(loads) <= max(sizes)          # greedy LPT balance bound
 
 
+def test_batch_budget_and_batches(monkeypatch):
+    """About 8 pipeline batches per model (32 MiB floor, batch_bytes cap); processing order
+    kept; a tensor larger than the budget is a batch of its own."""
+    from awq_quantizer.main import _batch_budget, _batches
+    from awq_quantizer.model_loading.safetensors_loader import TensorInfo
+    monkeypatch.delenv("AWQ_CLI_BATCH_MB", raising=False)
+    MiB = 1 << 20
+    assert _batch_budget(662 * MiB, 1 << 30) == 662 * MiB // 8        # opt-350m: ~83 MB batches
+    assert _batch_budget(100 * MiB, 1 << 30) == 32 * MiB               # floor
+    assert _batch_budget(16 << 30, 1 << 30) == 1 << 30                 # Llama-3-8B: the cap
+    monkeypatch.setenv("AWQ_CLI_BATCH_MB", "5")
+    assert _batch_budget(16 << 30, 1 << 30) == 5 * MiB
+    infos = [TensorInfo(f"t{i}", "f", torch.bfloat16, (n,)) for i, n in enumerate([10, 20, 100, 5, 5, 30])]
+    bs = _batches(infos, 60)                                           # bytes: 20 40 200 10 10 60
+    assert [[i.name for i in b] for b in bs] == [["t0", "t1"], ["t2"], ["t3", "t4"], ["t5"]]
+
+
 def test_save_layout(tmp_path):
     from awq_quantizer.main import save_model_in_chunks
     res = {f"t{i}": {"tensor_q": torch.zeros(4, 8, dtype=torch.int32), "scales": torch.ones(4, 1, dtype=torch.float16),

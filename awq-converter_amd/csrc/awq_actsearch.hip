@@ -449,7 +449,11 @@ __global__ __launch_bounds__(kTableThreads) void scale_table_kernel(const float*
         __syncthreads();
     }
     const double norm = snan[0] ? __builtin_nan("") : sqrt(smx[0] * smn[0]);
-    for (int64_t k = tid; k < K; k += kTableThreads) {
+    // this workgroup's slice of the row (blockIdx.y of gridDim.y: every slice's workgroup
+    // finds the same max / min, so the row's normaliser is the same in all of them)
+    const int64_t per = (K + gridDim.y - 1) / gridDim.y;
+    const int64_t k0 = (int64_t)blockIdx.y * per, k1 = (k0 + per < K) ? k0 + per : K;
+    for (int64_t k = k0 + tid; k < k1; k += kTableThreads) {
         double s = raw_scale(x_mean, w_mean, k, r) / norm;
         if (s != s || __builtin_isinf(s)) s = 1.0;
         table[(int64_t)i * K + k] = (float)s;
@@ -797,8 +801,12 @@ hipError_t launch_colmean(const double* part, int64_t nblk, int64_t K, double di
 
 hipError_t launch_scale_table(const float* x_mean, const float* w_mean, int64_t K, int n_grid, float* table,
                               hipStream_t stream) {
-    hipLaunchKernelGGL(scale_table_kernel, dim3((unsigned)n_grid), dim3(kTableThreads), 0, stream, x_mean, w_mean, K,
-                       n_grid, table);
+    // the normalising max / min pass is repeated by each slice's workgroup (no cross-workgroup
+    // exchange); the second pow pass is split over the slices
+    const unsigned slices = (unsigned)((K + 2 * kTableThreads - 1) / (2 * kTableThreads) < 8
+                                           ? (K + 2 * kTableThreads - 1) / (2 * kTableThreads) : 8);
+    hipLaunchKernelGGL(scale_table_kernel, dim3((unsigned)n_grid, slices), dim3(kTableThreads), 0, stream, x_mean,
+                       w_mean, K, n_grid, table);
     return hipPeekAtLastError();
 }
 

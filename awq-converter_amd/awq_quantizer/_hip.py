@@ -43,6 +43,7 @@ SIGNATURES = {
     "awq_ragged_eligible": (_I32, [_I32, _I64, _I64, _I64]),
     "awq_plan_ragged": (_I64, [ctypes.POINTER(TensorDesc), _I32, _I32, _I64]),
     "awq_stream_copy": (_I32, [_P, _P, _I64, _P]),
+    "awq_stream_ceiling": (_I32, [_P, _P, _I64, _P]),
     "awq_export_autoawq_gemm": (_I32, [_P, _P, _P, _I64, _I64, _I64, _I32, _P, _P, _P, _P]),
     "awq_plan_block_tensor": (_I64, [ctypes.POINTER(TensorDesc), _I32, _I64, _P, _I64]),
     "awq_ragged_flags": (_I32, [ctypes.POINTER(TensorDesc), _I32, _I64]),
@@ -201,6 +202,15 @@ def quantize_ragged(descs_dev: torch.Tensor, n: int, total_tiles: int, bits: int
 def stream_copy(src: torch.Tensor, dst: torch.Tensor, stream: int) -> None:
     rc = load_library().awq_stream_copy(ptr(src), ptr(dst), src.numel() * src.element_size(), ctypes.c_void_p(stream))
     check(rc, "awq_stream_copy")
+
+
+def stream_ceiling(src: torch.Tensor, dst: torch.Tensor, stream: int) -> None:
+    """Read `src` whole, write len(src) / 4 bytes of dst (bench.py's read-dominant ceiling)."""
+    n = src.numel() * src.element_size()
+    if dst.numel() * dst.element_size() < n // 4:
+        raise ValueError("stream_ceiling: dst must hold a quarter of src's bytes")
+    rc = load_library().awq_stream_ceiling(ptr(src), ptr(dst), n, ctypes.c_void_p(stream))
+    check(rc, "awq_stream_ceiling")
 
 
 def export_autoawq_gemm(qweight, qzeros, scales, N: int, K: int, L: int, bits: int, qweight_t, qzeros_t,

@@ -272,6 +272,14 @@ int awq_stream_copy(const void* src, void* dst, int64_t bytes, void* stream) {
     return hip_status(awq::launch_stream_copy(src, dst, bytes, (hipStream_t)stream), "awq stream copy");
 }
 
+int awq_stream_ceiling(const void* src, void* dst, int64_t bytes, void* stream) {
+    g_err.clear();
+    if (bytes < 0 || bytes % 4096 != 0) return fail(AWQ_EINVAL, "bytes must be a non-negative multiple of 4096");
+    if (bytes > 0 && (!src || !dst || !aligned(src, 16) || !aligned(dst, 16)))
+        return fail(AWQ_EINVAL, "null or misaligned buffer");
+    return hip_status(awq::launch_stream_ceiling(src, dst, bytes, (hipStream_t)stream), "awq stream ceiling");
+}
+
 // ---- activation-aware scale search (include/awq_hip.h awq_act_*) ----
 namespace {
 int check_act_shape(int dtype, int64_t rows, int64_t K, int64_t group_size) {

@@ -1108,6 +1108,35 @@ hipError_t launch_stream_copy(const void* src, void* dst, int64_t bytes, hipStre
     return hipPeekAtLastError();
 }
 
+// Measurement helper (bench.py's read-dominant ceiling): the quantizer's memory structure
+// and read:write ratio without its arithmetic — one wave per 4 KiB of input (4 x 16-B nt
+// loads per lane), the four vectors xor-folded to one, ONE 16-B nt store per lane (1 KiB
+// per wave).  Read 4 : write 1, against the packed quantizer's 4096 : 1064 per tile.
+__global__ __launch_bounds__(64 * kWavesPerBlock) void awq_stream_ceiling_kernel(const uint8_t* __restrict__ src,
+                                                                                uint8_t* __restrict__ dst,
+                                                                                int64_t bytes) {
+    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    const int64_t tile = (int64_t)blockIdx.x * kWavesPerBlock + wid;
+    const int64_t base = tile * 4096;
+    if (base >= bytes) return;
+    const uint32_t n = (uint32_t)min((int64_t)4096, bytes - base);
+    const __amdgpu_buffer_rsrc_t rs = rsrc(src + base, n), rd = rsrc(dst + tile * 1024, n / 4);
+    u4 v[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, (uint32_t)(j * 1024 + lane * 16), 0, 2);
+    const u4 x = v[0] ^ v[1] ^ v[2] ^ v[3];
+    __builtin_amdgcn_raw_buffer_store_b128(x, rd, (uint32_t)(lane * 16), 0, 2);
+}
+
+hipError_t launch_stream_ceiling(const void* src, void* dst, int64_t bytes, hipStream_t stream) {
+    if (bytes <= 0) return hipSuccess;
+    const int64_t per_block = 4096LL * kWavesPerBlock;
+    hipLaunchKernelGGL(awq_stream_ceiling_kernel, dim3((unsigned)((bytes + per_block - 1) / per_block)),
+                       dim3(64 * kWavesPerBlock), 0, stream, (const uint8_t*)src, (uint8_t*)dst, bytes);
+    return hipPeekAtLastError();
+}
+
 hipError_t launch_selftest(int which, unsigned long long* out, hipStream_t stream) {
     if (which != 0) return hipErrorInvalidValue;
     hipLaunchKernelGGL(awq_selftest_recip_kernel, dim3(0x8000 / 256), dim3(256), 0, stream, out);

@@ -4,21 +4,30 @@
 Metric (BASELINE.json): bf16 GB quantized/sec at group_size=128 (input bytes, 2 B/elem),
 plus the HBM-roofline fraction of the quantize+pack kernel.
 
-A *step* = one ragged launch of the streaming kernel over a whole synthetic tensor set
-with the exact shapes of the named model, bits=4, group_size=128,
-asymmetric (the CLI default, reference main.py:59-63), outputs = packed qweight/qzeros +
-fp16 scales, inputs resident in HBM.  Multi-GPU: one process per GPU (torchrun); every
-rank quantizes its own replica of the tensor set (weak scaling, no data-path collective:
-tensors are independent).  value = all ranks' input bytes / max-over-ranks time.
---shard: strong scaling instead — one copy of the set, its tensor list LPT-sharded over the
-ranks (the CLI's torchrun mode), value = the set's bytes / max-over-ranks time.
+Default workload = the north_star set: the Llama-3-70B tensor list (723 tensors, 70.55 G
+elements, 141 GB bf16), which fits one MI355X (141 GB in + 37 GB
+packed out of 288 GB).  A *step* = one ragged launch of the streaming kernel over the
+rank's tensors, bits=4, group_size=128, asymmetric (the CLI default, reference
+main.py:59-63), outputs = packed qweight/qzeros + fp16 scales, inputs resident in HBM.
 
-Usage: python bench.py [--gpus N --steps K --warmup W --workload opt-125m]
+Multi-GPU (default): one process per GPU (torchrun), ONE copy of the tensor set, its
+tensor list LPT-sharded over the ranks exactly as the CLI's torchrun mode does (the
+reference's own partition_tensors, main.py:395-427) -> "scaling": "strong", value = the
+set's bytes / max-over-ranks time.  The exchange (gather of the packed shards to rank 0,
+RCCL point-to-point over xGMI) runs after the timed region and is reported as "exchange".
+--replica: weak scaling instead (every rank quantizes its own copy of the set).
+
+Clocks: the chip's clocks settle only after ~20-30 ms of back-to-back HBM streaming
+(profiles/r60_sustain_probe.log), so the read-dominant ceiling probe (>= 150 ms of
+streaming) runs on every rank BEFORE the warmup launches, whatever --warmup is.
+
+Usage: python bench.py [--gpus N --steps K --warmup W --workload llama3-70b]
        N>1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 """
 import argparse
 import json
 import os
+import subprocess
 import sys
 import time
 
@@ -30,7 +39,7 @@ for _p in (ROOT, os.path.join(ROOT, "awq-converter_amd")):
 import torch  # noqa: E402
 
 METRIC = "bf16 GB quantized/sec at group_size=128, 1/2/4/8 MI355X; % HBM roofline"
-HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec peak (MI355X_MICROARCH.md); 6.29 TB/s measured copy
+HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 
 # Shape manifests (every float tensor with numel >= 128 = the
 # reference CLI's filter, main.py:244-253).
@@ -49,6 +58,8 @@ DESCR = {"c1": "single 1024x4096 linear", "opt-125m": "facebook/opt-125m tensor 
          "opt-350m": "facebook/opt-350m tensor set (388 tensors, 331.2M params)",
          "llama3-8b": "Llama-3-8B tensor set (291 tensors, 8.03B params)",
          "llama3-70b": "Llama-3-70B tensor set (723 tensors, 70.55B params)"}
+# reference awq.py itself, measured in the survey container
+REFERENCE_CPU = "reference awq.py itself: 4.61 MB/s on 1 process (8 torch threads), 23.6 MB/s with 8 processes (BASELINE.md)"
 
 
 def shapes_of(workload):
@@ -59,17 +70,13 @@ def shapes_of(workload):
     return sorted(out, key=lambda s: -int(torch.Size(s).numel()))
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    # Defaults measure the sustained rate: the chip's clocks settle only after ~20-30 ms of
-    # back-to-back launches (scripts/sustain_probe.py, profiles/r60: opt-125m launches run
-    # 54-66 us during the first ~300, then a steady 53.9 us), so 500 warmup launches
-    # (~28 ms) precede 1000 timed ones (~54 ms; the ~35 us launch / sync edge of the timed
-    # region is then < 0.1 %).
-    ap.add_argument("--steps", type=int, default=1000)
-    ap.add_argument("--warmup", type=int, default=500)
-    ap.add_argument("--workload", default="opt-125m", choices=sorted(WORKLOADS))
+    # Llama-3-70B: one launch is ~30 ms, so 20 timed launches are ~0.6 s of kernel time
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--workload", default="llama3-70b", choices=sorted(WORKLOADS))
     ap.add_argument("--bits", type=int, default=4, choices=[4, 8])
     ap.add_argument("--symmetric", action="store_true")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "f16", "f32"],
@@ -77,19 +84,26 @@ def parse():
     ap.add_argument("--group-size", type=int, default=128, choices=[32, 64, 128, 256],
                     help="128 = the BASELINE metric; other sizes are extra lines (metric names the size)")
     ap.add_argument("--parity", action="store_true", help="also write unpacked int32 tensor_q/zero_points")
-    ap.add_argument("--shard", action="store_true",
-                    help="strong scaling: ONE copy of the tensor set, its tensor list LPT-sharded across the "
-                         "ranks (distributed.shard, the CLI's torchrun mode; SURVEY 8e) instead of a replica "
-                         "per rank")
+    ap.add_argument("--replica", action="store_true",
+                    help="weak scaling: every rank quantizes its own replica of the tensor set, instead of the "
+                         "default ONE copy LPT-sharded across the ranks (distributed.shard, the CLI's torchrun "
+                         "mode; SURVEY 8e)")
+    ap.add_argument("--shard", action="store_true", help="(the default; kept for old command lines)")
     ap.add_argument("--replicas", type=int, default=0,
-                    help="input replicas rotated across steps (0 = enough to exceed the 256 MiB Infinity Cache)")
+                    help="input copies rotated across steps (0 = enough to exceed the 256 MiB Infinity Cache)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-seconds", type=float, default=15.0)
     ap.add_argument("--events", default="span", choices=["step", "span"])
-    ap.add_argument("--no-copy-ceiling", action="store_true")
+    ap.add_argument("--no-copy-ceiling", action="store_true",
+                    help="skip the read-dominant ceiling probe (it also warms the clocks before the warmup)")
+    ap.add_argument("--clock-warm-ms", type=float, default=150.0,
+                    help="ms of ceiling-probe streaming before the warmup launches (clock ramp)")
     ap.add_argument("--no-gather", action="store_true", help="N>1: skip the (untimed) gather-to-rank-0 leg")
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
-    return ap.parse_args()
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "round2", "pmc_traffic.json"))
+    a = ap.parse_args(argv)
+    if a.replica and a.shard:
+        ap.error("--replica and --shard are exclusive")
+    return a
 
 
 DTYPES = {"bf16": torch.bfloat16, "f16": torch.float16, "f32": torch.float32}
@@ -97,77 +111,109 @@ DTYPES = {"bf16": torch.bfloat16, "f16": torch.float16, "f32": torch.float32}
 
 def make_set(shapes, seed0, dev, dtype=torch.bfloat16, only=None):
     """Synthetic N(0, 0.02) tensors, tensor i seeded by seed0 + i; `only`: the indices to
-    materialise (a rank's shard)."""
+    materialise (a rank's shard).  Generated in row blocks so the fp32 temporary stays
+    small next to a 141 GB set."""
     g = torch.Generator(device=dev)
     tensors = {}
     for i, s in enumerate(shapes):
         if only is not None and i not in only:
             continue
         g.manual_seed(seed0 + i)
-        tensors[f"t{i:04d}"] = (torch.randn(*s, generator=g, device=dev, dtype=torch.float32) * 0.02).to(dtype)
+        t = torch.empty(*s, device=dev, dtype=dtype)
+        flat = t.view(s[0], -1) if len(s) > 1 else t.view(1, -1)
+        step = max(1, (1 << 28) // flat.shape[1])
+        for r0 in range(0, flat.shape[0], step):
+            blk = flat[r0:r0 + step]
+            blk.copy_(torch.randn(blk.shape, generator=g, device=dev, dtype=torch.float32).mul_(0.02))
+        tensors[f"t{i:04d}"] = t
     return tensors
 
 
-def copy_ceiling(dev, stream, nbytes=1 << 30, iters=10):
-    """HBM copy of `nbytes` (read + write counted) by the library's stream-copy kernel, which
-    has the quantizer's memory structure (one wave per 4 KiB, 16-B nt accesses): the
-    achievable-bandwidth reference SURVEY.md §8(d) asks the kernel to be quoted against."""
+def stream_ceiling(dev, stream, warm_ms, nbytes=1 << 30, iters=20):
+    """Read-dominant ceiling: the library's awq_stream_ceiling kernel (the quantizer's memory
+    structure — one wave per 4 KiB, 16-B nt loads — and its read:write ratio, 4 : 1 against
+    the packed quantizer's 4096 : 1064, without the arithmetic), read + write counted.  Runs
+    first, for >= warm_ms of back-to-back streaming, so the timed region starts on settled
+    clocks."""
     from awq_quantizer import _hip
     src = torch.empty(nbytes // 4, dtype=torch.int32, device=dev).fill_(1)
-    dst = torch.empty_like(src)
-    for _ in range(3):
-        _hip.stream_copy(src, dst, stream.cuda_stream)
+    dst = torch.empty(nbytes // 16, dtype=torch.int32, device=dev)
+    t0 = time.perf_counter()
+    while True:
+        for _ in range(8):
+            _hip.stream_ceiling(src, dst, stream.cuda_stream)
+        torch.cuda.synchronize(dev)
+        if (time.perf_counter() - t0) * 1e3 >= warm_ms:
+            break
     a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     a.record(stream)
     for _ in range(iters):
-        _hip.stream_copy(src, dst, stream.cuda_stream)
+        _hip.stream_ceiling(src, dst, stream.cuda_stream)
     b.record(stream)
-    torch.cuda.synchronize()
-    gbs = 2 * nbytes * iters / (a.elapsed_time(b) / 1e3) / 1e9
+    torch.cuda.synchronize(dev)
+    gbs = 1.25 * nbytes * iters / (a.elapsed_time(b) / 1e3) / 1e9
     del src, dst
     return gbs
 
 
-def cpu_threads():
-    """Host threads for the CPU baseline: OMP_NUM_THREADS if set (16 on the GPU box),
-    else the CPUs this process may run on."""
+def host_cpus():
+    """(threads used, node CPUs, CPUs in this process's affinity set).  On the GPU box
+    os.cpu_count() and the affinity set show the whole machine, while the box's CPU share
+    is OMP_NUM_THREADS (16, set by the harness): the baseline uses that share."""
+    node = os.cpu_count() or 1
+    aff = len(os.sched_getaffinity(0))
     env = os.environ.get("OMP_NUM_THREADS", "")
-    if env.isdigit() and int(env) > 0:
-        return int(env)
-    return len(os.sched_getaffinity(0))
+    used = int(env) if env.isdigit() and int(env) > 0 else aff
+    return min(used, aff), node, aff
 
 
-def cpu_baseline(shapes, budget_s, group_size=128, dtype=torch.bfloat16):
-    """The oracle (oracle/awq_oracle.c, OpenMP over rows) on a bounded sample of the SAME
-    workload: the tensor set in processing order, pass after pass, until about budget_s of
-    CPU work (the last tensor may be cut to a row block).  Returns (GB/s of input,
-    seconds, bytes, tensors, threads)."""
+def _time_oracle(x, rows, K, group_size, bits=4):
     from oracle import awq_oracle as orc
-    threads = orc.set_threads(cpu_threads())
+    t0 = time.perf_counter()
+    orc.quantize_groups(x, rows, K, group_size, bits, False)
+    return time.perf_counter() - t0
+
+
+def cpu_baseline(workload, budget_s, group_size=128, dtype=torch.bfloat16):
+    """The oracle (oracle/awq_oracle.c, OpenMP over rows, bit-exact restatement of awq.py)
+    on the host cores, SURVEY §8(d): C1 (1024x4096, sigma 1) in full, then a row sample of
+    every distinct shape of the workload, each extrapolated to the shape's full row count
+    and multiplicity; value = the workload's input bytes / the extrapolated time."""
+    from oracle import awq_oracle as orc
+    threads, node, aff = host_cpus()
+    orc.set_threads(threads)
     g = torch.Generator().manual_seed(1234)
-    done_bytes, t_total, parts = 0, 0.0, 0
-    cache = {}
-    while t_total < budget_s - 0.2:
-        for s in shapes:
-            rows = 1 if len(s) == 1 else s[0]
-            K = int(torch.Size(s).numel()) // rows
-            remaining = budget_s - t_total
-            if remaining <= 0.2:
-                break
-            take = rows
-            est = 3e-8 * rows * K / threads
-            if est > remaining:
-                take = max(1, int(rows * remaining / est))
-            key = (take, K)
-            if key not in cache:
-                cache[key] = (torch.randn(take, K, generator=g) * 0.02).to(dtype)
-            x = cache[key]
-            t0 = time.perf_counter()
-            orc.quantize_groups(x, take, K, group_size, 4, False)
-            t_total += time.perf_counter() - t0
-            done_bytes += x.numel() * x.element_size()
-            parts += 1
-    return done_bytes / t_total / 1e9, t_total, done_bytes, parts, threads
+    esize = torch.empty((), dtype=dtype).element_size()
+    c1 = (torch.randn(1024, 4096, generator=torch.Generator().manual_seed(0))).to(dtype)
+    _time_oracle(c1, 1024, 4096, group_size)                             # warm (page-in, OpenMP pool)
+    c1_s = min(_time_oracle(c1, 1024, 4096, group_size) for _ in range(3))
+    per_shape = budget_s / len(WORKLOADS[workload])
+    rate0 = 1024 * 4096 * esize / c1_s                                   # bytes/s, for sizing the samples
+    total_s, sampled, lines = 0.0, 0, []
+    for shape, count in WORKLOADS[workload]:
+        rows = 1 if len(shape) == 1 else shape[0]
+        K = int(torch.Size(shape).numel()) // rows
+        # a sample of <= 128 MB (or the whole tensor), timed repeatedly for ~half the shape's share
+        take = max(1, min(rows, int(per_shape * 0.5 * rate0 / (K * esize)), (128 << 20) // (K * esize)))
+        x = (torch.randn(take, K, generator=g) * 0.02).to(dtype)
+        t, reps = 0.0, 0
+        while reps < 2 or (t < per_shape * 0.5 and reps < 1000):
+            t += _time_oracle(x, take, K, group_size)
+            reps += 1
+        t_full = t / reps * rows / take
+        total_s += t_full * count
+        sampled += take * K * esize * reps
+        lines.append(f"{shape}x{count}: {take}/{rows} rows")
+    wl_bytes = sum(int(torch.Size(s).numel()) * c for s, c in WORKLOADS[workload]) * esize
+    return {"value": round(wl_bytes / total_s / 1e9, 5), "unit": "GB/s", "cores": threads, "kind": "port",
+            "node_cpus": node, "affinity_cpus": aff,
+            "c1_full": {"seconds": round(c1_s, 4), "GBs": round(1024 * 4096 * esize / c1_s / 1e9, 4)},
+            "extrapolated_seconds": round(total_s, 2), "shapes_sampled": len(lines),
+            "sample": (f"oracle/awq_oracle.c (bit-exact restatement of awq.py, OpenMP over rows, {threads} "
+                       f"threads = the box's CPU share OMP_NUM_THREADS; node shows {node} CPUs) - C1 in full, "
+                       f"then row samples of every {workload} shape ({'; '.join(lines)}; "
+                       f"{sampled / 1e9:.2f} GB sampled), EXTRAPOLATED by row count and multiplicity to the whole "
+                       f"set; {REFERENCE_CPU}")}
 
 
 def packed_out_shapes(shape, bits, gs):
@@ -179,10 +225,10 @@ def packed_out_shapes(shape, bits, gs):
             "scales": ((rows, G), torch.float16)}
 
 
-def gather_leg(batch, rank, world, dev, backend, iters=3, shard_owner=None, all_shapes=None, bits=4, gs=128):
+def gather_leg(batch, rank, world, dev, backend, iters=2, shard_owner=None, all_shapes=None, bits=4, gs=128):
     """N>1 only, after the timed region: the CLI's exchange step (distributed.gather_to_rank0,
-    one coalesced message per peer) on every rank's packed outputs of one replica (or, with
-    --shard, of its shard: the real exchange of the CLI's torchrun mode).  Reported beside
+    one coalesced message per peer) on every rank's packed outputs of its shard (the real
+    exchange of the CLI's torchrun mode; with --replica, of its replica).  Reported beside
     `value`, never inside it (the gather is a separate line)."""
     from awq_quantizer import distributed as D
     comm = dev if backend == "nccl" else torch.device("cpu")
@@ -200,12 +246,14 @@ def gather_leg(batch, rank, world, dev, backend, iters=3, shard_owner=None, all_
             shapes[f"t{i:04d}"] = packed_out_shapes(all_shapes[i], bits, gs)
         local = {n: {f: batch.out[n][f].to(comm) for f in fields} for n in batch.names}
     per_rank = sum(batch.out[n][f].numel() * batch.out[n][f].element_size() for n in batch.names for f in fields)
-    D.gather_to_rank0(local, owner, shapes, comm)                     # warmup (connects the P2P channels)
+    got = D.gather_to_rank0(local, owner, shapes, comm)               # warmup (connects the P2P channels)
+    del got
     torch.cuda.synchronize(dev)
     D.barrier()
     t0 = time.perf_counter()
     for _ in range(iters):
-        D.gather_to_rank0(local, owner, shapes, comm)
+        got = D.gather_to_rank0(local, owner, shapes, comm)
+        del got
     torch.cuda.synchronize(dev)
     D.barrier()
     t = D.max_over_ranks((time.perf_counter() - t0) / iters, dev)
@@ -218,6 +266,32 @@ def gather_leg(batch, rank, world, dev, backend, iters=3, shard_owner=None, all_
             "gather of every rank's packed outputs (one replica) to rank 0")
     return {"what": what + f", one P2P message per peer ({backend}); outside the timed region",
             "bytes_to_rank0": moved, "ms": round(t * 1e3, 3), "GBs_into_rank0": round(moved / t / 1e9, 2)}
+
+
+def git_head():
+    try:
+        return subprocess.run(["git", "-C", ROOT, "rev-parse", "--short=12", "HEAD"], capture_output=True,
+                              text=True, timeout=5).stdout.strip() or None
+    except (OSError, subprocess.SubprocessError):
+        return None
+
+
+def recorded_traffic(path, key):
+    """HBM traffic per launch recorded by a separate rocprofv3 --pmc run of this same
+    command (scripts/profile_round.sh -> scripts/pmc_traffic.py; FETCH_SIZE x2 gfx950
+    correction).  Counters cannot be read in-process, so the field is a RECORDED figure,
+    labelled with its file, the commit it was measured on and the date."""
+    try:
+        with open(path) as f:
+            rec = json.load(f).get(key)
+    except (OSError, ValueError):
+        return None, None
+    if not rec:
+        return None, None
+    src = {"file": os.path.relpath(path, ROOT), "key": key, "commit": rec.get("commit"), "date": rec.get("date"),
+           "traffic_over_algorithmic": rec.get("traffic_over_algorithmic"),
+           "note": "recorded by a separate rocprofv3 --pmc pass (FETCH_SIZE x2 + WRITE_SIZE), not this run"}
+    return rec.get("hbm_bytes_per_launch"), src
 
 
 def main():
@@ -233,36 +307,41 @@ def main():
     torch.cuda.set_device(dev)
     _hip.require_device(dev)
 
+    shard = not args.replica
     all_shapes = shapes_of(args.workload)
     dtype = DTYPES[args.dtype]
     esize = torch.empty((), dtype=dtype).element_size()
-    if args.shard:
+    if shard:
         # strong scaling: rank r quantizes the tensors LPT assigns it (tensor i is seeded by
         # its index, so the data do not depend on the world size)
         owner = D.shard([int(torch.Size(s).numel()) for s in all_shapes], world)
         mine = [i for i in range(len(all_shapes)) if owner[i] == rank]
     else:
+        owner = None
         mine = list(range(len(all_shapes)))
     shapes = [all_shapes[i] for i in mine]
     elems = sum(int(torch.Size(s).numel()) for s in shapes)
     total_elems = sum(int(torch.Size(s).numel()) for s in all_shapes)
     in_bytes = elems * esize
     # bytes all ranks quantize per step: the whole set once (shard) or one replica per rank
-    step_bytes = total_elems * esize if args.shard else in_bytes * world
+    step_bytes = total_elems * esize if shard else in_bytes * world
     reps = args.replicas or max(1, -(-(1 << 30) // max(1, in_bytes)))   # >= 1 GiB of inputs in rotation
     batches = []
     for r in range(reps):
-        if args.shard:
+        if shard:
             inputs = make_set(all_shapes, r * 100003, dev, dtype, only=set(mine))
         else:
             inputs = make_set(shapes, (rank * 64 + r) * 100003, dev, dtype)
         batches.append(PackedBatch(inputs, bits=args.bits, symmetric=args.symmetric, parity=args.parity,
                                    group_size=args.group_size))
+        del inputs
     torch.cuda.synchronize()
     algo_bytes = batches[0].algorithmic_bytes()
 
     barrier = D.barrier
     stream = torch.cuda.current_stream(dev)
+    # clock warm-up on every rank (and the ceiling figure) before the warmup launches
+    ceiling = None if args.no_copy_ceiling else stream_ceiling(dev, stream, args.clock_warm_ms)
     for i in range(args.warmup):
         batches[i % reps].run(stream)
     torch.cuda.synchronize()
@@ -291,10 +370,12 @@ def main():
     elapsed = time.perf_counter() - t0
     kern_ms = [a.elapsed_time(b) for a, b in ev]
     kern_avg_s = sum(kern_ms) / args.steps / 1e3
-    ceiling = None if args.no_copy_ceiling or rank != 0 else copy_ceiling(dev, stream)
 
     elapsed = D.max_over_ranks(elapsed, dev)
-    gather = (gather_leg(batches[0], rank, world, dev, backend, shard_owner=owner if args.shard else None,
+    kern_max_s = D.max_over_ranks(kern_avg_s, dev)
+    del batches[1:]
+    torch.cuda.empty_cache()
+    gather = (gather_leg(batches[0], rank, world, dev, backend, shard_owner=owner,
                          all_shapes=all_shapes, bits=args.bits, gs=args.group_size)
               if world > 1 and not args.no_gather else None)
 
@@ -306,47 +387,43 @@ def main():
 
     value = step_bytes * args.steps / elapsed / 1e9
     achieved = algo_bytes / kern_avg_s / 1e9
-    traffic = None
-    try:
-        with open(args.traffic_json) as f:
-            tj = json.load(f)
-        key = f"{args.workload}.b{args.bits}.{'sym' if args.symmetric else 'asym'}.{'parity' if args.parity else 'packed'}"
-        if args.group_size != 128:
-            key += f".gs{args.group_size}"
-        if args.dtype != "bf16":
-            key += f".{args.dtype}"
-        traffic = tj.get(key, {}).get("hbm_bytes_per_launch")
-    except (OSError, ValueError):
-        pass
+    key = f"{args.workload}.b{args.bits}.{'sym' if args.symmetric else 'asym'}.{'parity' if args.parity else 'packed'}"
+    if args.group_size != 128:
+        key += f".gs{args.group_size}"
+    if args.dtype != "bf16":
+        key += f".{args.dtype}"
+    if world > 1:
+        key += f".{'shard' if shard else 'replica'}{world}"
+    traffic, traffic_src = recorded_traffic(args.traffic_json, key)
     line = {
         "metric": METRIC.replace("group_size=128", f"group_size={args.group_size}").replace("bf16", args.dtype),
         "value": round(value, 3), "unit": "GB/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
-        "scaling": "strong" if args.shard else "weak", "vs_baseline": None, "dtype": args.dtype, "data": "synthetic",
+        "scaling": "strong" if shard else "weak", "vs_baseline": None, "dtype": args.dtype, "data": "synthetic",
         "config": {"workload": f"{args.workload}: {DESCR[args.workload]}", "tensors": len(all_shapes),
                    "elements": total_elems, "group_size": args.group_size, "bits": args.bits, "symmetric": args.symmetric,
                    "outputs": "qweight+qzeros+fp16 scales" + (" + int32 tensor_q/zero_points" if args.parity else ""),
                    "launches_per_step": 1, "input_replicas_rotated": reps,
-                   "parallelism": (f"shard{world} (tensor list LPT-sharded over the ranks; rank 0 holds "
-                                   f"{len(shapes)} tensors, {elems} elements)") if args.shard else
-                                  f"dp{world} (each rank quantizes its own replica of the tensor set)"},
+                   "parallelism": (f"shard{world} (ONE copy of the set, tensor list LPT-sharded over the ranks; "
+                                   f"rank 0 holds {len(shapes)} tensors, {elems} elements)") if shard else
+                                  f"replica{world} (each rank quantizes its own replica of the tensor set)"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                      "algorithmic_bytes_per_launch": algo_bytes,
-                     "kernel_avg_us": round(kern_avg_s * 1e6, 2), "timing": f"hip events ({args.events})"},
+                     "kernel_avg_us": round(kern_avg_s * 1e6, 2),
+                     "kernel_avg_us_max_over_ranks": round(kern_max_s * 1e6, 2),
+                     "timing": f"hip events ({args.events}) on the launch stream, rank 0's launches",
+                     "head": git_head()},
     }
+    if traffic_src:
+        line["roofline"]["traffic_source"] = traffic_src
     if gather:
         line["exchange"] = gather
     if ceiling:
-        line["roofline"]["copy_ceiling"] = round(ceiling, 1)
-        line["roofline"]["frac_of_copy"] = round(achieved / ceiling, 4)
-    if not args.no_cpu_baseline:
-        gbs, secs, nbytes, nparts, threads = cpu_baseline(shapes, args.cpu_sample_seconds, args.group_size, dtype)
-        line["cpu_baseline"] = {"value": round(gbs, 5), "unit": "GB/s", "cores": threads, "kind": "port",
-                                "sample": f"oracle/awq_oracle.c (OpenMP over rows, {threads} threads) on "
-                                          f"{nbytes / 1e6:.1f} MB of the {args.workload} set ({nparts} tensors/row-"
-                                          f"blocks in processing order, repeated passes, {secs:.1f} s); reference "
-                                          f"awq.py itself: 4.6 MB/s on 1 core, 23.6 MB/s on 8 (BASELINE.md)"}
+        line["roofline"]["read_dominant_ceiling"] = round(ceiling, 1)
+        line["roofline"]["frac_of_ceiling"] = round(achieved / ceiling, 4)
+    if not args.no_cpu_baseline and world == 1:
+        line["cpu_baseline"] = cpu_baseline(args.workload, args.cpu_sample_seconds, args.group_size, dtype)
     print(json.dumps(line), flush=True)
     if world > 1:
         import torch.distributed as dist

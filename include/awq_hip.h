@@ -151,6 +151,12 @@ int awq_export_autoawq_gemm(const int32_t* qweight, const int32_t* qzeros, const
  * quotes the kernel against this copy's rate. */
 int awq_stream_copy(const void* src, void* dst, int64_t bytes, void* stream);
 
+/* Measurement helper: the quantizer's read-dominant memory structure without its
+ * arithmetic — reads `bytes` (multiple of 4096, 16-B aligned) in 4 KiB waves and writes
+ * bytes / 4 to dst (one 16-B store per lane per 4 KiB).  bench.py quotes the kernel
+ * against this stream's (read + write) rate. */
+int awq_stream_ceiling(const void* src, void* dst, int64_t bytes, void* stream);
+
 /* Reference dequantize (awq.py:459-539): out fp32 [rows, K] =
  * fp16( fp16(tensor_q - zeros) * scales ) per element. */
 int awq_dequantize(const int32_t* tensor_q, const uint16_t* scales, const int32_t* zeros,

@@ -21,13 +21,12 @@ run() {  # run <name> <seconds> <cmd...>
   return $rc
 }
 run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || exit 1
-run pytest_gpu 1200 python -m pytest tests -m gpu -q --maxfail=30 -p no:cacheprovider
+run pytest_gpu 900 python -u -m pytest tests -m gpu -q -x --timeout 120 --timeout-method thread -p no:cacheprovider || exit 1
 run bench 600 python bench.py
 for WL in ${BENCH_EXTRA:-}; do
   run bench_$WL 900 python bench.py --workload $WL --steps 10 --warmup 3 --no-cpu-baseline
 done
 if [ "${PROFILE:-1}" = 1 ]; then
-  run rocprof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- \
-      python bench.py --no-cpu-baseline
+  COMMIT=${COMMIT:-unknown} bash scripts/profile_round.sh "$TAG/prof" || exit 1
 fi
 echo done

@@ -7,7 +7,7 @@ gfx950 corrections (MI355X_MICROARCH.md §HBM / cdna_hip_programming.md §7):
     (16 B/lane loads, which is what the kernel issues) -> doubled;
   * WRITE_SIZE is exact for 16-B/lane stores; the kernel's 4-B/lane qweight stores are
     uncalibrated (noted in the output).
-Usage: pmc_traffic.py --fetch dirA --write dirB --key opt-125m.b4.asym.packed [--out profiles/pmc_traffic.json]
+Usage: pmc_traffic.py --fetch dirA --write dirB --key llama3-70b.b4.asym.packed [--out profiles/round2/pmc_traffic.json]
 """
 import argparse
 import csv
@@ -39,8 +39,10 @@ def main():
     ap.add_argument("--write", required=True)
     ap.add_argument("--key", required=True)
     ap.add_argument("--algo-bytes", type=float, default=None)
+    ap.add_argument("--commit", default=None, help="commit the counters were measured on")
+    ap.add_argument("--date", default=None)
     ap.add_argument("--out", default=os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
-                                                  "profiles", "pmc_traffic.json"))
+                                                  "profiles", "round2", "pmc_traffic.json"))
     a = ap.parse_args()
     fetch = read_counter(a.fetch, "FETCH_SIZE")
     write = read_counter(a.write, "WRITE_SIZE")
@@ -52,6 +54,7 @@ def main():
     rec = {"hbm_bytes_per_launch": rd + wr, "read_bytes": rd, "write_bytes": wr,
            "fetch_size_kib_median": f_kib, "write_size_kib_median": w_kib, "dispatches": [len(fetch), len(write)],
            "correction": "FETCH_SIZE x2 (gfx950 half-count of 16B/lane streaming reads); WRITE_SIZE as reported"}
+    rec["commit"], rec["date"] = a.commit, a.date
     if a.algo_bytes:
         rec["algorithmic_bytes_per_launch"] = a.algo_bytes
         rec["traffic_over_algorithmic"] = (rd + wr) / a.algo_bytes

@@ -6,6 +6,7 @@ codes.  GPU test: end-to-end run on a small safetensors model, every result equa
 oracle."""
 import json
 import os
+import sys
 
 import pytest
 import torch
@@ -304,11 +305,11 @@ def test_bench_two_ranks_gpu():
     env = dict(os.environ, AWQ_DIST_BACKEND="gloo")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
            "--master-addr=127.0.0.1", f"--master-port={port}", os.path.join(root, "bench.py"), "--gpus", "2",
-           "--steps", "3", "--warmup", "1", "--workload", "c1", "--no-cpu-baseline", "--no-copy-ceiling"]
+           "--steps", "3", "--warmup", "1", "--workload", "c1", "--replica", "--no-cpu-baseline", "--no-copy-ceiling"]
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300, cwd=root)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
     line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
-    assert line["n_gpus"] == 2 and line["value"] > 0
+    assert line["n_gpus"] == 2 and line["value"] > 0 and line["scaling"] == "weak"
     # one peer's packed outputs of the 1024x4096 tensor: qweight 2 MiB + qzeros 16 KiB + scales 64 KiB
     assert line["exchange"]["bytes_to_rank0"] == 1024 * 512 * 4 + 1024 * 4 * 4 + 1024 * 32 * 2
     assert line["exchange"]["ms"] > 0
@@ -334,8 +335,8 @@ def test_bench_two_ranks_shard_gpu():
     env = dict(os.environ, AWQ_DIST_BACKEND="gloo")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
            "--master-addr=127.0.0.1", f"--master-port={port}", os.path.join(root, "bench.py"), "--gpus", "2",
-           "--steps", "3", "--warmup", "1", "--workload", "opt-125m", "--shard", "--replicas", "1",
-           "--no-cpu-baseline", "--no-copy-ceiling"]
+           "--steps", "3", "--warmup", "1", "--workload", "opt-125m", "--replicas", "1",
+           "--no-cpu-baseline", "--clock-warm-ms", "20"]
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300, cwd=root)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
     line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
@@ -349,6 +350,35 @@ def test_bench_two_ranks_shard_gpu():
             for (dims, dt) in bench.packed_out_shapes(sh, 4, 128).values():
                 want += int(torch.Size(dims).numel()) * torch.empty((), dtype=dt).element_size()
     assert line["exchange"]["bytes_to_rank0"] == want
+    assert line["roofline"]["read_dominant_ceiling"] > 0 and "cpu_baseline" not in line   # baseline: N=1 only
+
+
+def test_bench_defaults_north_star():
+    """The default (driver-run) bench line is the north_star config: the Llama-3-70B tensor
+    set, one copy LPT-sharded over the ranks (strong scaling), bf16, gs 128, 4-bit asym."""
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    import bench
+    a = bench.parse([])
+    assert (a.workload, a.replica, a.dtype, a.group_size, a.bits, a.symmetric) == (
+        "llama3-70b", False, "bf16", 128, 4, False)
+    shapes = bench.shapes_of("llama3-70b")
+    assert len(shapes) == 723 and sum(int(torch.Size(s).numel()) for s in shapes) == 70553706496
+    with pytest.raises(SystemExit):
+        bench.parse(["--replica", "--shard"])
+
+
+def test_bench_cpu_baseline_extrapolates(monkeypatch):
+    """cpu_baseline: C1 in full + a row sample of every distinct shape,
+    extrapolated to the workload; cores = threads used, the node's CPU count beside it."""
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    import bench
+    monkeypatch.setenv("OMP_NUM_THREADS", "2")
+    cb = bench.cpu_baseline("opt-125m", 1.0)
+    assert cb["kind"] == "port" and cb["cores"] == 2 and cb["node_cpus"] == os.cpu_count()
+    assert cb["value"] > 0 and cb["c1_full"]["seconds"] > 0 and "EXTRAPOLATED" in cb["sample"]
+    assert cb["shapes_sampled"] == len(bench.WORKLOADS["opt-125m"])
 
 
 def test_act_stats_file_and_flags(tmp_path):

@@ -268,3 +268,18 @@ def test_stream_copy_helper_copies_exactly():
         _hip.stream_copy(src, dst, torch.cuda.current_stream(dev).cuda_stream)
         torch.cuda.synchronize()
         assert torch.equal(src, dst)
+
+
+def test_stream_ceiling_helper_reads_all_writes_quarter():
+    """bench.py's read-dominant ceiling kernel: every 4 KiB of src is read (its four 1-KiB
+    quarters xor-folded per lane) and 1 KiB of dst written per 4 KiB."""
+    from awq_quantizer import _hip
+    dev = torch.device(DEV, 0)
+    for n in (4096, 4096 * 8 * 3 + 4096):
+        src = torch.randint(-2 ** 31, 2 ** 31 - 1, (n // 4,), dtype=torch.int32, device=dev)
+        dst = torch.zeros(n // 16, dtype=torch.int32, device=dev)
+        _hip.stream_ceiling(src, dst, torch.cuda.current_stream(dev).cuda_stream)
+        torch.cuda.synchronize()
+        q = src.view(-1, 4, 256)
+        want = q[:, 0] ^ q[:, 1] ^ q[:, 2] ^ q[:, 3]
+        assert torch.equal(dst.view(-1, 256), want)

@@ -27,7 +27,6 @@ Usage: python bench.py [--gpus N --steps K --warmup W --workload llama3-70b]
 import argparse
 import json
 import os
-import subprocess
 import sys
 import time
 
@@ -268,14 +267,6 @@ def gather_leg(batch, rank, world, dev, backend, iters=2, shard_owner=None, all_
             "bytes_to_rank0": moved, "ms": round(t * 1e3, 3), "GBs_into_rank0": round(moved / t / 1e9, 2)}
 
 
-def git_head():
-    try:
-        return subprocess.run(["git", "-C", ROOT, "rev-parse", "--short=12", "HEAD"], capture_output=True,
-                              text=True, timeout=5).stdout.strip() or None
-    except (OSError, subprocess.SubprocessError):
-        return None
-
-
 def recorded_traffic(path, key):
     """HBM traffic per launch recorded by a separate rocprofv3 --pmc run of this same
     command (scripts/profile_round.sh -> scripts/pmc_traffic.py; FETCH_SIZE x2 gfx950
@@ -412,8 +403,7 @@ def main():
                      "algorithmic_bytes_per_launch": algo_bytes,
                      "kernel_avg_us": round(kern_avg_s * 1e6, 2),
                      "kernel_avg_us_max_over_ranks": round(kern_max_s * 1e6, 2),
-                     "timing": f"hip events ({args.events}) on the launch stream, rank 0's launches",
-                     "head": git_head()},
+                     "timing": f"hip events ({args.events}) on the launch stream, rank 0's launches"},
     }
     if traffic_src:
         line["roofline"]["traffic_source"] = traffic_src

@@ -88,6 +88,9 @@ def build_parser() -> argparse.ArgumentParser:
                         "packed: int32 qweight/qzeros (bits-packed) + fp16 scales; "
                         "autoawq: a 4-bit checkpoint in AutoAWQ's GEMM layout (linear weights quantized, "
                         "everything else copied) + quant_config.json")
+    p.add_argument("--dist_output", type=str, default="per_rank", choices=["per_rank", "gather"],
+                   help="torchrun mode: per_rank = every rank writes its own chunk files (rank 0 adds "
+                        "metadata.json over all of them); gather = results sent to rank 0, which writes everything")
     return p
 
 
@@ -220,9 +223,16 @@ def save_model_in_chunks(tensors: Dict[str, Dict[str, torch.Tensor]], output_dir
                     logger)
 
 
+CHUNK_STEM = "model_chunk_{:04d}"   # reference main.py:485
+
+
+def _chunk_path(output_dir: str, c: int, use_safetensors: bool, stem: str = CHUNK_STEM) -> str:
+    return os.path.join(output_dir, stem.format(c) + (".safetensors" if use_safetensors else ".pt"))
+
+
 def _write_chunk(chunk: Dict[str, Dict[str, torch.Tensor]], output_dir: str, c: int, use_safetensors: bool,
-                 logger=None, label: str = "") -> None:
-    path = os.path.join(output_dir, f"model_chunk_{c:04d}")
+                 logger=None, label: str = "", stem: str = CHUNK_STEM) -> None:
+    path = os.path.join(output_dir, stem.format(c))
     if use_safetensors:
         from safetensors.torch import save_file
         save_file(_flatten(chunk), path + ".safetensors")
@@ -253,12 +263,20 @@ class ChunkWriter:
     save_model_in_chunks on the finished dict (failed tensors are skipped in the same order;
     chunk numbers are only known once every earlier tensor has finished).  Complete chunks
     are written by a small thread pool: torch.save releases the GIL while it writes, so
-    chunks serialise in parallel (1 -> 4 threads: 0.9 -> 3.9 GB/s in the build container)."""
+    chunks serialise in parallel (1 -> 4 threads: 0.9 -> 3.9 GB/s in the build container).
+
+    stem / metadata: torchrun's per-rank mode writes under a rank-private file stem and no
+    metadata.json; after close(), `t2c` (name -> local chunk), `n_chunks`, `n_ok` and
+    `qparams` describe what was written (_commit_rank_chunks renumbers the files)."""
 
     def __init__(self, order: List[str], output_dir: str, chunk_size: int, use_safetensors: bool, logger=None,
-                 writers: int = 0):
+                 writers: int = 0, stem: str = CHUNK_STEM, metadata: bool = True):
         self.order, self.dir, self.size, self.st, self.logger = order, output_dir, chunk_size, use_safetensors, logger
         self.writers = writers or min(8, max(2, (os.cpu_count() or 4) // 2))
+        self.stem, self.metadata = stem, metadata
+        self.t2c: Dict[str, int] = {}
+        self.n_chunks = self.n_ok = 0
+        self.qparams: Optional[Dict] = None
         self.status: Dict[str, Optional[Dict[str, torch.Tensor]]] = {}
         self.closed = False
         self.error: Optional[BaseException] = None
@@ -291,14 +309,16 @@ class ChunkWriter:
                     t2c[name] = c
                     n_ok += 1
                     if len(chunk) == self.size:
-                        futs.append(pool.submit(_write_chunk, chunk, self.dir, c, self.st, self.logger))
+                        futs.append(pool.submit(_write_chunk, chunk, self.dir, c, self.st, self.logger,
+                                                stem=self.stem))
                         chunk, c = {}, c + 1
                 if chunk:
-                    futs.append(pool.submit(_write_chunk, chunk, self.dir, c, self.st, self.logger))
+                    futs.append(pool.submit(_write_chunk, chunk, self.dir, c, self.st, self.logger, stem=self.stem))
                     c += 1
                 for f in futs:
                     f.result()
-            if n_ok:
+            self.t2c, self.n_chunks, self.n_ok, self.qparams = t2c, c, n_ok, qparams
+            if n_ok and self.metadata:
                 _write_metadata(self.dir, c, self.size, t2c, self.st, n_ok, qparams, self.logger)
         except BaseException as e:  # noqa: BLE001  (reported by close())
             self.error = e
@@ -331,21 +351,29 @@ def is_linear_weight(info: TensorInfo, group_size: int) -> bool:
     return n % 8 == 0 and k % group_size == 0
 
 
-def save_autoawq(quantized: Dict[str, Dict[str, torch.Tensor]], loader, passthrough: List[TensorInfo],
-                 output_dir: str, args, logger=None) -> None:
-    """model.safetensors with `<layer>.qweight/.qzeros/.scales` for every quantized linear
-    weight and every other tensor copied unchanged, quant_config.json (AutoAWQ) and, when
-    the source has one, config.json with a transformers `quantization_config`."""
-    from safetensors.torch import save_file
+def autoawq_tensors(quantized: Dict[str, Dict[str, torch.Tensor]], loader, passthrough: List[TensorInfo],
+                    failed: List[TensorInfo] = ()) -> Dict[str, torch.Tensor]:
+    """The tensors of an AutoAWQ checkpoint (or one shard of it): `<layer>.qweight/.qzeros/
+    .scales` per quantized linear weight; every passthrough tensor and every linear weight
+    that failed to quantize copied unchanged (those layers stay unquantized:
+    modules_to_not_convert)."""
     tensors = {}
     for name, r in quantized.items():
         prefix = name[: -len(".weight")]
         for f in ("qweight", "qzeros", "scales"):
             tensors[f"{prefix}.{f}"] = r[f].contiguous()
-    for info in passthrough:
+    for info in list(passthrough) + list(failed):
         tensors[info.name] = loader.read(info).contiguous()
-    save_file(tensors, os.path.join(output_dir, "model.safetensors"), metadata={"format": "pt"})
+    return tensors
+
+
+def write_autoawq_configs(output_dir: str, args, loader, not_converted: List[str], logger=None) -> None:
+    """quant_config.json (AutoAWQ) and, when the source has one, config.json with a
+    transformers `quantization_config`; `not_converted` = module names of linear weights
+    left unquantized (their quantization failed and they were copied through)."""
     qcfg = {"zero_point": not args.symmetric, "q_group_size": args.group_size, "w_bit": 4, "version": "GEMM"}
+    if not_converted:
+        qcfg["modules_to_not_convert"] = list(not_converted)
     with open(os.path.join(output_dir, "quant_config.json"), "w") as f:
         json.dump(qcfg, f, indent=2)
     src = os.path.join(getattr(loader, "model_path", "") or "", "config.json")
@@ -354,11 +382,28 @@ def save_autoawq(quantized: Dict[str, Dict[str, torch.Tensor]], loader, passthro
             cfg = json.load(f)
         cfg["quantization_config"] = {"quant_method": "awq", "bits": 4, "group_size": args.group_size,
                                       "zero_point": not args.symmetric, "version": "gemm"}
+        if not_converted:
+            cfg["quantization_config"]["modules_to_not_convert"] = list(not_converted)
         with open(os.path.join(output_dir, "config.json"), "w") as f:
             json.dump(cfg, f, indent=2)
+    if not_converted and logger:
+        logger.warning(f"{len(not_converted)} linear weight(s) failed to quantize and were copied unquantized "
+                       f"(modules_to_not_convert): {not_converted}")
+
+
+def save_autoawq(quantized: Dict[str, Dict[str, torch.Tensor]], loader, passthrough: List[TensorInfo],
+                 output_dir: str, args, logger=None, failed: List[TensorInfo] = ()) -> None:
+    """model.safetensors with `<layer>.qweight/.qzeros/.scales` for every quantized linear
+    weight and every other tensor copied unchanged (linear weights that failed to quantize
+    included, listed in modules_to_not_convert so the checkpoint still loads), plus the
+    configs of write_autoawq_configs."""
+    from safetensors.torch import save_file
+    tensors = autoawq_tensors(quantized, loader, passthrough, failed)
+    save_file(tensors, os.path.join(output_dir, "model.safetensors"), metadata={"format": "pt"})
+    write_autoawq_configs(output_dir, args, loader, [i.name[: -len(".weight")] for i in failed], logger)
     if logger:
         logger.info(f"Saved AutoAWQ checkpoint: {len(quantized)} quantized linear weights, "
-                    f"{len(passthrough)} tensors copied")
+                    f"{len(passthrough) + len(failed)} tensors copied")
 
 
 def _batches(infos: List[TensorInfo], budget: int) -> List[List[TensorInfo]]:
@@ -724,7 +769,8 @@ def main(argv: Optional[List[str]] = None) -> int:
         logger.info(f"Saving quantized model to {args.output_dir}")
         try:
             if autoawq:
-                save_autoawq(quantized, loader, passthrough, args.output_dir, args, logger)
+                save_autoawq(quantized, loader, passthrough, args.output_dir, args, logger,
+                             failed=[i for i in ordered if i.name not in quantized])
             elif writer is not None:
                 writer.close()
             else:
@@ -752,10 +798,25 @@ TIMINGS: Dict[str, float] = {}   # phase times of the last main() call (scripts/
 
 def _main_distributed(args, loader, ordered: List[TensorInfo], logger, start: float,
                       passthrough: Optional[List[TensorInfo]] = None, act_stats=None) -> int:
-    """torchrun mode: rank r quantizes the tensors an LPT partition by bytes assigns it
-    (identical on every rank, no exchange), keeps its results in HBM, then every result
-    is sent to rank 0 in one batched point-to-point round over RCCL (xGMI) and rank 0
-    writes the reference output layout.  Exit code agreed by all ranks."""
+    """torchrun mode: one process per GPU; rank r quantizes the tensors an LPT partition by
+    bytes assigns it (identical on every rank, derived from the header index with no
+    exchange; the reference's own partition_tensors, main.py:395-427).  Output
+    (--dist_output):
+
+      per_rank (default): every rank writes its own results as they come off its GPU
+        (ChunkWriter under a rank-private file stem, disk writes overlapping its later
+        batches); one all_gather_object of the per-rank chunk tables, then each rank renames
+        its files to global chunk numbers (rank r's chunks follow rank r-1's) and rank 0
+        writes metadata.json over every tensor in processing order (reference main.py:
+        430-512).  No result bytes cross the fabric.  AutoAWQ: one safetensors shard per rank
+        + model.safetensors.index.json.
+      gather: every result is sent to rank 0 in one batched point-to-point round over RCCL
+        (xGMI) and rank 0 writes the single-process layout.
+
+    A rank whose pipeline fails as a whole (no device, no library, a batch error) still
+    joins every collective, with no results; the failure is agreed (MAX over ranks), nothing
+    is published and every rank exits 1.  Per-tensor failures are skipped and logged as in
+    the single-process CLI."""
     from . import distributed as D
     import torch.distributed as dist
     backend = os.environ.get("AWQ_DIST_BACKEND", "nccl")      # gloo: tests with 2 ranks on one GPU
@@ -766,26 +827,214 @@ def _main_distributed(args, loader, ordered: List[TensorInfo], logger, start: fl
     comm = torch.device(device) if backend == "nccl" else torch.device("cpu")
     owner = dict(zip((i.name for i in ordered), D.shard([i.nbytes for i in ordered], world)))
     mine = [i for i in ordered if owner[i.name] == rank]
-    q = AWQQuantizer(bits=args.bits, group_size=args.group_size, symmetric=args.symmetric, zero_point=args.zero_point,
-                     percentile=args.percentile, scale_method=args.scale_method, per_channel=args.per_channel,
-                     search_grid=args.search_grid, search_max_shrink=args.search_max_shrink,
-                     duo_scaling=not args.no_duo_scaling, device=device,
-                     logger_name=f"awq_quantizer_{device}", logger_level=args.log_level,
-                     logger_to_file=args.log_file is not None, logger_file_path=args.log_file)
-    logger.info(f"rank {rank}/{world}: {len(mine)} of {len(ordered)} tensors on {device}")
-    results: Dict[str, Dict[str, torch.Tensor]] = {}
     autoawq = args.output_format == "autoawq"
-    quantize_stream(loader, mine, q, device, args.num_workers, max(1, args.prefetch_factor * args.batch_size),
-                    args.output_format in ("packed", "autoawq"), results, threading.Lock(), logger,
-                    args.memory_efficient, keep_on_device=True, export_autoawq=autoawq, act_stats=act_stats)
+    per_rank = args.dist_output == "per_rank"
+    results: Dict[str, Dict[str, torch.Tensor]] = {}
+    writer, failed = None, 0
+    t0 = time.time()
+    try:
+        q = AWQQuantizer(bits=args.bits, group_size=args.group_size, symmetric=args.symmetric,
+                         zero_point=args.zero_point, percentile=args.percentile, scale_method=args.scale_method,
+                         per_channel=args.per_channel, search_grid=args.search_grid,
+                         search_max_shrink=args.search_max_shrink, duo_scaling=not args.no_duo_scaling, device=device,
+                         logger_name=f"awq_quantizer_{device}", logger_level=args.log_level,
+                         logger_to_file=args.log_file is not None, logger_file_path=args.log_file)
+        logger.info(f"rank {rank}/{world}: {len(mine)} of {len(ordered)} tensors on {device}")
+        if per_rank and not autoawq:
+            writer = ChunkWriter([i.name for i in mine], args.output_dir, args.chunk_size, args.save_safetensors,
+                                 logger, stem=_rank_stem(rank), metadata=False)
+        # per-rank chunks: the writer holds each result until its chunk is on disk, nothing else does
+        sink = _NullSink() if writer is not None else results
+        quantize_stream(loader, mine, q, device, args.num_workers, max(1, args.prefetch_factor * args.batch_size),
+                        args.output_format in ("packed", "autoawq"), sink, threading.Lock(), logger,
+                        args.memory_efficient, keep_on_device=not per_rank, export_autoawq=autoawq,
+                        act_stats=act_stats, on_done=writer.done if writer else None)
+    except Exception as e:  # noqa: BLE001  (agreed below: every rank exits 1)
+        logger.error(f"rank {rank}: quantization failed: {e}")
+        failed = 1
+    if writer is not None:
+        try:
+            writer.close()
+        except Exception as e:  # noqa: BLE001
+            logger.error(f"rank {rank}: writing chunks failed: {e}")
+            failed = 1
+    if failed:
+        results = {}
+    TIMINGS[f"rank{rank}_quantize_write_s"] = round(time.time() - t0, 4)
+    try:
+        if per_rank and autoawq:
+            rc = _commit_rank_autoawq(args, loader, ordered, mine, results, passthrough or [], rank, world, failed,
+                                      comm, logger)
+        elif per_rank:
+            rc = _commit_rank_chunks(args, ordered, writer, rank, world, failed, comm, logger)
+        else:
+            rc = _gather_and_write(args, loader, ordered, results, passthrough or [], rank, world, failed, comm,
+                                   logger)
+    finally:
+        dist.destroy_process_group()
+    if rank == 0 and rc == 0:
+        logger.info(f"Quantization complete in {time.time() - start:.2f} seconds")
+    return rc
+
+
+class _NullSink(dict):
+    """quantize_stream's result dict when a ChunkWriter already owns every result."""
+
+    def update(self, *a, **k) -> None:
+        pass
+
+
+def _rank_stem(rank: int) -> str:
+    """Rank-private chunk file stem (renamed to CHUNK_STEM numbers once all ranks agree)."""
+    return f".rank{rank:05d}_chunk_{{:04d}}"
+
+
+def _agree(flag: int, comm: torch.device) -> int:
+    """MAX of a per-rank int over all ranks (a failure anywhere fails everyone)."""
+    from . import distributed as D
+    return int(D.max_over_ranks(float(flag), comm))
+
+
+def _commit_rank_chunks(args, ordered: List[TensorInfo], writer: Optional["ChunkWriter"], rank: int, world: int,
+                        failed: int, comm: torch.device, logger) -> int:
+    """Per-rank chunk files -> the reference layout: global chunk numbers in rank order,
+    metadata.json (rank 0) whose tensor_to_chunk lists every tensor in processing order.
+    Loading the chunks through metadata.json gives exactly the single-process result dicts
+    (tests/test_dist_output.py)."""
+    import torch.distributed as dist
+    st = args.save_safetensors
+    mine = {"failed": failed, "t2c": dict(writer.t2c) if writer and not failed else {},
+            "n_chunks": writer.n_chunks if writer and not failed else 0,
+            "qparams": writer.qparams if writer and not failed else None}
+    infos = [None] * world
+    dist.all_gather_object(infos, mine)
+    n_own = mine["n_chunks"]
+    if any(i["failed"] for i in infos):
+        tmp = _rank_stem(rank).split("{")[0]        # every chunk this rank wrote, whatever its state
+        for f in os.listdir(args.output_dir):
+            if f.startswith(tmp):
+                try:
+                    os.remove(os.path.join(args.output_dir, f))
+                except OSError:
+                    pass
+        if rank == 0:
+            logger.error("A rank failed; no output was published")
+        return 1
+    offs = [0] * world
+    for r in range(1, world):
+        offs[r] = offs[r - 1] + infos[r - 1]["n_chunks"]
+    bad = 0
+    try:
+        for c in range(n_own):
+            os.replace(_chunk_path(args.output_dir, c, st, _rank_stem(rank)),
+                       _chunk_path(args.output_dir, offs[rank] + c, st))
+    except OSError as e:
+        logger.error(f"rank {rank}: renaming chunk files failed: {e}")
+        bad = 1
+    rc = _agree(bad, comm)
+    if rank == 0 and rc == 0:
+        t2c = {}
+        for info in ordered:           # processing order = bytes descending (main.py:259)
+            for r, i in enumerate(infos):
+                if info.name in i["t2c"]:
+                    t2c[info.name] = offs[r] + i["t2c"][info.name]
+                    break
+        total = offs[-1] + infos[-1]["n_chunks"]
+        if not t2c:
+            logger.error("No tensors were successfully quantized")
+            rc = 1
+        else:
+            qparams = next(i["qparams"] for i in infos if i["qparams"] is not None)
+            try:
+                _write_metadata(args.output_dir, total, args.chunk_size, t2c, st, len(t2c), qparams, logger)
+                logger.info(f"Successfully quantized {len(t2c)} tensors on {world} GPUs; {total} chunk files "
+                            f"written by their ranks")
+            except OSError as e:
+                logger.error(f"Failed to save quantized model: {e}")
+                rc = 1
+    return _agree(rc, comm)
+
+
+def _commit_rank_autoawq(args, loader, ordered: List[TensorInfo], mine: List[TensorInfo],
+                         results: Dict[str, Dict[str, torch.Tensor]], passthrough: List[TensorInfo], rank: int,
+                         world: int, failed: int, comm: torch.device, logger) -> int:
+    """AutoAWQ checkpoint written by its ranks: rank r writes its quantized linears (and its
+    linears that failed, unquantized) as one safetensors shard, rank 0 adds the passthrough
+    tensors, and rank 0 writes model.safetensors.index.json (the transformers sharded-
+    checkpoint index) plus the configs.  One rank with tensors writes model.safetensors."""
+    import torch.distributed as dist
+    from safetensors.torch import save_file
+    not_quant = [i for i in mine if i.name not in results]
+    has = bool(results or not_quant or (rank == 0 and passthrough))
+    flags = [None] * world
+    dist.all_gather_object(flags, {"failed": failed, "has": has, "n_ok": len(results)})
+    if any(f["failed"] for f in flags):
+        if rank == 0:
+            logger.error("A rank failed; no output was published")
+        return 1
+    if sum(f["n_ok"] for f in flags) == 0:
+        if rank == 0:
+            logger.error("No tensors were successfully quantized")
+        return 1
+    writers = [r for r in range(world) if flags[r]["has"]]
+    fname = ("model.safetensors" if len(writers) == 1 else
+             f"model-{writers.index(rank) + 1:05d}-of-{len(writers):05d}.safetensors") if has else None
+    keys, size, bad = [], 0, 0
+    if has:
+        try:
+            tensors = autoawq_tensors(results, loader, passthrough if rank == 0 else [], not_quant)
+            save_file(tensors, os.path.join(args.output_dir, fname), metadata={"format": "pt"})
+            keys = list(tensors)
+            size = sum(t.numel() * t.element_size() for t in tensors.values())
+        except Exception as e:  # noqa: BLE001
+            logger.error(f"rank {rank}: writing {fname} failed: {e}")
+            bad = 1
+    shards = [None] * world
+    dist.all_gather_object(shards, {"file": fname, "keys": keys, "size": size, "bad": bad,
+                                    "not_converted": [i.name[: -len(".weight")] for i in not_quant]})
+    if any(s["bad"] for s in shards):
+        return 1
+    rc = 0
+    if rank == 0:
+        try:
+            if len(writers) > 1:
+                wmap = {k: s["file"] for s in shards for k in s["keys"]}
+                index = {"metadata": {"total_size": sum(s["size"] for s in shards)},
+                         "weight_map": {k: wmap[k] for k in sorted(wmap)}}
+                with open(os.path.join(args.output_dir, "model.safetensors.index.json"), "w") as f:
+                    json.dump(index, f, indent=2)
+            order = {i.name[: -len(".weight")]: k for k, i in enumerate(ordered)}
+            nc = sorted((m for s in shards for m in s["not_converted"]), key=lambda m: order.get(m, 0))
+            write_autoawq_configs(args.output_dir, args, loader, nc, logger)
+            logger.info(f"Saved AutoAWQ checkpoint from {world} ranks: {sum(f['n_ok'] for f in flags)} quantized "
+                        f"linear weights in {len(writers)} shard file(s)")
+        except Exception as e:  # noqa: BLE001
+            logger.error(f"Failed to save quantized model: {e}")
+            rc = 1
+    return _agree(rc, comm)
+
+
+def _gather_and_write(args, loader, ordered: List[TensorInfo], results: Dict[str, Dict[str, torch.Tensor]],
+                      passthrough: List[TensorInfo], rank: int, world: int, failed: int, comm: torch.device,
+                      logger) -> int:
+    """--dist_output gather: the packed results of every rank go to rank 0 in one batched
+    point-to-point round (distributed.gather_to_rank0), rank 0 writes the single-process
+    layout."""
+    import torch.distributed as dist
+    from . import distributed as D
+    autoawq = args.output_format == "autoawq"
     # which tensors succeeded, and the shapes rank 0 must receive (tiny metadata)
     meta = {n: {f: (tuple(t.shape), str(t.dtype)) for f, t in r.items() if f not in _SCALARS}
             for n, r in results.items()}
     all_meta = [None] * world
-    dist.all_gather_object(all_meta, meta)
+    dist.all_gather_object(all_meta, {"failed": failed, "meta": meta})
+    if any(m["failed"] for m in all_meta):
+        if rank == 0:
+            logger.error("A rank failed; no output was published")
+        return 1
     ok_owner, shapes = {}, {}
     for r, m in enumerate(all_meta):
-        for n, fields in m.items():
+        for n, fields in m["meta"].items():
             ok_owner[n] = r
             shapes[n] = {f: (shp, getattr(torch, dt.split(".")[-1])) for f, (shp, dt) in fields.items()}
     payload = {n: {f: t.to(comm) for f, t in r.items() if f not in _SCALARS} for n, r in results.items()}
@@ -811,18 +1060,15 @@ def _main_distributed(args, loader, ordered: List[TensorInfo], logger, start: fl
             logger.info(f"Successfully quantized {len(quantized)} tensors on {world} GPUs")
             try:
                 if autoawq:
-                    save_autoawq(quantized, loader, passthrough or [], args.output_dir, args, logger)
+                    save_autoawq(quantized, loader, passthrough, args.output_dir, args, logger,
+                                 failed=[i for i in ordered if i.name not in quantized])
                 else:
                     save_model_in_chunks(quantized, args.output_dir, chunk_size=args.chunk_size,
                                          use_safetensors=args.save_safetensors, logger=logger)
-                logger.info(f"Quantization complete in {time.time() - start:.2f} seconds")
             except Exception as e:  # noqa: BLE001
                 logger.error(f"Failed to save quantized model: {e}")
                 rc = 1
-    flag = torch.tensor([rc], dtype=torch.int32, device=comm)
-    dist.broadcast(flag, 0)
-    dist.destroy_process_group()
-    return int(flag.item())
+    return _agree(rc, comm)
 
 
 if __name__ == "__main__":

@@ -22,7 +22,7 @@ import torch
 from safetensors import safe_open
 
 from ..utils.logger import get_logger
-from ..utils.tensor_utils import filter_consolidated_files, get_model_files
+from ..utils.tensor_utils import convert_bf16_to_fp16, filter_consolidated_files, get_model_files, get_tensor_type
 
 _DT = {"BF16": torch.bfloat16, "F16": torch.float16, "F32": torch.float32, "F64": torch.float64,
        "I64": torch.int64, "I32": torch.int32, "I16": torch.int16, "I8": torch.int8, "U8": torch.uint8,
@@ -174,3 +174,13 @@ class SafetensorsLoader:
         path = os.path.join(output_dir, filename)
         save_file(tensors, path)
         self.logger.info(f"Saved {len(tensors)} tensors to {path}")
+
+    def convert_tensors_bf16_to_fp16(self, tensors: Dict[str, torch.Tensor]) -> Dict[str, torch.Tensor]:
+        """bf16 tensors of the dict as fp16 (RNE; out-of-range values become inf), others
+        unchanged (reference safetensors_loader.py:205-225)."""
+        out = {}
+        for name, t in tensors.items():
+            out[name] = convert_bf16_to_fp16(t)
+            if out[name].dtype != t.dtype:
+                self.logger.debug(f"Converted tensor {name} from {get_tensor_type(t)} to {get_tensor_type(out[name])}")
+        return out

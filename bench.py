@@ -98,6 +98,10 @@ def parse(argv=None):
     ap.add_argument("--clock-warm-ms", type=float, default=150.0,
                     help="ms of ceiling-probe streaming before the warmup launches (clock ramp)")
     ap.add_argument("--no-gather", action="store_true", help="N>1: skip the (untimed) gather-to-rank-0 leg")
+    ap.add_argument("--write-dir", default=None,
+                    help="after the timed region: every rank copies its packed shard to the host and writes it as "
+                         "chunk files into this directory (the CLI's per-rank output, main.ChunkWriter), reported as "
+                         "\"write\" (max over ranks); the files are removed afterwards")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "round2", "pmc_traffic.json"))
     a = ap.parse_args(argv)
     if a.replica and a.shard:
@@ -267,6 +271,40 @@ def gather_leg(batch, rank, world, dev, backend, iters=2, shard_owner=None, all_
             "bytes_to_rank0": moved, "ms": round(t * 1e3, 3), "GBs_into_rank0": round(moved / t / 1e9, 2)}
 
 
+def write_leg(batch, rank, dev, out_dir, chunk_size=10):
+    """The CLI's per-rank output step (torchrun mode, --dist_output per_rank) on this rank's
+    packed results: D2H into pinned memory, then chunk files written by main.ChunkWriter
+    under the rank's private stem.  Outside the timed region; max over ranks."""
+    import shutil
+    from awq_quantizer import distributed as D
+    from awq_quantizer.main import ChunkWriter, _rank_stem
+    d = os.path.join(out_dir, f"bench_write_rank{rank:05d}")
+    os.makedirs(d, exist_ok=True)
+    torch.cuda.synchronize(dev)
+    D.barrier()
+    t0 = time.perf_counter()
+    res = batch.results()
+    host = {}
+    for n in batch.names:
+        host[n] = {f: (v.to("cpu", non_blocking=True) if isinstance(v, torch.Tensor) and v.is_cuda else v)
+                   for f, v in res[n].items()}
+    torch.cuda.synchronize(dev)
+    t_d2h = time.perf_counter() - t0
+    w = ChunkWriter(list(batch.names), d, chunk_size, False, stem=_rank_stem(rank), metadata=False)
+    for n in batch.names:
+        w.done(n, host[n])
+    w.close()
+    os.sync()
+    t = time.perf_counter() - t0
+    nbytes = sum(os.path.getsize(os.path.join(d, f)) for f in os.listdir(d))
+    t_max = D.max_over_ranks(t, dev)
+    shutil.rmtree(d, ignore_errors=True)
+    return {"what": "per-rank output: D2H of the rank's packed shard + chunk files (main.ChunkWriter, torch.save) "
+                    "+ sync; outside the timed region",
+            "bytes_rank0": nbytes, "chunks_rank0": w.n_chunks, "d2h_s_rank0": round(t_d2h, 4),
+            "s_rank0": round(t, 4), "s_max_over_ranks": round(t_max, 4), "GBs_rank0": round(nbytes / t / 1e9, 3)}
+
+
 def recorded_traffic(path, key):
     """HBM traffic per launch recorded by a separate rocprofv3 --pmc run of this same
     command (scripts/profile_round.sh -> scripts/pmc_traffic.py; FETCH_SIZE x2 gfx950
@@ -370,6 +408,8 @@ def main():
                          all_shapes=all_shapes, bits=args.bits, gs=args.group_size)
               if world > 1 and not args.no_gather else None)
 
+    written = write_leg(batches[0], rank, dev, args.write_dir) if args.write_dir else None
+
     if rank != 0:
         if world > 1:
             import torch.distributed as dist
@@ -409,6 +449,8 @@ def main():
         line["roofline"]["traffic_source"] = traffic_src
     if gather:
         line["exchange"] = gather
+    if written:
+        line["write"] = written
     if ceiling:
         line["roofline"]["read_dominant_ceiling"] = round(ceiling, 1)
         line["roofline"]["frac_of_ceiling"] = round(achieved / ceiling, 4)

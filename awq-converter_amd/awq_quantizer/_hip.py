@@ -15,7 +15,7 @@ import torch
 
 LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib")
 LIB_PATH = os.path.join(LIB_DIR, "libawq_hip.so")
-ABI_VERSION = 7
+ABI_VERSION = 8
 
 AWQ_DTYPE = {torch.bfloat16: 0, torch.float16: 1, torch.float32: 2, torch.float64: 3}
 
@@ -183,7 +183,9 @@ def plan_block_tensor(descs, total_tiles: int, device: torch.device) -> torch.Te
     tensor (the kernel then skips the per-wave descriptor search)."""
     lib = load_library()
     arr = (TensorDesc * len(descs))(*descs)
-    nblk = -(-int(total_tiles) // 4)
+    nblk = lib.awq_plan_block_tensor(arr, len(descs), total_tiles, None, 0)   # size query
+    if nblk < 0:
+        raise RuntimeError(f"awq_plan_block_tensor failed: {last_error()}")
     host = torch.empty(max(nblk, 1), dtype=torch.int32)
     rc = lib.awq_plan_block_tensor(arr, len(descs), total_tiles, ctypes.c_void_p(host.data_ptr()), host.numel())
     if rc < 0:

@@ -952,9 +952,9 @@ void awq_fast_kernel(
         if (block_tensor != nullptr) {
             // host-planned tensor of the block's first tile (awq_plan_block_tensor): one
             // scalar load; blocks spanning tensors (small tensors) take a few more steps
-            const int32_t e = __builtin_amdgcn_readfirstlane(block_tensor[blockIdx.x]);
+            const int32_t e = __builtin_amdgcn_readfirstlane(block_tensor[wave / kTableTiles]);
             cur = e & 0x7FFFFFFF;
-            if (e < 0)   // the block's tiles span tensors (bit 31): step to this wave's one
+            if (e < 0)   // the entry's tiles span tensors (bit 31): step to this wave's one
                 while (cur + 1 < n && descs[cur + 1].tile_begin <= wave) ++cur;
         } else {
             cur = find_tensor(descs, n, 0, wave);
@@ -1029,7 +1029,7 @@ hipError_t launch_fast(const awq_tensor_desc* descs_dev, const int32_t* block_te
     if (blocks > max_blocks) blocks = max_blocks;
     awq_tensor_desc one{};
     if (single) one = *single;
-    // the table describes the one-tile-per-wave grid only
+    // the table is indexed by the wave's first tile: valid for the one-tile-per-wave grid only
     const int32_t* bt = (tpw == 1 && blocks * per_block >= total_tiles) ? block_tensor : nullptr;
     const dim3 grid((unsigned)blocks), block(64 * kWavesPerBlock);
 #define AWQ_LAUNCH_GS(Fm, B, S, G)                                                                                  \

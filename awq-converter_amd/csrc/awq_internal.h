@@ -35,10 +35,17 @@ namespace awq {
 constexpr int kTileElems = 2048;     // elements per wave-tile (4 loads x 64 lanes x 8)
 constexpr int kGroup = 128;          // the benchmark's group size (BASELINE.json)
 #ifndef AWQ_WPB
-#define AWQ_WPB AWQ_BLOCK_TILES   // include/awq_hip.h (tuning builds may override)
+#define AWQ_WPB 1
 #endif
-constexpr int kWavesPerBlock = AWQ_WPB;   // waves (= tiles) per workgroup: 8 = 512 threads (halves the
-                                          // workgroup dispatch rate the one-wave-per-tile grid needs)
+// waves (= tiles) per workgroup of the one-wave-per-tile grid.  1 (64-thread workgroups):
+// measured best on every large set (r2e, profiles/round2/r2e_kbench_wpb.log: Llama-3-8B
+// set 0.778 -> 0.803 of 8 TB/s from 8 -> 1; opt-125m 0.716 -> 0.737) — a finished wave's
+// slot is refilled one wave at a time instead of waiting for its workgroup's slowest wave
+constexpr int kWavesPerBlock = AWQ_WPB;
+// tiles per entry of the host-planned tensor table (include/awq_hip.h AWQ_BLOCK_TILES),
+// independent of the workgroup size: entry t / kTableTiles names the tensor of tile
+// kTableTiles * (t / kTableTiles)
+constexpr int kTableTiles = AWQ_BLOCK_TILES;
 
 // group sizes the streaming kernel is instantiated for (8 elements per lane: GS / 8 lanes
 // per group, a power of two between 4 and 32 so the group reductions stay inside DPP rows

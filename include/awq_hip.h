@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define AWQ_HIP_ABI_VERSION 7
+#define AWQ_HIP_ABI_VERSION 8
 
 /* dtype codes of the input weights (torch dtypes the reference accepts, awq.py:397) */
 enum { AWQ_DTYPE_BF16 = 0, AWQ_DTYPE_F16 = 1, AWQ_DTYPE_F32 = 2, AWQ_DTYPE_F64 = 3 };
@@ -110,13 +110,16 @@ int awq_ragged_eligible(int dtype, int64_t rows, int64_t K, int64_t group_size);
  * group_size (32, 64, 128 or 256; a tile is 2048 elements = 2048 / group_size groups). */
 int64_t awq_plan_ragged(awq_tensor_desc* descs_host, int n, int bits, int64_t group_size);
 
-/* Tiles (= waves) per workgroup of the ragged kernel's one-wave-per-tile grid. */
+/* Tiles per entry of the ragged launch's tensor table (awq_plan_block_tensor); the kernel's
+ * workgroup size is the library's own business (one 64-lane wave per tile). */
 #define AWQ_BLOCK_TILES 8
 
-/* HOST helper: block_tensor[b] = index of the tensor holding tile AWQ_BLOCK_TILES * b (the
- * first tile of workgroup b), with bit 31 set when the workgroup's tiles span more than
- * one tensor; b < ceil(total_tiles / AWQ_BLOCK_TILES) = the return value (< 0 on error:
- * len too small).  descs_host as planned by awq_plan_ragged. */
+/* HOST helper: block_tensor[b] = index of the tensor holding tile AWQ_BLOCK_TILES * b, with
+ * bit 31 set when tiles AWQ_BLOCK_TILES * b .. + AWQ_BLOCK_TILES - 1 span more than one
+ * tensor (a wave then steps forward from there to its own); b < ceil(total_tiles / AWQ_BLOCK_TILES) = the return value (< 0 on error:
+ * len too small).  block_tensor_host = NULL with len = 0: returns the length needed
+ * without writing (the workgroup size is the library's).  descs_host as planned by
+ * awq_plan_ragged. */
 int64_t awq_plan_block_tensor(const awq_tensor_desc* descs_host, int n, int64_t total_tiles,
                               int32_t* block_tensor_host, int64_t len);
 

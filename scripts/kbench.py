@@ -108,7 +108,8 @@ def main():
         key = (lp, id(bt))
         if key not in tables:
             arr = (_hip.TensorDesc * len(bt.descs))(*bt.descs)
-            host = torch.empty(-(-bt.total_tiles // 4), dtype=torch.int32)
+            need = lib.awq_plan_block_tensor(arr, len(bt.descs), bt.total_tiles, None, 0)   # size query
+            host = torch.empty(max(need, -(-bt.total_tiles // 4)), dtype=torch.int32)
             rc = lib.awq_plan_block_tensor(arr, len(bt.descs), bt.total_tiles, ctypes.c_void_p(host.data_ptr()),
                                            host.numel())
             assert rc > 0, lib.awq_last_error()

@@ -71,6 +71,14 @@
 #ifndef AWQ_F16_PLAIN
 #define AWQ_F16_PLAIN 1
 #endif
+// XCD runs: consecutive workgroups are dealt round-robin over the 8 XCDs (each with its
+// own L2), so with one-wave workgroups neighbouring tiles — which share the 128-B lines of
+// the scales (32 B per tile) and qzeros (8 B per tile) outputs — would write those lines
+// partially from different L2s.  Remapping block b so every XCD takes runs of
+// AWQ_XCD_RUN consecutive blocks keeps each line's writers on one L2 (0 = no remap)
+#ifndef AWQ_XCD_RUN
+#define AWQ_XCD_RUN 0
+#endif
 
 namespace awq {
 namespace {
@@ -889,6 +897,17 @@ __device__ __forceinline__ void compute_tile(const TileCtx& c, const Chunk<F::NW
 
 }
 
+// Bijective block renumbering for XCD runs (AWQ_XCD_RUN): block b, dealt to XCD b % 8,
+// takes the (b / 8) % R-th block of XCD b % 8's run inside super-chunk b / (8 R); blocks of
+// the last, partial super-chunk keep their index.
+__device__ __forceinline__ int64_t xcd_run_block(int64_t b, int64_t nblocks) {
+    constexpr int64_t R = AWQ_XCD_RUN, X = 8;
+    const int64_t full = nblocks / (X * R) * (X * R);
+    if (b >= full) return b;
+    const int64_t x = b % X, i = b / X;
+    return (i / R) * (X * R) + x * R + (i % R);
+}
+
 // Index of the tensor owning tile t, searching descs[base..n) (tile_begin ascending,
 // descs[base].tile_begin <= t).  64 lanes probe 64 evenly spaced descriptors per round
 // and a ballot narrows the range: one dependent load per round, 1 round for <= 64
@@ -931,8 +950,10 @@ void awq_fast_kernel(
     // wave index made provably uniform so tile/tensor bookkeeping and the buffer
     // descriptors live in SGPRs (no waterfall loops around the descriptors)
     const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int64_t wave = (int64_t)blockIdx.x * kWavesPerBlock + wid;
     const int64_t nwaves = (int64_t)gridDim.x * kWavesPerBlock;
+    int64_t blk = blockIdx.x;
+    if (AWQ_XCD_RUN > 0 && nwaves >= total_tiles) blk = xcd_run_block(blk, gridDim.x);   // one-shot grid only
+    const int64_t wave = blk * kWavesPerBlock + wid;
     if (wave >= total_tiles) return;
     uint32_t* zw = zwords[wid];
 #if AWQ_WIDE_STORE

@@ -40,6 +40,8 @@ SIGNATURES = {
     "awq_device_check": (_I32, [ctypes.c_char_p, _I32]),
     "awq_quantize_groups": (_I32, [_P, _I32, _I64, _I64, _I64, _I32, _I32, _P, _P, _P, _P, _P, _P]),
     "awq_quantize_search": (_I32, [_P, _I32, _I64, _I64, _I64, _I32, _I32, _I32, _I32, _P, _P, _P, _P, _P, _P]),
+    "awq_group_params": (_I32, [_P, _I32, _I64, _I64, _I64, _I32, _I32, _P, _P, _P]),
+    "awq_apply_params": (_I32, [_P, _I32, _I64, _I64, _I64, _P, _P, _I32, _I32, _I32, _P, _P]),
     "awq_ragged_eligible": (_I32, [_I32, _I64, _I64, _I64]),
     "awq_plan_ragged": (_I64, [ctypes.POINTER(TensorDesc), _I32, _I32, _I64]),
     "awq_stream_copy": (_I32, [_P, _P, _I64, _P]),
@@ -148,6 +150,27 @@ def quantize_search(x: torch.Tensor, rows: int, K: int, L: int, bits: int, symme
                                  int(n_grid), int(n_candidates), ptr(qweight), ptr(qzeros), ptr(scales),
                                  ptr(tensor_q), ptr(zeros), ctypes.c_void_p(stream_ptr(x.device)))
     check(rc, "awq_quantize_search")
+
+
+def group_params(x: torch.Tensor, rows: int, K: int, L: int, bits: int, symmetric: bool):
+    """awq_group_params: the reference's per-group (scale, zero point) in x's own arithmetic,
+    as exact float64 device tensors [rows, ceil(K / L)]."""
+    G = -(-K // L) if K else 0
+    s = torch.empty((rows, G), dtype=torch.float64, device=x.device)
+    z = torch.empty((rows, G), dtype=torch.float64, device=x.device)
+    check(load_library().awq_group_params(ptr(x), AWQ_DTYPE[x.dtype], rows, K, L, bits, int(bool(symmetric)), ptr(s),
+                                          ptr(z), _stream(x)), "awq_group_params")
+    return s, z
+
+
+def apply_params(x: torch.Tensor, rows: int, K: int, L: int, scales: torch.Tensor, zeros: torch.Tensor, qmin: int,
+                 qmax: int, mode: int) -> torch.Tensor:
+    """awq_apply_params: mode 0 quantize / mode 1 dequantize x (device, contiguous) with
+    float64 per-group parameters; result in x's dtype and shape."""
+    out = torch.empty_like(x)
+    check(load_library().awq_apply_params(ptr(x), AWQ_DTYPE[x.dtype], rows, K, L, ptr(scales), ptr(zeros), int(qmin),
+                                          int(qmax), int(mode), ptr(out), _stream(x)), "awq_apply_params")
+    return out
 
 
 def ragged_eligible(dtype: torch.dtype, rows: int, K: int, L: int) -> bool:

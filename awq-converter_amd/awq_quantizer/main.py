@@ -337,18 +337,36 @@ def _to_cpu(d: Dict[str, torch.Tensor]) -> Dict[str, torch.Tensor]:
     return {k: (v.cpu() if isinstance(v, torch.Tensor) else v) for k, v in d.items()}
 
 
-_NOT_LINEAR = ("embed", "lm_head", "norm", "wte", "wpe", "ln_")
+_NOT_LINEAR = ("embed", "lm_head", "norm", "wte", "wpe", "ln_", "router")
+# model types whose projection weights are transformers Conv1D modules, stored [in, out]
+# (quantizing them as [out, in] would group along the wrong axis): copied, not quantized
+CONV1D_MODEL_TYPES = ("gpt2",)
 
 
-def is_linear_weight(info: TensorInfo, group_size: int) -> bool:
-    """The tensors an AutoAWQ checkpoint quantizes: 2-D `*.weight` of linear layers (not
-    embeddings, the LM head or norms) whose shape the GEMM layout can hold."""
+def is_linear_weight(info: TensorInfo, group_size: int, model_type: Optional[str] = None) -> bool:
+    """The tensors an AutoAWQ checkpoint quantizes: 2-D `*.weight` of nn.Linear layers whose
+    shape the GEMM layout can hold.  Heuristic on names (no module graph in a checkpoint):
+    not embeddings, the LM head, norms, MoE routers (`*.router.*`, and `*.gate.weight` —
+    Mixtral's block_sparse_moe.gate / Qwen-MoE's mlp.gate; `gate_proj` is a linear) which
+    AutoAWQ keeps in fp16, nor any weight of a Conv1D model (CONV1D_MODEL_TYPES)."""
     if len(info.shape) != 2 or not info.name.endswith(".weight") or not info.dtype.is_floating_point:
         return False
-    if any(s in info.name for s in _NOT_LINEAR):
+    if model_type in CONV1D_MODEL_TYPES:
+        return False
+    if any(s in info.name for s in _NOT_LINEAR) or info.name.endswith(".gate.weight"):
         return False
     n, k = info.shape
     return n % 8 == 0 and k % group_size == 0
+
+
+def model_type_of(loader) -> Optional[str]:
+    """config.json's model_type next to the weights, if any."""
+    path = os.path.join(getattr(loader, "model_path", "") or "", "config.json")
+    try:
+        with open(path) as f:
+            return json.load(f).get("model_type")
+    except (OSError, ValueError):
+        return None
 
 
 def autoawq_tensors(quantized: Dict[str, Dict[str, torch.Tensor]], loader, passthrough: List[TensorInfo],
@@ -707,7 +725,10 @@ def main(argv: Optional[List[str]] = None) -> int:
             if args.bits != 4:
                 logger.error("--output_format autoawq writes 4-bit checkpoints (AutoAWQ GEMM layout)")
                 return 1
-            linear = {i.name for i in ordered if is_linear_weight(i, args.group_size)}
+            mtype = model_type_of(loader)
+            if mtype in CONV1D_MODEL_TYPES:
+                logger.warning(f"model_type {mtype}: Conv1D projection weights ([in, out]) are copied unquantized")
+            linear = {i.name for i in ordered if is_linear_weight(i, args.group_size, mtype)}
             passthrough = [i for i in index if i.name not in linear]
             ordered = [i for i in ordered if i.name in linear]
             logger.info(f"AutoAWQ export: {len(ordered)} linear weights quantized, {len(passthrough)} copied")

@@ -27,6 +27,18 @@ from .. import _hip
 from ..utils.logger import get_logger
 
 
+def _aligned(x: torch.Tensor) -> torch.Tensor:
+    """The streaming kernel's 16-B vector loads need a 16-B aligned base: a misaligned
+    device view (e.g. flat[4:4100]) is copied into fresh (aligned) storage."""
+    return x if x.data_ptr() % 16 == 0 else x.clone()
+
+
+def _device_input(v: torch.Tensor, dev: torch.device) -> torch.Tensor:
+    if v.device == dev and v.is_contiguous():
+        return _aligned(v)
+    return v.detach().to(dev).contiguous()
+
+
 class AWQQuantizer:
     """
     AWQ Quantizer (group-wise min/max RTN quantization, HIP backend).
@@ -191,7 +203,7 @@ class AWQQuantizer:
         rows, K, L, small = self._layout(tensor)
         self._check_mode()
         dev = self.compute_device()
-        x = tensor.detach().to(dev).contiguous()
+        x = _aligned(tensor.detach().to(dev).contiguous())
         G = -(-K // L)
         tensor_q = torch.empty(rows * K, dtype=torch.int32, device=dev)
         scales = torch.empty((rows, G), dtype=torch.float16, device=dev)
@@ -247,6 +259,121 @@ class AWQQuantizer:
                             zeros.to(dev, torch.int32).contiguous(), rows, K, L, out)
         return out.cpu()
 
+    # ------------------------------------------------------------------ reference private methods
+    # awq.py:130-374.  Subclasses and callers of the reference reach into these; they keep the
+    # reference's signatures, result dtypes and shapes (pinned bit for bit by
+    # tests/test_private_methods.py against 1 024 calls of the reference) and run on the HIP
+    # kernels: awq_group_params (scale / zero point of every group in the input dtype's own
+    # arithmetic), awq_apply_params (element-wise quantize / dequantize with given parameters)
+    # and awq_quantize_groups.  They are the reference's round-to-nearest whatever
+    # scale_method says (the clip search is reached through quantize / quantize_packed).
+    # Results are placed on self.device, as the reference places them.
+
+    def _home(self, t: torch.Tensor) -> torch.Tensor:
+        return t.to(self.device) if self.device.startswith("cuda") else t.cpu()
+
+    def _on_gpu(self, tensor: torch.Tensor) -> torch.Tensor:
+        self._check_input(tensor)
+        return tensor.detach().to(self.compute_device()).contiguous()
+
+    def _compute_scale_zp_for_group(self, tensor: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+        """awq.py:173-213: (scale, zero_point) of the whole tensor as one group, 0-d tensors
+        of its dtype (zero_point = 0 when symmetric)."""
+        self._check_mode()
+        x = self._on_gpu(tensor)
+        n = x.numel()
+        if n == 0:
+            raise RuntimeError("min(): Expected reduction dim to be specified for input.numel() == 0. "
+                               "Specify the reduction dim with the 'dim' argument.")
+        s, z = _hip.group_params(x, 1, n, n, self.bits, self.symmetric)
+        return self._home(s.reshape(()).to(tensor.dtype)), self._home(z.reshape(()).to(tensor.dtype))
+
+    def _calculate_scale_zp(self, tensor: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+        """awq.py:130-171: one group for the whole tensor (dim <= 1 or per_channel=False),
+        else one per dim-0 channel ([C] tensors of the input dtype)."""
+        if tensor.dim() <= 1 or not self.per_channel:
+            return self._compute_scale_zp_for_group(tensor)
+        self._check_mode()
+        C = tensor.size(0)
+        if C == 0:
+            raise RuntimeError("stack expects a non-empty TensorList")
+        x = self._on_gpu(tensor)
+        K = x.numel() // C
+        if K == 0:
+            raise RuntimeError("min(): Expected reduction dim to be specified for input.numel() == 0. "
+                               "Specify the reduction dim with the 'dim' argument.")
+        s, z = _hip.group_params(x, C, K, K, self.bits, self.symmetric)
+        return self._home(s.reshape(C).to(tensor.dtype)), self._home(z.reshape(C).to(tensor.dtype))
+
+    def _apply(self, tensor: torch.Tensor, scale, zero_point, mode: int) -> torch.Tensor:
+        """_quantize_tensor (mode 0) / _dequantize_tensor (mode 1) with the reference's
+        broadcasting (awq.py:237-242, 274-279): per dim-0 channel when per_channel and the
+        parameters are 1-D, else torch broadcasting (one parameter per element)."""
+        scale, zero_point = torch.as_tensor(scale), torch.as_tensor(zero_point)
+        meta = lambda t: torch.empty(t.shape, dtype=t.dtype, device="meta")
+        x_m, s_m, z_m = meta(tensor), meta(scale), meta(zero_point)
+        per_ch = self.per_channel and tensor.dim() > 1 and scale.dim() == 1
+        if per_ch:
+            shp = [scale.size(0)] + [1] * (tensor.dim() - 1)
+            s_m, z_m = s_m.reshape(shp), z_m.reshape(shp)
+        first = (x_m / s_m) if mode == 0 else (x_m - z_m)
+        res = (first + z_m) if mode == 0 else (first * s_m)
+        if tuple(res.shape) != tuple(tensor.shape):
+            raise NotImplementedError(f"parameters of shape {tuple(scale.shape)} / {tuple(zero_point.shape)} "
+                                      f"broadcast {tuple(tensor.shape)} to {tuple(res.shape)}")
+        if not tensor.is_floating_point():          # e.g. quantize()'s int32 tensor_q: torch casts it
+            tensor = tensor.to(first.dtype)         # to the op's dtype first
+        if first.dtype != tensor.dtype or res.dtype != tensor.dtype:
+            raise NotImplementedError(f"{tensor.dtype} with {scale.dtype} / {zero_point.dtype} parameters promotes "
+                                      f"to {res.dtype}; pass parameters of the tensor's dtype")
+        # (0-d / scalar parameters of another dtype do not promote: they enter the op at their
+        # own value in its compute type, like torch's original_scalar_value — as the kernel does)
+        x = self._on_gpu(tensor)
+        dev = x.device
+        n = x.numel()
+        if scale.numel() == 1 and zero_point.numel() == 1:
+            rows, K, L = 1, n, max(n, 1)
+        elif per_ch:
+            rows = tensor.size(0)
+            K = n // max(rows, 1)
+            L = max(K, 1)
+        else:
+            rows, K, L = 1, n, 1
+        s64 = scale.detach().to(dev, torch.float64)
+        z64 = zero_point.detach().to(dev, torch.float64)
+        if L == 1 and rows == 1 and n > 1:            # one parameter per element
+            s64 = s64.expand(tensor.shape).reshape(-1)
+            z64 = z64.expand(tensor.shape).reshape(-1)
+        elif per_ch:
+            s64, z64 = s64.reshape(-1).expand(rows), z64.reshape(-1).expand(rows)
+        out = _hip.apply_params(x, rows, K, L, s64.contiguous(), z64.contiguous(), self.qmin, self.qmax, mode)
+        return self._home(out)
+
+    def _quantize_tensor(self, tensor: torch.Tensor, scale: torch.Tensor, zero_point: torch.Tensor) -> torch.Tensor:
+        """awq.py:215-250: clamp(round(tensor / scale + zero_point), qmin, qmax), a float
+        tensor of the input dtype (NaN stays NaN)."""
+        return self._apply(tensor, scale, zero_point, 0)
+
+    def _dequantize_tensor(self, tensor_q: torch.Tensor, scale: torch.Tensor, zero_point: torch.Tensor) -> torch.Tensor:
+        """awq.py:252-284: (tensor_q - zero_point) * scale in the tensors' dtype."""
+        return self._apply(tensor_q, scale, zero_point, 1)
+
+    def _quantize_per_group(self, tensor: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
+        """awq.py:286-374: (tensor_q int32 of the input shape, scales fp32 [rows, G],
+        zero_points fp32 [rows, G]); tensors smaller than one group take
+        _calculate_scale_zp + _quantize_tensor (awq.py:297-300)."""
+        if tensor.numel() < self.group_size:
+            scale, zero_point = self._calculate_scale_zp(tensor)
+            return self._quantize_tensor(tensor, scale, zero_point), scale, zero_point
+        self._check_mode()
+        x = self._on_gpu(tensor)
+        rows = 1 if x.dim() <= 1 else x.shape[0]
+        K = x.numel() // rows
+        tq = torch.empty(rows * K, dtype=torch.int32, device=x.device)
+        _hip.quantize_groups(x, rows, K, self.group_size, self.bits, self.symmetric, tensor_q=tq)
+        s, z = _hip.group_params(x, rows, K, self.group_size, self.bits, self.symmetric)
+        return self._home(tq.reshape(tensor.shape)), self._home(s.float()), self._home(z.float())
+
     # ------------------------------------------------------------------ packed extension
     def packed_shapes(self, shape) -> dict:
         """Shapes of the packed outputs for an input of `shape` (group path only)."""
@@ -267,7 +394,7 @@ class AWQQuantizer:
         if tensor.numel() < self.group_size:
             raise ValueError("quantize_packed needs at least one full group (numel >= group_size)")
         dev = self.compute_device()
-        x = tensor.detach().to(dev).contiguous()
+        x = _aligned(tensor.detach().to(dev).contiguous())
         sh = self.packed_shapes(tuple(tensor.shape))
         qweight = torch.empty(sh["qweight"], dtype=torch.int32, device=dev)
         qzeros = torch.empty(sh["qzeros"], dtype=torch.int32, device=dev)
@@ -310,12 +437,16 @@ class AWQQuantizer:
         if eligible:
             dev = self.compute_device()
             for dt in (torch.bfloat16, torch.float16, torch.float32):   # one ragged launch per input dtype
-                part = {k: (v if v.device == dev and v.is_contiguous() else v.detach().to(dev).contiguous())
-                        for k, v in eligible.items() if v.dtype == dt}
+                part = {k: _device_input(v, dev) for k, v in eligible.items() if v.dtype == dt}
                 if part:
-                    batch = PackedBatch(part, bits=self.bits, symmetric=self.symmetric, group_size=self.group_size)
-                    batch.run()
-                    out.update(batch.results())
+                    try:
+                        batch = PackedBatch(part, bits=self.bits, symmetric=self.symmetric, group_size=self.group_size)
+                        batch.run()
+                        out.update(batch.results())
+                    except Exception as e:   # the batch as a whole failed: every tensor on its own
+                        self.logger.error(f"ragged launch of {len(part)} tensors failed ({e}); quantizing them "
+                                          f"one by one")
+                        rest.update(part)
         for name, t in rest.items():
             try:
                 out[name] = self.quantize_packed(t)
@@ -352,16 +483,26 @@ class AWQQuantizer:
         if eligible:
             dev = self.compute_device()
             for dt in (torch.bfloat16, torch.float16, torch.float32):
-                part = {k: (v if v.device == dev and v.is_contiguous() else v.detach().to(dev).contiguous())
-                        for k, v in eligible.items() if v.dtype == dt}
-                if part:
+                part = {k: _device_input(v, dev) for k, v in eligible.items() if v.dtype == dt}
+                if not part:
+                    continue
+                try:
                     batch = PackedBatch(part, bits=self.bits, symmetric=self.symmetric, parity=True, packed=False,
                                         group_size=self.group_size)
                     batch.run()
-                    for name, r in batch.results().items():
-                        out[name] = {"tensor_q": r["tensor_q"], "scales": r["scales"],
-                                     "zero_points": r["zero_points"], "bits": r["bits"],
-                                     "group_size": r["group_size"], "symmetric": r["symmetric"]}
+                    res = batch.results()
+                except Exception as e:   # the batch as a whole failed: every tensor on its own
+                    self.logger.error(f"ragged launch of {len(part)} tensors failed ({e}); quantizing them one by one")
+                    for name, t in part.items():
+                        try:
+                            out[name] = self._quantize_device(t)
+                        except Exception as e2:
+                            self.logger.error(f"Error quantizing tensor: {name}, error: {e2}")
+                    continue
+                for name, r in res.items():
+                    out[name] = {"tensor_q": r["tensor_q"], "scales": r["scales"],
+                                 "zero_points": r["zero_points"], "bits": r["bits"],
+                                 "group_size": r["group_size"], "symmetric": r["symmetric"]}
         return {k: out[k] for k in tensors if k in out}
 
     def quantize_layer_group(self, weights: Dict[str, torch.Tensor], activations: Optional[torch.Tensor] = None,

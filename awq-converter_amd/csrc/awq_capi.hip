@@ -155,6 +155,32 @@ int awq_quantize_search(const void* w, int dtype, int64_t rows, int64_t K, int64
     return AWQ_OK;
 }
 
+int awq_group_params(const void* w, int dtype, int64_t rows, int64_t K, int64_t group_size, int bits,
+                     int symmetric, double* scales, double* zeros, void* stream) {
+    g_err.clear();
+    if (int rc = check_common(rows, K, group_size, bits)) return rc;
+    if (dtype < AWQ_DTYPE_BF16 || dtype > AWQ_DTYPE_F64) return fail(AWQ_EINVAL, "unknown dtype code %d", dtype);
+    if (!scales && !zeros) return fail(AWQ_EINVAL, "no output requested");
+    if (rows * K == 0) return AWQ_OK;
+    if (!w) return fail(AWQ_EINVAL, "null input");
+    return hip_status(awq::launch_generic(w, dtype, rows, K, group_size, bits, symmetric, nullptr, nullptr, nullptr,
+                                          (hipStream_t)stream, 1, 0, scales, zeros), "awq group params");
+}
+
+int awq_apply_params(const void* x, int dtype, int64_t rows, int64_t K, int64_t group_size, const double* scales,
+                     const double* zeros, int qmin, int qmax, int mode, void* out, void* stream) {
+    g_err.clear();
+    if (group_size <= 0) return fail(AWQ_EINVAL, "Group size must be a positive integer: %lld", (long long)group_size);
+    if (rows < 0 || K < 0) return fail(AWQ_EINVAL, "negative shape (%lld, %lld)", (long long)rows, (long long)K);
+    if (dtype < AWQ_DTYPE_BF16 || dtype > AWQ_DTYPE_F64) return fail(AWQ_EINVAL, "unknown dtype code %d", dtype);
+    if (mode != 0 && mode != 1) return fail(AWQ_EINVAL, "unknown mode %d (0 quantize, 1 dequantize)", mode);
+    if (mode == 0 && qmin > qmax) return fail(AWQ_EINVAL, "qmin %d > qmax %d", qmin, qmax);
+    if (rows * K == 0) return AWQ_OK;
+    if (!x || !scales || !zeros || !out) return fail(AWQ_EINVAL, "null argument");
+    return hip_status(awq::launch_apply(x, dtype, rows, K, group_size, scales, zeros, qmin, qmax, mode, out,
+                                        (hipStream_t)stream), "awq apply params");
+}
+
 int64_t awq_plan_ragged(awq_tensor_desc* descs, int n, int bits, int64_t group_size) {
     g_err.clear();
     if (n < 0 || (n > 0 && !descs)) return fail(AWQ_EINVAL, "bad descriptor array"), -1;

@@ -30,7 +30,9 @@ __global__ __launch_bounds__(256) void awq_generic_kernel(const void* __restrict
                                                           int sym, int n_grid, int n_cand,
                                                           int32_t* __restrict__ tensor_q,
                                                           uint16_t* __restrict__ scales,
-                                                          int32_t* __restrict__ zeros) {
+                                                          int32_t* __restrict__ zeros,
+                                                          double* __restrict__ s_exact,
+                                                          double* __restrict__ z_exact) {
     typedef Traits<DT> T;
     typedef typename T::C C;
     const typename T::S* w = (const typename T::S*)wv;
@@ -94,11 +96,42 @@ __global__ __launch_bounds__(256) void awq_generic_kernel(const void* __restrict
         if (lane == 0) {
             if (scales) scales[gi] = canon_f16((float)s);         // fp64: via fp32 (awq.py:327)
             if (zeros) zeros[gi] = to_i32(z);
+            if (s_exact) s_exact[gi] = (double)s;                 // the input dtype's values, exact
+            if (z_exact) z_exact[gi] = (double)z;
         }
         if (tensor_q) {
             for (int64_t k = k0 + lane; k < k1; k += 64)
                 tensor_q[base + k] = to_i32(quant1<DT>(T::load(w, base + k), s, z, qmin, qmax));
         }
+    }
+}
+
+// Reference _quantize_tensor (awq.py:215-250, mode 0: clamp(round(RN(RN(x / s) + z))) and
+// _dequantize_tensor (awq.py:252-284, mode 1: RN(RN(x - z) * s)) with caller-given per-group
+// parameters, output in the input dtype.  The parameters (double) enter the op in its
+// compute type (fp32; fp64 for fp64 inputs) without a rounding to the dtype: what torch's
+// CPU kernels do with a 0-d / Python-number operand (its original value), and exact for
+// parameters of the tensor's own dtype.  Group g of row r covers elements [g L, g L + L) of
+// the row; L = 1 is a per-element parameter array (any broadcast).
+template <int DT>
+__global__ __launch_bounds__(256) void awq_apply_kernel(const void* __restrict__ xv, int64_t rows, int64_t K,
+                                                        int64_t L, const double* __restrict__ sp,
+                                                        const double* __restrict__ zp, int qmin, int qmax, int mode,
+                                                        void* __restrict__ outv) {
+    typedef Traits<DT> T;
+    typedef typename T::C C;
+    const typename T::S* x = (const typename T::S*)xv;
+    typename T::S* out = (typename T::S*)outv;
+    const int64_t G = (K + L - 1) / L;
+    const int64_t total = rows * K;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t r = i / K, k = i - r * K;
+        const int64_t gi = r * G + k / L;
+        const C s = (C)sp[gi], z = (C)zp[gi];
+        const C v = T::load(x, i);
+        const C res = mode == 0 ? quant1<DT>(v, s, z, qmin, qmax) : T::rn(T::rn(v - z) * s);
+        out[i] = T::store(res);
     }
 }
 
@@ -161,7 +194,7 @@ inline unsigned grid_for(int64_t work, int64_t per_block, int64_t cap) {
 
 hipError_t launch_generic(const void* w, int dtype, int64_t rows, int64_t K, int64_t L, int bits,
                           int symmetric, int32_t* tensor_q, uint16_t* scales, int32_t* zeros,
-                          hipStream_t stream, int n_grid, int n_cand) {
+                          hipStream_t stream, int n_grid, int n_cand, double* s_exact, double* z_exact) {
     const int qmin = symmetric ? -(1 << (bits - 1)) : 0;
     const int qmax = symmetric ? (1 << (bits - 1)) - 1 : (1 << bits) - 1;
     const int64_t G = (K + L - 1) / L;
@@ -171,10 +204,12 @@ hipError_t launch_generic(const void* w, int dtype, int64_t rows, int64_t K, int
     do {                                                                                             \
         if (search)                                                                                  \
             hipLaunchKernelGGL((awq_generic_kernel<D, true>), dim3(grid), dim3(256), 0, stream, w, rows, \
-                               K, L, qmin, qmax, symmetric, n_grid, n_cand, tensor_q, scales, zeros);  \
+                               K, L, qmin, qmax, symmetric, n_grid, n_cand, tensor_q, scales, zeros,   \
+                               s_exact, z_exact);                                                      \
         else                                                                                         \
             hipLaunchKernelGGL((awq_generic_kernel<D, false>), dim3(grid), dim3(256), 0, stream, w,     \
-                               rows, K, L, qmin, qmax, symmetric, 1, 0, tensor_q, scales, zeros);      \
+                               rows, K, L, qmin, qmax, symmetric, 1, 0, tensor_q, scales, zeros,       \
+                               s_exact, z_exact);                                                      \
     } while (0)
     switch (dtype) {
     case AWQ_DTYPE_BF16: AWQ_GEN(AWQ_DTYPE_BF16); break;
@@ -184,6 +219,33 @@ hipError_t launch_generic(const void* w, int dtype, int64_t rows, int64_t K, int
     default: return hipErrorInvalidValue;
     }
 #undef AWQ_GEN
+    return hipPeekAtLastError();
+}
+
+hipError_t launch_apply(const void* x, int dtype, int64_t rows, int64_t K, int64_t L, const double* scales,
+                        const double* zeros, int qmin, int qmax, int mode, void* out, hipStream_t stream) {
+    const int64_t total = rows * K;
+    if (total <= 0) return hipSuccess;
+    const dim3 grid(grid_for(total, 256, 256 * 16)), block(256);
+    switch (dtype) {
+    case AWQ_DTYPE_BF16:
+        hipLaunchKernelGGL((awq_apply_kernel<AWQ_DTYPE_BF16>), grid, block, 0, stream, x, rows, K, L, scales, zeros,
+                           qmin, qmax, mode, out);
+        break;
+    case AWQ_DTYPE_F16:
+        hipLaunchKernelGGL((awq_apply_kernel<AWQ_DTYPE_F16>), grid, block, 0, stream, x, rows, K, L, scales, zeros,
+                           qmin, qmax, mode, out);
+        break;
+    case AWQ_DTYPE_F32:
+        hipLaunchKernelGGL((awq_apply_kernel<AWQ_DTYPE_F32>), grid, block, 0, stream, x, rows, K, L, scales, zeros,
+                           qmin, qmax, mode, out);
+        break;
+    case AWQ_DTYPE_F64:
+        hipLaunchKernelGGL((awq_apply_kernel<AWQ_DTYPE_F64>), grid, block, 0, stream, x, rows, K, L, scales, zeros,
+                           qmin, qmax, mode, out);
+        break;
+    default: return hipErrorInvalidValue;
+    }
     return hipPeekAtLastError();
 }
 

@@ -57,24 +57,28 @@ template <> struct Traits<AWQ_DTYPE_BF16> {
     static __device__ float load(const S* p, int64_t i) { return __uint_as_float((uint32_t)p[i] << 16); }
     static __device__ float rn(float v) { return sw_rn_bf16(v); }
     static __device__ float lo() { return __uint_as_float(0x2EDC0000u); }   // RN_bf16(1e-10)
+    static __device__ S store(float v) { return (S)(__float_as_uint(sw_rn_bf16(v)) >> 16); }
 };
 template <> struct Traits<AWQ_DTYPE_F16> {
     typedef uint16_t S; typedef float C;
     static __device__ float load(const S* p, int64_t i) { return sw_f16_to_f32(p[i]); }
     static __device__ float rn(float v) { return sw_f16_to_f32(sw_f32_to_f16(v)); }
     static __device__ float lo() { return 0.0f; }                           // RN_f16(1e-10) = 0
+    static __device__ S store(float v) { return sw_f32_to_f16(v); }
 };
 template <> struct Traits<AWQ_DTYPE_F32> {
     typedef float S; typedef float C;
     static __device__ float load(const S* p, int64_t i) { return p[i]; }
     static __device__ float rn(float v) { return v; }
     static __device__ float lo() { return 1e-10f; }
+    static __device__ S store(float v) { return v; }
 };
 template <> struct Traits<AWQ_DTYPE_F64> {
     typedef double S; typedef double C;
     static __device__ double load(const S* p, int64_t i) { return p[i]; }
     static __device__ double rn(double v) { return v; }
     static __device__ double lo() { return 1e-10; }
+    static __device__ S store(double v) { return v; }
 };
 
 template <typename C> __device__ __forceinline__ C wave_min(C v) {

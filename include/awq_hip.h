@@ -102,6 +102,24 @@ int awq_quantize_search(const void* w, int dtype, int64_t rows, int64_t K, int64
                         int symmetric, int n_grid, int n_candidates, int32_t* qweight, int32_t* qzeros,
                         uint16_t* scales, int32_t* tensor_q, int32_t* zeros, void* stream);
 
+/* The reference's per-group scale and zero point (_compute_scale_zp_for_group, awq.py:173-213)
+ * in the input dtype's own arithmetic, as exact doubles [rows, G] (bf16 / fp16 / fp32 / fp64
+ * values; NaN groups give NaN).  What _quantize_per_group stores in its fp32 scale / zero
+ * tensors (awq.py:327-328, 352-353) is these values rounded to fp32; the small-tensor path
+ * (awq.py:130-171) is group_size = K.  Either output may be NULL. */
+int awq_group_params(const void* w, int dtype, int64_t rows, int64_t K, int64_t group_size, int bits,
+                     int symmetric, double* scales, double* zeros, void* stream);
+
+/* Elementwise with caller-given parameters per group (scales / zeros double [rows, G], used
+ * in the op's compute type — fp32, fp64 for fp64 inputs — unrounded to the input dtype, as
+ * torch's CPU kernels use a 0-d operand; group_size 1 = one parameter per element), result
+ * in the input dtype (out [rows, K]):
+ *   mode 0: clamp(round(RN(RN(x / s) + z)), qmin, qmax)   (_quantize_tensor, awq.py:215-250;
+ *           NaN stays NaN)
+ *   mode 1: RN(RN(x - z) * s)                             (_dequantize_tensor, awq.py:252-284) */
+int awq_apply_params(const void* x, int dtype, int64_t rows, int64_t K, int64_t group_size, const double* scales,
+                     const double* zeros, int qmin, int qmax, int mode, void* out, void* stream);
+
 /* True (1) if a tensor of this dtype/shape is eligible for awq_quantize_ragged. */
 int awq_ragged_eligible(int dtype, int64_t rows, int64_t K, int64_t group_size);
 

@@ -196,6 +196,73 @@ int oracle_quantize(const void* x, int dtype, int64_t rows, int64_t K, int64_t L
     return 0;
 }
 
+/* awq.py:173-213 per group, the scale / zero point themselves (exact doubles of the dtype's
+ * values): what _compute_scale_zp_for_group returns (0-d, dtype D) and, rounded to fp32,
+ * what _quantize_per_group stores (awq.py:327-328, 352-353). */
+int oracle_group_params(const void* x, int dtype, int64_t rows, int64_t K, int64_t L, int bits, int sym,
+                        double* scales, double* zeros) {
+    if (!x || rows < 0 || K < 0 || L <= 0 || (bits != 4 && bits != 8)) return -1;
+    int qmin = sym ? -(1 << (bits - 1)) : 0;
+    int qmax = sym ? (1 << (bits - 1)) - 1 : (1 << bits) - 1;
+    int64_t G = (K + L - 1) / L;
+    for (int64_t r = 0; r < rows; ++r) {
+        for (int64_t g = 0; g < G; ++g) {
+            int64_t k0 = g * L, k1 = k0 + L;
+            int padded = k1 > K;
+            if (k1 > K) k1 = K;
+            double mn = padded ? 0.0 : INFINITY, mx = padded ? 0.0 : -INFINITY;
+            int nan = 0;
+            for (int64_t k = k0; k < k1; ++k) {
+                double v = load_elem(x, dtype, r * K + k);
+                if (isnan(v)) nan = 1;
+                if (v < mn) mn = v;
+                if (v > mx) mx = v;
+            }
+            if (nan) { mn = NAN; mx = NAN; }
+            double s, z;
+            group_scale_zp(mn, mx, dtype, qmin, qmax, sym, &s, &z);
+            if (scales) scales[r * G + g] = s;
+            if (zeros) zeros[r * G + g] = z;
+        }
+    }
+    return 0;
+}
+
+/* awq.py:215-250 (_quantize_tensor, mode 0) and awq.py:252-284 (_dequantize_tensor, mode 1)
+ * with given per-group parameters (double), which enter each op in its compute type (fp32;
+ * fp64 for D = f64) unrounded to D, as torch's CPU kernels use a 0-d operand's original
+ * value; out in dtype D (bf16 / f16 bits, f32, f64). */
+static inline void store_elem(void* out, int dtype, int64_t i, double v) {
+    switch (dtype) {
+    case AWQ_ORACLE_BF16: ((uint16_t*)out)[i] = oracle_f32_to_bf16((float)v); break;
+    case AWQ_ORACLE_F16: ((uint16_t*)out)[i] = oracle_f32_to_f16((float)v); break;
+    case AWQ_ORACLE_F32: ((float*)out)[i] = (float)v; break;
+    default: ((double*)out)[i] = v;
+    }
+}
+int oracle_apply_params(const void* x, int dtype, int64_t rows, int64_t K, int64_t L, const double* scales,
+                        const double* zeros, int qmin, int qmax, int mode, void* out) {
+    if (!x || !scales || !zeros || !out || rows < 0 || K < 0 || L <= 0) return -1;
+    int64_t G = (K + L - 1) / L;
+    for (int64_t r = 0; r < rows; ++r) {
+        for (int64_t k = 0; k < K; ++k) {
+            int64_t gi = r * G + k / L;
+            double s = scales[gi], z = zeros[gi];
+            if (dtype != AWQ_ORACLE_F64) { s = (double)(float)s; z = (double)(float)z; }
+            double v = load_elem(x, dtype, r * K + k), t;
+            if (mode == 0) {
+                t = op_add(op_div(v, s, dtype), z, dtype);                 /* awq.py:245 */
+                t = op_clamp(op_round(t, dtype), qmin, qmax);              /* awq.py:248 */
+            } else {
+                t = op_sub(v, z, dtype);                                   /* awq.py:282 */
+                t = (dtype == AWQ_ORACLE_F64) ? t * s : rn((double)((float)t * (float)s), dtype);
+            }
+            store_elem(out, dtype, r * K + k, t);
+        }
+    }
+    return 0;
+}
+
 /* Opt-in clip search (scale_method="search").  NOT in the reference (it stores
  * scale_method, awq.py:66, validates it, :111-112, and never reads it again), so this
  * restates the product's own definition (include/awq_hip.h, awq_quantize_search) — parity

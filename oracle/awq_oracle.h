@@ -15,6 +15,12 @@ int oracle_quantize(const void* x, int dtype, int64_t rows, int64_t K, int64_t L
 /* opt-in clip search (product definition, include/awq_hip.h awq_quantize_search) */
 int oracle_quantize_search(const void* x, int dtype, int64_t rows, int64_t K, int64_t L, int bits, int sym,
                            int n_grid, int n_cand, int32_t* tensor_q, uint16_t* scales_f16, int32_t* zeros);
+/* awq.py:173-213 per group: scale / zero point as exact doubles [rows, G] */
+int oracle_group_params(const void* x, int dtype, int64_t rows, int64_t K, int64_t L, int bits, int sym,
+                        double* scales, double* zeros);
+/* awq.py:215-250 (mode 0) / 252-284 (mode 1) with given per-group parameters; out in dtype */
+int oracle_apply_params(const void* x, int dtype, int64_t rows, int64_t K, int64_t L, const double* scales,
+                        const double* zeros, int qmin, int qmax, int mode, void* out);
 int oracle_dequantize(const int32_t* tensor_q, const uint16_t* scales_f16, const int32_t* zeros,
                       int64_t rows, int64_t K, int64_t L, float* out);
 int oracle_pack_rows(const int32_t* v, int64_t rows, int64_t n, int bits, int qmin, int32_t* packed);

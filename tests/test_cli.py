@@ -258,6 +258,15 @@ def test_linear_selection_for_autoawq():
     assert not is_linear_weight(mk("model.layers.0.x.weight", (250, 256)), 128)      # out % 8
     assert not is_linear_weight(mk("model.layers.0.x.weight", (256, 200)), 128)      # in % group
     assert not is_linear_weight(mk("model.layers.0.x.bias", (256, 256)), 128)
+    # MoE routers stay fp16 (AutoAWQ); gate_proj is a linear
+    assert not is_linear_weight(mk("model.layers.0.block_sparse_moe.gate.weight", (8, 4096)), 128)
+    assert not is_linear_weight(mk("model.layers.0.mlp.gate.weight", (64, 2048)), 128)
+    assert not is_linear_weight(mk("model.layers.0.mlp.router.weight", (64, 2048)), 128)
+    assert is_linear_weight(mk("model.layers.0.mlp.gate_proj.weight", (14336, 4096)), 128)
+    assert is_linear_weight(mk("model.layers.0.block_sparse_moe.experts.0.w1.weight", (14336, 4096)), 128)
+    # GPT-2 Conv1D weights are [in, out]: never quantized as linears
+    assert not is_linear_weight(mk("h.0.attn.c_attn.weight", (768, 2304)), 128, "gpt2")
+    assert is_linear_weight(mk("h.0.attn.c_attn.weight", (768, 2304)), 128, "llama")
 
 
 @pytest.mark.gpu

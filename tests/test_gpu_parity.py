@@ -283,3 +283,24 @@ def test_stream_ceiling_helper_reads_all_writes_quarter():
         q = src.view(-1, 4, 256)
         want = q[:, 0] ^ q[:, 1] ^ q[:, 2] ^ q[:, 3]
         assert torch.equal(dst.view(-1, 256), want)
+
+
+def test_misaligned_device_views():
+    """a contiguous device view whose base is not 16-B aligned (flat[4:4100]) is
+    quantized correctly by quantize / quantize_packed / quantize_model_packed /
+    quantize_model_device, and does not take its batch down with it."""
+    dev = torch.device(DEV, 0)
+    flat = rand_bf16((8192,), 77, 0.02).to(dev)
+    views = {"mis": flat[4:4100], "mis2": flat[1:3073].view(3, 1024), "ok": flat[:4096]}
+    assert views["mis"].data_ptr() % 16 != 0
+    q = Q(bits=4, symmetric=False)
+    packed = q.quantize_model_packed(dict(views))
+    device = q.quantize_model_device(dict(views), packed=False)
+    for name, v in views.items():
+        ref = orc.quantize(v.cpu(), bits=4, group_size=128, symmetric=False)
+        rows = 1 if v.dim() <= 1 else v.shape[0]
+        for pk in (q.quantize_packed(v), packed[name]):
+            assert torch.equal(pk["qweight"].cpu(), orc.pack_rows(ref["tensor_q"].reshape(rows, -1), 4, 0)), name
+            assert torch.equal(pk["scales"].cpu(), ref["scales"]), name
+        assert torch.equal(device[name]["tensor_q"].cpu(), ref["tensor_q"]), name
+        assert torch.equal(q.quantize(v)["tensor_q"], ref["tensor_q"]), name

@@ -195,10 +195,27 @@ def plan_ragged(descs, bits: int, group_size: int = 128) -> int:
     return total
 
 
+def _pageable_tables() -> bool:
+    # A/B switch for scripts/cli_bench.py: the round-1 path (tables copied from pageable
+    # memory: a host-synchronous copy per batch on the compute stream)
+    return os.environ.get("AWQ_PAGEABLE_TABLES", "0") == "1"
+
+
+def _upload(host: torch.Tensor, device: torch.device) -> torch.Tensor:
+    """Host table -> device on the current stream.  From page-locked memory the copy is
+    asynchronous (the CLI pipeline keeps running); torch's caching host allocator holds the
+    staging block until the copy has completed, so it may be dropped right away."""
+    if _pageable_tables():
+        return host.to(device)
+    pinned = torch.empty(host.shape, dtype=host.dtype, pin_memory=True)
+    pinned.copy_(host)
+    return pinned.to(device, non_blocking=True)
+
+
 def descs_to_device(descs, device: torch.device) -> torch.Tensor:
     arr = (TensorDesc * len(descs))(*descs)
     host = torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8)
-    return host.to(device)
+    return _upload(host, device)
 
 
 def plan_block_tensor(descs, total_tiles: int, device: torch.device) -> torch.Tensor:
@@ -213,7 +230,7 @@ def plan_block_tensor(descs, total_tiles: int, device: torch.device) -> torch.Te
     rc = lib.awq_plan_block_tensor(arr, len(descs), total_tiles, ctypes.c_void_p(host.data_ptr()), host.numel())
     if rc < 0:
         raise RuntimeError(f"awq_plan_block_tensor failed: {last_error()}")
-    return host.to(device)
+    return _upload(host, device)
 
 
 def quantize_ragged(descs_dev: torch.Tensor, n: int, total_tiles: int, bits: int, symmetric: bool,

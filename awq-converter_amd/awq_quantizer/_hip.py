@@ -42,6 +42,7 @@ SIGNATURES = {
     "awq_quantize_search": (_I32, [_P, _I32, _I64, _I64, _I64, _I32, _I32, _I32, _I32, _P, _P, _P, _P, _P, _P]),
     "awq_group_params": (_I32, [_P, _I32, _I64, _I64, _I64, _I32, _I32, _P, _P, _P]),
     "awq_apply_params": (_I32, [_P, _I32, _I64, _I64, _I64, _P, _P, _I32, _I32, _I32, _P, _P]),
+    "awq_packs_directly": (_I32, [_I32, _I64, _I64, _I64]),
     "awq_ragged_eligible": (_I32, [_I32, _I64, _I64, _I64]),
     "awq_plan_ragged": (_I64, [ctypes.POINTER(TensorDesc), _I32, _I32, _I64]),
     "awq_stream_copy": (_I32, [_P, _P, _I64, _P]),
@@ -171,6 +172,13 @@ def apply_params(x: torch.Tensor, rows: int, K: int, L: int, scales: torch.Tenso
     check(load_library().awq_apply_params(ptr(x), AWQ_DTYPE[x.dtype], rows, K, L, ptr(scales), ptr(zeros), int(qmin),
                                           int(qmax), int(mode), ptr(out), _stream(x)), "awq_apply_params")
     return out
+
+
+def packs_directly(dtype: torch.dtype, rows: int, K: int, L: int) -> bool:
+    """awq_quantize_groups writes packed outputs without int32 staging buffers."""
+    if dtype not in AWQ_DTYPE:
+        return False
+    return bool(load_library().awq_packs_directly(AWQ_DTYPE[dtype], rows, K, L))
 
 
 def ragged_eligible(dtype: torch.dtype, rows: int, K: int, L: int) -> bool:

@@ -400,7 +400,7 @@ class AWQQuantizer:
         qzeros = torch.empty(sh["qzeros"], dtype=torch.int32, device=dev)
         scales = torch.empty(sh["scales"], dtype=torch.float16, device=dev)
         kw = {}
-        if not _hip.ragged_eligible(x.dtype, sh["rows"], sh["K"], self.group_size):
+        if self.search_candidates or not _hip.packs_directly(x.dtype, sh["rows"], sh["K"], self.group_size):
             kw = dict(tensor_q=torch.empty(sh["rows"] * sh["K"], dtype=torch.int32, device=dev),
                       zeros=torch.empty(sh["scales"], dtype=torch.int32, device=dev))
         self._launch(x, sh["rows"], sh["K"], self.group_size, qweight=qweight, qzeros=qzeros, scales=scales,

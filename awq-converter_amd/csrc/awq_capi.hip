@@ -7,6 +7,7 @@
 #include <algorithm>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 
@@ -46,9 +47,28 @@ bool fast_eligible(int dtype, int64_t rows, int64_t K, int64_t group_size) {
            awq::fast_shape_ok(rows, K, group_size);
 }
 
+// the row-segment kernel (any group size <= 512, bf16 / fp16 / fp32): 16-B aligned input,
+// dword-aligned outputs, segment offsets within int range
+bool rowgroup_shape(int dtype, int64_t rows, int64_t K, int64_t group_size) {
+    if (const char* e = getenv("AWQ_NO_ROWGROUP"))   // A/B against the generic kernel (scripts/generic_bench.py)
+        if (e[0] == '1') return false;
+    return awq::rowgroup_gpt(dtype, K, group_size) > 0 && rows > 0 && rows * K < ((int64_t)1 << 40);
+}
+
+bool rowgroup_ok(int dtype, int64_t rows, int64_t K, int64_t group_size, const void* w, const void* qweight,
+                 const void* qzeros, const void* scales, const void* tensor_q, const void* zeros) {
+    return rowgroup_shape(dtype, rows, K, group_size) && aligned(w, 16) && (!qweight || aligned(qweight, 4)) &&
+           (!qzeros || aligned(qzeros, 4)) && (!scales || aligned(scales, 2)) && (!tensor_q || aligned(tensor_q, 4)) &&
+           (!zeros || aligned(zeros, 4));
+}
+
 }  // namespace
 
 extern "C" {
+
+int awq_packs_directly(int dtype, int64_t rows, int64_t K, int64_t group_size) {
+    return (fast_eligible(dtype, rows, K, group_size) || rowgroup_shape(dtype, rows, K, group_size)) ? 1 : 0;
+}
 
 int awq_abi_version(void) { return AWQ_HIP_ABI_VERSION; }
 
@@ -96,6 +116,9 @@ int awq_quantize_groups(const void* w, int dtype, int64_t rows, int64_t K, int64
         return hip_status(awq::launch_fast(nullptr, nullptr, &d, 1, d.tile_count, dtype, bits, symmetric,
                                            (int)group_size, (K % group_size) != 0, s), "awq fast kernel");
     }
+    if (rowgroup_ok(dtype, rows, K, group_size, w, qweight, qzeros, scales, tensor_q, zeros))
+        return hip_status(awq::launch_rowgroup(w, dtype, rows, K, group_size, bits, symmetric, qweight, qzeros, scales,
+                                               tensor_q, zeros, s), "awq row-group kernel");
     // generic path: per-group int32 values first, then packing (needs tensor_q / zeros buffers)
     if ((qweight && !tensor_q) || (qzeros && !zeros))
         return fail(AWQ_EINVAL, "this shape/dtype takes the generic kernel: packed outputs need the int32 "

@@ -37,6 +37,7 @@
 // wave finds its tensor from a host-planned per-workgroup table (or, without it, a
 // 64-lane ballot search of the descriptors).
 #include <cstdlib>
+#include <type_traits>
 
 #include "awq_internal.h"
 
@@ -901,11 +902,231 @@ __device__ __forceinline__ void compute_tile(const TileCtx& c, const Chunk<F::NW
 // takes the (b / 8) % R-th block of XCD b % 8's run inside super-chunk b / (8 R); blocks of
 // the last, partial super-chunk keep their index.
 __device__ __forceinline__ int64_t xcd_run_block(int64_t b, int64_t nblocks) {
-    constexpr int64_t R = AWQ_XCD_RUN, X = 8;
+    constexpr int64_t R = AWQ_XCD_RUN > 0 ? AWQ_XCD_RUN : 1, X = 8;   // (only called when AWQ_XCD_RUN > 0)
     const int64_t full = nblocks / (X * R) * (X * R);
     if (b >= full) return b;
     const int64_t x = b % X, i = b / X;
     return (i / R) * (X * R) + x * R + (i % R);
+}
+
+// ---------------------------------------------------------------------------------------
+// Any group size up to 512 (bf16 / fp16; 256 for fp32), any K: row-segment tiles.
+//
+// A tile = GPT consecutive groups of one row (GPT in {8, 16, 32, 64}, host-chosen for the
+// best lane use), one 64-lane wave per tile: the segment's bytes go to LDS with 16-B
+// loads (16-B aligned start, the range check zero-fills past the tensor end), lane
+// (grp, j) owns chunk j of group grp (P = 64 / GPT lanes per group, C = ceil(L / P)
+// elements each), reduces the raw-bits min/max over its chunk and the group's P lanes
+// (the streaming kernel's group_range / params_from_range: the same verified arithmetic),
+// then overwrites each of its elements in LDS by its packed field; the wave then packs
+// qweight / qzeros words and stores them coalesced.  Tile boundaries fall on qweight and
+// qzeros word boundaries (GPT * L and GPT are multiples of 8), so no word is shared
+// between waves.  Replaces the one-wave-per-group generic kernel plus its int32 staging
+// and pack passes (~10.5 B moved per element) for these shapes.
+// ---------------------------------------------------------------------------------------
+constexpr int kRgStageBytes = 8192;
+
+template <typename F>
+struct RgSlot {
+    typedef typename std::conditional<F::kBytes == 2, uint16_t, uint32_t>::type T;
+    static constexpr uint32_t kNan = F::kBytes == 2 ? 0xFFFFu : 0xFFFFFFFFu;   // field code of NaN
+    __device__ static int sext(uint32_t v) { return F::kBytes == 2 ? (int)(int16_t)v : (int)v; }
+    __device__ static float dec(uint32_t v) { return F::kBytes == 2 ? F::dec(v) : __uint_as_float(v); }
+};
+
+// packed field (q - qmin) of one element of a group with a positive finite scale
+template <typename F, int BITS, bool SYM, bool PLAIN>
+__device__ __forceinline__ float field1_fast(float x, float r, float z, float s) {
+    constexpr float QR = (float)((1 << BITS) - 1);
+    constexpr float HALF = (float)(1 << (BITS - 1));
+    const float t = PLAIN ? F::quot_plain(x, r) : F::quot(x, s, r);
+    float u;
+    if (SYM && F::kWide) u = __builtin_rintf(t) + HALF;
+    else if (SYM) u = t + HALF;
+    else u = F::rn(t + F::as_fmt(z));
+    return __builtin_fminf(__builtin_fmaxf(__builtin_rintf(u), 0.0f), QR);
+}
+
+#ifndef AWQ_RG_UNROLL
+#define AWQ_RG_UNROLL 8
+#endif
+
+// fields of elements [cb, ce) of one group with a positive finite scale: AWQ_RG_UNROLL
+// independent elements per step (their LDS reads in flight together)
+template <typename F, int BITS, bool SYM, bool PLAIN, typename S>
+__device__ __forceinline__ void rg_fields(S* stage, int base, int cb, int ce, const GroupParams& p) {
+    int i = cb;
+    for (; i + AWQ_RG_UNROLL <= ce; i += AWQ_RG_UNROLL) {
+        uint32_t v[AWQ_RG_UNROLL];
+#pragma unroll
+        for (int u = 0; u < AWQ_RG_UNROLL; ++u) v[u] = stage[base + i + u];
+#pragma unroll
+        for (int u = 0; u < AWQ_RG_UNROLL; ++u)
+            stage[base + i + u] = (S)(uint32_t)field1_fast<F, BITS, SYM, PLAIN>(RgSlot<F>::dec(v[u]), p.r, p.z, p.s);
+    }
+    for (; i < ce; ++i)
+        stage[base + i] = (S)(uint32_t)field1_fast<F, BITS, SYM, PLAIN>(RgSlot<F>::dec(stage[base + i]), p.r, p.z, p.s);
+}
+
+// (8 KiB + 16 B of LDS per one-wave workgroup: at most 19 waves per CU)
+template <typename F, int BITS, bool SYM>
+__global__ __launch_bounds__(64, 4) void awq_rowgroup_kernel(const void* __restrict__ w, int64_t rows, int64_t K,
+                                                             int64_t L, int P, int GPT, int64_t tiles_per_row,
+                                                             int32_t* __restrict__ qweight, int32_t* __restrict__ qzeros,
+                                                             uint16_t* __restrict__ scales,
+                                                             int32_t* __restrict__ tensor_q, int32_t* __restrict__ zeros) {
+    typedef RgSlot<F> SL;
+    typedef typename SL::T S;
+    constexpr int QMIN = SYM ? -(1 << (BITS - 1)) : 0;
+    constexpr uint32_t MASK = (1u << BITS) - 1u;
+    constexpr int PER = 32 / BITS;             // elements (and groups) per packed word
+    constexpr uint32_t NANF = (uint32_t)(0u - (uint32_t)QMIN) & MASK;   // field of INT32_MIN - qmin
+    __shared__ __attribute__((aligned(16))) S stage[(kRgStageBytes + 16) / sizeof(S)];   // + the alignment skew
+    __shared__ uint32_t zst[64];
+    const int lane = threadIdx.x;
+    const int64_t tile = blockIdx.x;
+    const int64_t r = tile / tiles_per_row;
+    const int64_t G = (K + L - 1) / L;
+    const int64_t g0 = (tile - r * tiles_per_row) * GPT;
+    const int ng = (int)min((int64_t)GPT, G - g0);
+    const int64_t kb = g0 * L, ke = min((g0 + ng) * L, K);     // the row segment [kb, ke)
+    const int n_el = (int)(ke - kb);
+    // ---- stage the segment's bytes (from a 16-B aligned start) in LDS ----
+    const uint64_t byte0 = (uint64_t)(r * K + kb) * F::kBytes;
+    const uint64_t a0 = byte0 & ~(uint64_t)15;
+    const int skew = (int)(byte0 - a0) / F::kBytes;               // slot of element kb
+    const uint64_t total = (uint64_t)rows * (uint64_t)K * F::kBytes;
+    const int nbytes = (int)(byte0 - a0) + n_el * F::kBytes;
+    const int nch = (nbytes + 15) >> 4;
+    const uint32_t lim = (uint32_t)min(total - a0, (uint64_t)nch * 16);
+    const __amdgpu_buffer_rsrc_t rw = rsrc((const char*)w + a0, lim);
+#pragma unroll 4
+    for (int c = lane; c < nch; c += 64) {
+        if (__builtin_expect(16u * c + 16u <= lim, 1)) {
+            *(u4*)((char*)stage + 16 * c) = __builtin_amdgcn_raw_buffer_load_b128(rw, (uint32_t)(16 * c), 0, AWQ_LOAD_AUX);
+        } else {   // the tensor's last bytes: a 16-B load straddling the range end would read as all zeros
+            for (int h = 0; h < 8; ++h)
+                ((uint16_t*)stage)[8 * c + h] = __builtin_amdgcn_raw_buffer_load_b16(rw, (uint32_t)(16 * c + 2 * h), 0, 0);
+        }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    // ---- this lane's chunk of its group ----
+    const int grp = lane / P, j = lane - grp * P;
+    const bool active = grp < ng;
+    const int glen = active ? (int)min(L, K - (g0 + grp) * L) : 0;   // elements in the row (tail: fewer)
+    const int C = (int)((L + P - 1) / P);
+    const int cb = min(j * C, glen), ce = min(cb + C, glen);
+    const int base = skew + grp * (int)L;
+    const bool padded = active && glen < L;                    // awq.py:337-339: zeros join the min/max
+    int smax = padded ? 0 : INT_MIN;
+    uint32_t umax = 0, umin = padded ? 0u : F::kOnes;
+    int i1 = cb;
+    for (; i1 + AWQ_RG_UNROLL <= ce; i1 += AWQ_RG_UNROLL) {   // independent LDS reads in flight
+        uint32_t v[AWQ_RG_UNROLL];
+#pragma unroll
+        for (int u = 0; u < AWQ_RG_UNROLL; ++u) v[u] = stage[base + i1 + u];
+#pragma unroll
+        for (int u = 0; u < AWQ_RG_UNROLL; ++u) {
+            smax = max(smax, SL::sext(v[u]));
+            umax = max(umax, v[u]);
+            umin = min(umin, v[u]);
+        }
+    }
+    for (; i1 < ce; ++i1) {
+        const uint32_t v = stage[base + i1];
+        smax = max(smax, SL::sext(v));
+        umax = max(umax, v);
+        umin = min(umin, v);
+    }
+    for (int o = 1; o < P; o <<= 1) {                          // the group's P lanes (adjacent)
+        smax = max(smax, __shfl_xor(smax, o, 64));
+        umax = max(umax, (uint32_t)__shfl_xor((int)umax, o, 64));
+        umin = min(umin, (uint32_t)__shfl_xor((int)umin, o, 64));
+    }
+    float gmn, gmx;
+    bool gnan;
+    group_range<F, SYM>(smax, umax, umin, gmn, gmx, gnan);
+    const GroupParams p = params_from_range<F, BITS, SYM>(gmn, gmx);
+    const bool special = !F::fast(p.r);
+    const bool plain = F::kHasPlain && __builtin_amdgcn_ballot_w64(active && !F::plain_ok(p.s)) == 0;
+    // ---- each element's packed field, in place (NaN elements: the field of INT32_MIN, or in
+    //      parity mode a NaN code that tensor_q turns into INT32_MIN) ----
+    const bool codes = tensor_q != nullptr;
+    if (__builtin_expect(special, 0)) {
+        for (int i = cb; i < ce; ++i) {
+            const float x = SL::dec(stage[base + i]);
+            const float t = F::rn(opaque(x) / p.s);
+            const float u = SYM ? t : F::rn(t + p.z);
+            const float rr = __builtin_rintf(u);
+            uint32_t code = SL::kNan;
+            if (!__builtin_isnan(rr))
+                code = (uint32_t)((int)__builtin_fminf(__builtin_fmaxf(rr, (float)QMIN),
+                                                       (float)(SYM ? (1 << (BITS - 1)) - 1 : (1 << BITS) - 1)) - QMIN);
+            stage[base + i] = (S)(code == SL::kNan && !codes ? NANF : code);
+        }
+    } else if (plain) {
+        rg_fields<F, BITS, SYM, true>(stage, base, cb, ce, p);
+    } else {
+        rg_fields<F, BITS, SYM, false>(stage, base, cb, ce, p);
+    }
+    if (active && j == 0) {
+        const int64_t gi = r * G + g0 + grp;
+        if (scales) scales[gi] = f16_bits(p.s);
+        if (zeros) zeros[gi] = __builtin_isnan(p.z) ? INT32_MIN : (int32_t)p.z;
+        zst[grp] = __builtin_isnan(p.z) ? NANF : ((uint32_t)((int)p.z - QMIN) & MASK);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    // ---- packed words of the segment (kb is a word boundary: GPT * L % PER == 0) ----
+    if (qweight) {
+        const int64_t wpr = (K + PER - 1) / PER;
+        const int nw = (n_el + PER - 1) / PER;
+        int32_t* dst = qweight + r * wpr + kb / PER;
+        // 16-bit fields of a 16-B aligned segment (skew 0: the row starts on 8 elements, i.e.
+        // K % 8 == 0) read as whole vectors; anything else field by field
+        const bool vec = sizeof(S) == 2 && skew == 0 && !codes && (n_el % PER) == 0;
+        for (int wd = lane; wd < nw; wd += 64) {
+            uint32_t word = 0;
+            if (vec && BITS == 4) {                  // 8 fields (<= 15) in 4 dwords -> 8 nibbles
+                const u4 q = *(const u4*)(stage + 8 * wd);
+                const uint32_t b0 = q.x | (q.x >> 12), b1 = q.y | (q.y >> 12);   // low byte: nibble pair
+                const uint32_t b2 = q.z | (q.z >> 12), b3 = q.w | (q.w >> 12);
+                word = __builtin_amdgcn_perm(b1, b0, 0x0c0c0400u) | (__builtin_amdgcn_perm(b3, b2, 0x0c0c0400u) << 16);
+            } else if (vec) {                        // 4 fields (<= 255) in 2 dwords -> 4 bytes
+                const u2v q = *(const u2v*)(stage + 4 * wd);
+                word = __builtin_amdgcn_perm(q.y, q.x, 0x06040200u);
+            } else {
+#pragma unroll
+                for (int i = 0; i < PER; ++i) {
+                    const int e = wd * PER + i;
+                    if (e < n_el) {
+                        const uint32_t code = stage[skew + e];
+                        word |= ((code == SL::kNan ? NANF : code) & MASK) << (BITS * i);
+                    }
+                }
+            }
+            dst[wd] = (int32_t)word;
+        }
+    }
+    if (tensor_q) {
+        int32_t* dst = tensor_q + r * K + kb;
+        for (int e = lane; e < n_el; e += 64) {
+            const uint32_t code = stage[skew + e];
+            dst[e] = code == SL::kNan ? INT32_MIN : (int32_t)code + QMIN;
+        }
+    }
+    if (qzeros) {                                 // g0 is a word boundary: GPT % PER == 0
+        const int64_t zpr = (G + PER - 1) / PER;
+        const int nwz = (ng + PER - 1) / PER;
+        if (lane < nwz) {
+            uint32_t word = 0;
+            for (int i = 0; i < PER && lane * PER + i < ng; ++i) word |= zst[lane * PER + i] << (BITS * i);
+            qzeros[r * zpr + g0 / PER + lane] = (int32_t)word;
+        }
+    }
 }
 
 // Index of the tensor owning tile t, searching descs[base..n) (tile_begin ascending,
@@ -1093,6 +1314,55 @@ hipError_t launch_fast(const awq_tensor_desc* descs_dev, const int32_t* block_te
 #undef AWQ_LAUNCH_FMT
 #undef AWQ_LAUNCH
 #undef AWQ_LAUNCH_GS
+    return hipPeekAtLastError();
+}
+
+// Row-segment tiles of awq_rowgroup_kernel: groups per tile (8..64, a power of two: tile
+// boundaries on packed-word boundaries) with the best lane use G / (ceil(G / GPT) * GPT),
+// larger on ties; 0 if the shape does not fit the LDS stage.
+int rowgroup_gpt(int dtype, int64_t K, int64_t L) {
+    if (dtype != AWQ_DTYPE_BF16 && dtype != AWQ_DTYPE_F16 && dtype != AWQ_DTYPE_F32) return 0;
+    const int64_t slots = kRgStageBytes / (dtype == AWQ_DTYPE_F32 ? 4 : 2);   // (+ 16 B of skew slack)
+    if (L <= 0 || K <= 0) return 0;
+    const int64_t G = (K + L - 1) / L;
+    int best = 0;
+    double best_use = -1.0;
+    for (int gpt = 8; gpt <= 64; gpt *= 2) {
+        if (gpt * L > slots) break;
+        const double use = (double)G / (double)(((G + gpt - 1) / gpt) * gpt);
+        if (use >= best_use) { best_use = use; best = gpt; }
+    }
+    return best;
+}
+
+hipError_t launch_rowgroup(const void* w, int dtype, int64_t rows, int64_t K, int64_t L, int bits, int symmetric,
+                           int32_t* qweight, int32_t* qzeros, uint16_t* scales, int32_t* tensor_q, int32_t* zeros,
+                           hipStream_t stream) {
+    const int gpt = rowgroup_gpt(dtype, K, L);
+    if (gpt == 0 || rows <= 0) return hipErrorInvalidValue;
+    const int64_t G = (K + L - 1) / L;
+    const int64_t tpr = (G + gpt - 1) / gpt;
+    const int P = 64 / gpt;
+    const dim3 grid((unsigned)(rows * tpr)), block(64);
+#define AWQ_RG(Fm, B, S)                                                                                         \
+    hipLaunchKernelGGL((awq_rowgroup_kernel<Fm, B, S>), grid, block, 0, stream, w, rows, K, L, P, gpt, tpr, qweight, \
+                       qzeros, scales, tensor_q, zeros)
+#define AWQ_RG_FMT(Fm)                                                     \
+    switch ((bits == 8 ? 2 : 0) + (symmetric ? 1 : 0)) {                  \
+    case 0: AWQ_RG(Fm, 4, false); break;                                   \
+    case 1: AWQ_RG(Fm, 4, true); break;                                    \
+    case 2: AWQ_RG(Fm, 8, false); break;                                   \
+    default: AWQ_RG(Fm, 8, true); break;                                   \
+    }
+    if (dtype == AWQ_DTYPE_F16) {
+        AWQ_RG_FMT(FmtF16)
+    } else if (dtype == AWQ_DTYPE_F32) {
+        AWQ_RG_FMT(FmtF32)
+    } else {
+        AWQ_RG_FMT(FmtBF16)
+    }
+#undef AWQ_RG_FMT
+#undef AWQ_RG
     return hipPeekAtLastError();
 }
 

@@ -113,6 +113,11 @@ hipError_t launch_generic(const void* w, int dtype, int64_t rows, int64_t K, int
                           double* z_exact = nullptr);
 hipError_t launch_apply(const void* x, int dtype, int64_t rows, int64_t K, int64_t L, const double* scales,
                         const double* zeros, int qmin, int qmax, int mode, void* out, hipStream_t stream);
+// any group size <= 512 (fp32: 256), bf16 / fp16 / fp32, any K; rowgroup_gpt() = 0: not eligible
+int rowgroup_gpt(int dtype, int64_t K, int64_t L);
+hipError_t launch_rowgroup(const void* w, int dtype, int64_t rows, int64_t K, int64_t L, int bits, int symmetric,
+                           int32_t* qweight, int32_t* qzeros, uint16_t* scales, int32_t* tensor_q, int32_t* zeros,
+                           hipStream_t stream);
 hipError_t launch_selftest(int which, unsigned long long* out, hipStream_t stream);
 hipError_t launch_stream_copy(const void* src, void* dst, int64_t bytes, hipStream_t stream);
 hipError_t launch_stream_ceiling(const void* src, void* dst, int64_t bytes, hipStream_t stream);

@@ -76,11 +76,14 @@ int awq_device_check(char* arch, int len);
 
 /* Quantize one [rows, K] tensor (replaces awq.py:286-374 incl. the small-tensor
  * path awq.py:130-171, which a caller expresses as group_size = K).
- * bits in {4, 8}; symmetric selects qmin/qmax per awq.py:114-128.
- * bf16 / fp16 / fp32 with group_size in {32, 64, 128, 256} and K % group_size == 0, or
- * K % 8 == 0 (padded rows, awq.py:337-339), take the streaming fast kernel; every other
- * shape/dtype (fp64, other group sizes, K % 8 != 0 tails) takes the generic kernel (same
- * results). */
+ * bits in {4, 8}; symmetric selects qmin/qmax per awq.py:114-128.  Kernels, all with the
+ * same results:
+ *   bf16 / fp16 / fp32, group_size in {32, 64, 128, 256}, K % group_size == 0 or K % 8 == 0
+ *     (padded rows, awq.py:337-339): the streaming kernel;
+ *   bf16 / fp16 with any other group_size <= 512 (fp32: <= 256), or any K: the row-segment
+ *     kernel (packed outputs written directly);
+ *   everything else (fp64, larger groups): the generic kernel, whose packed outputs need
+ *     tensor_q / zeros as staging buffers (awq_packs_directly() == 0). */
 int awq_quantize_groups(const void* w, int dtype, int64_t rows, int64_t K, int64_t group_size,
                         int bits, int symmetric, int32_t* qweight, int32_t* qzeros,
                         uint16_t* scales, int32_t* tensor_q, int32_t* zeros, void* stream);
@@ -119,6 +122,10 @@ int awq_group_params(const void* w, int dtype, int64_t rows, int64_t K, int64_t 
  *   mode 1: RN(RN(x - z) * s)                             (_dequantize_tensor, awq.py:252-284) */
 int awq_apply_params(const void* x, int dtype, int64_t rows, int64_t K, int64_t group_size, const double* scales,
                      const double* zeros, int qmin, int qmax, int mode, void* out, void* stream);
+
+/* 1 if awq_quantize_groups writes qweight / qzeros for this dtype / shape without the int32
+ * tensor_q / zeros staging buffers (streaming or row-segment kernel; 16-B aligned input). */
+int awq_packs_directly(int dtype, int64_t rows, int64_t K, int64_t group_size);
 
 /* True (1) if a tensor of this dtype/shape is eligible for awq_quantize_ragged. */
 int awq_ragged_eligible(int dtype, int64_t rows, int64_t K, int64_t group_size);

@@ -1,8 +1,11 @@
 #!/usr/bin/env python3
 """Throughput of the single-tensor entry point (awq_quantize_groups / awq_quantize_search)
-per input dtype: bf16 takes the streaming kernel, fp16/fp32 the generic one.
+per input dtype and group size: group sizes 32/64/128/256 take the streaming kernel, other
+sizes <= 512 the row-segment kernel, larger ones (and fp64) the generic kernel.
+--compare-generic runs every case a second time with AWQ_NO_ROWGROUP=1 (generic kernel +
+int32 staging + pack passes), interleaved in this process.
 
-  python scripts/generic_bench.py --shape 14336,4096 --dtypes bf16,f16,f32
+  python scripts/generic_bench.py --shape 14336,4096 --dtypes bf16,f16,f32 --group-sizes 100,128
   python scripts/generic_bench.py --shape "1024,4096;4096,4096" --dtypes bf16   (";" separates shapes)
 """
 import argparse
@@ -23,33 +26,40 @@ def main():
     ap.add_argument("--dtypes", default="bf16,f16,f32")
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--search", type=int, default=0, help="clip-search candidates (0 = RTN)")
+    ap.add_argument("--group-sizes", default="128")
+    ap.add_argument("--bits", type=int, default=4)
+    ap.add_argument("--compare-generic", action="store_true")
     args = ap.parse_args()
     from awq_quantizer import _hip
     dev = torch.device("cuda", 0)
     _hip.require_device(dev)
     for shape in args.shape.split(";"):
         for name in args.dtypes.split(","):
-            one(args, _hip, dev, shape, name)
+            for gs in (int(v) for v in args.group_sizes.split(",")):
+                for generic in ((False, True) if args.compare_generic else (False,)):
+                    one(args, _hip, dev, shape, name, gs, generic)
 
 
-def one(args, _hip, dev, shape, name):
+def one(args, _hip, dev, shape, name, gs, generic):
     R, K = (int(v) for v in shape.split(","))
-    G = K // 128
+    G = -(-K // gs)
+    per = 32 // args.bits
     x = (torch.randn(R, K, device=dev) * 0.02).to(DT[name])
-    qw = torch.empty(R, K // 8, dtype=torch.int32, device=dev)
-    qz = torch.empty(R, -(-G // 8), dtype=torch.int32, device=dev)
+    qw = torch.empty(R, -(-K // per), dtype=torch.int32, device=dev)
+    qz = torch.empty(R, -(-G // per), dtype=torch.int32, device=dev)
     sc = torch.empty(R, G, dtype=torch.float16, device=dev)
+    os.environ["AWQ_NO_ROWGROUP"] = "1" if generic else "0"
     stage = {}
-    if args.search or not _hip.ragged_eligible(DT[name], R, K, 128):
+    if args.search or generic or not _hip.packs_directly(DT[name], R, K, gs):
         stage = dict(tensor_q=torch.empty(R * K, dtype=torch.int32, device=dev),
                      zeros=torch.empty(R, G, dtype=torch.int32, device=dev))
 
     def run():
         if args.search:
-            _hip.quantize_search(x, R, K, 128, 4, False, 20, args.search, qweight=qw, qzeros=qz, scales=sc,
+            _hip.quantize_search(x, R, K, gs, args.bits, False, 20, args.search, qweight=qw, qzeros=qz, scales=sc,
                                  **stage)
         else:
-            _hip.quantize_groups(x, R, K, 128, 4, False, qweight=qw, qzeros=qz, scales=sc, **stage)
+            _hip.quantize_groups(x, R, K, gs, args.bits, False, qweight=qw, qzeros=qz, scales=sc, **stage)
     for _ in range(3):
         run()
     a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -58,10 +68,16 @@ def one(args, _hip, dev, shape, name):
         run()
     b.record()
     torch.cuda.synchronize()
+    os.environ.pop("AWQ_NO_ROWGROUP", None)
     us = a.elapsed_time(b) / args.iters * 1e3
     nbytes = x.numel() * x.element_size()
-    print(json.dumps({"dtype": name, "shape": [R, K], "search": args.search, "us": round(us, 1),
-                      "input_GBs": round(nbytes / us / 1e3, 1)}))
+    algo = nbytes + sum(t.numel() * t.element_size() for t in (qw, qz, sc))
+    kernel = ("generic+pack" if stage and not args.search else "search" if args.search else
+              "streaming" if _hip.ragged_eligible(DT[name], R, K, gs) else "row-segment")
+    print(json.dumps({"dtype": name, "shape": [R, K], "group_size": gs, "bits": args.bits, "kernel": kernel,
+                      "search": args.search, "us": round(us, 1), "input_GBs": round(nbytes / us / 1e3, 1),
+                      "algorithmic_GBs": round(algo / us / 1e3, 1), "frac_8TBs": round(algo / us / 1e3 / 8000, 3)}),
+          flush=True)
 
 
 if __name__ == "__main__":

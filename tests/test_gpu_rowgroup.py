@@ -1,0 +1,127 @@
+"""The row-segment kernel (awq_fast.hip awq_rowgroup_kernel): bf16 / fp16 / fp32 with group
+sizes outside {32, 64, 128, 256} (up to 512; fp32 up to 256) and K % 8 != 0 rows — the
+shapes that round 1 sent to the one-wave-per-group generic kernel plus int32 staging and
+pack passes.  Reference arithmetic: awq.py:173-250 per group, awq.py:286-374 for the row
+layout (zero-padded tail group).
+
+Bar: bit-exact vs the oracle for tensor_q / zero_points / fp16 scales (quantize) and for
+the packed words (quantize_packed, which must not need staging buffers here), every dtype,
+4 / 8 bits, sym / asym, special values; a full-size 14336 x 4096 tensor at group size 100
+compared whole.  (The reference's own group-size-100 outputs are pinned separately by the
+golden cases in tests/test_gpu_parity.py::test_golden_case.)"""
+import pytest
+import torch
+
+import golden_io as gio
+from oracle import awq_oracle as orc
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from awq_quantizer import _hip
+    _hip.require_device(torch.device("cuda", 0))
+
+
+def Q(**kw):
+    from awq_quantizer.quantization import AWQQuantizer
+    return AWQQuantizer(device=DEV, logger_level="ERROR", **kw)
+
+
+def rand(shape, seed, scale=1.0, dtype=torch.bfloat16):
+    g = torch.Generator().manual_seed(seed)
+    return (torch.randn(*shape, generator=g) * scale).to(dtype)
+
+
+def specials(x, seed):
+    x = x.float()
+    flat = x.view(-1)
+    g = torch.Generator().manual_seed(seed)
+    idx = torch.randperm(flat.numel(), generator=g)[: max(6, flat.numel() // 400)]
+    kinds = [float("nan"), float("inf"), float("-inf"), 0.0, -0.0, 1e-30]
+    for i, j in enumerate(idx.tolist()):
+        flat[j] = kinds[i % len(kinds)]
+    x[0, : min(40, x.shape[1])] = 0.0           # constant (all-zero) group
+    return x
+
+
+CASES = [  # (dtype, shape, group size) — K % gs != 0 tails, K % 8 != 0, odd and large groups
+    (torch.bfloat16, (37, 1000), 100), (torch.bfloat16, (5, 4099), 100), (torch.bfloat16, (9, 777), 3),
+    (torch.bfloat16, (64, 1536), 96), (torch.bfloat16, (7, 2000), 500), (torch.bfloat16, (3, 1024), 512),
+    (torch.bfloat16, (11, 900), 24), (torch.bfloat16, (13, 4100), 128), (torch.bfloat16, (200, 61), 7),
+    (torch.float16, (37, 1000), 100), (torch.float16, (6, 3001), 200), (torch.float16, (17, 250), 50),
+    (torch.float32, (37, 1000), 100), (torch.float32, (9, 2050), 256), (torch.float32, (4, 777), 37),
+    (torch.bfloat16, (4097,), 100), (torch.bfloat16, (3, 5, 70), 48),
+]
+
+
+def _assert_parity(x, gs, bits, sym):
+    from awq_quantizer import _hip
+    q = Q(bits=bits, group_size=gs, symmetric=sym)
+    ref = orc.quantize(x, bits=bits, group_size=gs, symmetric=sym)
+    res = q.quantize(x)
+    assert torch.equal(res["tensor_q"], ref["tensor_q"])
+    assert torch.equal(res["zero_points"], ref["zero_points"])
+    assert gio.same_bits_nan_eq(res["scales"], ref["scales"])
+    rows = 1 if x.dim() <= 1 else x.shape[0]
+    assert _hip.packs_directly(x.dtype, rows, x.numel() // rows, gs)
+    pk = q.quantize_packed(x)
+    assert torch.equal(pk["qweight"].cpu(), orc.pack_rows(ref["tensor_q"].reshape(rows, -1), bits, q.qmin))
+    assert torch.equal(pk["qzeros"].cpu(), orc.pack_rows(ref["zero_points"], bits, q.qmin))
+    assert gio.same_bits_nan_eq(pk["scales"].cpu(), ref["scales"])
+
+
+@pytest.mark.parametrize("bits,sym", [(4, False), (4, True), (8, False), (8, True)], ids=str)
+@pytest.mark.parametrize("dtype,shape,gs", CASES, ids=str)
+def test_rowgroup_vs_oracle(dtype, shape, gs, bits, sym):
+    _assert_parity(rand(shape, hash((shape, gs, bits, sym)) & 0xFFFF, 0.5, dtype), gs, bits, sym)
+
+
+@pytest.mark.parametrize("bits,sym", [(4, False), (4, True), (8, True)], ids=str)
+@pytest.mark.parametrize("dtype,gs", [(torch.bfloat16, 100), (torch.float16, 100), (torch.float32, 60),
+                                      (torch.bfloat16, 300)], ids=str)
+def test_rowgroup_special_values(dtype, gs, bits, sym):
+    x = specials(rand((24, 1300), 5 + gs, 1.0), 9 + bits).to(dtype)
+    _assert_parity(x, gs, bits, sym)
+
+
+def test_rowgroup_full_size_gs100():
+    """14336 x 4096 (a Llama-3-8B MLP weight) at group size 100: 41 groups per row, the
+    last padded (K % 100 = 96); the whole tensor equals the oracle."""
+    dev = torch.device(DEV, 0)
+    g = torch.Generator(device=dev).manual_seed(100)
+    x = (torch.randn(14336, 4096, generator=g, device=dev) * 0.02).to(torch.bfloat16)
+    q = Q(bits=4, group_size=100, symmetric=False)
+    pk = q.quantize_packed(x)
+    ref = orc.quantize(x.cpu(), bits=4, group_size=100, symmetric=False)
+    assert torch.equal(pk["qweight"].cpu(), orc.pack_rows(ref["tensor_q"], 4, 0))
+    assert torch.equal(pk["qzeros"].cpu(), orc.pack_rows(ref["zero_points"], 4, 0))
+    assert torch.equal(pk["scales"].cpu(), ref["scales"])
+
+
+def test_generic_kernel_still_serves_the_rest():
+    """fp64, groups larger than the row-segment stage, and AWQ_NO_ROWGROUP=1 take the generic
+    kernel (staging buffers required for packed outputs) with the same results."""
+    import os
+    from awq_quantizer import _hip
+    assert not _hip.packs_directly(torch.float64, 4, 1000, 100)
+    assert not _hip.packs_directly(torch.bfloat16, 4, 5000, 1000)
+    assert not _hip.packs_directly(torch.float32, 4, 1000, 500)
+    _assert_parity_generic = lambda x, gs: orc.quantize(x, bits=4, group_size=gs, symmetric=False)
+    for x, gs in ((rand((4, 1000), 1, 1.0, torch.float64), 100), (rand((4, 5000), 2), 1000)):
+        q = Q(bits=4, group_size=gs, symmetric=False)
+        ref = _assert_parity_generic(x, gs)
+        assert torch.equal(q.quantize(x)["tensor_q"], ref["tensor_q"])
+        pk = q.quantize_packed(x)
+        assert torch.equal(pk["qweight"].cpu(), orc.pack_rows(ref["tensor_q"], 4, 0))
+    os.environ["AWQ_NO_ROWGROUP"] = "1"
+    try:
+        x = rand((37, 1000), 3)
+        ref = orc.quantize(x, bits=4, group_size=100, symmetric=False)
+        assert torch.equal(Q(bits=4, group_size=100, symmetric=False).quantize(x)["tensor_q"], ref["tensor_q"])
+    finally:
+        os.environ.pop("AWQ_NO_ROWGROUP", None)

@@ -951,26 +951,9 @@ __device__ __forceinline__ float field1_fast(float x, float r, float z, float s)
 #define AWQ_RG_UNROLL 8
 #endif
 
-// fields of elements [cb, ce) of one group with a positive finite scale: AWQ_RG_UNROLL
-// independent elements per step (their LDS reads in flight together)
-template <typename F, int BITS, bool SYM, bool PLAIN, typename S>
-__device__ __forceinline__ void rg_fields(S* stage, int base, int cb, int ce, const GroupParams& p) {
-    int i = cb;
-    for (; i + AWQ_RG_UNROLL <= ce; i += AWQ_RG_UNROLL) {
-        uint32_t v[AWQ_RG_UNROLL];
-#pragma unroll
-        for (int u = 0; u < AWQ_RG_UNROLL; ++u) v[u] = stage[base + i + u];
-#pragma unroll
-        for (int u = 0; u < AWQ_RG_UNROLL; ++u)
-            stage[base + i + u] = (S)(uint32_t)field1_fast<F, BITS, SYM, PLAIN>(RgSlot<F>::dec(v[u]), p.r, p.z, p.s);
-    }
-    for (; i < ce; ++i)
-        stage[base + i] = (S)(uint32_t)field1_fast<F, BITS, SYM, PLAIN>(RgSlot<F>::dec(stage[base + i]), p.r, p.z, p.s);
-}
-
-// (8 KiB + 16 B of LDS per one-wave workgroup: at most 19 waves per CU)
+// LDS: the segment's stage (dynamic, sized by the launch to the tile: 1.6-8 KiB) + 1.3 KiB
 template <typename F, int BITS, bool SYM>
-__global__ __launch_bounds__(64, 4) void awq_rowgroup_kernel(const void* __restrict__ w, int64_t rows, int64_t K,
+__global__ __launch_bounds__(64, 8) void awq_rowgroup_kernel(const void* __restrict__ w, int64_t rows, int64_t K,
                                                              int64_t L, int P, int GPT, int64_t tiles_per_row,
                                                              int32_t* __restrict__ qweight, int32_t* __restrict__ qzeros,
                                                              uint16_t* __restrict__ scales,
@@ -981,8 +964,10 @@ __global__ __launch_bounds__(64, 4) void awq_rowgroup_kernel(const void* __restr
     constexpr uint32_t MASK = (1u << BITS) - 1u;
     constexpr int PER = 32 / BITS;             // elements (and groups) per packed word
     constexpr uint32_t NANF = (uint32_t)(0u - (uint32_t)QMIN) & MASK;   // field of INT32_MIN - qmin
-    __shared__ __attribute__((aligned(16))) S stage[(kRgStageBytes + 16) / sizeof(S)];   // + the alignment skew
+    extern __shared__ __attribute__((aligned(16))) unsigned char rg_lds[];
+    S* stage = (S*)rg_lds;                              // rg_stage_bytes(): the segment + its alignment skew
     __shared__ uint32_t zst[64];
+    __shared__ float4 prm[64];                          // per group: r, z, s, special
     const int lane = threadIdx.x;
     const int64_t tile = blockIdx.x;
     const int64_t r = tile / tiles_per_row;
@@ -1022,23 +1007,62 @@ __global__ __launch_bounds__(64, 4) void awq_rowgroup_kernel(const void* __restr
     const bool padded = active && glen < L;                    // awq.py:337-339: zeros join the min/max
     int smax = padded ? 0 : INT_MIN;
     uint32_t umax = 0, umin = padded ? 0u : F::kOnes;
-    int i1 = cb;
-    for (; i1 + AWQ_RG_UNROLL <= ce; i1 += AWQ_RG_UNROLL) {   // independent LDS reads in flight
-        uint32_t v[AWQ_RG_UNROLL];
-#pragma unroll
-        for (int u = 0; u < AWQ_RG_UNROLL; ++u) v[u] = stage[base + i1 + u];
-#pragma unroll
-        for (int u = 0; u < AWQ_RG_UNROLL; ++u) {
-            smax = max(smax, SL::sext(v[u]));
-            umax = max(umax, v[u]);
-            umin = min(umin, v[u]);
+    if constexpr (F::kBytes == 2) {
+        // raw 16-bit pairs with packed max/min (v_pk_*_i16/u16: two elements per instruction);
+        // an edge dword holding one foreign element gets a copy of its own element there
+        const int s_lo = base + cb, s_hi = base + ce;
+        if (s_hi > s_lo) {
+            const uint32_t* st32 = (const uint32_t*)stage;
+            const int d_lo = s_lo >> 1, d_hi = (s_hi + 1) >> 1;
+            s2 sm = {(short)(padded ? 0 : -32768), (short)(padded ? 0 : -32768)};
+            us2 um = {0, 0};
+            us2 un = {(unsigned short)(padded ? 0 : 0xFFFF), (unsigned short)(padded ? 0 : 0xFFFF)};
+            auto acc = [&](uint32_t v) {
+                sm = __builtin_elementwise_max(sm, as_s2(v));
+                um = __builtin_elementwise_max(um, as_us2(v));
+                un = __builtin_elementwise_min(un, as_us2(v));
+            };
+            uint32_t first = st32[d_lo];
+            if (s_lo & 1) first = __builtin_amdgcn_perm(first, first, 0x03020302u);   // low half := high
+            if (d_hi - d_lo == 1 && (s_hi & 1)) first = __builtin_amdgcn_perm(first, first, 0x01000100u);
+            acc(first);
+            if (d_hi - d_lo > 1) {
+                int d = d_lo + 1;
+                for (; d + 4 <= d_hi - 1; d += 4) {
+                    const uint32_t v0 = st32[d], v1 = st32[d + 1], v2 = st32[d + 2], v3 = st32[d + 3];
+                    acc(v0);
+                    acc(v1);
+                    acc(v2);
+                    acc(v3);
+                }
+                for (; d < d_hi - 1; ++d) acc(st32[d]);
+                uint32_t last = st32[d_hi - 1];
+                if (s_hi & 1) last = __builtin_amdgcn_perm(last, last, 0x01000100u);        // high half := low
+                acc(last);
+            }
+            smax = max((int)sm.x, (int)sm.y);
+            umax = (uint32_t)max((int)um.x, (int)um.y);
+            umin = (uint32_t)min((int)un.x, (int)un.y);
         }
-    }
-    for (; i1 < ce; ++i1) {
-        const uint32_t v = stage[base + i1];
-        smax = max(smax, SL::sext(v));
-        umax = max(umax, v);
-        umin = min(umin, v);
+    } else {
+        int i1 = cb;
+        for (; i1 + AWQ_RG_UNROLL <= ce; i1 += AWQ_RG_UNROLL) {   // independent LDS reads in flight
+            uint32_t v[AWQ_RG_UNROLL];
+#pragma unroll
+            for (int u = 0; u < AWQ_RG_UNROLL; ++u) v[u] = stage[base + i1 + u];
+#pragma unroll
+            for (int u = 0; u < AWQ_RG_UNROLL; ++u) {
+                smax = max(smax, SL::sext(v[u]));
+                umax = max(umax, v[u]);
+                umin = min(umin, v[u]);
+            }
+        }
+        for (; i1 < ce; ++i1) {
+            const uint32_t v = stage[base + i1];
+            smax = max(smax, SL::sext(v));
+            umax = max(umax, v);
+            umin = min(umin, v);
+        }
     }
     for (int o = 1; o < P; o <<= 1) {                          // the group's P lanes (adjacent)
         smax = max(smax, __shfl_xor(smax, o, 64));
@@ -1050,72 +1074,133 @@ __global__ __launch_bounds__(64, 4) void awq_rowgroup_kernel(const void* __restr
     group_range<F, SYM>(smax, umax, umin, gmn, gmx, gnan);
     const GroupParams p = params_from_range<F, BITS, SYM>(gmn, gmx);
     const bool special = !F::fast(p.r);
+    // wave-uniform: every group of the tile admits the plain quotient (F::plain_ok)
     const bool plain = F::kHasPlain && __builtin_amdgcn_ballot_w64(active && !F::plain_ok(p.s)) == 0;
-    // ---- each element's packed field, in place (NaN elements: the field of INT32_MIN, or in
-    //      parity mode a NaN code that tensor_q turns into INT32_MIN) ----
-    const bool codes = tensor_q != nullptr;
-    if (__builtin_expect(special, 0)) {
-        for (int i = cb; i < ce; ++i) {
-            const float x = SL::dec(stage[base + i]);
-            const float t = F::rn(opaque(x) / p.s);
-            const float u = SYM ? t : F::rn(t + p.z);
-            const float rr = __builtin_rintf(u);
-            uint32_t code = SL::kNan;
-            if (!__builtin_isnan(rr))
-                code = (uint32_t)((int)__builtin_fminf(__builtin_fmaxf(rr, (float)QMIN),
-                                                       (float)(SYM ? (1 << (BITS - 1)) - 1 : (1 << BITS) - 1)) - QMIN);
-            stage[base + i] = (S)(code == SL::kNan && !codes ? NANF : code);
-        }
-    } else if (plain) {
-        rg_fields<F, BITS, SYM, true>(stage, base, cb, ce, p);
-    } else {
-        rg_fields<F, BITS, SYM, false>(stage, base, cb, ce, p);
-    }
     if (active && j == 0) {
         const int64_t gi = r * G + g0 + grp;
         if (scales) scales[gi] = f16_bits(p.s);
         if (zeros) zeros[gi] = __builtin_isnan(p.z) ? INT32_MIN : (int32_t)p.z;
         zst[grp] = __builtin_isnan(p.z) ? NANF : ((uint32_t)((int)p.z - QMIN) & MASK);
+        prm[grp] = (float4){p.r, p.z, p.s, special ? 1.0f : 0.0f};
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    // ---- packed words of the segment (kb is a word boundary: GPT * L % PER == 0) ----
-    if (qweight) {
-        const int64_t wpr = (K + PER - 1) / PER;
-        const int nw = (n_el + PER - 1) / PER;
-        int32_t* dst = qweight + r * wpr + kb / PER;
-        // 16-bit fields of a 16-B aligned segment (skew 0: the row starts on 8 elements, i.e.
-        // K % 8 == 0) read as whole vectors; anything else field by field
-        const bool vec = sizeof(S) == 2 && skew == 0 && !codes && (n_el % PER) == 0;
-        for (int wd = lane; wd < nw; wd += 64) {
-            uint32_t word = 0;
-            if (vec && BITS == 4) {                  // 8 fields (<= 15) in 4 dwords -> 8 nibbles
-                const u4 q = *(const u4*)(stage + 8 * wd);
-                const uint32_t b0 = q.x | (q.x >> 12), b1 = q.y | (q.y >> 12);   // low byte: nibble pair
-                const uint32_t b2 = q.z | (q.z >> 12), b3 = q.w | (q.w >> 12);
-                word = __builtin_amdgcn_perm(b1, b0, 0x0c0c0400u) | (__builtin_amdgcn_perm(b3, b2, 0x0c0c0400u) << 16);
-            } else if (vec) {                        // 4 fields (<= 255) in 2 dwords -> 4 bytes
-                const u2v q = *(const u2v*)(stage + 4 * wd);
-                word = __builtin_amdgcn_perm(q.y, q.x, 0x06040200u);
-            } else {
+    // ---- pass 2: lane = 8 consecutive elements of the segment (one qweight word at 4 bits):
+    //      its groups' parameters from LDS, quantize, pack, store (kb is a word boundary) ----
+    const int nck = (n_el + 7) >> 3;
+    const float invL = 1.0f / (float)L;                   // exact group index: e < 2^13, L <= 512
+    const int64_t wpr = (K + PER - 1) / PER;
+    int32_t* qdst = qweight ? qweight + r * wpr + kb / PER : nullptr;
+    for (int c = lane; c < nck; c += 64) {
+        const int e0c = 8 * c;
+        float x[8];
+        if (skew == 0) {                                  // 16-B aligned chunk (K % 8 == 0 rows)
+            const u4 v0 = *(const u4*)(stage + e0c);
+            if constexpr (F::kBytes == 2) {
 #pragma unroll
-                for (int i = 0; i < PER; ++i) {
-                    const int e = wd * PER + i;
-                    if (e < n_el) {
-                        const uint32_t code = stage[skew + e];
-                        word |= ((code == SL::kNan ? NANF : code) & MASK) << (BITS * i);
-                    }
+                for (int i = 0; i < 4; ++i) {
+                    const uint32_t wd = v0[i];
+                    x[2 * i] = F::lo(wd);
+                    x[2 * i + 1] = F::hi(wd);
+                }
+            } else {
+                const u4 v1 = *(const u4*)(stage + e0c + 4);
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    x[i] = __uint_as_float(v0[i]);
+                    x[4 + i] = __uint_as_float(v1[i]);
                 }
             }
-            dst[wd] = (int32_t)word;
+        } else {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) x[i] = SL::dec(stage[skew + min(e0c + i, n_el - 1)]);
         }
-    }
-    if (tensor_q) {
-        int32_t* dst = tensor_q + r * K + kb;
-        for (int e = lane; e < n_el; e += 64) {
-            const uint32_t code = stage[skew + e];
-            dst[e] = code == SL::kNan ? INT32_MIN : (int32_t)code + QMIN;
+        // parameters per element: the chunk meets at most two groups when L >= 8
+        float rr[8], zz[8], ss[8];
+        bool spec = false;
+        if (L >= 8) {
+            const int gA = (int)(((float)e0c + 0.5f) * invL);
+            const int bnd = (gA + 1) * (int)L - e0c;      // first element of the next group
+            const float4 pA = prm[gA], pB = prm[min(gA + 1, ng - 1)];
+            spec = pA.w != 0.0f || (bnd < 8 && pB.w != 0.0f);
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const bool a = i < bnd;
+                rr[i] = a ? pA.x : pB.x;
+                zz[i] = a ? pA.y : pB.y;
+                ss[i] = a ? pA.z : pB.z;
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const int gi = min((int)(((float)(e0c + i) + 0.5f) * invL), ng - 1);
+                const float4 pi = prm[gi];
+                spec |= pi.w != 0.0f;
+                rr[i] = pi.x;
+                zz[i] = pi.y;
+                ss[i] = pi.z;
+            }
+        }
+        int32_t qv[8];                                    // q (reference value), INT32_MIN for NaN
+        uint32_t word0 = 0, word1 = 0;
+        const bool tail = e0c + 8 > n_el;                 // the row's last, partial chunk
+        if (__builtin_expect(!spec, 1)) {
+            float q[8];
+#pragma unroll
+            for (int i = 0; i < 8; ++i)
+                q[i] = plain ? field1_fast<F, BITS, SYM, true>(x[i], rr[i], zz[i], ss[i])
+                             : field1_fast<F, BITS, SYM, false>(x[i], rr[i], zz[i], ss[i]);
+            if (__builtin_expect(tail, 0)) {
+#pragma unroll
+                for (int i = 0; i < 8; ++i)
+                    if (e0c + i >= n_el) q[i] = 0.0f;     // past the row end: zero fields
+            }
+            if (tensor_q) {
+#pragma unroll
+                for (int i = 0; i < 8; ++i) qv[i] = (int32_t)q[i] + QMIN;
+            }
+            if (BITS == 4) {
+#pragma unroll
+                for (int i = 0; i < 4; ++i)   // nibble pair as one exact float in [0, 255] -> byte i
+                    word0 = __builtin_amdgcn_cvt_pk_u8_f32(__builtin_fmaf(q[2 * i + 1], 16.0f, q[2 * i]), i, word0);
+            } else {
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    word0 = __builtin_amdgcn_cvt_pk_u8_f32(q[i], i, word0);
+                    word1 = __builtin_amdgcn_cvt_pk_u8_f32(q[4 + i], i, word1);
+                }
+            }
+        } else {                                          // a group with scale 0 / inf / NaN: IEEE division
+            constexpr int QMAX = SYM ? (1 << (BITS - 1)) - 1 : (1 << BITS) - 1;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const float t = F::rn(opaque(x[i]) / ss[i]);
+                const float u = SYM ? t : F::rn(t + zz[i]);
+                const float rq = __builtin_rintf(u);
+                int32_t qi = __builtin_isnan(rq) ? INT32_MIN
+                                                 : (int32_t)__builtin_fminf(__builtin_fmaxf(rq, (float)QMIN), (float)QMAX);
+                uint32_t f = ((uint32_t)qi - (uint32_t)QMIN) & MASK;
+                if (e0c + i >= n_el) { f = 0; qi = QMIN; }
+                qv[i] = qi;
+                if (BITS == 4) word0 |= f << (4 * i);
+                else if (i < 4) word0 |= f << (8 * i);
+                else word1 |= f << (8 * (i - 4));
+            }
+        }
+        if (qdst) {
+            if (BITS == 4) {
+                qdst[c] = (int32_t)word0;
+            } else {
+                qdst[2 * c] = (int32_t)word0;
+                if (e0c + 4 < n_el) qdst[2 * c + 1] = (int32_t)word1;
+            }
+        }
+        if (tensor_q) {
+            int32_t* tq = tensor_q + r * K + kb + e0c;
+#pragma unroll
+            for (int i = 0; i < 8; ++i)
+                if (e0c + i < n_el) tq[i] = qv[i];
         }
     }
     if (qzeros) {                                 // g0 is a word boundary: GPT % PER == 0
@@ -1317,20 +1402,30 @@ hipError_t launch_fast(const awq_tensor_desc* descs_dev, const int32_t* block_te
     return hipPeekAtLastError();
 }
 
-// Row-segment tiles of awq_rowgroup_kernel: groups per tile (8..64, a power of two: tile
-// boundaries on packed-word boundaries) with the best lane use G / (ceil(G / GPT) * GPT),
-// larger on ties; 0 if the shape does not fit the LDS stage.
+// Row-segment tiles of awq_rowgroup_kernel: groups per tile GPT (8..64, a power of two: tile
+// boundaries on packed-word boundaries) minimising a per-row cost fitted to measurements
+// (profiles/round2/r2_rowgroup/r2r_*: 14336 x 4096, group sizes 48 / 100, GPT 8..32):
+// tiles x (fixed wave cost 8 + 0.6 per element of a lane's pass-1 chunk C = L / (64 / GPT)
+// + 2.3 per 512-element pass-2 sweep); 0 if the shape does not fit the LDS stage.
 int rowgroup_gpt(int dtype, int64_t K, int64_t L) {
     if (dtype != AWQ_DTYPE_BF16 && dtype != AWQ_DTYPE_F16 && dtype != AWQ_DTYPE_F32) return 0;
+    if (const char* e = getenv("AWQ_RG_GPT")) {        // tuning override (scripts/generic_bench.py)
+        const int v = atoi(e);
+        const int64_t es = dtype == AWQ_DTYPE_F32 ? 4 : 2;
+        if ((v == 8 || v == 16 || v == 32 || v == 64) && v * L * es <= kRgStageBytes) return v;
+    }
     const int64_t slots = kRgStageBytes / (dtype == AWQ_DTYPE_F32 ? 4 : 2);   // (+ 16 B of skew slack)
     if (L <= 0 || K <= 0) return 0;
     const int64_t G = (K + L - 1) / L;
     int best = 0;
-    double best_use = -1.0;
+    double best_cost = 0.0;
     for (int gpt = 8; gpt <= 64; gpt *= 2) {
         if (gpt * L > slots) break;
-        const double use = (double)G / (double)(((G + gpt - 1) / gpt) * gpt);
-        if (use >= best_use) { best_use = use; best = gpt; }
+        const int64_t tiles = (G + gpt - 1) / gpt;
+        const int64_t C = (L + (64 / gpt) - 1) / (64 / gpt);
+        const int64_t el = min((int64_t)gpt, G) * L;                  // elements of a full tile
+        const double cost = (double)tiles * (8.0 + 0.6 * (double)C + 2.3 * (double)((el + 511) / 512));
+        if (best == 0 || cost < best_cost) { best_cost = cost; best = gpt; }
     }
     return best;
 }
@@ -1344,8 +1439,11 @@ hipError_t launch_rowgroup(const void* w, int dtype, int64_t rows, int64_t K, in
     const int64_t tpr = (G + gpt - 1) / gpt;
     const int P = 64 / gpt;
     const dim3 grid((unsigned)(rows * tpr)), block(64);
-#define AWQ_RG(Fm, B, S)                                                                                         \
-    hipLaunchKernelGGL((awq_rowgroup_kernel<Fm, B, S>), grid, block, 0, stream, w, rows, K, L, P, gpt, tpr, qweight, \
+    // stage: the tile's elements rounded up to 16 B, + the up-to-16-B alignment skew and the
+    // last 8-element vector read past the segment end
+    const size_t lds = ((size_t)gpt * L * (dtype == AWQ_DTYPE_F32 ? 4 : 2) + 15) / 16 * 16 + 48;
+#define AWQ_RG(Fm, B, S)                                                                                           \
+    hipLaunchKernelGGL((awq_rowgroup_kernel<Fm, B, S>), grid, block, lds, stream, w, rows, K, L, P, gpt, tpr, qweight, \
                        qzeros, scales, tensor_q, zeros)
 #define AWQ_RG_FMT(Fm)                                                     \
     switch ((bits == 8 ? 2 : 0) + (symmetric ? 1 : 0)) {                  \

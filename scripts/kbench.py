@@ -46,6 +46,8 @@ def main():
     ap.add_argument("--parity", action="store_true")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "f16", "f32"])
     ap.add_argument("--group-size", type=int, default=128)
+    ap.add_argument("--arena", action="store_true",
+                    help="inputs as views of ONE device buffer per replica instead of one allocation per tensor")
     args = ap.parse_args()
     from awq_quantizer import _hip
     from awq_quantizer.quantization.batch import PackedBatch
@@ -91,10 +93,21 @@ def main():
         for r in range(reps):
             g = torch.Generator(device=dev)
             inputs = {}
+            dt = {"f16": torch.float16, "f32": torch.float32}.get(args.dtype, torch.bfloat16)
+            arena, off = None, 0
+            if args.arena:
+                arena = torch.empty(sum(-(-int(torch.Size(s).numel()) // 8) * 8 for s in shapes), dtype=dt, device=dev)
             for i, s in enumerate(shapes):
                 g.manual_seed(r * 1000 + i)
-                inputs[f"t{i}"] = (torch.randn(*s, generator=g, device=dev) * 0.02).to(
-                    {"f16": torch.float16, "f32": torch.float32}.get(args.dtype, torch.bfloat16))
+                n = int(torch.Size(s).numel())
+                t = arena[off:off + n].view(s) if arena is not None else torch.empty(s, dtype=dt, device=dev)
+                off += -(-n // 8) * 8
+                flat = t.view(s[0], -1) if len(s) > 1 else t.view(1, -1)
+                step = max(1, (1 << 28) // flat.shape[1])
+                for r0 in range(0, flat.shape[0], step):
+                    blk = flat[r0:r0 + step]
+                    blk.copy_(torch.randn(blk.shape, generator=g, device=dev) * 0.02)
+                inputs[f"t{i}"] = t
             bl.append(PackedBatch(inputs, bits=args.bits, symmetric=args.symmetric, parity=args.parity,
                                   group_size=args.group_size))
         batches[sname] = bl

@@ -52,7 +52,10 @@ bool fast_eligible(int dtype, int64_t rows, int64_t K, int64_t group_size) {
 bool rowgroup_shape(int dtype, int64_t rows, int64_t K, int64_t group_size) {
     if (const char* e = getenv("AWQ_NO_ROWGROUP"))   // A/B against the generic kernel (scripts/generic_bench.py)
         if (e[0] == '1') return false;
-    return awq::rowgroup_gpt(dtype, K, group_size) > 0 && rows > 0 && rows * K < ((int64_t)1 << 40);
+    const int gpt = awq::rowgroup_gpt(dtype, K, group_size);
+    if (gpt == 0 || rows <= 0 || rows * K >= ((int64_t)1 << 40)) return false;
+    const int64_t tiles = rows * (((K + group_size - 1) / group_size + gpt - 1) / gpt);
+    return tiles < ((int64_t)1 << 31);                  // one 32-bit grid dimension
 }
 
 bool rowgroup_ok(int dtype, int64_t rows, int64_t K, int64_t group_size, const void* w, const void* qweight,

@@ -954,7 +954,8 @@ __device__ __forceinline__ float field1_fast(float x, float r, float z, float s)
 // LDS: the segment's stage (dynamic, sized by the launch to the tile: 1.6-8 KiB) + 1.3 KiB
 template <typename F, int BITS, bool SYM>
 __global__ __launch_bounds__(64, 8) void awq_rowgroup_kernel(const void* __restrict__ w, int64_t rows, int64_t K,
-                                                             int64_t L, int P, int GPT, int64_t tiles_per_row,
+                                                             int64_t L, int lgP, int GPT, uint32_t tiles_per_row,
+                                                             int64_t G, int C,
                                                              int32_t* __restrict__ qweight, int32_t* __restrict__ qzeros,
                                                              uint16_t* __restrict__ scales,
                                                              int32_t* __restrict__ tensor_q, int32_t* __restrict__ zeros) {
@@ -969,10 +970,13 @@ __global__ __launch_bounds__(64, 8) void awq_rowgroup_kernel(const void* __restr
     __shared__ uint32_t zst[64];
     __shared__ float4 prm[64];                          // per group: r, z, s, special
     const int lane = threadIdx.x;
-    const int64_t tile = blockIdx.x;
-    const int64_t r = tile / tiles_per_row;
-    const int64_t G = (K + L - 1) / L;
-    const int64_t g0 = (tile - r * tiles_per_row) * GPT;
+    // (host-side G, C, log2 P and a 32-bit tile split: 64-bit divisions per wave on the
+    //  CU's shared scalar unit were a visible part of the per-tile cost)
+    const uint32_t tile = blockIdx.x;
+    const uint32_t r32 = tile / tiles_per_row;
+    const int64_t r = r32;
+    const int64_t g0 = (int64_t)(tile - r32 * tiles_per_row) * GPT;
+    const int P = 1 << lgP;
     const int ng = (int)min((int64_t)GPT, G - g0);
     const int64_t kb = g0 * L, ke = min((g0 + ng) * L, K);     // the row segment [kb, ke)
     const int n_el = (int)(ke - kb);
@@ -998,10 +1002,9 @@ __global__ __launch_bounds__(64, 8) void awq_rowgroup_kernel(const void* __restr
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     // ---- this lane's chunk of its group ----
-    const int grp = lane / P, j = lane - grp * P;
+    const int grp = lane >> lgP, j = lane & (P - 1);
     const bool active = grp < ng;
     const int glen = active ? (int)min(L, K - (g0 + grp) * L) : 0;   // elements in the row (tail: fewer)
-    const int C = (int)((L + P - 1) / P);
     const int cb = min(j * C, glen), ce = min(cb + C, glen);
     const int base = skew + grp * (int)L;
     const bool padded = active && glen < L;                    // awq.py:337-339: zeros join the min/max
@@ -1438,13 +1441,15 @@ hipError_t launch_rowgroup(const void* w, int dtype, int64_t rows, int64_t K, in
     const int64_t G = (K + L - 1) / L;
     const int64_t tpr = (G + gpt - 1) / gpt;
     const int P = 64 / gpt;
+    const int lgP = __builtin_ctz((unsigned)P);
+    const int C = (int)((L + P - 1) / P);
     const dim3 grid((unsigned)(rows * tpr)), block(64);
     // stage: the tile's elements rounded up to 16 B, + the up-to-16-B alignment skew and the
     // last 8-element vector read past the segment end
     const size_t lds = ((size_t)gpt * L * (dtype == AWQ_DTYPE_F32 ? 4 : 2) + 15) / 16 * 16 + 48;
 #define AWQ_RG(Fm, B, S)                                                                                           \
-    hipLaunchKernelGGL((awq_rowgroup_kernel<Fm, B, S>), grid, block, lds, stream, w, rows, K, L, P, gpt, tpr, qweight, \
-                       qzeros, scales, tensor_q, zeros)
+    hipLaunchKernelGGL((awq_rowgroup_kernel<Fm, B, S>), grid, block, lds, stream, w, rows, K, L, lgP, gpt,           \
+                       (uint32_t)tpr, G, C, qweight, qzeros, scales, tensor_q, zeros)
 #define AWQ_RG_FMT(Fm)                                                     \
     switch ((bits == 8 ? 2 : 0) + (symmetric ? 1 : 0)) {                  \
     case 0: AWQ_RG(Fm, 4, false); break;                                   \

@@ -15,7 +15,7 @@ import torch
 
 LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib")
 LIB_PATH = os.path.join(LIB_DIR, "libawq_hip.so")
-ABI_VERSION = 8
+ABI_VERSION = 9
 
 AWQ_DTYPE = {torch.bfloat16: 0, torch.float16: 1, torch.float32: 2, torch.float64: 3}
 
@@ -38,8 +38,8 @@ SIGNATURES = {
     "awq_abi_version": (_I32, []),
     "awq_last_error": (ctypes.c_char_p, []),
     "awq_device_check": (_I32, [ctypes.c_char_p, _I32]),
-    "awq_quantize_groups": (_I32, [_P, _I32, _I64, _I64, _I64, _I32, _I32, _P, _P, _P, _P, _P, _P]),
-    "awq_quantize_search": (_I32, [_P, _I32, _I64, _I64, _I64, _I32, _I32, _I32, _I32, _P, _P, _P, _P, _P, _P]),
+    "awq_quantize_groups": (_I32, [_P, _I32, _I64, _I64, _I32, _I32, _I32, _P, _P, _P, _P, _P, _P]),
+    "awq_quantize_search": (_I32, [_P, _I32, _I64, _I64, _I32, _I32, _I32, _I32, _I32, _P, _P, _P, _P, _P, _P]),
     "awq_group_params": (_I32, [_P, _I32, _I64, _I64, _I64, _I32, _I32, _P, _P, _P]),
     "awq_apply_params": (_I32, [_P, _I32, _I64, _I64, _I64, _P, _P, _I32, _I32, _I32, _P, _P]),
     "awq_packs_directly": (_I32, [_I32, _I64, _I64, _I64]),

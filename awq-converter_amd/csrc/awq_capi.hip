@@ -98,10 +98,11 @@ int awq_ragged_eligible(int dtype, int64_t rows, int64_t K, int64_t group_size) 
     return fast_eligible(dtype, rows, K, group_size) ? 1 : 0;
 }
 
-int awq_quantize_groups(const void* w, int dtype, int64_t rows, int64_t K, int64_t group_size,
+int awq_quantize_groups(const void* w, int dtype, int64_t rows, int64_t K, int32_t group_size32,
                         int bits, int symmetric, int32_t* qweight, int32_t* qzeros,
                         uint16_t* scales, int32_t* tensor_q, int32_t* zeros, void* stream) {
     g_err.clear();
+    const int64_t group_size = group_size32;   // (int32 at the boundary: SURVEY.md §8(b))
     if (int rc = check_common(rows, K, group_size, bits)) return rc;
     if (dtype < AWQ_DTYPE_BF16 || dtype > AWQ_DTYPE_F64) return fail(AWQ_EINVAL, "unknown dtype code %d", dtype);
     if (!qweight && !qzeros && !scales && !tensor_q && !zeros) return fail(AWQ_EINVAL, "no output requested");
@@ -139,10 +140,11 @@ int awq_quantize_groups(const void* w, int dtype, int64_t rows, int64_t K, int64
     return AWQ_OK;
 }
 
-int awq_quantize_search(const void* w, int dtype, int64_t rows, int64_t K, int64_t group_size, int bits,
+int awq_quantize_search(const void* w, int dtype, int64_t rows, int64_t K, int32_t group_size32, int bits,
                         int symmetric, int n_grid, int n_candidates, int32_t* qweight, int32_t* qzeros,
                         uint16_t* scales, int32_t* tensor_q, int32_t* zeros, void* stream) {
     g_err.clear();
+    const int64_t group_size = group_size32;
     if (int rc = check_common(rows, K, group_size, bits)) return rc;
     if (dtype < AWQ_DTYPE_BF16 || dtype > AWQ_DTYPE_F64) return fail(AWQ_EINVAL, "unknown dtype code %d", dtype);
     if (n_grid < 1 || n_candidates < 1 || n_candidates > n_grid)

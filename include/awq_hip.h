@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define AWQ_HIP_ABI_VERSION 8
+#define AWQ_HIP_ABI_VERSION 9
 
 /* dtype codes of the input weights (torch dtypes the reference accepts, awq.py:397) */
 enum { AWQ_DTYPE_BF16 = 0, AWQ_DTYPE_F16 = 1, AWQ_DTYPE_F32 = 2, AWQ_DTYPE_F64 = 3 };
@@ -84,7 +84,7 @@ int awq_device_check(char* arch, int len);
  *     kernel (packed outputs written directly);
  *   everything else (fp64, larger groups): the generic kernel, whose packed outputs need
  *     tensor_q / zeros as staging buffers (awq_packs_directly() == 0). */
-int awq_quantize_groups(const void* w, int dtype, int64_t rows, int64_t K, int64_t group_size,
+int awq_quantize_groups(const void* w, int dtype, int64_t rows, int64_t K, int32_t group_size,
                         int bits, int symmetric, int32_t* qweight, int32_t* qzeros,
                         uint16_t* scales, int32_t* tensor_q, int32_t* zeros, void* stream);
 
@@ -101,7 +101,7 @@ int awq_quantize_groups(const void* w, int dtype, int64_t rows, int64_t K, int64
  * order, then a pairwise tree over 64 chunk slots, adjacent pairs first (empty slots = 0):
  * group_size <= 512.
  * Packed outputs need tensor_q / zeros as staging buffers. */
-int awq_quantize_search(const void* w, int dtype, int64_t rows, int64_t K, int64_t group_size, int bits,
+int awq_quantize_search(const void* w, int dtype, int64_t rows, int64_t K, int32_t group_size, int bits,
                         int symmetric, int n_grid, int n_candidates, int32_t* qweight, int32_t* qzeros,
                         uint16_t* scales, int32_t* tensor_q, int32_t* zeros, void* stream);
 

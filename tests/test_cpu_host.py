@@ -27,7 +27,7 @@ def test_library_exports_every_declared_symbol():
     for s in syms:
         assert hasattr(lib, s), s
     assert set(syms) == set(_hip.SIGNATURES), "python binding out of sync with include/awq_hip.h"
-    assert lib.awq_abi_version() == _hip.ABI_VERSION == 8
+    assert lib.awq_abi_version() == _hip.ABI_VERSION == 9
 
 
 def test_library_is_gfx950_code_object():

@@ -198,8 +198,14 @@ __device__ __forceinline__ float grp_sum(float v, int lpg) {
 }
 
 
-constexpr int kRowBlock = 256;     // rows per canonical fp64 column-sum block
-constexpr int kGroupBlock = 1024;  // groups per canonical fp64 loss block
+// Canonical fp64 summation orders (oracle/awq_oracle.c ACT_*; include/awq_hip.h): two or
+// three levels, so that a workgroup runs many short dependent chains instead of a few long
+// ones (every level is still a fixed, ascending order: the bits do not depend on the launch)
+constexpr int kRowBlock = 256;       // rows per column-sum block
+constexpr int kRowSub = 32;          // rows per sub-block (a block = its sub-blocks' sums)
+constexpr int kGroupBlock = 1024;    // groups per loss block
+constexpr int kGroupSub = 64;        // groups per sub-block of a loss block
+constexpr int kSuperBlocks = 32;     // loss blocks per super-block of a candidate's total
 
 // 8 consecutive elements as fp32 (compute type of bf16 / fp16 / fp32 inputs)
 template <int DT>
@@ -226,13 +232,15 @@ __device__ __forceinline__ void load8(const void* base, int64_t i, float (&v)[8]
     }
 }
 
-// ---- column sums (canonical: rows ascending inside a 256-row block, fp64) ----
+// ---- column sums (canonical, fp64: rows ascending inside a 32-row sub-block, the
+//      sub-blocks ascending inside a 256-row block) ----
 // MODE 0, activations x [T, K]:  part0[b][k] = sum |x|,  part1[b][k] = sum x*x
 // MODE 1, weights w [R, K]:      part0[b][k] = sum fp32(|w| / fp32(gmax[r, k/L] + 1e-6f))
-// One lane per column and block; the sum is a dependent fp64 chain, so the loads go out
-// kColBatch rows ahead of it (a lane's loads are independent of its sums): the chain
+// One lane per column and block; the sums are dependent fp64 chains, so the loads go out
+// kColBatch rows ahead of them (a lane's loads are independent of its sums): the chain
 // order is unchanged, only the memory latency overlaps.
 constexpr int kColBatch = 16;
+static_assert(kRowSub % kColBatch == 0, "a load batch stays inside one sub-block");
 
 template <int DT, int MODE>
 __global__ __launch_bounds__(256) void colsum_kernel(const void* __restrict__ src, int64_t rows, int64_t K,
@@ -246,7 +254,7 @@ __global__ __launch_bounds__(256) void colsum_kernel(const void* __restrict__ sr
     const int64_t r1 = (r0 + kRowBlock < rows) ? r0 + kRowBlock : rows;
     const typename T::S* p = (const typename T::S*)src;
     const int64_t G = K / L, gk = k / L;
-    double s0 = 0.0, s1 = 0.0;
+    double s0 = 0.0, s1 = 0.0, u0 = 0.0, u1 = 0.0;
     for (int64_t r = r0; r < r1; r += kColBatch) {
         float v[kColBatch], den[kColBatch];
 #pragma unroll
@@ -260,12 +268,18 @@ __global__ __launch_bounds__(256) void colsum_kernel(const void* __restrict__ sr
             if (r + j < r1) {
                 if (MODE == 0) {
                     const double d = (double)v[j];     // |x| and x*x are exact in fp64
-                    s0 += __builtin_fabs(d);
-                    s1 += d * d;
+                    u0 += __builtin_fabs(d);
+                    u1 += d * d;
                 } else {
-                    s0 += (double)(__builtin_fabsf(v[j]) / den[j]);
+                    u0 += (double)(__builtin_fabsf(v[j]) / den[j]);
                 }
             }
+        }
+        if ((r + kColBatch - r0) % kRowSub == 0 || r + kColBatch >= r1) {   // a sub-block ends
+            s0 += u0;
+            s1 += u1;
+            u0 = 0.0;
+            u1 = 0.0;
         }
     }
     part0[b * K + k] = s0;
@@ -335,15 +349,20 @@ __global__ __launch_bounds__(256) void colsum_tile_kernel(const void* __restrict
         *(float4*)&sv[rr][8 * oc + 4] = make_float4(v[it][4], v[it][5], v[it][6], v[it][7]);
     }
     __syncthreads();
-    if (tid >= kColTile || kt + tid >= K) return;
+    // every thread: one column of one 32-row sub-block (rows ascending, fp64); then kColTile
+    // lanes add the block's sub-block sums in order
+    constexpr int NSUB = kRowBlock / kRowSub;
+    static_assert(NSUB * kColTile == 256, "one sub-block chain per thread");
+    const int col = tid % kColTile, sub = tid / kColTile;
+    const int ra = sub * kRowSub, rb = min(ra + kRowSub, nr);
     double s0 = 0.0, s1 = 0.0;
-    for (int r = 0; r < nr; r += 16) {
+    for (int r = ra; r < rb; r += 16) {
         float t[16];
 #pragma unroll
-        for (int j = 0; j < 16; ++j) t[j] = sv[(r + j < nr) ? r + j : nr - 1][tid];
+        for (int j = 0; j < 16; ++j) t[j] = sv[(r + j < rb) ? r + j : rb - 1][col];
 #pragma unroll
         for (int j = 0; j < 16; ++j) {
-            if (r + j < nr) {
+            if (r + j < rb) {
                 const double d = (double)t[j];
                 if (MODE == 0) {
                     s0 += __builtin_fabs(d);
@@ -354,8 +373,18 @@ __global__ __launch_bounds__(256) void colsum_tile_kernel(const void* __restrict
             }
         }
     }
-    part0[b * K + kt + tid] = s0;
-    if (MODE == 0) part1[b * K + kt + tid] = s1;
+    __shared__ double ss0[NSUB][kColTile], ss1[NSUB][kColTile];
+    ss0[sub][col] = s0;
+    if (MODE == 0) ss1[sub][col] = s1;
+    __syncthreads();
+    if (tid >= kColTile || kt + tid >= K) return;
+    double a0 = 0.0, a1 = 0.0;
+    for (int u = 0; u < NSUB && u * kRowSub < nr; ++u) {   // non-empty sub-blocks, ascending
+        a0 += ss0[u][tid];
+        if (MODE == 0) a1 += ss1[u][tid];
+    }
+    part0[b * K + kt + tid] = a0;
+    if (MODE == 0) part1[b * K + kt + tid] = a1;
 }
 
 // Lane layout shared by the group kernels: LPG = L / 8 lanes per group (8 consecutive
@@ -583,13 +612,23 @@ __global__ __launch_bounds__(256) void act_loss_kernel(const void* __restrict__ 
     }
 }
 
-// work[i * nblk + b] = sum of part[i][b*1024 .. +1024) ascending, fp64.  A workgroup takes
-// kLossChains consecutive (i, b) chains: their floats come in through LDS with coalesced
-// loads (all in flight at once), then one lane per chain runs its fp64 chain from LDS.
-constexpr int kLossChains = 16;   // r92: 8 or 4 chains per workgroup were 5-30 % slower
+// work[i * nblk + b] = block b of candidate i's losses, fp64: 64-group sub-blocks summed
+// ascending, then the block's 16 sub-block sums ascending.  A workgroup takes kLossChains
+// consecutive (i, b) blocks: their floats come in through LDS with coalesced loads (all in
+// flight at once), every thread runs one sub-block chain from LDS, kLossChains lanes add the
+// sub-block sums.  LDS layout: block c's sub-block u at c * 1024 + 64 u, its 64 floats
+// rotated by (u + 16 c) mod 64 so that the 64 lanes of a wave (4 blocks x 16 sub-blocks)
+// read 64 distinct banks at every step of their chains.
+constexpr int kLossChains = 16;   // r92: 8 or 4 blocks per workgroup were 5-30 % slower
+constexpr int kLossSubs = kGroupBlock / kGroupSub;
+static_assert(kLossChains * kLossSubs == 256, "one sub-block chain per thread");
+__device__ __forceinline__ int loss_lds_index(int c, int g) {
+    return c * kGroupBlock + (g & ~(kGroupSub - 1)) + ((g + (g >> 6) + 16 * c) & (kGroupSub - 1));
+}
 __global__ __launch_bounds__(256) void loss_block_kernel(const float* __restrict__ part, int n_grid, int64_t stride,
                                                          int64_t nblk, double* __restrict__ work) {
-    __shared__ __attribute__((aligned(16))) float sp[kLossChains][kGroupBlock];
+    __shared__ __attribute__((aligned(16))) float sp[kLossChains * kGroupBlock];
+    __shared__ double su[kLossChains][kLossSubs];
     const int tid = threadIdx.x;
     const int64_t c0 = (int64_t)blockIdx.x * kLossChains;
     const int64_t nch = (int64_t)n_grid * nblk;
@@ -610,70 +649,81 @@ __global__ __launch_bounds__(256) void loss_block_kernel(const float* __restrict
 #pragma unroll
     for (int c = 0; c < kLossChains; ++c)
 #pragma unroll
-        for (int e = 0; e < NE; ++e) sp[c][e * 256 + tid] = t[c][e];
+        for (int e = 0; e < NE; ++e) sp[loss_lds_index(c, e * 256 + tid)] = t[c][e];
+    __syncthreads();
+    {
+        const int c = tid / kLossSubs, u = tid % kLossSubs;
+        const int64_t idx = c0 + c;
+        int n = 0;
+        if (idx < nch) {
+            const int64_t b = idx % nblk, g0 = b * kGroupBlock;
+            n = (int)((g0 + kGroupBlock < stride) ? kGroupBlock : stride - g0);
+        }
+        const int ga = u * kGroupSub, gb = min(ga + kGroupSub, n);
+        const float* q = sp + c * kGroupBlock + ga;
+        const int rot = (ga / kGroupSub + 16 * c) & (kGroupSub - 1);   // (g >> 6) == u here
+        double s = 0.0;
+        for (int g = ga; g < gb; g += 16) {               // 16 LDS values ahead of the chain
+            float v[16];
+#pragma unroll
+            for (int j = 0; j < 16; ++j) v[j] = q[(g - ga + j + rot) & (kGroupSub - 1)];
+#pragma unroll
+            for (int j = 0; j < 16; ++j)
+                if (g + j < gb) s += (double)v[j];
+        }
+        su[c][u] = s;
+    }
     __syncthreads();
     const int64_t idx = c0 + tid;
     if (tid >= kLossChains || idx >= nch) return;
-    const int64_t i = idx / nblk, b = idx - i * nblk;
-    const int64_t g0 = b * kGroupBlock;
+    const int64_t b = idx % nblk, g0 = b * kGroupBlock;
     const int n = (int)((g0 + kGroupBlock < stride) ? kGroupBlock : stride - g0);
-    const float* q = sp[tid];
     double s = 0.0;
-    for (int g = 0; g < n; g += 16) {                    // 16 LDS values ahead of the chain
-        float t[16];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) *(float4*)&t[4 * j] = *(const float4*)&q[g + 4 * j];
-#pragma unroll
-        for (int j = 0; j < 16; ++j)
-            if (g + j < n) s += (double)t[j];
-    }
+    for (int u = 0; u < kLossSubs && u * kGroupSub < n; ++u) s += su[tid][u];   // non-empty, ascending
     work[idx] = s;
 }
 
-// losses[i] = blocks ascending (fp64); best = first minimum (NaN never wins; all NaN -> 0);
-// s_best = table[best].  The [n_grid, nblk] block sums come through LDS in column chunks
-// (coalesced loads), each candidate's chain continuing over the chunks in block order.
+// losses[i] = the candidate's blocks summed in 32-block super-blocks (blocks ascending),
+// then the super-block sums ascending (fp64); best = first minimum (NaN never wins; all NaN
+// -> 0); s_best = table[best].  Candidates go in batches whose super-block sums fit LDS:
+// every thread runs (candidate, super-block) chains of <= 32 block sums from global memory
+// (loads first, then the adds), then one lane per candidate adds its super-block sums.
+constexpr int kSelectLds = 6144;   // fp64 super-block sums per batch (48 KiB)
 __global__ __launch_bounds__(256) void select_kernel(const double* __restrict__ work, int n_grid, int64_t nblk,
                                                      const float* __restrict__ table, int64_t K,
                                                      double* __restrict__ losses, int32_t* __restrict__ best,
                                                      float* __restrict__ s_best) {
-    constexpr int kChunkElems = 4096;                  // 32 KiB of fp64
-    __shared__ double sw[kChunkElems];
-    __shared__ double sl[256];
+    __shared__ double sw[kSelectLds];
+    __shared__ double sl[AWQ_ACT_MAX_GRID];
     __shared__ int sb;
     const int tid = threadIdx.x;
-    const int64_t cb = (kChunkElems / n_grid < nblk) ? kChunkElems / n_grid : nblk;   // blocks per chunk
-    double s = 0.0;
-    for (int64_t b0 = 0; b0 < nblk; b0 += cb) {
-        const int64_t nb = (b0 + cb < nblk) ? cb : nblk - b0;
-        __syncthreads();
-        double t[kChunkElems / 256];                   // all loads in flight, then the stores
-        const int64_t ne = (int64_t)n_grid * nb;
+    const int nsb = (int)((nblk + kSuperBlocks - 1) / kSuperBlocks);   // host-checked <= kSelectLds
+    const int per = kSelectLds / nsb;                                  // candidates per batch
+    for (int i0 = 0; i0 < n_grid; i0 += per) {
+        const int nc = min(per, n_grid - i0);
+        for (int it = tid; it < nc * nsb; it += 256) {
+            const int ci = it / nsb, q = it - ci * nsb;
+            const int64_t b0 = (int64_t)q * kSuperBlocks;
+            const int nb = (int)min((int64_t)kSuperBlocks, nblk - b0);
+            const double* p = work + (int64_t)(i0 + ci) * nblk + b0;
+            double v[kSuperBlocks];
 #pragma unroll
-        for (int u = 0; u < kChunkElems / 256; ++u) {
-            const int64_t e = tid + 256 * u;
-            const int64_t i = e / nb, j = e - i * nb;
-            t[u] = (e < ne) ? work[i * nblk + b0 + j] : 0.0;
+            for (int j = 0; j < kSuperBlocks; ++j) v[j] = p[j < nb ? j : nb - 1];
+            double s = 0.0;
+#pragma unroll
+            for (int j = 0; j < kSuperBlocks; ++j)
+                if (j < nb) s += v[j];
+            sw[it] = s;
         }
-#pragma unroll
-        for (int u = 0; u < kChunkElems / 256; ++u)
-            if (tid + 256 * u < ne) sw[tid + 256 * u] = t[u];
         __syncthreads();
-        if (tid < n_grid)
-            for (int64_t j = 0; j < nb; j += 8) {          // 8 LDS values ahead of the chain
-                double t[8];
-#pragma unroll
-                for (int u = 0; u < 8; ++u) t[u] = sw[tid * nb + ((j + u < nb) ? j + u : nb - 1)];
-#pragma unroll
-                for (int u = 0; u < 8; ++u)
-                    if (j + u < nb) s += t[u];
-            }
+        if (tid < nc) {
+            double s = 0.0;
+            for (int q = 0; q < nsb; ++q) s += sw[tid * nsb + q];
+            sl[i0 + tid] = s;
+            if (losses) losses[i0 + tid] = s;
+        }
+        __syncthreads();
     }
-    if (tid < n_grid) {
-        sl[tid] = s;
-        if (losses) losses[tid] = s;
-    }
-    __syncthreads();
     if (tid == 0) {
         double bv = __builtin_inf();
         int bi = 0;
@@ -876,6 +926,8 @@ hipError_t launch_act_losses(const void* w, int dtype, int64_t R, int64_t K, int
 hipError_t launch_act_select(const float* part, int n_grid, int64_t stride, const float* table, int64_t K,
                              double* work, double* losses, int32_t* best, float* s_best, hipStream_t stream) {
     const int64_t nblk = (stride + kGroupBlock - 1) / kGroupBlock;
+    if (n_grid < 1 || n_grid > AWQ_ACT_MAX_GRID || (nblk + kSuperBlocks - 1) / kSuperBlocks > kSelectLds)
+        return hipErrorInvalidValue;
     hipLaunchKernelGGL(loss_block_kernel, dim3(blocks_for((int64_t)n_grid * nblk, kLossChains, INT32_MAX)), dim3(256),
                        0, stream, part, n_grid, stride, nblk, work);
     if (hipError_t e = hipPeekAtLastError()) return e;

@@ -952,7 +952,7 @@ __device__ __forceinline__ float field1_fast(float x, float r, float z, float s)
 #endif
 
 // LDS: the segment's stage (dynamic, sized by the launch to the tile: 1.6-8 KiB) + 1.3 KiB
-template <typename F, int BITS, bool SYM>
+template <typename F, int BITS, bool SYM, int SPLIT>
 __global__ __launch_bounds__(64, 8) void awq_rowgroup_kernel(const void* __restrict__ w, int64_t rows, int64_t K,
                                                              int64_t L, int lgP, int GPT, uint32_t tiles_per_row,
                                                              int64_t G, int C,
@@ -1092,14 +1092,16 @@ __global__ __launch_bounds__(64, 8) void awq_rowgroup_kernel(const void* __restr
     // ---- pass 2: lane = 8 consecutive elements of the segment (one qweight word at 4 bits):
     //      its groups' parameters from LDS, quantize, pack, store (kb is a word boundary) ----
     const int nck = (n_el + 7) >> 3;
-    const float invL = 1.0f / (float)L;                   // exact group index: e < 2^13, L <= 512
+    const int L32 = (int)L;
+    const float invL = 1.0f / (float)L32;                 // exact group index: e < 2^13, L <= 512
     const int64_t wpr = (K + PER - 1) / PER;
     int32_t* qdst = qweight ? qweight + r * wpr + kb / PER : nullptr;
     for (int c = lane; c < nck; c += 64) {
         const int e0c = 8 * c;
+        const bool tail = e0c + 8 > n_el;                 // the row's last, partial chunk
         float x[8];
         if (skew == 0) {                                  // 16-B aligned chunk (K % 8 == 0 rows)
-            const u4 v0 = *(const u4*)(stage + e0c);
+            const u4 v0 = *(const u4*)(stage + e0c);      // (past n_el: the stage's slack)
             if constexpr (F::kBytes == 2) {
 #pragma unroll
                 for (int i = 0; i < 4; ++i) {
@@ -1119,12 +1121,26 @@ __global__ __launch_bounds__(64, 8) void awq_rowgroup_kernel(const void* __restr
 #pragma unroll
             for (int i = 0; i < 8; ++i) x[i] = SL::dec(stage[skew + min(e0c + i, n_el - 1)]);
         }
-        // parameters per element: the chunk meets at most two groups when L >= 8
+        // parameters per element.  SPLIT 8 (L % 8 == 0): the chunk lies in one group; SPLIT 4
+        // (L % 4 == 0): each half does (no per-element selects); SPLIT 1: at most two groups
+        // meet in the chunk when L >= 8, one lookup per element below that
         float rr[8], zz[8], ss[8];
-        bool spec = false;
-        if (L >= 8) {
+        bool spec;
+        if constexpr (SPLIT == 8 || SPLIT == 4) {
+            const int gA = min((int)(((float)e0c + 0.5f) * invL), ng - 1);
+            const float4 pA = prm[gA];
+            float4 pB = pA;
+            if constexpr (SPLIT == 4) pB = prm[min((int)(((float)(e0c + 4) + 0.5f) * invL), ng - 1)];
+            spec = pA.w != 0.0f || pB.w != 0.0f;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                rr[i] = i < 4 ? pA.x : pB.x;
+                zz[i] = i < 4 ? pA.y : pB.y;
+                ss[i] = i < 4 ? pA.z : pB.z;
+            }
+        } else if (L32 >= 8) {
             const int gA = (int)(((float)e0c + 0.5f) * invL);
-            const int bnd = (gA + 1) * (int)L - e0c;      // first element of the next group
+            const int bnd = (gA + 1) * L32 - e0c;         // first element of the next group
             const float4 pA = prm[gA], pB = prm[min(gA + 1, ng - 1)];
             spec = pA.w != 0.0f || (bnd < 8 && pB.w != 0.0f);
 #pragma unroll
@@ -1135,6 +1151,7 @@ __global__ __launch_bounds__(64, 8) void awq_rowgroup_kernel(const void* __restr
                 ss[i] = a ? pA.z : pB.z;
             }
         } else {
+            spec = false;
 #pragma unroll
             for (int i = 0; i < 8; ++i) {
                 const int gi = min((int)(((float)(e0c + i) + 0.5f) * invL), ng - 1);
@@ -1147,7 +1164,6 @@ __global__ __launch_bounds__(64, 8) void awq_rowgroup_kernel(const void* __restr
         }
         int32_t qv[8];                                    // q (reference value), INT32_MIN for NaN
         uint32_t word0 = 0, word1 = 0;
-        const bool tail = e0c + 8 > n_el;                 // the row's last, partial chunk
         if (__builtin_expect(!spec, 1)) {
             float q[8];
 #pragma unroll
@@ -1155,9 +1171,10 @@ __global__ __launch_bounds__(64, 8) void awq_rowgroup_kernel(const void* __restr
                 q[i] = plain ? field1_fast<F, BITS, SYM, true>(x[i], rr[i], zz[i], ss[i])
                              : field1_fast<F, BITS, SYM, false>(x[i], rr[i], zz[i], ss[i]);
             if (__builtin_expect(tail, 0)) {
+                const int nv = n_el - e0c;
 #pragma unroll
-                for (int i = 0; i < 8; ++i)
-                    if (e0c + i >= n_el) q[i] = 0.0f;     // past the row end: zero fields
+                for (int i = 1; i < 8; ++i)
+                    if (i >= nv) q[i] = 0.0f;             // past the row end: zero fields
             }
             if (tensor_q) {
 #pragma unroll
@@ -1176,6 +1193,7 @@ __global__ __launch_bounds__(64, 8) void awq_rowgroup_kernel(const void* __restr
             }
         } else {                                          // a group with scale 0 / inf / NaN: IEEE division
             constexpr int QMAX = SYM ? (1 << (BITS - 1)) - 1 : (1 << BITS) - 1;
+            const int nv = n_el - e0c;
 #pragma unroll
             for (int i = 0; i < 8; ++i) {
                 const float t = F::rn(opaque(x[i]) / ss[i]);
@@ -1184,7 +1202,7 @@ __global__ __launch_bounds__(64, 8) void awq_rowgroup_kernel(const void* __restr
                 int32_t qi = __builtin_isnan(rq) ? INT32_MIN
                                                  : (int32_t)__builtin_fminf(__builtin_fmaxf(rq, (float)QMIN), (float)QMAX);
                 uint32_t f = ((uint32_t)qi - (uint32_t)QMIN) & MASK;
-                if (e0c + i >= n_el) { f = 0; qi = QMIN; }
+                if (i >= nv) { f = 0; qi = QMIN; }
                 qv[i] = qi;
                 if (BITS == 4) word0 |= f << (4 * i);
                 else if (i < 4) word0 |= f << (8 * i);
@@ -1196,14 +1214,20 @@ __global__ __launch_bounds__(64, 8) void awq_rowgroup_kernel(const void* __restr
                 qdst[c] = (int32_t)word0;
             } else {
                 qdst[2 * c] = (int32_t)word0;
-                if (e0c + 4 < n_el) qdst[2 * c + 1] = (int32_t)word1;
+                if (!tail || e0c + 4 < n_el) qdst[2 * c + 1] = (int32_t)word1;
             }
         }
         if (tensor_q) {
             int32_t* tq = tensor_q + r * K + kb + e0c;
+            if (__builtin_expect(!tail, 1)) {
 #pragma unroll
-            for (int i = 0; i < 8; ++i)
-                if (e0c + i < n_el) tq[i] = qv[i];
+                for (int i = 0; i < 8; ++i) tq[i] = qv[i];
+            } else {
+                const int nv = n_el - e0c;
+#pragma unroll
+                for (int i = 0; i < 8; ++i)
+                    if (i < nv) tq[i] = qv[i];
+            }
         }
     }
     if (qzeros) {                                 // g0 is a word boundary: GPT % PER == 0
@@ -1447,9 +1471,13 @@ hipError_t launch_rowgroup(const void* w, int dtype, int64_t rows, int64_t K, in
     // stage: the tile's elements rounded up to 16 B, + the up-to-16-B alignment skew and the
     // last 8-element vector read past the segment end
     const size_t lds = ((size_t)gpt * L * (dtype == AWQ_DTYPE_F32 ? 4 : 2) + 15) / 16 * 16 + 48;
-#define AWQ_RG(Fm, B, S)                                                                                           \
-    hipLaunchKernelGGL((awq_rowgroup_kernel<Fm, B, S>), grid, block, lds, stream, w, rows, K, L, lgP, gpt,           \
+#define AWQ_RG_SPLIT(Fm, B, S, SP)                                                                                 \
+    hipLaunchKernelGGL((awq_rowgroup_kernel<Fm, B, S, SP>), grid, block, lds, stream, w, rows, K, L, lgP, gpt,      \
                        (uint32_t)tpr, G, C, qweight, qzeros, scales, tensor_q, zeros)
+#define AWQ_RG(Fm, B, S)                                                                                           \
+    if (L % 8 == 0) AWQ_RG_SPLIT(Fm, B, S, 8);                                                                      \
+    else if (L % 4 == 0) AWQ_RG_SPLIT(Fm, B, S, 4);                                                                 \
+    else AWQ_RG_SPLIT(Fm, B, S, 1)
 #define AWQ_RG_FMT(Fm)                                                     \
     switch ((bits == 8 ? 2 : 0) + (symmetric ? 1 : 0)) {                  \
     case 0: AWQ_RG(Fm, 4, false); break;                                   \
@@ -1466,6 +1494,7 @@ hipError_t launch_rowgroup(const void* w, int dtype, int64_t rows, int64_t K, in
     }
 #undef AWQ_RG_FMT
 #undef AWQ_RG
+#undef AWQ_RG_SPLIT
     return hipPeekAtLastError();
 }
 

@@ -206,8 +206,8 @@ int awq_pack_rows(const int32_t* v, int64_t rows, int64_t n, int bits, int qmin,
  * of n >= 1 linears W_j [R_j, K] that read the same input x [tokens, K]:
  *
  *   x_mean[k] = fp32(sum_t |x[t,k]| / T),  x_sq[k] = fp32(sum_t x[t,k]^2 / T)
- *       (awq_act_stats; sums in fp64, t ascending inside 256-token blocks, then the
- *        blocks ascending)
+ *       (awq_act_stats; sums in fp64: t ascending inside 32-token sub-blocks, the
+ *        sub-blocks ascending inside 256-token blocks, then the blocks ascending)
  *   w_mean[k] = fp32(sum_{j,r} fp32(|W_j[r,k]| / fp32(gmax_j[r, k/gs] + 1e-6f)) / sum_j R_j)
  *       (duo scaling only; gmax = max |W| of the group; same fp64 block order, the
  *        linears' blocks in list order; awq_weight_colsum per linear + awq_column_mean)
@@ -223,8 +223,10 @@ int awq_pack_rows(const int32_t* v, int64_t rows, int64_t n, int bits, int qmin,
  *   group loss: each 8-element chunk summed in order, then the pairwise tree over the
  *       group's gs/8 chunks (fp32) -> part[i * part_stride + group]
  *       (awq_act_search_losses, per linear at its offset in one group list)
- *   loss_i = sum over 1024-group blocks (ascending, fp64) of the blocks' ascending fp64
- *       sums; best = first minimum (NaN never wins; all NaN -> 0) (awq_act_search_select)
+ *   loss_i = fp64 sum in four ascending levels: groups inside a 64-group sub-block,
+ *       sub-blocks inside a 1024-group block, blocks inside a 32-block super-block, then
+ *       the super-blocks; best = first minimum (NaN never wins; all NaN -> 0)
+ *       (awq_act_search_select)
  *   result: every W_j quantized as W_j * diag(s_best) (awq_apply_input_scale, then
  *       awq_quantize_groups); s_best is returned to be folded into the op producing x
  *       (x / s_best, e.g. the preceding norm's weight).

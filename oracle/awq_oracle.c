@@ -429,7 +429,10 @@ int oracle_pack_rows(const int32_t* v, int64_t rows, int64_t n, int bits, int qm
  * pow differs between math libraries by <= 1 fp32 ulp, checked separately); parity with
  * AutoAWQ is unpinned. */
 #define ACT_ROW_BLOCK 256
+#define ACT_ROW_SUB 32       /* rows per sub-block: a block sums its sub-blocks' sums */
 #define ACT_GROUP_BLOCK 1024
+#define ACT_GROUP_SUB 64     /* groups per sub-block of a loss block */
+#define ACT_SUPER_BLOCKS 32  /* loss blocks per super-block of a candidate's total */
 
 static inline float load_f(const void* x, int dtype, int64_t i) { return (float)load_elem(x, dtype, i); }
 
@@ -439,13 +442,21 @@ int oracle_act_stats(const void* x, int dtype, int64_t T, int64_t K, float* x_me
 #pragma omp parallel for schedule(static) if (T * K >= (1 << 16))
     for (int64_t k = 0; k < K; ++k) {
         double a = 0.0, q = 0.0;
-        for (int64_t b = 0; b < nblk; ++b) {   /* fp64, tokens ascending inside a block */
+        for (int64_t b = 0; b < nblk; ++b) {   /* fp64: tokens ascending inside a 32-token
+                                                  sub-block, sub-blocks ascending inside a
+                                                  256-token block, blocks ascending */
             double pa = 0.0, pq = 0.0;
             int64_t t1 = (b + 1) * ACT_ROW_BLOCK < T ? (b + 1) * ACT_ROW_BLOCK : T;
-            for (int64_t t = b * ACT_ROW_BLOCK; t < t1; ++t) {
-                double v = (double)load_f(x, dtype, t * K + k);
-                pa += fabs(v);
-                pq += v * v;
+            for (int64_t u = b * ACT_ROW_BLOCK; u < t1; u += ACT_ROW_SUB) {   /* 32-token sub-blocks */
+                double sa = 0.0, sq = 0.0;
+                int64_t u1 = u + ACT_ROW_SUB < t1 ? u + ACT_ROW_SUB : t1;
+                for (int64_t t = u; t < u1; ++t) {
+                    double v = (double)load_f(x, dtype, t * K + k);
+                    sa += fabs(v);
+                    sq += v * v;
+                }
+                pa += sa;
+                pq += sq;
             }
             a += pa;
             q += pq;
@@ -477,9 +488,14 @@ int oracle_weight_colsum(const void* w, int dtype, int64_t R, int64_t K, int64_t
         for (int64_t k = 0; k < K; ++k) {
             double s = 0.0;
             int64_t r1 = (b + 1) * ACT_ROW_BLOCK < R ? (b + 1) * ACT_ROW_BLOCK : R;
-            for (int64_t r = b * ACT_ROW_BLOCK; r < r1; ++r) {
-                float den = gmax[r * G + k / L] + 1e-6f;
-                s += (double)(fabsf(load_f(w, dtype, r * K + k)) / den);
+            for (int64_t u = b * ACT_ROW_BLOCK; u < r1; u += ACT_ROW_SUB) {   /* as oracle_act_stats */
+                double su = 0.0;
+                int64_t u1 = u + ACT_ROW_SUB < r1 ? u + ACT_ROW_SUB : r1;
+                for (int64_t r = u; r < u1; ++r) {
+                    float den = gmax[r * G + k / L] + 1e-6f;
+                    su += (double)(fabsf(load_f(w, dtype, r * K + k)) / den);
+                }
+                s += su;
             }
             partial[b * K + k] = s;
         }
@@ -585,12 +601,25 @@ int oracle_act_search_select(const float* part, int n_grid, int64_t stride, doub
     double bv = INFINITY;
     int bi = 0;
     for (int i = 0; i < n_grid; ++i) {
+        /* fp64, three levels: groups ascending inside a 64-group sub-block; sub-blocks
+         * ascending inside a 1024-group block; blocks ascending inside a 32-block super-block;
+         * super-blocks ascending */
         double tot = 0.0;
-        for (int64_t b = 0; b < nblk; ++b) {
-            double s = 0.0;
-            int64_t g1 = (b + 1) * ACT_GROUP_BLOCK < stride ? (b + 1) * ACT_GROUP_BLOCK : stride;
-            for (int64_t g = b * ACT_GROUP_BLOCK; g < g1; ++g) s += (double)part[(int64_t)i * stride + g];
-            tot += s;
+        for (int64_t sb = 0; sb < nblk; sb += ACT_SUPER_BLOCKS) {
+            double ss = 0.0;
+            int64_t b1 = sb + ACT_SUPER_BLOCKS < nblk ? sb + ACT_SUPER_BLOCKS : nblk;
+            for (int64_t b = sb; b < b1; ++b) {
+                double s = 0.0;
+                int64_t g1 = (b + 1) * ACT_GROUP_BLOCK < stride ? (b + 1) * ACT_GROUP_BLOCK : stride;
+                for (int64_t u = b * ACT_GROUP_BLOCK; u < g1; u += ACT_GROUP_SUB) {
+                    double su = 0.0;
+                    int64_t u1 = u + ACT_GROUP_SUB < g1 ? u + ACT_GROUP_SUB : g1;
+                    for (int64_t g = u; g < u1; ++g) su += (double)part[(int64_t)i * stride + g];
+                    s += su;
+                }
+                ss += s;
+            }
+            tot += ss;
         }
         if (losses) losses[i] = tot;
         if (tot < bv) { bv = tot; bi = i; }

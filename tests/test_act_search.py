@@ -129,6 +129,46 @@ def test_capi_validation_without_gpu():
     assert lib.awq_act_recip_table(P, 0, 128, P, None) != 0 and "n_grid" in _hip.last_error()
 
 
+def _levels_sum(v, sizes):
+    """fp64 sum of v in nested ascending levels (sizes innermost first), as include/awq_hip.h
+    defines the canonical orders: [64, 16, 32] for the loss totals, [32, 8] for a column block."""
+    import numpy as np
+    v = np.asarray(v, dtype=np.float64)
+    if not sizes:
+        s = 0.0
+        for t in v:
+            s += t
+        return s
+    n = sizes[0]
+    return _levels_sum([_levels_sum(v[i:i + n], []) for i in range(0, len(v), n)], sizes[1:])
+
+
+def test_oracle_select_order():
+    """The oracle's loss totals follow the header's four-level order (checked against an
+    independent restatement on a part array spanning two super-blocks, magnitudes chosen so
+    that the order changes the bits)."""
+    g = torch.Generator().manual_seed(3)
+    stride = 33 * 1024 + 517
+    part = (torch.rand(3, stride, generator=g) * 10.0 ** torch.randint(-6, 6, (3, stride), generator=g)).float()
+    losses, best = orc.act_search_select(part)
+    for i in range(3):
+        want = _levels_sum(part[i].double().numpy(), [64, 16, 32])
+        assert losses[i].item() == want
+    assert best == int(torch.argmin(losses))
+
+
+def test_oracle_stats_order():
+    g = torch.Generator().manual_seed(4)
+    x = (torch.randn(300, 5, generator=g) * 10.0 ** torch.randint(-4, 4, (300, 5), generator=g)).float()
+    xm, xs = orc.act_stats(x)
+    xd = x.double().numpy()
+    for k in range(5):
+        blocks = [_levels_sum(abs(xd[b:b + 256, k]), [32]) for b in (0, 256)]
+        assert xm[k].item() == float(torch.tensor(_levels_sum(blocks, []) / 300).float())
+        blocks = [_levels_sum(xd[b:b + 256, k] ** 2, [32]) for b in (0, 256)]
+        assert xs[k].item() == float(torch.tensor(_levels_sum(blocks, []) / 300).float())
+
+
 # ---------------------------------------------------------------- GPU: kernels vs oracle
 def _gpu():
     if not torch.cuda.is_available():
@@ -202,6 +242,41 @@ def test_gpu_losses_bit_exact(dtype, gs, bits, sym):
     assert torch.equal(losses.cpu().view(torch.int64), ol.view(torch.int64))
     assert int(best.item()) == ob
     assert torch.equal(s_best.cpu(), table.cpu()[ob])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n_grid,stride", [(1, 1), (5, 1023), (7, 64 * 1024 + 100), (20, 917504),
+                                           (256, 40 * 1024), (64, 3200 * 1024)], ids=str)
+def test_gpu_select_bit_exact(n_grid, stride):
+    """awq_act_search_select on part arrays of every shape class: partial sub-blocks, one
+    block, several super-blocks (a Llama-3-8B gate/up group list: 917 504 groups), the
+    maximum grid, and candidate batches (n_grid x super-blocks beyond one LDS batch)."""
+    dev = _gpu()
+    from awq_quantizer import _hip
+    g = torch.Generator(device=dev).manual_seed(n_grid)
+    part = torch.rand(n_grid, stride, generator=g, device=dev)
+    part *= torch.exp2(torch.randint(-20, 20, (n_grid, stride), generator=g, device=dev).float())
+    table = torch.rand(n_grid, 64, generator=g, device=dev)
+    losses, best, s_best = _hip.act_search_select(part, table)
+    ol, ob = orc.act_search_select(part)
+    assert torch.equal(losses.cpu().view(torch.int64), ol.view(torch.int64))
+    assert int(best.item()) == ob and torch.equal(s_best.cpu(), table.cpu()[ob])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("T", [31, 32, 33, 257, 4096])
+def test_gpu_stats_sub_blocks(T):
+    """Sub-block edges (32 tokens) and many blocks; K % 8 != 0 takes the per-column kernel."""
+    dev = _gpu()
+    from awq_quantizer import _hip
+    g = torch.Generator().manual_seed(T)
+    for K in (64, 100):
+        x = (torch.randn(T, K, generator=g) * torch.exp2(torch.randint(-10, 10, (T, K), generator=g).float()))
+        x = x.bfloat16()
+        xm, xs = _hip.act_stats(x.to(dev))
+        om, os_ = orc.act_stats(x)
+        assert torch.equal(xm.cpu().view(torch.int32), om.view(torch.int32))
+        assert torch.equal(xs.cpu().view(torch.int32), os_.view(torch.int32))
 
 
 @pytest.mark.gpu

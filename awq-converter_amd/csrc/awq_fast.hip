@@ -912,19 +912,25 @@ __device__ __forceinline__ int64_t xcd_run_block(int64_t b, int64_t nblocks) {
 // ---------------------------------------------------------------------------------------
 // Any group size up to 512 (bf16 / fp16; 256 for fp32), any K: row-segment tiles.
 //
-// A tile = GPT consecutive groups of one row (GPT in {8, 16, 32, 64}, host-chosen for the
-// best lane use), one 64-lane wave per tile: the segment's bytes go to LDS with 16-B
-// loads (16-B aligned start, the range check zero-fills past the tensor end), lane
-// (grp, j) owns chunk j of group grp (P = 64 / GPT lanes per group, C = ceil(L / P)
-// elements each), reduces the raw-bits min/max over its chunk and the group's P lanes
-// (the streaming kernel's group_range / params_from_range: the same verified arithmetic),
-// then overwrites each of its elements in LDS by its packed field; the wave then packs
-// qweight / qzeros words and stores them coalesced.  Tile boundaries fall on qweight and
-// qzeros word boundaries (GPT * L and GPT are multiples of 8), so no word is shared
-// between waves.  Replaces the one-wave-per-group generic kernel plus its int32 staging
-// and pack passes (~10.5 B moved per element) for these shapes.
+// A tile = GPT consecutive groups of one row (GPT a multiple of 8 up to 64; the cost model
+// picks 8, 16, 32 or 64), one 64-lane wave per tile:
+//   stage   the segment's bytes go to LDS with 16-B loads, all in flight at once (16-B
+//           aligned start; the tensor's last bytes go by 2-B loads);
+//   pass 1  lane (grp, j) owns chunk j of group grp (P lanes per group = the largest power
+//           of two <= 64 / the tile's groups, C = ceil(L / P) elements each) and reduces
+//           the raw-bits min/max over it (packed 16-bit max/min, two chains) and over the
+//           group's P lanes, then computes the group's parameters (the streaming kernel's
+//           group_range / params_from_range: the same verified arithmetic) into LDS;
+//   pass 2  lane = 8 consecutive elements (one qweight word at 4 bits): parameters from LDS
+//           per half (L % 4 == 0) or per element, the field chain (bf16: packed f32 mul /
+//           add), one coalesced word store.
+// Tile boundaries fall on qweight and qzeros word boundaries (GPT * L and GPT are multiples
+// of 8), so no word is shared between waves.  Replaces the one-wave-per-group generic
+// kernel plus its int32 staging and pack passes (~10.5 B moved per element) for these
+// shapes.
 // ---------------------------------------------------------------------------------------
-constexpr int kRgStageBytes = 8192;
+constexpr int kRgStageBytes = 8192;    // eligibility: 8 groups fit (any GPT the cost model picks)
+constexpr int kRgStageMax = 16384;     // tuning override ceiling (AWQ_RG_GPT)
 
 template <typename F>
 struct RgSlot {
@@ -947,6 +953,29 @@ __device__ __forceinline__ float field1_fast(float x, float r, float z, float s)
     return __builtin_fminf(__builtin_fmaxf(__builtin_rintf(u), 0.0f), QR);
 }
 
+// the same for 8 bf16 elements, multiply and add as packed f32 pairs (v_pk_mul_f32 /
+// v_pk_add_f32: each half is the IEEE f32 op, rounded to bf16 after it as above)
+template <int BITS, bool SYM>
+__device__ __forceinline__ void field8_bf16(const float (&x)[8], const float (&r)[8], const float (&z)[8],
+                                            float (&q)[8]) {
+    constexpr float QR = (float)((1 << BITS) - 1);
+    constexpr float HALF = (float)(1 << (BITS - 1));
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const f2 p = (f2){x[2 * i], x[2 * i + 1]} * (f2){r[2 * i], r[2 * i + 1]};
+        const f2 t = {rn_bf16(p.x), rn_bf16(p.y)};
+        f2 u;
+        if (SYM) {
+            u = t + (f2){HALF, HALF};                       // exact (as field1_fast)
+        } else {
+            const f2 a = t + (f2){z[2 * i], z[2 * i + 1]};
+            u = (f2){rn_bf16(a.x), rn_bf16(a.y)};
+        }
+        q[2 * i] = __builtin_fminf(__builtin_fmaxf(__builtin_rintf(u.x), 0.0f), QR);
+        q[2 * i + 1] = __builtin_fminf(__builtin_fmaxf(__builtin_rintf(u.y), 0.0f), QR);
+    }
+}
+
 #ifndef AWQ_RG_UNROLL
 #define AWQ_RG_UNROLL 8
 #endif
@@ -955,7 +984,7 @@ __device__ __forceinline__ float field1_fast(float x, float r, float z, float s)
 template <typename F, int BITS, bool SYM, int SPLIT>
 __global__ __launch_bounds__(64, 8) void awq_rowgroup_kernel(const void* __restrict__ w, int64_t rows, int64_t K,
                                                              int64_t L, int lgP, int GPT, uint32_t tiles_per_row,
-                                                             int64_t G, int C,
+                                                             int64_t G, int C, float invL,
                                                              int32_t* __restrict__ qweight, int32_t* __restrict__ qzeros,
                                                              uint16_t* __restrict__ scales,
                                                              int32_t* __restrict__ tensor_q, int32_t* __restrict__ zeros) {
@@ -972,12 +1001,16 @@ __global__ __launch_bounds__(64, 8) void awq_rowgroup_kernel(const void* __restr
     const int lane = threadIdx.x;
     // (host-side G, C, log2 P and a 32-bit tile split: 64-bit divisions per wave on the
     //  CU's shared scalar unit were a visible part of the per-tile cost)
-    const uint32_t tile = blockIdx.x;
+    const uint32_t tile = blockIdx.x;   // (an XCD-contiguous tile order measured no different: r2z3)
     const uint32_t r32 = tile / tiles_per_row;
     const int64_t r = r32;
     const int64_t g0 = (int64_t)(tile - r32 * tiles_per_row) * GPT;
-    const int P = 1 << lgP;
     const int ng = (int)min((int64_t)GPT, G - g0);
+    if (ng < GPT) {   // the row's last, partial tile: more lanes per group (wave-uniform)
+        lgP = 31 - __builtin_clz(64u / (unsigned)ng);
+        C = (int)((L + (1 << lgP) - 1) >> lgP);
+    }
+    const int P = 1 << lgP;
     const int64_t kb = g0 * L, ke = min((g0 + ng) * L, K);     // the row segment [kb, ke)
     const int n_el = (int)(ke - kb);
     // ---- stage the segment's bytes (from a 16-B aligned start) in LDS ----
@@ -989,6 +1022,22 @@ __global__ __launch_bounds__(64, 8) void awq_rowgroup_kernel(const void* __restr
     const int nch = (nbytes + 15) >> 4;
     const uint32_t lim = (uint32_t)min(total - a0, (uint64_t)nch * 16);
     const __amdgpu_buffer_rsrc_t rw = rsrc((const char*)w + a0, lim);
+    if (__builtin_expect(16u * (uint32_t)nch <= lim, 1)) {
+        // every 16-B load of the segment in flight before the first LDS store (a load ->
+        // store loop waits out one memory round trip per load); lanes past the end repeat
+        // the last chunk's address and store nothing
+        for (int c0 = 0; c0 < nch; c0 += 512) {
+            u4 v[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k)
+                if (c0 + 64 * k < nch)                   // wave-uniform
+                    v[k] = __builtin_amdgcn_raw_buffer_load_b128(rw, (uint32_t)(16 * min(c0 + 64 * k + lane, nch - 1)),
+                                                                 0, AWQ_LOAD_AUX);
+#pragma unroll
+            for (int k = 0; k < 8; ++k)
+                if (c0 + 64 * k + lane < nch) *(u4*)((char*)stage + 16 * (c0 + 64 * k + lane)) = v[k];
+        }
+    } else
 #pragma unroll 4
     for (int c = lane; c < nch; c += 64) {
         if (__builtin_expect(16u * c + 16u <= lim, 1)) {
@@ -1020,10 +1069,17 @@ __global__ __launch_bounds__(64, 8) void awq_rowgroup_kernel(const void* __restr
             s2 sm = {(short)(padded ? 0 : -32768), (short)(padded ? 0 : -32768)};
             us2 um = {0, 0};
             us2 un = {(unsigned short)(padded ? 0 : 0xFFFF), (unsigned short)(padded ? 0 : 0xFFFF)};
+            s2 sm_b = sm;                                 // a second, independent set of chains
+            us2 um_b = um, un_b = un;
             auto acc = [&](uint32_t v) {
                 sm = __builtin_elementwise_max(sm, as_s2(v));
                 um = __builtin_elementwise_max(um, as_us2(v));
                 un = __builtin_elementwise_min(un, as_us2(v));
+            };
+            auto acc_b = [&](uint32_t v) {
+                sm_b = __builtin_elementwise_max(sm_b, as_s2(v));
+                um_b = __builtin_elementwise_max(um_b, as_us2(v));
+                un_b = __builtin_elementwise_min(un_b, as_us2(v));
             };
             uint32_t first = st32[d_lo];
             if (s_lo & 1) first = __builtin_amdgcn_perm(first, first, 0x03020302u);   // low half := high
@@ -1034,15 +1090,18 @@ __global__ __launch_bounds__(64, 8) void awq_rowgroup_kernel(const void* __restr
                 for (; d + 4 <= d_hi - 1; d += 4) {
                     const uint32_t v0 = st32[d], v1 = st32[d + 1], v2 = st32[d + 2], v3 = st32[d + 3];
                     acc(v0);
-                    acc(v1);
+                    acc_b(v1);
                     acc(v2);
-                    acc(v3);
+                    acc_b(v3);
                 }
                 for (; d < d_hi - 1; ++d) acc(st32[d]);
                 uint32_t last = st32[d_hi - 1];
                 if (s_hi & 1) last = __builtin_amdgcn_perm(last, last, 0x01000100u);        // high half := low
                 acc(last);
             }
+            sm = __builtin_elementwise_max(sm, sm_b);
+            um = __builtin_elementwise_max(um, um_b);
+            un = __builtin_elementwise_min(un, un_b);
             smax = max((int)sm.x, (int)sm.y);
             umax = (uint32_t)max((int)um.x, (int)um.y);
             umin = (uint32_t)min((int)un.x, (int)un.y);
@@ -1092,8 +1151,8 @@ __global__ __launch_bounds__(64, 8) void awq_rowgroup_kernel(const void* __restr
     // ---- pass 2: lane = 8 consecutive elements of the segment (one qweight word at 4 bits):
     //      its groups' parameters from LDS, quantize, pack, store (kb is a word boundary) ----
     const int nck = (n_el + 7) >> 3;
-    const int L32 = (int)L;
-    const float invL = 1.0f / (float)L32;                 // exact group index: e < 2^13, L <= 512
+    const int L32 = (int)L;                               // invL = RN(1 / L): exact group index e * invL
+                                                          // for e < 2^13, L <= 512 (host-computed)
     const int64_t wpr = (K + PER - 1) / PER;
     int32_t* qdst = qweight ? qweight + r * wpr + kb / PER : nullptr;
     for (int c = lane; c < nck; c += 64) {
@@ -1166,10 +1225,14 @@ __global__ __launch_bounds__(64, 8) void awq_rowgroup_kernel(const void* __restr
         uint32_t word0 = 0, word1 = 0;
         if (__builtin_expect(!spec, 1)) {
             float q[8];
+            if constexpr (std::is_same<F, FmtBF16>::value) {
+                field8_bf16<BITS, SYM>(x, rr, zz, q);
+            } else {
 #pragma unroll
-            for (int i = 0; i < 8; ++i)
-                q[i] = plain ? field1_fast<F, BITS, SYM, true>(x[i], rr[i], zz[i], ss[i])
-                             : field1_fast<F, BITS, SYM, false>(x[i], rr[i], zz[i], ss[i]);
+                for (int i = 0; i < 8; ++i)
+                    q[i] = plain ? field1_fast<F, BITS, SYM, true>(x[i], rr[i], zz[i], ss[i])
+                                 : field1_fast<F, BITS, SYM, false>(x[i], rr[i], zz[i], ss[i]);
+            }
             if (__builtin_expect(tail, 0)) {
                 const int nv = n_el - e0c;
 #pragma unroll
@@ -1436,18 +1499,17 @@ hipError_t launch_fast(const awq_tensor_desc* descs_dev, const int32_t* block_te
 // + 2.3 per 512-element pass-2 sweep); 0 if the shape does not fit the LDS stage.
 int rowgroup_gpt(int dtype, int64_t K, int64_t L) {
     if (dtype != AWQ_DTYPE_BF16 && dtype != AWQ_DTYPE_F16 && dtype != AWQ_DTYPE_F32) return 0;
+    const int64_t es = dtype == AWQ_DTYPE_F32 ? 4 : 2;
+    if (L <= 0 || K <= 0 || 8 * L * es > kRgStageBytes) return 0;
     if (const char* e = getenv("AWQ_RG_GPT")) {        // tuning override (scripts/generic_bench.py)
         const int v = atoi(e);
-        const int64_t es = dtype == AWQ_DTYPE_F32 ? 4 : 2;
-        if ((v == 8 || v == 16 || v == 32 || v == 64) && v * L * es <= kRgStageBytes) return v;
+        if (v >= 8 && v <= 64 && v % 8 == 0 && v * L * es <= kRgStageMax) return v;
     }
-    const int64_t slots = kRgStageBytes / (dtype == AWQ_DTYPE_F32 ? 4 : 2);   // (+ 16 B of skew slack)
-    if (L <= 0 || K <= 0) return 0;
     const int64_t G = (K + L - 1) / L;
     int best = 0;
     double best_cost = 0.0;
     for (int gpt = 8; gpt <= 64; gpt *= 2) {
-        if (gpt * L > slots) break;
+        if (gpt * L * es > kRgStageBytes) break;
         const int64_t tiles = (G + gpt - 1) / gpt;
         const int64_t C = (L + (64 / gpt) - 1) / (64 / gpt);
         const int64_t el = min((int64_t)gpt, G) * L;                  // elements of a full tile
@@ -1464,8 +1526,8 @@ hipError_t launch_rowgroup(const void* w, int dtype, int64_t rows, int64_t K, in
     if (gpt == 0 || rows <= 0) return hipErrorInvalidValue;
     const int64_t G = (K + L - 1) / L;
     const int64_t tpr = (G + gpt - 1) / gpt;
-    const int P = 64 / gpt;
-    const int lgP = __builtin_ctz((unsigned)P);
+    const int lgP = 31 - __builtin_clz((unsigned)(64 / gpt));   // P = lanes per group: a power of two
+    const int P = 1 << lgP;
     const int C = (int)((L + P - 1) / P);
     const dim3 grid((unsigned)(rows * tpr)), block(64);
     // stage: the tile's elements rounded up to 16 B, + the up-to-16-B alignment skew and the
@@ -1473,7 +1535,7 @@ hipError_t launch_rowgroup(const void* w, int dtype, int64_t rows, int64_t K, in
     const size_t lds = ((size_t)gpt * L * (dtype == AWQ_DTYPE_F32 ? 4 : 2) + 15) / 16 * 16 + 48;
 #define AWQ_RG_SPLIT(Fm, B, S, SP)                                                                                 \
     hipLaunchKernelGGL((awq_rowgroup_kernel<Fm, B, S, SP>), grid, block, lds, stream, w, rows, K, L, lgP, gpt,      \
-                       (uint32_t)tpr, G, C, qweight, qzeros, scales, tensor_q, zeros)
+                       (uint32_t)tpr, G, C, 1.0f / (float)L, qweight, qzeros, scales, tensor_q, zeros)
 #define AWQ_RG(Fm, B, S)                                                                                           \
     if (L % 8 == 0) AWQ_RG_SPLIT(Fm, B, S, 8);                                                                      \
     else if (L % 4 == 0) AWQ_RG_SPLIT(Fm, B, S, 4);                                                                 \

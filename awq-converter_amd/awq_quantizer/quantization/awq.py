@@ -93,6 +93,9 @@ class AWQQuantizer:
         self.qmin, self.qmax = self._calculate_qmin_qmax()
         self.logger.info(f"Initialized AWQ Quantizer with bits={bits}, group_size={group_size}, symmetric={symmetric}")
         self.logger.info(f"Quantization range: [{self.qmin}, {self.qmax}]")
+        if self.device == "cpu" and torch.cuda.is_available():
+            self.logger.info("device='cpu': this build has no CPU path; the HIP kernels run on the current GPU "
+                             "and results are returned on the CPU (bit-identical to the reference's CPU results)")
         if self.scale_method == "awq":
             self.logger.info("scale_method='awq': the activation-aware search runs in quantize_layer_group(); "
                              "tensors quantized without activations (quantize, quantize_model) are RTN")

@@ -976,6 +976,42 @@ __device__ __forceinline__ void field8_bf16(const float (&x)[8], const float (&r
     }
 }
 
+// raw-bits min/max over each aligned block of 2^lgP lanes (a group's lanes in pass 1):
+// DPP quad / mirror steps and the row-pair swaps (wave-uniform lgP), every lane ends with
+// its block's result
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp_mov(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xF, 0xF, true);
+}
+template <int CTRL>
+__device__ __forceinline__ void rg_step(int& smax, uint32_t& umax, uint32_t& umin) {
+    smax = max(smax, (int)dpp_mov<CTRL>((uint32_t)smax));
+    umax = max(umax, dpp_mov<CTRL>(umax));
+    umin = min(umin, dpp_mov<CTRL>(umin));
+}
+__device__ __forceinline__ void rg_reduce(int& smax, uint32_t& umax, uint32_t& umin, int lgP) {
+    if (lgP >= 1) rg_step<0xB1>(smax, umax, umin);     // quad_perm [1,0,3,2]
+    if (lgP >= 2) rg_step<0x4E>(smax, umax, umin);     // quad_perm [2,3,0,1]
+    if (lgP >= 3) rg_step<0x141>(smax, umax, umin);    // row_half_mirror
+    if (lgP >= 4) rg_step<0x140>(smax, umax, umin);    // row_mirror
+    if (lgP >= 5) {                                    // rows 2k <-> 2k+1
+        const auto a = __builtin_amdgcn_permlane16_swap((unsigned)smax, (unsigned)smax, false, false);
+        const auto b = __builtin_amdgcn_permlane16_swap(umax, umax, false, false);
+        const auto c = __builtin_amdgcn_permlane16_swap(umin, umin, false, false);
+        smax = max((int)a[0], (int)a[1]);
+        umax = max((uint32_t)b[0], (uint32_t)b[1]);
+        umin = min((uint32_t)c[0], (uint32_t)c[1]);
+    }
+    if (lgP >= 6) {                                    // halves
+        const auto a = __builtin_amdgcn_permlane32_swap((unsigned)smax, (unsigned)smax, false, false);
+        const auto b = __builtin_amdgcn_permlane32_swap(umax, umax, false, false);
+        const auto c = __builtin_amdgcn_permlane32_swap(umin, umin, false, false);
+        smax = max((int)a[0], (int)a[1]);
+        umax = max((uint32_t)b[0], (uint32_t)b[1]);
+        umin = min((uint32_t)c[0], (uint32_t)c[1]);
+    }
+}
+
 #ifndef AWQ_RG_UNROLL
 #define AWQ_RG_UNROLL 8
 #endif
@@ -1053,7 +1089,7 @@ __global__ __launch_bounds__(64, 8) void awq_rowgroup_kernel(const void* __restr
     // ---- this lane's chunk of its group ----
     const int grp = lane >> lgP, j = lane & (P - 1);
     const bool active = grp < ng;
-    const int glen = active ? (int)min(L, K - (g0 + grp) * L) : 0;   // elements in the row (tail: fewer)
+    const int glen = active ? min((int)L, n_el - grp * (int)L) : 0;   // elements in the row (tail: fewer)
     const int cb = min(j * C, glen), ce = min(cb + C, glen);
     const int base = skew + grp * (int)L;
     const bool padded = active && glen < L;                    // awq.py:337-339: zeros join the min/max
@@ -1094,7 +1130,13 @@ __global__ __launch_bounds__(64, 8) void awq_rowgroup_kernel(const void* __restr
                     acc(v2);
                     acc_b(v3);
                 }
-                for (; d < d_hi - 1; ++d) acc(st32[d]);
+                if (d + 2 <= d_hi - 1) {                  // <= 3 left: no loop
+                    const uint32_t v0 = st32[d], v1 = st32[d + 1];
+                    acc(v0);
+                    acc_b(v1);
+                    d += 2;
+                }
+                if (d < d_hi - 1) acc_b(st32[d]);
                 uint32_t last = st32[d_hi - 1];
                 if (s_hi & 1) last = __builtin_amdgcn_perm(last, last, 0x01000100u);        // high half := low
                 acc(last);
@@ -1126,11 +1168,7 @@ __global__ __launch_bounds__(64, 8) void awq_rowgroup_kernel(const void* __restr
             umin = min(umin, v);
         }
     }
-    for (int o = 1; o < P; o <<= 1) {                          // the group's P lanes (adjacent)
-        smax = max(smax, __shfl_xor(smax, o, 64));
-        umax = max(umax, (uint32_t)__shfl_xor((int)umax, o, 64));
-        umin = min(umin, (uint32_t)__shfl_xor((int)umin, o, 64));
-    }
+    rg_reduce(smax, umax, umin, lgP);                          // the group's P lanes (aligned)
     float gmn, gmx;
     bool gnan;
     group_range<F, SYM>(smax, umax, umin, gmn, gmx, gnan);

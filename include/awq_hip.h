@@ -237,7 +237,8 @@ int awq_pack_rows(const int32_t* v, int64_t rows, int64_t n, int bits, int qmin,
  *   awq_weight_colsum  gmax_work fp32 [R * K/gs]; partial fp64 [ceil(R/256) * K] (this
  *                      linear's slice of the group's [sum_j ceil(R_j/256), K] array)
  *   awq_act_search_select work fp64 [n_grid * ceil(part_stride / 1024)]
- * n_grid <= AWQ_ACT_MAX_GRID. */
+ * n_grid <= AWQ_ACT_MAX_GRID; part_stride <= 6144 * 32 * 1024 groups (201 326 592: the
+ * select kernel's super-block sums of one candidate fit its LDS), else hipErrorInvalidValue. */
 #define AWQ_ACT_MAX_GRID 256
 
 int awq_act_stats(const void* x, int dtype, int64_t tokens, int64_t K, double* work, float* x_mean, float* x_sq,

@@ -125,3 +125,20 @@ def test_generic_kernel_still_serves_the_rest():
         assert torch.equal(Q(bits=4, group_size=100, symmetric=False).quantize(x)["tensor_q"], ref["tensor_q"])
     finally:
         os.environ.pop("AWQ_NO_ROWGROUP", None)
+
+
+@pytest.mark.parametrize("gpt", [24, 40, 64], ids=str)
+@pytest.mark.parametrize("dtype,shape,gs", [(torch.bfloat16, (37, 1000), 100), (torch.bfloat16, (9, 4100), 96),
+                                            (torch.float16, (5, 3001), 60), (torch.float32, (6, 2050), 48),
+                                            (torch.bfloat16, (200, 61), 7)], ids=str)
+def test_rowgroup_groups_per_tile_override(dtype, shape, gs, gpt):
+    """Groups per tile that are not powers of two (AWQ_RG_GPT tuning override, any multiple
+    of 8): P = the largest power of two <= 64 / the tile's groups, the row's light last
+    tile with more lanes per group, word-aligned tile boundaries — same bits as the oracle."""
+    import os
+    os.environ["AWQ_RG_GPT"] = str(gpt)
+    try:
+        for bits, sym in ((4, False), (8, True)):
+            _assert_parity(rand(shape, gpt + gs + bits, 0.5, dtype), gs, bits, sym)
+    finally:
+        os.environ.pop("AWQ_RG_GPT", None)

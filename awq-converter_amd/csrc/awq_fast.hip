@@ -1018,7 +1018,7 @@ __device__ __forceinline__ void rg_reduce(int& smax, uint32_t& umax, uint32_t& u
 
 // LDS: the segment's stage (dynamic, sized by the launch to the tile: 1.6-8 KiB) + 1.3 KiB
 template <typename F, int BITS, bool SYM, int SPLIT>
-__global__ __launch_bounds__(64, 8) void awq_rowgroup_kernel(const void* __restrict__ w, int64_t rows, int64_t K,
+__global__ __launch_bounds__(128) void awq_rowgroup_kernel(const void* __restrict__ w, int64_t rows, int64_t K,
                                                              int64_t L, int lgP, int GPT, uint32_t tiles_per_row,
                                                              int64_t G, int C, float invL,
                                                              int32_t* __restrict__ qweight, int32_t* __restrict__ qzeros,
@@ -1034,7 +1034,10 @@ __global__ __launch_bounds__(64, 8) void awq_rowgroup_kernel(const void* __restr
     S* stage = (S*)rg_lds;                              // rg_stage_bytes(): the segment + its alignment skew
     __shared__ uint32_t zst[64];
     __shared__ float4 prm[64];                          // per group: r, z, s, special
-    const int lane = threadIdx.x;
+    __shared__ int not_plain;                           // a group of the tile needs the full quotient
+    // one tile per workgroup of 1 or 2 waves (host-chosen: two waves share a large tile's LDS
+    // stage, so a whole-row tile keeps 8 waves per SIMD resident)
+    const int lane = threadIdx.x, NT = blockDim.x;
     // (host-side G, C, log2 P and a 32-bit tile split: 64-bit divisions per wave on the
     //  CU's shared scalar unit were a visible part of the per-tile cost)
     const uint32_t tile = blockIdx.x;   // (an XCD-contiguous tile order measured no different: r2z3)
@@ -1043,7 +1046,7 @@ __global__ __launch_bounds__(64, 8) void awq_rowgroup_kernel(const void* __restr
     const int64_t g0 = (int64_t)(tile - r32 * tiles_per_row) * GPT;
     const int ng = (int)min((int64_t)GPT, G - g0);
     if (ng < GPT) {   // the row's last, partial tile: more lanes per group (wave-uniform)
-        lgP = 31 - __builtin_clz(64u / (unsigned)ng);
+        lgP = min(6, 31 - __builtin_clz((unsigned)NT / (unsigned)ng));
         C = (int)((L + (1 << lgP) - 1) >> lgP);
     }
     const int P = 1 << lgP;
@@ -1062,20 +1065,20 @@ __global__ __launch_bounds__(64, 8) void awq_rowgroup_kernel(const void* __restr
         // every 16-B load of the segment in flight before the first LDS store (a load ->
         // store loop waits out one memory round trip per load); lanes past the end repeat
         // the last chunk's address and store nothing
-        for (int c0 = 0; c0 < nch; c0 += 512) {
+        for (int c0 = 0; c0 < nch; c0 += 8 * NT) {
             u4 v[8];
 #pragma unroll
             for (int k = 0; k < 8; ++k)
-                if (c0 + 64 * k < nch)                   // wave-uniform
-                    v[k] = __builtin_amdgcn_raw_buffer_load_b128(rw, (uint32_t)(16 * min(c0 + 64 * k + lane, nch - 1)),
+                if (c0 + NT * k < nch)                   // uniform
+                    v[k] = __builtin_amdgcn_raw_buffer_load_b128(rw, (uint32_t)(16 * min(c0 + NT * k + lane, nch - 1)),
                                                                  0, AWQ_LOAD_AUX);
 #pragma unroll
             for (int k = 0; k < 8; ++k)
-                if (c0 + 64 * k + lane < nch) *(u4*)((char*)stage + 16 * (c0 + 64 * k + lane)) = v[k];
+                if (c0 + NT * k + lane < nch) *(u4*)((char*)stage + 16 * (c0 + NT * k + lane)) = v[k];
         }
     } else
 #pragma unroll 4
-    for (int c = lane; c < nch; c += 64) {
+    for (int c = lane; c < nch; c += NT) {
         if (__builtin_expect(16u * c + 16u <= lim, 1)) {
             *(u4*)((char*)stage + 16 * c) = __builtin_amdgcn_raw_buffer_load_b128(rw, (uint32_t)(16 * c), 0, AWQ_LOAD_AUX);
         } else {   // the tensor's last bytes: a 16-B load straddling the range end would read as all zeros
@@ -1083,9 +1086,8 @@ __global__ __launch_bounds__(64, 8) void awq_rowgroup_kernel(const void* __restr
                 ((uint16_t*)stage)[8 * c + h] = __builtin_amdgcn_raw_buffer_load_b16(rw, (uint32_t)(16 * c + 2 * h), 0, 0);
         }
     }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (lane == 0) not_plain = 0;
+    __syncthreads();
     // ---- this lane's chunk of its group ----
     const int grp = lane >> lgP, j = lane & (P - 1);
     const bool active = grp < ng;
@@ -1175,7 +1177,7 @@ __global__ __launch_bounds__(64, 8) void awq_rowgroup_kernel(const void* __restr
     const GroupParams p = params_from_range<F, BITS, SYM>(gmn, gmx);
     const bool special = !F::fast(p.r);
     // wave-uniform: every group of the tile admits the plain quotient (F::plain_ok)
-    const bool plain = F::kHasPlain && __builtin_amdgcn_ballot_w64(active && !F::plain_ok(p.s)) == 0;
+    if (F::kHasPlain && active && j == 0 && !F::plain_ok(p.s)) not_plain = 1;
     if (active && j == 0) {
         const int64_t gi = r * G + g0 + grp;
         if (scales) scales[gi] = f16_bits(p.s);
@@ -1183,9 +1185,9 @@ __global__ __launch_bounds__(64, 8) void awq_rowgroup_kernel(const void* __restr
         zst[grp] = __builtin_isnan(p.z) ? NANF : ((uint32_t)((int)p.z - QMIN) & MASK);
         prm[grp] = (float4){p.r, p.z, p.s, special ? 1.0f : 0.0f};
     }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    __syncthreads();
+    // uniform: every group of the tile admits the plain quotient (F::plain_ok)
+    const bool plain = F::kHasPlain && not_plain == 0;
     // ---- pass 2: lane = 8 consecutive elements of the segment (one qweight word at 4 bits):
     //      its groups' parameters from LDS, quantize, pack, store (kb is a word boundary) ----
     const int nck = (n_el + 7) >> 3;
@@ -1193,7 +1195,7 @@ __global__ __launch_bounds__(64, 8) void awq_rowgroup_kernel(const void* __restr
                                                           // for e < 2^13, L <= 512 (host-computed)
     const int64_t wpr = (K + PER - 1) / PER;
     int32_t* qdst = qweight ? qweight + r * wpr + kb / PER : nullptr;
-    for (int c = lane; c < nck; c += 64) {
+    for (int c = lane; c < nck; c += NT) {
         const int e0c = 8 * c;
         const bool tail = e0c + 8 > n_el;                 // the row's last, partial chunk
         float x[8];
@@ -1530,21 +1532,42 @@ hipError_t launch_fast(const awq_tensor_desc* descs_dev, const int32_t* block_te
     return hipPeekAtLastError();
 }
 
-// Row-segment tiles of awq_rowgroup_kernel: groups per tile GPT (8..64, a power of two: tile
-// boundaries on packed-word boundaries) minimising a per-row cost fitted to measurements
-// (profiles/round2/r2_rowgroup/r2r_*: 14336 x 4096, group sizes 48 / 100, GPT 8..32):
-// tiles x (fixed wave cost 8 + 0.6 per element of a lane's pass-1 chunk C = L / (64 / GPT)
-// + 2.3 per 512-element pass-2 sweep); 0 if the shape does not fit the LDS stage.
-int rowgroup_gpt(int dtype, int64_t K, int64_t L) {
-    if (dtype != AWQ_DTYPE_BF16 && dtype != AWQ_DTYPE_F16 && dtype != AWQ_DTYPE_F32) return 0;
+// Row-segment tiles of awq_rowgroup_kernel.  Whole-row tiles shared by two waves when a
+// 16-bit row of >= 2560 elements has <= 64 groups and fits a 16 KiB stage (r2ae / r2af: a
+// whole-row tile runs 1 059 VALU per row against 1 551 for 16-group one-wave tiles, and two
+// waves per LDS stage keep the SIMDs occupied; r2ag: +8..44 % at K = 3000 / 4096, e.g. bf16
+// gs 100 47.6 -> 42.5 us; -10..15 % at K = 2048, hence the threshold).  Otherwise one wave per tile and GPT (8..64, a power of two) from a
+// per-row cost fitted to measurements (profiles/round2/r2_rowgroup/r2r_*: 14336 x 4096,
+// group sizes 48 / 100, GPT 8..32): tiles x (fixed wave cost 8 + 0.6 per element of a
+// lane's pass-1 chunk C = L / (64 / GPT) + 2.3 per 512-element pass-2 sweep).  gpt = 0 if
+// the shape does not fit the LDS stage.  AWQ_RG_GPT / AWQ_RG_WAVES override (tuning).
+struct RgPlan {
+    int gpt, waves;
+};
+RgPlan rowgroup_plan(int dtype, int64_t K, int64_t L) {
+    RgPlan pl = {0, 1};
+    if (dtype != AWQ_DTYPE_BF16 && dtype != AWQ_DTYPE_F16 && dtype != AWQ_DTYPE_F32) return pl;
     const int64_t es = dtype == AWQ_DTYPE_F32 ? 4 : 2;
-    if (L <= 0 || K <= 0 || 8 * L * es > kRgStageBytes) return 0;
-    if (const char* e = getenv("AWQ_RG_GPT")) {        // tuning override (scripts/generic_bench.py)
+    if (L <= 0 || K <= 0 || 8 * L * es > kRgStageBytes) return pl;
+    const char* ew = getenv("AWQ_RG_WAVES");
+    if (ew) {
+        const int v = atoi(ew);
+        if (v == 1 || v == 2) pl.waves = v;
+    }
+    if (const char* e = getenv("AWQ_RG_GPT")) {
         const int v = atoi(e);
-        if (v >= 8 && v <= 64 && v % 8 == 0 && v * L * es <= kRgStageMax) return v;
+        if (v >= 8 && v <= 64 && v % 8 == 0 && v * L * es <= kRgStageMax) {
+            pl.gpt = v;
+            return pl;
+        }
     }
     const int64_t G = (K + L - 1) / L;
-    int best = 0;
+    const int64_t whole = (G + 7) / 8 * 8;
+    if (!ew && es == 2 && K >= 2560 && whole <= 64 && whole * L * es <= kRgStageMax) {
+        pl.gpt = (int)whole;
+        pl.waves = 2;
+        return pl;
+    }
     double best_cost = 0.0;
     for (int gpt = 8; gpt <= 64; gpt *= 2) {
         if (gpt * L * es > kRgStageBytes) break;
@@ -1552,22 +1575,25 @@ int rowgroup_gpt(int dtype, int64_t K, int64_t L) {
         const int64_t C = (L + (64 / gpt) - 1) / (64 / gpt);
         const int64_t el = min((int64_t)gpt, G) * L;                  // elements of a full tile
         const double cost = (double)tiles * (8.0 + 0.6 * (double)C + 2.3 * (double)((el + 511) / 512));
-        if (best == 0 || cost < best_cost) { best_cost = cost; best = gpt; }
+        if (pl.gpt == 0 || cost < best_cost) { best_cost = cost; pl.gpt = gpt; }
     }
-    return best;
+    return pl;
 }
+int rowgroup_gpt(int dtype, int64_t K, int64_t L) { return rowgroup_plan(dtype, K, L).gpt; }
 
 hipError_t launch_rowgroup(const void* w, int dtype, int64_t rows, int64_t K, int64_t L, int bits, int symmetric,
                            int32_t* qweight, int32_t* qzeros, uint16_t* scales, int32_t* tensor_q, int32_t* zeros,
                            hipStream_t stream) {
-    const int gpt = rowgroup_gpt(dtype, K, L);
+    const RgPlan pl = rowgroup_plan(dtype, K, L);
+    const int gpt = pl.gpt;
     if (gpt == 0 || rows <= 0) return hipErrorInvalidValue;
     const int64_t G = (K + L - 1) / L;
     const int64_t tpr = (G + gpt - 1) / gpt;
-    const int lgP = 31 - __builtin_clz((unsigned)(64 / gpt));   // P = lanes per group: a power of two
+    const int nt = 64 * pl.waves;                                      // threads per tile
+    const int lgP = min(6, 31 - __builtin_clz((unsigned)(nt / gpt)));  // P = lanes per group: a power of two
     const int P = 1 << lgP;
     const int C = (int)((L + P - 1) / P);
-    const dim3 grid((unsigned)(rows * tpr)), block(64);
+    const dim3 grid((unsigned)(rows * tpr)), block((unsigned)nt);
     // stage: the tile's elements rounded up to 16 B, + the up-to-16-B alignment skew and the
     // last 8-element vector read past the segment end
     const size_t lds = ((size_t)gpt * L * (dtype == AWQ_DTYPE_F32 ? 4 : 2) + 15) / 16 * 16 + 48;

@@ -1195,7 +1195,9 @@ __global__ __launch_bounds__(128) void awq_rowgroup_kernel(const void* __restric
                                                           // for e < 2^13, L <= 512 (host-computed)
     const int64_t wpr = (K + PER - 1) / PER;
     int32_t* qdst = qweight ? qweight + r * wpr + kb / PER : nullptr;
-    for (int c = lane; c < nck; c += NT) {
+    float efA = 8.0f * (float)lane + 0.5f;                // e0c + 0.5 as an exact float induction
+    const float efStep = 8.0f * (float)NT;
+    for (int c = lane; c < nck; c += NT, efA += efStep) {
         const int e0c = 8 * c;
         const bool tail = e0c + 8 > n_el;                 // the row's last, partial chunk
         float x[8];
@@ -1226,10 +1228,10 @@ __global__ __launch_bounds__(128) void awq_rowgroup_kernel(const void* __restric
         float rr[8], zz[8], ss[8];
         bool spec;
         if constexpr (SPLIT == 8 || SPLIT == 4) {
-            const int gA = min((int)(((float)e0c + 0.5f) * invL), ng - 1);
+            const int gA = (int)(efA * invL);             // < ng: e0c < n_el
             const float4 pA = prm[gA];
             float4 pB = pA;
-            if constexpr (SPLIT == 4) pB = prm[min((int)(((float)(e0c + 4) + 0.5f) * invL), ng - 1)];
+            if constexpr (SPLIT == 4) pB = prm[min((int)((efA + 4.0f) * invL), ng - 1)];
             spec = pA.w != 0.0f || pB.w != 0.0f;
 #pragma unroll
             for (int i = 0; i < 8; ++i) {

@@ -70,7 +70,9 @@ bool rowgroup_ok(int dtype, int64_t rows, int64_t K, int64_t group_size, const v
 extern "C" {
 
 int awq_packs_directly(int dtype, int64_t rows, int64_t K, int64_t group_size) {
-    return (fast_eligible(dtype, rows, K, group_size) || rowgroup_shape(dtype, rows, K, group_size)) ? 1 : 0;
+    // every kernel writes qweight / qzeros directly since the generic kernel's span rewrite
+    (void)rows; (void)K; (void)group_size;
+    return (dtype >= AWQ_DTYPE_BF16 && dtype <= AWQ_DTYPE_F64) ? 1 : 0;
 }
 
 int awq_abi_version(void) { return AWQ_HIP_ABI_VERSION; }
@@ -109,7 +111,6 @@ int awq_quantize_groups(const void* w, int dtype, int64_t rows, int64_t K, int32
     if (rows * K == 0) return AWQ_OK;
     if (!w) return fail(AWQ_EINVAL, "null input");
     hipStream_t s = (hipStream_t)stream;
-    const int qmin = symmetric ? -(1 << (bits - 1)) : 0;
     if (fast_eligible(dtype, rows, K, group_size) && aligned(w, 16) && (!qweight || aligned(qweight, 8)) &&
         (!tensor_q || aligned(tensor_q, 16)) && (!zeros || aligned(zeros, 4)) && (!qzeros || aligned(qzeros, 4)) &&
         (!scales || aligned(scales, 2))) {
@@ -123,21 +124,9 @@ int awq_quantize_groups(const void* w, int dtype, int64_t rows, int64_t K, int32
     if (rowgroup_ok(dtype, rows, K, group_size, w, qweight, qzeros, scales, tensor_q, zeros))
         return hip_status(awq::launch_rowgroup(w, dtype, rows, K, group_size, bits, symmetric, qweight, qzeros, scales,
                                                tensor_q, zeros, s), "awq row-group kernel");
-    // generic path: per-group int32 values first, then packing (needs tensor_q / zeros buffers)
-    if ((qweight && !tensor_q) || (qzeros && !zeros))
-        return fail(AWQ_EINVAL, "this shape/dtype takes the generic kernel: packed outputs need the int32 "
-                                "tensor_q/zeros buffers as staging (pass them too)");
-    if (int rc = hip_status(awq::launch_generic(w, dtype, rows, K, group_size, bits, symmetric, tensor_q,
-                                                scales, zeros, s), "awq generic kernel"))
-        return rc;
-    const int64_t G = (K + group_size - 1) / group_size;
-    if (qweight)
-        if (int rc = hip_status(awq::launch_pack(tensor_q, rows, K, bits, qmin, qweight, s), "awq pack"))
-            return rc;
-    if (qzeros)
-        if (int rc = hip_status(awq::launch_pack(zeros, rows, G, bits, qmin, qzeros, s), "awq pack"))
-            return rc;
-    return AWQ_OK;
+    // generic path (fp64, groups > 512): one wave per qzeros word's span, packed words direct
+    return hip_status(awq::launch_generic(w, dtype, rows, K, group_size, bits, symmetric, tensor_q, scales, zeros,
+                                          qweight, qzeros, s), "awq generic kernel");
 }
 
 int awq_quantize_search(const void* w, int dtype, int64_t rows, int64_t K, int32_t group_size32, int bits,
@@ -155,7 +144,6 @@ int awq_quantize_search(const void* w, int dtype, int64_t rows, int64_t K, int32
     if (rows * K == 0) return AWQ_OK;
     if (!w) return fail(AWQ_EINVAL, "null input");
     hipStream_t s = (hipStream_t)stream;
-    const int qmin = symmetric ? -(1 << (bits - 1)) : 0;
     if (fast_eligible(dtype, rows, K, group_size) && aligned(w, 16) && (!qweight || aligned(qweight, 8)) &&
         (!tensor_q || aligned(tensor_q, 16)) && (!zeros || aligned(zeros, 4)) && (!qzeros || aligned(qzeros, 4)) &&
         (!scales || aligned(scales, 2))) {
@@ -167,20 +155,8 @@ int awq_quantize_search(const void* w, int dtype, int64_t rows, int64_t K, int32
                                            (int)group_size, (K % group_size) != 0, s, n_grid, n_candidates),
                           "awq fast search kernel");
     }
-    if ((qweight && !tensor_q) || (qzeros && !zeros))
-        return fail(AWQ_EINVAL, "packed outputs of the generic search kernel need the int32 tensor_q/zeros "
-                                "buffers as staging (pass them too)");
-    if (int rc = hip_status(awq::launch_generic(w, dtype, rows, K, group_size, bits, symmetric, tensor_q,
-                                                scales, zeros, s, n_grid, n_candidates), "awq search kernel"))
-        return rc;
-    const int64_t G = (K + group_size - 1) / group_size;
-    if (qweight)
-        if (int rc = hip_status(awq::launch_pack(tensor_q, rows, K, bits, qmin, qweight, s), "awq pack"))
-            return rc;
-    if (qzeros)
-        if (int rc = hip_status(awq::launch_pack(zeros, rows, G, bits, qmin, qzeros, s), "awq pack"))
-            return rc;
-    return AWQ_OK;
+    return hip_status(awq::launch_generic(w, dtype, rows, K, group_size, bits, symmetric, tensor_q, scales, zeros,
+                                          qweight, qzeros, s, n_grid, n_candidates), "awq search kernel");
 }
 
 int awq_group_params(const void* w, int dtype, int64_t rows, int64_t K, int64_t group_size, int bits,
@@ -192,7 +168,8 @@ int awq_group_params(const void* w, int dtype, int64_t rows, int64_t K, int64_t 
     if (rows * K == 0) return AWQ_OK;
     if (!w) return fail(AWQ_EINVAL, "null input");
     return hip_status(awq::launch_generic(w, dtype, rows, K, group_size, bits, symmetric, nullptr, nullptr, nullptr,
-                                          (hipStream_t)stream, 1, 0, scales, zeros), "awq group params");
+                                          nullptr, nullptr, (hipStream_t)stream, 1, 0, scales, zeros),
+                      "awq group params");
 }
 
 int awq_apply_params(const void* x, int dtype, int64_t rows, int64_t K, int64_t group_size, const double* scales,

@@ -5,8 +5,9 @@
 // reference awq.py:337-339) and the small-tensor path (numel < group_size, awq.py:130-171,
 // expressed by the caller as one group per row: group_size = K).
 //
-// One wave per group: lanes stride over the group's elements, min/max/NaN reduced across
-// the wave with cross-lane shuffles, then a second pass (L1/L2-hot) quantizes.  Each
+// One wave per span of groups (one qzeros word): lanes stride over a group's elements,
+// min/max/NaN reduced across the wave with cross-lane shuffles, then a pass over the span
+// (L1/L2-hot) quantizes and packs.  Each
 // element-wise op of the reference is evaluated the way torch's CPU kernels do for the
 // input dtype D: fp32 math (fp64 for D = fp64), then round-to-nearest-even to D
 // (software RNE here — independent of the hardware conversions the fast kernel uses),
@@ -24,84 +25,136 @@ using namespace refmath;
 // fp16(fp16(q - z) * fp16(s)), awq.py:459-539) has the smallest squared error wins; ties and
 // NaN/inf groups keep i = 0, i.e. exactly the RTN result.  Group size <= 512 (one 8-element
 // chunk per lane).
+//
+// One wave per SPAN = the PER = 32 / bits consecutive groups of a row whose zero points share
+// one qzeros word (the row's last span may hold fewer).  A span starts at element s * PER * L
+// of its row, a multiple of PER, so its packed qweight words are whole too: after the
+// per-group passes (min/max/NaN, then the parameters), one pass over the span quantizes lane
+// by lane (element span0 + 64 i + lane, its group found by a running index) and ORs each
+// aligned run of PER lanes into one qweight word with cross-lane shuffles.  qweight / qzeros
+// are written directly for every group size (no int32 staging, no pack pass: round 1 staged
+// 4 B per element and re-read it); tensor_q / zeros / scales / exact parameters are optional.
 template <int DT, bool SEARCH>
 __global__ __launch_bounds__(256) void awq_generic_kernel(const void* __restrict__ wv, int64_t rows,
-                                                          int64_t K, int64_t L, int qmin, int qmax,
+                                                          int64_t K, int64_t L, int bits, int qmin, int qmax,
                                                           int sym, int n_grid, int n_cand,
                                                           int32_t* __restrict__ tensor_q,
                                                           uint16_t* __restrict__ scales,
                                                           int32_t* __restrict__ zeros,
+                                                          int32_t* __restrict__ qweight,
+                                                          int32_t* __restrict__ qzeros,
                                                           double* __restrict__ s_exact,
                                                           double* __restrict__ z_exact) {
     typedef Traits<DT> T;
     typedef typename T::C C;
     const typename T::S* w = (const typename T::S*)wv;
     const int lane = threadIdx.x & 63;
+    const int per = 32 / bits;                       // 8 (4-bit) or 4 (8-bit)
+    const uint32_t mask = (1u << bits) - 1u;
     const int64_t G = (K + L - 1) / L;
-    const int64_t ngroups = rows * G;
+    const int64_t SP = (G + per - 1) / per;          // spans per row = qzeros words per row
+    const int64_t wpr = (K + per - 1) / per;         // qweight words per row
+    const int64_t nspans = rows * SP;
     const int64_t wave = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     const int64_t nwaves = (int64_t)gridDim.x * 4;
-    for (int64_t gi = wave; gi < ngroups; gi += nwaves) {
-        const int64_t r = gi / G, g = gi - r * G;
-        const int64_t k0 = g * L;
-        int64_t k1 = k0 + L;
-        const bool padded = k1 > K;                  // awq.py:337-339 zero padding
-        if (k1 > K) k1 = K;
+    for (int64_t si = wave; si < nspans; si += nwaves) {
+        const int64_t r = si / SP, sp = si - r * SP;
+        const int64_t g0 = sp * per;
+        const int ng = (int)((G - g0) < per ? (G - g0) : per);
         const int64_t base = r * K;
-        C mn = padded ? (C)0 : (C)INFINITY, mx = padded ? (C)0 : (C)-INFINITY;
-        int nan = 0;
-        for (int64_t k = k0 + lane; k < k1; k += 64) {
-            C v = T::load(w, base + k);
-            nan |= (v != v);
-            mn = v < mn ? v : mn;
-            mx = v > mx ? v : mx;
-        }
-        mn = wave_min(mn);
-        mx = wave_max(mx);
-        nan = wave_or(nan);
-        if (nan) { mn = (C)NAN; mx = (C)NAN; }
-        if (SEARCH && !nan) {
-            if (sym) {
-                C a = (absv(mx) > absv(mn)) ? absv(mx) : absv(mn);
-                mn = -a;
-                mx = a;
+        C sa[8], za[8];
+        uint32_t zword = 0;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            sa[j] = (C)0;
+            za[j] = (C)0;
+            if (j >= ng) continue;
+            const int64_t gi = r * G + g0 + j;
+            const int64_t k0 = (g0 + j) * L;
+            int64_t k1 = k0 + L;
+            const bool padded = k1 > K;                  // awq.py:337-339 zero padding
+            if (k1 > K) k1 = K;
+            C mn = padded ? (C)0 : (C)INFINITY, mx = padded ? (C)0 : (C)-INFINITY;
+            int nan = 0;
+            for (int64_t k = k0 + lane; k < k1; k += 64) {
+                C v = T::load(w, base + k);
+                nan |= (v != v);
+                mn = v < mn ? v : mn;
+                mx = v > mx ? v : mx;
             }
-            C best = (C)INFINITY;
-            int bi = 0;
-            for (int i = 0; i < n_cand; ++i) {
-                const C al = (C)(n_grid - i) / (C)n_grid;
-                C cs, cz;
-                group_params<DT>(T::rn(mn * al), T::rn(mx * al), 0, qmin, qmax, sym, cs, cz);
-                const float sh = sw_f16_to_f32(canon_f16((float)cs));
-                // canonical error sum (include/awq_hip.h): lane l sums chunk l = elements
-                // 8l .. 8l+7 of the group in order, then the pairwise tree over the lanes
-                C acc = (C)0;
-                const int64_t c0 = k0 + 8 * lane, c1 = (c0 + 8 < k1) ? c0 + 8 : k1;
-                for (int64_t k = c0; k < c1; ++k) {
-                    const C v = T::load(w, base + k);
-                    const C q = quant1<DT>(v, cs, cz, qmin, qmax);
-                    const float h = sw_f16_to_f32(sw_f32_to_f16((float)(q - cz)));
-                    const C d = v - (C)sw_f16_to_f32(sw_f32_to_f16(h * sh));
-                    acc = acc + d * d;
+            mn = wave_min(mn);
+            mx = wave_max(mx);
+            nan = wave_or(nan);
+            if (nan) { mn = (C)NAN; mx = (C)NAN; }
+            if (SEARCH && !nan) {
+                if (sym) {
+                    C a = (absv(mx) > absv(mn)) ? absv(mx) : absv(mn);
+                    mn = -a;
+                    mx = a;
                 }
-                acc = wave_sum(acc);
-                if (acc < best) { best = acc; bi = i; }
+                C best = (C)INFINITY;
+                int bi = 0;
+                for (int i = 0; i < n_cand; ++i) {
+                    const C al = (C)(n_grid - i) / (C)n_grid;
+                    C cs, cz;
+                    group_params<DT>(T::rn(mn * al), T::rn(mx * al), 0, qmin, qmax, sym, cs, cz);
+                    const float sh = sw_f16_to_f32(canon_f16((float)cs));
+                    // canonical error sum (include/awq_hip.h): lane l sums chunk l = elements
+                    // 8l .. 8l+7 of the group in order, then the pairwise tree over the lanes
+                    C acc = (C)0;
+                    const int64_t c0 = k0 + 8 * lane, c1 = (c0 + 8 < k1) ? c0 + 8 : k1;
+                    for (int64_t k = c0; k < c1; ++k) {
+                        const C v = T::load(w, base + k);
+                        const C q = quant1<DT>(v, cs, cz, qmin, qmax);
+                        const float h = sw_f16_to_f32(sw_f32_to_f16((float)(q - cz)));
+                        const C d = v - (C)sw_f16_to_f32(sw_f32_to_f16(h * sh));
+                        acc = acc + d * d;
+                    }
+                    acc = wave_sum(acc);
+                    if (acc < best) { best = acc; bi = i; }
+                }
+                const C al = (C)(n_grid - bi) / (C)n_grid;
+                mn = T::rn(mn * al);
+                mx = T::rn(mx * al);
             }
-            const C al = (C)(n_grid - bi) / (C)n_grid;
-            mn = T::rn(mn * al);
-            mx = T::rn(mx * al);
+            C s, z;
+            group_params<DT>(mn, mx, nan, qmin, qmax, sym, s, z);
+            sa[j] = s;
+            za[j] = z;
+            zword |= (((uint32_t)to_i32(z) - (uint32_t)qmin) & mask) << (bits * j);
+            if (lane == 0) {
+                if (scales) scales[gi] = canon_f16((float)s);         // fp64: via fp32 (awq.py:327)
+                if (zeros) zeros[gi] = to_i32(z);
+                if (s_exact) s_exact[gi] = (double)s;                 // the input dtype's values, exact
+                if (z_exact) z_exact[gi] = (double)z;
+            }
         }
-        C s, z;
-        group_params<DT>(mn, mx, nan, qmin, qmax, sym, s, z);
-        if (lane == 0) {
-            if (scales) scales[gi] = canon_f16((float)s);         // fp64: via fp32 (awq.py:327)
-            if (zeros) zeros[gi] = to_i32(z);
-            if (s_exact) s_exact[gi] = (double)s;                 // the input dtype's values, exact
-            if (z_exact) z_exact[gi] = (double)z;
-        }
-        if (tensor_q) {
-            for (int64_t k = k0 + lane; k < k1; k += 64)
-                tensor_q[base + k] = to_i32(quant1<DT>(T::load(w, base + k), s, z, qmin, qmax));
+        if (qzeros && lane == 0) qzeros[r * SP + sp] = (int32_t)zword;
+        if (!tensor_q && !qweight) continue;
+        // quantize the span: element k = span0 + 64 i + lane of group j (running index, rem = k - j L)
+        const int64_t span0 = g0 * L;
+        int64_t span1 = span0 + (int64_t)ng * L;
+        if (span1 > K) span1 = K;
+        int j = 0;
+        int64_t rem = lane;
+        while (rem >= L) { rem -= L; ++j; }
+        const int sh = bits * (lane & (per - 1));
+        for (int64_t k = span0 + lane; k - lane < span1; k += 64) {
+            const bool act = k < span1;
+            C s = sa[0], z = za[0];
+#pragma unroll
+            for (int jj = 1; jj < 8; ++jj)
+                if (j == jj) { s = sa[jj]; z = za[jj]; }
+            int32_t q = 0;
+            if (act) q = to_i32(quant1<DT>(T::load(w, base + k), s, z, qmin, qmax));
+            if (tensor_q && act) tensor_q[base + k] = q;
+            if (qweight) {
+                uint32_t wd = act ? (((uint32_t)q - (uint32_t)qmin) & mask) << sh : 0u;
+                for (int o = 1; o < per; o <<= 1) wd |= (uint32_t)__shfl_xor((int)wd, o, 64);
+                if (act && (lane & (per - 1)) == 0) qweight[r * wpr + k / per] = (int32_t)wd;
+            }
+            rem += 64;
+            while (rem >= L) { rem -= L; ++j; }
         }
     }
 }
@@ -183,6 +236,52 @@ __global__ __launch_bounds__(256) void awq_dequant_kernel(
     }
 }
 
+// awq_dequantize_packed for word-aligned groups (K % PER == 0, L % PER == 0; PER = 32 / bits):
+// one thread per qweight word — its PER elements share one row and one group — so one
+// division per word instead of three per element, one scale and one qzeros load per word,
+// and the PER fp32 outputs leave as 16-B stores.  Arithmetic (awq.py:459-539): q - z is an
+// integer of at most 8 bits, exact in fp16; h * s of that integer and an fp16 scale needs
+// at most 19 significand bits, so the f32 product is exact and one hardware RNE conversion
+// to fp16 gives RN_f16(h * s) bit for bit (NaN lanes take the software conversion, which
+// keeps the payload as torch does).  Memory-bound: 0.5 B (4-bit) read + 4 B written per element.
+template <int BITS>
+__global__ __launch_bounds__(256) void awq_dequant_words_kernel(
+    const int32_t* __restrict__ qweight, const uint16_t* __restrict__ scales, const int32_t* __restrict__ qzeros,
+    int64_t words, uint32_t wpr, uint32_t L, uint32_t G, uint32_t zpr, int qmin, float* __restrict__ out) {
+    constexpr int PER = 32 / BITS;
+    constexpr uint32_t MASK = (1u << BITS) - 1u;
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= words) return;
+    int64_t r;
+    uint32_t c;
+    if (words <= (int64_t)0xFFFFFFFFu) {                 // 32-bit index arithmetic
+        const uint32_t r32 = (uint32_t)i / wpr;
+        r = r32;
+        c = (uint32_t)i - r32 * wpr;
+    } else {
+        r = i / wpr;
+        c = (uint32_t)(i - r * wpr);
+    }
+    const uint32_t g = (c * PER) / L;
+    const uint32_t wq = (uint32_t)__builtin_nontemporal_load(qweight + i);
+    const float s = (float)__builtin_bit_cast(_Float16, scales[r * G + g]);
+    const int32_t z = (int32_t)(((uint32_t)qzeros[r * zpr + g / PER] >> (BITS * (g % PER))) & MASK) + qmin;
+    float v[PER];
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+        const int32_t q = (int32_t)((wq >> (BITS * j)) & MASK) + qmin;
+        const float p = (float)(q - z) * s;
+        v[j] = __builtin_isnan(p) ? sw_f16_to_f32(sw_f32_to_f16(p)) : (float)(_Float16)p;
+    }
+    typedef float f4 __attribute__((ext_vector_type(4)));
+    f4* o = (f4*)(out + i * PER);
+#pragma unroll
+    for (int j = 0; j < PER / 4; ++j) {
+        const f4 t = {v[4 * j], v[4 * j + 1], v[4 * j + 2], v[4 * j + 3]};
+        __builtin_nontemporal_store(t, o + j);
+    }
+}
+
 inline unsigned grid_for(int64_t work, int64_t per_block, int64_t cap) {
     int64_t b = (work + per_block - 1) / per_block;
     if (b < 1) b = 1;
@@ -194,22 +293,24 @@ inline unsigned grid_for(int64_t work, int64_t per_block, int64_t cap) {
 
 hipError_t launch_generic(const void* w, int dtype, int64_t rows, int64_t K, int64_t L, int bits,
                           int symmetric, int32_t* tensor_q, uint16_t* scales, int32_t* zeros,
-                          hipStream_t stream, int n_grid, int n_cand, double* s_exact, double* z_exact) {
+                          int32_t* qweight, int32_t* qzeros, hipStream_t stream, int n_grid, int n_cand,
+                          double* s_exact, double* z_exact) {
     const int qmin = symmetric ? -(1 << (bits - 1)) : 0;
     const int qmax = symmetric ? (1 << (bits - 1)) - 1 : (1 << bits) - 1;
+    const int per = 32 / bits;
     const int64_t G = (K + L - 1) / L;
-    const unsigned grid = grid_for(rows * G, 4, 256 * 16);
+    const unsigned grid = grid_for(rows * ((G + per - 1) / per), 4, 256 * 16);
     const bool search = n_cand > 0;
 #define AWQ_GEN(D)                                                                                   \
     do {                                                                                             \
         if (search)                                                                                  \
             hipLaunchKernelGGL((awq_generic_kernel<D, true>), dim3(grid), dim3(256), 0, stream, w, rows, \
-                               K, L, qmin, qmax, symmetric, n_grid, n_cand, tensor_q, scales, zeros,   \
-                               s_exact, z_exact);                                                      \
+                               K, L, bits, qmin, qmax, symmetric, n_grid, n_cand, tensor_q, scales,    \
+                               zeros, qweight, qzeros, s_exact, z_exact);                              \
         else                                                                                         \
             hipLaunchKernelGGL((awq_generic_kernel<D, false>), dim3(grid), dim3(256), 0, stream, w,     \
-                               rows, K, L, qmin, qmax, symmetric, 1, 0, tensor_q, scales, zeros,       \
-                               s_exact, z_exact);                                                      \
+                               rows, K, L, bits, qmin, qmax, symmetric, 1, 0, tensor_q, scales, zeros, \
+                               qweight, qzeros, s_exact, z_exact);                                     \
     } while (0)
     switch (dtype) {
     case AWQ_DTYPE_BF16: AWQ_GEN(AWQ_DTYPE_BF16); break;
@@ -264,6 +365,21 @@ hipError_t launch_dequant(const int32_t* tensor_q, const int32_t* qweight, const
                           int64_t L, int bits, int qmin, float* out, hipStream_t stream) {
     const int64_t total = rows * K;
     if (total <= 0) return hipSuccess;
+    const int per = 32 / bits;
+    const int64_t G = (K + L - 1) / L;
+    if (!tensor_q && K % per == 0 && L % per == 0 && ((uintptr_t)out & 15) == 0 && K / per <= 0x7FFFFFFF &&
+        L <= 0x7FFFFFFF && G <= 0x7FFFFFFF && total / per <= ((int64_t)1 << 40)) {
+        const int64_t words = total / per;
+        const uint32_t wpr = (uint32_t)(K / per), zpr = (uint32_t)((G + per - 1) / per);
+        const dim3 grid((unsigned)((words + 255) / 256)), block(256);
+        if (bits == 4)
+            hipLaunchKernelGGL(awq_dequant_words_kernel<4>, grid, block, 0, stream, qweight, scales, qzeros, words,
+                               wpr, (uint32_t)L, (uint32_t)G, zpr, qmin, out);
+        else
+            hipLaunchKernelGGL(awq_dequant_words_kernel<8>, grid, block, 0, stream, qweight, scales, qzeros, words,
+                               wpr, (uint32_t)L, (uint32_t)G, zpr, qmin, out);
+        return hipPeekAtLastError();
+    }
     hipLaunchKernelGGL(awq_dequant_kernel, dim3(grid_for(total, 256, 256 * 16)), dim3(256), 0, stream,
                        tensor_q, qweight, scales, zeros, qzeros, rows, K, L, bits, qmin, out);
     return hipPeekAtLastError();

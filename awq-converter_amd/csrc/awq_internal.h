@@ -109,7 +109,8 @@ hipError_t launch_fast(const awq_tensor_desc* descs_dev, const int32_t* block_te
                        int n_cand = 0);
 hipError_t launch_generic(const void* w, int dtype, int64_t rows, int64_t K, int64_t L, int bits,
                           int symmetric, int32_t* tensor_q, uint16_t* scales, int32_t* zeros,
-                          hipStream_t stream, int n_grid = 1, int n_cand = 0, double* s_exact = nullptr,
+                          int32_t* qweight, int32_t* qzeros, hipStream_t stream, int n_grid = 1,
+                          int n_cand = 0, double* s_exact = nullptr,
                           double* z_exact = nullptr);
 hipError_t launch_apply(const void* x, int dtype, int64_t rows, int64_t K, int64_t L, const double* scales,
                         const double* zeros, int qmin, int qmax, int mode, void* out, hipStream_t stream);

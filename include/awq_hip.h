@@ -82,8 +82,9 @@ int awq_device_check(char* arch, int len);
  *     (padded rows, awq.py:337-339): the streaming kernel;
  *   bf16 / fp16 with any other group_size <= 512 (fp32: <= 256), or any K: the row-segment
  *     kernel (packed outputs written directly);
- *   everything else (fp64, larger groups): the generic kernel, whose packed outputs need
- *     tensor_q / zeros as staging buffers (awq_packs_directly() == 0). */
+ *   everything else (fp64, larger groups): the generic kernel (one wave per span of groups
+ *     sharing a qzeros word; packed outputs written directly too, since round 2).
+ * tensor_q / zeros are optional outputs on every path. */
 int awq_quantize_groups(const void* w, int dtype, int64_t rows, int64_t K, int32_t group_size,
                         int bits, int symmetric, int32_t* qweight, int32_t* qzeros,
                         uint16_t* scales, int32_t* tensor_q, int32_t* zeros, void* stream);
@@ -100,7 +101,7 @@ int awq_quantize_groups(const void* w, int dtype, int64_t rows, int64_t K, int32
  * every kernel gets the same bits: chunk c = the group's elements 8c .. 8c+7 summed in
  * order, then a pairwise tree over 64 chunk slots, adjacent pairs first (empty slots = 0):
  * group_size <= 512.
- * Packed outputs need tensor_q / zeros as staging buffers. */
+ * tensor_q / zeros are optional outputs (no staging buffers needed). */
 int awq_quantize_search(const void* w, int dtype, int64_t rows, int64_t K, int32_t group_size, int bits,
                         int symmetric, int n_grid, int n_candidates, int32_t* qweight, int32_t* qzeros,
                         uint16_t* scales, int32_t* tensor_q, int32_t* zeros, void* stream);
@@ -124,7 +125,8 @@ int awq_apply_params(const void* x, int dtype, int64_t rows, int64_t K, int64_t 
                      const double* zeros, int qmin, int qmax, int mode, void* out, void* stream);
 
 /* 1 if awq_quantize_groups writes qweight / qzeros for this dtype / shape without the int32
- * tensor_q / zeros staging buffers (streaming or row-segment kernel; 16-B aligned input). */
+ * tensor_q / zeros staging buffers.  Since round 2 every kernel does (the generic kernel packs
+ * per span of groups), so this is 1 for every supported dtype; kept for ABI compatibility. */
 int awq_packs_directly(int dtype, int64_t rows, int64_t K, int64_t group_size);
 
 /* True (1) if a tensor of this dtype/shape is eligible for awq_quantize_ragged. */

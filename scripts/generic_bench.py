@@ -17,7 +17,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "awq-converter_amd")]
 import torch  # noqa: E402
 
-DT = {"bf16": torch.bfloat16, "f16": torch.float16, "f32": torch.float32}
+DT = {"bf16": torch.bfloat16, "f16": torch.float16, "f32": torch.float32, "f64": torch.float64}
 
 
 def main():
@@ -29,6 +29,7 @@ def main():
     ap.add_argument("--group-sizes", default="128")
     ap.add_argument("--bits", type=int, default=4)
     ap.add_argument("--compare-generic", action="store_true")
+    ap.add_argument("--dequant", action="store_true", help="also time dequantize_packed of the packed result")
     args = ap.parse_args()
     from awq_quantizer import _hip
     dev = torch.device("cuda", 0)
@@ -73,11 +74,29 @@ def one(args, _hip, dev, shape, name, gs, generic):
     nbytes = x.numel() * x.element_size()
     algo = nbytes + sum(t.numel() * t.element_size() for t in (qw, qz, sc))
     kernel = ("generic+pack" if stage and not args.search else "search" if args.search else
+              "generic" if generic or name == "f64" or gs > (256 if name == "f32" else 512) else
               "streaming" if _hip.ragged_eligible(DT[name], R, K, gs) else "row-segment")
     print(json.dumps({"dtype": name, "shape": [R, K], "group_size": gs, "bits": args.bits, "kernel": kernel,
                       "search": args.search, "us": round(us, 1), "input_GBs": round(nbytes / us / 1e3, 1),
                       "algorithmic_GBs": round(algo / us / 1e3, 1), "frac_8TBs": round(algo / us / 1e3 / 8000, 3)}),
           flush=True)
+    if args.dequant:
+        out = torch.empty(R, K, dtype=torch.float32, device=dev)
+
+        def dq():
+            _hip.dequantize_packed(qw, qz, sc, R, K, gs, args.bits, False, out)
+        for _ in range(3):
+            dq()
+        a.record()
+        for _ in range(args.iters):
+            dq()
+        b.record()
+        torch.cuda.synchronize()
+        us = a.elapsed_time(b) / args.iters * 1e3
+        algo = out.numel() * 4 + sum(t.numel() * t.element_size() for t in (qw, qz, sc))
+        print(json.dumps({"op": "dequantize_packed", "shape": [R, K], "group_size": gs, "bits": args.bits,
+                          "us": round(us, 1), "algorithmic_GBs": round(algo / us / 1e3, 1),
+                          "frac_8TBs": round(algo / us / 1e3 / 8000, 3)}), flush=True)
 
 
 if __name__ == "__main__":

@@ -1,0 +1,95 @@
+"""The generic kernel after its span rewrite (awq_generic.hip awq_generic_kernel): one wave per
+span of 32 / bits groups of a row (the groups sharing one qzeros word), qweight / qzeros
+packed in the kernel with cross-lane shuffles — no int32 staging, no pack pass.  It serves
+fp64 inputs and groups larger than the row-segment stage (> 512; fp32 > 256), and every
+dtype under AWQ_NO_ROWGROUP=1.  Reference arithmetic: awq.py:173-250 per group, awq.py:286-374
+for the row layout (zero-padded tail group), awq.py:130-171 for numel < group_size.
+
+Bar: bit-exact vs the oracle for tensor_q / zero_points / fp16 scales (quantize) and for the
+packed words (quantize_packed without staging buffers): group sizes below 64 lanes, not a
+multiple of the pack width, larger than a wave's stride, a row's last span with fewer
+groups, 4 / 8 bits, sym / asym, NaN / inf / constant groups, and the clip search."""
+import os
+
+import pytest
+import torch
+
+import golden_io as gio
+from oracle import awq_oracle as orc
+from test_gpu_rowgroup import Q, _assert_parity, _need_gpu, rand, specials  # noqa: F401
+
+pytestmark = pytest.mark.gpu
+
+F64_CASES = [  # (shape, group size): spans of 8 (4-bit) / 4 (8-bit) groups, ragged last spans
+    ((37, 1000), 100), ((5, 3001), 60), ((9, 4100), 96), ((3, 200), 7), ((4, 1024), 128),
+    ((6, 777), 37), ((2, 5000), 1000), ((3, 2048), 32), ((4097,), 100), ((3, 5, 70), 48),
+]
+
+
+@pytest.mark.parametrize("bits,sym", [(4, False), (4, True), (8, False), (8, True)], ids=str)
+@pytest.mark.parametrize("shape,gs", F64_CASES, ids=str)
+def test_generic_f64_vs_oracle(shape, gs, bits, sym):
+    _assert_parity(rand(shape, hash((shape, gs, bits, sym)) & 0xFFFF, 0.5, torch.float64), gs, bits, sym)
+
+
+@pytest.mark.parametrize("bits,sym", [(4, False), (8, True)], ids=str)
+@pytest.mark.parametrize("gs", [100, 13, 640], ids=str)
+def test_generic_f64_special_values(gs, bits, sym):
+    x = specials(rand((24, 1300), 7 + gs, 1.0), 11 + bits).to(torch.float64)
+    _assert_parity(x, gs, bits, sym)
+
+
+@pytest.mark.parametrize("dtype,shape,gs", [(torch.bfloat16, (7, 5000), 1000), (torch.float16, (3, 4500), 900),
+                                            (torch.float32, (5, 3000), 300), (torch.bfloat16, (2, 9000), 4500)],
+                         ids=str)
+def test_generic_large_groups(dtype, shape, gs):
+    """Groups beyond the row-segment stage: lanes stride over a group several times."""
+    for bits, sym in ((4, False), (8, True)):
+        _assert_parity(rand(shape, gs + bits, 0.5, dtype), gs, bits, sym)
+
+
+@pytest.mark.parametrize("dtype,shape,gs", [(torch.bfloat16, (37, 1000), 100), (torch.float16, (9, 777), 3),
+                                            (torch.float32, (13, 4100), 128)], ids=str)
+def test_generic_forced_by_env(dtype, shape, gs):
+    """AWQ_NO_ROWGROUP=1 sends the row-segment shapes to the generic kernel: same bits."""
+    os.environ["AWQ_NO_ROWGROUP"] = "1"
+    try:
+        for bits, sym in ((4, False), (4, True), (8, False)):
+            _assert_parity(specials(rand(shape, gs + bits, 0.5), 3).to(dtype), gs, bits, sym)
+    finally:
+        os.environ.pop("AWQ_NO_ROWGROUP", None)
+
+
+@pytest.mark.parametrize("gs", [100, 64], ids=str)
+def test_generic_f64_search_packed(gs):
+    """Clip search on fp64 (generic kernel): the packed words are the oracle's search result packed."""
+    from awq_quantizer import _hip
+    x = rand((9, 1000), 21 + gs, 0.5, torch.float64)
+    rows, K = x.shape
+    G = -(-K // gs)
+    ref = orc.quantize(x, bits=4, group_size=gs, symmetric=False, search=(20, 10))
+    d = x.to("cuda")
+    qw = torch.empty(rows, -(-K // 8), dtype=torch.int32, device="cuda")
+    qz = torch.empty(rows, -(-G // 8), dtype=torch.int32, device="cuda")
+    sc = torch.empty(rows, G, dtype=torch.float16, device="cuda")
+    _hip.quantize_search(d, rows, K, gs, 4, False, 20, 10, qweight=qw, qzeros=qz, scales=sc)
+    torch.cuda.synchronize()
+    assert torch.equal(qw.cpu(), orc.pack_rows(ref["tensor_q"].reshape(rows, -1), 4, 0))
+    assert torch.equal(qz.cpu(), orc.pack_rows(ref["zero_points"], 4, 0))
+
+
+@pytest.mark.parametrize("bits,sym", [(4, False), (4, True), (8, False), (8, True)], ids=str)
+@pytest.mark.parametrize("dtype,shape,gs", [(torch.bfloat16, (64, 4096), 128), (torch.float16, (33, 1024), 32),
+                                            (torch.bfloat16, (17, 2000), 200), (torch.float32, (5, 4096), 256),
+                                            (torch.bfloat16, (9, 1000), 100), (torch.bfloat16, (7, 1001), 91),
+                                            (torch.float64, (6, 1024), 64)], ids=str)
+def test_dequantize_packed_vs_oracle(dtype, shape, gs, bits, sym):
+    """dequantize_packed (awq.py:459-539 arithmetic): word-aligned groups (K and L multiples of
+    32 / bits) take the word-per-thread kernel, the rest the per-element kernel; NaN / inf /
+    constant groups included.  Bit-exact (NaN payloads compared as NaN) vs the oracle's
+    dequantize of the oracle's quantize."""
+    x = specials(rand(shape, gs + bits + sym, 0.5), 5).to(dtype)
+    q = Q(bits=bits, group_size=gs, symmetric=sym)
+    ref = orc.quantize(x, bits=bits, group_size=gs, symmetric=sym)
+    dq = q.dequantize_packed(q.quantize_packed(x)).cpu()
+    assert gio.same_bits_nan_eq(dq, orc.dequantize(ref))

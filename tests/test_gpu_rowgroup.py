@@ -105,12 +105,12 @@ def test_rowgroup_full_size_gs100():
 
 def test_generic_kernel_still_serves_the_rest():
     """fp64, groups larger than the row-segment stage, and AWQ_NO_ROWGROUP=1 take the generic
-    kernel (staging buffers required for packed outputs) with the same results."""
+    kernel (packed outputs written directly per span of groups, no staging) with the same results."""
     import os
     from awq_quantizer import _hip
-    assert not _hip.packs_directly(torch.float64, 4, 1000, 100)
-    assert not _hip.packs_directly(torch.bfloat16, 4, 5000, 1000)
-    assert not _hip.packs_directly(torch.float32, 4, 1000, 500)
+    assert _hip.packs_directly(torch.float64, 4, 1000, 100)
+    assert _hip.packs_directly(torch.bfloat16, 4, 5000, 1000)
+    assert _hip.packs_directly(torch.float32, 4, 1000, 500)
     _assert_parity_generic = lambda x, gs: orc.quantize(x, bits=4, group_size=gs, symmetric=False)
     for x, gs in ((rand((4, 1000), 1, 1.0, torch.float64), 100), (rand((4, 5000), 2), 1000)):
         q = Q(bits=4, group_size=gs, symmetric=False)

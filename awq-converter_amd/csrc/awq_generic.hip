@@ -14,6 +14,8 @@
 // and a true IEEE division for x / s.
 #include "awq_refmath.h"
 
+#include <cstdlib>
+
 namespace awq {
 namespace {
 
@@ -155,6 +157,85 @@ __global__ __launch_bounds__(256) void awq_generic_kernel(const void* __restrict
             }
             rem += 64;
             while (rem >= L) { rem -= L; ++j; }
+        }
+    }
+}
+
+// The same span for fp64 RTN at group sizes 64 * LPI (64, 128): the whole span (PER groups of
+// LPI elements per lane) is loaded into registers with every load in flight at once, the
+// per-group reductions and the quantize + pack pass run on the registers (no re-read), and a
+// wave's groups are wave-uniform per register slot (slot i of every lane is in group i / LPI).
+template <int LPI, int PER>
+__global__ __launch_bounds__(256) void awq_generic_span_reg_kernel(const double* __restrict__ w, int64_t rows,
+                                                                   int64_t K, int qmin, int qmax, int sym,
+                                                                   int32_t* __restrict__ tensor_q,
+                                                                   uint16_t* __restrict__ scales,
+                                                                   int32_t* __restrict__ zeros,
+                                                                   int32_t* __restrict__ qweight,
+                                                                   int32_t* __restrict__ qzeros) {
+    constexpr int BITS = 32 / PER, NI = LPI * PER;
+    constexpr int64_t L = 64 * LPI;
+    constexpr uint32_t MASK = (1u << BITS) - 1u;
+    const int lane = threadIdx.x & 63;
+    const int64_t G = (K + L - 1) / L;
+    const int64_t SP = (G + PER - 1) / PER;
+    const int64_t wpr = (K + PER - 1) / PER;
+    const int64_t si = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (si >= rows * SP) return;
+    const int64_t r = si / SP, sp = si - r * SP;
+    const int64_t g0 = sp * PER;
+    const int64_t base = r * K, span0 = g0 * L;
+    double v[NI];
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {                   // zero beyond K: the reference's padding
+        const int64_t k = span0 + 64 * i + lane;
+        v[i] = (k < K) ? __builtin_nontemporal_load(w + base + k) : 0.0;
+    }
+    uint32_t zword = 0;
+    double sa[PER], za[PER];
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+        sa[j] = 1.0;
+        za[j] = 0.0;
+        if (g0 + j >= G) continue;                   // wave-uniform
+        double mn = v[j * LPI], mx = v[j * LPI];
+        int nan = v[j * LPI] != v[j * LPI];
+#pragma unroll
+        for (int i = 1; i < LPI; ++i) {
+            const double t = v[j * LPI + i];
+            nan |= (t != t);
+            mn = t < mn ? t : mn;
+            mx = t > mx ? t : mx;
+        }
+        mn = wave_min(mn);
+        mx = wave_max(mx);
+        nan = wave_or(nan);
+        if (nan) { mn = NAN; mx = NAN; }
+        double sc, z;
+        group_params<AWQ_DTYPE_F64>(mn, mx, nan, qmin, qmax, sym, sc, z);
+        sa[j] = sc;
+        za[j] = z;
+        zword |= (((uint32_t)to_i32(z) - (uint32_t)qmin) & MASK) << (BITS * j);
+        if (lane == 0) {
+            const int64_t gi = r * G + g0 + j;
+            if (scales) scales[gi] = canon_f16((float)sc);
+            if (zeros) zeros[gi] = to_i32(z);
+        }
+    }
+    if (qzeros && lane == 0) qzeros[r * SP + sp] = (int32_t)zword;
+    const int sh = BITS * (lane & (PER - 1));
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+        const int64_t k = span0 + 64 * i + lane;
+        if (span0 + 64 * i >= K) break;              // wave-uniform
+        const bool act = k < K;
+        const int32_t q = act ? to_i32(quant1<AWQ_DTYPE_F64>(v[i], sa[i / LPI], za[i / LPI], qmin, qmax)) : 0;
+        if (tensor_q && act) tensor_q[base + k] = q;
+        if (qweight) {
+            uint32_t wd = act ? (((uint32_t)q - (uint32_t)qmin) & MASK) << sh : 0u;
+#pragma unroll
+            for (int o = 1; o < PER; o <<= 1) wd |= (uint32_t)__shfl_xor((int)wd, o, 64);
+            if (act && (lane & (PER - 1)) == 0) qweight[r * wpr + k / PER] = (int32_t)wd;
         }
     }
 }
@@ -301,6 +382,22 @@ hipError_t launch_generic(const void* w, int dtype, int64_t rows, int64_t K, int
     const int64_t G = (K + L - 1) / L;
     const unsigned grid = grid_for(rows * ((G + per - 1) / per), 4, 256 * 16);
     const bool search = n_cand > 0;
+    const char* ne = getenv("AWQ_GEN_NOREG");    // A/B of the register-resident fp64 span
+    const bool noreg = ne && ne[0] == '1';
+    if (dtype == AWQ_DTYPE_F64 && !search && !s_exact && !z_exact && (L == 64 || L == 128) && !noreg) {
+        const unsigned blocks = (unsigned)((rows * ((G + per - 1) / per) + 3) / 4);
+        const double* wd = (const double*)w;
+#define AWQ_SPAN_REG(LPI, PER)                                                                              \
+        hipLaunchKernelGGL((awq_generic_span_reg_kernel<LPI, PER>), dim3(blocks), dim3(256), 0, stream, wd, rows, K, \
+                           qmin, qmax, symmetric, tensor_q, scales, zeros, qweight, qzeros)
+        if (L == 64) {
+            if (per == 8) AWQ_SPAN_REG(1, 8); else AWQ_SPAN_REG(1, 4);
+        } else {
+            if (per == 8) AWQ_SPAN_REG(2, 8); else AWQ_SPAN_REG(2, 4);
+        }
+#undef AWQ_SPAN_REG
+        return hipPeekAtLastError();
+    }
 #define AWQ_GEN(D)                                                                                   \
     do {                                                                                             \
         if (search)                                                                                  \

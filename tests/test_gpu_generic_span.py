@@ -23,6 +23,8 @@ pytestmark = pytest.mark.gpu
 F64_CASES = [  # (shape, group size): spans of 8 (4-bit) / 4 (8-bit) groups, ragged last spans
     ((37, 1000), 100), ((5, 3001), 60), ((9, 4100), 96), ((3, 200), 7), ((4, 1024), 128),
     ((6, 777), 37), ((2, 5000), 1000), ((3, 2048), 32), ((4097,), 100), ((3, 5, 70), 48),
+    # group sizes 64 / 128 take the register-resident span (padded tails, K % 8 != 0, G < 8)
+    ((5, 1000), 128), ((7, 1001), 64), ((3, 640), 128), ((9, 4096), 64), ((2, 100), 64),
 ]
 
 
@@ -33,7 +35,7 @@ def test_generic_f64_vs_oracle(shape, gs, bits, sym):
 
 
 @pytest.mark.parametrize("bits,sym", [(4, False), (8, True)], ids=str)
-@pytest.mark.parametrize("gs", [100, 13, 640], ids=str)
+@pytest.mark.parametrize("gs", [100, 13, 640, 128, 64], ids=str)
 def test_generic_f64_special_values(gs, bits, sym):
     x = specials(rand((24, 1300), 7 + gs, 1.0), 11 + bits).to(torch.float64)
     _assert_parity(x, gs, bits, sym)
@@ -87,9 +89,30 @@ def test_dequantize_packed_vs_oracle(dtype, shape, gs, bits, sym):
     """dequantize_packed (awq.py:459-539 arithmetic): word-aligned groups (K and L multiples of
     32 / bits) take the word-per-thread kernel, the rest the per-element kernel; NaN / inf /
     constant groups included.  Bit-exact (NaN payloads compared as NaN) vs the oracle's
-    dequantize of the oracle's quantize."""
+    dequantize of the oracle's quantize, its int32 values taken through the packed format
+    first (a nibble / byte holds (v - qmin) mod 2^bits: the INT_MIN of an inf / inf element
+    becomes qmin, so such an element of an inf-scale group dequantizes to NaN, not -inf)."""
     x = specials(rand(shape, gs + bits + sym, 0.5), 5).to(dtype)
     q = Q(bits=bits, group_size=gs, symmetric=sym)
-    ref = orc.quantize(x, bits=bits, group_size=gs, symmetric=sym)
+    ref = dict(orc.quantize(x, bits=bits, group_size=gs, symmetric=sym))
+    for key in ("tensor_q", "zero_points"):
+        ref[key] = (((ref[key].long() - q.qmin) & ((1 << bits) - 1)) + q.qmin).to(torch.int32)
     dq = q.dequantize_packed(q.quantize_packed(x)).cpu()
     assert gio.same_bits_nan_eq(dq, orc.dequantize(ref))
+
+
+@pytest.mark.parametrize("gs", [64, 128], ids=str)
+def test_generic_f64_reg_span_matches_strided(gs):
+    """The register-resident fp64 span (group sizes 64 / 128) and the strided span kernel
+    (AWQ_GEN_NOREG=1) give the same bits on a ragged shape with special values."""
+    x = specials(rand((33, 1000), gs, 1.0), 17).to(torch.float64)
+    q = Q(bits=4, group_size=gs, symmetric=False)
+    a = q.quantize_packed(x)
+    os.environ["AWQ_GEN_NOREG"] = "1"
+    try:
+        b = Q(bits=4, group_size=gs, symmetric=False).quantize_packed(x)
+    finally:
+        os.environ.pop("AWQ_GEN_NOREG", None)
+    for key in ("qweight", "qzeros"):
+        assert torch.equal(a[key], b[key])
+    assert gio.same_bits_nan_eq(a["scales"], b["scales"])

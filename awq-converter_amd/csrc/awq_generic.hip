@@ -191,30 +191,44 @@ __global__ __launch_bounds__(256) void awq_generic_span_reg_kernel(const double*
         const int64_t k = span0 + 64 * i + lane;
         v[i] = (k < K) ? __builtin_nontemporal_load(w + base + k) : 0.0;
     }
-    uint32_t zword = 0;
-    double sa[PER], za[PER];
+    // lane-local min/max per group, then the PER groups' butterflies interleaved (independent
+    // chains: one shuffle latency per level instead of one per level and group); NaN by ballot
+    double mn[PER], mx[PER];
+    uint64_t nanm[PER];
 #pragma unroll
     for (int j = 0; j < PER; ++j) {
-        sa[j] = 1.0;
-        za[j] = 0.0;
-        if (g0 + j >= G) continue;                   // wave-uniform
-        double mn = v[j * LPI], mx = v[j * LPI];
-        int nan = v[j * LPI] != v[j * LPI];
+        double a = v[j * LPI], b = a;
+        int nan = a != a;
 #pragma unroll
         for (int i = 1; i < LPI; ++i) {
             const double t = v[j * LPI + i];
             nan |= (t != t);
-            mn = t < mn ? t : mn;
-            mx = t > mx ? t : mx;
+            a = t < a ? t : a;
+            b = t > b ? t : b;
         }
-        mn = wave_min(mn);
-        mx = wave_max(mx);
-        nan = wave_or(nan);
-        if (nan) { mn = NAN; mx = NAN; }
+        mn[j] = a;
+        mx[j] = b;
+        nanm[j] = __ballot(nan);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+#pragma unroll
+        for (int j = 0; j < PER; ++j) {
+            const double a = __shfl_xor(mn[j], o, 64), b = __shfl_xor(mx[j], o, 64);
+            mn[j] = a < mn[j] ? a : mn[j];
+            mx[j] = b > mx[j] ? b : mx[j];
+        }
+    }
+    uint32_t zword = 0;
+    double sa[PER], za[PER];
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+        const int nan = nanm[j] != 0;
         double sc, z;
-        group_params<AWQ_DTYPE_F64>(mn, mx, nan, qmin, qmax, sym, sc, z);
+        group_params<AWQ_DTYPE_F64>(nan ? NAN : mn[j], nan ? NAN : mx[j], nan, qmin, qmax, sym, sc, z);
         sa[j] = sc;
         za[j] = z;
+        if (g0 + j >= G) continue;                   // wave-uniform: past the row's last group
         zword |= (((uint32_t)to_i32(z) - (uint32_t)qmin) & MASK) << (BITS * j);
         if (lane == 0) {
             const int64_t gi = r * G + g0 + j;

@@ -161,6 +161,23 @@ __global__ __launch_bounds__(256) void awq_generic_kernel(const void* __restrict
     }
 }
 
+// DPP lane moves (VALU, no LDS round trip) for the register span's in-row levels:
+// quad_perm [1,0,3,2] (xor 1), quad_perm [2,3,0,1] (xor 2), row_half_mirror (lane i <-> 7 - i
+// of its 8), row_mirror (i <-> 15 - i of its 16).  After xor 1 and xor 2 every lane of a quad
+// holds the quad's value, so the two mirrors finish the 8- and 16-lane levels.
+template <int CTRL>
+__device__ __forceinline__ double dpp_d(double x) {
+    const long long b = __double_as_longlong(x);
+    const int lo = __builtin_amdgcn_mov_dpp((int)b, CTRL, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_mov_dpp((int)(b >> 32), CTRL, 0xF, 0xF, false);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp_u(uint32_t x) {
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, CTRL, 0xF, 0xF, false);
+}
+constexpr int kDppXor1 = 0xB1, kDppXor2 = 0x4E, kDppHalfMirror = 0x141, kDppMirror = 0x140;
+
 // The same span for fp64 RTN at group sizes 64 * LPI (64, 128): the whole span (PER groups of
 // LPI elements per lane) is loaded into registers with every load in flight at once, the
 // per-group reductions and the quantize + pack pass run on the registers (no re-read), and a
@@ -210,15 +227,23 @@ __global__ __launch_bounds__(256) void awq_generic_span_reg_kernel(const double*
         mx[j] = b;
         nanm[j] = __ballot(nan);
     }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-#pragma unroll
-        for (int j = 0; j < PER; ++j) {
-            const double a = __shfl_xor(mn[j], o, 64), b = __shfl_xor(mx[j], o, 64);
-            mn[j] = a < mn[j] ? a : mn[j];
-            mx[j] = b > mx[j] ? b : mx[j];
-        }
+#define AWQ_RED_LEVEL(MOVE)                                                                      \
+    _Pragma("unroll") for (int j = 0; j < PER; ++j) {                                            \
+        const double a = MOVE(mn[j]), b = MOVE(mx[j]);                                          \
+        mn[j] = a < mn[j] ? a : mn[j];                                                           \
+        mx[j] = b > mx[j] ? b : mx[j];                                                           \
     }
+    AWQ_RED_LEVEL(dpp_d<kDppXor1>)
+    AWQ_RED_LEVEL(dpp_d<kDppXor2>)
+    AWQ_RED_LEVEL(dpp_d<kDppHalfMirror>)
+    AWQ_RED_LEVEL(dpp_d<kDppMirror>)
+#define AWQ_SHFL16(x) __shfl_xor((x), 16, 64)
+#define AWQ_SHFL32(x) __shfl_xor((x), 32, 64)
+    AWQ_RED_LEVEL(AWQ_SHFL16)
+    AWQ_RED_LEVEL(AWQ_SHFL32)
+#undef AWQ_SHFL16
+#undef AWQ_SHFL32
+#undef AWQ_RED_LEVEL
     uint32_t zword = 0;
     double sa[PER], za[PER];
 #pragma unroll
@@ -247,8 +272,9 @@ __global__ __launch_bounds__(256) void awq_generic_span_reg_kernel(const double*
         if (tensor_q && act) tensor_q[base + k] = q;
         if (qweight) {
             uint32_t wd = act ? (((uint32_t)q - (uint32_t)qmin) & MASK) << sh : 0u;
-#pragma unroll
-            for (int o = 1; o < PER; o <<= 1) wd |= (uint32_t)__shfl_xor((int)wd, o, 64);
+            wd |= dpp_u<kDppXor1>(wd);
+            wd |= dpp_u<kDppXor2>(wd);
+            if (PER == 8) wd |= dpp_u<kDppHalfMirror>(wd);
             if (act && (lane & (PER - 1)) == 0) qweight[r * wpr + k / PER] = (int32_t)wd;
         }
     }

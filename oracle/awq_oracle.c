@@ -18,7 +18,8 @@
  *                                 flattened, tail group zero-padded)
  *   quantization/awq.py:130-171  _calculate_scale_zp (numel < group_size:
  *                                 whole tensor or whole rows, no padding)
- *   quantization/awq.py:409-412  result dtypes (int32 / fp16 / int32)
+ *   quantization/awq.py:409-412  result dtypes (int32 / fp16 / int32), incl. the
+ *                                 bits of NaN scales (oracle_nan_scale_f16)
  *   quantization/awq.py:459-539  dequantize ((q - z) * fp16 scale -> fp16)
  *
  * Arithmetic model (torch CPU eager semantics for one element-wise op on a
@@ -134,6 +135,73 @@ static inline double load_elem(const void* x, int dtype, int64_t i) {
     }
 }
 
+/* fp16 bits of a NaN scale, as the reference's CPU ops leave them (awq.py:192-205, the fp32
+ * scale buffer of awq.py:327/352, .to(float16) of awq.py:411).  Derived from the op chain and
+ * pinned by every NaN scale of tests/golden/golden_nan.* (1 852 of them) and golden_small.*:
+ *   - torch.min/max over n >= 2 elements holding a NaN return the all-ones NaN of the compute
+ *     type (ATen's vectorised maximum/minimum OR the unordered-compare mask into the result);
+ *     rounded to fp16 by the scalar c10 conversion that is 0xFE00, to bf16 0x7FC0; over n = 1
+ *     they return the element itself;
+ *   - abs clears the sign, Python max() keeps its first argument, fp32/fp64 a - b of two NaNs
+ *     returns b (fp16, computed in fp32: a); inf - inf is the x86 default NaN (sign set);
+ *   - bf16 rounding gives 0x7FC0 for any NaN; the fp16 -> fp32 store into the scale buffer
+ *     (scales[c, g] = scale) gives 0x7FFFFFFF for any fp16 NaN; fp64 -> fp32 keeps the sign and
+ *     the top mantissa bits; fp32 -> fp16 (awq.py:411) keeps the sign and the top 10 mantissa
+ *     bits with the quiet bit set.
+ * small = 1: the small-tensor path (awq.py:130-171), whose input-dtype scales go to fp16
+ * directly (no fp32 buffer).  n = group length; has_nan = the group holds a NaN (else the NaN
+ * came from inf - inf); e = bits of the group's NaN element (used when n == 1). */
+uint16_t oracle_nan_scale_f16(int dtype, int sym, int small, int64_t n, int has_nan, uint64_t e) {
+    switch (dtype) {
+    case AWQ_ORACLE_BF16:
+        return 0x7E00;
+    case AWQ_ORACLE_F16:
+        if (!small) return 0x7FFF;
+        if (sym) return 0x7E00;
+        return (n == 1 && has_nan) ? (uint16_t)((e & 0x8000u) | 0x7E00u) : 0xFE00;
+    default: {
+        if (!has_nan) return 0xFE00;
+        if (n >= 2) return 0xFFFF;
+        const int f64 = dtype == AWQ_ORACLE_F64;
+        uint16_t sign = (uint16_t)(f64 ? (e >> 48) & 0x8000u : (e >> 16) & 0x8000u);
+        uint16_t m10 = (uint16_t)(f64 ? (e >> 42) & 0x3FFu : (e >> 13) & 0x3FFu);
+        if (sym) sign = 0x8000;
+        return (uint16_t)(sign | 0x7E00u | m10);
+    }
+    }
+}
+
+static inline uint64_t load_bits(const void* x, int dtype, int64_t i) {
+    switch (dtype) {
+    case AWQ_ORACLE_BF16:
+    case AWQ_ORACLE_F16: return ((const uint16_t*)x)[i];
+    case AWQ_ORACLE_F32: return ((const uint32_t*)x)[i];
+    default: return ((const uint64_t*)x)[i];
+    }
+}
+
+static inline int bits_nan(uint64_t b, int dtype) {
+    switch (dtype) {
+    case AWQ_ORACLE_BF16: return (b & 0x7FFFu) > 0x7F80u;
+    case AWQ_ORACLE_F16: return (b & 0x7FFFu) > 0x7C00u;
+    case AWQ_ORACLE_F32: return (b & 0x7FFFFFFFu) > 0x7F800000u;
+    default: return (b & 0x7FFFFFFFFFFFFFFFull) > 0x7FF0000000000000ull;
+    }
+}
+
+/* fp16 bits of the scale of group [k0, k1) of row r (n = L elements incl. padding) */
+static uint16_t scale_f16(double s, const void* x, int dtype, int64_t base, int64_t k0, int64_t k1, int64_t L,
+                          int sym, int small) {
+    if (!isnan(s)) return oracle_f32_to_f16((float)s);
+    int has_nan = 0;
+    uint64_t e = 0;
+    for (int64_t k = k0; k < k1 && !has_nan; ++k) {
+        uint64_t b = load_bits(x, dtype, base + k);
+        if (bits_nan(b, dtype)) { has_nan = 1; e = b; }
+    }
+    return oracle_nan_scale_f16(dtype, sym, small, L, has_nan, e);
+}
+
 /* awq.py:173-213 — scale and zero point of one group (values already in compute type). */
 static void group_scale_zp(double mn, double mx, int dtype, int qmin, int qmax, int sym,
                            double* s_out, double* z_out) {
@@ -159,6 +227,12 @@ static void group_scale_zp(double mn, double mx, int dtype, int qmin, int qmax, 
 
 int oracle_quantize(const void* x, int dtype, int64_t rows, int64_t K, int64_t L, int bits,
                     int sym, int32_t* tensor_q, uint16_t* scales_f16, int32_t* zeros) {
+    return oracle_quantize_ex(x, dtype, rows, K, L, bits, sym, 0, tensor_q, scales_f16, zeros);
+}
+
+/* small = 1: the small-tensor path (awq.py:130-171, L = K): only NaN scale bits differ */
+int oracle_quantize_ex(const void* x, int dtype, int64_t rows, int64_t K, int64_t L, int bits,
+                       int sym, int small, int32_t* tensor_q, uint16_t* scales_f16, int32_t* zeros) {
     if (!x || rows < 0 || K < 0 || L <= 0 || (bits != 4 && bits != 8)) return -1;
     int qmin = sym ? -(1 << (bits - 1)) : 0;                                  /* awq.py:114-128 */
     int qmax = sym ? (1 << (bits - 1)) - 1 : (1 << bits) - 1;
@@ -181,7 +255,7 @@ int oracle_quantize(const void* x, int dtype, int64_t rows, int64_t K, int64_t L
             if (nan) { mn = NAN; mx = NAN; }
             double s, z;
             group_scale_zp(mn, mx, dtype, qmin, qmax, sym, &s, &z);
-            if (scales_f16) scales_f16[r * G + g] = oracle_f32_to_f16((float)s);
+            if (scales_f16) scales_f16[r * G + g] = scale_f16(s, x, dtype, r * K, k0, k1, L, sym, small);
             if (zeros) zeros[r * G + g] = to_i32(z);
             if (tensor_q) {
                 for (int64_t k = k0; k < k1; ++k) {
@@ -295,6 +369,13 @@ static double tree_sum64(double* a, int f64) {
 int oracle_quantize_search(const void* x, int dtype, int64_t rows, int64_t K, int64_t L, int bits,
                            int sym, int n_grid, int n_cand, int32_t* tensor_q, uint16_t* scales_f16,
                            int32_t* zeros) {
+    return oracle_quantize_search_ex(x, dtype, rows, K, L, bits, sym, 0, n_grid, n_cand, tensor_q, scales_f16,
+                                     zeros);
+}
+
+int oracle_quantize_search_ex(const void* x, int dtype, int64_t rows, int64_t K, int64_t L, int bits,
+                              int sym, int small, int n_grid, int n_cand, int32_t* tensor_q, uint16_t* scales_f16,
+                              int32_t* zeros) {
     if (!x || rows < 0 || K < 0 || L <= 0 || (bits != 4 && bits != 8)) return -1;
     if (n_grid < 1 || n_cand < 1 || n_cand > n_grid) return -1;
     if (L > 512 && K > 512) return -1;   /* one 8-element chunk per slot, 64 slots */
@@ -356,7 +437,7 @@ int oracle_quantize_search(const void* x, int dtype, int64_t rows, int64_t K, in
             }
             double s, z;
             group_scale_zp(mn, mx, dtype, qmin, qmax, sym, &s, &z);
-            if (scales_f16) scales_f16[r * G + g] = oracle_f32_to_f16((float)s);
+            if (scales_f16) scales_f16[r * G + g] = scale_f16(s, x, dtype, r * K, k0, k1, L, sym, small);
             if (zeros) zeros[r * G + g] = to_i32(z);
             if (tensor_q) {
                 for (int64_t k = k0; k < k1; ++k) {
@@ -382,7 +463,11 @@ int oracle_set_threads(int n) {
 #endif
 }
 
-/* awq.py:459-539: dq = (q - z) [int32] * scale [fp16 0-d]  -> fp16 math -> stored fp32 */
+/* awq.py:459-539: dq = (q - z) [int32] * scale [fp16 0-d]  -> fp16 math -> stored fp32.
+ * NaN bits: the fp16 product keeps the scale's NaN (inf * 0: the default NaN 0xFE00); the
+ * group's n = min(L, K - g L) results are copied into the fp32 output by ATen's fp16 -> fp32
+ * copy (awq.py:527/531), which widens 8-element vectors bit-preservingly and converts the last
+ * n % 8 elements one by one, turning any NaN into 0x7FFFFFFF (pinned: golden_nan.* .dq). */
 int oracle_dequantize(const int32_t* tensor_q, const uint16_t* scales_f16, const int32_t* zeros,
                       int64_t rows, int64_t K, int64_t L, float* out) {
     if (!tensor_q || !scales_f16 || !zeros || !out || L <= 0) return -1;
@@ -393,7 +478,10 @@ int oracle_dequantize(const int32_t* tensor_q, const uint16_t* scales_f16, const
             int32_t diff = (int32_t)((uint32_t)tensor_q[r * K + k] - (uint32_t)zeros[r * G + g]);
             float h = oracle_f16_to_f32(oracle_f32_to_f16((float)diff));
             float s = oracle_f16_to_f32(scales_f16[r * G + g]);
-            out[r * K + k] = oracle_f16_to_f32(oracle_f32_to_f16(h * s));
+            float v = oracle_f16_to_f32(oracle_f32_to_f16(h * s));
+            int64_t n = K - g * L < L ? K - g * L : L;
+            if (isnan(v) && k - g * L >= (n & ~(int64_t)7)) v = u2f(0x7FFFFFFFu);
+            out[r * K + k] = v;
         }
     }
     return 0;

@@ -12,6 +12,13 @@ enum { AWQ_ORACLE_BF16 = 0, AWQ_ORACLE_F16 = 1, AWQ_ORACLE_F32 = 2, AWQ_ORACLE_F
  * Outputs (any may be NULL): tensor_q int32 [rows, K], scales fp16 bits [rows, G], zeros int32 [rows, G]. */
 int oracle_quantize(const void* x, int dtype, int64_t rows, int64_t K, int64_t L, int bits, int sym,
                     int32_t* tensor_q, uint16_t* scales_f16, int32_t* zeros);
+/* small = 1: the small-tensor path (awq.py:130-171); only the bits of NaN scales differ */
+int oracle_quantize_ex(const void* x, int dtype, int64_t rows, int64_t K, int64_t L, int bits, int sym, int small,
+                       int32_t* tensor_q, uint16_t* scales_f16, int32_t* zeros);
+uint16_t oracle_nan_scale_f16(int dtype, int sym, int small, int64_t n, int has_nan, uint64_t e);
+int oracle_quantize_search_ex(const void* x, int dtype, int64_t rows, int64_t K, int64_t L, int bits, int sym,
+                              int small, int n_grid, int n_cand, int32_t* tensor_q, uint16_t* scales_f16,
+                              int32_t* zeros);
 /* opt-in clip search (product definition, include/awq_hip.h awq_quantize_search) */
 int oracle_quantize_search(const void* x, int dtype, int64_t rows, int64_t K, int64_t L, int bits, int sym,
                            int n_grid, int n_cand, int32_t* tensor_q, uint16_t* scales_f16, int32_t* zeros);

@@ -15,6 +15,7 @@ reference is never imported by tests, bench.py or the product; the GPU box
 never sees /root/reference.  Re-run with:
 
     PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py --nan   (golden_nan.*)
 
 Reference call sites pinned here:
   awq.py:376-433  quantize()            awq.py:459-539 dequantize()
@@ -223,5 +224,131 @@ def main():
           "bytes", os.path.getsize(os.path.join(HERE, "golden_small.safetensors")))
 
 
+# ---------------------------------------------------------------- NaN-origin cases (--nan)
+# The fp16 bits of a NaN scale depend on where the NaN came from and on the input dtype
+# (awq.py:192-205 reductions and arithmetic, the fp32 scale buffer of awq.py:327/352, the
+# .to(float16) of awq.py:411).  These cases pin that: +NaN / -NaN / payload / signalling
+# NaNs, NaN next to +-inf, all-inf groups (inf - inf), NaN in a zero-padded tail group,
+# group sizes 1 / 2 / 3, scale tensors of 1, 7, 8, 9, 16, 17, 33 and 51 elements, and the
+# small-tensor path (awq.py:130-171: whole tensor and per row, one element and more).
+# Written to golden_nan.safetensors / golden_nan.json.
+
+_IT = {torch.bfloat16: torch.int16, torch.float16: torch.int16, torch.float32: torch.int32,
+       torch.float64: torch.int64}
+
+
+def nan_bits(dt, kind):
+    """A NaN of dtype dt as a 0-d tensor: 'p' +qNaN, 'n' -qNaN, 'pay' qNaN with a payload,
+    's' signalling NaN (payload 1), 'nspay' negative signalling NaN with payload 3."""
+    w = {torch.bfloat16: 16, torch.float16: 16, torch.float32: 32, torch.float64: 64}[dt]
+    e = {torch.bfloat16: 8, torch.float16: 5, torch.float32: 8, torch.float64: 11}[dt]
+    m = w - 1 - e
+    exp = ((1 << e) - 1) << m
+    q = 1 << (m - 1)
+    v = {"p": exp | q, "n": (1 << (w - 1)) | exp | q, "pay": exp | q | 1 | (q >> 2) | (q >> 5),
+         "s": exp | 1, "nspay": (1 << (w - 1)) | exp | 3}[kind]
+    if v >= 1 << (w - 1):
+        v -= 1 << w
+    return torch.tensor([v], dtype=torch.int64).to(_IT[dt]).view(dt)[0]
+
+
+def nan_inputs(dt):
+    """(name, tensor, [(bits, gs, sym, per_channel) ...]) of the NaN-origin cases."""
+    g = torch.Generator().manual_seed(777)
+    rnd = lambda *s: torch.randn(*s, generator=g).to(dt)
+    PS = [(b, 128, s, True) for b in (4, 8) for s in (False, True)]
+    out = []
+    # 17 rows x 3 groups of 128 (51 scales): one NaN origin per row
+    x = rnd(17, 384)
+    inf, ninf = float("inf"), float("-inf")
+    x[0, 5] = nan_bits(dt, "p")
+    x[1, 130] = nan_bits(dt, "n")
+    x[2, 300] = nan_bits(dt, "pay")
+    x[3, 0] = nan_bits(dt, "s")
+    x[4, 127] = nan_bits(dt, "nspay")
+    x[5, 10] = nan_bits(dt, "p"); x[5, 11] = inf                     # NaN next to +inf
+    x[6, 200] = nan_bits(dt, "n"); x[6, 201] = ninf                  # -NaN next to -inf
+    x[7, 0:128] = inf                                                # all +inf: inf - inf
+    x[8, 128:256] = ninf                                             # all -inf
+    x[9, 256] = inf; x[9, 300] = ninf                                # +-inf, no NaN
+    x[10, 0:128] = nan_bits(dt, "p")                                 # all NaN
+    x[11, 0] = nan_bits(dt, "p"); x[11, 127] = nan_bits(dt, "n")     # both signs
+    x[12, 383] = nan_bits(dt, "pay")                                 # last element
+    x[13, 0:128] = 0.0; x[13, 64] = nan_bits(dt, "p")                # NaN among zeros
+    x[14, 128:256] = 2.5; x[14, 129] = nan_bits(dt, "s")             # NaN in a constant group
+    out.append(("rows17x384", x, PS + [(4, gs, s, True) for gs in (32, 64, 100, 256) for s in (False, True)]))
+    # scale tensors of 1, 7, 8, 9, 16, 17, 33 elements
+    for R in (1, 7, 8, 9, 16, 17, 33):
+        x = rnd(R, 128)
+        x[0, 3] = nan_bits(dt, "p")
+        x[R // 2, 64] = nan_bits(dt, "n")
+        x[R - 1, 127] = nan_bits(dt, "pay")
+        out.append((f"r{R}x128", x, PS))
+    # NaN / inf in a zero-padded tail group (K = 300, gs 128: tail of 44 elements + 84 zeros)
+    x = rnd(5, 300)
+    x[0, 280] = nan_bits(dt, "p")
+    x[1, 256:300] = inf                                             # all-inf tail: the padding is 0
+    x[2, 299] = nan_bits(dt, "n")
+    x[3, 260] = ninf
+    out.append(("tail5x300", x, PS + [(4, 100, s, True) for s in (False, True)]))
+    # group sizes 1, 2, 3 (one NaN per group: the element itself is the group's min and max)
+    x = rnd(6, 12)
+    x[0, 0] = nan_bits(dt, "p"); x[0, 5] = nan_bits(dt, "n"); x[0, 7] = nan_bits(dt, "pay")
+    x[1, 1] = nan_bits(dt, "s"); x[1, 2] = nan_bits(dt, "nspay"); x[1, 11] = inf
+    x[2, 3] = ninf; x[2, 4] = inf; x[2, 5] = ninf
+    x[3, 6] = nan_bits(dt, "p"); x[3, 7] = inf
+    out.append(("gsmall6x12", x, [(b, gs, s, True) for gs in (1, 2, 3) for b in (4, 8) for s in (False, True)]))
+    # small-tensor path (numel < group_size): whole tensor / per row, n = 1 and n > 1
+    SP = [(b, 128, s, pc) for b in (4, 8) for s in (False, True) for pc in (True, False)]
+    for name, shape, marks in (
+            ("sm_v1_p", (1,), [((0,), "p")]), ("sm_v1_n", (1,), [((0,), "n")]),
+            ("sm_v1_pay", (1,), [((0,), "pay")]), ("sm_v1_s", (1,), [((0,), "s")]),
+            ("sm_v1_inf", (1,), [((0,), "inf")]), ("sm_v1_ninf", (1,), [((0,), "ninf")]),
+            ("sm_v5", (5,), [((2,), "pay")]), ("sm_v7_inf", (7,), [((i,), "inf") for i in range(7)]),
+            ("sm_c6x1", (6, 1), [((0, 0), "p"), ((1, 0), "n"), ((2, 0), "pay"), ((3, 0), "inf"), ((4, 0), "nspay")]),
+            ("sm_c3x4", (3, 4), [((0, 1), "p"), ((2, 3), "n")]),
+            ("sm_c9x3", (9, 3), [((0, 0), "p"), ((4, 1), "pay"), ((8, 2), "n")] + [((5, i), "ninf") for i in range(3)]),
+            ("sm_t2x3x4", (2, 3, 4), [((1, 2, 3), "pay")])):
+        x = rnd(*shape)
+        for idx, kind in marks:
+            x[idx] = inf if kind == "inf" else (ninf if kind == "ninf" else nan_bits(dt, kind))
+        out.append((name, x, SP))
+    x = nan_bits(dt, "pay").clone()                                  # 0-d
+    out.append(("sm_0d_pay", x, SP))
+    return out
+
+
+def main_nan():
+    tensors, cases = {}, []
+    for dn in ("bf16", "f16", "f32", "f64"):
+        dt = DTYPES[dn]
+        for sn, x, plist in nan_inputs(dt):
+            in_key = f"in.{dn}.{sn}"
+            xs = x.view(torch.int16) if dt == torch.bfloat16 else x
+            tensors[in_key] = xs.contiguous().clone()
+            for bits, gs, sym, pc in plist:
+                name = f"{dn}.{sn}.{'sym' if sym else 'asym'}.b{bits}.g{gs}.pc{int(pc)}"
+                params = dict(bits=bits, group_size=gs, symmetric=sym, per_channel=pc)
+                rec, res = run_case(params, x)
+                rec.update(name=name, params=params, shape=list(x.shape), dtype=str(x.dtype), input=in_key)
+                if res is not None:
+                    r, dq = res
+                    for k in ("tensor_q", "scales", "zero_points"):
+                        tensors[f"{name}.{k}"] = r[k].contiguous()
+                    rec["out_shapes"] = {k: list(r[k].shape) for k in ("tensor_q", "scales", "zero_points")}
+                    if dq is not None:
+                        tensors[name + ".dq"] = dq.contiguous()
+                cases.append(rec)
+    save_file(tensors, os.path.join(HERE, "golden_nan.safetensors"))
+    with open(os.path.join(HERE, "golden_nan.json"), "w") as f:
+        json.dump({"generator": "tests/golden/make_golden.py --nan", "torch": torch.__version__,
+                   "reference": "shanefitch/AWQ-Converter src/awq_quantizer/quantization/awq.py",
+                   "cases": cases}, f, indent=1, sort_keys=True)
+    print("nan cases", len(cases), "bytes", os.path.getsize(os.path.join(HERE, "golden_nan.safetensors")))
+
+
 if __name__ == "__main__":
-    main()
+    if "--nan" in sys.argv[1:]:
+        main_nan()
+    else:
+        main()

@@ -52,16 +52,37 @@ def sha(t):
     return hashlib.sha256(t.numpy().tobytes()).hexdigest()
 
 
-def same_bits_nan_eq(a, b):
-    """Bit equality, except that any NaN matches any NaN (NaN payload/sign is not pinned)."""
-    a, b = a.contiguous(), b.contiguous()
+def same_bits(a, b):
+    """Exact bit equality of two tensors (NaN payloads and signs included)."""
+    a, b = a.contiguous().cpu(), b.contiguous().cpu()
     if a.shape != b.shape or a.dtype != b.dtype:
         return False
     if a.is_floating_point():
-        an, bn = torch.isnan(a), torch.isnan(b)
-        if not torch.equal(an, bn):
-            return False
-        ia = a.view(torch.int16 if a.element_size() == 2 else (torch.int32 if a.element_size() == 4 else torch.int64))
-        ib = b.view(ia.dtype)
-        return bool(torch.equal(ia[~an], ib[~bn]))
+        it = {2: torch.int16, 4: torch.int32, 8: torch.int64}[a.element_size()]
+        return bool(torch.equal(a.view(it), b.view(it)))
     return bool(torch.equal(a, b))
+
+
+# ---- NaN-origin fixtures (make_golden.py --nan) ----
+def nan_manifest():
+    if "nm" not in _cache:
+        with open(os.path.join(GOLDEN_DIR, "golden_nan.json")) as f:
+            _cache["nm"] = json.load(f)
+    return _cache["nm"]
+
+
+def nan_tensors():
+    if "nt" not in _cache:
+        _cache["nt"] = load_file(os.path.join(GOLDEN_DIR, "golden_nan.safetensors"))
+    return _cache["nt"]
+
+
+def nan_cases():
+    return [c for c in nan_manifest()["cases"] if c.get("ok")]
+
+
+def nan_case_input(case):
+    t = nan_tensors()[case["input"]]
+    if _DT[case["dtype"]] == torch.bfloat16:
+        t = t.view(torch.bfloat16)
+    return t.reshape(case["shape"])

@@ -2,8 +2,9 @@
 
 The fixtures were produced by importing the reference awq.py in the build
 container (tests/golden/make_golden.py).  Every case must match bit for bit
-(int32 tensor_q/zero_points, fp16 scales, fp32 dequantize); the only latitude is
-NaN payload/sign in floating outputs (see golden_io.same_bits_nan_eq).
+(int32 tensor_q/zero_points, fp16 scales, fp32 dequantize) — NaN payloads and signs
+included: the NaN-origin fixtures (make_golden.py --nan, golden_nan.*) pin the bits of NaN
+scales for every input dtype, group size, NaN origin and the small-tensor path.
 """
 import pytest
 import torch
@@ -22,15 +23,40 @@ def test_oracle_matches_reference_case(case):
     name = case["name"]
     assert torch.equal(res["tensor_q"], T[name + ".tensor_q"]), "tensor_q"
     assert torch.equal(res["zero_points"], T[name + ".zero_points"]), "zero_points"
-    assert gio.same_bits_nan_eq(res["scales"], T[name + ".scales"]), "scales"
+    assert gio.same_bits(res["scales"], T[name + ".scales"]), "scales"
     if "out_shapes" in case:
         assert list(res["scales"].shape) == case["out_shapes"]["scales"]
     if name + ".dq" in T:
         dq = orc.dequantize(res)
-        assert gio.same_bits_nan_eq(dq, T[name + ".dq"]), "dequantize"
+        assert gio.same_bits(dq, T[name + ".dq"]), "dequantize"
     elif case.get("dequantize") == "IndexError":
         with pytest.raises(IndexError):
             orc.dequantize(res)
+
+
+@pytest.mark.parametrize("case", gio.nan_cases(), ids=lambda c: c["name"])
+def test_oracle_matches_reference_nan_case(case):
+    x = gio.nan_case_input(case)
+    p = case["params"]
+    res = orc.quantize(x, bits=p["bits"], group_size=p["group_size"], symmetric=p["symmetric"],
+                       per_channel=p["per_channel"])
+    T = gio.nan_tensors()
+    name = case["name"]
+    assert torch.equal(res["tensor_q"], T[name + ".tensor_q"]), "tensor_q"
+    assert torch.equal(res["zero_points"], T[name + ".zero_points"]), "zero_points"
+    assert gio.same_bits(res["scales"], T[name + ".scales"]), "scales"
+    if name + ".dq" in T:
+        assert gio.same_bits(orc.dequantize(res), T[name + ".dq"]), "dequantize"
+
+
+def test_nan_fixtures_cover_every_origin():
+    """The NaN-origin fixtures hold NaN scales of every kind the rule distinguishes."""
+    T = gio.nan_tensors()
+    seen = set()
+    for c in gio.nan_cases():
+        s = T[c["name"] + ".scales"].reshape(-1).view(torch.int16)
+        seen |= {int(v) & 0xFFFF for v in s.tolist() if (int(v) & 0x7FFF) > 0x7C00}
+    assert {0x7E00, 0xFE00, 0x7FFF, 0xFFFF, 0x7E90, 0xFE90} <= seen, sorted(map(hex, seen))
 
 
 @pytest.mark.parametrize("rec", gio.manifest()["hashed"], ids=lambda r: r["name"])

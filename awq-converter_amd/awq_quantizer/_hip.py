@@ -6,6 +6,7 @@ the arithmetic is the HIP kernels in awq-converter_amd/csrc.
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes
 import os
 import threading
@@ -15,7 +16,8 @@ import torch
 
 LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib")
 LIB_PATH = os.path.join(LIB_DIR, "libawq_hip.so")
-ABI_VERSION = 9
+ABI_VERSION = 10
+Q_SMALL_TENSOR = 1      # include/awq_hip.h AWQ_Q_SMALL_TENSOR
 
 AWQ_DTYPE = {torch.bfloat16: 0, torch.float16: 1, torch.float32: 2, torch.float64: 3}
 
@@ -33,6 +35,12 @@ class TensorDesc(ctypes.Structure):
 
 assert ctypes.sizeof(TensorDesc) == 80
 
+
+class Tuning(ctypes.Structure):
+    """Mirror of awq_tuning (include/awq_hip_tuning.h): diagnostics / A-B controls only."""
+    _fields_ = [("max_blocks", _I32), ("tiles_per_wave", _I32), ("no_rowgroup", _I32), ("rg_waves", _I32),
+                ("rg_gpt", _I32), ("gen_noreg", _I32)]
+
 # symbol -> (restype, argtypes); the CPU test suite checks every one is exported.
 SIGNATURES = {
     "awq_abi_version": (_I32, []),
@@ -40,6 +48,9 @@ SIGNATURES = {
     "awq_device_check": (_I32, [ctypes.c_char_p, _I32]),
     "awq_quantize_groups": (_I32, [_P, _I32, _I64, _I64, _I32, _I32, _I32, _P, _P, _P, _P, _P, _P]),
     "awq_quantize_search": (_I32, [_P, _I32, _I64, _I64, _I32, _I32, _I32, _I32, _I32, _P, _P, _P, _P, _P, _P]),
+    "awq_quantize_groups_ex": (_I32, [_P, _I32, _I64, _I64, _I32, _I32, _I32, _I32, _P, _P, _P, _P, _P, _P]),
+    "awq_quantize_search_ex": (_I32, [_P, _I32, _I64, _I64, _I32, _I32, _I32, _I32, _I32, _I32, _P, _P, _P, _P, _P,
+                                      _P]),
     "awq_group_params": (_I32, [_P, _I32, _I64, _I64, _I64, _I32, _I32, _P, _P, _P]),
     "awq_apply_params": (_I32, [_P, _I32, _I64, _I64, _I64, _P, _P, _I32, _I32, _I32, _P, _P]),
     "awq_packs_directly": (_I32, [_I32, _I64, _I64, _I64]),
@@ -55,6 +66,7 @@ SIGNATURES = {
     "awq_dequantize_packed": (_I32, [_P, _P, _P, _I64, _I64, _I64, _I32, _I32, _P, _P]),
     "awq_pack_rows": (_I32, [_P, _I64, _I64, _I32, _I32, _P, _P]),
     "awq_selftest": (_I32, [_I32, _P, _P]),
+    "awq_set_tuning": (_I32, [ctypes.POINTER(Tuning)]),
     "awq_act_stats": (_I32, [_P, _I32, _I64, _I64, _P, _P, _P, _P]),
     "awq_weight_colsum": (_I32, [_P, _I32, _I64, _I64, _I64, _P, _P, _P]),
     "awq_column_mean": (_I32, [_P, _I64, _I64, ctypes.c_double, _P, _P]),
@@ -75,13 +87,13 @@ class HipUnavailable(RuntimeError):
 
 
 def load_library(path: str = LIB_PATH):
-    """Load libawq_hip.so and bind every entry point (works without a GPU)."""
+    """Load libawq_hip.so and bind every entry point (works without a GPU).  The first call
+    decides the library (diagnostics scripts pass another in-tree build explicitly; nothing
+    in the environment redirects it)."""
     global _lib
     with _lock:
         if _lib is not None:
             return _lib
-        if path == LIB_PATH:   # tuning hook: run everything against another in-tree build
-            path = os.environ.get("AWQ_HIP_LIB", path)
         if not os.path.exists(path):
             raise HipUnavailable(
                 f"awq_quantizer: {path} is missing — build it with "
@@ -133,23 +145,25 @@ def ptr(t):
 
 
 def quantize_groups(x: torch.Tensor, rows: int, K: int, L: int, bits: int, symmetric: bool, *,
-                    qweight=None, qzeros=None, scales=None, tensor_q=None, zeros=None) -> None:
-    """Launch awq_quantize_groups on x (device, contiguous) with caller-allocated outputs."""
+                    qweight=None, qzeros=None, scales=None, tensor_q=None, zeros=None, small: bool = False) -> None:
+    """Launch awq_quantize_groups_ex on x (device, contiguous) with caller-allocated outputs.
+    small: the reference's small-tensor path (awq.py:130-171, L = K; AWQ_Q_SMALL_TENSOR)."""
     lib = load_library()
-    rc = lib.awq_quantize_groups(ptr(x), AWQ_DTYPE[x.dtype], rows, K, L, bits, int(bool(symmetric)),
-                                 ptr(qweight), ptr(qzeros), ptr(scales), ptr(tensor_q), ptr(zeros),
-                                 ctypes.c_void_p(stream_ptr(x.device)))
+    rc = lib.awq_quantize_groups_ex(ptr(x), AWQ_DTYPE[x.dtype], rows, K, L, bits, int(bool(symmetric)),
+                                    Q_SMALL_TENSOR if small else 0, ptr(qweight), ptr(qzeros), ptr(scales),
+                                    ptr(tensor_q), ptr(zeros), ctypes.c_void_p(stream_ptr(x.device)))
     check(rc, "awq_quantize_groups")
 
 
 def quantize_search(x: torch.Tensor, rows: int, K: int, L: int, bits: int, symmetric: bool, n_grid: int,
                     n_candidates: int, *, qweight=None, qzeros=None, scales=None, tensor_q=None,
-                    zeros=None) -> None:
-    """Launch awq_quantize_search (opt-in clip search, include/awq_hip.h)."""
+                    zeros=None, small: bool = False) -> None:
+    """Launch awq_quantize_search_ex (opt-in clip search, include/awq_hip.h)."""
     lib = load_library()
-    rc = lib.awq_quantize_search(ptr(x), AWQ_DTYPE[x.dtype], rows, K, L, bits, int(bool(symmetric)),
-                                 int(n_grid), int(n_candidates), ptr(qweight), ptr(qzeros), ptr(scales),
-                                 ptr(tensor_q), ptr(zeros), ctypes.c_void_p(stream_ptr(x.device)))
+    rc = lib.awq_quantize_search_ex(ptr(x), AWQ_DTYPE[x.dtype], rows, K, L, bits, int(bool(symmetric)),
+                                    Q_SMALL_TENSOR if small else 0, int(n_grid), int(n_candidates), ptr(qweight),
+                                    ptr(qzeros), ptr(scales), ptr(tensor_q), ptr(zeros),
+                                    ctypes.c_void_p(stream_ptr(x.device)))
     check(rc, "awq_quantize_search")
 
 
@@ -203,18 +217,24 @@ def plan_ragged(descs, bits: int, group_size: int = 128) -> int:
     return total
 
 
-def _pageable_tables() -> bool:
-    # A/B switch for scripts/cli_bench.py: the round-1 path (tables copied from pageable
-    # memory: a host-synchronous copy per batch on the compute stream)
-    return os.environ.get("AWQ_PAGEABLE_TABLES", "0") == "1"
+@contextlib.contextmanager
+def tuning(**kw):
+    """Diagnostics / A-B only (include/awq_hip_tuning.h): launches from this thread inside the
+    block use the given overrides (max_blocks, tiles_per_wave, no_rowgroup, rg_waves, rg_gpt,
+    gen_noreg); same results, other speed.  Restores the defaults on exit."""
+    lib = load_library()
+    t = Tuning(**{k: int(v) for k, v in kw.items()})
+    check(lib.awq_set_tuning(ctypes.byref(t)), "awq_set_tuning")
+    try:
+        yield
+    finally:
+        lib.awq_set_tuning(None)
 
 
 def _upload(host: torch.Tensor, device: torch.device) -> torch.Tensor:
     """Host table -> device on the current stream.  From page-locked memory the copy is
     asynchronous (the CLI pipeline keeps running); torch's caching host allocator holds the
     staging block until the copy has completed, so it may be dropped right away."""
-    if _pageable_tables():
-        return host.to(device)
     pinned = torch.empty(host.shape, dtype=host.dtype, pin_memory=True)
     pinned.copy_(host)
     return pinned.to(device, non_blocking=True)

@@ -10,9 +10,9 @@ only communication is optional and happens after it:
     index without exchanging anything;
   * max_over_ranks(): the bench's max-of-ranks wall time;
   * gather_to_rank0(): point-to-point transfer of every rank's packed outputs to rank 0,
-    one coalesced message per peer (batched isend/irecv: over xGMI each peer has its own
-    link to rank 0, so the 7 senders do not share bandwidth; a ring/all-gather would move
-    7x the bytes).
+    straight from the senders' result tensors into rank 0's final output tensors (batched
+    isend/irecv: over xGMI each peer has its own link to rank 0, so the 7 senders do not
+    share bandwidth; a ring/all-gather would move 7x the bytes).
 
 Everything here runs with the gloo backend on CPU as well (tests/test_distributed.py).
 """
@@ -72,17 +72,16 @@ def max_over_ranks(value: float, device: torch.device) -> float:
     return float(t.item())
 
 
-def _layout(names: Sequence[str], shapes: Dict[str, Dict[str, Tuple[Tuple[int, ...], torch.dtype]]]):
-    """Byte offsets of every (name, field) in one peer's flat message, 16-B aligned so every
-    slice can be viewed back as its dtype; identical on sender and receiver."""
-    off, lay = 0, []
-    for name in names:
-        for field in sorted(shapes[name]):
-            shp, dt = shapes[name][field]
-            nb = int(torch.Size(shp).numel()) * torch.empty((), dtype=dt).element_size()
-            lay.append((name, field, off, nb, tuple(shp), dt))
-            off += -(-nb // 16) * 16
-    return lay, off
+def all_gather_floats(values: Sequence[float], device: torch.device) -> List[List[float]]:
+    """Every rank's small list of floats (same length everywhere), rank-ordered."""
+    if not (dist.is_initialized() and dist.get_world_size() > 1):
+        return [list(map(float, values))]
+    if dist.get_backend() != "nccl":
+        device = torch.device("cpu")
+    t = torch.tensor([float(v) for v in values], dtype=torch.float64, device=device)
+    out = [torch.empty_like(t) for _ in range(dist.get_world_size())]
+    dist.all_gather(out, t)
+    return [o.cpu().tolist() for o in out]
 
 
 def gather_to_rank0(local: Dict[str, Dict[str, torch.Tensor]], owner: Dict[str, int],
@@ -96,44 +95,42 @@ def gather_to_rank0(local: Dict[str, Dict[str, torch.Tensor]], owner: Dict[str, 
             index, identical everywhere) so rank 0 can post its receives up front.
     Returns the merged dict on rank 0 and `local` elsewhere.
 
-    One message per peer: each sender coalesces its results into one flat byte buffer
-    (a device copy of ~0.52 B per quantized element, in the layout _layout() derives from
-    `shapes`), so the exchange is world-1 large point-to-point transfers in one batch —
-    each over its own xGMI link into rank 0 — instead of one small message per tensor field.
+    Zero-copy on both ends: rank 0 allocates each result field once, at its final shape and
+    dtype, and receives straight into it; a sender sends its own result tensors as they are.
+    Rank 0's receive footprint is therefore exactly the merged outputs (no staging buffers,
+    no clones).  All transfers go out as one batch of point-to-point operations, so each
+    peer streams over its own xGMI link into rank 0 concurrently with the others.
     """
     if not (dist.is_initialized() and dist.get_world_size() > 1):
         return local
     rank, world = dist.get_rank(), dist.get_world_size()
-    by_rank: Dict[int, List[str]] = {}
-    for name in sorted(owner):
-        by_rank.setdefault(owner[name], []).append(name)
-    ops, recv = [], {}
-    for src in range(1, world):
-        lay, total = _layout(by_rank.get(src, []), shapes)
-        if total == 0:
+    ops, merged = [], {}
+    for name in sorted(owner):          # the same order on every rank: sends and receives pair up
+        src = owner[name]
+        if src == 0 or rank not in (0, src):
             continue
-        if rank == 0:
-            buf = torch.empty(total, dtype=torch.uint8, device=device)
-            recv[src] = (buf, lay)
-            ops.append(dist.P2POp(dist.irecv, buf, src))
-        elif rank == src:
-            buf = torch.empty(total, dtype=torch.uint8, device=device)
-            for name, field, off, nb, _, _ in lay:
-                t = local[name][field].contiguous()
-                if nb:
-                    buf[off:off + nb].copy_(t.reshape(-1).view(torch.uint8))
-            ops.append(dist.P2POp(dist.isend, buf, 0))
+        for field in sorted(shapes[name]):
+            shp, dt = shapes[name][field]
+            if torch.Size(shp).numel() == 0:
+                continue
+            if rank == 0:
+                t = torch.empty(shp, dtype=dt, device=device)
+                merged.setdefault(name, {})[field] = t
+                ops.append(dist.P2POp(dist.irecv, t, src))
+            else:
+                ops.append(dist.P2POp(dist.isend, local[name][field].contiguous(), 0))
     if ops:
         for req in dist.batch_isend_irecv(ops):
             req.wait()
     if rank != 0:
         return local
-    merged: Dict[str, Dict[str, torch.Tensor]] = {n: local[n] for n in by_rank.get(0, [])}
-    for src in list(recv):
-        buf, lay = recv.pop(src)
-        # own storage per result (a device copy): views of one buffer under different dtypes
-        # cannot be torch.save'd, and the receive buffer is freed peer by peer
-        for name, field, off, nb, shp, dt in lay:
-            merged.setdefault(name, {})[field] = buf[off:off + nb].view(dt).view(shp).clone()
-        del buf
+    for name in owner:
+        if owner[name] == 0:
+            merged[name] = local[name]
+        else:       # (empty fields of a peer's result: nothing crossed the fabric)
+            d = merged.setdefault(name, {})
+            for field in shapes[name]:
+                if field not in d:
+                    shp, dt = shapes[name][field]
+                    d[field] = torch.empty(shp, dtype=dt, device=device)
     return {n: merged[n] for n in owner}

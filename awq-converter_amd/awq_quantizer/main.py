@@ -340,7 +340,7 @@ def _to_cpu(d: Dict[str, torch.Tensor]) -> Dict[str, torch.Tensor]:
 _NOT_LINEAR = ("embed", "lm_head", "norm", "wte", "wpe", "ln_", "router")
 # model types whose projection weights are transformers Conv1D modules, stored [in, out]
 # (quantizing them as [out, in] would group along the wrong axis): copied, not quantized
-CONV1D_MODEL_TYPES = ("gpt2",)
+CONV1D_MODEL_TYPES = ("gpt2", "openai-gpt", "imagegpt", "decision_transformer")
 
 
 def is_linear_weight(info: TensorInfo, group_size: int, model_type: Optional[str] = None) -> bool:
@@ -850,6 +850,13 @@ def _main_distributed(args, loader, ordered: List[TensorInfo], logger, start: fl
     mine = [i for i in ordered if owner[i.name] == rank]
     autoawq = args.output_format == "autoawq"
     per_rank = args.dist_output == "per_rank"
+    if per_rank and not _shared_output_dir(args.output_dir, rank, world, logger):
+        # node-local disks (multi-node torchrun): rank 0's metadata.json could not reach the
+        # other ranks' chunk files, so every result goes to rank 0 instead
+        if rank == 0:
+            logger.warning(f"{args.output_dir} is not one shared directory for all {world} ranks; "
+                           f"falling back to --dist_output gather")
+        per_rank = False
     results: Dict[str, Dict[str, torch.Tensor]] = {}
     writer, failed = None, 0
     t0 = time.time()
@@ -896,6 +903,36 @@ def _main_distributed(args, loader, ordered: List[TensorInfo], logger, start: fl
     if rank == 0 and rc == 0:
         logger.info(f"Quantization complete in {time.time() - start:.2f} seconds")
     return rc
+
+
+def _shared_output_dir(output_dir: str, rank: int, world: int, logger) -> bool:
+    """True if every rank sees the same output directory (per-rank chunk files are only a
+    checkpoint when rank 0's metadata.json and every rank's chunks land in one directory):
+    rank 0 creates a sentinel file with a random name, every rank looks for it."""
+    import secrets
+    import torch.distributed as dist
+    token = [secrets.token_hex(8) if rank == 0 else None]
+    dist.broadcast_object_list(token, src=0)
+    path = os.path.join(output_dir, f".awq_shared_{token[0]}")
+    made = 1
+    if rank == 0:
+        try:
+            os.makedirs(output_dir, exist_ok=True)
+            with open(path, "w") as f:
+                f.write("awq_quantizer per-rank output check\n")
+        except OSError as e:
+            logger.error(f"cannot write to {output_dir}: {e}")
+            made = 0
+    dist.barrier()
+    seen = [None] * world
+    dist.all_gather_object(seen, bool(made) and os.path.exists(path))
+    dist.barrier()
+    if rank == 0 and made:
+        try:
+            os.remove(path)
+        except OSError:
+            pass
+    return all(seen)
 
 
 class _NullSink(dict):
@@ -945,10 +982,12 @@ def _commit_rank_chunks(args, ordered: List[TensorInfo], writer: Optional["Chunk
     for r in range(1, world):
         offs[r] = offs[r - 1] + infos[r - 1]["n_chunks"]
     bad = 0
+    renamed = []
     try:
         for c in range(n_own):
-            os.replace(_chunk_path(args.output_dir, c, st, _rank_stem(rank)),
-                       _chunk_path(args.output_dir, offs[rank] + c, st))
+            dst = _chunk_path(args.output_dir, offs[rank] + c, st)
+            os.replace(_chunk_path(args.output_dir, c, st, _rank_stem(rank)), dst)
+            renamed.append(dst)
     except OSError as e:
         logger.error(f"rank {rank}: renaming chunk files failed: {e}")
         bad = 1
@@ -973,7 +1012,17 @@ def _commit_rank_chunks(args, ordered: List[TensorInfo], writer: Optional["Chunk
             except OSError as e:
                 logger.error(f"Failed to save quantized model: {e}")
                 rc = 1
-    return _agree(rc, comm)
+    rc = _agree(rc, comm)
+    if rc:      # nothing is published: every rank removes the chunk files it wrote
+        tmp = _rank_stem(rank).split("{")[0]
+        leftovers = renamed + [os.path.join(args.output_dir, f) for f in os.listdir(args.output_dir)
+                               if f.startswith(tmp)]
+        for f in leftovers:
+            try:
+                os.remove(f)
+            except OSError:
+                pass
+    return rc
 
 
 def _commit_rank_autoawq(args, loader, ordered: List[TensorInfo], mine: List[TensorInfo],
@@ -1013,7 +1062,15 @@ def _commit_rank_autoawq(args, loader, ordered: List[TensorInfo], mine: List[Ten
     shards = [None] * world
     dist.all_gather_object(shards, {"file": fname, "keys": keys, "size": size, "bad": bad,
                                     "not_converted": [i.name[: -len(".weight")] for i in not_quant]})
+
+    def unpublish():   # nothing is published: every rank removes the shard it wrote
+        if fname and os.path.exists(os.path.join(args.output_dir, fname)):
+            try:
+                os.remove(os.path.join(args.output_dir, fname))
+            except OSError:
+                pass
     if any(s["bad"] for s in shards):
+        unpublish()
         return 1
     rc = 0
     if rank == 0:
@@ -1032,7 +1089,10 @@ def _commit_rank_autoawq(args, loader, ordered: List[TensorInfo], mine: List[Ten
         except Exception as e:  # noqa: BLE001
             logger.error(f"Failed to save quantized model: {e}")
             rc = 1
-    return _agree(rc, comm)
+    rc = _agree(rc, comm)
+    if rc:
+        unpublish()
+    return rc
 
 
 def _gather_and_write(args, loader, ordered: List[TensorInfo], results: Dict[str, Dict[str, torch.Tensor]],

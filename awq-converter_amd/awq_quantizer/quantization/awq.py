@@ -129,12 +129,12 @@ class AWQQuantizer:
             return 0
         return min(self.search_grid, max(1, int(self.search_max_shrink * self.search_grid)))
 
-    def _launch(self, x, rows, K, L, **outs) -> None:
+    def _launch(self, x, rows, K, L, small: bool = False, **outs) -> None:
         if self.scale_method == "search":
             _hip.quantize_search(x, rows, K, L, self.bits, self.symmetric, self.search_grid,
-                                 self.search_candidates, **outs)
+                                 self.search_candidates, small=small, **outs)
         else:
-            _hip.quantize_groups(x, rows, K, L, self.bits, self.symmetric, **outs)
+            _hip.quantize_groups(x, rows, K, L, self.bits, self.symmetric, small=small, **outs)
 
     def _calculate_qmin_qmax(self) -> Tuple[int, int]:
         """awq.py:114-128."""
@@ -211,7 +211,9 @@ class AWQQuantizer:
         tensor_q = torch.empty(rows * K, dtype=torch.int32, device=dev)
         scales = torch.empty((rows, G), dtype=torch.float16, device=dev)
         zeros = torch.empty((rows, G), dtype=torch.int32, device=dev)
-        self._launch(x, rows, K, L, scales=scales, tensor_q=tensor_q, zeros=zeros)
+        # (small-tensor path: its scales reach fp16 straight from the input dtype, awq.py:130-171
+        #  -> 411, not through the fp32 buffer of awq.py:327 — only NaN scale bits differ)
+        self._launch(x, rows, K, L, small=small is not None, scales=scales, tensor_q=tensor_q, zeros=zeros)
         if small == "tensor":
             scales, zeros = scales.reshape(()), zeros.reshape(())
         elif small == "row":

@@ -67,12 +67,19 @@ class PackedBatch:
         self.total_tiles = _hip.plan_ragged(descs, bits, gs)
         self.flags = _hip.ragged_flags(descs, gs)       # padded rows -> the row-tile kernel instance
         self.descs = descs
+        # the tables go up asynchronously on the construction stream (pinned H2D); `ready`
+        # orders any other stream run() is given after them
+        self._stream0 = torch.cuda.current_stream(dev)
         self.descs_dev = _hip.descs_to_device(descs, dev)
         self.block_tensor = _hip.plan_block_tensor(descs, self.total_tiles, dev) if use_block_table else None
+        self._ready = torch.cuda.Event()
+        self._ready.record(self._stream0)
         self.elements = sum(inputs[n].numel() for n in self.names)
 
     def run(self, stream: Optional[torch.cuda.Stream] = None) -> None:
         s = stream if stream is not None else torch.cuda.current_stream(self.device)
+        if s != self._stream0:       # the kernel reads the uploaded tables (raw output pointers)
+            s.wait_event(self._ready)
         _hip.quantize_ragged(self.descs_dev, len(self.descs), self.total_tiles, self.bits, self.symmetric,
                              s.cuda_stream, self.block_tensor, self.dtype, self.group_size, self.flags)
 

@@ -16,6 +16,7 @@
 namespace {
 
 thread_local std::string g_err;
+thread_local awq_tuning g_tuning{};   // include/awq_hip_tuning.h (diagnostics only)
 
 int fail(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
 int fail(int code, const char* fmt, ...) {
@@ -50,8 +51,7 @@ bool fast_eligible(int dtype, int64_t rows, int64_t K, int64_t group_size) {
 // the row-segment kernel (any group size <= 512, bf16 / fp16 / fp32): 16-B aligned input,
 // dword-aligned outputs, segment offsets within int range
 bool rowgroup_shape(int dtype, int64_t rows, int64_t K, int64_t group_size) {
-    if (const char* e = getenv("AWQ_NO_ROWGROUP"))   // A/B against the generic kernel (scripts/generic_bench.py)
-        if (e[0] == '1') return false;
+    if (g_tuning.no_rowgroup) return false;   // A/B against the generic kernel (scripts/generic_bench.py)
     const int gpt = awq::rowgroup_gpt(dtype, K, group_size);
     if (gpt == 0 || rows <= 0 || rows * K >= ((int64_t)1 << 40)) return false;
     const int64_t tiles = rows * (((K + group_size - 1) / group_size + gpt - 1) / gpt);
@@ -67,7 +67,24 @@ bool rowgroup_ok(int dtype, int64_t rows, int64_t K, int64_t group_size, const v
 
 }  // namespace
 
+namespace awq {
+const awq_tuning& tuning() { return g_tuning; }
+}  // namespace awq
+
 extern "C" {
+
+int awq_set_tuning(const awq_tuning* t) {
+    g_err.clear();
+    if (!t) {
+        g_tuning = awq_tuning{};
+        return AWQ_OK;
+    }
+    if (t->max_blocks < 0 || t->tiles_per_wave < 0 || t->rg_waves < 0 || t->rg_waves > 2 || t->rg_gpt < 0 ||
+        t->rg_gpt > 64 || t->rg_gpt % 8 != 0)
+        return fail(AWQ_EINVAL, "bad tuning values");
+    g_tuning = *t;
+    return AWQ_OK;
+}
 
 int awq_packs_directly(int dtype, int64_t rows, int64_t K, int64_t group_size) {
     // every kernel writes qweight / qzeros directly since the generic kernel's span rewrite
@@ -103,9 +120,19 @@ int awq_ragged_eligible(int dtype, int64_t rows, int64_t K, int64_t group_size) 
 int awq_quantize_groups(const void* w, int dtype, int64_t rows, int64_t K, int32_t group_size32,
                         int bits, int symmetric, int32_t* qweight, int32_t* qzeros,
                         uint16_t* scales, int32_t* tensor_q, int32_t* zeros, void* stream) {
+    return awq_quantize_groups_ex(w, dtype, rows, K, group_size32, bits, symmetric, 0, qweight, qzeros, scales,
+                                  tensor_q, zeros, stream);
+}
+
+int awq_quantize_groups_ex(const void* w, int dtype, int64_t rows, int64_t K, int32_t group_size32,
+                           int bits, int symmetric, int flags, int32_t* qweight, int32_t* qzeros,
+                           uint16_t* scales, int32_t* tensor_q, int32_t* zeros, void* stream) {
     g_err.clear();
     const int64_t group_size = group_size32;   // (int32 at the boundary: SURVEY.md §8(b))
     if (int rc = check_common(rows, K, group_size, bits)) return rc;
+    if (flags & ~AWQ_Q_SMALL_TENSOR) return fail(AWQ_EINVAL, "unknown flags 0x%x", flags);
+    const bool small = (flags & AWQ_Q_SMALL_TENSOR) != 0;
+    const uint32_t nan_code = awq::nan_scale_code(dtype, symmetric, small);
     if (dtype < AWQ_DTYPE_BF16 || dtype > AWQ_DTYPE_F64) return fail(AWQ_EINVAL, "unknown dtype code %d", dtype);
     if (!qweight && !qzeros && !scales && !tensor_q && !zeros) return fail(AWQ_EINVAL, "no output requested");
     if (rows * K == 0) return AWQ_OK;
@@ -119,22 +146,31 @@ int awq_quantize_groups(const void* w, int dtype, int64_t rows, int64_t K, int32
         d.tensor_q = tensor_q; d.zeros = zeros; d.tile_begin = 0;
         d.tile_count = awq::fast_tiles(rows, K, bits, (int)group_size);
         return hip_status(awq::launch_fast(nullptr, nullptr, &d, 1, d.tile_count, dtype, bits, symmetric,
-                                           (int)group_size, (K % group_size) != 0, s), "awq fast kernel");
+                                           (int)group_size, (K % group_size) != 0, s, nan_code), "awq fast kernel");
     }
     if (rowgroup_ok(dtype, rows, K, group_size, w, qweight, qzeros, scales, tensor_q, zeros))
         return hip_status(awq::launch_rowgroup(w, dtype, rows, K, group_size, bits, symmetric, qweight, qzeros, scales,
-                                               tensor_q, zeros, s), "awq row-group kernel");
+                                               tensor_q, zeros, s, nan_code), "awq row-group kernel");
     // generic path (fp64, groups > 512): one wave per qzeros word's span, packed words direct
     return hip_status(awq::launch_generic(w, dtype, rows, K, group_size, bits, symmetric, tensor_q, scales, zeros,
-                                          qweight, qzeros, s), "awq generic kernel");
+                                          qweight, qzeros, s, small), "awq generic kernel");
 }
 
 int awq_quantize_search(const void* w, int dtype, int64_t rows, int64_t K, int32_t group_size32, int bits,
                         int symmetric, int n_grid, int n_candidates, int32_t* qweight, int32_t* qzeros,
                         uint16_t* scales, int32_t* tensor_q, int32_t* zeros, void* stream) {
+    return awq_quantize_search_ex(w, dtype, rows, K, group_size32, bits, symmetric, 0, n_grid, n_candidates, qweight,
+                                  qzeros, scales, tensor_q, zeros, stream);
+}
+
+int awq_quantize_search_ex(const void* w, int dtype, int64_t rows, int64_t K, int32_t group_size32, int bits,
+                           int symmetric, int flags, int n_grid, int n_candidates, int32_t* qweight, int32_t* qzeros,
+                           uint16_t* scales, int32_t* tensor_q, int32_t* zeros, void* stream) {
     g_err.clear();
     const int64_t group_size = group_size32;
     if (int rc = check_common(rows, K, group_size, bits)) return rc;
+    if (flags & ~AWQ_Q_SMALL_TENSOR) return fail(AWQ_EINVAL, "unknown flags 0x%x", flags);
+    const bool small = (flags & AWQ_Q_SMALL_TENSOR) != 0;
     if (dtype < AWQ_DTYPE_BF16 || dtype > AWQ_DTYPE_F64) return fail(AWQ_EINVAL, "unknown dtype code %d", dtype);
     if (n_grid < 1 || n_candidates < 1 || n_candidates > n_grid)
         return fail(AWQ_EINVAL, "search grid needs 1 <= n_candidates (%d) <= n_grid (%d)", n_candidates, n_grid);
@@ -152,11 +188,12 @@ int awq_quantize_search(const void* w, int dtype, int64_t rows, int64_t K, int32
         d.tensor_q = tensor_q; d.zeros = zeros; d.tile_begin = 0;
         d.tile_count = awq::fast_tiles(rows, K, bits, (int)group_size);
         return hip_status(awq::launch_fast(nullptr, nullptr, &d, 1, d.tile_count, dtype, bits, symmetric,
-                                           (int)group_size, (K % group_size) != 0, s, n_grid, n_candidates),
+                                           (int)group_size, (K % group_size) != 0, s,
+                                           awq::nan_scale_code(dtype, symmetric, small), n_grid, n_candidates),
                           "awq fast search kernel");
     }
     return hip_status(awq::launch_generic(w, dtype, rows, K, group_size, bits, symmetric, tensor_q, scales, zeros,
-                                          qweight, qzeros, s, n_grid, n_candidates), "awq search kernel");
+                                          qweight, qzeros, s, small, n_grid, n_candidates), "awq search kernel");
 }
 
 int awq_group_params(const void* w, int dtype, int64_t rows, int64_t K, int64_t group_size, int bits,
@@ -168,7 +205,7 @@ int awq_group_params(const void* w, int dtype, int64_t rows, int64_t K, int64_t 
     if (rows * K == 0) return AWQ_OK;
     if (!w) return fail(AWQ_EINVAL, "null input");
     return hip_status(awq::launch_generic(w, dtype, rows, K, group_size, bits, symmetric, nullptr, nullptr, nullptr,
-                                          nullptr, nullptr, (hipStream_t)stream, 1, 0, scales, zeros),
+                                          nullptr, nullptr, (hipStream_t)stream, false, 1, 0, scales, zeros),
                       "awq group params");
 }
 
@@ -250,7 +287,8 @@ int awq_quantize_ragged(const awq_tensor_desc* descs_device, int n, int64_t tota
     if (!descs_device) return fail(AWQ_EINVAL, "null descriptor array");
     return hip_status(awq::launch_fast(descs_device, block_tensor_device, nullptr, n, total_tiles, dtype, bits,
                                        symmetric, (int)group_size, (flags & AWQ_RAGGED_PADDED) != 0,
-                                       (hipStream_t)stream), "awq ragged kernel");
+                                       (hipStream_t)stream, awq::nan_scale_code(dtype, symmetric, false)),
+                      "awq ragged kernel");
 }
 
 int awq_dequantize(const int32_t* tensor_q, const uint16_t* scales, const int32_t* zeros, int64_t rows,

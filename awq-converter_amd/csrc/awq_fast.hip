@@ -459,8 +459,10 @@ __device__ __forceinline__ void quant8_special(const Chunk<F::NW>& v, float z, f
     }
 }
 
-__device__ __forceinline__ uint16_t f16_bits(float s) {
-    if (__builtin_isnan(s)) return 0x7E00;
+// fp16 bits of a group's scale (awq.py:411); NaN scales per nan_scale_code (awq_internal.h):
+// gnan = the group holds a NaN (else the NaN came from inf - inf)
+__device__ __forceinline__ uint16_t f16_bits(float s, bool gnan, uint32_t nan_code) {
+    if (__builtin_isnan(s)) return nan_scale_pick(nan_code, gnan);
     _Float16 h = (_Float16)s;                          // v_cvt_f16_f32: RNE, subnormals kept
     return __builtin_bit_cast(uint16_t, h);
 }
@@ -685,7 +687,7 @@ __device__ __forceinline__ void search_range(const Chunk<F::NW> (&v)[4], float& 
 
 template <typename F, int BITS, bool SYM, bool SEARCH, int GS>
 __device__ __forceinline__ void compute_tile(const TileCtx& c, const Chunk<F::NW> (&v)[4], uint32_t* zw, uint32_t* qstage,
-                                             int n_grid, int n_cand) {
+                                             int n_grid, int n_cand, uint32_t nan_code) {
     constexpr int QMIN = SYM ? -(1 << (BITS - 1)) : 0;
     constexpr uint32_t C = 32u / BITS;   // groups per qzeros word
     constexpr int L = GS / 8;            // lanes per group (8 elements = 16 B per lane)
@@ -838,7 +840,7 @@ __device__ __forceinline__ void compute_tile(const TileCtx& c, const Chunk<F::NW
     if (ch < 4) {
         if (c.scales) {
             __amdgpu_buffer_rsrc_t rs = rsrc(c.scales + c.start, ng * 2u);
-            __builtin_amdgcn_raw_buffer_store_b16(f16_bits(p.s), rs, my_slot * 2u, 0, AWQ_SMALL_AUX);
+            __builtin_amdgcn_raw_buffer_store_b16(f16_bits(p.s, gnan, nan_code), rs, my_slot * 2u, 0, AWQ_SMALL_AUX);
         }
         if (c.zeros) {
             __amdgpu_buffer_rsrc_t rz = rsrc(c.zeros + c.start, ng * 4u);
@@ -930,7 +932,7 @@ __device__ __forceinline__ int64_t xcd_run_block(int64_t b, int64_t nblocks) {
 // shapes.
 // ---------------------------------------------------------------------------------------
 constexpr int kRgStageBytes = 8192;    // eligibility: 8 groups fit (any GPT the cost model picks)
-constexpr int kRgStageMax = 16384;     // tuning override ceiling (AWQ_RG_GPT)
+constexpr int kRgStageMax = 16384;     // tuning override ceiling (rg_gpt)
 
 template <typename F>
 struct RgSlot {
@@ -1023,7 +1025,8 @@ __global__ __launch_bounds__(128) void awq_rowgroup_kernel(const void* __restric
                                                              int64_t G, int C, float invL,
                                                              int32_t* __restrict__ qweight, int32_t* __restrict__ qzeros,
                                                              uint16_t* __restrict__ scales,
-                                                             int32_t* __restrict__ tensor_q, int32_t* __restrict__ zeros) {
+                                                             int32_t* __restrict__ tensor_q, int32_t* __restrict__ zeros,
+                                                             uint32_t nan_code) {
     typedef RgSlot<F> SL;
     typedef typename SL::T S;
     constexpr int QMIN = SYM ? -(1 << (BITS - 1)) : 0;
@@ -1180,7 +1183,7 @@ __global__ __launch_bounds__(128) void awq_rowgroup_kernel(const void* __restric
     if (F::kHasPlain && active && j == 0 && !F::plain_ok(p.s)) not_plain = 1;
     if (active && j == 0) {
         const int64_t gi = r * G + g0 + grp;
-        if (scales) scales[gi] = f16_bits(p.s);
+        if (scales) scales[gi] = f16_bits(p.s, gnan, nan_code);
         if (zeros) zeros[gi] = __builtin_isnan(p.z) ? INT32_MIN : (int32_t)p.z;
         zst[grp] = __builtin_isnan(p.z) ? NANF : ((uint32_t)((int)p.z - QMIN) & MASK);
         prm[grp] = (float4){p.r, p.z, p.s, special ? 1.0f : 0.0f};
@@ -1371,7 +1374,7 @@ __device__ uint64_t* g_trace = nullptr;
 #endif
 
 // One wave per tile.  The grid normally covers every tile once (launch_fast); a smaller
-// grid (AWQ_HIP_MAX_BLOCKS, tests) makes each wave walk tiles t, t + nwaves, ... with a
+// grid (awq_hip_tuning.h max_blocks, tests) makes each wave walk tiles t, t + nwaves, ... with a
 // tensor cursor.
 template <typename F, int BITS, bool SYM, bool SEARCH, int GS, bool PAD>
 __global__ __launch_bounds__(64 * kWavesPerBlock, SEARCH ? 4 : (F::kWide ? AWQ_MIN_WAVES_WIDE : AWQ_MIN_WAVES))
@@ -1380,7 +1383,7 @@ void awq_fast_kernel(
     // preload window of a -mllvm -amdgpu-kernarg-preload-count build); the 80-B single-
     // tensor descriptor goes last
     const int32_t* __restrict__ block_tensor, const awq_tensor_desc* __restrict__ descs, int64_t total_tiles,
-    int n, int n_grid, int n_cand, awq_tensor_desc single) {
+    int n, int n_grid, int n_cand, uint32_t nan_code, awq_tensor_desc single) {
     __shared__ uint32_t zwords[kWavesPerBlock][kTileElems / GS];
 #if AWQ_WIDE_STORE
     __shared__ __attribute__((aligned(16))) uint32_t qstage_all[kWavesPerBlock][BITS == 4 ? 256 : 512];
@@ -1440,7 +1443,7 @@ void awq_fast_kernel(
             tr2 = __builtin_amdgcn_s_memrealtime();
         }
 #endif
-        compute_tile<F, BITS, SYM, SEARCH, GS>(make_ctx<BITS, GS, PAD>(d, tile), va, zw, qs, n_grid, n_cand);
+        compute_tile<F, BITS, SYM, SEARCH, GS>(make_ctx<BITS, GS, PAD>(d, tile), va, zw, qs, n_grid, n_cand, nan_code);
     }
 #ifdef AWQ_TRACE
     if (g_trace != nullptr && (threadIdx.x & 63) == 0) {
@@ -1470,19 +1473,14 @@ __global__ void awq_selftest_recip_kernel(unsigned long long* mismatches) {
 
 hipError_t launch_fast(const awq_tensor_desc* descs_dev, const int32_t* block_tensor,
                        const awq_tensor_desc* single, int n, int64_t total_tiles, int dtype, int bits,
-                       int symmetric, int group_size, bool padded, hipStream_t stream, int n_grid, int n_cand) {
+                       int symmetric, int group_size, bool padded, hipStream_t stream, uint32_t nan_code, int n_grid,
+                       int n_cand) {
     if (total_tiles <= 0) return hipSuccess;
-    // one wave per tile (tuning / tests: AWQ_HIP_TILES_PER_WAVE = tiles per wave,
-    // AWQ_HIP_MAX_BLOCKS = grid cap; either makes waves walk several tiles)
+    // one wave per tile (diagnostics, include/awq_hip_tuning.h: tiles_per_wave, max_blocks =
+    // grid cap; either makes waves walk several tiles)
     int64_t tpw = 1, max_blocks = INT32_MAX;
-    if (const char* e = getenv("AWQ_HIP_TILES_PER_WAVE")) {
-        const long v = atol(e);
-        if (v > 0) tpw = v;
-    }
-    if (const char* e = getenv("AWQ_HIP_MAX_BLOCKS")) {
-        const long v = atol(e);
-        if (v > 0) max_blocks = v;
-    }
+    if (tuning().tiles_per_wave > 1) tpw = tuning().tiles_per_wave;
+    if (tuning().max_blocks > 0) max_blocks = tuning().max_blocks;
     const int64_t per_block = kWavesPerBlock * tpw;
     int64_t blocks = (total_tiles + per_block - 1) / per_block;
     if (blocks > max_blocks) blocks = max_blocks;
@@ -1495,16 +1493,16 @@ hipError_t launch_fast(const awq_tensor_desc* descs_dev, const int32_t* block_te
     do {                                                                                                            \
         if (n_cand > 1 && padded)                                                                                   \
             hipLaunchKernelGGL((awq_fast_kernel<Fm, B, S, true, G, true>), grid, block, 0, stream, bt, descs_dev,   \
-                               total_tiles, n, n_grid, n_cand, one);                                                \
+                               total_tiles, n, n_grid, n_cand, nan_code, one);                                                \
         else if (n_cand > 1)                                                                                        \
             hipLaunchKernelGGL((awq_fast_kernel<Fm, B, S, true, G, false>), grid, block, 0, stream, bt, descs_dev,  \
-                               total_tiles, n, n_grid, n_cand, one);                                                \
+                               total_tiles, n, n_grid, n_cand, nan_code, one);                                                \
         else if (padded)                                                                                            \
             hipLaunchKernelGGL((awq_fast_kernel<Fm, B, S, false, G, true>), grid, block, 0, stream, bt, descs_dev,  \
-                               total_tiles, n, 1, 0, one);                                                          \
+                               total_tiles, n, 1, 0, nan_code, one);                                                          \
         else                                                                                                        \
             hipLaunchKernelGGL((awq_fast_kernel<Fm, B, S, false, G, false>), grid, block, 0, stream, bt, descs_dev, \
-                               total_tiles, n, 1, 0, one);                                                          \
+                               total_tiles, n, 1, 0, nan_code, one);                                                          \
     } while (0)
 #define AWQ_LAUNCH(Fm, B, S)                                   \
     switch (group_size) {                                      \
@@ -1542,7 +1540,7 @@ hipError_t launch_fast(const awq_tensor_desc* descs_dev, const int32_t* block_te
 // per-row cost fitted to measurements (profiles/round2/r2_rowgroup/r2r_*: 14336 x 4096,
 // group sizes 48 / 100, GPT 8..32): tiles x (fixed wave cost 8 + 0.6 per element of a
 // lane's pass-1 chunk C = L / (64 / GPT) + 2.3 per 512-element pass-2 sweep).  gpt = 0 if
-// the shape does not fit the LDS stage.  AWQ_RG_GPT / AWQ_RG_WAVES override (tuning).
+// the shape does not fit the LDS stage.  rg_gpt / rg_waves override (awq_hip_tuning.h).
 struct RgPlan {
     int gpt, waves;
 };
@@ -1550,14 +1548,11 @@ RgPlan rowgroup_plan(int dtype, int64_t K, int64_t L) {
     RgPlan pl = {0, 1};
     if (dtype != AWQ_DTYPE_BF16 && dtype != AWQ_DTYPE_F16 && dtype != AWQ_DTYPE_F32) return pl;
     const int64_t es = dtype == AWQ_DTYPE_F32 ? 4 : 2;
-    if (L <= 0 || K <= 0 || 8 * L * es > kRgStageBytes) return pl;
-    const char* ew = getenv("AWQ_RG_WAVES");
-    if (ew) {
-        const int v = atoi(ew);
-        if (v == 1 || v == 2) pl.waves = v;
-    }
-    if (const char* e = getenv("AWQ_RG_GPT")) {
-        const int v = atoi(e);
+    // (L = 1: a one-element group's NaN scale keeps the element's own NaN bits — generic kernel)
+    if (L < 2 || K <= 0 || 8 * L * es > kRgStageBytes) return pl;
+    const bool ew = tuning().rg_waves == 1 || tuning().rg_waves == 2;
+    if (ew) pl.waves = tuning().rg_waves;
+    if (const int v = tuning().rg_gpt) {
         if (v >= 8 && v <= 64 && v % 8 == 0 && v * L * es <= kRgStageMax) {
             pl.gpt = v;
             return pl;
@@ -1585,7 +1580,7 @@ int rowgroup_gpt(int dtype, int64_t K, int64_t L) { return rowgroup_plan(dtype, 
 
 hipError_t launch_rowgroup(const void* w, int dtype, int64_t rows, int64_t K, int64_t L, int bits, int symmetric,
                            int32_t* qweight, int32_t* qzeros, uint16_t* scales, int32_t* tensor_q, int32_t* zeros,
-                           hipStream_t stream) {
+                           hipStream_t stream, uint32_t nan_code) {
     const RgPlan pl = rowgroup_plan(dtype, K, L);
     const int gpt = pl.gpt;
     if (gpt == 0 || rows <= 0) return hipErrorInvalidValue;
@@ -1601,7 +1596,8 @@ hipError_t launch_rowgroup(const void* w, int dtype, int64_t rows, int64_t K, in
     const size_t lds = ((size_t)gpt * L * (dtype == AWQ_DTYPE_F32 ? 4 : 2) + 15) / 16 * 16 + 48;
 #define AWQ_RG_SPLIT(Fm, B, S, SP)                                                                                 \
     hipLaunchKernelGGL((awq_rowgroup_kernel<Fm, B, S, SP>), grid, block, lds, stream, w, rows, K, L, lgP, gpt,      \
-                       (uint32_t)tpr, G, C, 1.0f / (float)L, qweight, qzeros, scales, tensor_q, zeros)
+                       (uint32_t)tpr, G, C, 1.0f / (float)L, qweight, qzeros, scales, tensor_q, zeros,  \
+                       nan_code)
 #define AWQ_RG(Fm, B, S)                                                                                           \
     if (L % 8 == 0) AWQ_RG_SPLIT(Fm, B, S, 8);                                                                      \
     else if (L % 4 == 0) AWQ_RG_SPLIT(Fm, B, S, 4);                                                                 \

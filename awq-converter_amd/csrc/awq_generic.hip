@@ -36,10 +36,27 @@ using namespace refmath;
 // aligned run of PER lanes into one qweight word with cross-lane shuffles.  qweight / qzeros
 // are written directly for every group size (no int32 staging, no pack pass: round 1 staged
 // 4 B per element and re-read it); tensor_q / zeros / scales / exact parameters are optional.
+// fp16 bits of a group's scale (awq.py:411; fp64 via the fp32 buffer of awq.py:327).  NaN
+// scales per nan_scale_code / nan_scale_one (awq_internal.h): a one-element group (L = 1)
+// keeps its element's NaN, larger groups take the dtype's pattern.
+template <int DT>
+__device__ __forceinline__ uint16_t gen_scale_bits(typename Traits<DT>::C s, int nan, int64_t L, int sym, int small,
+                                                   const typename Traits<DT>::S* w, int64_t at) {
+    if (!(s != s)) return sw_f32_to_f16((float)s);
+    if (L == 1) {
+        uint64_t e;
+        if constexpr (DT == AWQ_DTYPE_F64) e = (uint64_t)__double_as_longlong(w[at]);
+        else if constexpr (DT == AWQ_DTYPE_F32) e = __float_as_uint(w[at]);
+        else e = w[at];
+        return nan_scale_one(DT, sym, small != 0, e, nan != 0);
+    }
+    return nan_scale_pick(nan_scale_code(DT, sym, small != 0), nan != 0);
+}
+
 template <int DT, bool SEARCH>
 __global__ __launch_bounds__(256) void awq_generic_kernel(const void* __restrict__ wv, int64_t rows,
                                                           int64_t K, int64_t L, int bits, int qmin, int qmax,
-                                                          int sym, int n_grid, int n_cand,
+                                                          int sym, int small, int n_grid, int n_cand,
                                                           int32_t* __restrict__ tensor_q,
                                                           uint16_t* __restrict__ scales,
                                                           int32_t* __restrict__ zeros,
@@ -125,7 +142,7 @@ __global__ __launch_bounds__(256) void awq_generic_kernel(const void* __restrict
             za[j] = z;
             zword |= (((uint32_t)to_i32(z) - (uint32_t)qmin) & mask) << (bits * j);
             if (lane == 0) {
-                if (scales) scales[gi] = canon_f16((float)s);         // fp64: via fp32 (awq.py:327)
+                if (scales) scales[gi] = gen_scale_bits<DT>(s, nan, L, sym, small, w, base + k0);
                 if (zeros) zeros[gi] = to_i32(z);
                 if (s_exact) s_exact[gi] = (double)s;                 // the input dtype's values, exact
                 if (z_exact) z_exact[gi] = (double)z;
@@ -185,7 +202,7 @@ constexpr int kDppXor1 = 0xB1, kDppXor2 = 0x4E, kDppHalfMirror = 0x141, kDppMirr
 template <int LPI, int PER>
 __global__ __launch_bounds__(256) void awq_generic_span_reg_kernel(const double* __restrict__ w, int64_t rows,
                                                                    int64_t K, int qmin, int qmax, int sym,
-                                                                   int32_t* __restrict__ tensor_q,
+                                                                   uint32_t nan_code, int32_t* __restrict__ tensor_q,
                                                                    uint16_t* __restrict__ scales,
                                                                    int32_t* __restrict__ zeros,
                                                                    int32_t* __restrict__ qweight,
@@ -257,7 +274,7 @@ __global__ __launch_bounds__(256) void awq_generic_span_reg_kernel(const double*
         zword |= (((uint32_t)to_i32(z) - (uint32_t)qmin) & MASK) << (BITS * j);
         if (lane == 0) {
             const int64_t gi = r * G + g0 + j;
-            if (scales) scales[gi] = canon_f16((float)sc);
+            if (scales) scales[gi] = sc != sc ? nan_scale_pick(nan_code, nan) : sw_f32_to_f16((float)sc);
             if (zeros) zeros[gi] = to_i32(z);
         }
     }
@@ -353,7 +370,10 @@ __global__ __launch_bounds__(256) void awq_dequant_kernel(
         const int32_t diff = (int32_t)((uint32_t)q - (uint32_t)z);
         const float h = sw_f16_to_f32(sw_f32_to_f16((float)diff));
         const float s = sw_f16_to_f32(scales[r * G + g]);
-        out[i] = sw_f16_to_f32(sw_f32_to_f16(h * s));
+        const uint16_t d16 = sw_f32_to_f16(h * s);
+        float v = sw_f16_to_f32(d16);
+        if (v != v) v = __uint_as_float(dq_nan_bits(d16, k - g * L, min(L, K - g * L)));
+        out[i] = v;
     }
 }
 
@@ -383,7 +403,7 @@ __global__ __launch_bounds__(256) void awq_dequant_words_kernel(
         r = i / wpr;
         c = (uint32_t)(i - r * wpr);
     }
-    const uint32_t g = (c * PER) / L;
+    const uint32_t g = (uint32_t)(((uint64_t)c * PER) / L);   // (64-bit: c * PER may pass 2^32)
     const uint32_t wq = (uint32_t)__builtin_nontemporal_load(qweight + i);
     const float s = (float)__builtin_bit_cast(_Float16, scales[r * G + g]);
     const int32_t z = (int32_t)(((uint32_t)qzeros[r * zpr + g / PER] >> (BITS * (g % PER))) & MASK) + qmin;
@@ -392,7 +412,12 @@ __global__ __launch_bounds__(256) void awq_dequant_words_kernel(
     for (int j = 0; j < PER; ++j) {
         const int32_t q = (int32_t)((wq >> (BITS * j)) & MASK) + qmin;
         const float p = (float)(q - z) * s;
-        v[j] = __builtin_isnan(p) ? sw_f16_to_f32(sw_f32_to_f16(p)) : (float)(_Float16)p;
+        if (__builtin_expect(__builtin_isnan(p), 0)) {   // NaN bits of the reference's fp32 copy
+            const int64_t k = (int64_t)c * PER + j, K = (int64_t)wpr * PER, g0 = (int64_t)g * L;
+            v[j] = __uint_as_float(dq_nan_bits(sw_f32_to_f16(p), k - g0, min((int64_t)L, K - g0)));
+        } else {
+            v[j] = (float)(_Float16)p;
+        }
     }
     typedef float f4 __attribute__((ext_vector_type(4)));
     f4* o = (f4*)(out + i * PER);
@@ -414,22 +439,22 @@ inline unsigned grid_for(int64_t work, int64_t per_block, int64_t cap) {
 
 hipError_t launch_generic(const void* w, int dtype, int64_t rows, int64_t K, int64_t L, int bits,
                           int symmetric, int32_t* tensor_q, uint16_t* scales, int32_t* zeros,
-                          int32_t* qweight, int32_t* qzeros, hipStream_t stream, int n_grid, int n_cand,
-                          double* s_exact, double* z_exact) {
+                          int32_t* qweight, int32_t* qzeros, hipStream_t stream, bool small, int n_grid,
+                          int n_cand, double* s_exact, double* z_exact) {
     const int qmin = symmetric ? -(1 << (bits - 1)) : 0;
     const int qmax = symmetric ? (1 << (bits - 1)) - 1 : (1 << bits) - 1;
     const int per = 32 / bits;
     const int64_t G = (K + L - 1) / L;
     const unsigned grid = grid_for(rows * ((G + per - 1) / per), 4, 256 * 16);
     const bool search = n_cand > 0;
-    const char* ne = getenv("AWQ_GEN_NOREG");    // A/B of the register-resident fp64 span
-    const bool noreg = ne && ne[0] == '1';
+    const bool noreg = tuning().gen_noreg != 0;  // A/B of the register-resident fp64 span
     if (dtype == AWQ_DTYPE_F64 && !search && !s_exact && !z_exact && (L == 64 || L == 128) && !noreg) {
         const unsigned blocks = (unsigned)((rows * ((G + per - 1) / per) + 3) / 4);
         const double* wd = (const double*)w;
 #define AWQ_SPAN_REG(LPI, PER)                                                                              \
         hipLaunchKernelGGL((awq_generic_span_reg_kernel<LPI, PER>), dim3(blocks), dim3(256), 0, stream, wd, rows, K, \
-                           qmin, qmax, symmetric, tensor_q, scales, zeros, qweight, qzeros)
+                           qmin, qmax, symmetric, nan_scale_code(AWQ_DTYPE_F64, symmetric, small), tensor_q,     \
+                           scales, zeros, qweight, qzeros)
         if (L == 64) {
             if (per == 8) AWQ_SPAN_REG(1, 8); else AWQ_SPAN_REG(1, 4);
         } else {
@@ -442,12 +467,12 @@ hipError_t launch_generic(const void* w, int dtype, int64_t rows, int64_t K, int
     do {                                                                                             \
         if (search)                                                                                  \
             hipLaunchKernelGGL((awq_generic_kernel<D, true>), dim3(grid), dim3(256), 0, stream, w, rows, \
-                               K, L, bits, qmin, qmax, symmetric, n_grid, n_cand, tensor_q, scales,    \
-                               zeros, qweight, qzeros, s_exact, z_exact);                              \
+                               K, L, bits, qmin, qmax, symmetric, small, n_grid, n_cand, tensor_q,    \
+                               scales, zeros, qweight, qzeros, s_exact, z_exact);                      \
         else                                                                                         \
             hipLaunchKernelGGL((awq_generic_kernel<D, false>), dim3(grid), dim3(256), 0, stream, w,     \
-                               rows, K, L, bits, qmin, qmax, symmetric, 1, 0, tensor_q, scales, zeros, \
-                               qweight, qzeros, s_exact, z_exact);                                     \
+                               rows, K, L, bits, qmin, qmax, symmetric, small, 1, 0, tensor_q, scales, \
+                               zeros, qweight, qzeros, s_exact, z_exact);                              \
     } while (0)
     switch (dtype) {
     case AWQ_DTYPE_BF16: AWQ_GEN(AWQ_DTYPE_BF16); break;

@@ -5,6 +5,7 @@
 #include <stdint.h>
 
 #include "../../include/awq_hip.h"
+#include "../../include/awq_hip_tuning.h"
 
 namespace awq {
 
@@ -102,14 +103,62 @@ __host__ __device__ inline bool fast_shape_ok(int64_t R, int64_t K, int64_t gs) 
     return R * G < (int64_t)0x7FFFFFFF && R * (G + 1) < (int64_t)0x7FFFFFFF;
 }
 
-// launchers (awq_fast.hip / awq_generic.hip)
+// ---------------------------------------------------------------------------
+// fp16 bits of a NaN scale, as the reference's CPU ops leave them (restated and pinned in
+// oracle/awq_oracle.c oracle_nan_scale_f16 against tests/golden/golden_nan.*): torch.min/max
+// over >= 2 elements holding a NaN give the all-ones NaN of the compute type, the scale
+// arithmetic and the stores of awq.py:202-205, 327/352 and 411 then leave
+//   bf16 0x7E00;  fp16 0x7FFF (0xFE00 asym / 0x7E00 sym on the small-tensor path
+//   awq.py:130-171, whose scales skip the fp32 buffer);  fp32 / fp64 0xFFFF, and 0xFE00 for a
+//   NaN made by inf - inf (an asymmetric all-+inf or all--inf group).
+// nan_scale_code packs (group holds a NaN) in the low half and (inf - inf) in the high half.
+// One-element groups (n = 1) keep the element's own NaN: nan_scale_one.
+// ---------------------------------------------------------------------------
+__host__ __device__ inline uint32_t nan_scale_code(int dtype, int sym, bool small) {
+    uint32_t in = 0xFFFFu, ar = 0xFE00u;                   // fp32 / fp64
+    if (dtype == AWQ_DTYPE_BF16) in = ar = 0x7E00u;
+    if (dtype == AWQ_DTYPE_F16) in = ar = !small ? 0x7FFFu : (sym ? 0x7E00u : 0xFE00u);
+    return in | (ar << 16);
+}
+__host__ __device__ inline uint16_t nan_scale_pick(uint32_t code, bool group_nan) {
+    return (uint16_t)(group_nan ? code & 0xFFFFu : code >> 16);
+}
+// n = 1: e = raw bits of the group's element (a NaN, or +-inf for an asymmetric inf - inf)
+__host__ __device__ inline uint16_t nan_scale_one(int dtype, int sym, bool small, uint64_t e, bool e_nan) {
+    if (dtype == AWQ_DTYPE_BF16) return 0x7E00u;
+    if (dtype == AWQ_DTYPE_F16) {
+        if (!small) return 0x7FFFu;
+        if (sym) return 0x7E00u;
+        return e_nan ? (uint16_t)((e & 0x8000u) | 0x7E00u) : (uint16_t)0xFE00u;
+    }
+    if (!e_nan) return 0xFE00u;
+    const bool f64 = dtype == AWQ_DTYPE_F64;
+    uint16_t sign = (uint16_t)(f64 ? (e >> 48) & 0x8000u : (e >> 16) & 0x8000u);
+    const uint16_t m10 = (uint16_t)(f64 ? (e >> 42) & 0x3FFu : (e >> 13) & 0x3FFu);
+    if (sym) sign = 0x8000u;
+    return (uint16_t)(sign | 0x7E00u | m10);
+}
+// dequantize (awq.py:459-539): the fp32 output of a NaN product at in-group position i of a
+// group of n = min(L, K - g L) elements — ATen's fp16 -> fp32 copy (awq.py:527/531) widens
+// 8-element vectors bit-preservingly (f16 NaN bits h) and converts the last n % 8 one by one,
+// which turns any NaN into 0x7FFFFFFF
+__host__ __device__ inline uint32_t dq_nan_bits(uint16_t h, int64_t i, int64_t n) {
+    if (i >= (n & ~(int64_t)7)) return 0x7FFFFFFFu;
+    return ((uint32_t)(h & 0x8000u) << 16) | 0x7F800000u | ((uint32_t)(h & 0x3FFu) << 13);
+}
+
+// the calling thread's diagnostics overrides (include/awq_hip_tuning.h; all zero = defaults)
+const awq_tuning& tuning();
+
+// launchers (awq_fast.hip / awq_generic.hip).  nan_code: nan_scale_code() of the call.
 hipError_t launch_fast(const awq_tensor_desc* descs_dev, const int32_t* block_tensor,
                        const awq_tensor_desc* single, int n, int64_t total_tiles, int dtype, int bits,
-                       int symmetric, int group_size, bool padded, hipStream_t stream, int n_grid = 1,
-                       int n_cand = 0);
+                       int symmetric, int group_size, bool padded, hipStream_t stream, uint32_t nan_code,
+                       int n_grid = 1, int n_cand = 0);
+// small: the small-tensor path (NaN scale bits, see nan_scale_code)
 hipError_t launch_generic(const void* w, int dtype, int64_t rows, int64_t K, int64_t L, int bits,
                           int symmetric, int32_t* tensor_q, uint16_t* scales, int32_t* zeros,
-                          int32_t* qweight, int32_t* qzeros, hipStream_t stream, int n_grid = 1,
+                          int32_t* qweight, int32_t* qzeros, hipStream_t stream, bool small, int n_grid = 1,
                           int n_cand = 0, double* s_exact = nullptr,
                           double* z_exact = nullptr);
 hipError_t launch_apply(const void* x, int dtype, int64_t rows, int64_t K, int64_t L, const double* scales,
@@ -118,7 +167,7 @@ hipError_t launch_apply(const void* x, int dtype, int64_t rows, int64_t K, int64
 int rowgroup_gpt(int dtype, int64_t K, int64_t L);
 hipError_t launch_rowgroup(const void* w, int dtype, int64_t rows, int64_t K, int64_t L, int bits, int symmetric,
                            int32_t* qweight, int32_t* qzeros, uint16_t* scales, int32_t* tensor_q, int32_t* zeros,
-                           hipStream_t stream);
+                           hipStream_t stream, uint32_t nan_code);
 hipError_t launch_selftest(int which, unsigned long long* out, hipStream_t stream);
 hipError_t launch_stream_copy(const void* src, void* dst, int64_t bytes, hipStream_t stream);
 hipError_t launch_stream_ceiling(const void* src, void* dst, int64_t bytes, hipStream_t stream);

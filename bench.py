@@ -230,7 +230,7 @@ def packed_out_shapes(shape, bits, gs):
 
 def gather_leg(batch, rank, world, dev, backend, iters=2, shard_owner=None, all_shapes=None, bits=4, gs=128):
     """N>1 only, after the timed region: the CLI's exchange step (distributed.gather_to_rank0,
-    one coalesced message per peer) on every rank's packed outputs of its shard (the real
+    zero-copy point-to-point into rank 0's outputs) on every rank's packed outputs of its shard (the real
     exchange of the CLI's torchrun mode; with --replica, of its replica).  Reported beside
     `value`, never inside it (the gather is a separate line)."""
     from awq_quantizer import distributed as D
@@ -267,7 +267,7 @@ def gather_leg(batch, rank, world, dev, backend, iters=2, shard_owner=None, all_
                     for i, r in enumerate(shard_owner) if r != 0 for sh, dt in shapes[f"t{i:04d}"].values())
     what = ("gather of the other ranks' packed shards to rank 0" if shard_owner is not None else
             "gather of every rank's packed outputs (one replica) to rank 0")
-    return {"what": what + f", one P2P message per peer ({backend}); outside the timed region",
+    return {"what": what + f", batched P2P straight into rank 0's output tensors ({backend}); outside the timed region",
             "bytes_to_rank0": moved, "ms": round(t * 1e3, 3), "GBs_into_rank0": round(moved / t / 1e9, 2)}
 
 
@@ -402,6 +402,7 @@ def main():
 
     elapsed = D.max_over_ranks(elapsed, dev)
     kern_max_s = D.max_over_ranks(kern_avg_s, dev)
+    per_rank = D.all_gather_floats([kern_avg_s * 1e6, float(elems)], dev)   # [kernel us, elements] by rank
     del batches[1:]
     torch.cuda.empty_cache()
     gather = (gather_leg(batches[0], rank, world, dev, backend, shard_owner=owner,
@@ -447,6 +448,12 @@ def main():
     }
     if traffic_src:
         line["roofline"]["traffic_source"] = traffic_src
+    if world > 1:       # the LPT shard's balance: per-rank kernel time and elements
+        ku = [r[0] for r in per_rank]
+        el = [int(r[1]) for r in per_rank]
+        line["ranks"] = {"kernel_avg_us": [round(v, 2) for v in ku], "elements": el,
+                         "kernel_max_over_min": round(max(ku) / max(min(ku), 1e-9), 4),
+                         "elements_max_over_min": round(max(el) / max(min(el), 1), 4)}
     if gather:
         line["exchange"] = gather
     if written:

@@ -30,7 +30,12 @@
  *             k/(32/bits), bits [bits*(k%(32/bits)), +bits), value (q - qmin) & (2^bits-1)
  *   qzeros    int32     [rows, ceil(G*bits/32)]  same packing of the zero points
  * NaN groups/elements follow the reference: int32 outputs are INT32_MIN (x86 cvtt), packed
- * fields hold (INT32_MIN - qmin) & mask, NaN scales are 0x7E00.
+ * fields hold (INT32_MIN - qmin) & mask, and NaN scales carry the reference's own bits
+ * (awq.py:192-205 -> 327/352 -> 411 on x86 torch CPU; pinned by tests/golden/golden_nan.*):
+ *   bf16 input 0x7E00; fp16 input 0x7FFF (small-tensor path: 0xFE00 asymmetric, 0x7E00
+ *   symmetric); fp32 / fp64 input 0xFFFF when the group holds a NaN, 0xFE00 when the NaN is
+ *   inf - inf (an asymmetric group of all +inf or all -inf); a one-element group keeps its
+ *   element's NaN (sign — set when symmetric — and top 10 mantissa bits, quiet bit set).
  */
 #ifndef AWQ_HIP_H
 #define AWQ_HIP_H
@@ -41,7 +46,7 @@
 extern "C" {
 #endif
 
-#define AWQ_HIP_ABI_VERSION 9
+#define AWQ_HIP_ABI_VERSION 10
 
 /* dtype codes of the input weights (torch dtypes the reference accepts, awq.py:397) */
 enum { AWQ_DTYPE_BF16 = 0, AWQ_DTYPE_F16 = 1, AWQ_DTYPE_F32 = 2, AWQ_DTYPE_F64 = 3 };
@@ -89,6 +94,17 @@ int awq_quantize_groups(const void* w, int dtype, int64_t rows, int64_t K, int32
                         int bits, int symmetric, int32_t* qweight, int32_t* qzeros,
                         uint16_t* scales, int32_t* tensor_q, int32_t* zeros, void* stream);
 
+/* flags of the _ex entry points: the call is the small-tensor path (awq.py:297-300 ->
+ * _calculate_scale_zp awq.py:130-171, numel < group_size, expressed as group_size = K): its
+ * input-dtype scales reach fp16 directly (awq.py:411) instead of through the fp32 [R, G]
+ * buffer of awq.py:327 — only the bits of NaN scales differ (fp16 input, see above). */
+#define AWQ_Q_SMALL_TENSOR 1
+
+/* awq_quantize_groups with flags (0 = awq_quantize_groups). */
+int awq_quantize_groups_ex(const void* w, int dtype, int64_t rows, int64_t K, int32_t group_size,
+                           int bits, int symmetric, int flags, int32_t* qweight, int32_t* qzeros,
+                           uint16_t* scales, int32_t* tensor_q, int32_t* zeros, void* stream);
+
 /* Opt-in per-group clip search (scale_method="search"; no reference counterpart: the
  * reference stores scale_method but never uses it, awq.py:66,111-112 — SURVEY.md §8a).
  * Same inputs/outputs as awq_quantize_groups.  For every group the min/max (after the
@@ -105,6 +121,10 @@ int awq_quantize_groups(const void* w, int dtype, int64_t rows, int64_t K, int32
 int awq_quantize_search(const void* w, int dtype, int64_t rows, int64_t K, int32_t group_size, int bits,
                         int symmetric, int n_grid, int n_candidates, int32_t* qweight, int32_t* qzeros,
                         uint16_t* scales, int32_t* tensor_q, int32_t* zeros, void* stream);
+/* awq_quantize_search with flags (AWQ_Q_SMALL_TENSOR). */
+int awq_quantize_search_ex(const void* w, int dtype, int64_t rows, int64_t K, int32_t group_size, int bits,
+                           int symmetric, int flags, int n_grid, int n_candidates, int32_t* qweight,
+                           int32_t* qzeros, uint16_t* scales, int32_t* tensor_q, int32_t* zeros, void* stream);
 
 /* The reference's per-group scale and zero point (_compute_scale_zp_for_group, awq.py:173-213)
  * in the input dtype's own arithmetic, as exact doubles [rows, G] (bf16 / fp16 / fp32 / fp64
@@ -188,7 +208,9 @@ int awq_stream_copy(const void* src, void* dst, int64_t bytes, void* stream);
 int awq_stream_ceiling(const void* src, void* dst, int64_t bytes, void* stream);
 
 /* Reference dequantize (awq.py:459-539): out fp32 [rows, K] =
- * fp16( fp16(tensor_q - zeros) * scales ) per element. */
+ * fp16( fp16(tensor_q - zeros) * scales ) per element.  A NaN result widens its fp16 bits,
+ * except in the last n % 8 elements of a group of n = min(group_size, K - g group_size)
+ * elements, where it is 0x7FFFFFFF (the reference's fp16 -> fp32 copy, awq.py:527/531). */
 int awq_dequantize(const int32_t* tensor_q, const uint16_t* scales, const int32_t* zeros,
                    int64_t rows, int64_t K, int64_t group_size, float* out, void* stream);
 

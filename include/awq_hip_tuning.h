@@ -1,0 +1,34 @@
+/*
+ * awq_hip_tuning.h — diagnostics / A-B measurement controls of libawq_hip.so.
+ *
+ * NOT part of the drop-in contract (include/awq_hip.h): a caller that never calls
+ * awq_set_tuning gets the library's measured defaults, and nothing else (no environment
+ * variable, no file) changes which kernel or grid produces a result.  Every setting here
+ * gives the same bits as the default (the GPU tests check that); only speed differs.
+ * Thread-local: it applies to launches made from the calling thread.
+ */
+#ifndef AWQ_HIP_TUNING_H
+#define AWQ_HIP_TUNING_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct awq_tuning {
+    int32_t max_blocks;      /* > 0: cap the streaming kernel's grid (waves then walk many tiles) */
+    int32_t tiles_per_wave;  /* > 1: tiles per wave of the streaming kernel's non-persistent grid */
+    int32_t no_rowgroup;     /* 1: shapes of the row-segment kernel take the generic kernel */
+    int32_t rg_waves;        /* 1 or 2: waves per row-segment tile (0 = cost model) */
+    int32_t rg_gpt;          /* 8..64, multiple of 8: groups per row-segment tile (0 = cost model) */
+    int32_t gen_noreg;       /* 1: fp64 gs 64/128 take the strided span instead of the register span */
+} awq_tuning;
+
+/* Set (t != NULL) or reset to the defaults (t == NULL) this thread's tuning. */
+int awq_set_tuning(const awq_tuning* t);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* AWQ_HIP_TUNING_H */

@@ -2,13 +2,14 @@
 """Throughput of the single-tensor entry point (awq_quantize_groups / awq_quantize_search)
 per input dtype and group size: group sizes 32/64/128/256 take the streaming kernel, other
 sizes <= 512 the row-segment kernel, larger ones (and fp64) the generic kernel.
---compare-generic runs every case a second time with AWQ_NO_ROWGROUP=1 (generic kernel +
+--compare-generic runs every case a second time with tuning no_rowgroup=1 (generic kernel +
 int32 staging + pack passes), interleaved in this process.
 
   python scripts/generic_bench.py --shape 14336,4096 --dtypes bf16,f16,f32 --group-sizes 100,128
   python scripts/generic_bench.py --shape "1024,4096;4096,4096" --dtypes bf16   (";" separates shapes)
 """
 import argparse
+import ctypes
 import json
 import os
 import sys
@@ -49,7 +50,7 @@ def one(args, _hip, dev, shape, name, gs, generic):
     qw = torch.empty(R, -(-K // per), dtype=torch.int32, device=dev)
     qz = torch.empty(R, -(-G // per), dtype=torch.int32, device=dev)
     sc = torch.empty(R, G, dtype=torch.float16, device=dev)
-    os.environ["AWQ_NO_ROWGROUP"] = "1" if generic else "0"
+    _hip.load_library().awq_set_tuning(ctypes.byref(_hip.Tuning(no_rowgroup=int(generic))))
     stage = {}
     if args.search or generic or not _hip.packs_directly(DT[name], R, K, gs):
         stage = dict(tensor_q=torch.empty(R * K, dtype=torch.int32, device=dev),
@@ -69,7 +70,7 @@ def one(args, _hip, dev, shape, name, gs, generic):
         run()
     b.record()
     torch.cuda.synchronize()
-    os.environ.pop("AWQ_NO_ROWGROUP", None)
+    _hip.load_library().awq_set_tuning(None)
     us = a.elapsed_time(b) / args.iters * 1e3
     nbytes = x.numel() * x.element_size()
     algo = nbytes + sum(t.numel() * t.element_size() for t in (qw, qz, sc))

@@ -133,12 +133,13 @@ def main():
         for sname, bl in batches.items():
             for lp, lib in handles.items():
                 for blk in args.blocks.split(","):
-                    os.environ.pop("AWQ_HIP_MAX_BLOCKS", None)
-                    os.environ.pop("AWQ_HIP_TILES_PER_WAVE", None)
+                    tun = _hip.Tuning()
                     if blk.startswith("t"):          # t<N>: non-persistent grid, N tiles per wave
-                        os.environ["AWQ_HIP_TILES_PER_WAVE"] = blk[1:]
+                        tun.tiles_per_wave = int(blk[1:])
                     elif blk not in ("0", "nt"):     # nt: no per-block tensor table
-                        os.environ["AWQ_HIP_MAX_BLOCKS"] = blk
+                        tun.max_blocks = int(blk)
+                    if hasattr(lib, "awq_set_tuning"):   # (include/awq_hip_tuning.h; thread-local)
+                        lib.awq_set_tuning(ctypes.byref(tun))
                     evs = []
                     for it in range(args.iters + 3):
                         bt = bl[it % len(bl)]
@@ -159,8 +160,9 @@ def main():
                     us = [a.elapsed_time(b) * 1e3 for a, b in evs]
                     key = (sname, os.path.basename(lp), blk)
                     results.setdefault(key, []).append(statistics.median(us))
-    os.environ.pop("AWQ_HIP_MAX_BLOCKS", None)
-    os.environ.pop("AWQ_HIP_TILES_PER_WAVE", None)
+    for lib in handles.values():
+        if hasattr(lib, "awq_set_tuning"):
+            lib.awq_set_tuning(None)
     print(f"{'set':16s} {'lib':28s} {'blocks':>6s} {'us':>9s} {'algoGB/s':>9s} {'inGB/s':>8s} {'frac8T':>6s}")
     for (sname, lname, blk), v in results.items():
         bt = batches[sname][0]

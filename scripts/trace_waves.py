@@ -34,12 +34,9 @@ def main():
     ap.add_argument("--lib", default=os.path.join(ROOT, "awq-converter_amd/awq_quantizer/_lib/variants/libawq_hip_trace.so"))
     ap.add_argument("--reps", type=int, default=5)
     args = ap.parse_args()
-    for k in ("AWQ_HIP_MAX_BLOCKS", "AWQ_HIP_TILES_PER_WAVE"):
-        os.environ.pop(k, None)
-    os.environ["AWQ_HIP_LIB"] = args.lib
     from awq_quantizer import _hip
     from awq_quantizer.quantization.batch import PackedBatch
-    _hip.load_library()
+    _hip.load_library(args.lib)          # the AWQ_TRACE build, explicitly (first load decides)
     raw = ctypes.CDLL(args.lib)
     dev = torch.device("cuda", 0)
     _hip.require_device(dev)

@@ -59,14 +59,14 @@ def test_export_matches_autoawq_packing(shape, gs, sym, dtype):
     qw, qz, st = orc.autoawq_pack(iw, zz, ref["scales"])
     assert torch.equal(ex["qweight"].cpu(), qw)
     assert torch.equal(ex["qzeros"].cpu(), qz)
-    assert gio.same_bits_nan_eq(ex["scales"].cpu(), st)
+    assert gio.same_bits(ex["scales"].cpu(), st)
     # AutoAWQ-style dequantization of the export == the reference dequantize, transposed
     a, b = orc.autoawq_unpack(ex["qweight"].cpu(), ex["qzeros"].cpu())
     zfull = b.repeat_interleave(gs, dim=0)
     sfull = ex["scales"].cpu().float().repeat_interleave(gs, dim=0)
     diff = (a - zfull).to(torch.float16)
     dq = (diff * sfull.to(torch.float16)).float()
-    assert gio.same_bits_nan_eq(dq.t().contiguous(), orc.dequantize(ref))
+    assert gio.same_bits(dq.t().contiguous(), orc.dequantize(ref))
 
 
 @pytest.mark.gpu

@@ -266,6 +266,8 @@ def test_linear_selection_for_autoawq():
     assert is_linear_weight(mk("model.layers.0.block_sparse_moe.experts.0.w1.weight", (14336, 4096)), 128)
     # GPT-2 Conv1D weights are [in, out]: never quantized as linears
     assert not is_linear_weight(mk("h.0.attn.c_attn.weight", (768, 2304)), 128, "gpt2")
+    for mt in ("openai-gpt", "imagegpt", "decision_transformer"):   # other Conv1D [in, out] models
+        assert not is_linear_weight(mk("h.0.attn.c_attn.weight", (768, 2304)), 128, mt), mt
     assert is_linear_weight(mk("h.0.attn.c_attn.weight", (768, 2304)), 128, "llama")
 
 

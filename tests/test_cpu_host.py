@@ -14,8 +14,12 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def declared_symbols():
-    with open(os.path.join(ROOT, "include", "awq_hip.h")) as f:
-        src = f.read()
+    """Every entry point declared by include/*.h (awq_hip.h + awq_hip_tuning.h)."""
+    src = ""
+    for h in sorted(os.listdir(os.path.join(ROOT, "include"))):
+        if h.endswith(".h"):
+            with open(os.path.join(ROOT, "include", h)) as f:
+                src += f.read()
     return sorted(set(re.findall(r"^\s*(?:int|int64_t|const char\*)\s+(awq_\w+)\s*\(", src, re.M)))
 
 
@@ -26,8 +30,8 @@ def test_library_exports_every_declared_symbol():
     assert len(syms) >= 10
     for s in syms:
         assert hasattr(lib, s), s
-    assert set(syms) == set(_hip.SIGNATURES), "python binding out of sync with include/awq_hip.h"
-    assert lib.awq_abi_version() == _hip.ABI_VERSION == 9
+    assert set(syms) == set(_hip.SIGNATURES), "python binding out of sync with include/*.h"
+    assert lib.awq_abi_version() == _hip.ABI_VERSION == 10
 
 
 def test_library_is_gfx950_code_object():

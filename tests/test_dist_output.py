@@ -69,12 +69,18 @@ def _fake_stream(fmt, fail_rank, rank):
     return quantize_stream
 
 
-def _worker(rank, world, port, model_dir, out_dir, fmt, extra, fail_rank, q):
+def _worker(rank, world, port, model_dir, out_dir, fmt, extra, fail_rank, q, inject=""):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK=str(rank), AWQ_DIST_BACKEND="gloo")
+    if isinstance(out_dir, list):      # per-rank directories: not one shared output directory
+        out_dir = out_dir[rank]
     try:
         from awq_quantizer import main as M
         M.quantize_stream = _fake_stream(fmt, fail_rank, rank)
+        if inject == "meta" and rank == 0:          # the last commit step fails after the renames
+            def bad_meta(*a, **k):
+                raise OSError("disk full (injected)")
+            M._write_metadata = bad_meta
         rc = M.main(["--model_id", model_dir, "--output_dir", out_dir, "--log_level", "CRITICAL", "--chunk_size", "4",
                      "--output_format", fmt] + extra)
         q.put((rank, rc))
@@ -83,13 +89,14 @@ def _worker(rank, world, port, model_dir, out_dir, fmt, extra, fail_rank, q):
         raise
 
 
-def _run(world, model_dir, out_dir, fmt="packed", extra=(), fail_rank=-1):
+def _run(world, model_dir, out_dir, fmt="packed", extra=(), fail_rank=-1, inject=""):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
-    procs = [ctx.Process(target=_worker, args=(r, world, port, model_dir, out_dir, fmt, list(extra), fail_rank, q))
+    procs = [ctx.Process(target=_worker, args=(r, world, port, model_dir, out_dir, fmt, list(extra), fail_rank, q,
+                                               inject))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -227,3 +234,32 @@ def test_autoawq_shards_and_failed_linears(tmp_path, world):
     nc = sorted(n[: -len(".weight")] for n in FAIL_NAMES)
     assert sorted(qc["modules_to_not_convert"]) == nc
     assert sorted(cfg["quantization_config"]["modules_to_not_convert"]) == nc
+
+
+@pytest.mark.timeout(300)
+def test_per_rank_falls_back_to_gather_without_a_shared_directory(tmp_path):
+    """per-rank chunk files are only a checkpoint if every rank writes into the
+    directory rank 0's metadata.json describes.  Ranks that do not see one shared output
+    directory (node-local disks) fall back to the gather layout: rank 0 writes everything."""
+    model_dir, _ = _model(tmp_path)
+    outs = [str(tmp_path / "out0"), str(tmp_path / "out1")]
+    assert _run(2, model_dir, outs, "packed") == [0, 0]
+    ref_dir, _ = _single_process_files(tmp_path, model_dir, "packed", False)
+    meta, got = _load_chunks(outs[0])
+    ref_meta, want = _load_chunks(ref_dir)
+    assert meta == ref_meta
+    for n in want:
+        assert all(torch.equal(got[n][f], want[n][f]) for f in want[n]), n
+    assert not os.path.exists(outs[1]) or [f for f in os.listdir(outs[1]) if "chunk" in f or "shared" in f] == []
+    assert [f for f in os.listdir(outs[0]) if f.startswith(".awq_shared")] == []
+
+
+@pytest.mark.timeout(300)
+def test_failure_after_renames_unpublishes_every_chunk(tmp_path):
+    """when the commit fails after the ranks renamed their chunks to global names
+    (rank 0 cannot write metadata.json), every rank removes what it wrote: nothing stays."""
+    model_dir, _ = _model(tmp_path)
+    out = str(tmp_path / "out")
+    assert _run(2, model_dir, out, "packed", inject="meta") == [1, 1]
+    assert not os.path.exists(os.path.join(out, "metadata.json"))
+    assert [f for f in os.listdir(out) if "chunk" in f] == []

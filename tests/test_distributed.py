@@ -45,17 +45,35 @@ def _worker(rank, world, port, q):
         sizes = [64, 8, 32, 16, 16, 3, 1, 0]   # odd byte counts: 16-B aligned slots; an empty tensor
         owner = dict(zip(names, D.shard(sizes, world)))
         shapes = {n: {"qweight": ((s, 2), torch.int32), "scales": ((s,), torch.float16)} for n, s in zip(names, sizes)}
-        local = {n: {"qweight": torch.full((s, 2), 1000 * i + s, dtype=torch.int32),
-                     "scales": torch.full((s,), float(i), dtype=torch.float16)}
-                 for i, (n, s) in enumerate(zip(names, sizes)) if owner[n] == rank}
+        def content(i, s):     # random bits, NaN / inf patterns included (byte-exact transfer)
+            g = torch.Generator().manual_seed(i)
+            qw = torch.randint(-2 ** 31, 2 ** 31 - 1, (s, 2), generator=g, dtype=torch.int64).to(torch.int32)
+            sc = torch.randint(-2 ** 15, 2 ** 15 - 1, (s,), generator=g, dtype=torch.int32).to(torch.int16)
+            return qw, sc.view(torch.float16)
+        local = {}
+        for i, (n, s) in enumerate(zip(names, sizes)):
+            if owner[n] == rank:
+                qw, sc = content(i, s)
+                local[n] = {"qweight": qw, "scales": sc}
         merged = D.gather_to_rank0(local, owner, shapes, dev)
         t = D.max_over_ranks(float(rank + 1), dev)
+        fl = D.all_gather_floats([float(rank), 2.5 * rank], dev)
         D.barrier()
         if rank == 0:
             ok = sorted(merged) == sorted(names) and t == float(world)
+            ok &= fl == [[float(r), 2.5 * r] for r in range(world)]
+            ptrs = set()
             for i, (n, s) in enumerate(zip(names, sizes)):
-                ok &= bool(torch.equal(merged[n]["qweight"], torch.full((s, 2), 1000 * i + s, dtype=torch.int32)))
-                ok &= bool(torch.equal(merged[n]["scales"], torch.full((s,), float(i), dtype=torch.float16)))
+                qw, sc = content(i, s)
+                ok &= bool(torch.equal(merged[n]["qweight"], qw))
+                ok &= bool(torch.equal(merged[n]["scales"].view(torch.int16), sc.view(torch.int16)))
+                for f, v in merged[n].items():
+                    # bounded receive footprint: every received field is its own exact-size
+                    # allocation (no staging buffer behind views, no second copy)
+                    if owner[n] != 0 and v.numel():
+                        ok &= v.untyped_storage().nbytes() == v.numel() * v.element_size()
+                        ok &= v.data_ptr() not in ptrs
+                        ptrs.add(v.data_ptr())
             import io
             torch.save(merged, io.BytesIO())   # results own their storage (the CLI saves them)
             q.put(("ok" if ok else "mismatch", sorted(merged)))

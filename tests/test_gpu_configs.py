@@ -45,7 +45,7 @@ def _check_full(name, x, out, bits, sym, parity):
     tq = ref["tensor_q"].reshape(rows, -1)
     assert torch.equal(out["qweight"].cpu(), orc.pack_rows(tq, bits, qmin)), name
     assert torch.equal(out["qzeros"].cpu(), orc.pack_rows(ref["zero_points"], bits, qmin)), name
-    assert gio.same_bits_nan_eq(out["scales"].cpu(), ref["scales"]), name
+    assert gio.same_bits(out["scales"].cpu(), ref["scales"]), name
     if parity:
         assert torch.equal(out["tensor_q"].cpu().reshape(rows, -1), tq), name
         assert torch.equal(out["zero_points"].cpu(), ref["zero_points"]), name
@@ -113,10 +113,10 @@ def test_opt350m_streamed_through_cli(tmp_path, fmt):
         if fmt == "reference":
             assert torch.equal(r["tensor_q"], ref["tensor_q"]), name
             assert torch.equal(r["zero_points"], ref["zero_points"]), name
-            assert gio.same_bits_nan_eq(r["scales"], ref["scales"]), name
+            assert gio.same_bits(r["scales"], ref["scales"]), name
             assert (int(r["bits"]), int(r["group_size"]), bool(r["symmetric"])) == (4, 128, False)
         else:
             rows = 1 if x.dim() <= 1 else x.shape[0]
             assert torch.equal(r["qweight"], orc.pack_rows(ref["tensor_q"].reshape(rows, -1), 4, 0)), name
             assert torch.equal(r["qzeros"], orc.pack_rows(ref["zero_points"], 4, 0)), name
-            assert gio.same_bits_nan_eq(r["scales"], ref["scales"]), name
+            assert gio.same_bits(r["scales"], ref["scales"]), name

@@ -45,11 +45,11 @@ def check(x, bits, sym):
     res = q.quantize(x)
     assert torch.equal(res["tensor_q"], ref["tensor_q"])
     assert torch.equal(res["zero_points"], ref["zero_points"])
-    assert gio.same_bits_nan_eq(res["scales"], ref["scales"])
+    assert gio.same_bits(res["scales"], ref["scales"])
     pk = q.quantize_packed(x)
     assert torch.equal(pk["qweight"].cpu(), orc.pack_rows(ref["tensor_q"], bits, q.qmin))
     assert torch.equal(pk["qzeros"].cpu(), orc.pack_rows(ref["zero_points"], bits, q.qmin))
-    assert gio.same_bits_nan_eq(pk["scales"].cpu(), ref["scales"])
+    assert gio.same_bits(pk["scales"].cpu(), ref["scales"])
 
 
 def test_f16_takes_the_streaming_kernel():
@@ -108,7 +108,7 @@ def test_f16_ragged_and_model_packed():
         ref = orc.quantize(inputs[name].cpu(), bits=4, group_size=128, symmetric=False)
         assert torch.equal(res["tensor_q"].cpu(), ref["tensor_q"]), name
         assert torch.equal(res["qweight"].cpu(), orc.pack_rows(ref["tensor_q"], 4, 0)), name
-        assert gio.same_bits_nan_eq(res["scales"].cpu(), ref["scales"]), name
+        assert gio.same_bits(res["scales"].cpu(), ref["scales"]), name
     # mixed dtypes: one ragged launch per dtype
     mixed = {"a": rand16((256, 512), 1, 0.02), "b": rand16((512,), 2, 0.02).to(torch.bfloat16)}
     out = Q(bits=4, symmetric=False).quantize_model_packed(mixed)

@@ -52,14 +52,12 @@ def test_generic_large_groups(dtype, shape, gs):
 
 @pytest.mark.parametrize("dtype,shape,gs", [(torch.bfloat16, (37, 1000), 100), (torch.float16, (9, 777), 3),
                                             (torch.float32, (13, 4100), 128)], ids=str)
-def test_generic_forced_by_env(dtype, shape, gs):
-    """AWQ_NO_ROWGROUP=1 sends the row-segment shapes to the generic kernel: same bits."""
-    os.environ["AWQ_NO_ROWGROUP"] = "1"
-    try:
+def test_generic_forced_by_tuning(dtype, shape, gs):
+    """tuning no_rowgroup=1 sends the row-segment shapes to the generic kernel: same bits."""
+    from awq_quantizer import _hip
+    with _hip.tuning(no_rowgroup=1):
         for bits, sym in ((4, False), (4, True), (8, False)):
             _assert_parity(specials(rand(shape, gs + bits, 0.5), 3).to(dtype), gs, bits, sym)
-    finally:
-        os.environ.pop("AWQ_NO_ROWGROUP", None)
 
 
 @pytest.mark.parametrize("gs", [100, 64], ids=str)
@@ -98,21 +96,19 @@ def test_dequantize_packed_vs_oracle(dtype, shape, gs, bits, sym):
     for key in ("tensor_q", "zero_points"):
         ref[key] = (((ref[key].long() - q.qmin) & ((1 << bits) - 1)) + q.qmin).to(torch.int32)
     dq = q.dequantize_packed(q.quantize_packed(x)).cpu()
-    assert gio.same_bits_nan_eq(dq, orc.dequantize(ref))
+    assert gio.same_bits(dq, orc.dequantize(ref))
 
 
 @pytest.mark.parametrize("gs", [64, 128], ids=str)
 def test_generic_f64_reg_span_matches_strided(gs):
     """The register-resident fp64 span (group sizes 64 / 128) and the strided span kernel
-    (AWQ_GEN_NOREG=1) give the same bits on a ragged shape with special values."""
+    (tuning gen_noreg=1) give the same bits on a ragged shape with special values."""
+    from awq_quantizer import _hip
     x = specials(rand((33, 1000), gs, 1.0), 17).to(torch.float64)
     q = Q(bits=4, group_size=gs, symmetric=False)
     a = q.quantize_packed(x)
-    os.environ["AWQ_GEN_NOREG"] = "1"
-    try:
+    with _hip.tuning(gen_noreg=1):
         b = Q(bits=4, group_size=gs, symmetric=False).quantize_packed(x)
-    finally:
-        os.environ.pop("AWQ_GEN_NOREG", None)
     for key in ("qweight", "qzeros"):
         assert torch.equal(a[key], b[key])
-    assert gio.same_bits_nan_eq(a["scales"], b["scales"])
+    assert gio.same_bits(a["scales"], b["scales"])

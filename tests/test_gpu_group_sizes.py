@@ -52,11 +52,11 @@ def check(x, gs, sym, bits):
     res = q.quantize(x)
     assert torch.equal(res["tensor_q"], ref["tensor_q"])
     assert torch.equal(res["zero_points"], ref["zero_points"])
-    assert gio.same_bits_nan_eq(res["scales"], ref["scales"])
+    assert gio.same_bits(res["scales"], ref["scales"])
     pk = q.quantize_packed(x)
     assert torch.equal(pk["qweight"].cpu(), orc.pack_rows(ref["tensor_q"], bits, q.qmin))
     assert torch.equal(pk["qzeros"].cpu(), orc.pack_rows(ref["zero_points"], bits, q.qmin))
-    assert gio.same_bits_nan_eq(pk["scales"].cpu(), ref["scales"])
+    assert gio.same_bits(pk["scales"].cpu(), ref["scales"])
     return q, pk, ref
 
 
@@ -124,7 +124,7 @@ def test_group_size_ragged_batch(gs, dtype):
                 ref = orc.quantize(inputs[name].cpu(), bits=bits, group_size=gs, symmetric=sym)
                 assert torch.equal(res["tensor_q"].cpu(), ref["tensor_q"]), name
                 assert torch.equal(res["zero_points"].cpu(), ref["zero_points"]), name
-                assert gio.same_bits_nan_eq(res["scales"].cpu(), ref["scales"]), name
+                assert gio.same_bits(res["scales"].cpu(), ref["scales"]), name
                 assert torch.equal(res["qweight"].cpu(), orc.pack_rows(ref["tensor_q"], bits, qmin)), name
                 assert torch.equal(res["qzeros"].cpu(), orc.pack_rows(ref["zero_points"], bits, qmin)), name
 
@@ -157,7 +157,7 @@ def test_group_size_clip_search_vs_oracle(gs, dtype, sym):
     res = q.quantize(x)
     assert torch.equal(res["tensor_q"], ref["tensor_q"])
     assert torch.equal(res["zero_points"], ref["zero_points"])
-    assert gio.same_bits_nan_eq(res["scales"], ref["scales"])
+    assert gio.same_bits(res["scales"], ref["scales"])
 
 
 @pytest.mark.parametrize("gs", GROUP_SIZES)

@@ -45,7 +45,7 @@ def check_batch(b, inputs, gs, sym):
         ref = orc.quantize(x, bits=4, group_size=gs, symmetric=sym)
         assert torch.equal(res["qzeros"].cpu(), orc.pack_rows(ref["zero_points"].reshape(rows, -1), 4, qmin)), name
         assert torch.equal(res["qweight"].cpu(), orc.pack_rows(ref["tensor_q"].reshape(rows, -1), 4, qmin)), name
-        assert gio.same_bits_nan_eq(res["scales"].cpu(), ref["scales"].reshape(rows, -1)), name
+        assert gio.same_bits(res["scales"].cpu(), ref["scales"].reshape(rows, -1)), name
 
 
 def odd_shapes(gs):
@@ -82,7 +82,7 @@ def test_odd_groups_parity_mode_and_single(sym):
     res = q.quantize(x)
     assert torch.equal(res["tensor_q"], ref["tensor_q"])
     assert torch.equal(res["zero_points"], ref["zero_points"])
-    assert gio.same_bits_nan_eq(res["scales"], ref["scales"])
+    assert gio.same_bits(res["scales"], ref["scales"])
     pk = q.quantize_packed(x)
     assert torch.equal(pk["qzeros"].cpu(), orc.pack_rows(ref["zero_points"], 4, q.qmin))
     assert torch.equal(pk["qweight"].cpu(), orc.pack_rows(ref["tensor_q"], 4, q.qmin))
@@ -108,4 +108,4 @@ def test_odd_groups_full_size_embedding():
     ref = orc.quantize(x.cpu(), bits=4, group_size=128, symmetric=False)
     assert torch.equal(outs[0]["qzeros"].cpu(), orc.pack_rows(ref["zero_points"], 4, 0))
     assert torch.equal(outs[0]["qweight"].cpu(), orc.pack_rows(ref["tensor_q"], 4, 0))
-    assert gio.same_bits_nan_eq(outs[0]["scales"].cpu(), ref["scales"])
+    assert gio.same_bits(outs[0]["scales"].cpu(), ref["scales"])

@@ -49,13 +49,13 @@ def check(x, gs, sym, bits, dq=True):
     res = q.quantize(x)
     assert torch.equal(res["tensor_q"], ref["tensor_q"])
     assert torch.equal(res["zero_points"], ref["zero_points"])
-    assert gio.same_bits_nan_eq(res["scales"], ref["scales"])
+    assert gio.same_bits(res["scales"], ref["scales"])
     pk = q.quantize_packed(x)
     assert torch.equal(pk["qweight"].cpu(), orc.pack_rows(ref["tensor_q"].reshape(rows, K), bits, q.qmin))
     assert torch.equal(pk["qzeros"].cpu(), orc.pack_rows(ref["zero_points"], bits, q.qmin))
-    assert gio.same_bits_nan_eq(pk["scales"].cpu(), ref["scales"])
+    assert gio.same_bits(pk["scales"].cpu(), ref["scales"])
     if dq:   # (packed fields cannot carry the reference's INT32_MIN for NaN elements)
-        assert gio.same_bits_nan_eq(q.dequantize_packed(pk).cpu(), orc.dequantize(ref))
+        assert gio.same_bits(q.dequantize_packed(pk).cpu(), orc.dequantize(ref))
 
 
 @pytest.mark.parametrize("bits", [4, 8])
@@ -103,7 +103,7 @@ def test_padded_rows_ragged_mixed(gs):
             ref = orc.quantize(x, bits=bits, group_size=gs, symmetric=False)
             assert torch.equal(res["tensor_q"].cpu(), ref["tensor_q"]), name
             assert torch.equal(res["zero_points"].cpu(), ref["zero_points"].reshape(rows, -1)), name
-            assert gio.same_bits_nan_eq(res["scales"].cpu(), ref["scales"].reshape(rows, -1)), name
+            assert gio.same_bits(res["scales"].cpu(), ref["scales"].reshape(rows, -1)), name
             assert torch.equal(res["qweight"].cpu(), orc.pack_rows(ref["tensor_q"].reshape(rows, -1), bits, 0)), name
             assert torch.equal(res["qzeros"].cpu(), orc.pack_rows(ref["zero_points"].reshape(rows, -1), bits, 0)), name
 
@@ -116,4 +116,4 @@ def test_padded_rows_clip_search(sym):
     res = q.quantize(x)
     assert torch.equal(res["tensor_q"], ref["tensor_q"])
     assert torch.equal(res["zero_points"], ref["zero_points"])
-    assert gio.same_bits_nan_eq(res["scales"], ref["scales"])
+    assert gio.same_bits(res["scales"], ref["scales"])

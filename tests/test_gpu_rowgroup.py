@@ -66,13 +66,13 @@ def _assert_parity(x, gs, bits, sym):
     res = q.quantize(x)
     assert torch.equal(res["tensor_q"], ref["tensor_q"])
     assert torch.equal(res["zero_points"], ref["zero_points"])
-    assert gio.same_bits_nan_eq(res["scales"], ref["scales"])
+    assert gio.same_bits(res["scales"], ref["scales"])
     rows = 1 if x.dim() <= 1 else x.shape[0]
     assert _hip.packs_directly(x.dtype, rows, x.numel() // rows, gs)
     pk = q.quantize_packed(x)
     assert torch.equal(pk["qweight"].cpu(), orc.pack_rows(ref["tensor_q"].reshape(rows, -1), bits, q.qmin))
     assert torch.equal(pk["qzeros"].cpu(), orc.pack_rows(ref["zero_points"], bits, q.qmin))
-    assert gio.same_bits_nan_eq(pk["scales"].cpu(), ref["scales"])
+    assert gio.same_bits(pk["scales"].cpu(), ref["scales"])
 
 
 @pytest.mark.parametrize("bits,sym", [(4, False), (4, True), (8, False), (8, True)], ids=str)
@@ -104,9 +104,8 @@ def test_rowgroup_full_size_gs100():
 
 
 def test_generic_kernel_still_serves_the_rest():
-    """fp64, groups larger than the row-segment stage, and AWQ_NO_ROWGROUP=1 take the generic
+    """fp64, groups larger than the row-segment stage, and tuning no_rowgroup=1 take the generic
     kernel (packed outputs written directly per span of groups, no staging) with the same results."""
-    import os
     from awq_quantizer import _hip
     assert _hip.packs_directly(torch.float64, 4, 1000, 100)
     assert _hip.packs_directly(torch.bfloat16, 4, 5000, 1000)
@@ -118,13 +117,10 @@ def test_generic_kernel_still_serves_the_rest():
         assert torch.equal(q.quantize(x)["tensor_q"], ref["tensor_q"])
         pk = q.quantize_packed(x)
         assert torch.equal(pk["qweight"].cpu(), orc.pack_rows(ref["tensor_q"], 4, 0))
-    os.environ["AWQ_NO_ROWGROUP"] = "1"
-    try:
+    with _hip.tuning(no_rowgroup=1):
         x = rand((37, 1000), 3)
         ref = orc.quantize(x, bits=4, group_size=100, symmetric=False)
         assert torch.equal(Q(bits=4, group_size=100, symmetric=False).quantize(x)["tensor_q"], ref["tensor_q"])
-    finally:
-        os.environ.pop("AWQ_NO_ROWGROUP", None)
 
 
 @pytest.mark.parametrize("gpt", [24, 40, 64], ids=str)
@@ -132,13 +128,10 @@ def test_generic_kernel_still_serves_the_rest():
                                             (torch.float16, (5, 3001), 60), (torch.float32, (6, 2050), 48),
                                             (torch.bfloat16, (200, 61), 7)], ids=str)
 def test_rowgroup_groups_per_tile_override(dtype, shape, gs, gpt):
-    """Groups per tile that are not powers of two (AWQ_RG_GPT tuning override, any multiple
+    """Groups per tile that are not powers of two (rg_gpt tuning override, any multiple
     of 8): P = the largest power of two <= 64 / the tile's groups, the row's light last
     tile with more lanes per group, word-aligned tile boundaries — same bits as the oracle."""
-    import os
-    os.environ["AWQ_RG_GPT"] = str(gpt)
-    try:
+    from awq_quantizer import _hip
+    with _hip.tuning(rg_gpt=gpt):
         for bits, sym in ((4, False), (8, True)):
             _assert_parity(rand(shape, gpt + gs + bits, 0.5, dtype), gs, bits, sym)
-    finally:
-        os.environ.pop("AWQ_RG_GPT", None)

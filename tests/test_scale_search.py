@@ -39,7 +39,7 @@ def test_single_candidate_is_rtn_golden(case):
     T = gio.tensors()
     assert torch.equal(res["tensor_q"], T[case["name"] + ".tensor_q"])
     assert torch.equal(res["zero_points"], T[case["name"] + ".zero_points"])
-    assert gio.same_bits_nan_eq(res["scales"], T[case["name"] + ".scales"])
+    assert gio.same_bits(res["scales"], T[case["name"] + ".scales"])
 
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16, torch.float32])
@@ -65,7 +65,7 @@ def test_search_nan_groups_keep_rtn():
     rtn = orc.quantize(x, bits=4, group_size=128, symmetric=False)
     srch = orc.quantize(x, bits=4, group_size=128, symmetric=False, search=(20, 10))
     for r, g in [(1, 0), (2, 1)]:
-        assert gio.same_bits_nan_eq(srch["scales"][r, g], rtn["scales"][r, g])
+        assert gio.same_bits(srch["scales"][r, g], rtn["scales"][r, g])
         assert torch.equal(srch["tensor_q"][r, g * 128:(g + 1) * 128], rtn["tensor_q"][r, g * 128:(g + 1) * 128])
 
 
@@ -116,7 +116,7 @@ def test_search_gpu_vs_oracle(dtype, shape, gs, sym, bits):
     res = q.quantize(x)
     assert torch.equal(res["tensor_q"], ref["tensor_q"])
     assert torch.equal(res["zero_points"], ref["zero_points"])
-    assert gio.same_bits_nan_eq(res["scales"], ref["scales"])
+    assert gio.same_bits(res["scales"], ref["scales"])
     if x.numel() >= gs:
         pk = q.quantize_packed(x)
         assert torch.equal(pk["qweight"].cpu(), orc.pack_rows(ref["tensor_q"], bits, q.qmin))
@@ -156,7 +156,7 @@ def test_search_gpu_fast_path_special_groups(dtype):
         res = q.quantize(x)
         assert torch.equal(res["tensor_q"], ref["tensor_q"])
         assert torch.equal(res["zero_points"], ref["zero_points"])
-        assert gio.same_bits_nan_eq(res["scales"], ref["scales"])
+        assert gio.same_bits(res["scales"], ref["scales"])
 
 
 @pytest.mark.gpu
@@ -172,12 +172,12 @@ def test_search_gpu_special_values_and_rtn_identity():
                          logger_level="ERROR")
         res = q.quantize(x)
         assert torch.equal(res["tensor_q"], ref["tensor_q"])
-        assert gio.same_bits_nan_eq(res["scales"], ref["scales"])
+        assert gio.same_bits(res["scales"], ref["scales"])
         one = AWQQuantizer(bits=4, symmetric=sym, scale_method="search", search_grid=16,
                            search_max_shrink=1 / 16, device="cuda", logger_level="ERROR").quantize(x)
         rtn = AWQQuantizer(bits=4, symmetric=sym, device="cuda", logger_level="ERROR").quantize(x)
         assert torch.equal(one["tensor_q"], rtn["tensor_q"])
-        assert gio.same_bits_nan_eq(one["scales"], rtn["scales"])
+        assert gio.same_bits(one["scales"], rtn["scales"])
 
 
 @pytest.mark.gpu
@@ -193,4 +193,4 @@ def test_search_gpu_model_packed_routes_generic():
         ref = orc.quantize(t, bits=4, group_size=128, symmetric=False, search=(20, 10))
         rows = 1 if t.dim() == 1 else t.shape[0]
         assert torch.equal(out[n]["qweight"].cpu(), orc.pack_rows(ref["tensor_q"].reshape(rows, -1), 4, 0))
-        assert gio.same_bits_nan_eq(out[n]["scales"].cpu(), ref["scales"])
+        assert gio.same_bits(out[n]["scales"].cpu(), ref["scales"])

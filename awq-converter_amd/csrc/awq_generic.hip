@@ -428,6 +428,86 @@ __global__ __launch_bounds__(256) void awq_dequant_words_kernel(
     }
 }
 
+// The same, with the two memory-side fixes the round-2 PMC asked for (profiles/round2/r2as:
+// 1.15x algorithmic reads, 1.13x writes):
+//  * writes: a 4-bit thread's 8 fp32 results (32 B) went out as two 16-B stores 32 B apart,
+//    so every store instruction half-covered 2 KiB of 64-B lines; here the block's 8 KiB of
+//    results are staged in LDS and each store instruction of a wave writes 1 KiB contiguous
+//    (16 B per lane);
+//  * reads: consecutive blocks (neighbouring words of a row, which share the row's scale and
+//    qzeros lines) were dealt round-robin over the 8 XCDs, each XCD's L2 fetching the shared
+//    lines again; blocks are renumbered so each XCD takes a contiguous range of the words.
+constexpr int kDqThreads = 256;
+
+__device__ __forceinline__ uint32_t xcd_contiguous_block(uint32_t b, uint32_t nb) {
+    const uint32_t full = nb / 8u * 8u;           // blocks b are dealt to XCD b % 8
+    if (b >= full) return b;
+    return (b % 8u) * (full / 8u) + b / 8u;       // XCD x: blocks x * full/8 .. (x+1) * full/8 - 1
+}
+
+template <int BITS>
+__global__ __launch_bounds__(kDqThreads) void awq_dequant_words_v2_kernel(
+    const int32_t* __restrict__ qweight, const uint16_t* __restrict__ scales, const int32_t* __restrict__ qzeros,
+    int64_t words, uint32_t wpr, uint32_t L, uint32_t G, uint32_t zpr, int qmin, float* __restrict__ out) {
+    constexpr int PER = 32 / BITS;
+    constexpr uint32_t MASK = (1u << BITS) - 1u;
+    __shared__ __attribute__((aligned(16))) float stage[kDqThreads * PER];
+    const int64_t blk = xcd_contiguous_block(blockIdx.x, gridDim.x);
+    const int64_t w0 = blk * kDqThreads;
+    const int64_t i = w0 + threadIdx.x;
+    float v[PER];
+    if (i < words) {
+        int64_t r;
+        uint32_t c;
+        if (words <= (int64_t)0xFFFFFFFFu) {
+            const uint32_t r32 = (uint32_t)i / wpr;
+            r = r32;
+            c = (uint32_t)i - r32 * wpr;
+        } else {
+            r = i / wpr;
+            c = (uint32_t)(i - r * wpr);
+        }
+        const uint32_t g = (uint32_t)(((uint64_t)c * PER) / L);
+        const uint32_t wq = (uint32_t)__builtin_nontemporal_load(qweight + i);
+        const float s = (float)__builtin_bit_cast(_Float16, scales[r * G + g]);
+        const int32_t z = (int32_t)(((uint32_t)qzeros[r * zpr + g / PER] >> (BITS * (g % PER))) & MASK) + qmin;
+#pragma unroll
+        for (int j = 0; j < PER; ++j) {
+            const int32_t q = (int32_t)((wq >> (BITS * j)) & MASK) + qmin;
+            const float p = (float)(q - z) * s;
+            if (__builtin_expect(__builtin_isnan(p), 0)) {   // NaN bits of the reference's fp32 copy
+                const int64_t k = (int64_t)c * PER + j, K = (int64_t)wpr * PER, g0 = (int64_t)g * L;
+                v[j] = __uint_as_float(dq_nan_bits(sw_f32_to_f16(p), k - g0, min((int64_t)L, K - g0)));
+            } else {
+                v[j] = (float)(_Float16)p;
+            }
+        }
+    }
+    typedef float f4 __attribute__((ext_vector_type(4)));
+    const int64_t nw = min((int64_t)kDqThreads, words - w0);       // words of this block
+    if (PER == 4 || nw < kDqThreads) {
+        // 8-bit (16 B per thread: one contiguous 1 KiB per wave instruction already) and the
+        // grid's partial last block: direct stores
+        if (i < words) {
+            f4* o = (f4*)(out + i * PER);
+#pragma unroll
+            for (int j = 0; j < PER / 4; ++j)
+                __builtin_nontemporal_store((f4){v[4 * j], v[4 * j + 1], v[4 * j + 2], v[4 * j + 3]}, o + j);
+        }
+        return;
+    }
+    // 4-bit: stage the block's 8 KiB, then lane t of the block stores bytes 16 t + 4 KiB h
+#pragma unroll
+    for (int j = 0; j < PER / 4; ++j)
+        *(f4*)(stage + PER * threadIdx.x + 4 * j) = (f4){v[4 * j], v[4 * j + 1], v[4 * j + 2], v[4 * j + 3]};
+    __syncthreads();
+    f4* o = (f4*)(out + w0 * PER);
+#pragma unroll
+    for (int h = 0; h < PER / 4; ++h)
+        __builtin_nontemporal_store(*(const f4*)(stage + 4 * (threadIdx.x + kDqThreads * h)),
+                                    o + threadIdx.x + kDqThreads * h);
+}
+
 inline unsigned grid_for(int64_t work, int64_t per_block, int64_t cap) {
     int64_t b = (work + per_block - 1) / per_block;
     if (b < 1) b = 1;
@@ -530,15 +610,24 @@ hipError_t launch_dequant(const int32_t* tensor_q, const int32_t* qweight, const
     const int per = 32 / bits;
     const int64_t G = (K + L - 1) / L;
     if (!tensor_q && K % per == 0 && L % per == 0 && ((uintptr_t)out & 15) == 0 && K / per <= 0x7FFFFFFF &&
-        L <= 0x7FFFFFFF && G <= 0x7FFFFFFF && total / per <= ((int64_t)1 << 40)) {
+        L <= 0x7FFFFFFF && G <= 0x7FFFFFFF && total / per < ((int64_t)1 << 32) - 256) {   // one thread per word
         const int64_t words = total / per;
         const uint32_t wpr = (uint32_t)(K / per), zpr = (uint32_t)((G + per - 1) / per);
         const dim3 grid((unsigned)((words + 255) / 256)), block(256);
+        if (tuning().dq_words_v1) {      // round-2 kernel (A/B, awq_hip_tuning.h)
+            if (bits == 4)
+                hipLaunchKernelGGL(awq_dequant_words_kernel<4>, grid, block, 0, stream, qweight, scales, qzeros,
+                                   words, wpr, (uint32_t)L, (uint32_t)G, zpr, qmin, out);
+            else
+                hipLaunchKernelGGL(awq_dequant_words_kernel<8>, grid, block, 0, stream, qweight, scales, qzeros,
+                                   words, wpr, (uint32_t)L, (uint32_t)G, zpr, qmin, out);
+            return hipPeekAtLastError();
+        }
         if (bits == 4)
-            hipLaunchKernelGGL(awq_dequant_words_kernel<4>, grid, block, 0, stream, qweight, scales, qzeros, words,
+            hipLaunchKernelGGL(awq_dequant_words_v2_kernel<4>, grid, block, 0, stream, qweight, scales, qzeros, words,
                                wpr, (uint32_t)L, (uint32_t)G, zpr, qmin, out);
         else
-            hipLaunchKernelGGL(awq_dequant_words_kernel<8>, grid, block, 0, stream, qweight, scales, qzeros, words,
+            hipLaunchKernelGGL(awq_dequant_words_v2_kernel<8>, grid, block, 0, stream, qweight, scales, qzeros, words,
                                wpr, (uint32_t)L, (uint32_t)G, zpr, qmin, out);
         return hipPeekAtLastError();
     }

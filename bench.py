@@ -102,7 +102,7 @@ def parse(argv=None):
                     help="after the timed region: every rank copies its packed shard to the host and writes it as "
                          "chunk files into this directory (the CLI's per-rank output, main.ChunkWriter), reported as "
                          "\"write\" (max over ranks); the files are removed afterwards")
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "round2", "pmc_traffic.json"))
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "round3", "pmc_traffic.json"))
     a = ap.parse_args(argv)
     if a.replica and a.shard:
         ap.error("--replica and --shard are exclusive")
@@ -210,6 +210,10 @@ def cpu_baseline(workload, budget_s, group_size=128, dtype=torch.bfloat16):
     wl_bytes = sum(int(torch.Size(s).numel()) * c for s, c in WORKLOADS[workload]) * esize
     return {"value": round(wl_bytes / total_s / 1e9, 5), "unit": "GB/s", "cores": threads, "kind": "port",
             "node_cpus": node, "affinity_cpus": aff,
+            "cores_note": (f"{threads} threads = the CPU share this GPU box grants one GPU (the pool sets "
+                           f"OMP_NUM_THREADS={threads} and allots 16 CPUs per GPU; the {aff} CPUs of the affinity set "
+                           f"belong to the whole 8-GPU node and its other tenants), so this is the host side one "
+                           f"GPU's job actually gets"),
             "c1_full": {"seconds": round(c1_s, 4), "GBs": round(1024 * 4096 * esize / c1_s / 1e9, 4)},
             "extrapolated_seconds": round(total_s, 2), "shapes_sampled": len(lines),
             "sample": (f"oracle/awq_oracle.c (bit-exact restatement of awq.py, OpenMP over rows, {threads} "
@@ -305,11 +309,26 @@ def write_leg(batch, rank, dev, out_dir, chunk_size=10):
             "s_rank0": round(t, 4), "s_max_over_ranks": round(t_max, 4), "GBs_rank0": round(nbytes / t / 1e9, 3)}
 
 
+KERNEL_SOURCES = ("awq-converter_amd/csrc/awq_fast.hip", "awq-converter_amd/csrc/awq_internal.h")
+
+
+def kernel_source_hash():
+    """sha256 of the streaming kernel's sources (what a recorded PMC traffic figure is valid for)."""
+    import hashlib
+    h = hashlib.sha256()
+    for p in KERNEL_SOURCES:
+        with open(os.path.join(ROOT, p), "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()[:16]
+
+
 def recorded_traffic(path, key):
     """HBM traffic per launch recorded by a separate rocprofv3 --pmc run of this same
     command (scripts/profile_round.sh -> scripts/pmc_traffic.py; FETCH_SIZE x2 gfx950
     correction).  Counters cannot be read in-process, so the field is a RECORDED figure,
-    labelled with its file, the commit it was measured on and the date."""
+    labelled with its file, the commit and the kernel-source hash it was measured on; when
+    the streaming kernel's sources have changed since, it is marked stale and `traffic`
+    is null."""
     try:
         with open(path) as f:
             rec = json.load(f).get(key)
@@ -317,10 +336,13 @@ def recorded_traffic(path, key):
         return None, None
     if not rec:
         return None, None
+    now = kernel_source_hash()
+    stale = rec.get("kernel_source_sha256") != now
     src = {"file": os.path.relpath(path, ROOT), "key": key, "commit": rec.get("commit"), "date": rec.get("date"),
-           "traffic_over_algorithmic": rec.get("traffic_over_algorithmic"),
+           "kernel_source_sha256": rec.get("kernel_source_sha256"), "kernel_source_sha256_now": now,
+           "stale": stale, "traffic_over_algorithmic": rec.get("traffic_over_algorithmic"),
            "note": "recorded by a separate rocprofv3 --pmc pass (FETCH_SIZE x2 + WRITE_SIZE), not this run"}
-    return rec.get("hbm_bytes_per_launch"), src
+    return (None if stale else rec.get("hbm_bytes_per_launch")), src
 
 
 def main():

@@ -31,6 +31,8 @@ def main():
     ap.add_argument("--bits", type=int, default=4)
     ap.add_argument("--compare-generic", action="store_true")
     ap.add_argument("--dequant", action="store_true", help="also time dequantize_packed of the packed result")
+    ap.add_argument("--dq-ab", action="store_true", help="--dequant: also the round-2 word kernel (tuning dq_words_v1), "
+                                                          "interleaved, 3 rounds")
     args = ap.parse_args()
     from awq_quantizer import _hip
     dev = torch.device("cuda", 0)
@@ -86,18 +88,27 @@ def one(args, _hip, dev, shape, name, gs, generic):
 
         def dq():
             _hip.dequantize_packed(qw, qz, sc, R, K, gs, args.bits, False, out)
-        for _ in range(3):
-            dq()
-        a.record()
-        for _ in range(args.iters):
-            dq()
-        b.record()
-        torch.cuda.synchronize()
-        us = a.elapsed_time(b) / args.iters * 1e3
-        algo = out.numel() * 4 + sum(t.numel() * t.element_size() for t in (qw, qz, sc))
-        print(json.dumps({"op": "dequantize_packed", "shape": [R, K], "group_size": gs, "bits": args.bits,
-                          "us": round(us, 1), "algorithmic_GBs": round(algo / us / 1e3, 1),
-                          "frac_8TBs": round(algo / us / 1e3 / 8000, 3)}), flush=True)
+        variants = (0, 1) if args.dq_ab else (0,)
+        ref = None
+        for rnd in range(3 if args.dq_ab else 1):
+            for v in variants:
+                with _hip.tuning(dq_words_v1=v):
+                    for _ in range(3):
+                        dq()
+                    a.record()
+                    for _ in range(args.iters):
+                        dq()
+                    b.record()
+                    torch.cuda.synchronize()
+                if ref is None:
+                    ref = out.clone()
+                same = bool(torch.equal(out.view(torch.int32), ref.view(torch.int32)))
+                us = a.elapsed_time(b) / args.iters * 1e3
+                algo = out.numel() * 4 + sum(t.numel() * t.element_size() for t in (qw, qz, sc))
+                print(json.dumps({"op": "dequantize_packed", "kernel": "words_v1" if v else "words_v2", "round": rnd,
+                                  "shape": [R, K], "group_size": gs, "bits": args.bits, "same_bits": same,
+                                  "us": round(us, 1), "algorithmic_GBs": round(algo / us / 1e3, 1),
+                                  "frac_8TBs": round(algo / us / 1e3 / 8000, 3)}), flush=True)
 
 
 if __name__ == "__main__":

@@ -42,7 +42,7 @@ def main():
     ap.add_argument("--commit", default=None, help="commit the counters were measured on")
     ap.add_argument("--date", default=None)
     ap.add_argument("--out", default=os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
-                                                  "profiles", "round2", "pmc_traffic.json"))
+                                                  "profiles", "round3", "pmc_traffic.json"))
     a = ap.parse_args()
     fetch = read_counter(a.fetch, "FETCH_SIZE")
     write = read_counter(a.write, "WRITE_SIZE")
@@ -55,6 +55,10 @@ def main():
            "fetch_size_kib_median": f_kib, "write_size_kib_median": w_kib, "dispatches": [len(fetch), len(write)],
            "correction": "FETCH_SIZE x2 (gfx950 half-count of 16B/lane streaming reads); WRITE_SIZE as reported"}
     rec["commit"], rec["date"] = a.commit, a.date
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    rec["kernel_source_sha256"] = bench.kernel_source_hash()   # bench.py marks the record stale when it changes
     if a.algo_bytes:
         rec["algorithmic_bytes_per_launch"] = a.algo_bytes
         rec["traffic_over_algorithmic"] = (rd + wr) / a.algo_bytes

@@ -36,6 +36,30 @@ class TensorDesc(ctypes.Structure):
 assert ctypes.sizeof(TensorDesc) == 80
 
 
+class StreamItem(ctypes.Structure):
+    """Mirror of awq_stream_item (include/awq_hip.h)."""
+    _fields_ = [("fd", _I32), ("dtype", _I32), ("offset", _I64), ("rows", _I64), ("K", _I64), ("qweight", _P),
+                ("qzeros", _P), ("scales", _P), ("tensor_q", _P), ("zeros", _P), ("dev_out", _P), ("host_out", _P),
+                ("out_bytes", _I64)]
+
+
+class StreamConfig(ctypes.Structure):
+    """Mirror of awq_stream_config (include/awq_hip.h)."""
+    _fields_ = [("bits", _I32), ("symmetric", _I32), ("group_size", _I32), ("readers", _I32), ("nslots", _I32),
+                ("reserved", _I32), ("slot_bytes", _I64), ("first_batch_bytes", _I64), ("host_staging", _P),
+                ("dev_staging", _P), ("host_tables", _P), ("dev_tables", _P), ("compute_stream", _P),
+                ("h2d_stream", _P), ("d2h_stream", _P)]
+
+
+class StreamStats(ctypes.Structure):
+    """Mirror of awq_stream_stats (include/awq_hip.h)."""
+    _fields_ = [("batches", _I64), ("pieces", _I64), ("bytes_read", _I64), ("wall_s", ctypes.c_double),
+                ("read_busy_s", ctypes.c_double), ("wait_read_s", ctypes.c_double), ("wait_slot_s", ctypes.c_double)]
+
+
+assert ctypes.sizeof(StreamItem) == 96 and ctypes.sizeof(StreamConfig) == 96
+
+
 class Tuning(ctypes.Structure):
     """Mirror of awq_tuning (include/awq_hip_tuning.h): diagnostics / A-B controls only."""
     _fields_ = [("max_blocks", _I32), ("tiles_per_wave", _I32), ("no_rowgroup", _I32), ("rg_waves", _I32),
@@ -67,6 +91,12 @@ SIGNATURES = {
     "awq_pack_rows": (_I32, [_P, _I64, _I64, _I32, _I32, _P, _P]),
     "awq_selftest": (_I32, [_I32, _P, _P]),
     "awq_set_tuning": (_I32, [ctypes.POINTER(Tuning)]),
+    "awq_stream_table_bytes": (_I64, [_I64]),
+    "awq_stream_start": (_I32, [ctypes.POINTER(StreamItem), _I32, ctypes.POINTER(StreamConfig),
+                                ctypes.POINTER(ctypes.c_void_p)]),
+    "awq_stream_batches": (_I64, [_P]),
+    "awq_stream_wait": (_I32, [_P, _I64, ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int32)]),
+    "awq_stream_end": (_I32, [_P, ctypes.POINTER(StreamStats)]),
     "awq_act_stats": (_I32, [_P, _I32, _I64, _I64, _P, _P, _P, _P]),
     "awq_weight_colsum": (_I32, [_P, _I32, _I64, _I64, _I64, _P, _P, _P]),
     "awq_column_mean": (_I32, [_P, _I64, _I64, ctypes.c_double, _P, _P]),

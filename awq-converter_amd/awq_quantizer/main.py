@@ -25,6 +25,7 @@ What changes underneath, MI355X-first:
 """
 
 import argparse
+import ctypes
 import json
 import logging
 import os
@@ -91,6 +92,10 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--dist_output", type=str, default="per_rank", choices=["per_rank", "gather"],
                    help="torchrun mode: per_rank = every rank writes its own chunk files (rank 0 adds "
                         "metadata.json over all of them); gather = results sent to rank 0, which writes everything")
+    p.add_argument("--stream_engine", type=str, default="native", choices=["native", "python"],
+                   help="native: the C++ read -> H2D -> quantize -> D2H pipeline of libawq_hip.so (awq_stream_*); "
+                        "python: the same pipeline driven from Python (the round-2 path; also used for "
+                        "--act_stats and --output_format autoawq)")
     return p
 
 
@@ -230,12 +235,40 @@ def _chunk_path(output_dir: str, c: int, use_safetensors: bool, stem: str = CHUN
     return os.path.join(output_dir, stem.format(c) + (".safetensors" if use_safetensors else ".pt"))
 
 
+_ST_DTYPE = {torch.int32: "I32", torch.int64: "I64", torch.int16: "I16", torch.int8: "I8", torch.uint8: "U8",
+             torch.bool: "BOOL", torch.float16: "F16", torch.bfloat16: "BF16", torch.float32: "F32",
+             torch.float64: "F64"}
+
+
+def save_safetensors(flat: Dict[str, torch.Tensor], path: str) -> None:
+    """A safetensors file (8-byte header length, JSON header, the tensors' bytes back to back)
+    written straight from the tensors' memory: tensors may be views of one buffer (the native
+    pipeline's chunk buffers), which safetensors.torch.save_file refuses to write."""
+    import numpy as np
+    header, off, parts = {}, 0, []
+    for name in sorted(flat):
+        t = flat[name].detach().cpu().contiguous()
+        nb = t.numel() * t.element_size()
+        header[name] = {"dtype": _ST_DTYPE[t.dtype], "shape": list(t.shape), "data_offsets": [off, off + nb]}
+        parts.append(t)
+        off += nb
+    header["__metadata__"] = {"format": "pt"}
+    h = json.dumps(header, separators=(",", ":")).encode()
+    h += b" " * (-len(h) % 8)
+    with open(path, "wb") as f:
+        f.write(len(h).to_bytes(8, "little"))
+        f.write(h)
+        for t in parts:
+            if t.numel():
+                raw = t.reshape(-1).view(torch.uint8) if t.dtype != torch.bool else t.reshape(-1).to(torch.uint8)
+                f.write(memoryview(np.ascontiguousarray(raw.numpy())))
+
+
 def _write_chunk(chunk: Dict[str, Dict[str, torch.Tensor]], output_dir: str, c: int, use_safetensors: bool,
                  logger=None, label: str = "", stem: str = CHUNK_STEM) -> None:
     path = os.path.join(output_dir, stem.format(c))
     if use_safetensors:
-        from safetensors.torch import save_file
-        save_file(_flatten(chunk), path + ".safetensors")
+        save_safetensors(_flatten(chunk), path + ".safetensors")
         if logger:
             logger.info(f"Saved chunk {label or c + 1} with {len(chunk)} tensors in safetensors format")
     else:
@@ -455,12 +488,187 @@ def _pinned_copy(t: torch.Tensor) -> torch.Tensor:
     return p
 
 
+def _out_fields(info: TensorInfo, rows: int, K: int, gs: int, bits: int, packed: bool):
+    """(field, shape, dtype) of one tensor's results: the packed format (quantize_packed) or
+    the reference's result dict (awq.py:409-416)."""
+    per = 32 // bits
+    G = -(-K // gs)
+    if packed:
+        return [("qweight", (rows, -(-K // per)), torch.int32), ("qzeros", (rows, -(-G // per)), torch.int32),
+                ("scales", (rows, G), torch.float16)]
+    return [("tensor_q", tuple(info.shape), torch.int32), ("scales", (rows, G), torch.float16),
+            ("zero_points", (rows, G), torch.int32)]
+
+
+_STREAM_PTR_FIELD = {"qweight": "qweight", "qzeros": "qzeros", "scales": "scales", "tensor_q": "tensor_q",
+                     "zero_points": "zeros"}
+
+
+def quantize_stream_native(loader, infos: List[TensorInfo], quantizer: AWQQuantizer, device: str, readers: int,
+                           packed: bool, out: Dict, lock: threading.Lock, logger, keep_on_device: bool = False,
+                           on_done: Optional[Callable[[str, Optional[Dict[str, torch.Tensor]]], None]] = None,
+                           chunk_of: Optional[Dict[str, int]] = None, slot_bytes: int = 0) -> None:
+    """The CLI's read -> quantize -> collect loop on the native pipeline (include/awq_hip.h
+    awq_stream_*): reader threads pread every tensor from its file into pinned staging slots,
+    one H2D per slot, one ragged launch per dtype per batch, the D2H of the outputs — all
+    native, overlapped, no per-tensor Python in the loop.  Results are views of one device
+    arena and, on the host, of one pinned buffer per output chunk (`chunk_of`: the
+    ChunkWriter's chunk of every tensor, so a chunk file stores only its own tensors' bytes).
+    Tensors smaller than one group (awq.py:297-300) take the per-tensor path afterwards;
+    non-floating tensors are logged and skipped (main.py:387-390)."""
+    from . import _hip
+    t_enter = time.perf_counter()
+    if not (device.startswith("cuda") and torch.cuda.is_available()):
+        quantizer.compute_device()   # raises HipUnavailable: no CPU path
+    dev = torch.device(device)
+    if dev.index is None:
+        dev = torch.device("cuda", torch.cuda.current_device())
+    torch.cuda.set_device(dev)
+    quantizer.compute_device()
+    quantizer._check_mode()
+    gs, bits = quantizer.group_size, quantizer.bits
+    items, small = [], []
+    for info in infos:
+        if info.dtype not in _hip.AWQ_DTYPE:
+            if logger:
+                logger.error(f"Error quantizing tensor: {info.name}, error: Expected floating point tensor, "
+                             f"got {info.dtype}")
+            if on_done:
+                on_done(info.name, None)
+            continue
+        if info.numel < gs:
+            small.append(info)
+            continue
+        rows = 1 if len(info.shape) <= 1 else info.shape[0]
+        items.append((info, rows, info.numel // rows))
+    # output layout: every tensor's fields back to back (16-B aligned) in one device arena, and
+    # per output chunk one pinned host buffer (same relative layout: adjacent D2H ranges merge)
+    lay, dev_total, seg_of, seg_size = [], 0, [], {}
+    for info, rows, K in items:
+        fields, off = [], 0
+        for f, shp, dt in _out_fields(info, rows, K, gs, bits, packed):
+            nb = int(torch.Size(shp).numel()) * torch.empty((), dtype=dt).element_size()
+            fields.append((f, shp, dt, off, nb))
+            off += -(-nb // 16) * 16
+        seg = chunk_of.get(info.name, 0) if chunk_of else len(lay) // 16
+        lay.append((fields, off, dev_total, seg, seg_size.get(seg, 0)))
+        seg_size[seg] = seg_size.get(seg, 0) + off
+        dev_total += off
+    arena = torch.empty(max(dev_total, 16), dtype=torch.uint8, device=dev)
+    hosts = {} if keep_on_device else {s: torch.empty(max(n, 16), dtype=torch.uint8, pin_memory=True)
+                                       for s, n in seg_size.items()}
+    lib = _hip.load_library()
+    arr = (_hip.StreamItem * max(1, len(items)))()
+    base = arena.data_ptr()
+    for k, ((info, rows, K), (fields, nbytes, doff, seg, hoff)) in enumerate(zip(items, lay)):
+        fd, at = loader.data_location(info)
+        it = arr[k]
+        it.fd, it.dtype, it.offset = fd, _hip.AWQ_DTYPE[info.dtype], at
+        it.rows, it.K = rows, K
+        for f, _, _, off, _ in fields:
+            setattr(it, _STREAM_PTR_FIELD[f], base + doff + off)
+        it.dev_out, it.out_bytes = base + doff, nbytes
+        it.host_out = None if keep_on_device else hosts[seg].data_ptr() + hoff
+    total_in = sum(i.nbytes for i, _, _ in items)
+    slot = slot_bytes or min(256 << 20, max(32 << 20, total_in // 8))
+    slot = -(-slot // 4096) * 4096
+    nslots = 3
+    tb = int(lib.awq_stream_table_bytes(slot))
+    h_stage = torch.empty(nslots * slot, dtype=torch.uint8, pin_memory=True)
+    d_stage = torch.empty(nslots * slot, dtype=torch.uint8, device=dev)
+    h_tab = torch.empty(nslots * tb, dtype=torch.uint8, pin_memory=True)
+    d_tab = torch.empty(nslots * tb, dtype=torch.uint8, device=dev)
+    compute = torch.cuda.current_stream(dev)
+    h2d, d2h = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+    cfg = _hip.StreamConfig(bits=bits, symmetric=int(bool(quantizer.symmetric)), group_size=gs,
+                            readers=min(16, max(8, readers)), nslots=nslots, slot_bytes=slot,
+                            first_batch_bytes=max(4096, slot // 4 // 4096 * 4096),
+                            host_staging=h_stage.data_ptr(), dev_staging=d_stage.data_ptr(),
+                            host_tables=h_tab.data_ptr(), dev_tables=d_tab.data_ptr(),
+                            compute_stream=compute.cuda_stream, h2d_stream=h2d.cuda_stream,
+                            d2h_stream=d2h.cuda_stream)
+    handle = ctypes.c_void_p()
+    t_run = time.perf_counter()
+    _hip.check(lib.awq_stream_start(arr, len(items), ctypes.byref(cfg), ctypes.byref(handle)), "awq_stream_start")
+    stats = _hip.StreamStats()
+    t_wait = 0.0
+    try:
+        # while the pipeline runs: the result dicts (views of the arena / the chunk buffers)
+        scal = {"bits": torch.tensor(bits, dtype=torch.int32), "group_size": torch.tensor(gs, dtype=torch.int32),
+                "symmetric": torch.tensor(bool(quantizer.symmetric), dtype=torch.bool)}
+        results = []
+        for (info, rows, K), (fields, nbytes, doff, seg, hoff) in zip(items, lay):
+            src, at = (arena, doff) if keep_on_device else (hosts[seg], hoff)
+            r = {f: src[at + off:at + off + nb].view(dt).view(shp) for f, shp, dt, off, nb in fields}
+            r.update(scal)
+            if packed:
+                r["shape"] = torch.tensor(list(info.shape), dtype=torch.int64)
+            results.append(r)
+        nb_ = int(lib.awq_stream_batches(handle))
+        i0, i1 = ctypes.c_int32(), ctypes.c_int32()
+        for b in range(nb_):
+            t0 = time.perf_counter()
+            _hip.check(lib.awq_stream_wait(handle, b, ctypes.byref(i0), ctypes.byref(i1)), "awq_stream_wait")
+            t_wait += time.perf_counter() - t0
+            done = {items[k][0].name: results[k] for k in range(i0.value, i1.value)}
+            with lock:
+                out.update(done)
+            if on_done:
+                for name, r in done.items():
+                    on_done(name, r)
+    finally:
+        rc = lib.awq_stream_end(handle, ctypes.byref(stats))
+    _hip.check(rc, "awq_stream_end")
+    if keep_on_device:
+        compute.wait_stream(d2h)
+    for info in small:                    # awq.py:297-300: the per-tensor path
+        try:
+            x = loader.read(info)
+            res = quantizer.quantize_model_device({info.name: x}, packed=packed)
+            r = {k: (v.cpu() if isinstance(v, torch.Tensor) and not keep_on_device else v)
+                 for k, v in res.get(info.name, {}).items()} if info.name in res else None
+        except Exception as e:  # noqa: BLE001
+            if logger:
+                logger.error(f"Error quantizing tensor: {info.name}, error: {e}")
+            r = None
+        if r is not None:
+            with lock:
+                out[info.name] = r
+        if on_done:
+            on_done(info.name, r)
+    TIMINGS.update({f"stream_{device}": {"engine": "native", "wall_s": round(time.perf_counter() - t_enter, 4),
+                                          "setup_s": round(t_run - t_enter, 4), "batches": int(stats.batches),
+                                          "pieces": int(stats.pieces), "slot_MB": slot >> 20,
+                                          "pipeline_s": round(stats.wall_s, 4), "wait_s": round(t_wait, 4),
+                                          "read_busy_s": round(stats.read_busy_s, 4),
+                                          "submit_wait_read_s": round(stats.wait_read_s, 4),
+                                          "submit_wait_slot_s": round(stats.wait_slot_s, 4),
+                                          "bytes_read": int(stats.bytes_read)}})
+
+
 def quantize_stream(loader, infos: List[TensorInfo], quantizer: AWQQuantizer, device: str, readers: int,
                     lookahead: int, packed: bool, out: Dict, lock: threading.Lock, logger,
                     memory_efficient: bool = False, keep_on_device: bool = False,
                     batch_bytes: int = 1 << 30, export_autoawq: bool = False,
                     act_stats: Optional[Dict[str, Tuple[torch.Tensor, torch.Tensor]]] = None,
-                    on_done: Optional[Callable[[str, Optional[Dict[str, torch.Tensor]]], None]] = None) -> None:
+                    on_done: Optional[Callable[[str, Optional[Dict[str, torch.Tensor]]], None]] = None,
+                    chunk_of: Optional[Dict[str, int]] = None, engine: str = "native") -> None:
+    """Quantize `infos` on one GPU.  RTN to the packed or reference format runs on the native
+    pipeline (quantize_stream_native); the activation-aware search (`act_stats`), the
+    AutoAWQ export and `engine="python"` on the Python pipeline below."""
+    if engine == "native" and not act_stats and not export_autoawq and hasattr(loader, "data_location"):
+        return quantize_stream_native(loader, infos, quantizer, device, readers, packed, out, lock, logger,
+                                      keep_on_device=keep_on_device, on_done=on_done, chunk_of=chunk_of)
+    return quantize_stream_python(loader, infos, quantizer, device, readers, lookahead, packed, out, lock, logger,
+                                  memory_efficient, keep_on_device, batch_bytes, export_autoawq, act_stats, on_done)
+
+
+def quantize_stream_python(loader, infos: List[TensorInfo], quantizer: AWQQuantizer, device: str, readers: int,
+                           lookahead: int, packed: bool, out: Dict, lock: threading.Lock, logger,
+                           memory_efficient: bool = False, keep_on_device: bool = False,
+                           batch_bytes: int = 1 << 30, export_autoawq: bool = False,
+                           act_stats: Optional[Dict[str, Tuple[torch.Tensor, torch.Tensor]]] = None,
+                           on_done: Optional[Callable[[str, Optional[Dict[str, torch.Tensor]]], None]] = None) -> None:
     """Quantize `infos` on one GPU as a pipeline over batches of tensors (<= batch_bytes of
     input each):
 
@@ -762,18 +970,19 @@ def main(argv: Optional[List[str]] = None) -> int:
         lookahead = max(1, args.prefetch_factor * args.batch_size)
         packed = args.output_format in ("packed", "autoawq")
         # chunked output written while later batches are still being read and quantized
-        # (AWQ_CLI_SERIAL_SAVE=1: after everything, like the reference)
         writer = None
-        if not autoawq and os.environ.get("AWQ_CLI_SERIAL_SAVE", "0") != "1":
+        if not autoawq:
             writer = ChunkWriter([i.name for i in ordered], args.output_dir, args.chunk_size, args.save_safetensors,
                                  logger)
+        chunk_of = {i.name: k // args.chunk_size for k, i in enumerate(ordered)}
         threads = []
         for d, part in zip(devices, parts):
             logger.info(f"Processing {len(part)} tensors on {d}")
             th = threading.Thread(target=_device_worker, args=(loader, part, quantizers[d], d, args.num_workers,
                                                                lookahead, packed, results, lock, logger,
                                                                args.memory_efficient, False, 1 << 30, autoawq),
-                                  kwargs={"act_stats": act_stats, "on_done": writer.done if writer else None})
+                                  kwargs={"act_stats": act_stats, "on_done": writer.done if writer else None,
+                                          "chunk_of": chunk_of, "engine": args.stream_engine})
             th.start()
             threads.append(th)
         for th in threads:
@@ -876,7 +1085,9 @@ def _main_distributed(args, loader, ordered: List[TensorInfo], logger, start: fl
         quantize_stream(loader, mine, q, device, args.num_workers, max(1, args.prefetch_factor * args.batch_size),
                         args.output_format in ("packed", "autoawq"), sink, threading.Lock(), logger,
                         args.memory_efficient, keep_on_device=not per_rank, export_autoawq=autoawq,
-                        act_stats=act_stats, on_done=writer.done if writer else None)
+                        act_stats=act_stats, on_done=writer.done if writer else None,
+                        chunk_of={i.name: k // args.chunk_size for k, i in enumerate(mine)},
+                        engine=args.stream_engine)
     except Exception as e:  # noqa: BLE001  (agreed below: every rank exits 1)
         logger.error(f"rank {rank}: quantization failed: {e}")
         failed = 1

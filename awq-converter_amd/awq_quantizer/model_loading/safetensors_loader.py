@@ -111,6 +111,12 @@ class SafetensorsLoader:
                 self._fds[path] = os.open(path, os.O_RDONLY)
             return lay
 
+    def data_location(self, info: TensorInfo) -> Tuple[int, int]:
+        """(open file descriptor, absolute byte offset) of a tensor's data, for native
+        readers (include/awq_hip.h awq_stream_*); the descriptor lives until close()."""
+        start, offs = self._layout(info.file)
+        return self._fds[info.file], start + offs[info.name][0]
+
     def read_pinned(self, info: TensorInfo) -> torch.Tensor:
         """Read one tensor into page-locked host memory."""
         if info.dtype is None:

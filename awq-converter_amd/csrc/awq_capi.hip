@@ -29,6 +29,14 @@ int fail(int code, const char* fmt, ...) {
     return code;
 }
 
+}  // namespace
+
+namespace awq {
+int set_error(int code, const char* msg) { return fail(code, "%s", msg); }   // (awq_stream.hip)
+}  // namespace awq
+
+namespace {
+
 int hip_status(hipError_t e, const char* what) {
     if (e == hipSuccess) return AWQ_OK;
     return fail(AWQ_EHIP, "%s: %s", what, hipGetErrorString(e));

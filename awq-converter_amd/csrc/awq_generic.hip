@@ -445,14 +445,14 @@ __device__ __forceinline__ uint32_t xcd_contiguous_block(uint32_t b, uint32_t nb
     return (b % 8u) * (full / 8u) + b / 8u;       // XCD x: blocks x * full/8 .. (x+1) * full/8 - 1
 }
 
-template <int BITS>
+template <int BITS, bool REMAP>
 __global__ __launch_bounds__(kDqThreads) void awq_dequant_words_v2_kernel(
     const int32_t* __restrict__ qweight, const uint16_t* __restrict__ scales, const int32_t* __restrict__ qzeros,
     int64_t words, uint32_t wpr, uint32_t L, uint32_t G, uint32_t zpr, int qmin, float* __restrict__ out) {
     constexpr int PER = 32 / BITS;
     constexpr uint32_t MASK = (1u << BITS) - 1u;
     __shared__ __attribute__((aligned(16))) float stage[kDqThreads * PER];
-    const int64_t blk = xcd_contiguous_block(blockIdx.x, gridDim.x);
+    const int64_t blk = REMAP ? xcd_contiguous_block(blockIdx.x, gridDim.x) : blockIdx.x;
     const int64_t w0 = blk * kDqThreads;
     const int64_t i = w0 + threadIdx.x;
     float v[PER];
@@ -614,7 +614,7 @@ hipError_t launch_dequant(const int32_t* tensor_q, const int32_t* qweight, const
         const int64_t words = total / per;
         const uint32_t wpr = (uint32_t)(K / per), zpr = (uint32_t)((G + per - 1) / per);
         const dim3 grid((unsigned)((words + 255) / 256)), block(256);
-        if (tuning().dq_words_v1) {      // round-2 kernel (A/B, awq_hip_tuning.h)
+        if (tuning().dq_words_v1 == 1) {      // round-2 kernel (A/B, awq_hip_tuning.h)
             if (bits == 4)
                 hipLaunchKernelGGL(awq_dequant_words_kernel<4>, grid, block, 0, stream, qweight, scales, qzeros,
                                    words, wpr, (uint32_t)L, (uint32_t)G, zpr, qmin, out);
@@ -623,12 +623,21 @@ hipError_t launch_dequant(const int32_t* tensor_q, const int32_t* qweight, const
                                    words, wpr, (uint32_t)L, (uint32_t)G, zpr, qmin, out);
             return hipPeekAtLastError();
         }
+        if (tuning().dq_words_v1 == 2) {      // + XCD-contiguous blocks (A/B)
+            if (bits == 4)
+                hipLaunchKernelGGL((awq_dequant_words_v2_kernel<4, true>), grid, block, 0, stream, qweight, scales,
+                                   qzeros, words, wpr, (uint32_t)L, (uint32_t)G, zpr, qmin, out);
+            else
+                hipLaunchKernelGGL((awq_dequant_words_v2_kernel<8, true>), grid, block, 0, stream, qweight, scales,
+                                   qzeros, words, wpr, (uint32_t)L, (uint32_t)G, zpr, qmin, out);
+            return hipPeekAtLastError();
+        }
         if (bits == 4)
-            hipLaunchKernelGGL(awq_dequant_words_v2_kernel<4>, grid, block, 0, stream, qweight, scales, qzeros, words,
-                               wpr, (uint32_t)L, (uint32_t)G, zpr, qmin, out);
+            hipLaunchKernelGGL((awq_dequant_words_v2_kernel<4, false>), grid, block, 0, stream, qweight, scales, qzeros,
+                               words, wpr, (uint32_t)L, (uint32_t)G, zpr, qmin, out);
         else
-            hipLaunchKernelGGL(awq_dequant_words_v2_kernel<8>, grid, block, 0, stream, qweight, scales, qzeros, words,
-                               wpr, (uint32_t)L, (uint32_t)G, zpr, qmin, out);
+            hipLaunchKernelGGL((awq_dequant_words_v2_kernel<8, false>), grid, block, 0, stream, qweight, scales, qzeros,
+                               words, wpr, (uint32_t)L, (uint32_t)G, zpr, qmin, out);
         return hipPeekAtLastError();
     }
     hipLaunchKernelGGL(awq_dequant_kernel, dim3(grid_for(total, 256, 256 * 16)), dim3(256), 0, stream,

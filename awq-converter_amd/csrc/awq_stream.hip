@@ -1,0 +1,494 @@
+// awq_stream.hip — the host streaming pipeline of include/awq_hip.h (awq_stream_*).
+//
+// Replaces the CLI's per-tensor loop (reference main.py:216-392: every file loaded whole,
+// then tensor by tensor through the Python quantizer) with a native pipeline over batches
+// of tensors that fill fixed staging slots:
+//
+//   reader threads   pread the batch's tensors from their files into pinned slot b % nslots
+//                    (large tensors in 16 MiB pieces across the threads); a slot is refilled
+//                    once the H2D copy of the batch that used it before has completed
+//   submitter thread H2D of the whole slot (one copy, h2d stream), then on the compute
+//                    stream one ragged launch per dtype (awq_quantize_ragged, descriptor and
+//                    tensor tables uploaded from the slot's pinned table area) and
+//                    awq_quantize_groups_ex for the shapes the ragged kernel does not take,
+//                    then the D2H of the outputs of the tensors the batch completes (d2h
+//                    stream, adjacent ranges coalesced)
+//   caller           awq_stream_wait(b) per batch, then hands those tensors on (the CLI's
+//                    chunk writer), while the next batches are read, copied and quantized.
+//
+// It is a client of the quantizer's own C ABI (awq_plan_ragged, awq_plan_block_tensor,
+// awq_ragged_flags, awq_quantize_ragged, awq_quantize_groups_ex): the kernels see exactly the
+// launches a single-process caller would make, on sub-tensors of whole rows.
+#include <unistd.h>
+
+#include <algorithm>
+#include <cerrno>
+#include <chrono>
+#include <condition_variable>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "awq_internal.h"
+
+namespace {
+
+constexpr int64_t kAlign = 256;             // slot offset of every piece (the kernels' 16-B loads)
+constexpr int64_t kReadPiece = 16ll << 20;  // pread unit handed to one reader thread
+
+int64_t elem_bytes(int dtype) { return dtype == AWQ_DTYPE_F64 ? 8 : (dtype == AWQ_DTYPE_F32 ? 4 : 2); }
+int64_t align_up(int64_t v, int64_t a) { return (v + a - 1) / a * a; }
+double now_s() {
+    return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+bool aligned(const void* p, size_t a) { return ((uintptr_t)p % a) == 0; }
+
+struct Piece {
+    int item;
+    int64_t row0, nrows;
+    int64_t slot_off, bytes;
+};
+
+struct Batch {
+    int slot;
+    int64_t bytes;
+    std::vector<Piece> pieces;
+    int item_begin, item_end;   // the items whose last piece is in this batch
+};
+
+struct ReadJob {
+    int64_t batch;
+    int piece;
+    int64_t off, len;           // byte range inside the piece
+};
+
+struct Pipeline {
+    std::vector<awq_stream_item> items;
+    awq_stream_config cfg{};
+    int device = 0;
+    std::vector<Batch> batches;
+    std::vector<ReadJob> jobs;
+    std::vector<hipEvent_t> ev_h2d, ev_kern, ev_done;
+    std::mutex mu;
+    std::condition_variable cv;
+    std::vector<int64_t> reads_left;
+    int64_t h2d_recorded = -1, done_recorded = -1;
+    size_t next_job = 0;
+    int err = 0;
+    std::string err_msg;
+    std::vector<std::thread> readers;
+    std::thread submitter;
+    double t0 = 0, read_busy = 0, wait_read = 0, wait_slot = 0;
+    int64_t bytes_read = 0;
+
+    void fail(int code, const std::string& msg) {
+        std::lock_guard<std::mutex> g(mu);
+        if (!err) {
+            err = code;
+            err_msg = msg;
+        }
+        cv.notify_all();
+    }
+    bool hip_ok(hipError_t e, const char* what) {
+        if (e == hipSuccess) return true;
+        fail(AWQ_EHIP, std::string(what) + ": " + hipGetErrorString(e));
+        return false;
+    }
+};
+
+// ---- planning ---------------------------------------------------------------------------
+int plan(Pipeline& P, std::string& why) {
+    const int64_t slot = P.cfg.slot_bytes;
+    int64_t cap = P.cfg.first_batch_bytes > 0 ? std::min(P.cfg.first_batch_bytes, slot) : slot;
+    Batch cur{0, 0, {}, 0, 0};
+    auto close = [&](int item_end) {
+        cur.item_end = item_end;
+        P.batches.push_back(cur);
+        cur = Batch{(int)(P.batches.size() % (size_t)P.cfg.nslots), 0, {}, item_end, item_end};
+        cap = slot;
+    };
+    const int n = (int)P.items.size();
+    for (int i = 0; i < n; ++i) {
+        const awq_stream_item& it = P.items[i];
+        const int64_t rowbytes = it.K * elem_bytes(it.dtype);
+        int64_t r = 0;
+        while (r < it.rows && rowbytes > 0) {
+            const int64_t used = align_up(cur.bytes, kAlign);
+            const int64_t avail = cap - used;
+            const int64_t need = (it.rows - r) * rowbytes;
+            const bool room = (int64_t)cur.pieces.size() < AWQ_STREAM_MAX_BATCH_ITEMS;
+            int64_t take = 0;
+            if (room && need <= avail) {
+                take = it.rows - r;
+            } else if (room && avail >= rowbytes) {
+                take = avail / rowbytes;
+                if (take >= 8) take -= take % 8;   // row splits on multiples of 8: aligned output rows
+            }
+            if (take == 0) {
+                if (cur.pieces.empty()) {
+                    why = "a row of " + std::to_string(rowbytes) + " B does not fit a staging slot of " +
+                          std::to_string(slot) + " B";
+                    return AWQ_EINVAL;
+                }
+                close(i);
+                continue;
+            }
+            cur.pieces.push_back(Piece{i, r, take, used, take * rowbytes});
+            cur.bytes = used + take * rowbytes;
+            r += take;
+        }
+    }
+    if (!cur.pieces.empty() || P.batches.empty() || cur.item_begin < n) close(n);
+    // reads: every piece in kReadPiece units, batch by batch
+    P.reads_left.assign(P.batches.size(), 0);
+    for (size_t b = 0; b < P.batches.size(); ++b) {
+        const Batch& B = P.batches[b];
+        for (size_t k = 0; k < B.pieces.size(); ++k)
+            for (int64_t off = 0; off < B.pieces[k].bytes; off += kReadPiece) {
+                P.jobs.push_back(ReadJob{(int64_t)b, (int)k, off, std::min(kReadPiece, B.pieces[k].bytes - off)});
+                ++P.reads_left[b];
+            }
+    }
+    return AWQ_OK;
+}
+
+// ---- reader threads ---------------------------------------------------------------------
+void reader_main(Pipeline* P) {
+    (void)hipSetDevice(P->device);
+    const int64_t slot = P->cfg.slot_bytes;
+    for (;;) {
+        ReadJob j;
+        {
+            std::lock_guard<std::mutex> g(P->mu);
+            if (P->err || P->next_job >= P->jobs.size()) return;
+            j = P->jobs[P->next_job++];
+        }
+        const Batch& B = P->batches[j.batch];
+        const int64_t prev = j.batch - P->cfg.nslots;   // the batch that used this slot before
+        if (prev >= 0) {
+            {
+                std::unique_lock<std::mutex> lk(P->mu);
+                P->cv.wait(lk, [&] { return P->err || P->h2d_recorded >= prev; });
+                if (P->err) return;
+            }
+            if (!P->hip_ok(hipEventSynchronize(P->ev_h2d[prev]), "waiting for a staging slot")) return;
+        }
+        const Piece& pc = B.pieces[j.piece];
+        const awq_stream_item& it = P->items[pc.item];
+        char* dst = (char*)P->cfg.host_staging + (int64_t)B.slot * slot + pc.slot_off + j.off;
+        const int64_t src = it.offset + pc.row0 * it.K * elem_bytes(it.dtype) + j.off;
+        const double t = now_s();
+        int64_t done = 0;
+        while (done < j.len) {
+            const ssize_t got = pread(it.fd, dst + done, (size_t)(j.len - done), (off_t)(src + done));
+            if (got < 0 && errno == EINTR) continue;
+            if (got <= 0) {
+                P->fail(AWQ_EINVAL, "item " + std::to_string(pc.item) + ": read failed at byte " +
+                                        std::to_string(src + done) + (got < 0 ? std::string(": ") + strerror(errno)
+                                                                              : std::string(": end of file")));
+                return;
+            }
+            done += got;
+        }
+        std::lock_guard<std::mutex> g(P->mu);
+        P->read_busy += now_s() - t;
+        P->bytes_read += j.len;
+        if (--P->reads_left[j.batch] == 0) P->cv.notify_all();
+    }
+}
+
+// ---- submitter thread -------------------------------------------------------------------
+// outputs of rows [row0, row0 + nrows) of an item
+awq_tensor_desc piece_desc(const awq_stream_item& it, const Piece& pc, const void* w, int bits, int64_t gs) {
+    const int64_t per = 32 / bits;
+    const int64_t wpr = (it.K + per - 1) / per, G = (it.K + gs - 1) / gs, zpr = (G + per - 1) / per;
+    awq_tensor_desc d{};
+    d.w = w;
+    d.rows = pc.nrows;
+    d.K = it.K;
+    d.qweight = it.qweight ? it.qweight + pc.row0 * wpr : nullptr;
+    d.qzeros = it.qzeros ? it.qzeros + pc.row0 * zpr : nullptr;
+    d.scales = it.scales ? it.scales + pc.row0 * G : nullptr;
+    d.tensor_q = it.tensor_q ? it.tensor_q + pc.row0 * it.K : nullptr;
+    d.zeros = it.zeros ? it.zeros + pc.row0 * G : nullptr;
+    return d;
+}
+
+bool ragged_ok(const awq_tensor_desc& d, int dtype, int64_t gs) {
+    return (dtype == AWQ_DTYPE_BF16 || dtype == AWQ_DTYPE_F16 || dtype == AWQ_DTYPE_F32) &&
+           awq_ragged_eligible(dtype, d.rows, d.K, gs) && aligned(d.w, 16) && (!d.qweight || aligned(d.qweight, 8)) &&
+           (!d.tensor_q || aligned(d.tensor_q, 16)) && (!d.zeros || aligned(d.zeros, 4)) &&
+           (!d.qzeros || aligned(d.qzeros, 4)) && (!d.scales || aligned(d.scales, 2));
+}
+
+bool quantize_batch(Pipeline& P, const Batch& B, hipStream_t cs) {
+    const awq_stream_config& c = P.cfg;
+    const int64_t gs = c.group_size;
+    const char* dev_slot = (const char*)c.dev_staging + (int64_t)B.slot * c.slot_bytes;
+    const int64_t tb = awq_stream_table_bytes(c.slot_bytes);
+    char* htab = (char*)c.host_tables + (int64_t)B.slot * tb;
+    char* dtab = (char*)c.dev_tables + (int64_t)B.slot * tb;
+    awq_tensor_desc* descs = (awq_tensor_desc*)htab;   // [AWQ_STREAM_MAX_BATCH_ITEMS], grouped by dtype
+    const int64_t tables_at = align_up((int64_t)sizeof(awq_tensor_desc) * AWQ_STREAM_MAX_BATCH_ITEMS, kAlign);
+    struct Group {
+        int dtype, first, n;
+        int64_t tiles, table_off, table_len;
+        int flags;
+    };
+    std::vector<Group> groups;
+    std::vector<std::pair<awq_tensor_desc, int>> rest;   // (descriptor, dtype) of the per-tensor launches
+    int nd = 0;
+    int64_t toff = tables_at;
+    for (int dt : {AWQ_DTYPE_BF16, AWQ_DTYPE_F16, AWQ_DTYPE_F32, AWQ_DTYPE_F64}) {
+        const int first = nd;
+        for (const Piece& pc : B.pieces) {
+            const awq_stream_item& it = P.items[pc.item];
+            if (it.dtype != dt) continue;
+            const awq_tensor_desc d = piece_desc(it, pc, dev_slot + pc.slot_off, c.bits, gs);
+            if (ragged_ok(d, dt, gs)) descs[nd++] = d;
+            else rest.push_back({d, dt});
+        }
+        if (nd == first) continue;
+        Group g{dt, first, nd - first, 0, 0, 0, 0};
+        g.tiles = awq_plan_ragged(descs + first, g.n, c.bits, gs);
+        if (g.tiles < 0) {
+            P.fail(AWQ_EINVAL, std::string("awq_plan_ragged: ") + awq_last_error());
+            return false;
+        }
+        const int64_t need = awq_plan_block_tensor(descs + first, g.n, g.tiles, nullptr, 0);
+        g.table_off = toff;
+        g.table_len = need;
+        if (toff + need * 4 > tb) {
+            P.fail(AWQ_EINVAL, "stream tables overflow");
+            return false;
+        }
+        if (need > 0 && awq_plan_block_tensor(descs + first, g.n, g.tiles, (int32_t*)(htab + toff), need) < 0) {
+            P.fail(AWQ_EINVAL, std::string("awq_plan_block_tensor: ") + awq_last_error());
+            return false;
+        }
+        g.flags = awq_ragged_flags(descs + first, g.n, gs);
+        toff = align_up(toff + need * 4, 16);
+        groups.push_back(g);
+    }
+    if (!groups.empty()) {   // descriptors + tables in one copy, stream-ordered before the launches
+        if (!P.hip_ok(hipMemcpyAsync(dtab, htab, (size_t)(nd * (int64_t)sizeof(awq_tensor_desc)),
+                                     hipMemcpyHostToDevice, cs), "descriptor upload"))
+            return false;
+        if (!P.hip_ok(hipMemcpyAsync(dtab + tables_at, htab + tables_at, (size_t)(toff - tables_at),
+                                     hipMemcpyHostToDevice, cs), "table upload"))
+            return false;
+    }
+    for (const Group& g : groups) {
+        const int rc = awq_quantize_ragged((const awq_tensor_desc*)dtab + g.first, g.n, g.tiles,
+                                           g.table_len ? (const int32_t*)(dtab + g.table_off) : nullptr, g.dtype,
+                                           c.bits, c.symmetric, gs, g.flags, cs);
+        if (rc) {
+            P.fail(rc, std::string("awq_quantize_ragged: ") + awq_last_error());
+            return false;
+        }
+    }
+    for (const auto& r : rest) {
+        const awq_tensor_desc& d = r.first;
+        const int rc = awq_quantize_groups_ex(d.w, r.second, d.rows, d.K, (int32_t)gs, c.bits, c.symmetric, 0,
+                                              d.qweight, d.qzeros, d.scales, d.tensor_q, d.zeros, cs);
+        if (rc) {
+            P.fail(rc, std::string("awq_quantize_groups_ex: ") + awq_last_error());
+            return false;
+        }
+    }
+    return true;
+}
+
+void submitter_main(Pipeline* P) {
+    (void)hipSetDevice(P->device);
+    const awq_stream_config& c = P->cfg;
+    hipStream_t h2d = (hipStream_t)c.h2d_stream, cs = (hipStream_t)c.compute_stream, d2h = (hipStream_t)c.d2h_stream;
+    const int64_t nb = (int64_t)P->batches.size();
+    for (int64_t b = 0; b < nb; ++b) {
+        const Batch& B = P->batches[b];
+        double t = now_s();
+        {
+            std::unique_lock<std::mutex> lk(P->mu);
+            P->cv.wait(lk, [&] { return P->err || P->reads_left[b] == 0; });
+            if (P->err) return;
+        }
+        P->wait_read += now_s() - t;
+        if (b >= c.nslots) {   // the slot's previous batch: its kernels read the device slot and its tables
+            t = now_s();
+            if (!P->hip_ok(hipEventSynchronize(P->ev_kern[b - c.nslots]), "waiting for a slot's kernels")) return;
+            P->wait_slot += now_s() - t;
+        }
+        if (B.bytes > 0 &&
+            !P->hip_ok(hipMemcpyAsync((char*)c.dev_staging + (int64_t)B.slot * c.slot_bytes,
+                                      (const char*)c.host_staging + (int64_t)B.slot * c.slot_bytes, (size_t)B.bytes,
+                                      hipMemcpyHostToDevice, h2d), "H2D"))
+            return;
+        if (!P->hip_ok(hipEventRecord(P->ev_h2d[b], h2d), "event")) return;
+        {
+            std::lock_guard<std::mutex> g(P->mu);
+            P->h2d_recorded = b;
+        }
+        P->cv.notify_all();
+        if (!P->hip_ok(hipStreamWaitEvent(cs, P->ev_h2d[b], 0), "stream wait")) return;
+        if (!quantize_batch(*P, B, cs)) return;
+        if (!P->hip_ok(hipEventRecord(P->ev_kern[b], cs), "event")) return;
+        if (!P->hip_ok(hipStreamWaitEvent(d2h, P->ev_kern[b], 0), "stream wait")) return;
+        // outputs of the items this batch completes, adjacent ranges as one copy
+        char *hs = nullptr, *ds = nullptr;
+        int64_t len = 0;
+        auto flush = [&]() {
+            if (len > 0 && !P->hip_ok(hipMemcpyAsync(hs, ds, (size_t)len, hipMemcpyDeviceToHost, d2h), "D2H"))
+                return false;
+            len = 0;
+            return true;
+        };
+        for (int i = B.item_begin; i < B.item_end; ++i) {
+            const awq_stream_item& it = P->items[i];
+            if (!it.host_out || !it.dev_out || it.out_bytes <= 0) continue;
+            if (len > 0 && hs + len == (char*)it.host_out && ds + len == (char*)it.dev_out) {
+                len += it.out_bytes;
+                continue;
+            }
+            if (!flush()) return;
+            hs = (char*)it.host_out;
+            ds = (char*)it.dev_out;
+            len = it.out_bytes;
+        }
+        if (!flush()) return;
+        if (!P->hip_ok(hipEventRecord(P->ev_done[b], d2h), "event")) return;
+        {
+            std::lock_guard<std::mutex> g(P->mu);
+            P->done_recorded = b;
+        }
+        P->cv.notify_all();
+    }
+}
+
+}  // namespace
+
+namespace awq {
+int set_error(int code, const char* msg);   // awq_capi.hip
+}
+
+extern "C" {
+
+int64_t awq_stream_table_bytes(int64_t slot_bytes) {
+    const int64_t descs = align_up((int64_t)sizeof(awq_tensor_desc) * AWQ_STREAM_MAX_BATCH_ITEMS, kAlign);
+    // tensor tables: one int32 per AWQ_BLOCK_TILES tiles of >= 4 KiB of input, per dtype group
+    const int64_t tables = 4 * (slot_bytes / 4096 / AWQ_BLOCK_TILES + 4 * 4) + 4 * 16;
+    return align_up(descs + tables, 4096);
+}
+
+int awq_stream_start(const awq_stream_item* items, int n, const awq_stream_config* cfg, void** handle) {
+    if (!handle || !cfg || n < 0 || (n > 0 && !items)) return awq::set_error(AWQ_EINVAL, "null argument");
+    *handle = nullptr;
+    const awq_stream_config& c = *cfg;
+    if (c.bits != 4 && c.bits != 8) return awq::set_error(AWQ_EINVAL, "Unsupported bit width. Supported: 4, 8.");
+    if (c.group_size <= 0) return awq::set_error(AWQ_EINVAL, "Group size must be a positive integer");
+    if (c.nslots < 2 || c.readers < 1 || c.slot_bytes <= 0 || c.slot_bytes % 4096 || !c.host_staging ||
+        !c.dev_staging || !c.host_tables || !c.dev_tables)
+        return awq::set_error(AWQ_EINVAL, "bad stream configuration (nslots >= 2, readers >= 1, slot_bytes a "
+                                          "multiple of 4096, staging and table buffers)");
+    for (int i = 0; i < n; ++i) {
+        const awq_stream_item& it = items[i];
+        if (it.dtype < AWQ_DTYPE_BF16 || it.dtype > AWQ_DTYPE_F64 || it.rows < 0 || it.K < 0 || it.fd < 0 ||
+            it.offset < 0)
+            return awq::set_error(AWQ_EINVAL, ("item " + std::to_string(i) + ": bad dtype, shape, fd or offset").c_str());
+        if (!it.qweight && !it.qzeros && !it.scales && !it.tensor_q && !it.zeros)
+            return awq::set_error(AWQ_EINVAL, "an item requests no output");
+    }
+    Pipeline* P = new Pipeline();
+    P->items.assign(items, items + n);
+    P->cfg = c;
+    (void)hipGetDevice(&P->device);
+    std::string why;
+    if (int rc = plan(*P, why)) {
+        delete P;
+        return awq::set_error(rc, why.c_str());
+    }
+    const size_t nb = P->batches.size();
+    P->ev_h2d.resize(nb);
+    P->ev_kern.resize(nb);
+    P->ev_done.resize(nb);
+    for (size_t b = 0; b < nb; ++b)
+        for (hipEvent_t* e : {&P->ev_h2d[b], &P->ev_kern[b], &P->ev_done[b]})
+            if (hipEventCreateWithFlags(e, hipEventDisableTiming) != hipSuccess) {
+                delete P;   // (events created so far are reclaimed with the context)
+                return awq::set_error(AWQ_EHIP, "hipEventCreate failed");
+            }
+    P->t0 = now_s();
+    const int nr = std::max(1, std::min(c.readers, (int)std::max<size_t>(1, P->jobs.size())));
+    for (int r = 0; r < nr; ++r) P->readers.emplace_back(reader_main, P);
+    P->submitter = std::thread(submitter_main, P);
+    *handle = P;
+    return AWQ_OK;
+}
+
+int64_t awq_stream_batches(void* handle) {
+    return handle ? (int64_t)((Pipeline*)handle)->batches.size() : -1;
+}
+
+int awq_stream_wait(void* handle, int64_t batch, int32_t* first_item, int32_t* end_item) {
+    Pipeline* P = (Pipeline*)handle;
+    if (!P || batch < 0 || batch >= (int64_t)P->batches.size()) return awq::set_error(AWQ_EINVAL, "bad batch");
+    {
+        std::unique_lock<std::mutex> lk(P->mu);
+        P->cv.wait(lk, [&] { return P->err || P->done_recorded >= batch; });
+        if (P->err) return awq::set_error(P->err, P->err_msg.c_str());
+    }
+    const hipError_t e = hipEventSynchronize(P->ev_done[batch]);
+    if (e != hipSuccess) return awq::set_error(AWQ_EHIP, hipGetErrorString(e));
+    if (first_item) *first_item = P->batches[batch].item_begin;
+    if (end_item) *end_item = P->batches[batch].item_end;
+    return AWQ_OK;
+}
+
+int awq_stream_end(void* handle, awq_stream_stats* stats) {
+    Pipeline* P = (Pipeline*)handle;
+    if (!P) return awq::set_error(AWQ_EINVAL, "null handle");
+    if (P->submitter.joinable()) P->submitter.join();
+    {   // a failed submitter leaves readers waiting for slots: release them
+        std::lock_guard<std::mutex> g(P->mu);
+        if (P->done_recorded + 1 < (int64_t)P->batches.size() && !P->err) {
+            P->err = AWQ_EHIP;
+            P->err_msg = "stream pipeline stopped early";
+        }
+        P->cv.notify_all();
+    }
+    for (auto& t : P->readers) t.join();
+    int rc = P->err;
+    std::string msg = P->err_msg;
+    if (!rc && !P->batches.empty()) {
+        const hipError_t e = hipEventSynchronize(P->ev_done.back());
+        if (e != hipSuccess) {
+            rc = AWQ_EHIP;
+            msg = hipGetErrorString(e);
+        }
+    }
+    if (stats) {
+        stats->batches = (int64_t)P->batches.size();
+        int64_t pieces = 0;
+        for (const Batch& b : P->batches) pieces += (int64_t)b.pieces.size();
+        stats->pieces = pieces;
+        stats->bytes_read = P->bytes_read;
+        stats->wall_s = now_s() - P->t0;
+        stats->read_busy_s = P->read_busy;
+        stats->wait_read_s = P->wait_read;
+        stats->wait_slot_s = P->wait_slot;
+    }
+    // nothing of the pipeline may still run once the caller's buffers are released
+    for (void* s : {P->cfg.h2d_stream, P->cfg.compute_stream, P->cfg.d2h_stream}) (void)hipStreamSynchronize((hipStream_t)s);
+    for (size_t b = 0; b < P->batches.size(); ++b) {
+        (void)hipEventDestroy(P->ev_h2d[b]);
+        (void)hipEventDestroy(P->ev_kern[b]);
+        (void)hipEventDestroy(P->ev_done[b]);
+    }
+    delete P;
+    if (rc) return awq::set_error(rc, msg.c_str());
+    return AWQ_OK;
+}
+
+}  // extern "C"

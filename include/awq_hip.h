@@ -223,6 +223,80 @@ int awq_dequantize_packed(const int32_t* qweight, const int32_t* qzeros, const u
 int awq_pack_rows(const int32_t* v, int64_t rows, int64_t n, int bits, int qmin, int32_t* packed,
                   void* stream);
 
+/* ---- Host streaming pipeline ----------------------------------
+ * Replaces the CLI's read -> quantize -> collect loop (reference main.py:216-392, which
+ * loads every file whole and then quantizes tensor by tensor): tensors are pread from their
+ * safetensors files straight into pinned staging slots by native reader threads, copied to
+ * HBM on an H2D stream, quantized on the compute stream by one ragged launch per dtype and
+ * batch (awq_quantize_ragged; shapes it does not take: awq_quantize_groups_ex per tensor),
+ * and their outputs copied back on a D2H stream — read, H2D, kernels and D2H of neighbouring
+ * batches overlap, with no per-tensor work in the host language.  A 2-D tensor larger than
+ * what is left of a slot is split by rows (rows quantize independently, awq.py:332-368), so
+ * slots stay small (pipeline fill) whatever the largest tensor.
+ *
+ * Caller-owned memory (the library allocates none): staging slots (pinned host + device),
+ * per-slot descriptor tables (pinned host + device, awq_stream_table_bytes each), every
+ * item's device outputs and, when its results are wanted on the host, a pinned host range
+ * of the same size.  The three streams may be any hipStream_t (NULL = legacy default). */
+#define AWQ_STREAM_MAX_BATCH_ITEMS 4096
+
+typedef struct awq_stream_item {
+    int32_t fd;          /* readable file descriptor (pread) */
+    int32_t dtype;       /* AWQ_DTYPE_* of the stored tensor */
+    int64_t offset;      /* byte offset of the tensor's data in the file */
+    int64_t rows, K;     /* awq.py:306-320: rows = dim 0 (1 for a 1-D tensor), K = the rest */
+    int32_t* qweight;    /* device outputs (any may be NULL), as awq_quantize_groups */
+    int32_t* qzeros;
+    uint16_t* scales;
+    int32_t* tensor_q;
+    int32_t* zeros;
+    void* dev_out;       /* D2H of [dev_out, dev_out + out_bytes) (the item's outputs, laid out */
+    void* host_out;      /* by the caller inside that range) into pinned host_out; NULL: none */
+    int64_t out_bytes;
+} awq_stream_item;
+
+typedef struct awq_stream_config {
+    int32_t bits, symmetric, group_size, readers;   /* readers: pread threads (>= 1) */
+    int32_t nslots, reserved;                       /* nslots >= 2 */
+    int64_t slot_bytes;          /* input bytes per staging slot, multiple of 4096 */
+    int64_t first_batch_bytes;   /* capacity of the first batch (<= slot_bytes; 0 = slot_bytes) */
+    void* host_staging;          /* pinned host, nslots * slot_bytes */
+    void* dev_staging;           /* device, nslots * slot_bytes */
+    void* host_tables;           /* pinned host, nslots * awq_stream_table_bytes(slot_bytes) */
+    void* dev_tables;            /* device, the same size */
+    void* compute_stream;
+    void* h2d_stream;
+    void* d2h_stream;
+} awq_stream_config;
+
+typedef struct awq_stream_stats {
+    int64_t batches, pieces, bytes_read;
+    double wall_s;               /* start -> last batch's outputs ready */
+    double read_busy_s;          /* summed over reader threads */
+    double wait_read_s;          /* submitter waiting for a batch's reads */
+    double wait_slot_s;          /* submitter waiting for a slot's previous kernels */
+} awq_stream_stats;
+
+/* Per-slot descriptor-table bytes (descriptors + tensor tables of up to
+ * AWQ_STREAM_MAX_BATCH_ITEMS pieces). */
+int64_t awq_stream_table_bytes(int64_t slot_bytes);
+
+/* Plan the batches and start the pipeline on its own native threads; returns at once.
+ * *handle receives the pipeline (awq_stream_end frees it).  Items are processed in order. */
+int awq_stream_start(const awq_stream_item* items, int n, const awq_stream_config* cfg, void** handle);
+
+/* Number of batches of a started pipeline. */
+int64_t awq_stream_batches(void* handle);
+
+/* Block until batch b's outputs are ready (on the host for items with host_out, on the
+ * device otherwise); [*first_item, *end_item) = the items whose last piece is in batch b.
+ * Returns the pipeline's first error (its message in awq_last_error), if any. */
+int awq_stream_wait(void* handle, int64_t batch, int32_t* first_item, int32_t* end_item);
+
+/* Wait for the whole pipeline, join its threads, release the handle; stats may be NULL.
+ * Returns the first error of the pipeline. */
+int awq_stream_end(void* handle, awq_stream_stats* stats);
+
 /* ---- Activation-aware per-input-channel scale search (scale_method="awq") ----------
  * Not in the reference (it stores scale_method, awq.py:66, and collects no activations;
  * parity unpinned).  AutoAWQ's published search (third-party,

@@ -91,6 +91,7 @@ def main():
     ap.add_argument("--evict", action="store_true", help="run 0 of the first format reads from disk")
     ap.add_argument("--cprofile", default=None, help="cProfile the last run's pipeline thread to this file")
     ap.add_argument("--extra", default="", help="extra CLI flags")
+    ap.add_argument("--engines", default="native", help="--stream_engine values to run, e.g. native,python")
     args = ap.parse_args()
     from awq_quantizer import main as cli_mod
     work = args.workdir or tempfile.mkdtemp(prefix="awq_cli_")
@@ -101,22 +102,22 @@ def main():
     print(json.dumps({"workload": args.workload, "files": args.shards, "input_GB": round(nbytes / 1e9, 3),
                       "build_s": round(time.time() - t0, 1)}), flush=True)
     first = True
-    for fmt in args.formats.split(","):
+    for fmt, eng in [(f, e) for f in args.formats.split(",") for e in args.engines.split(",")]:
         for r in range(args.runs):
             if first and args.evict:
                 evict(model)
             out = os.path.join(work, f"out_{fmt}_{r}")
             cli_mod.TIMINGS.clear()
             if args.cprofile and r == args.runs - 1:
-                os.environ["AWQ_CLI_PROFILE"] = args.cprofile + f".{fmt}"
+                os.environ["AWQ_CLI_PROFILE"] = args.cprofile + f".{fmt}.{eng}"
             t0 = time.perf_counter()
             rc = cli_mod.main(["--model_id", model, "--output_dir", out, "--log_level", "WARNING",
-                               "--output_format", fmt] + args.extra.split())
+                               "--output_format", fmt, "--stream_engine", eng] + args.extra.split())
             wall = time.perf_counter() - t0
             os.environ.pop("AWQ_CLI_PROFILE", None)
             assert rc == 0
             ob = sum(os.path.getsize(os.path.join(out, f)) for f in os.listdir(out))
-            print(json.dumps({"workload": args.workload, "format": fmt, "run": r,
+            print(json.dumps({"workload": args.workload, "format": fmt, "engine": eng, "run": r,
                               "kind": ("process-first" + (", page cache evicted" if args.evict else "")) if first
                               else "warm", "input_GB": round(nbytes / 1e9, 3), "output_GB": round(ob / 1e9, 3),
                               "wall_s": round(wall, 4), "input_GBs": round(nbytes / wall / 1e9, 3),
@@ -126,10 +127,10 @@ def main():
     print(json.dumps({"ceilings": probes(model, 16)}), flush=True)
     if args.cprofile:
         import pstats
-        for fmt in args.formats.split(","):
-            p = args.cprofile + f".{fmt}"
+        for fmt, eng in [(f, e) for f in args.formats.split(",") for e in args.engines.split(",")]:
+            p = args.cprofile + f".{fmt}.{eng}"
             if os.path.exists(p):
-                print(f"--- cProfile {fmt} (pipeline thread, last run) ---")
+                print(f"--- cProfile {fmt} {eng} (pipeline thread, last run) ---")
                 pstats.Stats(p).sort_stats("cumulative").print_stats(30)
                 pstats.Stats(p).sort_stats("tottime").print_stats(25)
     if args.workdir is None:

@@ -10,7 +10,7 @@ import sys
 
 import pytest
 import torch
-from safetensors.torch import save_file
+from safetensors.torch import load_file, save_file
 
 
 def test_defaults_match_reference_cli():
@@ -183,23 +183,34 @@ def test_main_missing_model_returns_1(tmp_path):
                  "--log_level", "CRITICAL"]) == 1
 
 
+def _load_chunk(out, ci, st):
+    if st:
+        flat = load_file(str(out / f"model_chunk_{ci:04d}.safetensors"))
+        res = {}
+        for k, v in flat.items():
+            name, field = k.rsplit(".", 1)
+            res.setdefault(name, {})[field] = v
+        return res
+    return torch.load(str(out / f"model_chunk_{ci:04d}.pt"), weights_only=True)
+
+
 @pytest.mark.gpu
 @pytest.mark.skipif(not torch.cuda.is_available(), reason="needs the GPU")
 @pytest.mark.parametrize("fmt", ["reference", "packed"])
-def test_main_end_to_end_gpu(tmp_path, fmt):
+@pytest.mark.parametrize("engine,st", [("native", False), ("native", True), ("python", False)])
+def test_main_end_to_end_gpu(tmp_path, fmt, engine, st):
     from oracle import awq_oracle as orc
     from awq_quantizer.main import main
     tensors = _tensors()
     d = _model_dir(tmp_path, tensors, files=2)
     out = tmp_path / "out"
     rc = main(["--model_id", d, "--output_dir", str(out), "--log_level", "ERROR", "--chunk_size", "3",
-               "--output_format", fmt])
+               "--output_format", fmt, "--stream_engine", engine] + (["--save_safetensors"] if st else []))
     assert rc == 0
     meta = json.load(open(out / "metadata.json"))
     assert meta["num_tensors"] == 6
     for name, chunk_idx in meta["tensor_to_chunk"].items():
-        chunk = torch.load(str(out / f"model_chunk_{chunk_idx:04d}.pt"), weights_only=True)
-        res = chunk[name]
+        res = _load_chunk(out, chunk_idx, st)[name]
         ref = orc.quantize(tensors[name], bits=4, group_size=128, symmetric=False, per_channel=False)
         if fmt == "reference":
             assert torch.equal(res["tensor_q"], ref["tensor_q"]), name
@@ -455,3 +466,84 @@ def test_main_act_stats_gpu(tmp_path, fmt):
     other = torch.load(str(out / f"model_chunk_{meta['tensor_to_chunk']['model.embed.weight']:04d}.pt"),
                        weights_only=True)["model.embed.weight"]
     assert "input_scale" not in other
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not torch.cuda.is_available(), reason="needs the GPU")
+@pytest.mark.parametrize("packed", [True, False])
+def test_native_stream_small_slots_split_rows(tmp_path, packed):
+    """The native pipeline (include/awq_hip.h awq_stream_*) with 64 KiB staging slots: large
+    tensors split by rows over many batches, slots reused many times, one-tensor and
+    many-tensor batches, fp16 / fp32 / fp64 / bf16 items (ragged and per-tensor launches),
+    padded rows (K % 128 != 0) and a K % 8 != 0 tensor — every result equals the oracle's."""
+    import threading
+    from oracle import awq_oracle as orc
+    from awq_quantizer.main import quantize_stream_native
+    from awq_quantizer.model_loading import load_model_from_path
+    from awq_quantizer.quantization import AWQQuantizer
+    g = torch.Generator().manual_seed(7)
+    r = lambda *s, dt=torch.bfloat16: (torch.randn(*s, generator=g) * 0.02).to(dt)
+    tensors = {"big": r(700, 512), "f16": r(96, 384, dt=torch.float16), "f32": r(40, 256, dt=torch.float32),
+               "f64": r(33, 256, dt=torch.float64), "padded": r(50, 200), "odd": r(13, 203), "vec": r(4096),
+               "t3": r(24, 3, 128)}
+    for i in range(40):
+        tensors[f"tiny{i}"] = r(128)
+    d = _model_dir(tmp_path, tensors, files=3)
+    loader = load_model_from_path(d, logger_level="ERROR")
+    infos = loader.tensor_index()
+    q = AWQQuantizer(bits=4, group_size=128, symmetric=False, device="cuda", logger_level="ERROR")
+    out, done = {}, []
+    chunk_of = {i.name: k // 5 for k, i in enumerate(infos)}
+    quantize_stream_native(loader, infos, q, "cuda:0", 4, packed, out, threading.Lock(), None,
+                           on_done=lambda n, res: done.append(n), chunk_of=chunk_of, slot_bytes=64 << 10)
+    assert sorted(done) == sorted(tensors) == sorted(out)
+    for name, x in tensors.items():
+        ref = orc.quantize(x, bits=4, group_size=128, symmetric=False)
+        res = out[name]
+        rows = 1 if x.dim() <= 1 else x.shape[0]
+        if packed:
+            assert torch.equal(res["qweight"], orc.pack_rows(ref["tensor_q"].reshape(rows, -1), 4, 0)), name
+            assert torch.equal(res["qzeros"], orc.pack_rows(ref["zero_points"], 4, 0)), name
+            assert list(res["shape"]) == list(x.shape)
+        else:
+            assert torch.equal(res["tensor_q"], ref["tensor_q"]), name
+            assert torch.equal(res["zero_points"], ref["zero_points"]), name
+        assert torch.equal(res["scales"].view(torch.int16), ref["scales"].view(torch.int16)), name
+    st = __import__("awq_quantizer.main", fromlist=["TIMINGS"]).TIMINGS["stream_cuda:0"]
+    assert st["engine"] == "native" and st["batches"] > 10 and st["pieces"] > st["batches"]
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not torch.cuda.is_available(), reason="needs the GPU")
+@pytest.mark.parametrize("fmt", ["packed", "reference"])
+def test_cli_llama3_8b_shaped_multifile(tmp_path, fmt):
+    """BASELINE config 4's tensor set (Llama-3-8B: 291 tensors, every shape) with rows cut to
+    1/32 (K and the group structure kept), 4 safetensors files, through the CLI's native
+    pipeline: every tensor equals the oracle."""
+    import bench
+    from oracle import awq_oracle as orc
+    from awq_quantizer.main import main
+    g = torch.Generator().manual_seed(8)
+    tensors = {}
+    for i, shape in enumerate(bench.shapes_of("llama3-8b")):
+        shp = (max(1, shape[0] // 32),) + tuple(shape[1:]) if len(shape) == 2 else shape
+        tensors[f"model.layers.{i // 9}.t{i}.weight"] = (torch.randn(*shp, generator=g) * 0.02).to(torch.bfloat16)
+    d = _model_dir(tmp_path, tensors, files=4)
+    out = tmp_path / "out"
+    assert main(["--model_id", d, "--output_dir", str(out), "--log_level", "ERROR", "--output_format", fmt]) == 0
+    meta = json.load(open(out / "metadata.json"))
+    assert meta["num_tensors"] == len(tensors) == 291
+    cache = {}
+    for name, ci in meta["tensor_to_chunk"].items():
+        if ci not in cache:
+            cache = {ci: torch.load(str(out / f"model_chunk_{ci:04d}.pt"), weights_only=True)}
+        res = cache[ci][name]
+        x = tensors[name]
+        ref = orc.quantize(x, bits=4, group_size=128, symmetric=False)
+        if fmt == "packed":
+            rows = 1 if x.dim() <= 1 else x.shape[0]
+            assert torch.equal(res["qweight"], orc.pack_rows(ref["tensor_q"].reshape(rows, -1), 4, 0)), name
+        else:
+            assert torch.equal(res["tensor_q"], ref["tensor_q"]), name
+            assert torch.equal(res["zero_points"], ref["zero_points"]), name
+        assert torch.equal(res["scales"].view(torch.int16), ref["scales"].view(torch.int16)), name

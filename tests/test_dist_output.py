@@ -53,7 +53,7 @@ def fake_result(name, fmt, shape=(3, 16)):
 def _fake_stream(fmt, fail_rank, rank):
     def quantize_stream(loader, infos, quantizer, device, readers, lookahead, packed, out, lock, logger,
                         memory_efficient=False, keep_on_device=False, batch_bytes=0, export_autoawq=False,
-                        act_stats=None, on_done=None):
+                        act_stats=None, on_done=None, **_):
         for k, info in enumerate(infos):
             if rank == fail_rank and k == 1:
                 raise RuntimeError("device lost (injected)")

@@ -86,10 +86,10 @@ def test_stub_matches_reference_nan_cases(stub, case):
 
 def test_stub_fp32_scale_values_are_the_dtype_values(stub):
     """The stub's fp32 scales are the input dtype's own scale values (awq.py:352), not their
-    fp16 rounding: bf16 weights keep bf16-valued scales."""
+    fp16 rounding: fp32 weights keep fp32-valued scales (24-bit significands)."""
     from oracle import awq_oracle as orc
     g = torch.Generator().manual_seed(3)
-    x = (torch.randn(64, 512, generator=g) * 0.02).to(torch.bfloat16)
+    x = torch.randn(64, 512, generator=g) * 0.02
     q = _q(dict(bits=4, group_size=128, symmetric=False))
     _, s, _ = stub.quantize_per_group(q, x)
     want, _ = orc.group_params(x, 64, 512, 128, 4, False)

@@ -40,7 +40,7 @@ class StreamItem(ctypes.Structure):
     """Mirror of awq_stream_item (include/awq_hip.h)."""
     _fields_ = [("fd", _I32), ("dtype", _I32), ("offset", _I64), ("rows", _I64), ("K", _I64), ("qweight", _P),
                 ("qzeros", _P), ("scales", _P), ("tensor_q", _P), ("zeros", _P), ("dev_out", _P), ("host_out", _P),
-                ("out_bytes", _I64)]
+                ("out_bytes", _I64), ("dev_out2", _P), ("host_out2", _P), ("out_bytes2", _I64)]
 
 
 class StreamConfig(ctypes.Structure):
@@ -57,7 +57,7 @@ class StreamStats(ctypes.Structure):
                 ("read_busy_s", ctypes.c_double), ("wait_read_s", ctypes.c_double), ("wait_slot_s", ctypes.c_double)]
 
 
-assert ctypes.sizeof(StreamItem) == 96 and ctypes.sizeof(StreamConfig) == 96
+assert ctypes.sizeof(StreamItem) == 120 and ctypes.sizeof(StreamConfig) == 96
 
 
 class Tuning(ctypes.Structure):

@@ -541,34 +541,44 @@ def quantize_stream_native(loader, infos: List[TensorInfo], quantizer: AWQQuanti
             continue
         rows = 1 if len(info.shape) <= 1 else info.shape[0]
         items.append((info, rows, info.numel // rows))
-    # output layout: every tensor's fields back to back (16-B aligned) in one device arena, and
-    # per output chunk one pinned host buffer (same relative layout: adjacent D2H ranges merge)
-    lay, dev_total, seg_of, seg_size = [], 0, [], {}
+    # output layout: per dtype (int32 words / fp16 scales) every tensor's fields back to back
+    # (16-B aligned) in one device arena, and per output chunk one pinned host buffer of that
+    # dtype (torch.save stores a storage once per file, but only under one dtype) with the
+    # same relative layout, so adjacent D2H ranges merge
+    kinds = (torch.int32, torch.float16)
+    lay, dev_total = [], {dt: 0 for dt in kinds}
+    seg_size = {}
     for info, rows, K in items:
-        fields, off = [], 0
-        for f, shp, dt in _out_fields(info, rows, K, gs, bits, packed):
-            nb = int(torch.Size(shp).numel()) * torch.empty((), dtype=dt).element_size()
-            fields.append((f, shp, dt, off, nb))
-            off += -(-nb // 16) * 16
         seg = chunk_of.get(info.name, 0) if chunk_of else len(lay) // 16
-        lay.append((fields, off, dev_total, seg, seg_size.get(seg, 0)))
-        seg_size[seg] = seg_size.get(seg, 0) + off
-        dev_total += off
-    arena = torch.empty(max(dev_total, 16), dtype=torch.uint8, device=dev)
-    hosts = {} if keep_on_device else {s: torch.empty(max(n, 16), dtype=torch.uint8, pin_memory=True)
+        fields, size = [], {dt: 0 for dt in kinds}
+        for f, shp, dt in _out_fields(info, rows, K, gs, bits, packed):
+            n = int(torch.Size(shp).numel())
+            fields.append((f, shp, dt, size[dt], n))
+            size[dt] += -(-n * torch.empty((), dtype=dt).element_size() // 16) * 16 // torch.empty(
+                (), dtype=dt).element_size()
+        ss = seg_size.setdefault(seg, {dt: 0 for dt in kinds})
+        lay.append((fields, size, dict(dev_total), seg, dict(ss)))
+        for dt in kinds:
+            ss[dt] += size[dt]
+            dev_total[dt] += size[dt]
+    arena = {dt: torch.empty(max(dev_total[dt], 8), dtype=dt, device=dev) for dt in kinds}
+    hosts = {} if keep_on_device else {s: {dt: torch.empty(max(n[dt], 8), dtype=dt, pin_memory=True) for dt in kinds}
                                        for s, n in seg_size.items()}
     lib = _hip.load_library()
     arr = (_hip.StreamItem * max(1, len(items)))()
-    base = arena.data_ptr()
-    for k, ((info, rows, K), (fields, nbytes, doff, seg, hoff)) in enumerate(zip(items, lay)):
+    for k, ((info, rows, K), (fields, size, doff, seg, hoff)) in enumerate(zip(items, lay)):
         fd, at = loader.data_location(info)
         it = arr[k]
         it.fd, it.dtype, it.offset = fd, _hip.AWQ_DTYPE[info.dtype], at
         it.rows, it.K = rows, K
-        for f, _, _, off, _ in fields:
-            setattr(it, _STREAM_PTR_FIELD[f], base + doff + off)
-        it.dev_out, it.out_bytes = base + doff, nbytes
-        it.host_out = None if keep_on_device else hosts[seg].data_ptr() + hoff
+        for f, _, dt, off, _ in fields:
+            setattr(it, _STREAM_PTR_FIELD[f], arena[dt].data_ptr() + (doff[dt] + off) * arena[dt].element_size())
+        for dt, (dvf, hf, nf) in zip(kinds, (("dev_out", "host_out", "out_bytes"),
+                                            ("dev_out2", "host_out2", "out_bytes2"))):
+            es = arena[dt].element_size()
+            setattr(it, dvf, arena[dt].data_ptr() + doff[dt] * es)
+            setattr(it, nf, size[dt] * es)
+            setattr(it, hf, None if keep_on_device else hosts[seg][dt].data_ptr() + hoff[dt] * es)
     total_in = sum(i.nbytes for i, _, _ in items)
     slot = slot_bytes or min(256 << 20, max(32 << 20, total_in // 8))
     slot = -(-slot // 4096) * 4096
@@ -597,9 +607,9 @@ def quantize_stream_native(loader, infos: List[TensorInfo], quantizer: AWQQuanti
         scal = {"bits": torch.tensor(bits, dtype=torch.int32), "group_size": torch.tensor(gs, dtype=torch.int32),
                 "symmetric": torch.tensor(bool(quantizer.symmetric), dtype=torch.bool)}
         results = []
-        for (info, rows, K), (fields, nbytes, doff, seg, hoff) in zip(items, lay):
+        for (info, rows, K), (fields, size, doff, seg, hoff) in zip(items, lay):
             src, at = (arena, doff) if keep_on_device else (hosts[seg], hoff)
-            r = {f: src[at + off:at + off + nb].view(dt).view(shp) for f, shp, dt, off, nb in fields}
+            r = {f: src[dt][at[dt] + off:at[dt] + off + n].view(shp) for f, shp, dt, off, n in fields}
             r.update(scal)
             if packed:
                 r["shape"] = torch.tensor(list(info.shape), dtype=torch.int64)

@@ -258,17 +258,26 @@ int64_t awq_plan_ragged(awq_tensor_desc* descs, int n, int bits, int64_t group_s
 int64_t awq_plan_block_tensor(const awq_tensor_desc* descs, int n, int64_t total_tiles, int32_t* block_tensor,
                               int64_t len) {
     g_err.clear();
-    const int64_t need = (total_tiles + awq::kTableTiles - 1) / awq::kTableTiles;
+    const int64_t entries = (total_tiles + awq::kTableTiles - 1) / awq::kTableTiles;
+    const int64_t need = entries * awq::kTableEntryInts;   // int32 units
     if (!block_tensor && len == 0) return need;   // size query
-    if (!block_tensor || len < need) return fail(AWQ_EINVAL, "block table needs %lld entries", (long long)need), -1;
+    if (!block_tensor || len < need) return fail(AWQ_EINVAL, "block table needs %lld int32", (long long)need), -1;
+    if ((uintptr_t)block_tensor % 16) return fail(AWQ_EINVAL, "block table must be 16-B aligned"), -1;
     if (n <= 0 || !descs) return fail(AWQ_EINVAL, "bad descriptor array"), -1;
+    awq::TableEntry* tab = (awq::TableEntry*)block_tensor;
     int cur = 0;
-    for (int64_t b = 0; b < need; ++b) {
+    for (int64_t b = 0; b < entries; ++b) {
         const int64_t t = b * awq::kTableTiles;
         while (cur + 1 < n && descs[cur + 1].tile_begin <= t) ++cur;
         const int64_t last = std::min(t + awq::kTableTiles, total_tiles) - 1;
         const bool spans = cur + 1 < n && descs[cur + 1].tile_begin <= last;
-        block_tensor[b] = (int32_t)((uint32_t)cur | (spans ? 0x80000000u : 0u));
+        awq::TableEntry e{};
+        e.w = descs[cur].w;
+        e.tile_begin = descs[cur].tile_begin;
+        e.rows = descs[cur].rows;
+        e.K = descs[cur].K;
+        e.tensor = (int32_t)((uint32_t)cur | (spans ? 0x80000000u : 0u));
+        tab[b] = e;
     }
     return need;
 }

@@ -1410,32 +1410,63 @@ void awq_fast_kernel(
 #endif
     int cur = 0;
     awq_tensor_desc d = single;
+    // the current tensor's input, first tile and shape: what the loads need (from the
+    // table entry on a wave's first tile, else from the descriptor)
+    const void* src_w = single.w;
+    int64_t src_tb = single.tile_begin, src_rows = single.rows, src_K = single.K;
+    bool need_d = false;   // d not loaded yet (fast table path): fetched after the loads went out
     if (descs != nullptr) {
+        bool fast = false;
         if (block_tensor != nullptr) {
-            // host-planned tensor of the block's first tile (awq_plan_block_tensor): one
-            // scalar load; blocks spanning tensors (small tensors) take a few more steps
-            const int32_t e = __builtin_amdgcn_readfirstlane(block_tensor[wave / kTableTiles]);
+            // host-planned entry of the wave's tile group (awq_plan_block_tensor): ONE 64-B
+            // scalar load gives the tensor's input and shape; entries whose tiles span
+            // tensors (small tensors) step through the descriptors
+            const TableEntry* te = (const TableEntry*)block_tensor + wave / kTableTiles;
+            const int32_t e = __builtin_amdgcn_readfirstlane(te->tensor);
             cur = e & 0x7FFFFFFF;
-            if (e < 0)   // the entry's tiles span tensors (bit 31): step to this wave's one
+            if (e >= 0) {
+                fast = true;
+                src_w = te->w;
+                src_tb = te->tile_begin;
+                src_rows = te->rows;
+                src_K = te->K;
+                need_d = true;
+            } else {
                 while (cur + 1 < n && descs[cur + 1].tile_begin <= wave) ++cur;
+            }
         } else {
             cur = find_tensor(descs, n, 0, wave);
         }
-        d = descs[cur];
+        if (!fast) {
+            d = descs[cur];
+            src_w = d.w;
+            src_tb = d.tile_begin;
+            src_rows = d.rows;
+            src_K = d.K;
+        }
     }
     for (int64_t t = wave; t < total_tiles; t += nwaves) {
-        if (descs != nullptr && cur + 1 < n && descs[cur + 1].tile_begin <= t) {
+        if (descs != nullptr && t != wave && cur + 1 < n && descs[cur + 1].tile_begin <= t) {
             cur = find_tensor(descs, n, cur + 1, t);
             d = descs[cur];
+            need_d = false;
+            src_w = d.w;
+            src_tb = d.tile_begin;
+            src_rows = d.rows;
+            src_K = d.K;
         }
         // the input range first (no division for byte tiles): the loads go out before the
         // rest of the tile context (row / group divisions) is computed
-        const uint32_t tile = (uint32_t)(t - d.tile_begin);
+        const uint32_t tile = (uint32_t)(t - src_tb);
         uint64_t el_off;
         uint32_t valid;
-        tile_src<BITS, GS, PAD>(d.rows, d.K, tile, el_off, valid);
+        tile_src<BITS, GS, PAD>(src_rows, src_K, tile, el_off, valid);
         Chunk<F::NW> va[4];
-        load_tile<F, GS>((const char*)d.w + el_off * F::kBytes, valid, va);
+        load_tile<F, GS>((const char*)src_w + el_off * F::kBytes, valid, va);
+        if (need_d) {   // the descriptor (outputs) while the loads are in flight
+            d = descs[cur];
+            need_d = false;
+        }
 #ifdef AWQ_TRACE
         if (tr1 == 0) {
             tr1 = __builtin_amdgcn_s_memrealtime();

@@ -47,6 +47,19 @@ constexpr int kWavesPerBlock = AWQ_WPB;
 // independent of the workgroup size: entry t / kTableTiles names the tensor of tile
 // kTableTiles * (t / kTableTiles)
 constexpr int kTableTiles = AWQ_BLOCK_TILES;
+// One entry of the tensor table per kTableTiles tiles (awq_plan_block_tensor): everything a
+// wave needs to issue its tile's loads — the tensor's input, first tile and shape — in one
+// 64-B scalar load, so the loads no longer wait for a second, dependent load of the 80-B
+// descriptor (which the wave then fetches while its loads are in flight).
+struct alignas(16) TableEntry {
+    const void* w;        // the tensor's input
+    int64_t tile_begin;   // its first tile
+    int64_t rows, K;
+    int32_t tensor;       // descriptor index; bit 31: the entry's tiles span tensors (slow path)
+    int32_t pad[7];
+};
+static_assert(sizeof(TableEntry) == 64, "table entry");
+constexpr int kTableEntryInts = (int)(sizeof(TableEntry) / 4);
 
 // group sizes the streaming kernel is instantiated for (8 elements per lane: GS / 8 lanes
 // per group, a power of two between 4 and 32 so the group reductions stay inside DPP rows

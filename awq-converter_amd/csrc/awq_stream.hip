@@ -336,28 +336,37 @@ void submitter_main(Pipeline* P) {
         if (!quantize_batch(*P, B, cs)) return;
         if (!P->hip_ok(hipEventRecord(P->ev_kern[b], cs), "event")) return;
         if (!P->hip_ok(hipStreamWaitEvent(d2h, P->ev_kern[b], 0), "stream wait")) return;
-        // outputs of the items this batch completes, adjacent ranges as one copy
-        char *hs = nullptr, *ds = nullptr;
-        int64_t len = 0;
-        auto flush = [&]() {
-            if (len > 0 && !P->hip_ok(hipMemcpyAsync(hs, ds, (size_t)len, hipMemcpyDeviceToHost, d2h), "D2H"))
+        // outputs of the items this batch completes (two ranges per item), adjacent ranges as
+        // one copy
+        struct Run {
+            char *hs = nullptr, *ds = nullptr;
+            int64_t len = 0;
+        } run[2];
+        auto flush = [&](Run& r) {
+            if (r.len > 0 && !P->hip_ok(hipMemcpyAsync(r.hs, r.ds, (size_t)r.len, hipMemcpyDeviceToHost, d2h), "D2H"))
                 return false;
-            len = 0;
+            r.len = 0;
             return true;
         };
         for (int i = B.item_begin; i < B.item_end; ++i) {
             const awq_stream_item& it = P->items[i];
-            if (!it.host_out || !it.dev_out || it.out_bytes <= 0) continue;
-            if (len > 0 && hs + len == (char*)it.host_out && ds + len == (char*)it.dev_out) {
-                len += it.out_bytes;
-                continue;
+            const void* h[2] = {it.host_out, it.host_out2};
+            const void* dv[2] = {it.dev_out, it.dev_out2};
+            const int64_t nb[2] = {it.out_bytes, it.out_bytes2};
+            for (int k = 0; k < 2; ++k) {
+                if (!h[k] || !dv[k] || nb[k] <= 0) continue;
+                Run& r = run[k];
+                if (r.len > 0 && r.hs + r.len == (const char*)h[k] && r.ds + r.len == (const char*)dv[k]) {
+                    r.len += nb[k];
+                    continue;
+                }
+                if (!flush(r)) return;
+                r.hs = (char*)h[k];
+                r.ds = (char*)dv[k];
+                r.len = nb[k];
             }
-            if (!flush()) return;
-            hs = (char*)it.host_out;
-            ds = (char*)it.dev_out;
-            len = it.out_bytes;
         }
-        if (!flush()) return;
+        if (!flush(run[0]) || !flush(run[1])) return;
         if (!P->hip_ok(hipEventRecord(P->ev_done[b], d2h), "event")) return;
         {
             std::lock_guard<std::mutex> g(P->mu);
@@ -377,8 +386,8 @@ extern "C" {
 
 int64_t awq_stream_table_bytes(int64_t slot_bytes) {
     const int64_t descs = align_up((int64_t)sizeof(awq_tensor_desc) * AWQ_STREAM_MAX_BATCH_ITEMS, kAlign);
-    // tensor tables: one int32 per AWQ_BLOCK_TILES tiles of >= 4 KiB of input, per dtype group
-    const int64_t tables = 4 * (slot_bytes / 4096 / AWQ_BLOCK_TILES + 4 * 4) + 4 * 16;
+    // tensor tables: one 64-B entry per AWQ_BLOCK_TILES tiles of >= 4 KiB of input, per dtype group
+    const int64_t tables = 64 * (slot_bytes / 4096 / AWQ_BLOCK_TILES + 4 * 4) + 4 * 16;
     return align_up(descs + tables, 4096);
 }
 

@@ -161,12 +161,15 @@ int64_t awq_plan_ragged(awq_tensor_desc* descs_host, int n, int bits, int64_t gr
  * workgroup size is the library's own business (one 64-lane wave per tile). */
 #define AWQ_BLOCK_TILES 8
 
-/* HOST helper: block_tensor[b] = index of the tensor holding tile AWQ_BLOCK_TILES * b, with
- * bit 31 set when tiles AWQ_BLOCK_TILES * b .. + AWQ_BLOCK_TILES - 1 span more than one
- * tensor (a wave then steps forward from there to its own); b < ceil(total_tiles / AWQ_BLOCK_TILES) = the return value (< 0 on error:
- * len too small).  block_tensor_host = NULL with len = 0: returns the length needed
- * without writing (the workgroup size is the library's).  descs_host as planned by
- * awq_plan_ragged. */
+/* HOST helper: the ragged launch's tensor table, one 64-B entry per AWQ_BLOCK_TILES tiles
+ * (opaque to the caller: 16 int32 each): the input pointer, first tile and shape of the
+ * tensor holding tile AWQ_BLOCK_TILES * b (so a wave issues its loads after one scalar load)
+ * and its descriptor index, with bit 31 set when the entry's tiles span more than one
+ * tensor (a wave then steps forward from there to its own).  Returns the number of int32
+ * written (< 0 on error: len too small, or block_tensor_host not 16-B aligned);
+ * block_tensor_host = NULL with len = 0 returns the length needed without writing.
+ * descs_host as planned by awq_plan_ragged (the pointers are the device pointers the
+ * launch will read). */
 int64_t awq_plan_block_tensor(const awq_tensor_desc* descs_host, int n, int64_t total_tiles,
                               int32_t* block_tensor_host, int64_t len);
 
@@ -253,6 +256,9 @@ typedef struct awq_stream_item {
     void* dev_out;       /* D2H of [dev_out, dev_out + out_bytes) (the item's outputs, laid out */
     void* host_out;      /* by the caller inside that range) into pinned host_out; NULL: none */
     int64_t out_bytes;
+    void* dev_out2;      /* a second range (e.g. the fp16 scales, kept in a buffer of their */
+    void* host_out2;     /* own dtype), NULL: none */
+    int64_t out_bytes2;
 } awq_stream_item;
 
 typedef struct awq_stream_config {

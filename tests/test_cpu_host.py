@@ -56,13 +56,21 @@ def test_host_helpers_without_gpu():
     # 1024 rows x G=32 -> 16-group tiles -> 2048; G=6 (even) -> byte tiles: 16 flat groups
     assert d[0].tile_count == 2048 and d[1].tile_count == 1 and d[2].tile_count == 19
     assert total == 2048 + 1 + 19 and d[2].tile_begin == 2049
-    # per-workgroup tensor table: workgroup b holds tiles 8b..8b+7 (AWQ_BLOCK_TILES)
+    # tensor table: entry b (64 B = 16 int32) covers tiles 8b..8b+7 (AWQ_BLOCK_TILES): the
+    # tensor's input pointer, first tile, rows, K, then its index (bit 31: the entry spans)
     arr = (_hip.TensorDesc * 3)(*d)
-    tab = torch.full((300,), -7, dtype=torch.int32)
-    assert lib.awq_plan_block_tensor(arr, 3, total, ctypes.c_void_p(tab.data_ptr()), 300) == 259
+    assert lib.awq_plan_block_tensor(arr, 3, total, None, 0) == 259 * 16
+    tab = torch.full((300 * 16,), -7, dtype=torch.int32)
+    assert lib.awq_plan_block_tensor(arr, 3, total, ctypes.c_void_p(tab.data_ptr()), 300 * 16) == 259 * 16
+    e = tab[:259 * 16].view(259, 16)
+    idx = e[:, 8]
     # block 256 = tiles 2048 (t1), 2049-2055 (t2): spans -> bit 31
-    assert tab[:256].eq(0).all() and tab[256].item() == (1 | -2**31) and tab[257:259].eq(2).all()
-    assert tab[259:].eq(-7).all()
+    assert idx[:256].eq(0).all() and idx[256].item() == (1 | -2**31) and idx[257:259].eq(2).all()
+    q = e.view(torch.int64)                      # [259, 8]: w, tile_begin, rows, K, ...
+    for b, t in ((0, 0), (255, 0), (257, 2)):
+        assert q[b, 0].item() == d[t].w and q[b, 1].item() == arr[t].tile_begin
+        assert q[b, 2].item() == d[t].rows and q[b, 3].item() == d[t].K
+    assert tab[259 * 16:].eq(-7).all()
     assert lib.awq_plan_block_tensor(arr, 3, total, ctypes.c_void_p(tab.data_ptr()), 100) < 0
     # G odd at 4 bits -> word tiles: K=384 (G=3) -> 5 rows (15 groups) per tile
     d = [_hip.TensorDesc(4096 * 16, 11, 384, 0, 0, 2 * 4096, 0, 0, 0, 0)]

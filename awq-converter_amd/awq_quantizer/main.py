@@ -580,16 +580,17 @@ def quantize_stream_native(loader, infos: List[TensorInfo], quantizer: AWQQuanti
             setattr(it, nf, size[dt] * es)
             setattr(it, hf, None if keep_on_device else hosts[seg][dt].data_ptr() + hoff[dt] * es)
     total_in = sum(i.nbytes for i, _, _ in items)
-    slot = slot_bytes or min(256 << 20, max(32 << 20, total_in // 8))
+    slot = slot_bytes or STREAM_OPTS.get("slot_bytes") or min(256 << 20, max(32 << 20, total_in // 8))
     slot = -(-slot // 4096) * 4096
-    nslots = 3
+    nslots = int(STREAM_OPTS.get("nslots", 3))
     tb = int(lib.awq_stream_table_bytes(slot))
     h_stage = torch.empty(nslots * slot, dtype=torch.uint8, pin_memory=True)
     d_stage = torch.empty(nslots * slot, dtype=torch.uint8, device=dev)
     h_tab = torch.empty(nslots * tb, dtype=torch.uint8, pin_memory=True)
     d_tab = torch.empty(nslots * tb, dtype=torch.uint8, device=dev)
     compute = torch.cuda.current_stream(dev)
-    h2d, d2h = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+    h2d = torch.cuda.Stream(dev)
+    d2h = h2d if STREAM_OPTS.get("copy_streams", 2) == 1 else torch.cuda.Stream(dev)
     cfg = _hip.StreamConfig(bits=bits, symmetric=int(bool(quantizer.symmetric)), group_size=gs,
                             readers=min(16, max(8, readers)), nslots=nslots, slot_bytes=slot,
                             first_batch_bytes=max(4096, slot // 4 // 4096 * 4096),
@@ -986,6 +987,7 @@ def main(argv: Optional[List[str]] = None) -> int:
                                  logger)
         chunk_of = {i.name: k // args.chunk_size for k, i in enumerate(ordered)}
         threads = []
+        TIMINGS["pre_stream_s"] = time.time() - start
         for d, part in zip(devices, parts):
             logger.info(f"Processing {len(part)} tensors on {d}")
             th = threading.Thread(target=_device_worker, args=(loader, part, quantizers[d], d, args.num_workers,
@@ -1034,6 +1036,9 @@ def main(argv: Optional[List[str]] = None) -> int:
 
 _SCALARS = ("bits", "group_size", "symmetric", "shape")
 TIMINGS: Dict[str, float] = {}   # phase times of the last main() call (scripts/cli_bench.py)
+# native pipeline overrides for measurement scripts (scripts/cli_profile.py --stream-opts):
+# slot_bytes, nslots, copy_streams (1: H2D and D2H share one stream)
+STREAM_OPTS: Dict[str, int] = {}
 
 
 def _main_distributed(args, loader, ordered: List[TensorInfo], logger, start: float,

@@ -508,6 +508,59 @@ __global__ __launch_bounds__(kDqThreads) void awq_dequant_words_v2_kernel(
                                     o + threadIdx.x + kDqThreads * h);
 }
 
+// The same arithmetic with four outputs per lane: a 4-bit word is shared by two neighbouring
+// lanes (each converts one nibble half), so every lane issues exactly one 16-B store and a
+// wave's store instruction covers 1 KiB contiguous with no LDS round trip or barrier (v2's
+// staging); the word, scale and qzeros loads of the lane pair hit the same dwords.  REMAP: the
+// XCD-contiguous block order of v2.
+template <int BITS, bool REMAP>
+__global__ __launch_bounds__(256) void awq_dequant_quads_kernel(
+    const int32_t* __restrict__ qweight, const uint16_t* __restrict__ scales, const int32_t* __restrict__ qzeros,
+    int64_t words, uint32_t wpr, uint32_t L, uint32_t G, uint32_t zpr, int qmin, float* __restrict__ out) {
+    constexpr int PER = 32 / BITS;
+    constexpr int LPW = PER / 4;                        // lanes per word: 2 (4-bit), 1 (8-bit)
+    constexpr uint32_t MASK = (1u << BITS) - 1u;
+    const int64_t blk = REMAP ? xcd_contiguous_block(blockIdx.x, gridDim.x) : blockIdx.x;
+    const int64_t t = blk * 256 + threadIdx.x;
+    const int64_t i = t / LPW;                          // word
+    const int half = (int)(t - i * LPW);                // which 4 fields of the word
+    if (i >= words) return;
+    int64_t r;
+    uint32_t c;
+    if (words <= (int64_t)0xFFFFFFFFu) {
+        const uint32_t r32 = (uint32_t)i / wpr;
+        r = r32;
+        c = (uint32_t)i - r32 * wpr;
+    } else {
+        r = i / wpr;
+        c = (uint32_t)(i - r * wpr);
+    }
+    const uint32_t g = (uint32_t)(((uint64_t)c * PER) / L);
+    const uint32_t wq = (uint32_t)__builtin_nontemporal_load(qweight + i) >> (16 * half);
+    const float s = (float)__builtin_bit_cast(_Float16, scales[r * G + g]);
+    const int32_t z = (int32_t)(((uint32_t)qzeros[r * zpr + g / PER] >> (BITS * (g % PER))) & MASK) + qmin;
+    float v[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int32_t q = (int32_t)((wq >> (BITS * j)) & MASK) + qmin;
+        const float p = (float)(q - z) * s;
+        if (__builtin_expect(__builtin_isnan(p), 0)) {   // NaN bits of the reference's fp32 copy
+            const int64_t k = (int64_t)c * PER + 4 * half + j, K = (int64_t)wpr * PER, g0 = (int64_t)g * L;
+            v[j] = __uint_as_float(dq_nan_bits(sw_f32_to_f16(p), k - g0, min((int64_t)L, K - g0)));
+        } else {
+            v[j] = (float)(_Float16)p;
+        }
+    }
+    typedef float f4 __attribute__((ext_vector_type(4)));
+    __builtin_nontemporal_store((f4){v[0], v[1], v[2], v[3]}, (f4*)(out + 4 * t));
+}
+
+template <int B> constexpr auto dq_v2_remap = awq_dequant_words_v2_kernel<B, true>;
+template <int B> constexpr auto dq_v2_plain = awq_dequant_words_v2_kernel<B, false>;
+template <int B> constexpr auto dq_quads_plain = awq_dequant_quads_kernel<B, false>;
+template <int B> constexpr auto dq_quads_remap = awq_dequant_quads_kernel<B, true>;
+constexpr int kDqDefault = 3;   // profiles/round3: see DESIGN.md §5 (dequantize_packed)
+
 inline unsigned grid_for(int64_t work, int64_t per_block, int64_t cap) {
     int64_t b = (work + per_block - 1) / per_block;
     if (b < 1) b = 1;
@@ -614,30 +667,29 @@ hipError_t launch_dequant(const int32_t* tensor_q, const int32_t* qweight, const
         const int64_t words = total / per;
         const uint32_t wpr = (uint32_t)(K / per), zpr = (uint32_t)((G + per - 1) / per);
         const dim3 grid((unsigned)((words + 255) / 256)), block(256);
-        if (tuning().dq_words_v1 == 1) {      // round-2 kernel (A/B, awq_hip_tuning.h)
-            if (bits == 4)
-                hipLaunchKernelGGL(awq_dequant_words_kernel<4>, grid, block, 0, stream, qweight, scales, qzeros,
-                                   words, wpr, (uint32_t)L, (uint32_t)G, zpr, qmin, out);
-            else
-                hipLaunchKernelGGL(awq_dequant_words_kernel<8>, grid, block, 0, stream, qweight, scales, qzeros,
-                                   words, wpr, (uint32_t)L, (uint32_t)G, zpr, qmin, out);
-            return hipPeekAtLastError();
+        // kernel choice (awq_hip_tuning.h dq_words_v1, A/B only): 1 round-2 word kernel, 2 / 3
+        // LDS-staged v2 with / without XCD-contiguous blocks, 4 / 5 four-output lanes without /
+        // with XCD-contiguous blocks; 0 = the default
+        int v = tuning().dq_words_v1;
+        if (v <= 0 || v > 5) v = kDqDefault;
+#define AWQ_DQ(KER, GRID)                                                                                   \
+        do {                                                                                                \
+            if (bits == 4)                                                                                  \
+                hipLaunchKernelGGL(KER<4>, GRID, block, 0, stream, qweight, scales, qzeros, words, wpr,     \
+                                   (uint32_t)L, (uint32_t)G, zpr, qmin, out);                               \
+            else                                                                                            \
+                hipLaunchKernelGGL(KER<8>, GRID, block, 0, stream, qweight, scales, qzeros, words, wpr,     \
+                                   (uint32_t)L, (uint32_t)G, zpr, qmin, out);                               \
+        } while (0)
+        const dim3 grid_q((unsigned)((words * (per / 4) + 255) / 256));
+        switch (v) {
+        case 1: AWQ_DQ(awq_dequant_words_kernel, grid); break;
+        case 2: AWQ_DQ(dq_v2_remap, grid); break;
+        case 3: AWQ_DQ(dq_v2_plain, grid); break;
+        case 4: AWQ_DQ(dq_quads_plain, grid_q); break;
+        default: AWQ_DQ(dq_quads_remap, grid_q); break;
         }
-        if (tuning().dq_words_v1 == 2) {      // + XCD-contiguous blocks (A/B)
-            if (bits == 4)
-                hipLaunchKernelGGL((awq_dequant_words_v2_kernel<4, true>), grid, block, 0, stream, qweight, scales,
-                                   qzeros, words, wpr, (uint32_t)L, (uint32_t)G, zpr, qmin, out);
-            else
-                hipLaunchKernelGGL((awq_dequant_words_v2_kernel<8, true>), grid, block, 0, stream, qweight, scales,
-                                   qzeros, words, wpr, (uint32_t)L, (uint32_t)G, zpr, qmin, out);
-            return hipPeekAtLastError();
-        }
-        if (bits == 4)
-            hipLaunchKernelGGL((awq_dequant_words_v2_kernel<4, false>), grid, block, 0, stream, qweight, scales, qzeros,
-                               words, wpr, (uint32_t)L, (uint32_t)G, zpr, qmin, out);
-        else
-            hipLaunchKernelGGL((awq_dequant_words_v2_kernel<8, false>), grid, block, 0, stream, qweight, scales, qzeros,
-                               words, wpr, (uint32_t)L, (uint32_t)G, zpr, qmin, out);
+#undef AWQ_DQ
         return hipPeekAtLastError();
     }
     hipLaunchKernelGGL(awq_dequant_kernel, dim3(grid_for(total, 256, 256 * 16)), dim3(256), 0, stream,

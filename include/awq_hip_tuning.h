@@ -23,8 +23,9 @@ typedef struct awq_tuning {
     int32_t rg_waves;        /* 1 or 2: waves per row-segment tile (0 = cost model) */
     int32_t rg_gpt;          /* 8..64, multiple of 8: groups per row-segment tile (0 = cost model) */
     int32_t gen_noreg;       /* 1: fp64 gs 64/128 take the strided span instead of the register span */
-    int32_t dq_words_v1;     /* packed dequantize: 0 the staged word kernel, 1 the round-2 word kernel
-                                (per-thread stores), 2 staged + XCD-contiguous blocks */
+    int32_t dq_words_v1;     /* packed dequantize kernel: 0 the default, 1 the round-2 word kernel
+                                (per-thread stores), 2 / 3 LDS-staged words with / without
+                                XCD-contiguous blocks, 4 / 5 four-output lanes without / with */
 } awq_tuning;
 
 /* Set (t != NULL) or reset to the defaults (t == NULL) this thread's tuning. */

@@ -54,6 +54,18 @@ def probes(model_dir, threads):
                 dst.copy_(src, non_blocking=True)
         s.synchronize()
         out[name] = round(8 * n / (time.perf_counter() - t0) / 1e9, 2)
+    # both directions at once on two streams (the native pipeline's H2D and D2H overlap)
+    h2, d2, s2 = torch.empty_like(h).pin_memory(), torch.empty_like(d), torch.cuda.Stream(dev)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(8):
+        with torch.cuda.stream(s):
+            d.copy_(h, non_blocking=True)
+        with torch.cuda.stream(s2):
+            h2.copy_(d2, non_blocking=True)
+    torch.cuda.synchronize()
+    out["h2d_plus_d2h_concurrent_GBs"] = round(16 * n / (time.perf_counter() - t0) / 1e9, 2)
+    del h2, d2
     # page cache -> pinned (the CLI's read path): every file, `threads` preads in flight
     files = [os.path.join(model_dir, f) for f in sorted(os.listdir(model_dir)) if f.endswith(".safetensors")]
     total = sum(os.path.getsize(f) for f in files)
@@ -92,6 +104,9 @@ def main():
     ap.add_argument("--cprofile", default=None, help="cProfile the last run's pipeline thread to this file")
     ap.add_argument("--extra", default="", help="extra CLI flags")
     ap.add_argument("--engines", default="native", help="--stream_engine values to run, e.g. native,python")
+    ap.add_argument("--stream-opts", default="", help="'/'-separated settings of main.STREAM_OPTS to run the "
+                    "native engine under, each 'default' or k=v[,k=v] over slot_bytes / nslots / copy_streams, "
+                    "e.g. default/copy_streams=1/slot_bytes=536870912")
     args = ap.parse_args()
     from awq_quantizer import main as cli_mod
     work = args.workdir or tempfile.mkdtemp(prefix="awq_cli_")
@@ -102,7 +117,13 @@ def main():
     print(json.dumps({"workload": args.workload, "files": args.shards, "input_GB": round(nbytes / 1e9, 3),
                       "build_s": round(time.time() - t0, 1)}), flush=True)
     first = True
-    for fmt, eng in [(f, e) for f in args.formats.split(",") for e in args.engines.split(",")]:
+    opts_list = [{} if o == "default" else {k: int(v) for k, v in (kv.split("=") for kv in o.split(","))}
+                 for o in args.stream_opts.split("/") if o.strip()] or [{}]
+    combos = [(f, e, o) for f in args.formats.split(",") for e in args.engines.split(",")
+              for o in (opts_list if e == "native" else [{}])]
+    for fmt, eng, opts in combos:
+        cli_mod.STREAM_OPTS.clear()
+        cli_mod.STREAM_OPTS.update(opts)
         for r in range(args.runs):
             if first and args.evict:
                 evict(model)
@@ -117,7 +138,7 @@ def main():
             os.environ.pop("AWQ_CLI_PROFILE", None)
             assert rc == 0
             ob = sum(os.path.getsize(os.path.join(out, f)) for f in os.listdir(out))
-            print(json.dumps({"workload": args.workload, "format": fmt, "engine": eng, "run": r,
+            print(json.dumps({"workload": args.workload, "format": fmt, "engine": eng, "opts": opts, "run": r,
                               "kind": ("process-first" + (", page cache evicted" if args.evict else "")) if first
                               else "warm", "input_GB": round(nbytes / 1e9, 3), "output_GB": round(ob / 1e9, 3),
                               "wall_s": round(wall, 4), "input_GBs": round(nbytes / wall / 1e9, 3),

@@ -88,7 +88,7 @@ def one(args, _hip, dev, shape, name, gs, generic):
 
         def dq():
             _hip.dequantize_packed(qw, qz, sc, R, K, gs, args.bits, False, out)
-        variants = (0, 1, 2) if args.dq_ab else (0,)
+        variants = (1, 2, 3, 4, 5) if args.dq_ab else (0,)
         ref = None
         for rnd in range(3 if args.dq_ab else 1):
             for v in variants:
@@ -105,7 +105,7 @@ def one(args, _hip, dev, shape, name, gs, generic):
                 same = bool(torch.equal(out.view(torch.int32), ref.view(torch.int32)))
                 us = a.elapsed_time(b) / args.iters * 1e3
                 algo = out.numel() * 4 + sum(t.numel() * t.element_size() for t in (qw, qz, sc))
-                print(json.dumps({"op": "dequantize_packed", "kernel": ["words_v2", "words_v1", "words_v2_xcd"][v], "round": rnd,
+                print(json.dumps({"op": "dequantize_packed", "kernel": ["default", "words_v1", "words_v2_xcd", "words_v2", "quads", "quads_xcd"][v], "round": rnd,
                                   "shape": [R, K], "group_size": gs, "bits": args.bits, "same_bits": same,
                                   "us": round(us, 1), "algorithmic_GBs": round(algo / us / 1e3, 1),
                                   "frac_8TBs": round(algo / us / 1e3 / 8000, 3)}), flush=True)

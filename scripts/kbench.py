@@ -158,7 +158,7 @@ def main():
                             evs.append((s0, s1))
                     torch.cuda.synchronize()
                     us = [a.elapsed_time(b) * 1e3 for a, b in evs]
-                    key = (sname, os.path.basename(lp), blk)
+                    key = (sname, os.path.relpath(lp, ROOT) if os.path.isabs(lp) else lp, blk)
                     results.setdefault(key, []).append(statistics.median(us))
     for lib in handles.values():
         if hasattr(lib, "awq_set_tuning"):

@@ -16,7 +16,7 @@ import torch
 
 LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib")
 LIB_PATH = os.path.join(LIB_DIR, "libawq_hip.so")
-ABI_VERSION = 10
+ABI_VERSION = 11
 Q_SMALL_TENSOR = 1      # include/awq_hip.h AWQ_Q_SMALL_TENSOR
 
 AWQ_DTYPE = {torch.bfloat16: 0, torch.float16: 1, torch.float32: 2, torch.float64: 3}
@@ -46,9 +46,14 @@ class StreamItem(ctypes.Structure):
 class StreamConfig(ctypes.Structure):
     """Mirror of awq_stream_config (include/awq_hip.h)."""
     _fields_ = [("bits", _I32), ("symmetric", _I32), ("group_size", _I32), ("readers", _I32), ("nslots", _I32),
-                ("reserved", _I32), ("slot_bytes", _I64), ("first_batch_bytes", _I64), ("host_staging", _P),
+                ("trace_batches", _I32), ("slot_bytes", _I64), ("first_batch_bytes", _I64), ("host_staging", _P),
                 ("dev_staging", _P), ("host_tables", _P), ("dev_tables", _P), ("compute_stream", _P),
-                ("h2d_stream", _P), ("d2h_stream", _P)]
+                ("h2d_stream", _P), ("d2h_stream", _P), ("trace", _P)]
+
+
+STREAM_TRACE_FIELDS = 8   # AWQ_STREAM_TRACE_FIELDS
+STREAM_TRACE_NAMES = ("read_first", "read_last", "h2d_enq", "kern_enq", "d2h_enq", "h2d_done", "kern_done",
+                      "d2h_done")
 
 
 class StreamStats(ctypes.Structure):
@@ -57,13 +62,14 @@ class StreamStats(ctypes.Structure):
                 ("read_busy_s", ctypes.c_double), ("wait_read_s", ctypes.c_double), ("wait_slot_s", ctypes.c_double)]
 
 
-assert ctypes.sizeof(StreamItem) == 120 and ctypes.sizeof(StreamConfig) == 96
+assert ctypes.sizeof(StreamItem) == 120 and ctypes.sizeof(StreamConfig) == 104
 
 
 class Tuning(ctypes.Structure):
     """Mirror of awq_tuning (include/awq_hip_tuning.h): diagnostics / A-B controls only."""
     _fields_ = [("max_blocks", _I32), ("tiles_per_wave", _I32), ("no_rowgroup", _I32), ("rg_waves", _I32),
-                ("rg_gpt", _I32), ("gen_noreg", _I32), ("dq_words_v1", _I32)]
+                ("rg_gpt", _I32), ("gen_noreg", _I32), ("dq_words_v1", _I32),
+                ("rg_p1", _I32), ("rg_p2", _I32)]
 
 # symbol -> (restype, argtypes); the CPU test suite checks every one is exported.
 SIGNATURES = {

@@ -598,6 +598,11 @@ def quantize_stream_native(loader, infos: List[TensorInfo], quantizer: AWQQuanti
                             host_tables=h_tab.data_ptr(), dev_tables=d_tab.data_ptr(),
                             compute_stream=compute.cuda_stream, h2d_stream=h2d.cuda_stream,
                             d2h_stream=d2h.cuda_stream)
+    trace = None
+    if STREAM_OPTS.get("trace"):
+        cap = len(items) + total_in // slot + 2
+        trace = (ctypes.c_double * (cap * _hip.STREAM_TRACE_FIELDS))()
+        cfg.trace, cfg.trace_batches = ctypes.addressof(trace), cap
     handle = ctypes.c_void_p()
     t_run = time.perf_counter()
     _hip.check(lib.awq_stream_start(arr, len(items), ctypes.byref(cfg), ctypes.byref(handle)), "awq_stream_start")
@@ -655,6 +660,11 @@ def quantize_stream_native(loader, infos: List[TensorInfo], quantizer: AWQQuanti
                                           "submit_wait_read_s": round(stats.wait_read_s, 4),
                                           "submit_wait_slot_s": round(stats.wait_slot_s, 4),
                                           "bytes_read": int(stats.bytes_read)}})
+    if trace is not None:
+        nf = _hip.STREAM_TRACE_FIELDS
+        TIMINGS[f"stream_{device}"]["trace"] = [
+            dict(zip(_hip.STREAM_TRACE_NAMES, (round(v, 5) for v in trace[b * nf:(b + 1) * nf])))
+            for b in range(min(int(stats.batches), cfg.trace_batches))]
 
 
 def quantize_stream(loader, infos: List[TensorInfo], quantizer: AWQQuantizer, device: str, readers: int,
@@ -1037,7 +1047,8 @@ def main(argv: Optional[List[str]] = None) -> int:
 _SCALARS = ("bits", "group_size", "symmetric", "shape")
 TIMINGS: Dict[str, float] = {}   # phase times of the last main() call (scripts/cli_bench.py)
 # native pipeline overrides for measurement scripts (scripts/cli_profile.py --stream-opts):
-# slot_bytes, nslots, copy_streams (1: H2D and D2H share one stream)
+# slot_bytes, nslots, copy_streams (1: H2D and D2H share one stream), trace (1: per-batch
+# timestamps, include/awq_hip.h awq_stream_config.trace)
 STREAM_OPTS: Dict[str, int] = {}
 
 

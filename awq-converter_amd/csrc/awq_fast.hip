@@ -1018,8 +1018,59 @@ __device__ __forceinline__ void rg_reduce(int& smax, uint32_t& umax, uint32_t& u
 #define AWQ_RG_UNROLL 8
 #endif
 
+// raw-bits (signed max, unsigned max, unsigned min) of the 16-bit stage slots [s_lo, s_hi),
+// s_hi > s_lo, from the identities: packed 16-bit max/min over whole dwords (two chains); an
+// edge dword holding one foreign element gets a copy of its own element there
+__device__ __forceinline__ void rg_range16(const uint32_t* st32, int s_lo, int s_hi, int& smax, uint32_t& umax,
+                                           uint32_t& umin) {
+    const int d_lo = s_lo >> 1, d_hi = (s_hi + 1) >> 1;
+    s2 sm = {(short)-32768, (short)-32768}, sm_b = sm;
+    us2 um = {0, 0}, um_b = um;
+    us2 un = {(unsigned short)0xFFFF, (unsigned short)0xFFFF}, un_b = un;
+    auto acc = [&](uint32_t v) {
+        sm = __builtin_elementwise_max(sm, as_s2(v));
+        um = __builtin_elementwise_max(um, as_us2(v));
+        un = __builtin_elementwise_min(un, as_us2(v));
+    };
+    auto acc_b = [&](uint32_t v) {
+        sm_b = __builtin_elementwise_max(sm_b, as_s2(v));
+        um_b = __builtin_elementwise_max(um_b, as_us2(v));
+        un_b = __builtin_elementwise_min(un_b, as_us2(v));
+    };
+    uint32_t first = st32[d_lo];
+    if (s_lo & 1) first = __builtin_amdgcn_perm(first, first, 0x03020302u);   // low half := high
+    if (d_hi - d_lo == 1 && (s_hi & 1)) first = __builtin_amdgcn_perm(first, first, 0x01000100u);
+    acc(first);
+    if (d_hi - d_lo > 1) {
+        int d = d_lo + 1;
+        for (; d + 4 <= d_hi - 1; d += 4) {
+            const uint32_t v0 = st32[d], v1 = st32[d + 1], v2 = st32[d + 2], v3 = st32[d + 3];
+            acc(v0);
+            acc_b(v1);
+            acc(v2);
+            acc_b(v3);
+        }
+        if (d + 2 <= d_hi - 1) {
+            const uint32_t v0 = st32[d], v1 = st32[d + 1];
+            acc(v0);
+            acc_b(v1);
+            d += 2;
+        }
+        if (d < d_hi - 1) acc_b(st32[d]);
+        uint32_t last = st32[d_hi - 1];
+        if (s_hi & 1) last = __builtin_amdgcn_perm(last, last, 0x01000100u);        // high half := low
+        acc(last);
+    }
+    sm = __builtin_elementwise_max(sm, sm_b);
+    um = __builtin_elementwise_max(um, um_b);
+    un = __builtin_elementwise_min(un, un_b);
+    smax = max((int)sm.x, (int)sm.y);
+    umax = (uint32_t)max((int)um.x, (int)um.y);
+    umin = (uint32_t)min((int)un.x, (int)un.y);
+}
+
 // LDS: the segment's stage (dynamic, sized by the launch to the tile: 1.6-8 KiB) + 1.3 KiB
-template <typename F, int BITS, bool SYM, int SPLIT>
+template <typename F, int BITS, bool SYM, int SPLIT, bool P1C>
 __global__ __launch_bounds__(128) void awq_rowgroup_kernel(const void* __restrict__ w, int64_t rows, int64_t K,
                                                              int64_t L, int lgP, int GPT, uint32_t tiles_per_row,
                                                              int64_t G, int C, float invL,
@@ -1038,6 +1089,8 @@ __global__ __launch_bounds__(128) void awq_rowgroup_kernel(const void* __restric
     __shared__ uint32_t zst[64];
     __shared__ float4 prm[64];                          // per group: r, z, s, special
     __shared__ int not_plain;                           // a group of the tile needs the full quotient
+    __shared__ int acc_smax[P1C ? 64 : 1];              // P1C: per-group raw-bits reductions
+    __shared__ uint32_t acc_umax[P1C ? 64 : 1], acc_umin[P1C ? 64 : 1];
     // one tile per workgroup of 1 or 2 waves (host-chosen: two waves share a large tile's LDS
     // stage, so a whole-row tile keeps 8 waves per SIMD resident)
     const int lane = threadIdx.x, NT = blockDim.x;
@@ -1090,7 +1143,64 @@ __global__ __launch_bounds__(128) void awq_rowgroup_kernel(const void* __restric
         }
     }
     if (lane == 0) not_plain = 0;
+    if constexpr (P1C) {
+        // identities; the row's zero-padded last group starts from 0 (awq.py:337-339: the
+        // zeros join its min/max)
+        if (lane < ng) {
+            const bool pad = lane == ng - 1 && n_el - lane * (int)L < (int)L;
+            acc_smax[lane] = pad ? 0 : INT_MIN;
+            acc_umax[lane] = 0u;
+            acc_umin[lane] = pad ? 0u : F::kOnes;
+        }
+    }
     __syncthreads();
+    if constexpr (P1C) {
+        // ---- pass 1, contiguous chunks: lane = ceil(n_el / 8 / NT) consecutive 8-element
+        //      chunks of the segment, every lane busy; each run of the chunk inside one group
+        //      is reduced and merged into the group's LDS slots (ds_max / ds_min) ----
+        const int per = ((n_el + 7) >> 3) + NT - 1;
+        const int cpl = 8 * (per / NT);
+        int e = lane * cpl;
+        const int e_end = min(e + cpl, n_el);
+        while (e < e_end) {
+            const int g = (int)(((float)e + 0.5f) * invL);   // exact: e < 2^13, L <= 512
+            const int se = min((g + 1) * (int)L, e_end);
+            int smx;
+            uint32_t umx, umn;
+            if constexpr (F::kBytes == 2) {
+                rg_range16((const uint32_t*)stage, skew + e, skew + se, smx, umx, umn);
+            } else {
+                smx = INT_MIN;
+                umx = 0u;
+                umn = F::kOnes;
+                for (int i = e; i < se; ++i) {
+                    const uint32_t v = stage[skew + i];
+                    smx = max(smx, SL::sext(v));
+                    umx = max(umx, v);
+                    umn = min(umn, v);
+                }
+            }
+            atomicMax(&acc_smax[g], smx);
+            atomicMax(&acc_umax[g], umx);
+            atomicMin(&acc_umin[g], umn);
+            e = se;
+        }
+        __syncthreads();
+        // ---- the tile's group parameters: one lane per group (wave 0: ng <= 64) ----
+        if (lane < ng) {
+            float gmn, gmx;
+            bool gnan;
+            group_range<F, SYM>(acc_smax[lane], acc_umax[lane], acc_umin[lane], gmn, gmx, gnan);
+            const GroupParams p = params_from_range<F, BITS, SYM>(gmn, gmx);
+            const bool special = !F::fast(p.r);
+            if (F::kHasPlain && !F::plain_ok(p.s)) not_plain = 1;
+            const int64_t gi = r * G + g0 + lane;
+            if (scales) scales[gi] = f16_bits(p.s, gnan, nan_code);
+            if (zeros) zeros[gi] = __builtin_isnan(p.z) ? INT32_MIN : (int32_t)p.z;
+            zst[lane] = __builtin_isnan(p.z) ? NANF : ((uint32_t)((int)p.z - QMIN) & MASK);
+            prm[lane] = (float4){p.r, p.z, p.s, special ? 1.0f : 0.0f};
+        }
+    } else {
     // ---- this lane's chunk of its group ----
     const int grp = lane >> lgP, j = lane & (P - 1);
     const bool active = grp < ng;
@@ -1188,6 +1298,7 @@ __global__ __launch_bounds__(128) void awq_rowgroup_kernel(const void* __restric
         zst[grp] = __builtin_isnan(p.z) ? NANF : ((uint32_t)((int)p.z - QMIN) & MASK);
         prm[grp] = (float4){p.r, p.z, p.s, special ? 1.0f : 0.0f};
     }
+    }   // (pass 1 by groups)
     __syncthreads();
     // uniform: every group of the tile admits the plain quotient (F::plain_ok)
     const bool plain = F::kHasPlain && not_plain == 0;
@@ -1625,10 +1736,18 @@ hipError_t launch_rowgroup(const void* w, int dtype, int64_t rows, int64_t K, in
     // stage: the tile's elements rounded up to 16 B, + the up-to-16-B alignment skew and the
     // last 8-element vector read past the segment end
     const size_t lds = ((size_t)gpt * L * (dtype == AWQ_DTYPE_F32 ? 4 : 2) + 15) / 16 * 16 + 48;
+    const bool p1c = tuning().rg_p1 != 1;   // pass 1 by contiguous chunks (default) / by groups (A/B)
 #define AWQ_RG_SPLIT(Fm, B, S, SP)                                                                                 \
-    hipLaunchKernelGGL((awq_rowgroup_kernel<Fm, B, S, SP>), grid, block, lds, stream, w, rows, K, L, lgP, gpt,      \
-                       (uint32_t)tpr, G, C, 1.0f / (float)L, qweight, qzeros, scales, tensor_q, zeros,  \
-                       nan_code)
+    do {                                                                                                           \
+        if (p1c)                                                                                                   \
+            hipLaunchKernelGGL((awq_rowgroup_kernel<Fm, B, S, SP, true>), grid, block, lds, stream, w, rows, K, L, \
+                               lgP, gpt, (uint32_t)tpr, G, C, 1.0f / (float)L, qweight, qzeros, scales, tensor_q,  \
+                               zeros, nan_code);                                                                   \
+        else                                                                                                       \
+            hipLaunchKernelGGL((awq_rowgroup_kernel<Fm, B, S, SP, false>), grid, block, lds, stream, w, rows, K,   \
+                               L, lgP, gpt, (uint32_t)tpr, G, C, 1.0f / (float)L, qweight, qzeros, scales,         \
+                               tensor_q, zeros, nan_code);                                                         \
+    } while (0)
 #define AWQ_RG(Fm, B, S)                                                                                           \
     if (L % 8 == 0) AWQ_RG_SPLIT(Fm, B, S, 8);                                                                      \
     else if (L % 4 == 0) AWQ_RG_SPLIT(Fm, B, S, 4);                                                                 \

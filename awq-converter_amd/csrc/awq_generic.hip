@@ -555,10 +555,91 @@ __global__ __launch_bounds__(256) void awq_dequant_quads_kernel(
     __builtin_nontemporal_store((f4){v[0], v[1], v[2], v[3]}, (f4*)(out + 4 * t));
 }
 
+// Batched four-output lanes: each thread converts U quads (4 outputs, one 16-B store each) of
+// its block's 256 * U consecutive quads, with every load of the U quads (qweight word, scale,
+// qzeros word) issued before the first conversion — U independent loads in flight per lane
+// instead of one, and U times fewer waves (the one-quad kernels are bound by wave turnover:
+// one load round trip per short-lived wave).  RUN > 0: RUN consecutive blocks run on one XCD
+// (blocks are dealt round-robin over the 8 XCDs) so the scale and qzeros lines a run shares
+// are fetched by one L2 — without v2's one-range-per-XCD order, whose 8 concurrent streams
+// sit a power-of-two distance apart.
+__device__ __forceinline__ uint32_t dq_run_block(uint32_t b, uint32_t nb, uint32_t R) {
+    const uint32_t full = nb / (8u * R) * (8u * R);
+    if (b >= full) return b;
+    const uint32_t x = b % 8u, i = b / 8u;
+    return (i / R) * (8u * R) + x * R + (i % R);
+}
+
+template <int BITS, int U, int RUN>
+__global__ __launch_bounds__(256) void awq_dequant_batch_kernel(
+    const int32_t* __restrict__ qweight, const uint16_t* __restrict__ scales, const int32_t* __restrict__ qzeros,
+    int64_t words, uint32_t wpr, uint32_t L, uint32_t G, uint32_t zpr, int qmin, float* __restrict__ out) {
+    constexpr int PER = 32 / BITS;
+    constexpr int LPW = PER / 4;                        // lanes (quads) per word
+    constexpr uint32_t MASK = (1u << BITS) - 1u;
+    const int64_t blk = RUN > 0 ? dq_run_block(blockIdx.x, gridDim.x, RUN) : blockIdx.x;
+    const int64_t quads = words * LPW;
+    const int64_t q0 = blk * (256 * U) + threadIdx.x;
+    uint32_t wq[U], zq[U];
+    uint16_t sb[U];
+    int64_t ii[U];
+    uint32_t cc[U], gg[U];
+#pragma unroll
+    for (int k = 0; k < U; ++k) {
+        const int64_t q = min(q0 + 256 * k, quads - 1);   // (past the end: a valid address, no store)
+        const int64_t i = q / LPW;
+        int64_t r;
+        uint32_t c;
+        if (words <= (int64_t)0xFFFFFFFFu) {
+            const uint32_t r32 = (uint32_t)i / wpr;
+            r = r32;
+            c = (uint32_t)i - r32 * wpr;
+        } else {
+            r = i / wpr;
+            c = (uint32_t)(i - r * wpr);
+        }
+        const uint32_t g = (uint32_t)(((uint64_t)c * PER) / L);
+        ii[k] = i;
+        cc[k] = c;
+        gg[k] = g;
+        wq[k] = (uint32_t)__builtin_nontemporal_load(qweight + i);
+        sb[k] = scales[r * G + g];
+        zq[k] = (uint32_t)qzeros[r * zpr + g / PER];
+    }
+    typedef float f4 __attribute__((ext_vector_type(4)));
+#pragma unroll
+    for (int k = 0; k < U; ++k) {
+        const int64_t q = q0 + 256 * k;
+        if (q >= quads) break;
+        const int half = (int)(q - ii[k] * LPW);
+        const uint32_t w = wq[k] >> (16 * half);
+        const float s = (float)__builtin_bit_cast(_Float16, sb[k]);
+        const int32_t z = (int32_t)((zq[k] >> (BITS * (gg[k] % PER))) & MASK) + qmin;
+        float v[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int32_t qv = (int32_t)((w >> (BITS * j)) & MASK) + qmin;
+            const float p = (float)(qv - z) * s;
+            if (__builtin_expect(__builtin_isnan(p), 0)) {   // NaN bits of the reference's fp32 copy
+                const int64_t kk = (int64_t)cc[k] * PER + 4 * half + j, K = (int64_t)wpr * PER,
+                              g0 = (int64_t)gg[k] * L;
+                v[j] = __uint_as_float(dq_nan_bits(sw_f32_to_f16(p), kk - g0, min((int64_t)L, K - g0)));
+            } else {
+                v[j] = (float)(_Float16)p;
+            }
+        }
+        __builtin_nontemporal_store((f4){v[0], v[1], v[2], v[3]}, (f4*)(out + 4 * q));
+    }
+}
+
 template <int B> constexpr auto dq_v2_remap = awq_dequant_words_v2_kernel<B, true>;
 template <int B> constexpr auto dq_v2_plain = awq_dequant_words_v2_kernel<B, false>;
 template <int B> constexpr auto dq_quads_plain = awq_dequant_quads_kernel<B, false>;
 template <int B> constexpr auto dq_quads_remap = awq_dequant_quads_kernel<B, true>;
+template <int B> constexpr auto dq_batch4 = awq_dequant_batch_kernel<B, 4, 0>;
+template <int B> constexpr auto dq_batch8 = awq_dequant_batch_kernel<B, 8, 0>;
+template <int B> constexpr auto dq_batch4_run = awq_dequant_batch_kernel<B, 4, 4>;
+template <int B> constexpr auto dq_batch8_run = awq_dequant_batch_kernel<B, 8, 2>;
 constexpr int kDqDefault = 3;   // profiles/round3: see DESIGN.md §5 (dequantize_packed)
 
 inline unsigned grid_for(int64_t work, int64_t per_block, int64_t cap) {
@@ -669,9 +750,10 @@ hipError_t launch_dequant(const int32_t* tensor_q, const int32_t* qweight, const
         const dim3 grid((unsigned)((words + 255) / 256)), block(256);
         // kernel choice (awq_hip_tuning.h dq_words_v1, A/B only): 1 round-2 word kernel, 2 / 3
         // LDS-staged v2 with / without XCD-contiguous blocks, 4 / 5 four-output lanes without /
-        // with XCD-contiguous blocks; 0 = the default
+        // with XCD-contiguous blocks, 6 / 7 batched lanes (4 / 8 quads), 8 / 9 the same with
+        // XCD runs of 4 / 2 blocks; 0 = the default
         int v = tuning().dq_words_v1;
-        if (v <= 0 || v > 5) v = kDqDefault;
+        if (v <= 0 || v > 9) v = kDqDefault;
 #define AWQ_DQ(KER, GRID)                                                                                   \
         do {                                                                                                \
             if (bits == 4)                                                                                  \
@@ -682,7 +764,13 @@ hipError_t launch_dequant(const int32_t* tensor_q, const int32_t* qweight, const
                                    (uint32_t)L, (uint32_t)G, zpr, qmin, out);                               \
         } while (0)
         const dim3 grid_q((unsigned)((words * (per / 4) + 255) / 256));
+        const dim3 grid_b4((unsigned)((words * (per / 4) + 1023) / 1024)),
+            grid_b8((unsigned)((words * (per / 4) + 2047) / 2048));
         switch (v) {
+        case 6: AWQ_DQ(dq_batch4, grid_b4); break;
+        case 7: AWQ_DQ(dq_batch8, grid_b8); break;
+        case 8: AWQ_DQ(dq_batch4_run, grid_b4); break;
+        case 9: AWQ_DQ(dq_batch8_run, grid_b8); break;
         case 1: AWQ_DQ(awq_dequant_words_kernel, grid); break;
         case 2: AWQ_DQ(dq_v2_remap, grid); break;
         case 3: AWQ_DQ(dq_v2_plain, grid); break;

@@ -72,6 +72,8 @@ struct Pipeline {
     std::vector<Batch> batches;
     std::vector<ReadJob> jobs;
     std::vector<hipEvent_t> ev_h2d, ev_kern, ev_done;
+    hipEvent_t ev_start = nullptr;     // (trace only) the event clock's origin
+    std::vector<double> tr;            // (trace only) AWQ_STREAM_TRACE_FIELDS per batch, host part
     std::mutex mu;
     std::condition_variable cv;
     std::vector<int64_t> reads_left;
@@ -165,6 +167,8 @@ void reader_main(Pipeline* P) {
             std::lock_guard<std::mutex> g(P->mu);
             if (P->err || P->next_job >= P->jobs.size()) return;
             j = P->jobs[P->next_job++];
+            if (!P->tr.empty() && P->tr[j.batch * AWQ_STREAM_TRACE_FIELDS] < 0)
+                P->tr[j.batch * AWQ_STREAM_TRACE_FIELDS] = now_s() - P->t0;
         }
         const Batch& B = P->batches[j.batch];
         const int64_t prev = j.batch - P->cfg.nslots;   // the batch that used this slot before
@@ -194,8 +198,10 @@ void reader_main(Pipeline* P) {
             done += got;
         }
         std::lock_guard<std::mutex> g(P->mu);
-        P->read_busy += now_s() - t;
+        const double t1 = now_s();
+        P->read_busy += t1 - t;
         P->bytes_read += j.len;
+        if (!P->tr.empty()) P->tr[j.batch * AWQ_STREAM_TRACE_FIELDS + 1] = t1 - P->t0;
         if (--P->reads_left[j.batch] == 0) P->cv.notify_all();
     }
 }
@@ -327,6 +333,7 @@ void submitter_main(Pipeline* P) {
                                       hipMemcpyHostToDevice, h2d), "H2D"))
             return;
         if (!P->hip_ok(hipEventRecord(P->ev_h2d[b], h2d), "event")) return;
+        if (!P->tr.empty()) P->tr[b * AWQ_STREAM_TRACE_FIELDS + 2] = now_s() - P->t0;
         {
             std::lock_guard<std::mutex> g(P->mu);
             P->h2d_recorded = b;
@@ -335,6 +342,7 @@ void submitter_main(Pipeline* P) {
         if (!P->hip_ok(hipStreamWaitEvent(cs, P->ev_h2d[b], 0), "stream wait")) return;
         if (!quantize_batch(*P, B, cs)) return;
         if (!P->hip_ok(hipEventRecord(P->ev_kern[b], cs), "event")) return;
+        if (!P->tr.empty()) P->tr[b * AWQ_STREAM_TRACE_FIELDS + 3] = now_s() - P->t0;
         if (!P->hip_ok(hipStreamWaitEvent(d2h, P->ev_kern[b], 0), "stream wait")) return;
         // outputs of the items this batch completes (two ranges per item), adjacent ranges as
         // one copy
@@ -368,6 +376,7 @@ void submitter_main(Pipeline* P) {
         }
         if (!flush(run[0]) || !flush(run[1])) return;
         if (!P->hip_ok(hipEventRecord(P->ev_done[b], d2h), "event")) return;
+        if (!P->tr.empty()) P->tr[b * AWQ_STREAM_TRACE_FIELDS + 4] = now_s() - P->t0;
         {
             std::lock_guard<std::mutex> g(P->mu);
             P->done_recorded = b;
@@ -422,12 +431,21 @@ int awq_stream_start(const awq_stream_item* items, int n, const awq_stream_confi
     P->ev_h2d.resize(nb);
     P->ev_kern.resize(nb);
     P->ev_done.resize(nb);
+    const bool trace = c.trace != nullptr && c.trace_batches > 0;
     for (size_t b = 0; b < nb; ++b)
         for (hipEvent_t* e : {&P->ev_h2d[b], &P->ev_kern[b], &P->ev_done[b]})
-            if (hipEventCreateWithFlags(e, hipEventDisableTiming) != hipSuccess) {
+            if (hipEventCreateWithFlags(e, trace ? hipEventDefault : hipEventDisableTiming) != hipSuccess) {
                 delete P;   // (events created so far are reclaimed with the context)
                 return awq::set_error(AWQ_EHIP, "hipEventCreate failed");
             }
+    if (trace) {
+        P->tr.assign(nb * AWQ_STREAM_TRACE_FIELDS, -1.0);
+        if (hipEventCreate(&P->ev_start) != hipSuccess ||
+            hipEventRecord(P->ev_start, (hipStream_t)c.h2d_stream) != hipSuccess) {
+            delete P;
+            return awq::set_error(AWQ_EHIP, "trace event");
+        }
+    }
     P->t0 = now_s();
     const int nr = std::max(1, std::min(c.readers, (int)std::max<size_t>(1, P->jobs.size())));
     for (int r = 0; r < nr; ++r) P->readers.emplace_back(reader_main, P);
@@ -490,6 +508,19 @@ int awq_stream_end(void* handle, awq_stream_stats* stats) {
     }
     // nothing of the pipeline may still run once the caller's buffers are released
     for (void* s : {P->cfg.h2d_stream, P->cfg.compute_stream, P->cfg.d2h_stream}) (void)hipStreamSynchronize((hipStream_t)s);
+    if (P->ev_start) {
+        const size_t nt = std::min(P->batches.size(), (size_t)P->cfg.trace_batches);
+        for (size_t b = 0; b < nt; ++b) {
+            double* o = P->cfg.trace + b * AWQ_STREAM_TRACE_FIELDS;
+            for (int k = 0; k < 5; ++k) o[k] = P->tr[b * AWQ_STREAM_TRACE_FIELDS + k];
+            const hipEvent_t ev[3] = {P->ev_h2d[b], P->ev_kern[b], P->ev_done[b]};
+            for (int k = 0; k < 3; ++k) {
+                float ms = -1.0f;
+                o[5 + k] = (!rc && hipEventElapsedTime(&ms, P->ev_start, ev[k]) == hipSuccess) ? ms * 1e-3 : -1.0;
+            }
+        }
+        (void)hipEventDestroy(P->ev_start);
+    }
     for (size_t b = 0; b < P->batches.size(); ++b) {
         (void)hipEventDestroy(P->ev_h2d[b]);
         (void)hipEventDestroy(P->ev_kern[b]);

@@ -46,7 +46,7 @@
 extern "C" {
 #endif
 
-#define AWQ_HIP_ABI_VERSION 10
+#define AWQ_HIP_ABI_VERSION 11
 
 /* dtype codes of the input weights (torch dtypes the reference accepts, awq.py:397) */
 enum { AWQ_DTYPE_BF16 = 0, AWQ_DTYPE_F16 = 1, AWQ_DTYPE_F32 = 2, AWQ_DTYPE_F64 = 3 };
@@ -263,7 +263,8 @@ typedef struct awq_stream_item {
 
 typedef struct awq_stream_config {
     int32_t bits, symmetric, group_size, readers;   /* readers: pread threads (>= 1) */
-    int32_t nslots, reserved;                       /* nslots >= 2 */
+    int32_t nslots;                                 /* >= 2 */
+    int32_t trace_batches;                          /* capacity of `trace`, in batches */
     int64_t slot_bytes;          /* input bytes per staging slot, multiple of 4096 */
     int64_t first_batch_bytes;   /* capacity of the first batch (<= slot_bytes; 0 = slot_bytes) */
     void* host_staging;          /* pinned host, nslots * slot_bytes */
@@ -273,7 +274,16 @@ typedef struct awq_stream_config {
     void* compute_stream;
     void* h2d_stream;
     void* d2h_stream;
+    double* trace;               /* optional (NULL = off): AWQ_STREAM_TRACE_FIELDS doubles per
+                                    batch, seconds from the start, filled by awq_stream_end:
+                                    first read began, last read ended, H2D enqueued, kernels
+                                    enqueued, D2H enqueued (host clock); H2D done, kernels done,
+                                    D2H done (HIP event clock, from an event on the H2D stream
+                                    recorded at start); batches past
+                                    trace_batches are not traced. */
 } awq_stream_config;
+
+#define AWQ_STREAM_TRACE_FIELDS 8
 
 typedef struct awq_stream_stats {
     int64_t batches, pieces, bytes_read;

@@ -25,7 +25,12 @@ typedef struct awq_tuning {
     int32_t gen_noreg;       /* 1: fp64 gs 64/128 take the strided span instead of the register span */
     int32_t dq_words_v1;     /* packed dequantize kernel: 0 the default, 1 the round-2 word kernel
                                 (per-thread stores), 2 / 3 LDS-staged words with / without
-                                XCD-contiguous blocks, 4 / 5 four-output lanes without / with */
+                                XCD-contiguous blocks, 4 / 5 four-output lanes without / with,
+                                6 / 7 batched four-output lanes (4 / 8 per lane), 8 / 9 the
+                                same in XCD runs */
+    int32_t rg_p1;           /* row-segment pass 1: 0 the default (contiguous chunks per lane, LDS
+                                merges), 1 by groups (2^k lanes per group, DPP merges) */
+    int32_t rg_p2;           /* row-segment pass 2: 0 the default, 1 the round-2 form */
 } awq_tuning;
 
 /* Set (t != NULL) or reset to the defaults (t == NULL) this thread's tuning. */

@@ -30,7 +30,10 @@ def main():
     ap.add_argument("--group-sizes", default="128")
     ap.add_argument("--bits", type=int, default=4)
     ap.add_argument("--compare-generic", action="store_true")
+    ap.add_argument("--tunings", default="", help="'/'-separated awq_tuning settings to time the quantize under, "
+                    "each 'default' or k=v[,k=v] (include/awq_hip_tuning.h), e.g. default/rg_p1=1")
     ap.add_argument("--dequant", action="store_true", help="also time dequantize_packed of the packed result")
+    ap.add_argument("--dq-variants", default="1,3,6,7,8,9", help="--dq-ab: tuning dq_words_v1 values to time")
     ap.add_argument("--dq-ab", action="store_true", help="--dequant: also the round-2 word kernel (tuning dq_words_v1), "
                                                           "interleaved, 3 rounds")
     args = ap.parse_args()
@@ -41,10 +44,12 @@ def main():
         for name in args.dtypes.split(","):
             for gs in (int(v) for v in args.group_sizes.split(",")):
                 for generic in ((False, True) if args.compare_generic else (False,)):
-                    one(args, _hip, dev, shape, name, gs, generic)
+                    for tun in (args.tunings.split("/") if args.tunings else ["default"]):
+                        kw = {} if tun == "default" else {k: int(v) for k, v in (t.split("=") for t in tun.split(","))}
+                        one(args, _hip, dev, shape, name, gs, generic, kw)
 
 
-def one(args, _hip, dev, shape, name, gs, generic):
+def one(args, _hip, dev, shape, name, gs, generic, tun=None):
     R, K = (int(v) for v in shape.split(","))
     G = -(-K // gs)
     per = 32 // args.bits
@@ -52,7 +57,7 @@ def one(args, _hip, dev, shape, name, gs, generic):
     qw = torch.empty(R, -(-K // per), dtype=torch.int32, device=dev)
     qz = torch.empty(R, -(-G // per), dtype=torch.int32, device=dev)
     sc = torch.empty(R, G, dtype=torch.float16, device=dev)
-    _hip.load_library().awq_set_tuning(ctypes.byref(_hip.Tuning(no_rowgroup=int(generic))))
+    _hip.load_library().awq_set_tuning(ctypes.byref(_hip.Tuning(no_rowgroup=int(generic), **(tun or {}))))
     stage = {}
     if args.search or generic or not _hip.packs_directly(DT[name], R, K, gs):
         stage = dict(tensor_q=torch.empty(R * K, dtype=torch.int32, device=dev),
@@ -79,7 +84,7 @@ def one(args, _hip, dev, shape, name, gs, generic):
     kernel = ("generic+pack" if stage and not args.search else "search" if args.search else
               "generic" if generic or name == "f64" or gs > (256 if name == "f32" else 512) else
               "streaming" if _hip.ragged_eligible(DT[name], R, K, gs) else "row-segment")
-    print(json.dumps({"dtype": name, "shape": [R, K], "group_size": gs, "bits": args.bits, "kernel": kernel,
+    print(json.dumps({"dtype": name, "shape": [R, K], "group_size": gs, "bits": args.bits, "kernel": kernel, "tuning": tun or {},
                       "search": args.search, "us": round(us, 1), "input_GBs": round(nbytes / us / 1e3, 1),
                       "algorithmic_GBs": round(algo / us / 1e3, 1), "frac_8TBs": round(algo / us / 1e3 / 8000, 3)}),
           flush=True)
@@ -88,7 +93,7 @@ def one(args, _hip, dev, shape, name, gs, generic):
 
         def dq():
             _hip.dequantize_packed(qw, qz, sc, R, K, gs, args.bits, False, out)
-        variants = (1, 2, 3, 4, 5) if args.dq_ab else (0,)
+        variants = tuple(int(v) for v in args.dq_variants.split(",")) if args.dq_ab else (0,)
         ref = None
         for rnd in range(3 if args.dq_ab else 1):
             for v in variants:
@@ -105,7 +110,7 @@ def one(args, _hip, dev, shape, name, gs, generic):
                 same = bool(torch.equal(out.view(torch.int32), ref.view(torch.int32)))
                 us = a.elapsed_time(b) / args.iters * 1e3
                 algo = out.numel() * 4 + sum(t.numel() * t.element_size() for t in (qw, qz, sc))
-                print(json.dumps({"op": "dequantize_packed", "kernel": ["default", "words_v1", "words_v2_xcd", "words_v2", "quads", "quads_xcd"][v], "round": rnd,
+                print(json.dumps({"op": "dequantize_packed", "kernel": ["default", "words_v1", "words_v2_xcd", "words_v2", "quads", "quads_xcd", "batch4", "batch8", "batch4_run4", "batch8_run2"][v], "round": rnd,
                                   "shape": [R, K], "group_size": gs, "bits": args.bits, "same_bits": same,
                                   "us": round(us, 1), "algorithmic_GBs": round(algo / us / 1e3, 1),
                                   "frac_8TBs": round(algo / us / 1e3 / 8000, 3)}), flush=True)

@@ -112,3 +112,22 @@ def test_generic_f64_reg_span_matches_strided(gs):
     for key in ("qweight", "qzeros"):
         assert torch.equal(a[key], b[key])
     assert gio.same_bits(a["scales"], b["scales"])
+
+
+@pytest.mark.parametrize("variant", range(1, 10), ids=lambda v: f"dq{v}")
+@pytest.mark.parametrize("bits", [4, 8], ids=str)
+def test_dequantize_packed_kernel_variants(variant, bits):
+    """Every word-aligned dequantize kernel (tuning dq_words_v1 1..9: round-2 words, LDS-staged,
+    four-output lanes, batched lanes, with / without XCD block orders) gives the oracle's bits,
+    on a shape whose last block is partial (rows * K / 4 quads not a multiple of any block)
+    with special values."""
+    from awq_quantizer import _hip
+    x = specials(rand((37, 1536), variant + bits, 0.5), 11).to(torch.bfloat16)
+    q = Q(bits=bits, group_size=128, symmetric=False)
+    pk = q.quantize_packed(x)
+    ref = dict(orc.quantize(x, bits=bits, group_size=128, symmetric=False))
+    for key in ("tensor_q", "zero_points"):
+        ref[key] = (((ref[key].long() - q.qmin) & ((1 << bits) - 1)) + q.qmin).to(torch.int32)
+    with _hip.tuning(dq_words_v1=variant):
+        dq = q.dequantize_packed(pk).cpu()
+    assert gio.same_bits(dq, orc.dequantize(ref))

@@ -135,3 +135,13 @@ def test_rowgroup_groups_per_tile_override(dtype, shape, gs, gpt):
     with _hip.tuning(rg_gpt=gpt):
         for bits, sym in ((4, False), (8, True)):
             _assert_parity(rand(shape, gpt + gs + bits, 0.5, dtype), gs, bits, sym)
+
+
+@pytest.mark.parametrize("dtype,shape,gs", CASES[::3], ids=str)
+def test_rowgroup_pass1_by_groups(dtype, shape, gs):
+    """The round-2 pass 1 (tuning rg_p1=1: 2^k lanes per group, DPP merges) against the same
+    oracle as the default contiguous-chunk pass 1 (LDS ds_max / ds_min merges)."""
+    from awq_quantizer import _hip
+    with _hip.tuning(rg_p1=1):
+        for bits, sym in ((4, False), (8, True)):
+            _assert_parity(rand(shape, gs + bits + 7, 0.5, dtype), gs, bits, sym)

@@ -258,18 +258,25 @@ int64_t awq_plan_ragged(awq_tensor_desc* descs, int n, int bits, int64_t group_s
 int64_t awq_plan_block_tensor(const awq_tensor_desc* descs, int n, int64_t total_tiles, int32_t* block_tensor,
                               int64_t len) {
     g_err.clear();
-    const int64_t entries = (total_tiles + awq::kTableTiles - 1) / awq::kTableTiles;
+    const int64_t entries = awq::table_entries(total_tiles);
     const int64_t need = entries * awq::kTableEntryInts;   // int32 units
     if (!block_tensor && len == 0) return need;   // size query
     if (!block_tensor || len < need) return fail(AWQ_EINVAL, "block table needs %lld int32", (long long)need), -1;
     if ((uintptr_t)block_tensor % 16) return fail(AWQ_EINVAL, "block table must be 16-B aligned"), -1;
     if (n <= 0 || !descs) return fail(AWQ_EINVAL, "bad descriptor array"), -1;
     awq::TableEntry* tab = (awq::TableEntry*)block_tensor;
-    int cur = 0;
+    int pair_cur = 0;   // tensor of the current 128-tile pair's first tile (monotone over pairs)
     for (int64_t b = 0; b < entries; ++b) {
-        const int64_t t = b * awq::kTableTiles;
+        // the entry's tiles t0, t0 + 8, ..., t0 + 56 (awq_internal.h table_index); entries of
+        // one 128-tile pair are visited out of tile order, so each steps from the pair's tensor
+        const int64_t t = std::min(awq::table_first_tile(b), total_tiles - 1);
+        const int64_t last = std::max(t, std::min(t + 8 * (awq::kTableTiles - 1), total_tiles - 1));
+        if ((b & 15) == 0) {
+            const int64_t tp = std::min((b >> 4) * 128, total_tiles - 1);
+            while (pair_cur + 1 < n && descs[pair_cur + 1].tile_begin <= tp) ++pair_cur;
+        }
+        int cur = pair_cur;
         while (cur + 1 < n && descs[cur + 1].tile_begin <= t) ++cur;
-        const int64_t last = std::min(t + awq::kTableTiles, total_tiles) - 1;
         const bool spans = cur + 1 < n && descs[cur + 1].tile_begin <= last;
         awq::TableEntry e{};
         e.w = descs[cur].w;

@@ -1155,35 +1155,50 @@ __global__ __launch_bounds__(128) void awq_rowgroup_kernel(const void* __restric
     }
     __syncthreads();
     if constexpr (P1C) {
-        // ---- pass 1, contiguous chunks: lane = ceil(n_el / 8 / NT) consecutive 8-element
-        //      chunks of the segment, every lane busy; each run of the chunk inside one group
-        //      is reduced and merged into the group's LDS slots (ds_max / ds_min) ----
-        const int per = ((n_el + 7) >> 3) + NT - 1;
-        const int cpl = 8 * (per / NT);
-        int e = lane * cpl;
-        const int e_end = min(e + cpl, n_el);
-        while (e < e_end) {
-            const int g = (int)(((float)e + 0.5f) * invL);   // exact: e < 2^13, L <= 512
-            const int se = min((g + 1) * (int)L, e_end);
-            int smx;
-            uint32_t umx, umn;
-            if constexpr (F::kBytes == 2) {
-                rg_range16((const uint32_t*)stage, skew + e, skew + se, smx, umx, umn);
-            } else {
-                smx = INT_MIN;
-                umx = 0u;
-                umn = F::kOnes;
-                for (int i = e; i < se; ++i) {
-                    const uint32_t v = stage[skew + i];
-                    smx = max(smx, SL::sext(v));
-                    umx = max(umx, v);
-                    umn = min(umn, v);
+        // ---- pass 1, lanes split evenly over the tile's groups: Q = NT / ng lanes per group
+        //      (any count — not only a power of two; 3 for 41 groups of a 128-lane tile where
+        //      the by-groups pass keeps 2), each lane reduces one even-length run of its group
+        //      and merges it into the group's LDS slots (ds_max / ds_min) ----
+        const int Q = NT / ng;                            // >= 1: ng <= 64 <= NT
+        const int grp = (int)((float)lane * __builtin_amdgcn_rcpf((float)Q) + 1e-3f);   // lane / Q (lane < 128)
+        const int jq = lane - grp * Q;
+        if (grp < ng) {
+            const int glen = min((int)L, n_el - grp * (int)L);
+            const int cq = ((glen + Q - 1) / Q + 1) & ~1;   // even: runs start on dword pairs
+            const int cb = min(jq * cq, glen), ce = min(cb + cq, glen);
+            if (ce > cb) {
+                const int base = skew + grp * (int)L;
+                int smx;
+                uint32_t umx, umn;
+                if constexpr (F::kBytes == 2) {
+                    rg_range16((const uint32_t*)stage, base + cb, base + ce, smx, umx, umn);
+                } else {
+                    smx = INT_MIN;
+                    umx = 0u;
+                    umn = F::kOnes;
+                    int i1 = cb;
+                    for (; i1 + AWQ_RG_UNROLL <= ce; i1 += AWQ_RG_UNROLL) {
+                        uint32_t v[AWQ_RG_UNROLL];
+#pragma unroll
+                        for (int u = 0; u < AWQ_RG_UNROLL; ++u) v[u] = stage[base + i1 + u];
+#pragma unroll
+                        for (int u = 0; u < AWQ_RG_UNROLL; ++u) {
+                            smx = max(smx, SL::sext(v[u]));
+                            umx = max(umx, v[u]);
+                            umn = min(umn, v[u]);
+                        }
+                    }
+                    for (; i1 < ce; ++i1) {
+                        const uint32_t v = stage[base + i1];
+                        smx = max(smx, SL::sext(v));
+                        umx = max(umx, v);
+                        umn = min(umn, v);
+                    }
                 }
+                atomicMax(&acc_smax[grp], smx);
+                atomicMax(&acc_umax[grp], umx);
+                atomicMin(&acc_umin[grp], umn);
             }
-            atomicMax(&acc_smax[g], smx);
-            atomicMax(&acc_umax[g], umx);
-            atomicMin(&acc_umin[g], umn);
-            e = se;
         }
         __syncthreads();
         // ---- the tile's group parameters: one lane per group (wave 0: ng <= 64) ----
@@ -1532,7 +1547,7 @@ void awq_fast_kernel(
             // host-planned entry of the wave's tile group (awq_plan_block_tensor): ONE 64-B
             // scalar load gives the tensor's input and shape; entries whose tiles span
             // tensors (small tensors) step through the descriptors
-            const TableEntry* te = (const TableEntry*)block_tensor + wave / kTableTiles;
+            const TableEntry* te = (const TableEntry*)block_tensor + table_index(wave);
             const int32_t e = __builtin_amdgcn_readfirstlane(te->tensor);
             cur = e & 0x7FFFFFFF;
             if (e >= 0) {
@@ -1736,7 +1751,7 @@ hipError_t launch_rowgroup(const void* w, int dtype, int64_t rows, int64_t K, in
     // stage: the tile's elements rounded up to 16 B, + the up-to-16-B alignment skew and the
     // last 8-element vector read past the segment end
     const size_t lds = ((size_t)gpt * L * (dtype == AWQ_DTYPE_F32 ? 4 : 2) + 15) / 16 * 16 + 48;
-    const bool p1c = tuning().rg_p1 != 1;   // pass 1 by contiguous chunks (default) / by groups (A/B)
+    const bool p1c = tuning().rg_p1 == 2;   // pass 1 by groups (default) / evenly split runs (A/B)
 #define AWQ_RG_SPLIT(Fm, B, S, SP)                                                                                 \
     do {                                                                                                           \
         if (p1c)                                                                                                   \

@@ -640,7 +640,7 @@ template <int B> constexpr auto dq_batch4 = awq_dequant_batch_kernel<B, 4, 0>;
 template <int B> constexpr auto dq_batch8 = awq_dequant_batch_kernel<B, 8, 0>;
 template <int B> constexpr auto dq_batch4_run = awq_dequant_batch_kernel<B, 4, 4>;
 template <int B> constexpr auto dq_batch8_run = awq_dequant_batch_kernel<B, 8, 2>;
-constexpr int kDqDefault = 3;   // profiles/round3: see DESIGN.md §5 (dequantize_packed)
+constexpr int kDqDefault = 8;   // batched lanes in XCD runs: profiles/round3/dequant
 
 inline unsigned grid_for(int64_t work, int64_t per_block, int64_t cap) {
     int64_t b = (work + per_block - 1) / per_block;

@@ -43,10 +43,23 @@ constexpr int kGroup = 128;          // the benchmark's group size (BASELINE.jso
 // set 0.778 -> 0.803 of 8 TB/s from 8 -> 1; opt-125m 0.716 -> 0.737) — a finished wave's
 // slot is refilled one wave at a time instead of waiting for its workgroup's slowest wave
 constexpr int kWavesPerBlock = AWQ_WPB;
-// tiles per entry of the host-planned tensor table (include/awq_hip.h AWQ_BLOCK_TILES),
-// independent of the workgroup size: entry t / kTableTiles names the tensor of tile
-// kTableTiles * (t / kTableTiles)
+// tiles per entry of the host-planned tensor table (include/awq_hip.h AWQ_BLOCK_TILES).
+// One-wave workgroups are dealt round-robin over the 8 XCDs, so tile t runs on XCD t % 8;
+// an entry covers the 8 tiles of ONE XCD inside a 64-tile window (t0 + 8 j), and the two
+// entries of an XCD for windows 2k and 2k + 1 share a 128-B line, so each table line is
+// fetched by one XCD's L2 (entries of 8 consecutive tiles were fetched by all 8 L2s:
+// +2.3 % HBM reads on the 70B set, profiles/round3/r3k).
 constexpr int kTableTiles = AWQ_BLOCK_TILES;
+static_assert(AWQ_BLOCK_TILES == 8, "the XCD-interleaved table layout assumes 8 tiles per entry");
+__host__ __device__ inline int64_t table_index(int64_t t) {   // entry of tile t
+    return (t >> 7) * 16 + (t & 7) * 2 + ((t >> 6) & 1);
+}
+__host__ __device__ inline int64_t table_first_tile(int64_t b) {   // first tile of entry b
+    return (b >> 4) * 128 + (b & 1) * 64 + ((b & 15) >> 1);
+}
+__host__ __device__ inline int64_t table_entries(int64_t total_tiles) {
+    return (total_tiles + 127) / 128 * 16;
+}
 // One entry of the tensor table per kTableTiles tiles (awq_plan_block_tensor): everything a
 // wave needs to issue its tile's loads — the tensor's input, first tile and shape — in one
 // 64-B scalar load, so the loads no longer wait for a second, dependent load of the 80-B

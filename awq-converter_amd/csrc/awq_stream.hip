@@ -327,13 +327,17 @@ void submitter_main(Pipeline* P) {
             if (!P->hip_ok(hipEventSynchronize(P->ev_kern[b - c.nslots]), "waiting for a slot's kernels")) return;
             P->wait_slot += now_s() - t;
         }
+        const double t_h2d = now_s();
         if (B.bytes > 0 &&
             !P->hip_ok(hipMemcpyAsync((char*)c.dev_staging + (int64_t)B.slot * c.slot_bytes,
                                       (const char*)c.host_staging + (int64_t)B.slot * c.slot_bytes, (size_t)B.bytes,
                                       hipMemcpyHostToDevice, h2d), "H2D"))
             return;
         if (!P->hip_ok(hipEventRecord(P->ev_h2d[b], h2d), "event")) return;
-        if (!P->tr.empty()) P->tr[b * AWQ_STREAM_TRACE_FIELDS + 2] = now_s() - P->t0;
+        if (!P->tr.empty()) {
+            P->tr[b * AWQ_STREAM_TRACE_FIELDS + 2] = now_s() - P->t0;
+            P->tr[b * AWQ_STREAM_TRACE_FIELDS + 8] = now_s() - t_h2d;
+        }
         {
             std::lock_guard<std::mutex> g(P->mu);
             P->h2d_recorded = b;
@@ -350,9 +354,12 @@ void submitter_main(Pipeline* P) {
             char *hs = nullptr, *ds = nullptr;
             int64_t len = 0;
         } run[2];
+        double t_d2h = 0;
         auto flush = [&](Run& r) {
+            const double tc = now_s();
             if (r.len > 0 && !P->hip_ok(hipMemcpyAsync(r.hs, r.ds, (size_t)r.len, hipMemcpyDeviceToHost, d2h), "D2H"))
                 return false;
+            t_d2h += now_s() - tc;
             r.len = 0;
             return true;
         };
@@ -376,7 +383,10 @@ void submitter_main(Pipeline* P) {
         }
         if (!flush(run[0]) || !flush(run[1])) return;
         if (!P->hip_ok(hipEventRecord(P->ev_done[b], d2h), "event")) return;
-        if (!P->tr.empty()) P->tr[b * AWQ_STREAM_TRACE_FIELDS + 4] = now_s() - P->t0;
+        if (!P->tr.empty()) {
+            P->tr[b * AWQ_STREAM_TRACE_FIELDS + 4] = now_s() - P->t0;
+            P->tr[b * AWQ_STREAM_TRACE_FIELDS + 9] = t_d2h;
+        }
         {
             std::lock_guard<std::mutex> g(P->mu);
             P->done_recorded = b;
@@ -396,7 +406,7 @@ extern "C" {
 int64_t awq_stream_table_bytes(int64_t slot_bytes) {
     const int64_t descs = align_up((int64_t)sizeof(awq_tensor_desc) * AWQ_STREAM_MAX_BATCH_ITEMS, kAlign);
     // tensor tables: one 64-B entry per AWQ_BLOCK_TILES tiles of >= 4 KiB of input, per dtype group
-    const int64_t tables = 64 * (slot_bytes / 4096 / AWQ_BLOCK_TILES + 4 * 4) + 4 * 16;
+    const int64_t tables = 64 * (slot_bytes / 4096 / AWQ_BLOCK_TILES + 4 * 16) + 4 * 16;
     return align_up(descs + tables, 4096);
 }
 
@@ -513,6 +523,8 @@ int awq_stream_end(void* handle, awq_stream_stats* stats) {
         for (size_t b = 0; b < nt; ++b) {
             double* o = P->cfg.trace + b * AWQ_STREAM_TRACE_FIELDS;
             for (int k = 0; k < 5; ++k) o[k] = P->tr[b * AWQ_STREAM_TRACE_FIELDS + k];
+            o[8] = P->tr[b * AWQ_STREAM_TRACE_FIELDS + 8];
+            o[9] = P->tr[b * AWQ_STREAM_TRACE_FIELDS + 9];
             const hipEvent_t ev[3] = {P->ev_h2d[b], P->ev_kern[b], P->ev_done[b]};
             for (int k = 0; k < 3; ++k) {
                 float ms = -1.0f;

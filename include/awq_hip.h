@@ -162,10 +162,12 @@ int64_t awq_plan_ragged(awq_tensor_desc* descs_host, int n, int bits, int64_t gr
 #define AWQ_BLOCK_TILES 8
 
 /* HOST helper: the ragged launch's tensor table, one 64-B entry per AWQ_BLOCK_TILES tiles
- * (opaque to the caller: 16 int32 each): the input pointer, first tile and shape of the
- * tensor holding tile AWQ_BLOCK_TILES * b (so a wave issues its loads after one scalar load)
- * and its descriptor index, with bit 31 set when the entry's tiles span more than one
- * tensor (a wave then steps forward from there to its own).  Returns the number of int32
+ * (opaque to the caller: 16 int32 each; ceil(total_tiles / 128) * 16 entries): the input
+ * pointer, first tile and shape of the tensor holding the entry's first tile (so a wave
+ * issues its loads after one scalar load) and its descriptor index, with bit 31 set when
+ * the entry's tiles span more than one tensor (a wave then steps forward from there to its
+ * own).  An entry's tiles are the 8 tiles of one XCD in a 64-tile window (t0 + 8 j), so
+ * each 128-B line of the table is read by one XCD.  Returns the number of int32
  * written (< 0 on error: len too small, or block_tensor_host not 16-B aligned);
  * block_tensor_host = NULL with len = 0 returns the length needed without writing.
  * descs_host as planned by awq_plan_ragged (the pointers are the device pointers the
@@ -279,11 +281,12 @@ typedef struct awq_stream_config {
                                     first read began, last read ended, H2D enqueued, kernels
                                     enqueued, D2H enqueued (host clock); H2D done, kernels done,
                                     D2H done (HIP event clock, from an event on the H2D stream
-                                    recorded at start); batches past
-                                    trace_batches are not traced. */
+                                    recorded at start); seconds spent inside the H2D call and
+                                    inside the D2H calls; batches past trace_batches are not
+                                    traced. */
 } awq_stream_config;
 
-#define AWQ_STREAM_TRACE_FIELDS 8
+#define AWQ_STREAM_TRACE_FIELDS 10
 
 typedef struct awq_stream_stats {
     int64_t batches, pieces, bytes_read;

@@ -28,8 +28,9 @@ typedef struct awq_tuning {
                                 XCD-contiguous blocks, 4 / 5 four-output lanes without / with,
                                 6 / 7 batched four-output lanes (4 / 8 per lane), 8 / 9 the
                                 same in XCD runs */
-    int32_t rg_p1;           /* row-segment pass 1: 0 the default (contiguous chunks per lane, LDS
-                                merges), 1 by groups (2^k lanes per group, DPP merges) */
+    int32_t rg_p1;           /* row-segment pass 1: 0 / 1 by groups (2^k lanes per group, DPP
+                                merges), 2 evenly split runs (NT / groups lanes per group, LDS
+                                merges, parameters by one lane per group) */
     int32_t rg_p2;           /* row-segment pass 2: 0 the default, 1 the round-2 form */
 } awq_tuning;
 

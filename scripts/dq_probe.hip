@@ -1,0 +1,71 @@
+// dq_probe.hip — HBM ceiling of dequantize_packed's memory structure (not part of the library):
+// per four fp32 outputs (one 16-B store, 1 KiB per wave instruction) 2 B of packed words read
+// (4-bit: a dword shared by a lane pair) plus the row's scale / qzeros lines — a 1 : 8
+// read : write stream.  Variants: store only, and the 1 : 8 mix with U quads per lane (loads
+// issued first), the batched kernel's shape.  One JSON line per variant and size.
+//   hipcc -O3 --offload-arch=gfx950 scripts/dq_probe.hip -o /tmp/dq_probe && /tmp/dq_probe
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+
+typedef float f4 __attribute__((ext_vector_type(4)));
+
+// WR_ONLY: no loads.  Thread t of block b handles quads b * 256 U + 256 k + t, k < U.
+template <int U, bool WR_ONLY>
+__global__ __launch_bounds__(256) void dq_mix_kernel(const uint32_t* __restrict__ words, float* __restrict__ out,
+                                                     int64_t quads) {
+    const int64_t q0 = (int64_t)blockIdx.x * (256 * U) + threadIdx.x;
+    uint32_t w[U];
+#pragma unroll
+    for (int k = 0; k < U; ++k) {
+        const int64_t q = q0 + 256 * k;
+        w[k] = WR_ONLY ? (uint32_t)q : __builtin_nontemporal_load(words + min(q, quads - 1) / 2);
+    }
+#pragma unroll
+    for (int k = 0; k < U; ++k) {
+        const int64_t q = q0 + 256 * k;
+        if (q >= quads) break;
+        const uint32_t v = w[k] >> (16 * (int)(q & 1));
+        const f4 o = {(float)(v & 15u), (float)((v >> 4) & 15u), (float)((v >> 8) & 15u), (float)((v >> 12) & 15u)};
+        __builtin_nontemporal_store(o, (f4*)(out + 4 * q));
+    }
+}
+
+template <int U, bool WR_ONLY>
+static void run(const char* name, const uint32_t* words, float* out, int64_t elems, hipEvent_t a, hipEvent_t b) {
+    const int64_t quads = elems / 4;
+    const dim3 grid((unsigned)((quads + 256 * U - 1) / (256 * U)));
+    for (int i = 0; i < 3; ++i) hipLaunchKernelGGL((dq_mix_kernel<U, WR_ONLY>), grid, dim3(256), 0, 0, words, out, quads);
+    const int iters = 20;
+    (void)hipEventRecord(a, 0);
+    for (int i = 0; i < iters; ++i) hipLaunchKernelGGL((dq_mix_kernel<U, WR_ONLY>), grid, dim3(256), 0, 0, words, out, quads);
+    (void)hipEventRecord(b, 0);
+    (void)hipEventSynchronize(b);
+    float ms = 0;
+    (void)hipEventElapsedTime(&ms, a, b);
+    const double us = ms * 1e3 / iters;
+    const double bytes = (double)elems * 4 + (WR_ONLY ? 0.0 : (double)elems / 2);
+    printf("{\"probe\": \"%s\", \"U\": %d, \"elements\": %lld, \"us\": %.1f, \"GBs\": %.1f}\n", name, U,
+           (long long)elems, us, bytes / us / 1e3);
+}
+
+int main() {
+    const int64_t sizes[] = {14336LL * 4096, 128256LL * 4096};
+    for (int64_t elems : sizes) {
+        uint32_t* words;
+        float* out;
+        if (hipMalloc(&words, elems / 2) != hipSuccess || hipMalloc(&out, elems * 4) != hipSuccess) return 1;
+        (void)hipMemset(words, 0x5A, elems / 2);
+        hipEvent_t a, b;
+        (void)hipEventCreate(&a);
+        (void)hipEventCreate(&b);
+        run<4, true>("store_only", words, out, elems, a, b);
+        run<8, true>("store_only", words, out, elems, a, b);
+        run<1, false>("read1_write8", words, out, elems, a, b);
+        run<4, false>("read1_write8", words, out, elems, a, b);
+        run<8, false>("read1_write8", words, out, elems, a, b);
+        (void)hipFree(words);
+        (void)hipFree(out);
+    }
+    return 0;
+}

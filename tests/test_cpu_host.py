@@ -56,21 +56,34 @@ def test_host_helpers_without_gpu():
     # 1024 rows x G=32 -> 16-group tiles -> 2048; G=6 (even) -> byte tiles: 16 flat groups
     assert d[0].tile_count == 2048 and d[1].tile_count == 1 and d[2].tile_count == 19
     assert total == 2048 + 1 + 19 and d[2].tile_begin == 2049
-    # tensor table: entry b (64 B = 16 int32) covers tiles 8b..8b+7 (AWQ_BLOCK_TILES): the
+    # tensor table: entry b (64 B = 16 int32) covers the 8 tiles t0, t0 + 8, ..., t0 + 56 of
+    # one XCD (tile t runs on XCD t % 8) inside a 64-tile window, the two windows of a
+    # 128-tile pair side by side (index (t >> 7) * 16 + (t & 7) * 2 + ((t >> 6) & 1)): the
     # tensor's input pointer, first tile, rows, K, then its index (bit 31: the entry spans)
     arr = (_hip.TensorDesc * 3)(*d)
-    assert lib.awq_plan_block_tensor(arr, 3, total, None, 0) == 259 * 16
-    tab = torch.full((300 * 16,), -7, dtype=torch.int32)
-    assert lib.awq_plan_block_tensor(arr, 3, total, ctypes.c_void_p(tab.data_ptr()), 300 * 16) == 259 * 16
-    e = tab[:259 * 16].view(259, 16)
-    idx = e[:, 8]
-    # block 256 = tiles 2048 (t1), 2049-2055 (t2): spans -> bit 31
-    assert idx[:256].eq(0).all() and idx[256].item() == (1 | -2**31) and idx[257:259].eq(2).all()
-    q = e.view(torch.int64)                      # [259, 8]: w, tile_begin, rows, K, ...
-    for b, t in ((0, 0), (255, 0), (257, 2)):
-        assert q[b, 0].item() == d[t].w and q[b, 1].item() == arr[t].tile_begin
-        assert q[b, 2].item() == d[t].rows and q[b, 3].item() == d[t].K
-    assert tab[259 * 16:].eq(-7).all()
+    n_ent = -(-total // 128) * 16
+    assert lib.awq_plan_block_tensor(arr, 3, total, None, 0) == n_ent * 16
+    tab = torch.full(((n_ent + 20) * 16,), -7, dtype=torch.int32)
+    assert lib.awq_plan_block_tensor(arr, 3, total, ctypes.c_void_p(tab.data_ptr()), (n_ent + 20) * 16) == n_ent * 16
+    e = tab[:n_ent * 16].view(n_ent, 16)
+    q = e.view(torch.int64)                      # [n, 8]: w, tile_begin, rows, K, ...
+    begins = [arr[i].tile_begin for i in range(3)]
+
+    def owner(t):
+        return max(i for i in range(3) if begins[i] <= t)
+    for b in range(n_ent):
+        t0 = min((b >> 4) * 128 + (b & 1) * 64 + ((b & 15) >> 1), total - 1)
+        last = max(t0, min(t0 + 56, total - 1))
+        cur = owner(t0)
+        spans = owner(last) != cur
+        assert e[b, 8].item() == (cur | (-2**31 if spans else 0)), b
+        assert q[b, 0].item() == d[cur].w and q[b, 1].item() == begins[cur]
+        assert q[b, 2].item() == d[cur].rows and q[b, 3].item() == d[cur].K
+    for t in range(total):                       # every tile's entry starts at or before it
+        b = (t >> 7) * 16 + (t & 7) * 2 + ((t >> 6) & 1)
+        first = (b >> 4) * 128 + (b & 1) * 64 + ((b & 15) >> 1)
+        assert first <= t and (t - first) % 8 == 0 and t - first <= 56
+    assert tab[n_ent * 16:].eq(-7).all()
     assert lib.awq_plan_block_tensor(arr, 3, total, ctypes.c_void_p(tab.data_ptr()), 100) < 0
     # G odd at 4 bits -> word tiles: K=384 (G=3) -> 5 rows (15 groups) per tile
     d = [_hip.TensorDesc(4096 * 16, 11, 384, 0, 0, 2 * 4096, 0, 0, 0, 0)]

@@ -137,11 +137,12 @@ def test_rowgroup_groups_per_tile_override(dtype, shape, gs, gpt):
             _assert_parity(rand(shape, gpt + gs + bits, 0.5, dtype), gs, bits, sym)
 
 
-@pytest.mark.parametrize("dtype,shape,gs", CASES[::3], ids=str)
-def test_rowgroup_pass1_by_groups(dtype, shape, gs):
-    """The round-2 pass 1 (tuning rg_p1=1: 2^k lanes per group, DPP merges) against the same
-    oracle as the default contiguous-chunk pass 1 (LDS ds_max / ds_min merges)."""
+@pytest.mark.parametrize("dtype,shape,gs", CASES, ids=str)
+def test_rowgroup_pass1_split_runs(dtype, shape, gs):
+    """Pass 1 with the tile's lanes split evenly over its groups (tuning rg_p1=2: NT / groups
+    lanes per group, LDS ds_max / ds_min merges, parameters by one lane per group) against
+    the same oracle as the default by-groups pass 1."""
     from awq_quantizer import _hip
-    with _hip.tuning(rg_p1=1):
+    with _hip.tuning(rg_p1=2):
         for bits, sym in ((4, False), (8, True)):
             _assert_parity(rand(shape, gs + bits + 7, 0.5, dtype), gs, bits, sym)

@@ -28,7 +28,7 @@ pytestmark = pytest.mark.skipif(
 
 
 def _build(target):
-    r = subprocess.run(["make", "-s", "-C", NATIVE, os.path.join(OUT, target)],
+    r = subprocess.run(["make", "-s", "-C", NATIVE, f"OUT={OUT}", os.path.join(OUT, target)],
                        capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stdout[-4000:] + r.stderr[-4000:]
     return os.path.join(OUT, target)

@@ -51,9 +51,9 @@ class StreamConfig(ctypes.Structure):
                 ("h2d_stream", _P), ("d2h_stream", _P), ("trace", _P)]
 
 
-STREAM_TRACE_FIELDS = 10   # AWQ_STREAM_TRACE_FIELDS
+STREAM_TRACE_FIELDS = 14   # AWQ_STREAM_TRACE_FIELDS
 STREAM_TRACE_NAMES = ("read_first", "read_last", "h2d_enq", "kern_enq", "d2h_enq", "h2d_done", "kern_done",
-                      "d2h_done", "h2d_call", "d2h_call")
+                      "d2h_done", "h2d_call", "d2h_call", "plan", "table_upload", "ragged_launch", "other_launch")
 
 
 class StreamStats(ctypes.Structure):

@@ -314,6 +314,7 @@ class ChunkWriter:
         self.closed = False
         self.error: Optional[BaseException] = None
         self.cv = threading.Condition()
+        self.times: List[Tuple[float, float, float]] = []   # per chunk: submitted, started, ended (time.time)
         os.makedirs(output_dir, exist_ok=True)
         self.thread = threading.Thread(target=self._run, daemon=True)
         self.thread.start()
@@ -342,11 +343,10 @@ class ChunkWriter:
                     t2c[name] = c
                     n_ok += 1
                     if len(chunk) == self.size:
-                        futs.append(pool.submit(_write_chunk, chunk, self.dir, c, self.st, self.logger,
-                                                stem=self.stem))
+                        futs.append(pool.submit(self._timed_write, chunk, c, time.time()))
                         chunk, c = {}, c + 1
                 if chunk:
-                    futs.append(pool.submit(_write_chunk, chunk, self.dir, c, self.st, self.logger, stem=self.stem))
+                    futs.append(pool.submit(self._timed_write, chunk, c, time.time()))
                     c += 1
                 for f in futs:
                     f.result()
@@ -355,6 +355,11 @@ class ChunkWriter:
                 _write_metadata(self.dir, c, self.size, t2c, self.st, n_ok, qparams, self.logger)
         except BaseException as e:  # noqa: BLE001  (reported by close())
             self.error = e
+
+    def _timed_write(self, chunk, c: int, t_submit: float) -> None:
+        t0 = time.time()
+        _write_chunk(chunk, self.dir, c, self.st, self.logger, stem=self.stem)
+        self.times.append((t_submit, t0, time.time()))
 
     def close(self) -> None:
         """Every producer has finished: unfinished tensors count as failed; wait for the writes."""
@@ -1024,7 +1029,14 @@ def main(argv: Optional[List[str]] = None) -> int:
                 save_autoawq(quantized, loader, passthrough, args.output_dir, args, logger,
                              failed=[i for i in ordered if i.name not in quantized])
             elif writer is not None:
+                t_close = time.time()
                 writer.close()
+                if writer.times:
+                    TIMINGS["writer"] = {"chunks": len(writer.times), "close_wait_s": round(time.time() - t_close, 4),
+                                         "write_s_sum": round(sum(e - b for _, b, e in writer.times), 4),
+                                         "write_s_max": round(max(e - b for _, b, e in writer.times), 4),
+                                         "last_submit_to_end_s": round(max(e for _, _, e in writer.times)
+                                                                       - max(a for a, _, _ in writer.times), 4)}
             else:
                 save_model_in_chunks(quantized, args.output_dir, chunk_size=args.chunk_size,
                                      use_safetensors=args.save_safetensors, logger=logger)

@@ -384,14 +384,42 @@ __device__ __forceinline__ GroupParams params_from_range(float mn, float mx) {
     return p;
 }
 
+// The 8 fields of a lane packed from their unrounded values u: v_cvt_pk_u8_f32 rounds to
+// nearest even and saturates to [0, 255] (scripts/cvt_probe.hip, every tie and edge on
+// gfx950), so an 8-bit field is ONE conversion of u (= clamp(rint(u), 0, 255), the
+// reference's round + clamp for qmin = 0 and, sym, for the field q + 128); a 4-bit field
+// is a v_med3 clamp to [0, 15] then the conversion (rint(clamp(u)) == clamp(rint(u)) for
+// integer bounds), the even elements' bytes OR-ed with the odd elements' shifted by 4.
+template <int BITS>
+__device__ __forceinline__ void pack8_cvt(const float (&u)[8], uint32_t& w0, uint32_t& w1) {
+    if (BITS == 4) {
+        uint32_t a = 0, b = 0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            a = __builtin_amdgcn_cvt_pk_u8_f32(__builtin_amdgcn_fmed3f(u[2 * i], 0.0f, 15.0f), i, a);
+            b = __builtin_amdgcn_cvt_pk_u8_f32(__builtin_amdgcn_fmed3f(u[2 * i + 1], 0.0f, 15.0f), i, b);
+        }
+        w0 = a | (b << 4);
+        w1 = 0;
+    } else {
+        uint32_t a = 0, b = 0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            a = __builtin_amdgcn_cvt_pk_u8_f32(u[i], i, a);
+            b = __builtin_amdgcn_cvt_pk_u8_f32(u[4 + i], i, b);
+        }
+        w0 = a;
+        w1 = b;
+    }
+}
+
 // Quantize the 8 values of one lane (awq.py:245-248) for a group with a positive finite
 // scale and pack them: 4-bit -> w.x, 8-bit -> (w.x, w.y).  Field value = q - qmin.
 template <typename F, int BITS, bool SYM, bool PLAIN = false>
 __device__ __forceinline__ u2v quant8_fast(const Chunk<F::NW>& v, float r, float z, float s) {
-    constexpr float QR = (float)((1 << BITS) - 1);
     constexpr float HALF = (float)(1 << (BITS - 1));
     const float zf = F::as_fmt(z);
-    float q[8];
+    float q[8];   // the field before rounding: clamp + RNE are the pack's v_cvt_pk_u8_f32
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         // RN(x / s)
@@ -409,29 +437,17 @@ __device__ __forceinline__ u2v quant8_fast(const Chunk<F::NW>& v, float r, float
             u0 = F::rn(t0 + zf);                                     // RN(x/s + z)
             u1 = F::rn(t1 + zf);
         }
-        q[2 * i] = __builtin_fminf(__builtin_fmaxf(__builtin_rintf(u0), 0.0f), QR);
-        q[2 * i + 1] = __builtin_fminf(__builtin_fmaxf(__builtin_rintf(u1), 0.0f), QR);
+        q[2 * i] = u0;
+        q[2 * i + 1] = u1;
     }
+    uint32_t w0, w1;
+    pack8_cvt<BITS>(q, w0, w1);
     u2v w;
-    if (BITS == 4) {
-        uint32_t acc = 0;
-#pragma unroll
-        for (int i = 0; i < 4; ++i)   // nibble pair as one exact float in [0, 255] -> byte i
-            acc = __builtin_amdgcn_cvt_pk_u8_f32(__builtin_fmaf(q[2 * i + 1], 16.0f, q[2 * i]), i, acc);
-        w.x = acc;
-        w.y = 0;
-    } else {
-        uint32_t a = 0, b = 0;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            a = __builtin_amdgcn_cvt_pk_u8_f32(q[i], i, a);
-            b = __builtin_amdgcn_cvt_pk_u8_f32(q[4 + i], i, b);
-        }
-        w.x = a;
-        w.y = b;
-    }
+    w.x = w0;
+    w.y = w1;
     return w;
 }
+
 
 // Same with the reference's NaN/inf semantics (groups whose scale is 0, inf or NaN), with
 // a true IEEE division per element.
@@ -942,17 +958,23 @@ struct RgSlot {
     __device__ static float dec(uint32_t v) { return F::kBytes == 2 ? F::dec(v) : __uint_as_float(v); }
 };
 
-// packed field (q - qmin) of one element of a group with a positive finite scale
+// packed field (q - qmin) of one element of a group with a positive finite scale, before
+// the round + clamp (pack8_cvt / field_q)
 template <typename F, int BITS, bool SYM, bool PLAIN>
 __device__ __forceinline__ float field1_fast(float x, float r, float z, float s) {
-    constexpr float QR = (float)((1 << BITS) - 1);
     constexpr float HALF = (float)(1 << (BITS - 1));
     const float t = PLAIN ? F::quot_plain(x, r) : F::quot(x, s, r);
     float u;
     if (SYM && F::kWide) u = __builtin_rintf(t) + HALF;
     else if (SYM) u = t + HALF;
     else u = F::rn(t + F::as_fmt(z));
-    return __builtin_fminf(__builtin_fmaxf(__builtin_rintf(u), 0.0f), QR);
+    return u;
+}
+
+// the field's value: clamp(rint(u), 0, 2^BITS - 1)
+template <int BITS>
+__device__ __forceinline__ float field_q(float u) {
+    return __builtin_fminf(__builtin_fmaxf(__builtin_rintf(u), 0.0f), (float)((1 << BITS) - 1));
 }
 
 // the same for 8 bf16 elements, multiply and add as packed f32 pairs (v_pk_mul_f32 /
@@ -960,7 +982,6 @@ __device__ __forceinline__ float field1_fast(float x, float r, float z, float s)
 template <int BITS, bool SYM>
 __device__ __forceinline__ void field8_bf16(const float (&x)[8], const float (&r)[8], const float (&z)[8],
                                             float (&q)[8]) {
-    constexpr float QR = (float)((1 << BITS) - 1);
     constexpr float HALF = (float)(1 << (BITS - 1));
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -973,8 +994,8 @@ __device__ __forceinline__ void field8_bf16(const float (&x)[8], const float (&r
             const f2 a = t + (f2){z[2 * i], z[2 * i + 1]};
             u = (f2){rn_bf16(a.x), rn_bf16(a.y)};
         }
-        q[2 * i] = __builtin_fminf(__builtin_fmaxf(__builtin_rintf(u.x), 0.0f), QR);
-        q[2 * i + 1] = __builtin_fminf(__builtin_fmaxf(__builtin_rintf(u.y), 0.0f), QR);
+        q[2 * i] = u.x;
+        q[2 * i + 1] = u.y;
     }
 }
 
@@ -1412,19 +1433,9 @@ __global__ __launch_bounds__(128) void awq_rowgroup_kernel(const void* __restric
             }
             if (tensor_q) {
 #pragma unroll
-                for (int i = 0; i < 8; ++i) qv[i] = (int32_t)q[i] + QMIN;
+                for (int i = 0; i < 8; ++i) qv[i] = (int32_t)field_q<BITS>(q[i]) + QMIN;
             }
-            if (BITS == 4) {
-#pragma unroll
-                for (int i = 0; i < 4; ++i)   // nibble pair as one exact float in [0, 255] -> byte i
-                    word0 = __builtin_amdgcn_cvt_pk_u8_f32(__builtin_fmaf(q[2 * i + 1], 16.0f, q[2 * i]), i, word0);
-            } else {
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    word0 = __builtin_amdgcn_cvt_pk_u8_f32(q[i], i, word0);
-                    word1 = __builtin_amdgcn_cvt_pk_u8_f32(q[4 + i], i, word1);
-                }
-            }
+            pack8_cvt<BITS>(q, word0, word1);
         } else {                                          // a group with scale 0 / inf / NaN: IEEE division
             constexpr int QMAX = SYM ? (1 << (BITS - 1)) - 1 : (1 << BITS) - 1;
             const int nv = n_el - e0c;

@@ -230,8 +230,11 @@ bool ragged_ok(const awq_tensor_desc& d, int dtype, int64_t gs) {
            (!d.qzeros || aligned(d.qzeros, 4)) && (!d.scales || aligned(d.scales, 2));
 }
 
-bool quantize_batch(Pipeline& P, const Batch& B, hipStream_t cs) {
+// ph (trace): seconds in host planning, the table uploads, the ragged launches, the
+// per-tensor launches
+bool quantize_batch(Pipeline& P, const Batch& B, hipStream_t cs, double (&ph)[4]) {
     const awq_stream_config& c = P.cfg;
+    double tp = now_s();
     const int64_t gs = c.group_size;
     const char* dev_slot = (const char*)c.dev_staging + (int64_t)B.slot * c.slot_bytes;
     const int64_t tb = awq_stream_table_bytes(c.slot_bytes);
@@ -279,6 +282,8 @@ bool quantize_batch(Pipeline& P, const Batch& B, hipStream_t cs) {
         toff = align_up(toff + need * 4, 16);
         groups.push_back(g);
     }
+    ph[0] = now_s() - tp;
+    tp = now_s();
     if (!groups.empty()) {   // descriptors + tables in one copy, stream-ordered before the launches
         if (!P.hip_ok(hipMemcpyAsync(dtab, htab, (size_t)(nd * (int64_t)sizeof(awq_tensor_desc)),
                                      hipMemcpyHostToDevice, cs), "descriptor upload"))
@@ -287,6 +292,8 @@ bool quantize_batch(Pipeline& P, const Batch& B, hipStream_t cs) {
                                      hipMemcpyHostToDevice, cs), "table upload"))
             return false;
     }
+    ph[1] = now_s() - tp;
+    tp = now_s();
     for (const Group& g : groups) {
         const int rc = awq_quantize_ragged((const awq_tensor_desc*)dtab + g.first, g.n, g.tiles,
                                            g.table_len ? (const int32_t*)(dtab + g.table_off) : nullptr, g.dtype,
@@ -296,6 +303,8 @@ bool quantize_batch(Pipeline& P, const Batch& B, hipStream_t cs) {
             return false;
         }
     }
+    ph[2] = now_s() - tp;
+    tp = now_s();
     for (const auto& r : rest) {
         const awq_tensor_desc& d = r.first;
         const int rc = awq_quantize_groups_ex(d.w, r.second, d.rows, d.K, (int32_t)gs, c.bits, c.symmetric, 0,
@@ -305,6 +314,7 @@ bool quantize_batch(Pipeline& P, const Batch& B, hipStream_t cs) {
             return false;
         }
     }
+    ph[3] = now_s() - tp;
     return true;
 }
 
@@ -344,7 +354,10 @@ void submitter_main(Pipeline* P) {
         }
         P->cv.notify_all();
         if (!P->hip_ok(hipStreamWaitEvent(cs, P->ev_h2d[b], 0), "stream wait")) return;
-        if (!quantize_batch(*P, B, cs)) return;
+        double ph[4] = {0, 0, 0, 0};
+        if (!quantize_batch(*P, B, cs, ph)) return;
+        if (!P->tr.empty())
+            for (int k = 0; k < 4; ++k) P->tr[b * AWQ_STREAM_TRACE_FIELDS + 10 + k] = ph[k];
         if (!P->hip_ok(hipEventRecord(P->ev_kern[b], cs), "event")) return;
         if (!P->tr.empty()) P->tr[b * AWQ_STREAM_TRACE_FIELDS + 3] = now_s() - P->t0;
         if (!P->hip_ok(hipStreamWaitEvent(d2h, P->ev_kern[b], 0), "stream wait")) return;
@@ -523,8 +536,7 @@ int awq_stream_end(void* handle, awq_stream_stats* stats) {
         for (size_t b = 0; b < nt; ++b) {
             double* o = P->cfg.trace + b * AWQ_STREAM_TRACE_FIELDS;
             for (int k = 0; k < 5; ++k) o[k] = P->tr[b * AWQ_STREAM_TRACE_FIELDS + k];
-            o[8] = P->tr[b * AWQ_STREAM_TRACE_FIELDS + 8];
-            o[9] = P->tr[b * AWQ_STREAM_TRACE_FIELDS + 9];
+            for (int k = 8; k < AWQ_STREAM_TRACE_FIELDS; ++k) o[k] = P->tr[b * AWQ_STREAM_TRACE_FIELDS + k];
             const hipEvent_t ev[3] = {P->ev_h2d[b], P->ev_kern[b], P->ev_done[b]};
             for (int k = 0; k < 3; ++k) {
                 float ms = -1.0f;

@@ -282,11 +282,12 @@ typedef struct awq_stream_config {
                                     enqueued, D2H enqueued (host clock); H2D done, kernels done,
                                     D2H done (HIP event clock, from an event on the H2D stream
                                     recorded at start); seconds spent inside the H2D call and
-                                    inside the D2H calls; batches past trace_batches are not
-                                    traced. */
+                                    inside the D2H calls; seconds of the batch's host planning,
+                                    table uploads, ragged launches and per-tensor launches;
+                                    batches past trace_batches are not traced. */
 } awq_stream_config;
 
-#define AWQ_STREAM_TRACE_FIELDS 10
+#define AWQ_STREAM_TRACE_FIELDS 14
 
 typedef struct awq_stream_stats {
     int64_t batches, pieces, bytes_read;

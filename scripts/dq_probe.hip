@@ -49,6 +49,58 @@ static void run(const char* name, const uint32_t* words, float* out, int64_t ele
            (long long)elems, us, bytes / us / 1e3);
 }
 
+
+// WIDE: a wave's 512 quads need 1 KiB of packed words = ONE 16-B load per lane.  LDS = 1:
+// the words go through a per-wave LDS slice, quad k * 64 + lane reads its word back
+// (ds_read_b32) and every store instruction covers 1 KiB contiguous; LDS = 0: the lane
+// converts its own 4 words (8 quads = 128 B of output, 8 stores at a 128-B lane stride).
+template <bool LDS>
+__global__ __launch_bounds__(256) void dq_wide_kernel(const uint32_t* __restrict__ words, float* __restrict__ out,
+                                                      int64_t quads) {
+    __shared__ uint32_t slice[4][256];
+    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int64_t q0 = ((int64_t)blockIdx.x * 4 + wid) * 512;     // the wave's first quad
+    if (q0 >= quads) return;
+    typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+    const u4 w4 = __builtin_nontemporal_load((const u4*)(words + q0 / 2) + lane);
+    if (LDS) {
+        *(u4*)&slice[wid][4 * lane] = w4;
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const int qq = k * 64 + lane;
+            const uint32_t v = slice[wid][qq >> 1] >> (16 * (qq & 1));
+            const f4 o = {(float)(v & 15u), (float)((v >> 4) & 15u), (float)((v >> 8) & 15u), (float)((v >> 12) & 15u)};
+            __builtin_nontemporal_store(o, (f4*)(out + 4 * (q0 + qq)));
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const uint32_t v = w4[k >> 1] >> (16 * (k & 1));
+            const f4 o = {(float)(v & 15u), (float)((v >> 4) & 15u), (float)((v >> 8) & 15u), (float)((v >> 12) & 15u)};
+            __builtin_nontemporal_store(o, (f4*)(out + 4 * (q0 + 8 * lane + k)));
+        }
+    }
+}
+
+template <bool LDS>
+static void run_wide(const char* name, const uint32_t* words, float* out, int64_t elems, hipEvent_t a, hipEvent_t b) {
+    const int64_t quads = elems / 4;
+    const dim3 grid((unsigned)((quads + 2047) / 2048));
+    for (int i = 0; i < 3; ++i) hipLaunchKernelGGL((dq_wide_kernel<LDS>), grid, dim3(256), 0, 0, words, out, quads);
+    const int iters = 20;
+    (void)hipEventRecord(a, 0);
+    for (int i = 0; i < iters; ++i) hipLaunchKernelGGL((dq_wide_kernel<LDS>), grid, dim3(256), 0, 0, words, out, quads);
+    (void)hipEventRecord(b, 0);
+    (void)hipEventSynchronize(b);
+    float ms = 0;
+    (void)hipEventElapsedTime(&ms, a, b);
+    const double us = ms * 1e3 / iters;
+    printf("{\"probe\": \"%s\", \"elements\": %lld, \"us\": %.1f, \"GBs\": %.1f}\n", name, (long long)elems, us,
+           ((double)elems * 4 + (double)elems / 2) / us / 1e3);
+}
+
 int main() {
     const int64_t sizes[] = {14336LL * 4096, 128256LL * 4096};
     for (int64_t elems : sizes) {
@@ -64,6 +116,8 @@ int main() {
         run<1, false>("read1_write8", words, out, elems, a, b);
         run<4, false>("read1_write8", words, out, elems, a, b);
         run<8, false>("read1_write8", words, out, elems, a, b);
+        run_wide<true>("wide_load_lds", words, out, elems, a, b);
+        run_wide<false>("wide_load_lane_rows", words, out, elems, a, b);
         (void)hipFree(words);
         (void)hipFree(out);
     }

@@ -28,6 +28,7 @@ import argparse
 import ctypes
 import json
 import logging
+import math
 import os
 import sys
 import threading
@@ -551,16 +552,17 @@ def quantize_stream_native(loader, infos: List[TensorInfo], quantizer: AWQQuanti
     # dtype (torch.save stores a storage once per file, but only under one dtype) with the
     # same relative layout, so adjacent D2H ranges merge
     kinds = (torch.int32, torch.float16)
+    es_of = {torch.int32: 4, torch.float16: 2}
+    per16 = {dt: 16 // es for dt, es in es_of.items()}   # elements per 16 B
     lay, dev_total = [], {dt: 0 for dt in kinds}
     seg_size = {}
     for info, rows, K in items:
         seg = chunk_of.get(info.name, 0) if chunk_of else len(lay) // 16
         fields, size = [], {dt: 0 for dt in kinds}
         for f, shp, dt in _out_fields(info, rows, K, gs, bits, packed):
-            n = int(torch.Size(shp).numel())
+            n = math.prod(shp)
             fields.append((f, shp, dt, size[dt], n))
-            size[dt] += -(-n * torch.empty((), dtype=dt).element_size() // 16) * 16 // torch.empty(
-                (), dtype=dt).element_size()
+            size[dt] += -(-n // per16[dt]) * per16[dt]
         ss = seg_size.setdefault(seg, {dt: 0 for dt in kinds})
         lay.append((fields, size, dict(dev_total), seg, dict(ss)))
         for dt in kinds:
@@ -571,19 +573,20 @@ def quantize_stream_native(loader, infos: List[TensorInfo], quantizer: AWQQuanti
                                        for s, n in seg_size.items()}
     lib = _hip.load_library()
     arr = (_hip.StreamItem * max(1, len(items)))()
+    dptr = {dt: arena[dt].data_ptr() for dt in kinds}
+    hptr = {} if keep_on_device else {sg: {dt: h[dt].data_ptr() for dt in kinds} for sg, h in hosts.items()}
+    i32, f16 = kinds
     for k, ((info, rows, K), (fields, size, doff, seg, hoff)) in enumerate(zip(items, lay)):
         fd, at = loader.data_location(info)
         it = arr[k]
         it.fd, it.dtype, it.offset = fd, _hip.AWQ_DTYPE[info.dtype], at
         it.rows, it.K = rows, K
         for f, _, dt, off, _ in fields:
-            setattr(it, _STREAM_PTR_FIELD[f], arena[dt].data_ptr() + (doff[dt] + off) * arena[dt].element_size())
-        for dt, (dvf, hf, nf) in zip(kinds, (("dev_out", "host_out", "out_bytes"),
-                                            ("dev_out2", "host_out2", "out_bytes2"))):
-            es = arena[dt].element_size()
-            setattr(it, dvf, arena[dt].data_ptr() + doff[dt] * es)
-            setattr(it, nf, size[dt] * es)
-            setattr(it, hf, None if keep_on_device else hosts[seg][dt].data_ptr() + hoff[dt] * es)
+            setattr(it, _STREAM_PTR_FIELD[f], dptr[dt] + (doff[dt] + off) * es_of[dt])
+        it.dev_out, it.out_bytes = dptr[i32] + doff[i32] * 4, size[i32] * 4
+        it.dev_out2, it.out_bytes2 = dptr[f16] + doff[f16] * 2, size[f16] * 2
+        if not keep_on_device:
+            it.host_out, it.host_out2 = hptr[seg][i32] + hoff[i32] * 4, hptr[seg][f16] + hoff[f16] * 2
     total_in = sum(i.nbytes for i, _, _ in items)
     slot = slot_bytes or STREAM_OPTS.get("slot_bytes") or min(256 << 20, max(32 << 20, total_in // 8))
     slot = -(-slot // 4096) * 4096

@@ -297,6 +297,117 @@ __global__ __launch_bounds__(256) void awq_generic_span_reg_kernel(const double*
     }
 }
 
+// fp64 RTN for any other group size 2 <= L with the span in <= 16 KiB (4-bit: L <= 256,
+// 8-bit: L <= 512): one one-wave workgroup per span (PER groups of a row), the span staged in
+// LDS with every load of a batch in flight (8 per lane), then
+//   pass 1  P = 64 / PER lanes per group (8 at 4-bit), each over an even share of the
+//           group's elements, min / max / NaN merged over the P lanes by DPP moves (in-row);
+//           the group's (s, z) by the reference arithmetic (group_params), one lane per group
+//           storing scale / zero point;
+//   pass 2  lane = one qweight word (PER consecutive elements): each element's group from an
+//           exact float index (e + 0.5) * RN(1/L) (e < 2^13), its (s, z) from LDS, the IEEE
+//           fp64 quantize (quant1), the word assembled in the lane — no cross-lane OR.
+// The strided span (awq_generic_kernel) walks a wave's groups one after another with a
+// 64-lane butterfly each; here every group reduces at once and the quantize pass reads LDS.
+template <int PER>
+__global__ __launch_bounds__(64) void awq_f64_span_lds_kernel(const double* __restrict__ w, int64_t rows, int64_t K,
+                                                              int64_t L, float invL, int qmin, int qmax, int sym,
+                                                              uint32_t nan_code, int32_t* __restrict__ tensor_q,
+                                                              uint16_t* __restrict__ scales,
+                                                              int32_t* __restrict__ zeros,
+                                                              int32_t* __restrict__ qweight,
+                                                              int32_t* __restrict__ qzeros) {
+    constexpr int BITS = 32 / PER, P = 64 / PER;
+    constexpr uint32_t MASK = (1u << BITS) - 1u;
+    extern __shared__ double st[];                    // PER * L doubles
+    __shared__ double sp_s[PER], sp_z[PER];
+    const int lane = threadIdx.x;
+    const int64_t G = (K + L - 1) / L;
+    const int64_t SP = (G + PER - 1) / PER;
+    const int64_t wpr = (K + PER - 1) / PER;
+    const int64_t si = blockIdx.x;
+    const int64_t r = si / SP, sp = si - r * SP;
+    const int64_t g0 = sp * PER;
+    const int64_t span0 = g0 * L;
+    const int ng = (int)min((int64_t)PER, G - g0);
+    const int Li = (int)L;
+    const int n = (int)min((int64_t)ng * L, K - span0);   // the row's elements in the span
+    const int nz = ng * Li;                                 // + the padded tail group's zeros
+    const double* src = w + r * K + span0;
+    for (int e0 = 0; e0 < nz; e0 += 8 * 64) {
+        double v[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const int e = e0 + 64 * k + lane;
+            v[k] = e < n ? __builtin_nontemporal_load(src + e) : 0.0;
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const int e = e0 + 64 * k + lane;
+            if (e < nz) st[e] = v[k];
+        }
+    }
+    __syncthreads();
+    // ---- pass 1 ----
+    const int grp = lane / P, j = lane % P;
+    const int C = (Li + P - 1) / P;
+    const int cb = min(j * C, Li), ce = min(cb + C, Li);
+    double mn = INFINITY, mx = -INFINITY;
+    uint32_t nan = 0;
+    if (grp < ng) {
+        const double* gs = st + grp * Li;
+        for (int i = cb; i < ce; ++i) {
+            const double t = gs[i];
+            nan |= (t != t);
+            mn = t < mn ? t : mn;
+            mx = t > mx ? t : mx;
+        }
+    }
+#define AWQ_F64_LEVEL(CTRL)                                   \
+    {                                                         \
+        const double a = dpp_d<CTRL>(mn), b = dpp_d<CTRL>(mx); \
+        mn = a < mn ? a : mn;                                 \
+        mx = b > mx ? b : mx;                                 \
+        nan |= dpp_u<CTRL>(nan);                              \
+    }
+    AWQ_F64_LEVEL(kDppXor1)
+    AWQ_F64_LEVEL(kDppXor2)
+    AWQ_F64_LEVEL(kDppHalfMirror)
+    if (P >= 16) AWQ_F64_LEVEL(kDppMirror)
+#undef AWQ_F64_LEVEL
+    if (grp < ng && j == 0) {
+        double sc, z;
+        group_params<AWQ_DTYPE_F64>(nan ? NAN : mn, nan ? NAN : mx, (int)nan, qmin, qmax, sym, sc, z);
+        sp_s[grp] = sc;
+        sp_z[grp] = z;
+        const int64_t gi = r * G + g0 + grp;
+        if (scales) scales[gi] = sc != sc ? nan_scale_pick(nan_code, nan != 0) : sw_f32_to_f16((float)sc);
+        if (zeros) zeros[gi] = to_i32(z);
+    }
+    __syncthreads();
+    if (qzeros && lane == 0) {
+        uint32_t zword = 0;
+        for (int g = 0; g < ng; ++g) zword |= (((uint32_t)to_i32(sp_z[g]) - (uint32_t)qmin) & MASK) << (BITS * g);
+        qzeros[r * SP + sp] = (int32_t)zword;
+    }
+    if (!tensor_q && !qweight) return;
+    // ---- pass 2: lane = one word of PER elements ----
+    const int nwords = (n + PER - 1) / PER;
+    for (int c = lane; c < nwords; c += 64) {
+        uint32_t wd = 0;
+#pragma unroll
+        for (int i = 0; i < PER; ++i) {
+            const int e = c * PER + i;
+            if (e >= n) break;
+            const int g = (int)(((float)e + 0.5f) * invL);
+            const int32_t q = to_i32(quant1<AWQ_DTYPE_F64>(st[e], sp_s[g], sp_z[g], qmin, qmax));
+            if (tensor_q) tensor_q[r * K + span0 + e] = q;
+            wd |= (((uint32_t)q - (uint32_t)qmin) & MASK) << (BITS * i);
+        }
+        if (qweight) qweight[r * wpr + span0 / PER + c] = (int32_t)wd;
+    }
+}
+
 // Reference _quantize_tensor (awq.py:215-250, mode 0: clamp(round(RN(RN(x / s) + z))) and
 // _dequantize_tensor (awq.py:252-284, mode 1: RN(RN(x - z) * s)) with caller-given per-group
 // parameters, output in the input dtype.  The parameters (double) enter the op in its
@@ -675,6 +786,21 @@ hipError_t launch_generic(const void* w, int dtype, int64_t rows, int64_t K, int
             if (per == 8) AWQ_SPAN_REG(2, 8); else AWQ_SPAN_REG(2, 4);
         }
 #undef AWQ_SPAN_REG
+        return hipPeekAtLastError();
+    }
+    if (dtype == AWQ_DTYPE_F64 && !search && !s_exact && !z_exact && L >= 2 && per * L * 8 <= 16384 && !noreg) {
+        const int64_t SP = (G + per - 1) / per;
+        const size_t lds = (size_t)(per * L * 8);
+        const float invL = 1.0f / (float)L;
+        const uint32_t nc = nan_scale_code(AWQ_DTYPE_F64, symmetric, small);
+        if (per == 8)
+            hipLaunchKernelGGL(awq_f64_span_lds_kernel<8>, dim3((unsigned)(rows * SP)), dim3(64), lds, stream,
+                               (const double*)w, rows, K, L, invL, qmin, qmax, symmetric, nc, tensor_q, scales, zeros,
+                               qweight, qzeros);
+        else
+            hipLaunchKernelGGL(awq_f64_span_lds_kernel<4>, dim3((unsigned)(rows * SP)), dim3(64), lds, stream,
+                               (const double*)w, rows, K, L, invL, qmin, qmax, symmetric, nc, tensor_q, scales, zeros,
+                               qweight, qzeros);
         return hipPeekAtLastError();
     }
 #define AWQ_GEN(D)                                                                                   \

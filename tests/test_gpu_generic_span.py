@@ -131,3 +131,22 @@ def test_dequantize_packed_kernel_variants(variant, bits):
     with _hip.tuning(dq_words_v1=variant):
         dq = q.dequantize_packed(pk).cpu()
     assert gio.same_bits(dq, orc.dequantize(ref))
+
+
+@pytest.mark.parametrize("bits", [4, 8], ids=str)
+@pytest.mark.parametrize("shape,gs", [((33, 1000), 100), ((9, 777), 7), ((5, 1001), 2), ((6, 2049), 256),
+                                      ((4, 1600), 200), ((7, 3000), 500), ((3, 95), 96)], ids=str)
+def test_f64_lds_span_vs_oracle_and_strided(shape, gs, bits):
+    """fp64 at group sizes other than 64 / 128 (the LDS span kernel: 4-bit L <= 256, 8-bit
+    L <= 512) against the oracle (tensor_q, zero points, scales, packed words) and against
+    the strided span (tuning gen_noreg=1), ragged K and special values included."""
+    from awq_quantizer import _hip
+    x = specials(rand(shape, gs + bits, 1.0), 23 + gs).to(torch.float64)
+    for sym in (False, True):
+        _assert_parity(x, gs, bits, sym)
+        a = Q(bits=bits, group_size=gs, symmetric=sym).quantize_packed(x)
+        with _hip.tuning(gen_noreg=1):
+            b = Q(bits=bits, group_size=gs, symmetric=sym).quantize_packed(x)
+        for key in ("qweight", "qzeros"):
+            assert torch.equal(a[key], b[key])
+        assert gio.same_bits(a["scales"], b["scales"])

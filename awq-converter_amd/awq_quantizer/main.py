@@ -306,7 +306,7 @@ class ChunkWriter:
     def __init__(self, order: List[str], output_dir: str, chunk_size: int, use_safetensors: bool, logger=None,
                  writers: int = 0, stem: str = CHUNK_STEM, metadata: bool = True):
         self.order, self.dir, self.size, self.st, self.logger = order, output_dir, chunk_size, use_safetensors, logger
-        self.writers = writers or min(8, max(2, (os.cpu_count() or 4) // 2))
+        self.writers = writers or STREAM_OPTS.get("writers") or min(8, max(2, cpu_share() // 2))
         self.stem, self.metadata = stem, metadata
         self.t2c: Dict[str, int] = {}
         self.n_chunks = self.n_ok = 0
@@ -463,6 +463,21 @@ def save_autoawq(quantized: Dict[str, Dict[str, torch.Tensor]], loader, passthro
                     f"{len(passthrough) + len(failed)} tensors copied")
 
 
+def cpu_share() -> int:
+    """CPUs this process may actually use: its affinity set, capped by a cgroup v2 CPU quota
+    (`cpu.max`) — os.cpu_count() reports the whole machine, which on a shared GPU node is
+    many times the process's share."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            quota, period = f.read().split()[:2]
+        if quota != "max":
+            n = min(n, max(1, int(int(quota) // int(period))))
+    except (OSError, ValueError):
+        pass
+    return max(1, n)
+
+
 def _batches(infos: List[TensorInfo], budget: int) -> List[List[TensorInfo]]:
     """Consecutive runs of tensors (processing order kept) of at most `budget` input bytes
     (a larger tensor forms a batch of its own)."""
@@ -600,7 +615,8 @@ def quantize_stream_native(loader, infos: List[TensorInfo], quantizer: AWQQuanti
     h2d = torch.cuda.Stream(dev)
     d2h = h2d if STREAM_OPTS.get("copy_streams", 2) == 1 else torch.cuda.Stream(dev)
     cfg = _hip.StreamConfig(bits=bits, symmetric=int(bool(quantizer.symmetric)), group_size=gs,
-                            readers=min(16, max(8, readers)), nslots=nslots, slot_bytes=slot,
+                            readers=int(STREAM_OPTS.get("readers", min(16, max(8, readers)))), nslots=nslots,
+                            slot_bytes=slot,
                             first_batch_bytes=max(4096, slot // 4 // 4096 * 4096),
                             host_staging=h_stage.data_ptr(), dev_staging=d_stage.data_ptr(),
                             host_tables=h_tab.data_ptr(), dev_tables=d_tab.data_ptr(),
@@ -1063,7 +1079,8 @@ _SCALARS = ("bits", "group_size", "symmetric", "shape")
 TIMINGS: Dict[str, float] = {}   # phase times of the last main() call (scripts/cli_bench.py)
 # native pipeline overrides for measurement scripts (scripts/cli_profile.py --stream-opts):
 # slot_bytes, nslots, copy_streams (1: H2D and D2H share one stream), trace (1: per-batch
-# timestamps, include/awq_hip.h awq_stream_config.trace)
+# timestamps, include/awq_hip.h awq_stream_config.trace), readers (pread threads), writers
+# (ChunkWriter threads)
 STREAM_OPTS: Dict[str, int] = {}
 
 

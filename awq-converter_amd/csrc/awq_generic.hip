@@ -772,7 +772,9 @@ hipError_t launch_generic(const void* w, int dtype, int64_t rows, int64_t K, int
     const int64_t G = (K + L - 1) / L;
     const unsigned grid = grid_for(rows * ((G + per - 1) / per), 4, 256 * 16);
     const bool search = n_cand > 0;
-    const bool noreg = tuning().gen_noreg != 0;  // A/B of the register-resident fp64 span
+    // A/B of the fp64 spans: 1 = the strided span only, 2 = the LDS span also at gs 64 / 128
+    const int f64_span = tuning().gen_noreg;
+    const bool noreg = f64_span != 0;
     if (dtype == AWQ_DTYPE_F64 && !search && !s_exact && !z_exact && (L == 64 || L == 128) && !noreg) {
         const unsigned blocks = (unsigned)((rows * ((G + per - 1) / per) + 3) / 4);
         const double* wd = (const double*)w;
@@ -788,7 +790,8 @@ hipError_t launch_generic(const void* w, int dtype, int64_t rows, int64_t K, int
 #undef AWQ_SPAN_REG
         return hipPeekAtLastError();
     }
-    if (dtype == AWQ_DTYPE_F64 && !search && !s_exact && !z_exact && L >= 2 && per * L * 8 <= 16384 && !noreg) {
+    if (dtype == AWQ_DTYPE_F64 && !search && !s_exact && !z_exact && L >= 2 && per * L * 8 <= 16384 &&
+        f64_span != 1) {
         const int64_t SP = (G + per - 1) / per;
         const size_t lds = (size_t)(per * L * 8);
         const float invL = 1.0f / (float)L;

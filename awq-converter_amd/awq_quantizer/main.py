@@ -306,7 +306,7 @@ class ChunkWriter:
     def __init__(self, order: List[str], output_dir: str, chunk_size: int, use_safetensors: bool, logger=None,
                  writers: int = 0, stem: str = CHUNK_STEM, metadata: bool = True):
         self.order, self.dir, self.size, self.st, self.logger = order, output_dir, chunk_size, use_safetensors, logger
-        self.writers = writers or STREAM_OPTS.get("writers") or min(8, max(2, cpu_share() // 2))
+        self.writers = writers or min(8, max(2, cpu_share() // 2))
         self.stem, self.metadata = stem, metadata
         self.t2c: Dict[str, int] = {}
         self.n_chunks = self.n_ok = 0
@@ -476,6 +476,21 @@ def cpu_share() -> int:
     except (OSError, ValueError):
         pass
     return max(1, n)
+
+
+def writer_threads(infos: List[TensorInfo], packed: bool) -> int:
+    """Chunk-writer threads for an output of this size: more writers only pay when the
+    files are large — below ~2 GB of output, 8 concurrent writers stalled the pipeline's
+    HIP calls for 8-12 ms at a time while 3-4 did not (opt-350m, profiles/round3/r3o: 0.057 s
+    vs 0.066-0.072 s warm), and above it the writes are the bound (Llama-3-8B packed 0.36 s
+    at 8 writers vs 0.42-0.46 at 4).  STREAM_OPTS["writers"] overrides."""
+    forced = STREAM_OPTS.get("writers")
+    if forced:
+        return int(forced)
+    in_bytes = sum(i.nbytes for i in infos)
+    out_bytes = in_bytes * (0.26 if packed else 2.05)   # 4-bit packed ~ in / 4; reference ~ 2 x in
+    share = cpu_share()
+    return min(4, max(2, share // 4)) if out_bytes < (2 << 30) else min(8, max(2, share // 2))
 
 
 def _batches(infos: List[TensorInfo], budget: int) -> List[List[TensorInfo]]:
@@ -1018,7 +1033,7 @@ def main(argv: Optional[List[str]] = None) -> int:
         writer = None
         if not autoawq:
             writer = ChunkWriter([i.name for i in ordered], args.output_dir, args.chunk_size, args.save_safetensors,
-                                 logger)
+                                 logger, writers=writer_threads(ordered, packed))
         chunk_of = {i.name: k // args.chunk_size for k, i in enumerate(ordered)}
         threads = []
         TIMINGS["pre_stream_s"] = time.time() - start
@@ -1137,7 +1152,8 @@ def _main_distributed(args, loader, ordered: List[TensorInfo], logger, start: fl
         logger.info(f"rank {rank}/{world}: {len(mine)} of {len(ordered)} tensors on {device}")
         if per_rank and not autoawq:
             writer = ChunkWriter([i.name for i in mine], args.output_dir, args.chunk_size, args.save_safetensors,
-                                 logger, stem=_rank_stem(rank), metadata=False)
+                                 logger, stem=_rank_stem(rank), metadata=False,
+                                 writers=writer_threads(mine, args.output_format in ("packed", "autoawq")))
         # per-rank chunks: the writer holds each result until its chunk is on disk, nothing else does
         sink = _NullSink() if writer is not None else results
         quantize_stream(loader, mine, q, device, args.num_workers, max(1, args.prefetch_factor * args.batch_size),

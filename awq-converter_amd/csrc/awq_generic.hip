@@ -772,9 +772,11 @@ hipError_t launch_generic(const void* w, int dtype, int64_t rows, int64_t K, int
     const int64_t G = (K + L - 1) / L;
     const unsigned grid = grid_for(rows * ((G + per - 1) / per), 4, 256 * 16);
     const bool search = n_cand > 0;
-    // A/B of the fp64 spans: 1 = the strided span only, 2 = the LDS span also at gs 64 / 128
+    // fp64 spans (A/B, tuning gen_noreg): 0 = the LDS span wherever the span fits 16 KiB
+    // (3.2-3.7 TB/s of input at gs 64 / 128, against the register span's 1.4-2.4:
+    // profiles/round3/r3n), 1 = the strided span only, 2 = the register span at gs 64 / 128
     const int f64_span = tuning().gen_noreg;
-    const bool noreg = f64_span != 0;
+    const bool noreg = f64_span != 2;
     if (dtype == AWQ_DTYPE_F64 && !search && !s_exact && !z_exact && (L == 64 || L == 128) && !noreg) {
         const unsigned blocks = (unsigned)((rows * ((G + per - 1) / per) + 3) / 4);
         const double* wd = (const double*)w;

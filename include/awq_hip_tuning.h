@@ -22,9 +22,8 @@ typedef struct awq_tuning {
     int32_t no_rowgroup;     /* 1: shapes of the row-segment kernel take the generic kernel */
     int32_t rg_waves;        /* 1 or 2: waves per row-segment tile (0 = cost model) */
     int32_t rg_gpt;          /* 8..64, multiple of 8: groups per row-segment tile (0 = cost model) */
-    int32_t gen_noreg;       /* 1: fp64 takes the strided span instead of the register span (gs 64 /
-                                128) or the LDS span (other gs with the span in 16 KiB); 2: the
-                                LDS span at gs 64 / 128 too */
+    int32_t gen_noreg;       /* fp64 RTN: 0 the LDS span (any gs whose span fits 16 KiB), 1 the
+                                strided span, 2 the register span at gs 64 / 128 (A/B) */
     int32_t dq_words_v1;     /* packed dequantize kernel: 0 the default, 1 the round-2 word kernel
                                 (per-thread stores), 2 / 3 LDS-staged words with / without
                                 XCD-contiguous blocks, 4 / 5 four-output lanes without / with,

@@ -54,6 +54,23 @@ def probes(model_dir, threads):
                 dst.copy_(src, non_blocking=True)
         s.synchronize()
         out[name] = round(8 * n / (time.perf_counter() - t0) / 1e9, 2)
+    # D2H into a large pinned destination walked once (the reference format's per-chunk output
+    # buffers: tens of GB, each page written once) vs the same 1 GiB reused above
+    big = torch.empty(8 * n, dtype=torch.uint8, pin_memory=True)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    with torch.cuda.stream(s):
+        for k in range(8):
+            big[k * n:(k + 1) * n].copy_(d, non_blocking=True)
+    s.synchronize()
+    out["d2h_pinned_8GiB_walk_GBs"] = round(8 * n / (time.perf_counter() - t0) / 1e9, 2)
+    t0 = time.perf_counter()
+    with torch.cuda.stream(s):
+        for k in range(8):
+            big[k * n:(k + 1) * n].copy_(d, non_blocking=True)
+    s.synchronize()
+    out["d2h_pinned_8GiB_second_walk_GBs"] = round(8 * n / (time.perf_counter() - t0) / 1e9, 2)
+    del big
     # both directions at once on two streams (the native pipeline's H2D and D2H overlap)
     h2, d2, s2 = torch.empty_like(h).pin_memory(), torch.empty_like(d), torch.cuda.Stream(dev)
     torch.cuda.synchronize()

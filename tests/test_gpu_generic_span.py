@@ -99,12 +99,12 @@ def test_dequantize_packed_vs_oracle(dtype, shape, gs, bits, sym):
     assert gio.same_bits(dq, orc.dequantize(ref))
 
 
-@pytest.mark.parametrize("other", [1, 2], ids=["strided", "lds"])
+@pytest.mark.parametrize("other", [1, 2], ids=["strided", "register"])
 @pytest.mark.parametrize("gs", [64, 128], ids=str)
 def test_generic_f64_reg_span_matches_strided(gs, other):
-    """The register-resident fp64 span (group sizes 64 / 128), the strided span kernel
-    (tuning gen_noreg=1) and the LDS span (gen_noreg=2) give the same bits on a ragged shape
-    with special values."""
+    """At group sizes 64 / 128 the default fp64 LDS span, the strided span kernel (tuning
+    gen_noreg=1) and the register-resident span (gen_noreg=2) give the same bits on a ragged
+    shape with special values."""
     from awq_quantizer import _hip
     x = specials(rand((33, 1000), gs, 1.0), 17).to(torch.float64)
     q = Q(bits=4, group_size=gs, symmetric=False)

@@ -598,7 +598,9 @@ def quantize_stream_native(loader, infos: List[TensorInfo], quantizer: AWQQuanti
         for dt in kinds:
             ss[dt] += size[dt]
             dev_total[dt] += size[dt]
+    t_alloc = time.perf_counter()
     arena = {dt: torch.empty(max(dev_total[dt], 8), dtype=dt, device=dev) for dt in kinds}
+    t_arena = time.perf_counter()
     hosts = {} if keep_on_device else {s: {dt: torch.empty(max(n[dt], 8), dtype=dt, pin_memory=True) for dt in kinds}
                                        for s, n in seg_size.items()}
     lib = _hip.load_library()
@@ -622,6 +624,7 @@ def quantize_stream_native(loader, infos: List[TensorInfo], quantizer: AWQQuanti
     slot = -(-slot // 4096) * 4096
     nslots = int(STREAM_OPTS.get("nslots", 3))
     tb = int(lib.awq_stream_table_bytes(slot))
+    t_hosts = time.perf_counter()
     h_stage = torch.empty(nslots * slot, dtype=torch.uint8, pin_memory=True)
     d_stage = torch.empty(nslots * slot, dtype=torch.uint8, device=dev)
     h_tab = torch.empty(nslots * tb, dtype=torch.uint8, pin_memory=True)
@@ -692,7 +695,10 @@ def quantize_stream_native(loader, infos: List[TensorInfo], quantizer: AWQQuanti
         if on_done:
             on_done(info.name, r)
     TIMINGS.update({f"stream_{device}": {"engine": "native", "wall_s": round(time.perf_counter() - t_enter, 4),
-                                          "setup_s": round(t_run - t_enter, 4), "batches": int(stats.batches),
+                                          "setup_s": round(t_run - t_enter, 4),
+                                          "alloc_dev_s": round(t_arena - t_alloc, 4),
+                                          "alloc_host_out_s": round(t_hosts - t_arena, 4),
+                                          "batches": int(stats.batches),
                                           "pieces": int(stats.pieces), "slot_MB": slot >> 20,
                                           "pipeline_s": round(stats.wall_s, 4), "wait_s": round(t_wait, 4),
                                           "read_busy_s": round(stats.read_busy_s, 4),

@@ -307,6 +307,10 @@ class ChunkWriter:
                  writers: int = 0, stem: str = CHUNK_STEM, metadata: bool = True):
         self.order, self.dir, self.size, self.st, self.logger = order, output_dir, chunk_size, use_safetensors, logger
         self.writers = writers or min(8, max(2, cpu_share() // 2))
+        # while producers run, at most `writers` chunk writes at once (more stalled the GPU
+        # pipeline's HIP calls); once close() is called the backlog drains with tail_writers
+        self.tail_writers = max(self.writers, min(8, max(2, cpu_share() // 2)))
+        self.gate = threading.Semaphore(self.writers)
         self.stem, self.metadata = stem, metadata
         self.t2c: Dict[str, int] = {}
         self.n_chunks = self.n_ok = 0
@@ -328,7 +332,7 @@ class ChunkWriter:
 
     def _run(self) -> None:
         try:
-            with ThreadPoolExecutor(max_workers=self.writers) as pool:
+            with ThreadPoolExecutor(max_workers=self.tail_writers) as pool:
                 futs = []
                 chunk, c, t2c, qparams, n_ok = {}, 0, {}, None, 0
                 for name in self.order:
@@ -358,15 +362,18 @@ class ChunkWriter:
             self.error = e
 
     def _timed_write(self, chunk, c: int, t_submit: float) -> None:
-        t0 = time.time()
-        _write_chunk(chunk, self.dir, c, self.st, self.logger, stem=self.stem)
-        self.times.append((t_submit, t0, time.time()))
+        with self.gate:
+            t0 = time.time()
+            _write_chunk(chunk, self.dir, c, self.st, self.logger, stem=self.stem)
+            self.times.append((t_submit, t0, time.time()))
 
     def close(self) -> None:
         """Every producer has finished: unfinished tensors count as failed; wait for the writes."""
         with self.cv:
             self.closed = True
             self.cv.notify()
+        for _ in range(self.tail_writers - self.writers):   # the producers are done: widen the pool
+            self.gate.release()
         self.thread.join()
         if self.error is not None:
             raise self.error

@@ -16,7 +16,7 @@ import torch
 
 LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib")
 LIB_PATH = os.path.join(LIB_DIR, "libawq_hip.so")
-ABI_VERSION = 11
+ABI_VERSION = 12
 Q_SMALL_TENSOR = 1      # include/awq_hip.h AWQ_Q_SMALL_TENSOR
 
 AWQ_DTYPE = {torch.bfloat16: 0, torch.float16: 1, torch.float32: 2, torch.float64: 3}
@@ -47,13 +47,13 @@ class StreamConfig(ctypes.Structure):
     """Mirror of awq_stream_config (include/awq_hip.h)."""
     _fields_ = [("bits", _I32), ("symmetric", _I32), ("group_size", _I32), ("readers", _I32), ("nslots", _I32),
                 ("trace_batches", _I32), ("slot_bytes", _I64), ("first_batch_bytes", _I64), ("host_staging", _P),
-                ("dev_staging", _P), ("host_tables", _P), ("dev_tables", _P), ("compute_stream", _P),
+                ("dev_staging", _P), ("compute_stream", _P),
                 ("h2d_stream", _P), ("d2h_stream", _P), ("trace", _P)]
 
 
 STREAM_TRACE_FIELDS = 14   # AWQ_STREAM_TRACE_FIELDS
 STREAM_TRACE_NAMES = ("read_first", "read_last", "h2d_enq", "kern_enq", "d2h_enq", "h2d_done", "kern_done",
-                      "d2h_done", "h2d_call", "d2h_call", "plan", "table_upload", "ragged_launch", "other_launch")
+                      "d2h_done", "h2d_call", "d2h_call", "plan", "wait_slot", "ragged_launch", "other_launch")
 
 
 class StreamStats(ctypes.Structure):
@@ -62,7 +62,7 @@ class StreamStats(ctypes.Structure):
                 ("read_busy_s", ctypes.c_double), ("wait_read_s", ctypes.c_double), ("wait_slot_s", ctypes.c_double)]
 
 
-assert ctypes.sizeof(StreamItem) == 120 and ctypes.sizeof(StreamConfig) == 104
+assert ctypes.sizeof(StreamItem) == 120 and ctypes.sizeof(StreamConfig) == 88
 
 
 class Tuning(ctypes.Structure):

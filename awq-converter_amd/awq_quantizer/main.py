@@ -630,12 +630,10 @@ def quantize_stream_native(loader, infos: List[TensorInfo], quantizer: AWQQuanti
     slot = slot_bytes or STREAM_OPTS.get("slot_bytes") or min(256 << 20, max(32 << 20, total_in // 8))
     slot = -(-slot // 4096) * 4096
     nslots = int(STREAM_OPTS.get("nslots", 3))
-    tb = int(lib.awq_stream_table_bytes(slot))
+    tb = int(lib.awq_stream_table_bytes(slot))     # each slot: its table area, then its input
     t_hosts = time.perf_counter()
-    h_stage = torch.empty(nslots * slot, dtype=torch.uint8, pin_memory=True)
-    d_stage = torch.empty(nslots * slot, dtype=torch.uint8, device=dev)
-    h_tab = torch.empty(nslots * tb, dtype=torch.uint8, pin_memory=True)
-    d_tab = torch.empty(nslots * tb, dtype=torch.uint8, device=dev)
+    h_stage = torch.empty(nslots * (tb + slot), dtype=torch.uint8, pin_memory=True)
+    d_stage = torch.empty(nslots * (tb + slot), dtype=torch.uint8, device=dev)
     compute = torch.cuda.current_stream(dev)
     h2d = torch.cuda.Stream(dev)
     d2h = h2d if STREAM_OPTS.get("copy_streams", 2) == 1 else torch.cuda.Stream(dev)
@@ -644,7 +642,6 @@ def quantize_stream_native(loader, infos: List[TensorInfo], quantizer: AWQQuanti
                             slot_bytes=slot,
                             first_batch_bytes=max(4096, slot // 4 // 4096 * 4096),
                             host_staging=h_stage.data_ptr(), dev_staging=d_stage.data_ptr(),
-                            host_tables=h_tab.data_ptr(), dev_tables=d_tab.data_ptr(),
                             compute_stream=compute.cuda_stream, h2d_stream=h2d.cuda_stream,
                             d2h_stream=d2h.cuda_stream)
     trace = None

@@ -7,9 +7,11 @@
 //   reader threads   pread the batch's tensors from their files into pinned slot b % nslots
 //                    (large tensors in 16 MiB pieces across the threads); a slot is refilled
 //                    once the H2D copy of the batch that used it before has completed
-//   submitter thread H2D of the whole slot (one copy, h2d stream), then on the compute
-//                    stream one ragged launch per dtype (awq_quantize_ragged, descriptor and
-//                    tensor tables uploaded from the slot's pinned table area) and
+//   submitter thread plans the batch's descriptors and tensor tables into the slot's table
+//                    area (the first awq_stream_table_bytes of the slot), then ONE H2D of
+//                    tables + input (h2d stream: no small table copies — those stalled the
+//                    submitter for milliseconds, profiles/round3/r3m), then on the compute
+//                    stream one ragged launch per dtype (awq_quantize_ragged) and
 //                    awq_quantize_groups_ex for the shapes the ragged kernel does not take,
 //                    then the D2H of the outputs of the tensors the batch completes (d2h
 //                    stream, adjacent ranges coalesced)
@@ -72,6 +74,7 @@ struct Pipeline {
     std::vector<Batch> batches;
     std::vector<ReadJob> jobs;
     std::vector<hipEvent_t> ev_h2d, ev_kern, ev_done;
+    int64_t tb = 0, stride = 0;        // table area per slot; slot stride (tb + slot_bytes)
     hipEvent_t ev_start = nullptr;     // (trace only) the event clock's origin
     std::vector<double> tr;            // (trace only) AWQ_STREAM_TRACE_FIELDS per batch, host part
     std::mutex mu;
@@ -160,7 +163,6 @@ int plan(Pipeline& P, std::string& why) {
 // ---- reader threads ---------------------------------------------------------------------
 void reader_main(Pipeline* P) {
     (void)hipSetDevice(P->device);
-    const int64_t slot = P->cfg.slot_bytes;
     for (;;) {
         ReadJob j;
         {
@@ -182,7 +184,7 @@ void reader_main(Pipeline* P) {
         }
         const Piece& pc = B.pieces[j.piece];
         const awq_stream_item& it = P->items[pc.item];
-        char* dst = (char*)P->cfg.host_staging + (int64_t)B.slot * slot + pc.slot_off + j.off;
+        char* dst = (char*)P->cfg.host_staging + (int64_t)B.slot * P->stride + P->tb + pc.slot_off + j.off;
         const int64_t src = it.offset + pc.row0 * it.K * elem_bytes(it.dtype) + j.off;
         const double t = now_s();
         int64_t done = 0;
@@ -230,25 +232,28 @@ bool ragged_ok(const awq_tensor_desc& d, int dtype, int64_t gs) {
            (!d.qzeros || aligned(d.qzeros, 4)) && (!d.scales || aligned(d.scales, 2));
 }
 
-// ph (trace): seconds in host planning, the table uploads, the ragged launches, the
-// per-tensor launches
-bool quantize_batch(Pipeline& P, const Batch& B, hipStream_t cs, double (&ph)[4]) {
-    const awq_stream_config& c = P.cfg;
-    double tp = now_s();
-    const int64_t gs = c.group_size;
-    const char* dev_slot = (const char*)c.dev_staging + (int64_t)B.slot * c.slot_bytes;
-    const int64_t tb = awq_stream_table_bytes(c.slot_bytes);
-    char* htab = (char*)c.host_tables + (int64_t)B.slot * tb;
-    char* dtab = (char*)c.dev_tables + (int64_t)B.slot * tb;
-    awq_tensor_desc* descs = (awq_tensor_desc*)htab;   // [AWQ_STREAM_MAX_BATCH_ITEMS], grouped by dtype
-    const int64_t tables_at = align_up((int64_t)sizeof(awq_tensor_desc) * AWQ_STREAM_MAX_BATCH_ITEMS, kAlign);
-    struct Group {
-        int dtype, first, n;
-        int64_t tiles, table_off, table_len;
-        int flags;
-    };
+// A batch's launches, planned on the host into the slot's pinned table area (descriptors
+// grouped by dtype, then each group's XCD-interleaved tensor table) before the slot's H2D
+// carries them to the device together with the input.
+struct Group {
+    int dtype, first, n;
+    int64_t tiles, table_off, table_len;
+    int flags;
+};
+struct BatchPlan {
     std::vector<Group> groups;
     std::vector<std::pair<awq_tensor_desc, int>> rest;   // (descriptor, dtype) of the per-tensor launches
+};
+
+bool plan_batch(Pipeline& P, const Batch& B, BatchPlan& bp) {
+    const awq_stream_config& c = P.cfg;
+    const int64_t gs = c.group_size;
+    char* hslot = (char*)c.host_staging + (int64_t)B.slot * P.stride;
+    const char* dev_slot = (const char*)c.dev_staging + (int64_t)B.slot * P.stride + P.tb;
+    awq_tensor_desc* descs = (awq_tensor_desc*)hslot;   // [AWQ_STREAM_MAX_BATCH_ITEMS], grouped by dtype
+    const int64_t tables_at = align_up((int64_t)sizeof(awq_tensor_desc) * AWQ_STREAM_MAX_BATCH_ITEMS, kAlign);
+    bp.groups.clear();
+    bp.rest.clear();
     int nd = 0;
     int64_t toff = tables_at;
     for (int dt : {AWQ_DTYPE_BF16, AWQ_DTYPE_F16, AWQ_DTYPE_F32, AWQ_DTYPE_F64}) {
@@ -258,7 +263,7 @@ bool quantize_batch(Pipeline& P, const Batch& B, hipStream_t cs, double (&ph)[4]
             if (it.dtype != dt) continue;
             const awq_tensor_desc d = piece_desc(it, pc, dev_slot + pc.slot_off, c.bits, gs);
             if (ragged_ok(d, dt, gs)) descs[nd++] = d;
-            else rest.push_back({d, dt});
+            else bp.rest.push_back({d, dt});
         }
         if (nd == first) continue;
         Group g{dt, first, nd - first, 0, 0, 0, 0};
@@ -270,42 +275,39 @@ bool quantize_batch(Pipeline& P, const Batch& B, hipStream_t cs, double (&ph)[4]
         const int64_t need = awq_plan_block_tensor(descs + first, g.n, g.tiles, nullptr, 0);
         g.table_off = toff;
         g.table_len = need;
-        if (toff + need * 4 > tb) {
+        if (toff + need * 4 > P.tb) {
             P.fail(AWQ_EINVAL, "stream tables overflow");
             return false;
         }
-        if (need > 0 && awq_plan_block_tensor(descs + first, g.n, g.tiles, (int32_t*)(htab + toff), need) < 0) {
+        if (need > 0 && awq_plan_block_tensor(descs + first, g.n, g.tiles, (int32_t*)(hslot + toff), need) < 0) {
             P.fail(AWQ_EINVAL, std::string("awq_plan_block_tensor: ") + awq_last_error());
             return false;
         }
         g.flags = awq_ragged_flags(descs + first, g.n, gs);
         toff = align_up(toff + need * 4, 16);
-        groups.push_back(g);
+        bp.groups.push_back(g);
     }
-    ph[0] = now_s() - tp;
-    tp = now_s();
-    if (!groups.empty()) {   // descriptors + tables in one copy, stream-ordered before the launches
-        if (!P.hip_ok(hipMemcpyAsync(dtab, htab, (size_t)(nd * (int64_t)sizeof(awq_tensor_desc)),
-                                     hipMemcpyHostToDevice, cs), "descriptor upload"))
-            return false;
-        if (!P.hip_ok(hipMemcpyAsync(dtab + tables_at, htab + tables_at, (size_t)(toff - tables_at),
-                                     hipMemcpyHostToDevice, cs), "table upload"))
-            return false;
-    }
-    ph[1] = now_s() - tp;
-    tp = now_s();
-    for (const Group& g : groups) {
-        const int rc = awq_quantize_ragged((const awq_tensor_desc*)dtab + g.first, g.n, g.tiles,
-                                           g.table_len ? (const int32_t*)(dtab + g.table_off) : nullptr, g.dtype,
+    return true;
+}
+
+// ph (trace): seconds in the ragged launches and the per-tensor launches
+bool launch_batch(Pipeline& P, const Batch& B, const BatchPlan& bp, hipStream_t cs, double (&ph)[2]) {
+    const awq_stream_config& c = P.cfg;
+    const int64_t gs = c.group_size;
+    const char* dslot = (const char*)c.dev_staging + (int64_t)B.slot * P.stride;
+    double tp = now_s();
+    for (const Group& g : bp.groups) {
+        const int rc = awq_quantize_ragged((const awq_tensor_desc*)dslot + g.first, g.n, g.tiles,
+                                           g.table_len ? (const int32_t*)(dslot + g.table_off) : nullptr, g.dtype,
                                            c.bits, c.symmetric, gs, g.flags, cs);
         if (rc) {
             P.fail(rc, std::string("awq_quantize_ragged: ") + awq_last_error());
             return false;
         }
     }
-    ph[2] = now_s() - tp;
+    ph[0] = now_s() - tp;
     tp = now_s();
-    for (const auto& r : rest) {
+    for (const auto& r : bp.rest) {
         const awq_tensor_desc& d = r.first;
         const int rc = awq_quantize_groups_ex(d.w, r.second, d.rows, d.K, (int32_t)gs, c.bits, c.symmetric, 0,
                                               d.qweight, d.qzeros, d.scales, d.tensor_q, d.zeros, cs);
@@ -314,7 +316,7 @@ bool quantize_batch(Pipeline& P, const Batch& B, hipStream_t cs, double (&ph)[4]
             return false;
         }
     }
-    ph[3] = now_s() - tp;
+    ph[1] = now_s() - tp;
     return true;
 }
 
@@ -323,6 +325,7 @@ void submitter_main(Pipeline* P) {
     const awq_stream_config& c = P->cfg;
     hipStream_t h2d = (hipStream_t)c.h2d_stream, cs = (hipStream_t)c.compute_stream, d2h = (hipStream_t)c.d2h_stream;
     const int64_t nb = (int64_t)P->batches.size();
+    BatchPlan bp;
     for (int64_t b = 0; b < nb; ++b) {
         const Batch& B = P->batches[b];
         double t = now_s();
@@ -332,21 +335,30 @@ void submitter_main(Pipeline* P) {
             if (P->err) return;
         }
         P->wait_read += now_s() - t;
+        double t_slot = 0;
         if (b >= c.nslots) {   // the slot's previous batch: its kernels read the device slot and its tables
             t = now_s();
             if (!P->hip_ok(hipEventSynchronize(P->ev_kern[b - c.nslots]), "waiting for a slot's kernels")) return;
-            P->wait_slot += now_s() - t;
+            t_slot = now_s() - t;
+            P->wait_slot += t_slot;
         }
+        // plan the launches into the slot's table area (the slot's previous kernels are done:
+        // its device tables are free, and its H2D is done: so are the host ones)
+        double t_plan = now_s();
+        if (!plan_batch(*P, B, bp)) return;
+        t_plan = now_s() - t_plan;
         const double t_h2d = now_s();
-        if (B.bytes > 0 &&
-            !P->hip_ok(hipMemcpyAsync((char*)c.dev_staging + (int64_t)B.slot * c.slot_bytes,
-                                      (const char*)c.host_staging + (int64_t)B.slot * c.slot_bytes, (size_t)B.bytes,
-                                      hipMemcpyHostToDevice, h2d), "H2D"))
+        if (!P->hip_ok(hipMemcpyAsync((char*)c.dev_staging + (int64_t)B.slot * P->stride,
+                                      (const char*)c.host_staging + (int64_t)B.slot * P->stride,
+                                      (size_t)(P->tb + B.bytes), hipMemcpyHostToDevice, h2d),
+                       "H2D"))
             return;
         if (!P->hip_ok(hipEventRecord(P->ev_h2d[b], h2d), "event")) return;
         if (!P->tr.empty()) {
             P->tr[b * AWQ_STREAM_TRACE_FIELDS + 2] = now_s() - P->t0;
             P->tr[b * AWQ_STREAM_TRACE_FIELDS + 8] = now_s() - t_h2d;
+            P->tr[b * AWQ_STREAM_TRACE_FIELDS + 10] = t_plan;
+            P->tr[b * AWQ_STREAM_TRACE_FIELDS + 11] = t_slot;
         }
         {
             std::lock_guard<std::mutex> g(P->mu);
@@ -354,10 +366,10 @@ void submitter_main(Pipeline* P) {
         }
         P->cv.notify_all();
         if (!P->hip_ok(hipStreamWaitEvent(cs, P->ev_h2d[b], 0), "stream wait")) return;
-        double ph[4] = {0, 0, 0, 0};
-        if (!quantize_batch(*P, B, cs, ph)) return;
+        double ph[2] = {0, 0};
+        if (!launch_batch(*P, B, bp, cs, ph)) return;
         if (!P->tr.empty())
-            for (int k = 0; k < 4; ++k) P->tr[b * AWQ_STREAM_TRACE_FIELDS + 10 + k] = ph[k];
+            for (int k = 0; k < 2; ++k) P->tr[b * AWQ_STREAM_TRACE_FIELDS + 12 + k] = ph[k];
         if (!P->hip_ok(hipEventRecord(P->ev_kern[b], cs), "event")) return;
         if (!P->tr.empty()) P->tr[b * AWQ_STREAM_TRACE_FIELDS + 3] = now_s() - P->t0;
         if (!P->hip_ok(hipStreamWaitEvent(d2h, P->ev_kern[b], 0), "stream wait")) return;
@@ -430,9 +442,9 @@ int awq_stream_start(const awq_stream_item* items, int n, const awq_stream_confi
     if (c.bits != 4 && c.bits != 8) return awq::set_error(AWQ_EINVAL, "Unsupported bit width. Supported: 4, 8.");
     if (c.group_size <= 0) return awq::set_error(AWQ_EINVAL, "Group size must be a positive integer");
     if (c.nslots < 2 || c.readers < 1 || c.slot_bytes <= 0 || c.slot_bytes % 4096 || !c.host_staging ||
-        !c.dev_staging || !c.host_tables || !c.dev_tables)
+        !c.dev_staging)
         return awq::set_error(AWQ_EINVAL, "bad stream configuration (nslots >= 2, readers >= 1, slot_bytes a "
-                                          "multiple of 4096, staging and table buffers)");
+                                          "multiple of 4096, staging buffers)");
     for (int i = 0; i < n; ++i) {
         const awq_stream_item& it = items[i];
         if (it.dtype < AWQ_DTYPE_BF16 || it.dtype > AWQ_DTYPE_F64 || it.rows < 0 || it.K < 0 || it.fd < 0 ||
@@ -444,6 +456,8 @@ int awq_stream_start(const awq_stream_item* items, int n, const awq_stream_confi
     Pipeline* P = new Pipeline();
     P->items.assign(items, items + n);
     P->cfg = c;
+    P->tb = awq_stream_table_bytes(c.slot_bytes);
+    P->stride = P->tb + c.slot_bytes;
     (void)hipGetDevice(&P->device);
     std::string why;
     if (int rc = plan(*P, why)) {

@@ -46,7 +46,7 @@
 extern "C" {
 #endif
 
-#define AWQ_HIP_ABI_VERSION 11
+#define AWQ_HIP_ABI_VERSION 12
 
 /* dtype codes of the input weights (torch dtypes the reference accepts, awq.py:397) */
 enum { AWQ_DTYPE_BF16 = 0, AWQ_DTYPE_F16 = 1, AWQ_DTYPE_F32 = 2, AWQ_DTYPE_F64 = 3 };
@@ -269,10 +269,10 @@ typedef struct awq_stream_config {
     int32_t trace_batches;                          /* capacity of `trace`, in batches */
     int64_t slot_bytes;          /* input bytes per staging slot, multiple of 4096 */
     int64_t first_batch_bytes;   /* capacity of the first batch (<= slot_bytes; 0 = slot_bytes) */
-    void* host_staging;          /* pinned host, nslots * slot_bytes */
-    void* dev_staging;           /* device, nslots * slot_bytes */
-    void* host_tables;           /* pinned host, nslots * awq_stream_table_bytes(slot_bytes) */
-    void* dev_tables;            /* device, the same size */
+    void* host_staging;          /* pinned host, nslots * (awq_stream_table_bytes(slot_bytes) +
+                                    slot_bytes): each slot = its batch's descriptor / tensor-table
+                                    area, then its input; one H2D carries both */
+    void* dev_staging;           /* device, the same size */
     void* compute_stream;
     void* h2d_stream;
     void* d2h_stream;
@@ -283,7 +283,8 @@ typedef struct awq_stream_config {
                                     D2H done (HIP event clock, from an event on the H2D stream
                                     recorded at start); seconds spent inside the H2D call and
                                     inside the D2H calls; seconds of the batch's host planning,
-                                    table uploads, ragged launches and per-tensor launches;
+                                    of waiting for the slot's previous kernels, of the ragged
+                                    launches and of the per-tensor launches;
                                     batches past trace_batches are not traced. */
 } awq_stream_config;
 
@@ -297,8 +298,8 @@ typedef struct awq_stream_stats {
     double wait_slot_s;          /* submitter waiting for a slot's previous kernels */
 } awq_stream_stats;
 
-/* Per-slot descriptor-table bytes (descriptors + tensor tables of up to
- * AWQ_STREAM_MAX_BATCH_ITEMS pieces). */
+/* Per-slot descriptor / tensor-table bytes (descriptors + tensor tables of up to
+ * AWQ_STREAM_MAX_BATCH_ITEMS pieces): the head of every staging slot; a multiple of 4096. */
 int64_t awq_stream_table_bytes(int64_t slot_bytes);
 
 /* Plan the batches and start the pipeline on its own native threads; returns at once.

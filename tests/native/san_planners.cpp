@@ -46,7 +46,7 @@ int main() {
         checks += 4;
     }
     // ---- stream pipeline planning (events cannot be created without a GPU: error after planning) ----
-    static char host_stage[3 * 65536], host_tab[1 << 20];
+    static char host_stage[3 * (65536 + (1 << 20))];   // 3 slots of table area + input
     for (int trial = 0; trial < 200; ++trial) {
         const int n = (int)(next() % 60);
         std::vector<awq_stream_item> it(n);
@@ -65,7 +65,6 @@ int main() {
         c.bits = 4; c.symmetric = 0; c.group_size = 128; c.readers = 3; c.nslots = 3;
         c.slot_bytes = 65536; c.first_batch_bytes = (next() & 1) ? 16384 : 0;
         c.host_staging = host_stage; c.dev_staging = (void*)(uintptr_t)0x5000000;
-        c.host_tables = host_tab; c.dev_tables = (void*)(uintptr_t)0x6000000;
         void* h = nullptr;
         const int rc = awq_stream_start(it.data(), n, &c, &h);
         if (rc == 0) {   // (a GPU is present after all: run to completion would read fd 0; stop)

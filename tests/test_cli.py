@@ -154,6 +154,77 @@ def test_chunk_writer_close_marks_unfinished_failed(tmp_path):
     assert meta["num_tensors"] == 1 and meta["tensor_to_chunk"] == {"a": 0}
 
 
+def test_cpu_share_reads_cgroup_quota(monkeypatch, tmp_path):
+    """cpu_share: the affinity set, capped by a cgroup v2 quota (the GPU box: cpu.max 1600000
+    100000 = 16 CPUs while os.cpu_count() shows the node's 256)."""
+    import builtins
+    from awq_quantizer import main as m
+    real_open = builtins.open
+    monkeypatch.setattr(m.os, "sched_getaffinity", lambda pid: set(range(256)), raising=False)
+
+    def fake_open(path, *a, **k):
+        if path == "/sys/fs/cgroup/cpu.max":
+            q = tmp_path / "cpu.max"
+            q.write_text(quota)
+            return real_open(q, *a, **k)
+        return real_open(path, *a, **k)
+    monkeypatch.setattr(builtins, "open", fake_open)
+    quota = "1600000 100000\n"
+    assert m.cpu_share() == 16
+    quota = "max 100000\n"
+    assert m.cpu_share() == 256
+    quota = "50000 100000\n"
+    assert m.cpu_share() == 1
+
+
+def test_writer_threads_by_output_size(monkeypatch):
+    """Chunk-writer pool sized by output bytes: 2-4 writers below ~2 GB of output (more
+    stalled the pipeline's HIP calls), up to 8 above; STREAM_OPTS["writers"] overrides."""
+    from awq_quantizer import main as m
+    from awq_quantizer.model_loading.safetensors_loader import TensorInfo
+    monkeypatch.setattr(m, "cpu_share", lambda: 16)
+
+    def infos(total):
+        return [TensorInfo("w", "f", torch.bfloat16, (total // 2,))]
+    assert m.writer_threads(infos(662 << 20), packed=True) == 4          # opt-350m packed
+    assert m.writer_threads(infos(662 << 20), packed=False) == 4         # ~1.3 GB reference output
+    assert m.writer_threads(infos(16 << 30), packed=True) == 8           # Llama-3-8B packed: 4.2 GB out
+    monkeypatch.setattr(m, "cpu_share", lambda: 4)
+    assert m.writer_threads(infos(16 << 30), packed=False) == 2
+    monkeypatch.setitem(m.STREAM_OPTS, "writers", 3)
+    assert m.writer_threads(infos(16 << 30), packed=True) == 3
+
+
+def test_chunk_writer_widens_pool_at_close(tmp_path, monkeypatch):
+    """While producers run at most `writers` chunk writes run at once; close() releases the
+    rest of the pool for the backlog (same files either way)."""
+    import threading
+    import time as _t
+    from awq_quantizer import main as m
+    monkeypatch.setattr(m, "cpu_share", lambda: 16)          # tail pool: 8
+    active, peak, lock = [0], [0], threading.Lock()
+    real = m._write_chunk
+
+    def slow_write(*a, **k):
+        with lock:
+            active[0] += 1
+            peak[0] = max(peak[0], active[0])
+        _t.sleep(0.05)
+        real(*a, **k)
+        with lock:
+            active[0] -= 1
+    monkeypatch.setattr(m, "_write_chunk", slow_write)
+    order = [f"t{i}" for i in range(16)]
+    w = m.ChunkWriter(order, str(tmp_path), 1, False, writers=2)
+    for n in order:
+        w.done(n, {"q": torch.zeros(2), "bits": torch.tensor(4)})
+    _t.sleep(0.12)
+    assert peak[0] <= 2                                      # gated while "producing"
+    w.close()
+    assert peak[0] > 2                                       # the backlog drained wider
+    assert json.load(open(tmp_path / "metadata.json"))["num_chunks"] == 16
+
+
 def test_loader_read_into_matches_safetensors(tmp_path):
     """read_into (pread at the header offsets, the CLI's pinned-read path) == safetensors'
     own read for every dtype, empty tensors and several files."""

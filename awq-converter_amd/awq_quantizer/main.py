@@ -215,7 +215,7 @@ def save_model_in_chunks(tensors: Dict[str, Dict[str, torch.Tensor]], output_dir
     qparams = {k: (first[k].item() if k in first else None) for k in ("bits", "group_size", "symmetric")}
     tensor_to_chunk = {}
     # chunk files are independent: written by a small thread pool (torch.save releases the GIL)
-    with ThreadPoolExecutor(max_workers=min(8, max(2, (os.cpu_count() or 4) // 2))) as pool:
+    with ThreadPoolExecutor(max_workers=min(8, max(2, cpu_share() // 2))) as pool:
         futs = []
         for c in range(num_chunks):
             chunk_names = names[c * chunk_size:(c + 1) * chunk_size]
@@ -608,8 +608,15 @@ def quantize_stream_native(loader, infos: List[TensorInfo], quantizer: AWQQuanti
     t_alloc = time.perf_counter()
     arena = {dt: torch.empty(max(dev_total[dt], 8), dtype=dt, device=dev) for dt in kinds}
     t_arena = time.perf_counter()
-    hosts = {} if keep_on_device else {s: {dt: torch.empty(max(n[dt], 8), dtype=dt, pin_memory=True) for dt in kinds}
-                                       for s, n in seg_size.items()}
+    hosts = {}
+    if not keep_on_device:
+        # page-locking is the cost of a process's first run (≈0.1 s per GB): the per-chunk
+        # buffers are pinned by a few threads at once
+        jobs = [(sg, dt, max(n[dt], 8)) for sg, n in seg_size.items() for dt in kinds]
+        with ThreadPoolExecutor(max_workers=min(8, max(1, cpu_share() // 2), len(jobs))) as pool:
+            bufs = list(pool.map(lambda j: torch.empty(j[2], dtype=j[1], pin_memory=True), jobs))
+        for (sg, dt, _), b in zip(jobs, bufs):
+            hosts.setdefault(sg, {})[dt] = b
     lib = _hip.load_library()
     arr = (_hip.StreamItem * max(1, len(items)))()
     dptr = {dt: arena[dt].data_ptr() for dt in kinds}

@@ -1140,15 +1140,16 @@ __global__ __launch_bounds__(128) void awq_rowgroup_kernel(const void* __restric
     const __amdgpu_buffer_rsrc_t rw = rsrc((const char*)w + a0, lim);
     if (__builtin_expect(16u * (uint32_t)nch <= lim, 1)) {
         // every 16-B load of the segment in flight before the first LDS store (a load ->
-        // store loop waits out one memory round trip per load); lanes past the end repeat
-        // the last chunk's address and store nothing
+        // store loop waits out one memory round trip per load).  All 8 loads are issued
+        // unconditionally: offsets past the segment fall outside the buffer range (lim) and
+        // read zeros without a memory access, and no register needs a value on a skipped
+        // path (conditional loads cost 28 v_mov per wave of phi copies); lanes past the end
+        // store nothing
         for (int c0 = 0; c0 < nch; c0 += 8 * NT) {
             u4 v[8];
 #pragma unroll
             for (int k = 0; k < 8; ++k)
-                if (c0 + NT * k < nch)                   // uniform
-                    v[k] = __builtin_amdgcn_raw_buffer_load_b128(rw, (uint32_t)(16 * min(c0 + NT * k + lane, nch - 1)),
-                                                                 0, AWQ_LOAD_AUX);
+                v[k] = __builtin_amdgcn_raw_buffer_load_b128(rw, (uint32_t)(16 * (c0 + NT * k + lane)), 0, AWQ_LOAD_AUX);
 #pragma unroll
             for (int k = 0; k < 8; ++k)
                 if (c0 + NT * k + lane < nch) *(u4*)((char*)stage + 16 * (c0 + NT * k + lane)) = v[k];

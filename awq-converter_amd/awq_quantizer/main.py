@@ -609,7 +609,20 @@ def quantize_stream_native(loader, infos: List[TensorInfo], quantizer: AWQQuanti
     arena = {dt: torch.empty(max(dev_total[dt], 8), dtype=dt, device=dev) for dt in kinds}
     t_arena = time.perf_counter()
     hosts = {}
-    if not keep_on_device:
+    if not keep_on_device and STREAM_OPTS.get("host_arena"):
+        # (measurement option) one pinned allocation per dtype, every chunk's buffer a
+        # separate storage carved from it (torch.frombuffer: torch.save writes only the
+        # chunk's bytes)
+        for dt in kinds:
+            tot = sum(max(n[dt], 8) for n in seg_size.values())
+            big = torch.empty(tot, dtype=dt, pin_memory=True)
+            raw, off = big.view(torch.uint8).numpy(), 0
+            for sg, n in seg_size.items():
+                m = max(n[dt], 8)
+                hosts.setdefault(sg, {})[dt] = torch.frombuffer(raw, dtype=dt, count=m, offset=off * es_of[dt])
+                off += m
+            hosts.setdefault("_keep", {})[dt] = big
+    elif not keep_on_device:
         # page-locking is the cost of a process's first run (≈0.1 s per GB): the per-chunk
         # buffers are pinned by a few threads at once
         jobs = [(sg, dt, max(n[dt], 8)) for sg, n in seg_size.items() for dt in kinds]

@@ -609,10 +609,11 @@ def quantize_stream_native(loader, infos: List[TensorInfo], quantizer: AWQQuanti
     arena = {dt: torch.empty(max(dev_total[dt], 8), dtype=dt, device=dev) for dt in kinds}
     t_arena = time.perf_counter()
     hosts = {}
-    if not keep_on_device and STREAM_OPTS.get("host_arena"):
-        # (measurement option) one pinned allocation per dtype, every chunk's buffer a
-        # separate storage carved from it (torch.frombuffer: torch.save writes only the
-        # chunk's bytes)
+    if not keep_on_device and STREAM_OPTS.get("host_arena", 1):
+        # one pinned allocation per dtype, every chunk's buffer a separate storage carved
+        # from it (torch.frombuffer: torch.save writes only the chunk's bytes).  With one
+        # pinned allocation per chunk (STREAM_OPTS host_arena=0), D2H calls into a chunk's
+        # buffer stalled the submitter for 7-8 ms at a time (profiles/round3/cli/r3r_*)
         for dt in kinds:
             tot = sum(max(n[dt], 8) for n in seg_size.values())
             big = torch.empty(tot, dtype=dt, pin_memory=True)
@@ -1125,7 +1126,7 @@ TIMINGS: Dict[str, float] = {}   # phase times of the last main() call (scripts/
 # native pipeline overrides for measurement scripts (scripts/cli_profile.py --stream-opts):
 # slot_bytes, nslots, copy_streams (1: H2D and D2H share one stream), trace (1: per-batch
 # timestamps, include/awq_hip.h awq_stream_config.trace), readers (pread threads), writers
-# (ChunkWriter threads)
+# (ChunkWriter threads), host_arena (0: one pinned buffer per output chunk)
 STREAM_OPTS: Dict[str, int] = {}
 
 

@@ -1,0 +1,673 @@
+// awq_rowgroup.hip — row-segment quantizer: bf16 / fp16 / fp32 weights with any group size
+// up to 512 (fp32: 256) and any row length K (gfx950).
+//
+// Serves the reference's arbitrary group_size (src/awq_quantizer/quantization/awq.py:102,
+// 286-374: groups along each row, the last zero-padded, awq.py:337-339) outside the
+// streaming kernel's 32 / 64 / 128 / 256, with the same per-group arithmetic
+// (awq.py:173-250; awq_quant.h) and packed outputs written directly.
+#include "awq_quant.h"
+
+namespace awq {
+namespace {
+
+// ---------------------------------------------------------------------------------------
+// Any group size up to 512 (bf16 / fp16; 256 for fp32), any K: row-segment tiles.
+//
+// A tile = GPT consecutive groups of one row (GPT a multiple of 8 up to 64; the cost model
+// picks 8, 16, 32 or 64), one 64-lane wave per tile:
+//   stage   the segment's bytes go to LDS with 16-B loads, all in flight at once (16-B
+//           aligned start; the tensor's last bytes go by 2-B loads);
+//   pass 1  lane (grp, j) owns chunk j of group grp (P lanes per group = the largest power
+//           of two <= 64 / the tile's groups, C = ceil(L / P) elements each) and reduces
+//           the raw-bits min/max over it (packed 16-bit max/min, two chains) and over the
+//           group's P lanes, then computes the group's parameters (the streaming kernel's
+//           group_range / params_from_range: the same verified arithmetic) into LDS;
+//   pass 2  lane = 8 consecutive elements (one qweight word at 4 bits): parameters from LDS
+//           per half (L % 4 == 0) or per element, the field chain (bf16: packed f32 mul /
+//           add), one coalesced word store.
+// Tile boundaries fall on qweight and qzeros word boundaries (GPT * L and GPT are multiples
+// of 8), so no word is shared between waves.  Replaces the one-wave-per-group generic
+// kernel plus its int32 staging and pack passes (~10.5 B moved per element) for these
+// shapes.
+// ---------------------------------------------------------------------------------------
+constexpr int kRgStageBytes = 8192;    // eligibility: 8 groups fit (any GPT the cost model picks)
+constexpr int kRgStageMax = 16384;     // tuning override ceiling (rg_gpt)
+
+template <typename F>
+struct RgSlot {
+    typedef typename std::conditional<F::kBytes == 2, uint16_t, uint32_t>::type T;
+    static constexpr uint32_t kNan = F::kBytes == 2 ? 0xFFFFu : 0xFFFFFFFFu;   // field code of NaN
+    __device__ static int sext(uint32_t v) { return F::kBytes == 2 ? (int)(int16_t)v : (int)v; }
+    __device__ static float dec(uint32_t v) { return F::kBytes == 2 ? F::dec(v) : __uint_as_float(v); }
+};
+
+// packed field (q - qmin) of one element of a group with a positive finite scale, before
+// the round + clamp (pack8_cvt / field_q)
+template <typename F, int BITS, bool SYM, bool PLAIN>
+__device__ __forceinline__ float field1_fast(float x, float r, float z, float s) {
+    constexpr float HALF = (float)(1 << (BITS - 1));
+    const float t = PLAIN ? F::quot_plain(x, r) : F::quot(x, s, r);
+    float u;
+    if (SYM && F::kWide) u = __builtin_rintf(t) + HALF;
+    else if (SYM) u = t + HALF;
+    else u = F::rn(t + F::as_fmt(z));
+    return u;
+}
+
+// the field's value: clamp(rint(u), 0, 2^BITS - 1)
+template <int BITS>
+__device__ __forceinline__ float field_q(float u) {
+    return __builtin_fminf(__builtin_fmaxf(__builtin_rintf(u), 0.0f), (float)((1 << BITS) - 1));
+}
+
+// the same for 8 bf16 elements, multiply and add as packed f32 pairs (v_pk_mul_f32 /
+// v_pk_add_f32: each half is the IEEE f32 op, rounded to bf16 after it as above)
+template <int BITS, bool SYM>
+__device__ __forceinline__ void field8_bf16(const float (&x)[8], const float (&r)[8], const float (&z)[8],
+                                            float (&q)[8]) {
+    constexpr float HALF = (float)(1 << (BITS - 1));
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const f2 p = (f2){x[2 * i], x[2 * i + 1]} * (f2){r[2 * i], r[2 * i + 1]};
+        const f2 t = {rn_bf16(p.x), rn_bf16(p.y)};
+        f2 u;
+        if (SYM) {
+            u = t + (f2){HALF, HALF};                       // exact (as field1_fast)
+        } else {
+            const f2 a = t + (f2){z[2 * i], z[2 * i + 1]};
+            u = (f2){rn_bf16(a.x), rn_bf16(a.y)};
+        }
+        q[2 * i] = u.x;
+        q[2 * i + 1] = u.y;
+    }
+}
+
+// raw-bits min/max over each aligned block of 2^lgP lanes (a group's lanes in pass 1):
+// DPP quad / mirror steps and the row-pair swaps (wave-uniform lgP), every lane ends with
+// its block's result
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp_mov(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xF, 0xF, true);
+}
+template <int CTRL>
+__device__ __forceinline__ void rg_step(int& smax, uint32_t& umax, uint32_t& umin) {
+    smax = max(smax, (int)dpp_mov<CTRL>((uint32_t)smax));
+    umax = max(umax, dpp_mov<CTRL>(umax));
+    umin = min(umin, dpp_mov<CTRL>(umin));
+}
+__device__ __forceinline__ void rg_reduce(int& smax, uint32_t& umax, uint32_t& umin, int lgP) {
+    if (lgP >= 1) rg_step<0xB1>(smax, umax, umin);     // quad_perm [1,0,3,2]
+    if (lgP >= 2) rg_step<0x4E>(smax, umax, umin);     // quad_perm [2,3,0,1]
+    if (lgP >= 3) rg_step<0x141>(smax, umax, umin);    // row_half_mirror
+    if (lgP >= 4) rg_step<0x140>(smax, umax, umin);    // row_mirror
+    if (lgP >= 5) {                                    // rows 2k <-> 2k+1
+        const auto a = __builtin_amdgcn_permlane16_swap((unsigned)smax, (unsigned)smax, false, false);
+        const auto b = __builtin_amdgcn_permlane16_swap(umax, umax, false, false);
+        const auto c = __builtin_amdgcn_permlane16_swap(umin, umin, false, false);
+        smax = max((int)a[0], (int)a[1]);
+        umax = max((uint32_t)b[0], (uint32_t)b[1]);
+        umin = min((uint32_t)c[0], (uint32_t)c[1]);
+    }
+    if (lgP >= 6) {                                    // halves
+        const auto a = __builtin_amdgcn_permlane32_swap((unsigned)smax, (unsigned)smax, false, false);
+        const auto b = __builtin_amdgcn_permlane32_swap(umax, umax, false, false);
+        const auto c = __builtin_amdgcn_permlane32_swap(umin, umin, false, false);
+        smax = max((int)a[0], (int)a[1]);
+        umax = max((uint32_t)b[0], (uint32_t)b[1]);
+        umin = min((uint32_t)c[0], (uint32_t)c[1]);
+    }
+}
+
+#ifndef AWQ_RG_UNROLL
+#define AWQ_RG_UNROLL 8
+#endif
+
+// raw-bits (signed max, unsigned max, unsigned min) of the 16-bit stage slots [s_lo, s_hi),
+// s_hi > s_lo, from the identities: packed 16-bit max/min over whole dwords (two chains); an
+// edge dword holding one foreign element gets a copy of its own element there
+__device__ __forceinline__ void rg_range16(const uint32_t* st32, int s_lo, int s_hi, int& smax, uint32_t& umax,
+                                           uint32_t& umin) {
+    const int d_lo = s_lo >> 1, d_hi = (s_hi + 1) >> 1;
+    s2 sm = {(short)-32768, (short)-32768}, sm_b = sm;
+    us2 um = {0, 0}, um_b = um;
+    us2 un = {(unsigned short)0xFFFF, (unsigned short)0xFFFF}, un_b = un;
+    auto acc = [&](uint32_t v) {
+        sm = __builtin_elementwise_max(sm, as_s2(v));
+        um = __builtin_elementwise_max(um, as_us2(v));
+        un = __builtin_elementwise_min(un, as_us2(v));
+    };
+    auto acc_b = [&](uint32_t v) {
+        sm_b = __builtin_elementwise_max(sm_b, as_s2(v));
+        um_b = __builtin_elementwise_max(um_b, as_us2(v));
+        un_b = __builtin_elementwise_min(un_b, as_us2(v));
+    };
+    uint32_t first = st32[d_lo];
+    if (s_lo & 1) first = __builtin_amdgcn_perm(first, first, 0x03020302u);   // low half := high
+    if (d_hi - d_lo == 1 && (s_hi & 1)) first = __builtin_amdgcn_perm(first, first, 0x01000100u);
+    acc(first);
+    if (d_hi - d_lo > 1) {
+        int d = d_lo + 1;
+        for (; d + 4 <= d_hi - 1; d += 4) {
+            const uint32_t v0 = st32[d], v1 = st32[d + 1], v2 = st32[d + 2], v3 = st32[d + 3];
+            acc(v0);
+            acc_b(v1);
+            acc(v2);
+            acc_b(v3);
+        }
+        if (d + 2 <= d_hi - 1) {
+            const uint32_t v0 = st32[d], v1 = st32[d + 1];
+            acc(v0);
+            acc_b(v1);
+            d += 2;
+        }
+        if (d < d_hi - 1) acc_b(st32[d]);
+        uint32_t last = st32[d_hi - 1];
+        if (s_hi & 1) last = __builtin_amdgcn_perm(last, last, 0x01000100u);        // high half := low
+        acc(last);
+    }
+    sm = __builtin_elementwise_max(sm, sm_b);
+    um = __builtin_elementwise_max(um, um_b);
+    un = __builtin_elementwise_min(un, un_b);
+    smax = max((int)sm.x, (int)sm.y);
+    umax = (uint32_t)max((int)um.x, (int)um.y);
+    umin = (uint32_t)min((int)un.x, (int)un.y);
+}
+
+// LDS: the segment's stage (dynamic, sized by the launch to the tile: 1.6-8 KiB) + 1.3 KiB
+template <typename F, int BITS, bool SYM, int SPLIT, bool P1C>
+__global__ __launch_bounds__(128) void awq_rowgroup_kernel(const void* __restrict__ w, int64_t rows, int64_t K,
+                                                             int64_t L, int lgP, int GPT, uint32_t tiles_per_row,
+                                                             int64_t G, int C, float invL,
+                                                             int32_t* __restrict__ qweight, int32_t* __restrict__ qzeros,
+                                                             uint16_t* __restrict__ scales,
+                                                             int32_t* __restrict__ tensor_q, int32_t* __restrict__ zeros,
+                                                             uint32_t nan_code) {
+    typedef RgSlot<F> SL;
+    typedef typename SL::T S;
+    constexpr int QMIN = SYM ? -(1 << (BITS - 1)) : 0;
+    constexpr uint32_t MASK = (1u << BITS) - 1u;
+    constexpr int PER = 32 / BITS;             // elements (and groups) per packed word
+    constexpr uint32_t NANF = (uint32_t)(0u - (uint32_t)QMIN) & MASK;   // field of INT32_MIN - qmin
+    extern __shared__ __attribute__((aligned(16))) unsigned char rg_lds[];
+    S* stage = (S*)rg_lds;                              // rg_stage_bytes(): the segment + its alignment skew
+    __shared__ uint32_t zst[64];
+    __shared__ float4 prm[64];                          // per group: r, z, s, special
+    __shared__ int not_plain;                           // a group of the tile needs the full quotient
+    __shared__ int acc_smax[P1C ? 64 : 1];              // P1C: per-group raw-bits reductions
+    __shared__ uint32_t acc_umax[P1C ? 64 : 1], acc_umin[P1C ? 64 : 1];
+    // one tile per workgroup of 1 or 2 waves (host-chosen: two waves share a large tile's LDS
+    // stage, so a whole-row tile keeps 8 waves per SIMD resident)
+    const int lane = threadIdx.x, NT = blockDim.x;
+    // (host-side G, C, log2 P and a 32-bit tile split: 64-bit divisions per wave on the
+    //  CU's shared scalar unit were a visible part of the per-tile cost)
+    const uint32_t tile = blockIdx.x;   // (an XCD-contiguous tile order measured no different: r2z3)
+    const uint32_t r32 = tile / tiles_per_row;
+    const int64_t r = r32;
+    const int64_t g0 = (int64_t)(tile - r32 * tiles_per_row) * GPT;
+    const int ng = (int)min((int64_t)GPT, G - g0);
+    if (ng < GPT) {   // the row's last, partial tile: more lanes per group (wave-uniform)
+        lgP = min(6, 31 - __builtin_clz((unsigned)NT / (unsigned)ng));
+        C = (int)((L + (1 << lgP) - 1) >> lgP);
+    }
+    const int P = 1 << lgP;
+    const int64_t kb = g0 * L, ke = min((g0 + ng) * L, K);     // the row segment [kb, ke)
+    const int n_el = (int)(ke - kb);
+    // ---- stage the segment's bytes (from a 16-B aligned start) in LDS ----
+    const uint64_t byte0 = (uint64_t)(r * K + kb) * F::kBytes;
+    const uint64_t a0 = byte0 & ~(uint64_t)15;
+    const int skew = (int)(byte0 - a0) / F::kBytes;               // slot of element kb
+    const uint64_t total = (uint64_t)rows * (uint64_t)K * F::kBytes;
+    const int nbytes = (int)(byte0 - a0) + n_el * F::kBytes;
+    const int nch = (nbytes + 15) >> 4;
+    const uint32_t lim = (uint32_t)min(total - a0, (uint64_t)nch * 16);
+    const __amdgpu_buffer_rsrc_t rw = rsrc((const char*)w + a0, lim);
+    if (__builtin_expect(16u * (uint32_t)nch <= lim, 1)) {
+        // every 16-B load of the segment in flight before the first LDS store (a load ->
+        // store loop waits out one memory round trip per load).  All 8 loads are issued
+        // unconditionally: offsets past the segment fall outside the buffer range (lim) and
+        // read zeros without a memory access, and no register needs a value on a skipped
+        // path (conditional loads cost 28 v_mov per wave of phi copies); lanes past the end
+        // store nothing
+        for (int c0 = 0; c0 < nch; c0 += 8 * NT) {
+            u4 v[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k)
+                v[k] = __builtin_amdgcn_raw_buffer_load_b128(rw, (uint32_t)(16 * (c0 + NT * k + lane)), 0, AWQ_LOAD_AUX);
+#pragma unroll
+            for (int k = 0; k < 8; ++k)
+                if (c0 + NT * k + lane < nch) *(u4*)((char*)stage + 16 * (c0 + NT * k + lane)) = v[k];
+        }
+    } else
+#pragma unroll 4
+    for (int c = lane; c < nch; c += NT) {
+        if (__builtin_expect(16u * c + 16u <= lim, 1)) {
+            *(u4*)((char*)stage + 16 * c) = __builtin_amdgcn_raw_buffer_load_b128(rw, (uint32_t)(16 * c), 0, AWQ_LOAD_AUX);
+        } else {   // the tensor's last bytes: a 16-B load straddling the range end would read as all zeros
+            for (int h = 0; h < 8; ++h)
+                ((uint16_t*)stage)[8 * c + h] = __builtin_amdgcn_raw_buffer_load_b16(rw, (uint32_t)(16 * c + 2 * h), 0, 0);
+        }
+    }
+    if (lane == 0) not_plain = 0;
+    if constexpr (P1C) {
+        // identities; the row's zero-padded last group starts from 0 (awq.py:337-339: the
+        // zeros join its min/max)
+        if (lane < ng) {
+            const bool pad = lane == ng - 1 && n_el - lane * (int)L < (int)L;
+            acc_smax[lane] = pad ? 0 : INT_MIN;
+            acc_umax[lane] = 0u;
+            acc_umin[lane] = pad ? 0u : F::kOnes;
+        }
+    }
+    __syncthreads();
+    if constexpr (P1C) {
+        // ---- pass 1, lanes split evenly over the tile's groups: Q = NT / ng lanes per group
+        //      (any count — not only a power of two; 3 for 41 groups of a 128-lane tile where
+        //      the by-groups pass keeps 2), each lane reduces one even-length run of its group
+        //      and merges it into the group's LDS slots (ds_max / ds_min) ----
+        const int Q = NT / ng;                            // >= 1: ng <= 64 <= NT
+        const int grp = (int)((float)lane * __builtin_amdgcn_rcpf((float)Q) + 1e-3f);   // lane / Q (lane < 128)
+        const int jq = lane - grp * Q;
+        if (grp < ng) {
+            const int glen = min((int)L, n_el - grp * (int)L);
+            const int cq = ((glen + Q - 1) / Q + 1) & ~1;   // even: runs start on dword pairs
+            const int cb = min(jq * cq, glen), ce = min(cb + cq, glen);
+            if (ce > cb) {
+                const int base = skew + grp * (int)L;
+                int smx;
+                uint32_t umx, umn;
+                if constexpr (F::kBytes == 2) {
+                    rg_range16((const uint32_t*)stage, base + cb, base + ce, smx, umx, umn);
+                } else {
+                    smx = INT_MIN;
+                    umx = 0u;
+                    umn = F::kOnes;
+                    int i1 = cb;
+                    for (; i1 + AWQ_RG_UNROLL <= ce; i1 += AWQ_RG_UNROLL) {
+                        uint32_t v[AWQ_RG_UNROLL];
+#pragma unroll
+                        for (int u = 0; u < AWQ_RG_UNROLL; ++u) v[u] = stage[base + i1 + u];
+#pragma unroll
+                        for (int u = 0; u < AWQ_RG_UNROLL; ++u) {
+                            smx = max(smx, SL::sext(v[u]));
+                            umx = max(umx, v[u]);
+                            umn = min(umn, v[u]);
+                        }
+                    }
+                    for (; i1 < ce; ++i1) {
+                        const uint32_t v = stage[base + i1];
+                        smx = max(smx, SL::sext(v));
+                        umx = max(umx, v);
+                        umn = min(umn, v);
+                    }
+                }
+                atomicMax(&acc_smax[grp], smx);
+                atomicMax(&acc_umax[grp], umx);
+                atomicMin(&acc_umin[grp], umn);
+            }
+        }
+        __syncthreads();
+        // ---- the tile's group parameters: one lane per group (wave 0: ng <= 64) ----
+        if (lane < ng) {
+            float gmn, gmx;
+            bool gnan;
+            group_range<F, SYM>(acc_smax[lane], acc_umax[lane], acc_umin[lane], gmn, gmx, gnan);
+            const GroupParams p = params_from_range<F, BITS, SYM>(gmn, gmx);
+            const bool special = !F::fast(p.r);
+            if (F::kHasPlain && !F::plain_ok(p.s)) not_plain = 1;
+            const int64_t gi = r * G + g0 + lane;
+            if (scales) scales[gi] = f16_bits(p.s, gnan, nan_code);
+            if (zeros) zeros[gi] = __builtin_isnan(p.z) ? INT32_MIN : (int32_t)p.z;
+            zst[lane] = __builtin_isnan(p.z) ? NANF : ((uint32_t)((int)p.z - QMIN) & MASK);
+            prm[lane] = (float4){p.r, p.z, p.s, special ? 1.0f : 0.0f};
+        }
+    } else {
+    // ---- this lane's chunk of its group ----
+    const int grp = lane >> lgP, j = lane & (P - 1);
+    const bool active = grp < ng;
+    const int glen = active ? min((int)L, n_el - grp * (int)L) : 0;   // elements in the row (tail: fewer)
+    const int cb = min(j * C, glen), ce = min(cb + C, glen);
+    const int base = skew + grp * (int)L;
+    const bool padded = active && glen < L;                    // awq.py:337-339: zeros join the min/max
+    int smax = padded ? 0 : INT_MIN;
+    uint32_t umax = 0, umin = padded ? 0u : F::kOnes;
+    if constexpr (F::kBytes == 2) {
+        // raw 16-bit pairs with packed max/min (v_pk_*_i16/u16: two elements per instruction);
+        // an edge dword holding one foreign element gets a copy of its own element there
+        const int s_lo = base + cb, s_hi = base + ce;
+        if (s_hi > s_lo) {
+            const uint32_t* st32 = (const uint32_t*)stage;
+            const int d_lo = s_lo >> 1, d_hi = (s_hi + 1) >> 1;
+            s2 sm = {(short)(padded ? 0 : -32768), (short)(padded ? 0 : -32768)};
+            us2 um = {0, 0};
+            us2 un = {(unsigned short)(padded ? 0 : 0xFFFF), (unsigned short)(padded ? 0 : 0xFFFF)};
+            s2 sm_b = sm;                                 // a second, independent set of chains
+            us2 um_b = um, un_b = un;
+            auto acc = [&](uint32_t v) {
+                sm = __builtin_elementwise_max(sm, as_s2(v));
+                um = __builtin_elementwise_max(um, as_us2(v));
+                un = __builtin_elementwise_min(un, as_us2(v));
+            };
+            auto acc_b = [&](uint32_t v) {
+                sm_b = __builtin_elementwise_max(sm_b, as_s2(v));
+                um_b = __builtin_elementwise_max(um_b, as_us2(v));
+                un_b = __builtin_elementwise_min(un_b, as_us2(v));
+            };
+            uint32_t first = st32[d_lo];
+            if (s_lo & 1) first = __builtin_amdgcn_perm(first, first, 0x03020302u);   // low half := high
+            if (d_hi - d_lo == 1 && (s_hi & 1)) first = __builtin_amdgcn_perm(first, first, 0x01000100u);
+            acc(first);
+            if (d_hi - d_lo > 1) {
+                int d = d_lo + 1;
+                for (; d + 4 <= d_hi - 1; d += 4) {
+                    const uint32_t v0 = st32[d], v1 = st32[d + 1], v2 = st32[d + 2], v3 = st32[d + 3];
+                    acc(v0);
+                    acc_b(v1);
+                    acc(v2);
+                    acc_b(v3);
+                }
+                if (d + 2 <= d_hi - 1) {                  // <= 3 left: no loop
+                    const uint32_t v0 = st32[d], v1 = st32[d + 1];
+                    acc(v0);
+                    acc_b(v1);
+                    d += 2;
+                }
+                if (d < d_hi - 1) acc_b(st32[d]);
+                uint32_t last = st32[d_hi - 1];
+                if (s_hi & 1) last = __builtin_amdgcn_perm(last, last, 0x01000100u);        // high half := low
+                acc(last);
+            }
+            sm = __builtin_elementwise_max(sm, sm_b);
+            um = __builtin_elementwise_max(um, um_b);
+            un = __builtin_elementwise_min(un, un_b);
+            smax = max((int)sm.x, (int)sm.y);
+            umax = (uint32_t)max((int)um.x, (int)um.y);
+            umin = (uint32_t)min((int)un.x, (int)un.y);
+        }
+    } else {
+        int i1 = cb;
+        for (; i1 + AWQ_RG_UNROLL <= ce; i1 += AWQ_RG_UNROLL) {   // independent LDS reads in flight
+            uint32_t v[AWQ_RG_UNROLL];
+#pragma unroll
+            for (int u = 0; u < AWQ_RG_UNROLL; ++u) v[u] = stage[base + i1 + u];
+#pragma unroll
+            for (int u = 0; u < AWQ_RG_UNROLL; ++u) {
+                smax = max(smax, SL::sext(v[u]));
+                umax = max(umax, v[u]);
+                umin = min(umin, v[u]);
+            }
+        }
+        for (; i1 < ce; ++i1) {
+            const uint32_t v = stage[base + i1];
+            smax = max(smax, SL::sext(v));
+            umax = max(umax, v);
+            umin = min(umin, v);
+        }
+    }
+    rg_reduce(smax, umax, umin, lgP);                          // the group's P lanes (aligned)
+    float gmn, gmx;
+    bool gnan;
+    group_range<F, SYM>(smax, umax, umin, gmn, gmx, gnan);
+    const GroupParams p = params_from_range<F, BITS, SYM>(gmn, gmx);
+    const bool special = !F::fast(p.r);
+    // wave-uniform: every group of the tile admits the plain quotient (F::plain_ok)
+    if (F::kHasPlain && active && j == 0 && !F::plain_ok(p.s)) not_plain = 1;
+    if (active && j == 0) {
+        const int64_t gi = r * G + g0 + grp;
+        if (scales) scales[gi] = f16_bits(p.s, gnan, nan_code);
+        if (zeros) zeros[gi] = __builtin_isnan(p.z) ? INT32_MIN : (int32_t)p.z;
+        zst[grp] = __builtin_isnan(p.z) ? NANF : ((uint32_t)((int)p.z - QMIN) & MASK);
+        prm[grp] = (float4){p.r, p.z, p.s, special ? 1.0f : 0.0f};
+    }
+    }   // (pass 1 by groups)
+    __syncthreads();
+    // uniform: every group of the tile admits the plain quotient (F::plain_ok)
+    const bool plain = F::kHasPlain && not_plain == 0;
+    // ---- pass 2: lane = 8 consecutive elements of the segment (one qweight word at 4 bits):
+    //      its groups' parameters from LDS, quantize, pack, store (kb is a word boundary) ----
+    const int nck = (n_el + 7) >> 3;
+    const int L32 = (int)L;                               // invL = RN(1 / L): exact group index e * invL
+                                                          // for e < 2^13, L <= 512 (host-computed)
+    const int64_t wpr = (K + PER - 1) / PER;
+    int32_t* qdst = qweight ? qweight + r * wpr + kb / PER : nullptr;
+    float efA = 8.0f * (float)lane + 0.5f;                // e0c + 0.5 as an exact float induction
+    const float efStep = 8.0f * (float)NT;
+    for (int c = lane; c < nck; c += NT, efA += efStep) {
+        const int e0c = 8 * c;
+        const bool tail = e0c + 8 > n_el;                 // the row's last, partial chunk
+        float x[8];
+        if (skew == 0) {                                  // 16-B aligned chunk (K % 8 == 0 rows)
+            const u4 v0 = *(const u4*)(stage + e0c);      // (past n_el: the stage's slack)
+            if constexpr (F::kBytes == 2) {
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const uint32_t wd = v0[i];
+                    x[2 * i] = F::lo(wd);
+                    x[2 * i + 1] = F::hi(wd);
+                }
+            } else {
+                const u4 v1 = *(const u4*)(stage + e0c + 4);
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    x[i] = __uint_as_float(v0[i]);
+                    x[4 + i] = __uint_as_float(v1[i]);
+                }
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) x[i] = SL::dec(stage[skew + min(e0c + i, n_el - 1)]);
+        }
+        // parameters per element.  SPLIT 8 (L % 8 == 0): the chunk lies in one group; SPLIT 4
+        // (L % 4 == 0): each half does (no per-element selects); SPLIT 1: at most two groups
+        // meet in the chunk when L >= 8, one lookup per element below that
+        float rr[8], zz[8], ss[8];
+        bool spec;
+        if constexpr (SPLIT == 8 || SPLIT == 4) {
+            const int gA = (int)(efA * invL);             // < ng: e0c < n_el
+            const float4 pA = prm[gA];
+            float4 pB = pA;
+            if constexpr (SPLIT == 4) pB = prm[min((int)((efA + 4.0f) * invL), ng - 1)];
+            spec = pA.w != 0.0f || pB.w != 0.0f;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                rr[i] = i < 4 ? pA.x : pB.x;
+                zz[i] = i < 4 ? pA.y : pB.y;
+                ss[i] = i < 4 ? pA.z : pB.z;
+            }
+        } else if (L32 >= 8) {
+            const int gA = (int)(((float)e0c + 0.5f) * invL);
+            const int bnd = (gA + 1) * L32 - e0c;         // first element of the next group
+            const float4 pA = prm[gA], pB = prm[min(gA + 1, ng - 1)];
+            spec = pA.w != 0.0f || (bnd < 8 && pB.w != 0.0f);
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const bool a = i < bnd;
+                rr[i] = a ? pA.x : pB.x;
+                zz[i] = a ? pA.y : pB.y;
+                ss[i] = a ? pA.z : pB.z;
+            }
+        } else {
+            spec = false;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const int gi = min((int)(((float)(e0c + i) + 0.5f) * invL), ng - 1);
+                const float4 pi = prm[gi];
+                spec |= pi.w != 0.0f;
+                rr[i] = pi.x;
+                zz[i] = pi.y;
+                ss[i] = pi.z;
+            }
+        }
+        int32_t qv[8];                                    // q (reference value), INT32_MIN for NaN
+        uint32_t word0 = 0, word1 = 0;
+        if (__builtin_expect(!spec, 1)) {
+            float q[8];
+            if constexpr (std::is_same<F, FmtBF16>::value) {
+                field8_bf16<BITS, SYM>(x, rr, zz, q);
+            } else {
+#pragma unroll
+                for (int i = 0; i < 8; ++i)
+                    q[i] = plain ? field1_fast<F, BITS, SYM, true>(x[i], rr[i], zz[i], ss[i])
+                                 : field1_fast<F, BITS, SYM, false>(x[i], rr[i], zz[i], ss[i]);
+            }
+            if (__builtin_expect(tail, 0)) {
+                const int nv = n_el - e0c;
+#pragma unroll
+                for (int i = 1; i < 8; ++i)
+                    if (i >= nv) q[i] = 0.0f;             // past the row end: zero fields
+            }
+            if (tensor_q) {
+#pragma unroll
+                for (int i = 0; i < 8; ++i) qv[i] = (int32_t)field_q<BITS>(q[i]) + QMIN;
+            }
+            pack8_cvt<BITS>(q, word0, word1);
+        } else {                                          // a group with scale 0 / inf / NaN: IEEE division
+            constexpr int QMAX = SYM ? (1 << (BITS - 1)) - 1 : (1 << BITS) - 1;
+            const int nv = n_el - e0c;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const float t = F::rn(opaque(x[i]) / ss[i]);
+                const float u = SYM ? t : F::rn(t + zz[i]);
+                const float rq = __builtin_rintf(u);
+                int32_t qi = __builtin_isnan(rq) ? INT32_MIN
+                                                 : (int32_t)__builtin_fminf(__builtin_fmaxf(rq, (float)QMIN), (float)QMAX);
+                uint32_t f = ((uint32_t)qi - (uint32_t)QMIN) & MASK;
+                if (i >= nv) { f = 0; qi = QMIN; }
+                qv[i] = qi;
+                if (BITS == 4) word0 |= f << (4 * i);
+                else if (i < 4) word0 |= f << (8 * i);
+                else word1 |= f << (8 * (i - 4));
+            }
+        }
+        if (qdst) {
+            if (BITS == 4) {
+                qdst[c] = (int32_t)word0;
+            } else {
+                qdst[2 * c] = (int32_t)word0;
+                if (!tail || e0c + 4 < n_el) qdst[2 * c + 1] = (int32_t)word1;
+            }
+        }
+        if (tensor_q) {
+            int32_t* tq = tensor_q + r * K + kb + e0c;
+            if (__builtin_expect(!tail, 1)) {
+#pragma unroll
+                for (int i = 0; i < 8; ++i) tq[i] = qv[i];
+            } else {
+                const int nv = n_el - e0c;
+#pragma unroll
+                for (int i = 0; i < 8; ++i)
+                    if (i < nv) tq[i] = qv[i];
+            }
+        }
+    }
+    if (qzeros) {                                 // g0 is a word boundary: GPT % PER == 0
+        const int64_t zpr = (G + PER - 1) / PER;
+        const int nwz = (ng + PER - 1) / PER;
+        if (lane < nwz) {
+            uint32_t word = 0;
+            for (int i = 0; i < PER && lane * PER + i < ng; ++i) word |= zst[lane * PER + i] << (BITS * i);
+            qzeros[r * zpr + g0 / PER + lane] = (int32_t)word;
+        }
+    }
+}
+
+}  // namespace
+
+// Row-segment tiles of awq_rowgroup_kernel.  Whole-row tiles shared by two waves when a
+// 16-bit row of >= 2560 elements has <= 64 groups and fits a 16 KiB stage (r2ae / r2af: a
+// whole-row tile runs 1 059 VALU per row against 1 551 for 16-group one-wave tiles, and two
+// waves per LDS stage keep the SIMDs occupied; r2ag: +8..44 % at K = 3000 / 4096, e.g. bf16
+// gs 100 47.6 -> 42.5 us; -10..15 % at K = 2048, hence the threshold).  Otherwise one wave per tile and GPT (8..64, a power of two) from a
+// per-row cost fitted to measurements (profiles/round2/r2_rowgroup/r2r_*: 14336 x 4096,
+// group sizes 48 / 100, GPT 8..32): tiles x (fixed wave cost 8 + 0.6 per element of a
+// lane's pass-1 chunk C = L / (64 / GPT) + 2.3 per 512-element pass-2 sweep).  gpt = 0 if
+// the shape does not fit the LDS stage.  rg_gpt / rg_waves override (awq_hip_tuning.h).
+struct RgPlan {
+    int gpt, waves;
+};
+RgPlan rowgroup_plan(int dtype, int64_t K, int64_t L) {
+    RgPlan pl = {0, 1};
+    if (dtype != AWQ_DTYPE_BF16 && dtype != AWQ_DTYPE_F16 && dtype != AWQ_DTYPE_F32) return pl;
+    const int64_t es = dtype == AWQ_DTYPE_F32 ? 4 : 2;
+    // (L = 1: a one-element group's NaN scale keeps the element's own NaN bits — generic kernel)
+    if (L < 2 || K <= 0 || 8 * L * es > kRgStageBytes) return pl;
+    const bool ew = tuning().rg_waves == 1 || tuning().rg_waves == 2;
+    if (ew) pl.waves = tuning().rg_waves;
+    if (const int v = tuning().rg_gpt) {
+        if (v >= 8 && v <= 64 && v % 8 == 0 && v * L * es <= kRgStageMax) {
+            pl.gpt = v;
+            return pl;
+        }
+    }
+    const int64_t G = (K + L - 1) / L;
+    const int64_t whole = (G + 7) / 8 * 8;
+    if (!ew && es == 2 && K >= 2560 && whole <= 64 && whole * L * es <= kRgStageMax) {
+        pl.gpt = (int)whole;
+        pl.waves = 2;
+        return pl;
+    }
+    double best_cost = 0.0;
+    for (int gpt = 8; gpt <= 64; gpt *= 2) {
+        if (gpt * L * es > kRgStageBytes) break;
+        const int64_t tiles = (G + gpt - 1) / gpt;
+        const int64_t C = (L + (64 / gpt) - 1) / (64 / gpt);
+        const int64_t el = min((int64_t)gpt, G) * L;                  // elements of a full tile
+        const double cost = (double)tiles * (8.0 + 0.6 * (double)C + 2.3 * (double)((el + 511) / 512));
+        if (pl.gpt == 0 || cost < best_cost) { best_cost = cost; pl.gpt = gpt; }
+    }
+    return pl;
+}
+int rowgroup_gpt(int dtype, int64_t K, int64_t L) { return rowgroup_plan(dtype, K, L).gpt; }
+
+hipError_t launch_rowgroup(const void* w, int dtype, int64_t rows, int64_t K, int64_t L, int bits, int symmetric,
+                           int32_t* qweight, int32_t* qzeros, uint16_t* scales, int32_t* tensor_q, int32_t* zeros,
+                           hipStream_t stream, uint32_t nan_code) {
+    const RgPlan pl = rowgroup_plan(dtype, K, L);
+    const int gpt = pl.gpt;
+    if (gpt == 0 || rows <= 0) return hipErrorInvalidValue;
+    const int64_t G = (K + L - 1) / L;
+    const int64_t tpr = (G + gpt - 1) / gpt;
+    const int nt = 64 * pl.waves;                                      // threads per tile
+    const int lgP = min(6, 31 - __builtin_clz((unsigned)(nt / gpt)));  // P = lanes per group: a power of two
+    const int P = 1 << lgP;
+    const int C = (int)((L + P - 1) / P);
+    const dim3 grid((unsigned)(rows * tpr)), block((unsigned)nt);
+    // stage: the tile's elements rounded up to 16 B, + the up-to-16-B alignment skew and the
+    // last 8-element vector read past the segment end
+    const size_t lds = ((size_t)gpt * L * (dtype == AWQ_DTYPE_F32 ? 4 : 2) + 15) / 16 * 16 + 48;
+    const bool p1c = tuning().rg_p1 == 2;   // pass 1 by groups (default) / evenly split runs (A/B)
+#define AWQ_RG_SPLIT(Fm, B, S, SP)                                                                                 \
+    do {                                                                                                           \
+        if (p1c)                                                                                                   \
+            hipLaunchKernelGGL((awq_rowgroup_kernel<Fm, B, S, SP, true>), grid, block, lds, stream, w, rows, K, L, \
+                               lgP, gpt, (uint32_t)tpr, G, C, 1.0f / (float)L, qweight, qzeros, scales, tensor_q,  \
+                               zeros, nan_code);                                                                   \
+        else                                                                                                       \
+            hipLaunchKernelGGL((awq_rowgroup_kernel<Fm, B, S, SP, false>), grid, block, lds, stream, w, rows, K,   \
+                               L, lgP, gpt, (uint32_t)tpr, G, C, 1.0f / (float)L, qweight, qzeros, scales,         \
+                               tensor_q, zeros, nan_code);                                                         \
+    } while (0)
+#define AWQ_RG(Fm, B, S)                                                                                           \
+    if (L % 8 == 0) AWQ_RG_SPLIT(Fm, B, S, 8);                                                                      \
+    else if (L % 4 == 0) AWQ_RG_SPLIT(Fm, B, S, 4);                                                                 \
+    else AWQ_RG_SPLIT(Fm, B, S, 1)
+#define AWQ_RG_FMT(Fm)                                                     \
+    switch ((bits == 8 ? 2 : 0) + (symmetric ? 1 : 0)) {                  \
+    case 0: AWQ_RG(Fm, 4, false); break;                                   \
+    case 1: AWQ_RG(Fm, 4, true); break;                                    \
+    case 2: AWQ_RG(Fm, 8, false); break;                                   \
+    default: AWQ_RG(Fm, 8, true); break;                                   \
+    }
+    if (dtype == AWQ_DTYPE_F16) {
+        AWQ_RG_FMT(FmtF16)
+    } else if (dtype == AWQ_DTYPE_F32) {
+        AWQ_RG_FMT(FmtF32)
+    } else {
+        AWQ_RG_FMT(FmtBF16)
+    }
+#undef AWQ_RG_FMT
+#undef AWQ_RG
+#undef AWQ_RG_SPLIT
+    return hipPeekAtLastError();
+}
+
+}  // namespace awq

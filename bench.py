@@ -309,7 +309,8 @@ def write_leg(batch, rank, dev, out_dir, chunk_size=10):
             "s_rank0": round(t, 4), "s_max_over_ranks": round(t_max, 4), "GBs_rank0": round(nbytes / t / 1e9, 3)}
 
 
-KERNEL_SOURCES = ("awq-converter_amd/csrc/awq_fast.hip", "awq-converter_amd/csrc/awq_internal.h")
+KERNEL_SOURCES = ("awq-converter_amd/csrc/awq_fast.hip", "awq-converter_amd/csrc/awq_quant.h",
+                  "awq-converter_amd/csrc/awq_internal.h")
 
 
 def kernel_source_hash():

@@ -1,4 +1,4 @@
-"""The row-segment kernel (awq_fast.hip awq_rowgroup_kernel): bf16 / fp16 / fp32 with group
+"""The row-segment kernel (awq_rowgroup.hip awq_rowgroup_kernel): bf16 / fp16 / fp32 with group
 sizes outside {32, 64, 128, 256} (up to 512; fp32 up to 256) and K % 8 != 0 rows — the
 shapes that round 1 sent to the one-wave-per-group generic kernel plus int32 staging and
 pack passes.  Reference arithmetic: awq.py:173-250 per group, awq.py:286-374 for the row

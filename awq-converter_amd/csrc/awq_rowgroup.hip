@@ -633,7 +633,13 @@ hipError_t launch_rowgroup(const void* w, int dtype, int64_t rows, int64_t K, in
     const dim3 grid((unsigned)(rows * tpr)), block((unsigned)nt);
     // stage: the tile's elements rounded up to 16 B, + the up-to-16-B alignment skew and the
     // last 8-element vector read past the segment end
-    const size_t lds = ((size_t)gpt * L * (dtype == AWQ_DTYPE_F32 ? 4 : 2) + 15) / 16 * 16 + 48;
+    // (sized to the elements a tile can hold: a whole-row tile's groups are rounded up to a
+    //  multiple of 8 but its segment ends at K — 8.2 instead of 9.6 KiB for K = 4096 at gs 100
+    //  lets 16 two-wave workgroups (8 waves per SIMD) fit a CU's 160 KiB instead of 14;
+    //  rg_lds_full = 1 keeps the round-2 sizing for A/B)
+    const int64_t es = dtype == AWQ_DTYPE_F32 ? 4 : 2;
+    const int64_t stage_el = tuning().rg_lds_full == 1 ? (int64_t)gpt * L : min((int64_t)gpt * L, K);
+    const size_t lds = (size_t)((stage_el * es + 15) / 16 * 16 + 48);
     const bool p1c = tuning().rg_p1 == 2;   // pass 1 by groups (default) / evenly split runs (A/B)
 #define AWQ_RG_SPLIT(Fm, B, S, SP)                                                                                 \
     do {                                                                                                           \

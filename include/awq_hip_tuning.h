@@ -32,7 +32,8 @@ typedef struct awq_tuning {
     int32_t rg_p1;           /* row-segment pass 1: 0 / 1 by groups (2^k lanes per group, DPP
                                 merges), 2 evenly split runs (NT / groups lanes per group, LDS
                                 merges, parameters by one lane per group) */
-    int32_t rg_p2;           /* row-segment pass 2: 0 the default, 1 the round-2 form */
+    int32_t rg_lds_full;     /* row-segment LDS stage: 0 sized to the elements a tile holds (min(groups
+                                x group size, K)), 1 to its groups x group size (round-2 sizing, A/B) */
 } awq_tuning;
 
 /* Set (t != NULL) or reset to the defaults (t == NULL) this thread's tuning. */

@@ -74,6 +74,10 @@ class Tuning(ctypes.Structure):
 # symbol -> (restype, argtypes); the CPU test suite checks every one is exported.
 SIGNATURES = {
     "awq_abi_version": (_I32, []),
+    # chunk-file writer (include/awq_ptfile.h; awq_quantizer/ptfile.py)
+    "awq_crc32": (ctypes.c_uint32, [ctypes.c_uint32, _P, _I64, _I32]),
+    "awq_write_pt": (_I32, [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p, _I64, _I32, ctypes.POINTER(ctypes.c_void_p),
+                            ctypes.POINTER(ctypes.c_int64), ctypes.c_char_p]),
     "awq_last_error": (ctypes.c_char_p, []),
     "awq_device_check": (_I32, [ctypes.c_char_p, _I32]),
     "awq_quantize_groups": (_I32, [_P, _I32, _I64, _I64, _I32, _I32, _I32, _P, _P, _P, _P, _P, _P]),

@@ -14,13 +14,13 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def declared_symbols():
-    """Every entry point declared by include/*.h (awq_hip.h + awq_hip_tuning.h)."""
+    """Every entry point declared by include/*.h (awq_hip.h, awq_hip_tuning.h, awq_ptfile.h)."""
     src = ""
     for h in sorted(os.listdir(os.path.join(ROOT, "include"))):
         if h.endswith(".h"):
             with open(os.path.join(ROOT, "include", h)) as f:
                 src += f.read()
-    return sorted(set(re.findall(r"^\s*(?:int|int64_t|const char\*)\s+(awq_\w+)\s*\(", src, re.M)))
+    return sorted(set(re.findall(r"^\s*(?:int|int64_t|uint32_t|const char\*)\s+(awq_\w+)\s*\(", src, re.M)))
 
 
 def test_library_exports_every_declared_symbol():

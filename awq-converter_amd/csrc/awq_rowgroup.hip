@@ -174,14 +174,14 @@ __device__ __forceinline__ void rg_range16(const uint32_t* st32, int s_lo, int s
 }
 
 // LDS: the segment's stage (dynamic, sized by the launch to the tile: 1.6-8 KiB) + 1.3 KiB
-template <typename F, int BITS, bool SYM, int SPLIT, bool P1C>
+template <typename F, int BITS, bool SYM, int SPLIT, bool P1C, bool TQ>
 __global__ __launch_bounds__(128) void awq_rowgroup_kernel(const void* __restrict__ w, int64_t rows, int64_t K,
                                                              int64_t L, int lgP, int GPT, uint32_t tiles_per_row,
                                                              int64_t G, int C, float invL,
                                                              int32_t* __restrict__ qweight, int32_t* __restrict__ qzeros,
                                                              uint16_t* __restrict__ scales,
                                                              int32_t* __restrict__ tensor_q, int32_t* __restrict__ zeros,
-                                                             uint32_t nan_code) {
+                                                             uint32_t nan_code, int lgP_last, int C_last) {
     typedef RgSlot<F> SL;
     typedef typename SL::T S;
     constexpr int QMIN = SYM ? -(1 << (BITS - 1)) : 0;
@@ -193,6 +193,7 @@ __global__ __launch_bounds__(128) void awq_rowgroup_kernel(const void* __restric
     __shared__ uint32_t zst[64];
     __shared__ float4 prm[64];                          // per group: r, z, s, special
     __shared__ int not_plain;                           // a group of the tile needs the full quotient
+    __shared__ int any_special;                         // a group of the tile has scale 0 / inf / NaN
     __shared__ int acc_smax[P1C ? 64 : 1];              // P1C: per-group raw-bits reductions
     __shared__ uint32_t acc_umax[P1C ? 64 : 1], acc_umin[P1C ? 64 : 1];
     // one tile per workgroup of 1 or 2 waves (host-chosen: two waves share a large tile's LDS
@@ -201,13 +202,14 @@ __global__ __launch_bounds__(128) void awq_rowgroup_kernel(const void* __restric
     // (host-side G, C, log2 P and a 32-bit tile split: 64-bit divisions per wave on the
     //  CU's shared scalar unit were a visible part of the per-tile cost)
     const uint32_t tile = blockIdx.x;   // (an XCD-contiguous tile order measured no different: r2z3)
-    const uint32_t r32 = tile / tiles_per_row;
+    // (whole-row tiles, the common case, need no division: the scalar unit has no divider)
+    const uint32_t r32 = tiles_per_row == 1 ? tile : tile / tiles_per_row;
     const int64_t r = r32;
     const int64_t g0 = (int64_t)(tile - r32 * tiles_per_row) * GPT;
     const int ng = (int)min((int64_t)GPT, G - g0);
-    if (ng < GPT) {   // the row's last, partial tile: more lanes per group (wave-uniform)
-        lgP = min(6, 31 - __builtin_clz((unsigned)NT / (unsigned)ng));
-        C = (int)((L + (1 << lgP) - 1) >> lgP);
+    if (ng < GPT) {   // the row's last, partial tile: more lanes per group (host-computed)
+        lgP = lgP_last;
+        C = C_last;
     }
     const int P = 1 << lgP;
     const int64_t kb = g0 * L, ke = min((g0 + ng) * L, K);     // the row segment [kb, ke)
@@ -247,7 +249,13 @@ __global__ __launch_bounds__(128) void awq_rowgroup_kernel(const void* __restric
                 ((uint16_t*)stage)[8 * c + h] = __builtin_amdgcn_raw_buffer_load_b16(rw, (uint32_t)(16 * c + 2 * h), 0, 0);
         }
     }
-    if (lane == 0) not_plain = 0;
+    if (lane == 0) {
+        not_plain = 0;
+        any_special = 0;
+    }
+    // TQ: the parity outputs (tensor_q) are wanted (a compile-time switch: the packed-only
+    // kernel carries no per-sweep checks for them)
+    if constexpr (!TQ) tensor_q = nullptr;
     if constexpr (P1C) {
         // identities; the row's zero-padded last group starts from 0 (awq.py:337-339: the
         // zeros join its min/max)
@@ -314,6 +322,7 @@ __global__ __launch_bounds__(128) void awq_rowgroup_kernel(const void* __restric
             const GroupParams p = params_from_range<F, BITS, SYM>(gmn, gmx);
             const bool special = !F::fast(p.r);
             if (F::kHasPlain && !F::plain_ok(p.s)) not_plain = 1;
+            if (special) any_special = 1;
             const int64_t gi = r * G + g0 + lane;
             if (scales) scales[gi] = f16_bits(p.s, gnan, nan_code);
             if (zeros) zeros[gi] = __builtin_isnan(p.z) ? INT32_MIN : (int32_t)p.z;
@@ -411,6 +420,7 @@ __global__ __launch_bounds__(128) void awq_rowgroup_kernel(const void* __restric
     const bool special = !F::fast(p.r);
     // wave-uniform: every group of the tile admits the plain quotient (F::plain_ok)
     if (F::kHasPlain && active && j == 0 && !F::plain_ok(p.s)) not_plain = 1;
+    if (active && j == 0 && special) any_special = 1;
     if (active && j == 0) {
         const int64_t gi = r * G + g0 + grp;
         if (scales) scales[gi] = f16_bits(p.s, gnan, nan_code);
@@ -422,6 +432,8 @@ __global__ __launch_bounds__(128) void awq_rowgroup_kernel(const void* __restric
     __syncthreads();
     // uniform: every group of the tile admits the plain quotient (F::plain_ok)
     const bool plain = F::kHasPlain && not_plain == 0;
+    // uniform: no group of the tile takes the IEEE-division path (skips the per-sweep checks)
+    const bool tile_special = any_special != 0;
     // ---- pass 2: lane = 8 consecutive elements of the segment (one qweight word at 4 bits):
     //      its groups' parameters from LDS, quantize, pack, store (kb is a word boundary) ----
     const int nck = (n_el + 7) >> 3;
@@ -466,7 +478,7 @@ __global__ __launch_bounds__(128) void awq_rowgroup_kernel(const void* __restric
             const float4 pA = prm[gA];
             float4 pB = pA;
             if constexpr (SPLIT == 4) pB = prm[min((int)((efA + 4.0f) * invL), ng - 1)];
-            spec = pA.w != 0.0f || pB.w != 0.0f;
+            spec = tile_special && (pA.w != 0.0f || pB.w != 0.0f);
 #pragma unroll
             for (int i = 0; i < 8; ++i) {
                 rr[i] = i < 4 ? pA.x : pB.x;
@@ -477,7 +489,7 @@ __global__ __launch_bounds__(128) void awq_rowgroup_kernel(const void* __restric
             const int gA = (int)(((float)e0c + 0.5f) * invL);
             const int bnd = (gA + 1) * L32 - e0c;         // first element of the next group
             const float4 pA = prm[gA], pB = prm[min(gA + 1, ng - 1)];
-            spec = pA.w != 0.0f || (bnd < 8 && pB.w != 0.0f);
+            spec = tile_special && (pA.w != 0.0f || (bnd < 8 && pB.w != 0.0f));
 #pragma unroll
             for (int i = 0; i < 8; ++i) {
                 const bool a = i < bnd;
@@ -491,7 +503,7 @@ __global__ __launch_bounds__(128) void awq_rowgroup_kernel(const void* __restric
             for (int i = 0; i < 8; ++i) {
                 const int gi = min((int)(((float)(e0c + i) + 0.5f) * invL), ng - 1);
                 const float4 pi = prm[gi];
-                spec |= pi.w != 0.0f;
+                spec |= tile_special && pi.w != 0.0f;
                 rr[i] = pi.x;
                 zz[i] = pi.y;
                 ss[i] = pi.z;
@@ -630,6 +642,11 @@ hipError_t launch_rowgroup(const void* w, int dtype, int64_t rows, int64_t K, in
     const int lgP = min(6, 31 - __builtin_clz((unsigned)(nt / gpt)));  // P = lanes per group: a power of two
     const int P = 1 << lgP;
     const int C = (int)((L + P - 1) / P);
+    // the row's last tile when it holds fewer groups: the largest power of two <= nt / its
+    // groups lanes per group (<= 64)
+    const int64_t ng_last = G - (tpr - 1) * gpt;
+    const int lgP_last = min(6, 31 - __builtin_clz((unsigned)(nt / ng_last)));
+    const int C_last = (int)((L + (1 << lgP_last) - 1) >> lgP_last);
     const dim3 grid((unsigned)(rows * tpr)), block((unsigned)nt);
     // stage: the tile's elements rounded up to 16 B, + the up-to-16-B alignment skew and the
     // last 8-element vector read past the segment end
@@ -641,16 +658,16 @@ hipError_t launch_rowgroup(const void* w, int dtype, int64_t rows, int64_t K, in
     const int64_t stage_el = tuning().rg_lds_full == 1 ? (int64_t)gpt * L : min((int64_t)gpt * L, K);
     const size_t lds = (size_t)((stage_el * es + 15) / 16 * 16 + 48);
     const bool p1c = tuning().rg_p1 == 2;   // pass 1 by groups (default) / evenly split runs (A/B)
+#define AWQ_RG_GO(Fm, B, S, SP, P1, TQ)                                                                            \
+    hipLaunchKernelGGL((awq_rowgroup_kernel<Fm, B, S, SP, P1, TQ>), grid, block, lds, stream, w, rows, K, L, lgP,  \
+                       gpt, (uint32_t)tpr, G, C, 1.0f / (float)L, qweight, qzeros, scales, tensor_q, zeros, nan_code, \
+                       lgP_last, C_last)
+    // (the pass-1 A/B variant is built for the packed outputs only; with tensor_q it takes the default)
 #define AWQ_RG_SPLIT(Fm, B, S, SP)                                                                                 \
     do {                                                                                                           \
-        if (p1c)                                                                                                   \
-            hipLaunchKernelGGL((awq_rowgroup_kernel<Fm, B, S, SP, true>), grid, block, lds, stream, w, rows, K, L, \
-                               lgP, gpt, (uint32_t)tpr, G, C, 1.0f / (float)L, qweight, qzeros, scales, tensor_q,  \
-                               zeros, nan_code);                                                                   \
-        else                                                                                                       \
-            hipLaunchKernelGGL((awq_rowgroup_kernel<Fm, B, S, SP, false>), grid, block, lds, stream, w, rows, K,   \
-                               L, lgP, gpt, (uint32_t)tpr, G, C, 1.0f / (float)L, qweight, qzeros, scales,         \
-                               tensor_q, zeros, nan_code);                                                         \
+        if (tensor_q) AWQ_RG_GO(Fm, B, S, SP, false, true);                                                         \
+        else if (p1c) AWQ_RG_GO(Fm, B, S, SP, true, false);                                                         \
+        else AWQ_RG_GO(Fm, B, S, SP, false, false);                                                                 \
     } while (0)
 #define AWQ_RG(Fm, B, S)                                                                                           \
     if (L % 8 == 0) AWQ_RG_SPLIT(Fm, B, S, 8);                                                                      \
@@ -673,6 +690,7 @@ hipError_t launch_rowgroup(const void* w, int dtype, int64_t rows, int64_t K, in
 #undef AWQ_RG_FMT
 #undef AWQ_RG
 #undef AWQ_RG_SPLIT
+#undef AWQ_RG_GO
     return hipPeekAtLastError();
 }
 

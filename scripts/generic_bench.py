@@ -34,10 +34,13 @@ def main():
                     "each 'default' or k=v[,k=v] (include/awq_hip_tuning.h), e.g. default/rg_p1=1")
     ap.add_argument("--dequant", action="store_true", help="also time dequantize_packed of the packed result")
     ap.add_argument("--dq-variants", default="1,3,6,7,8,9", help="--dq-ab: tuning dq_words_v1 values to time")
+    ap.add_argument("--lib", default="", help="load this in-tree build instead of _lib/libawq_hip.so (A/B of builds)")
     ap.add_argument("--dq-ab", action="store_true", help="--dequant: also the round-2 word kernel (tuning dq_words_v1), "
                                                           "interleaved, 3 rounds")
     args = ap.parse_args()
     from awq_quantizer import _hip
+    if args.lib:
+        _hip.load_library(args.lib)
     dev = torch.device("cuda", 0)
     _hip.require_device(dev)
     for shape in args.shape.split(";"):
@@ -85,6 +88,7 @@ def one(args, _hip, dev, shape, name, gs, generic, tun=None):
               "generic" if generic or name == "f64" or gs > (256 if name == "f32" else 512) else
               "streaming" if _hip.ragged_eligible(DT[name], R, K, gs) else "row-segment")
     print(json.dumps({"dtype": name, "shape": [R, K], "group_size": gs, "bits": args.bits, "kernel": kernel, "tuning": tun or {},
+                      "lib": os.path.basename(args.lib) if args.lib else "libawq_hip.so",
                       "search": args.search, "us": round(us, 1), "input_GBs": round(nbytes / us / 1e3, 1),
                       "algorithmic_GBs": round(algo / us / 1e3, 1), "frac_8TBs": round(algo / us / 1e3 / 8000, 3)}),
           flush=True)

@@ -441,13 +441,15 @@ __global__ __launch_bounds__(128) void awq_rowgroup_kernel(const void* __restric
                                                           // for e < 2^13, L <= 512 (host-computed)
     const int64_t wpr = (K + PER - 1) / PER;
     int32_t* qdst = qweight ? qweight + r * wpr + kb / PER : nullptr;
-    float efA = 8.0f * (float)lane + 0.5f;                // e0c + 0.5 as an exact float induction
-    const float efStep = 8.0f * (float)NT;
-    for (int c = lane; c < nck; c += NT, efA += efStep) {
+    // one chunk: c = its index in the segment, efA = 8 c + 0.5 (exact float); ALIGNED: the
+    // segment starts 16-B aligned (skew 0); FULL: the chunk holds 8 elements of the row
+    auto sweep = [&](int c, float efA, auto aligned_t, auto full_t, auto plain_t) {
+        constexpr bool ALIGNED = decltype(aligned_t)::value, FULL = decltype(full_t)::value;
+        constexpr bool PLAIN = decltype(plain_t)::value;
         const int e0c = 8 * c;
-        const bool tail = e0c + 8 > n_el;                 // the row's last, partial chunk
+        const bool tail = !FULL && e0c + 8 > n_el;        // the row's last, partial chunk
         float x[8];
-        if (skew == 0) {                                  // 16-B aligned chunk (K % 8 == 0 rows)
+        if constexpr (ALIGNED) {                          // 16-B aligned chunk (K % 8 == 0 rows)
             const u4 v0 = *(const u4*)(stage + e0c);      // (past n_el: the stage's slack)
             if constexpr (F::kBytes == 2) {
 #pragma unroll
@@ -518,8 +520,7 @@ __global__ __launch_bounds__(128) void awq_rowgroup_kernel(const void* __restric
             } else {
 #pragma unroll
                 for (int i = 0; i < 8; ++i)
-                    q[i] = plain ? field1_fast<F, BITS, SYM, true>(x[i], rr[i], zz[i], ss[i])
-                                 : field1_fast<F, BITS, SYM, false>(x[i], rr[i], zz[i], ss[i]);
+                    q[i] = field1_fast<F, BITS, SYM, PLAIN>(x[i], rr[i], zz[i], ss[i]);
             }
             if (__builtin_expect(tail, 0)) {
                 const int nv = n_el - e0c;
@@ -570,7 +571,32 @@ __global__ __launch_bounds__(128) void awq_rowgroup_kernel(const void* __restric
                     if (i < nv) tq[i] = qv[i];
             }
         }
-    }
+    };
+    // sweeps over the segment's chunks, lane = chunk c, c + NT, ...: the sweeps in which every
+    // lane has a full chunk run as a uniform (scalar) loop with no per-lane bounds or tail
+    // checks, the rest (<= 1 sweep of full chunks + the row's last partial chunk) guarded
+    const float efStep = 8.0f * (float)NT;
+    const int lgNT = NT == 128 ? 7 : 6;
+    auto sweeps = [&](auto aligned_t, auto plain_t) {
+        const int full_sweeps = (n_el >> 3) >> lgNT;
+        float efA = 8.0f * (float)lane + 0.5f;
+        for (int sw = 0; sw < full_sweeps; ++sw, efA += efStep)
+            sweep(lane + (sw << lgNT), efA, aligned_t, std::true_type{}, plain_t);
+        for (int c = lane + (full_sweeps << lgNT); c < nck; c += NT, efA += efStep)
+            sweep(c, efA, aligned_t, std::false_type{}, plain_t);
+    };
+    // (uniform switches hoisted out of the sweeps: the alignment and, for fp16, whether every
+    //  group of the tile admits the plain quotient)
+    auto by_plain = [&](auto aligned_t) {
+        if constexpr (F::kHasPlain) {
+            if (plain) sweeps(aligned_t, std::true_type{});
+            else sweeps(aligned_t, std::false_type{});
+        } else {
+            sweeps(aligned_t, std::false_type{});
+        }
+    };
+    if (skew == 0) by_plain(std::true_type{});
+    else by_plain(std::false_type{});
     if (qzeros) {                                 // g0 is a word boundary: GPT % PER == 0
         const int64_t zpr = (G + PER - 1) / PER;
         const int nwz = (ng + PER - 1) / PER;

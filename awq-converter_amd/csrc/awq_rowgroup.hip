@@ -230,6 +230,16 @@ __global__ __launch_bounds__(128) void awq_rowgroup_kernel(const void* __restric
         // read zeros without a memory access, and no register needs a value on a skipped
         // path (conditional loads cost 28 v_mov per wave of phi copies); lanes past the end
         // store nothing
+        if (nch == 4 * NT) {
+            // (exactly 4 chunks per lane — a 4 096-element bf16 row on two waves: 4 loads
+            //  and 4 unmasked stores, no range-checked dummy loads)
+            u4 v[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                v[k] = __builtin_amdgcn_raw_buffer_load_b128(rw, (uint32_t)(16 * (NT * k + lane)), 0, AWQ_LOAD_AUX);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) *(u4*)((char*)stage + 16 * (NT * k + lane)) = v[k];
+        } else
         for (int c0 = 0; c0 < nch; c0 += 8 * NT) {
             u4 v[8];
 #pragma unroll

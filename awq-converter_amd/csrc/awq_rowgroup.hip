@@ -190,7 +190,7 @@ __global__ __launch_bounds__(128) void awq_rowgroup_kernel(const void* __restric
     constexpr uint32_t NANF = (uint32_t)(0u - (uint32_t)QMIN) & MASK;   // field of INT32_MIN - qmin
     extern __shared__ __attribute__((aligned(16))) unsigned char rg_lds[];
     S* stage = (S*)rg_lds;                              // rg_stage_bytes(): the segment + its alignment skew
-    __shared__ uint32_t zst[64];
+    __shared__ __attribute__((aligned(16))) uint32_t zst[64];
     __shared__ float4 prm[64];                          // per group: r, z, s, special
     __shared__ int not_plain;                           // a group of the tile needs the full quotient
     __shared__ int any_special;                         // a group of the tile has scale 0 / inf / NaN
@@ -205,23 +205,27 @@ __global__ __launch_bounds__(128) void awq_rowgroup_kernel(const void* __restric
     // (whole-row tiles, the common case, need no division: the scalar unit has no divider)
     const uint32_t r32 = tiles_per_row == 1 ? tile : tile / tiles_per_row;
     const int64_t r = r32;
-    const int64_t g0 = (int64_t)(tile - r32 * tiles_per_row) * GPT;
-    const int ng = (int)min((int64_t)GPT, G - g0);
+    // (32-bit row geometry: the host admits rows of < 2^30 elements; the scalar unit has no
+    //  64-bit compare, so 64-bit min()s went through VALU compares)
+    const int K32 = (int)K, L32g = (int)L;
+    const int g0 = (int)(tile - r32 * tiles_per_row) * GPT;
+    const int ng = min(GPT, (int)G - g0);
     if (ng < GPT) {   // the row's last, partial tile: more lanes per group (host-computed)
         lgP = lgP_last;
         C = C_last;
     }
     const int P = 1 << lgP;
-    const int64_t kb = g0 * L, ke = min((g0 + ng) * L, K);     // the row segment [kb, ke)
-    const int n_el = (int)(ke - kb);
+    const int kb = g0 * L32g;                                    // the row segment [kb, kb + n_el)
+    const int n_el = min((g0 + ng) * L32g, K32) - kb;
     // ---- stage the segment's bytes (from a 16-B aligned start) in LDS ----
-    const uint64_t byte0 = (uint64_t)(r * K + kb) * F::kBytes;
+    const uint64_t byte0 = ((uint64_t)r32 * (uint64_t)K32 + (uint64_t)kb) * F::kBytes;
     const uint64_t a0 = byte0 & ~(uint64_t)15;
     const int skew = (int)(byte0 - a0) / F::kBytes;               // slot of element kb
     const uint64_t total = (uint64_t)rows * (uint64_t)K * F::kBytes;
     const int nbytes = (int)(byte0 - a0) + n_el * F::kBytes;
     const int nch = (nbytes + 15) >> 4;
-    const uint32_t lim = (uint32_t)min(total - a0, (uint64_t)nch * 16);
+    const uint64_t rem = total - a0;                              // bytes from a0 to the tensor end
+    const uint32_t lim = (rem >> 32) ? 16u * (uint32_t)nch : min((uint32_t)rem, 16u * (uint32_t)nch);
     const __amdgpu_buffer_rsrc_t rw = rsrc((const char*)w + a0, lim);
     if (__builtin_expect(16u * (uint32_t)nch <= lim, 1)) {
         // every 16-B load of the segment in flight before the first LDS store (a load ->
@@ -610,9 +614,18 @@ __global__ __launch_bounds__(128) void awq_rowgroup_kernel(const void* __restric
     if (qzeros) {                                 // g0 is a word boundary: GPT % PER == 0
         const int64_t zpr = (G + PER - 1) / PER;
         const int nwz = (ng + PER - 1) / PER;
-        if (lane < nwz) {
+        if (lane < nwz) {                         // the word's PER fields: 16-B LDS reads, the
+            const int nz = min(PER, ng - lane * PER); // slots past the tile's groups masked
+            uint32_t zf[PER];
+#pragma unroll
+            for (int h = 0; h < PER / 4; ++h) {
+                const u4 q4 = *(const u4*)&zst[lane * PER + 4 * h];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) zf[4 * h + i] = q4[i];
+            }
             uint32_t word = 0;
-            for (int i = 0; i < PER && lane * PER + i < ng; ++i) word |= zst[lane * PER + i] << (BITS * i);
+#pragma unroll
+            for (int i = 0; i < PER; ++i) word |= (i < nz ? zf[i] : 0u) << (BITS * i);
             qzeros[r * zpr + g0 / PER + lane] = (int32_t)word;
         }
     }
@@ -637,7 +650,7 @@ RgPlan rowgroup_plan(int dtype, int64_t K, int64_t L) {
     if (dtype != AWQ_DTYPE_BF16 && dtype != AWQ_DTYPE_F16 && dtype != AWQ_DTYPE_F32) return pl;
     const int64_t es = dtype == AWQ_DTYPE_F32 ? 4 : 2;
     // (L = 1: a one-element group's NaN scale keeps the element's own NaN bits — generic kernel)
-    if (L < 2 || K <= 0 || 8 * L * es > kRgStageBytes) return pl;
+    if (L < 2 || K <= 0 || K >= ((int64_t)1 << 30) || 8 * L * es > kRgStageBytes) return pl;
     const bool ew = tuning().rg_waves == 1 || tuning().rg_waves == 2;
     if (ew) pl.waves = tuning().rg_waves;
     if (const int v = tuning().rg_gpt) {

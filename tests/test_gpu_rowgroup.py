@@ -146,3 +146,15 @@ def test_rowgroup_pass1_split_runs(dtype, shape, gs):
     with _hip.tuning(rg_p1=2):
         for bits, sym in ((4, False), (8, True)):
             _assert_parity(rand(shape, gs + bits + 7, 0.5, dtype), gs, bits, sym)
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16], ids=str)
+@pytest.mark.parametrize("K,gs", [(4096, 100), (4096, 96), (4096, 48), (4096, 200), (3000, 100), (4104, 100)], ids=str)
+def test_rowgroup_whole_row_tiles(dtype, K, gs):
+    """Whole-row two-wave tiles (K >= 2 560, <= 64 groups): the exactly-4-chunks-per-lane
+    stage (K = 4096: 512 chunks on 128 lanes), the uniform full sweeps of pass 2 and the
+    guarded remainder (K = 3000, 4104), the packed-only and parity kernels, special values."""
+    x = rand((96, K), K + gs, 0.5, dtype)
+    for bits, sym in ((4, False), (8, True)):
+        _assert_parity(x, gs, bits, sym)
+    _assert_parity(specials(rand((24, K), gs, 1.0), 3).to(dtype), gs, 4, False)

@@ -19,6 +19,8 @@ from typing import Any, List
 
 import torch
 
+_SYSRAND = random.SystemRandom()
+
 _STORAGE = {
     torch.float32: b"FloatStorage", torch.float64: b"DoubleStorage", torch.float16: b"HalfStorage",
     torch.bfloat16: b"BFloat16Storage", torch.int64: b"LongStorage", torch.int32: b"IntStorage",
@@ -104,7 +106,7 @@ def save(obj: Any, path: str) -> None:
     ptrs = (ctypes.c_void_p * max(n, 1))(*[t.data_ptr() for t in tensors])
     sizes = (ctypes.c_int64 * max(n, 1))(*[t.numel() * t.element_size() for t in tensors])
     archive = os.path.splitext(os.path.basename(path))[0]
-    sid = "".join(random.choice("0123456789") for _ in range(40))
+    sid = "".join(_SYSRAND.choice("0123456789") for _ in range(40))   # leaves the caller's RNG alone
     rc = _library().awq_write_pt(path.encode(), archive.encode(), pkl, len(pkl), n, ptrs, sizes, sid.encode())
     if rc in (1, 2):      # 2: would need ZIP64; 1: I/O error — torch.save raises it with its errno
         torch.save(obj, path)

@@ -258,7 +258,8 @@ int awq_write_pt(const char* path, const char* archive, const char* pkl, int64_t
         put32(cd, (uint32_t)r.offset);
         cd += r.name;
     }
-    if (off + cd.size() + 22 >= kLim) return 2;
+    // the EOCD's entry counts are 16-bit: a larger archive needs ZIP64 (torch.save writes it)
+    if (off + cd.size() + 22 >= kLim || recs.size() >= 0xFFFF) return 2;
     std::string eocd;
     put32(eocd, 0x06054b50u);
     put16(eocd, 0);

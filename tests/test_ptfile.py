@@ -109,3 +109,30 @@ def test_parallel_writers(tmp_path):
         assert zipfile.ZipFile(p).testzip() is None
         _assert_same(torch.load(p, weights_only=True), d)
     assert not os.path.exists(str(tmp_path / "model_chunk_0024.pt"))
+
+
+def test_too_many_records_falls_back_to_torch_save(tmp_path, lib):
+    """The EOCD entry counts are 16-bit: >= 0xFFFF records must go to torch.save (ZIP64)."""
+    import ctypes
+    n = 0xFFFF
+    buf = torch.zeros(n, dtype=torch.int32)
+    ptrs = (ctypes.c_void_p * n)(*[buf.data_ptr() + 4 * i for i in range(n)])
+    sizes = (ctypes.c_int64 * n)(*([4] * n))
+    p = str(tmp_path / "big.pt")
+    rc = lib.awq_write_pt(p.encode(), b"big", b"\x80\x02N.", 4, n, ptrs, sizes, b"0" * 40)
+    assert rc == 2
+    assert not os.path.exists(p)
+    # through ptfile.save: the torch.save fallback, which torch.load reads back whole
+    d = {f"t{i}": torch.tensor([i], dtype=torch.int32) for i in range(n)}
+    ptfile.save(d, p)
+    got = torch.load(p, weights_only=True)
+    assert len(got) == n and int(got["t65534"][0]) == 65534
+
+
+def test_save_leaves_python_rng_alone(tmp_path):
+    import random
+    random.seed(1234)
+    want = random.random()
+    random.seed(1234)
+    ptfile.save(_chunk(), str(tmp_path / "model_chunk_0000.pt"))
+    assert random.random() == want

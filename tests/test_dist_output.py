@@ -40,6 +40,17 @@ def _model(tmp_path):
 
 def fake_result(name, fmt, shape=(3, 16)):
     h = sum(map(ord, name)) % 1000
+    if fmt == "sized":      # packed fields at the tensor's own packed shapes, random bits
+        import zlib
+        rows = shape[0] if len(shape) > 1 else 1
+        K = int(torch.Size(shape).numel()) // rows
+        G = -(-K // 128)
+        g = torch.Generator().manual_seed(zlib.crc32(name.encode()))
+        rnd = lambda *sh: torch.randint(-2 ** 31, 2 ** 31 - 1, sh, generator=g, dtype=torch.int64).to(torch.int32)
+        return {"qweight": rnd(rows, -(-K // 8)), "qzeros": rnd(rows, -(-G // 8)),
+                "scales": (rnd(rows, G) >> 16).to(torch.int16).view(torch.float16),
+                "bits": torch.tensor(4, dtype=torch.int32), "group_size": torch.tensor(128, dtype=torch.int32),
+                "symmetric": torch.tensor(False), "shape": torch.tensor(list(shape), dtype=torch.int64)}
     if fmt == "autoawq":
         return {"qweight": torch.full((128, 1), h, dtype=torch.int32), "qzeros": torch.full((1, 1), h, dtype=torch.int32),
                 "scales": torch.full((1, 8), h / 1000, dtype=torch.float16)}
@@ -82,7 +93,7 @@ def _worker(rank, world, port, model_dir, out_dir, fmt, extra, fail_rank, q, inj
                 raise OSError("disk full (injected)")
             M._write_metadata = bad_meta
         rc = M.main(["--model_id", model_dir, "--output_dir", out_dir, "--log_level", "CRITICAL", "--chunk_size", "4",
-                     "--output_format", fmt] + extra)
+                     "--output_format", "packed" if fmt == "sized" else fmt] + extra)
         q.put((rank, rc))
     except BaseException as e:  # surface to the parent
         q.put((rank, repr(e)))
@@ -263,3 +274,55 @@ def test_failure_after_renames_unpublishes_every_chunk(tmp_path):
     assert _run(2, model_dir, out, "packed", inject="meta") == [1, 1]
     assert not os.path.exists(os.path.join(out, "metadata.json"))
     assert [f for f in os.listdir(out) if "chunk" in f] == []
+
+
+def _llama70b_scaled_model(tmp_path):
+    """The Llama-3-70B tensor set (723 names, tests/test_distributed.py) with rows / 256 and
+    row lengths / 64, so byte sizes keep the real set's ratios (2-D) and order."""
+    from test_distributed import _llama70b_names_shapes
+    d = tmp_path / "model70b"
+    d.mkdir()
+    ts = _llama70b_names_shapes()
+    g = torch.Generator().manual_seed(0)
+    t = {n: (torch.randn(*((sh[0] // 256, sh[1] // 64) if len(sh) > 1 else (sh[0] // 64,)), generator=g) * 0.02)
+         .bfloat16() for n, sh in ts.items()}
+    names = list(t)
+    for k in range(4):      # four shard files, like a real multi-file checkpoint
+        save_file({n: t[n] for n in names[k::4]}, str(d / f"model-{k + 1:05d}-of-00004.safetensors"))
+    return str(d)
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("mode", ["per_rank", "gather"])
+def test_world8_llama70b_per_rank_chunks(tmp_path, mode):
+    """the per-rank chunk commit at world 8 on the 70B ownership map (723
+    names, the scaled set's LPT shard): the union of the 8 ranks' renumbered chunk files,
+    read through metadata.json, is byte-exact against the single-process writer's files."""
+    model_dir = _llama70b_scaled_model(tmp_path)
+    out = str(tmp_path / "out")
+    assert _run(8, model_dir, out, "sized", ["--dist_output", mode]) == [0] * 8
+    from awq_quantizer.main import save_model_in_chunks, select_tensors
+    from awq_quantizer.model_loading import load_model_from_path
+    sel = select_tensors(load_model_from_path(model_dir, logger_level="ERROR").tensor_index())
+    assert len(sel) == 723
+    res = {i.name: fake_result(i.name, "sized", tuple(i.shape)) for i in sel if i.name not in FAIL_NAMES}
+    ref = str(tmp_path / "single")
+    save_model_in_chunks(res, ref, chunk_size=4)
+    meta, got = _load_chunks(out)
+    ref_meta, want = _load_chunks(ref)
+    # every tensor, processing order; per-rank chunks of <= 4, numbered 0.. over the ranks
+    assert list(meta["tensor_to_chunk"]) == list(ref_meta["tensor_to_chunk"]) == [i.name for i in sel]
+    for k in ("chunk_size", "format", "num_tensors", "quantization_params"):
+        assert meta[k] == ref_meta[k], k
+    if mode == "gather":        # rank 0 wrote everything: the single-process grouping
+        assert meta == ref_meta
+    files = sorted(f for f in os.listdir(out) if f != "metadata.json")
+    assert files == [f"model_chunk_{c:04d}.pt" for c in range(meta["num_chunks"])]
+    assert max(list(meta["tensor_to_chunk"].values()).count(c) for c in range(meta["num_chunks"])) <= 4
+    for n in want:
+        assert list(got[n]) == list(want[n]), n
+        for f in want[n]:
+            a, b = got[n][f], want[n][f]
+            assert a.dtype == b.dtype and a.shape == b.shape, (n, f)
+            assert torch.equal(a.view(torch.int16) if a.dtype == torch.float16 else a,
+                               b.view(torch.int16) if b.dtype == torch.float16 else b), (n, f)

@@ -16,7 +16,7 @@ import torch
 
 LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib")
 LIB_PATH = os.path.join(LIB_DIR, "libawq_hip.so")
-ABI_VERSION = 12
+ABI_VERSION = 13
 Q_SMALL_TENSOR = 1      # include/awq_hip.h AWQ_Q_SMALL_TENSOR
 
 AWQ_DTYPE = {torch.bfloat16: 0, torch.float16: 1, torch.float32: 2, torch.float64: 3}
@@ -40,13 +40,14 @@ class StreamItem(ctypes.Structure):
     """Mirror of awq_stream_item (include/awq_hip.h)."""
     _fields_ = [("fd", _I32), ("dtype", _I32), ("offset", _I64), ("rows", _I64), ("K", _I64), ("qweight", _P),
                 ("qzeros", _P), ("scales", _P), ("tensor_q", _P), ("zeros", _P), ("dev_out", _P), ("host_out", _P),
-                ("out_bytes", _I64), ("dev_out2", _P), ("host_out2", _P), ("out_bytes2", _I64)]
+                ("out_bytes", _I64), ("dev_out2", _P), ("host_out2", _P), ("out_bytes2", _I64),
+                ("dev_gate", _I32), ("host_gate", _I32)]
 
 
 class StreamConfig(ctypes.Structure):
     """Mirror of awq_stream_config (include/awq_hip.h)."""
     _fields_ = [("bits", _I32), ("symmetric", _I32), ("group_size", _I32), ("readers", _I32), ("nslots", _I32),
-                ("trace_batches", _I32), ("slot_bytes", _I64), ("first_batch_bytes", _I64), ("host_staging", _P),
+                ("trace_batches", _I32), ("search_grid", _I32), ("search_candidates", _I32), ("slot_bytes", _I64), ("first_batch_bytes", _I64), ("host_staging", _P),
                 ("dev_staging", _P), ("compute_stream", _P),
                 ("h2d_stream", _P), ("d2h_stream", _P), ("trace", _P)]
 
@@ -59,10 +60,11 @@ STREAM_TRACE_NAMES = ("read_first", "read_last", "h2d_enq", "kern_enq", "d2h_enq
 class StreamStats(ctypes.Structure):
     """Mirror of awq_stream_stats (include/awq_hip.h)."""
     _fields_ = [("batches", _I64), ("pieces", _I64), ("bytes_read", _I64), ("wall_s", ctypes.c_double),
-                ("read_busy_s", ctypes.c_double), ("wait_read_s", ctypes.c_double), ("wait_slot_s", ctypes.c_double)]
+                ("read_busy_s", ctypes.c_double), ("wait_read_s", ctypes.c_double), ("wait_slot_s", ctypes.c_double),
+                ("wait_release_s", ctypes.c_double)]
 
 
-assert ctypes.sizeof(StreamItem) == 120 and ctypes.sizeof(StreamConfig) == 88
+assert ctypes.sizeof(StreamItem) == 128 and ctypes.sizeof(StreamConfig) == 96
 
 
 class Tuning(ctypes.Structure):
@@ -105,6 +107,9 @@ SIGNATURES = {
     "awq_stream_start": (_I32, [ctypes.POINTER(StreamItem), _I32, ctypes.POINTER(StreamConfig),
                                 ctypes.POINTER(ctypes.c_void_p)]),
     "awq_stream_batches": (_I64, [_P]),
+    "awq_stream_plan": (_I64, [ctypes.POINTER(StreamItem), _I32, ctypes.POINTER(StreamConfig),
+                               ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int32)]),
+    "awq_stream_release": (_I32, [_P, _I32]),
     "awq_stream_wait": (_I32, [_P, _I64, ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int32)]),
     "awq_stream_end": (_I32, [_P, ctypes.POINTER(StreamStats)]),
     "awq_act_stats": (_I32, [_P, _I32, _I64, _I64, _P, _P, _P, _P]),

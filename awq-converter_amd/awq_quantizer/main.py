@@ -324,6 +324,8 @@ class ChunkWriter:
         self.error: Optional[BaseException] = None
         self.cv = threading.Condition()
         self.times: List[Tuple[float, float, float]] = []   # per chunk: submitted, started, ended (time.time)
+        self.failed: set = set()
+        self.hooks: List[Callable[[List[str]], None]] = []
         os.makedirs(output_dir, exist_ok=True)
         self.thread = threading.Thread(target=self._run, daemon=True)
         self.thread.start()
@@ -332,7 +334,25 @@ class ChunkWriter:
         """A tensor finished: its host result dict, or None if it failed."""
         with self.cv:
             self.status[name] = result
+            if result is None:
+                self.failed.add(name)
             self.cv.notify()
+
+    def add_written_hook(self, fn: Callable[[List[str]], None]) -> None:
+        """fn(names) after each chunk file is written: its results are no longer read."""
+        with self.cv:
+            self.hooks.append(fn)
+
+    def predict_groups(self) -> Dict[str, int]:
+        """The chunk every tensor not yet known to have failed lands in, if it succeeds."""
+        with self.cv:
+            failed = set(self.failed)
+        out, k = {}, 0
+        for name in self.order:
+            if name not in failed:
+                out[name] = k // self.size
+                k += 1
+        return out
 
     def _run(self) -> None:
         try:
@@ -370,6 +390,12 @@ class ChunkWriter:
             t0 = time.time()
             _write_chunk(chunk, self.dir, c, self.st, self.logger, stem=self.stem)
             self.times.append((t_submit, t0, time.time()))
+        names = list(chunk)
+        chunk.clear()               # the results are views of a ring the pipeline will reuse
+        with self.cv:
+            hooks = list(self.hooks)
+        for fn in hooks:
+            fn(names)
 
     def close(self) -> None:
         """Every producer has finished: unfinished tensors count as failed; wait for the writes."""
@@ -535,210 +561,25 @@ def _pinned_copy(t: torch.Tensor) -> torch.Tensor:
     return p
 
 
-def _out_fields(info: TensorInfo, rows: int, K: int, gs: int, bits: int, packed: bool):
-    """(field, shape, dtype) of one tensor's results: the packed format (quantize_packed) or
-    the reference's result dict (awq.py:409-416)."""
-    per = 32 // bits
-    G = -(-K // gs)
-    if packed:
-        return [("qweight", (rows, -(-K // per)), torch.int32), ("qzeros", (rows, -(-G // per)), torch.int32),
-                ("scales", (rows, G), torch.float16)]
-    return [("tensor_q", tuple(info.shape), torch.int32), ("scales", (rows, G), torch.float16),
-            ("zero_points", (rows, G), torch.int32)]
-
-
-_STREAM_PTR_FIELD = {"qweight": "qweight", "qzeros": "qzeros", "scales": "scales", "tensor_q": "tensor_q",
-                     "zero_points": "zeros"}
-
-
 def quantize_stream_native(loader, infos: List[TensorInfo], quantizer: AWQQuantizer, device: str, readers: int,
                            packed: bool, out: Dict, lock: threading.Lock, logger, keep_on_device: bool = False,
                            on_done: Optional[Callable[[str, Optional[Dict[str, torch.Tensor]]], None]] = None,
-                           chunk_of: Optional[Dict[str, int]] = None, slot_bytes: int = 0) -> None:
-    """The CLI's read -> quantize -> collect loop on the native pipeline (include/awq_hip.h
-    awq_stream_*): reader threads pread every tensor from its file into pinned staging slots,
-    one H2D per slot, one ragged launch per dtype per batch, the D2H of the outputs — all
-    native, overlapped, no per-tensor Python in the loop.  Results are views of one device
-    arena and, on the host, of one pinned buffer per output chunk (`chunk_of`: the
-    ChunkWriter's chunk of every tensor, so a chunk file stores only its own tensors' bytes).
-    Tensors smaller than one group (awq.py:297-300) take the per-tensor path afterwards;
-    non-floating tensors are logged and skipped (main.py:387-390)."""
-    from . import _hip
-    t_enter = time.perf_counter()
-    if not (device.startswith("cuda") and torch.cuda.is_available()):
-        quantizer.compute_device()   # raises HipUnavailable: no CPU path
-    dev = torch.device(device)
-    if dev.index is None:
-        dev = torch.device("cuda", torch.cuda.current_device())
-    torch.cuda.set_device(dev)
-    quantizer.compute_device()
-    quantizer._check_mode()
-    gs, bits = quantizer.group_size, quantizer.bits
-    items, small = [], []
-    for info in infos:
-        if info.dtype not in _hip.AWQ_DTYPE:
-            if logger:
-                logger.error(f"Error quantizing tensor: {info.name}, error: Expected floating point tensor, "
-                             f"got {info.dtype}")
-            if on_done:
-                on_done(info.name, None)
-            continue
-        if info.numel < gs:
-            small.append(info)
-            continue
-        rows = 1 if len(info.shape) <= 1 else info.shape[0]
-        items.append((info, rows, info.numel // rows))
-    # output layout: per dtype (int32 words / fp16 scales) every tensor's fields back to back
-    # (16-B aligned) in one device arena, and per output chunk one pinned host buffer of that
-    # dtype (torch.save stores a storage once per file, but only under one dtype) with the
-    # same relative layout, so adjacent D2H ranges merge
-    kinds = (torch.int32, torch.float16)
-    es_of = {torch.int32: 4, torch.float16: 2}
-    per16 = {dt: 16 // es for dt, es in es_of.items()}   # elements per 16 B
-    lay, dev_total = [], {dt: 0 for dt in kinds}
-    seg_size = {}
-    for info, rows, K in items:
-        seg = chunk_of.get(info.name, 0) if chunk_of else len(lay) // 16
-        fields, size = [], {dt: 0 for dt in kinds}
-        for f, shp, dt in _out_fields(info, rows, K, gs, bits, packed):
-            n = math.prod(shp)
-            fields.append((f, shp, dt, size[dt], n))
-            size[dt] += -(-n // per16[dt]) * per16[dt]
-        ss = seg_size.setdefault(seg, {dt: 0 for dt in kinds})
-        lay.append((fields, size, dict(dev_total), seg, dict(ss)))
-        for dt in kinds:
-            ss[dt] += size[dt]
-            dev_total[dt] += size[dt]
-    t_alloc = time.perf_counter()
-    arena = {dt: torch.empty(max(dev_total[dt], 8), dtype=dt, device=dev) for dt in kinds}
-    t_arena = time.perf_counter()
-    hosts = {}
-    if not keep_on_device and STREAM_OPTS.get("host_arena", 1):
-        # one pinned allocation per dtype, every chunk's buffer a separate storage carved
-        # from it (torch.frombuffer: torch.save writes only the chunk's bytes).  With one
-        # pinned allocation per chunk (STREAM_OPTS host_arena=0), D2H calls into a chunk's
-        # buffer stalled the submitter for 7-8 ms at a time (profiles/round3/cli/r3r_*)
-        for dt in kinds:
-            tot = sum(max(n[dt], 8) for n in seg_size.values())
-            big = torch.empty(tot, dtype=dt, pin_memory=True)
-            raw, off = big.view(torch.uint8).numpy(), 0
-            for sg, n in seg_size.items():
-                m = max(n[dt], 8)
-                hosts.setdefault(sg, {})[dt] = torch.frombuffer(raw, dtype=dt, count=m, offset=off * es_of[dt])
-                off += m
-            hosts.setdefault("_keep", {})[dt] = big
-    elif not keep_on_device:
-        # page-locking is the cost of a process's first run (≈0.1 s per GB): the per-chunk
-        # buffers are pinned by a few threads at once
-        jobs = [(sg, dt, max(n[dt], 8)) for sg, n in seg_size.items() for dt in kinds]
-        with ThreadPoolExecutor(max_workers=min(8, max(1, cpu_share() // 2), len(jobs))) as pool:
-            bufs = list(pool.map(lambda j: torch.empty(j[2], dtype=j[1], pin_memory=True), jobs))
-        for (sg, dt, _), b in zip(jobs, bufs):
-            hosts.setdefault(sg, {})[dt] = b
-    lib = _hip.load_library()
-    arr = (_hip.StreamItem * max(1, len(items)))()
-    dptr = {dt: arena[dt].data_ptr() for dt in kinds}
-    hptr = {} if keep_on_device else {sg: {dt: h[dt].data_ptr() for dt in kinds} for sg, h in hosts.items()}
-    i32, f16 = kinds
-    for k, ((info, rows, K), (fields, size, doff, seg, hoff)) in enumerate(zip(items, lay)):
-        fd, at = loader.data_location(info)
-        it = arr[k]
-        it.fd, it.dtype, it.offset = fd, _hip.AWQ_DTYPE[info.dtype], at
-        it.rows, it.K = rows, K
-        for f, _, dt, off, _ in fields:
-            setattr(it, _STREAM_PTR_FIELD[f], dptr[dt] + (doff[dt] + off) * es_of[dt])
-        it.dev_out, it.out_bytes = dptr[i32] + doff[i32] * 4, size[i32] * 4
-        it.dev_out2, it.out_bytes2 = dptr[f16] + doff[f16] * 2, size[f16] * 2
-        if not keep_on_device:
-            it.host_out, it.host_out2 = hptr[seg][i32] + hoff[i32] * 4, hptr[seg][f16] + hoff[f16] * 2
-    total_in = sum(i.nbytes for i, _, _ in items)
-    slot = slot_bytes or STREAM_OPTS.get("slot_bytes") or min(256 << 20, max(32 << 20, total_in // 8))
-    slot = -(-slot // 4096) * 4096
-    nslots = int(STREAM_OPTS.get("nslots", 3))
-    tb = int(lib.awq_stream_table_bytes(slot))     # each slot: its table area, then its input
-    t_hosts = time.perf_counter()
-    h_stage = torch.empty(nslots * (tb + slot), dtype=torch.uint8, pin_memory=True)
-    d_stage = torch.empty(nslots * (tb + slot), dtype=torch.uint8, device=dev)
-    compute = torch.cuda.current_stream(dev)
-    h2d = torch.cuda.Stream(dev)
-    d2h = h2d if STREAM_OPTS.get("copy_streams", 2) == 1 else torch.cuda.Stream(dev)
-    cfg = _hip.StreamConfig(bits=bits, symmetric=int(bool(quantizer.symmetric)), group_size=gs,
-                            readers=int(STREAM_OPTS.get("readers", min(16, max(8, readers)))), nslots=nslots,
-                            slot_bytes=slot,
-                            first_batch_bytes=max(4096, slot // 4 // 4096 * 4096),
-                            host_staging=h_stage.data_ptr(), dev_staging=d_stage.data_ptr(),
-                            compute_stream=compute.cuda_stream, h2d_stream=h2d.cuda_stream,
-                            d2h_stream=d2h.cuda_stream)
-    trace = None
-    if STREAM_OPTS.get("trace"):
-        cap = len(items) + total_in // slot + 2
-        trace = (ctypes.c_double * (cap * _hip.STREAM_TRACE_FIELDS))()
-        cfg.trace, cfg.trace_batches = ctypes.addressof(trace), cap
-    handle = ctypes.c_void_p()
-    t_run = time.perf_counter()
-    _hip.check(lib.awq_stream_start(arr, len(items), ctypes.byref(cfg), ctypes.byref(handle)), "awq_stream_start")
-    stats = _hip.StreamStats()
-    t_wait = 0.0
-    try:
-        # while the pipeline runs: the result dicts (views of the arena / the chunk buffers)
-        scal = {"bits": torch.tensor(bits, dtype=torch.int32), "group_size": torch.tensor(gs, dtype=torch.int32),
-                "symmetric": torch.tensor(bool(quantizer.symmetric), dtype=torch.bool)}
-        results = []
-        for (info, rows, K), (fields, size, doff, seg, hoff) in zip(items, lay):
-            src, at = (arena, doff) if keep_on_device else (hosts[seg], hoff)
-            r = {f: src[dt][at[dt] + off:at[dt] + off + n].view(shp) for f, shp, dt, off, n in fields}
-            r.update(scal)
-            if packed:
-                r["shape"] = torch.tensor(list(info.shape), dtype=torch.int64)
-            results.append(r)
-        nb_ = int(lib.awq_stream_batches(handle))
-        i0, i1 = ctypes.c_int32(), ctypes.c_int32()
-        for b in range(nb_):
-            t0 = time.perf_counter()
-            _hip.check(lib.awq_stream_wait(handle, b, ctypes.byref(i0), ctypes.byref(i1)), "awq_stream_wait")
-            t_wait += time.perf_counter() - t0
-            done = {items[k][0].name: results[k] for k in range(i0.value, i1.value)}
-            with lock:
-                out.update(done)
-            if on_done:
-                for name, r in done.items():
-                    on_done(name, r)
-    finally:
-        rc = lib.awq_stream_end(handle, ctypes.byref(stats))
-    _hip.check(rc, "awq_stream_end")
-    if keep_on_device:
-        compute.wait_stream(d2h)
-    for info in small:                    # awq.py:297-300: the per-tensor path
-        try:
-            x = loader.read(info)
-            res = quantizer.quantize_model_device({info.name: x}, packed=packed)
-            r = {k: (v.cpu() if isinstance(v, torch.Tensor) and not keep_on_device else v)
-                 for k, v in res.get(info.name, {}).items()} if info.name in res else None
-        except Exception as e:  # noqa: BLE001
-            if logger:
-                logger.error(f"Error quantizing tensor: {info.name}, error: {e}")
-            r = None
-        if r is not None:
-            with lock:
-                out[info.name] = r
-        if on_done:
-            on_done(info.name, r)
-    TIMINGS.update({f"stream_{device}": {"engine": "native", "wall_s": round(time.perf_counter() - t_enter, 4),
-                                          "setup_s": round(t_run - t_enter, 4),
-                                          "alloc_dev_s": round(t_arena - t_alloc, 4),
-                                          "alloc_host_out_s": round(t_hosts - t_arena, 4),
-                                          "batches": int(stats.batches),
-                                          "pieces": int(stats.pieces), "slot_MB": slot >> 20,
-                                          "pipeline_s": round(stats.wall_s, 4), "wait_s": round(t_wait, 4),
-                                          "read_busy_s": round(stats.read_busy_s, 4),
-                                          "submit_wait_read_s": round(stats.wait_read_s, 4),
-                                          "submit_wait_slot_s": round(stats.wait_slot_s, 4),
-                                          "bytes_read": int(stats.bytes_read)}})
-    if trace is not None:
-        nf = _hip.STREAM_TRACE_FIELDS
-        TIMINGS[f"stream_{device}"]["trace"] = [
-            dict(zip(_hip.STREAM_TRACE_NAMES, (round(v, 5) for v in trace[b * nf:(b + 1) * nf])))
-            for b in range(min(int(stats.batches), cfg.trace_batches))]
+                           writer: Optional["ChunkWriter"] = None, slot_bytes: int = 0, host_ring_bytes: int = 0,
+                           dev_ring_bytes: int = 0) -> None:
+    """The CLI's read -> quantize -> collect loop on the native pipeline with bounded output
+    memory (awq_quantizer/stream.py).  With `writer` (the ChunkWriter that consumes
+    `on_done`'s results) the host ring may wrap: results are released once their chunk is
+    written; without it the host ring holds the whole output."""
+    from .stream import quantize_stream_native as run
+    hook = groups = None
+    if writer is not None and not keep_on_device:
+        hook = writer.add_written_hook
+        groups = writer.predict_groups
+    run(loader, infos, quantizer, device, readers, packed, out, lock, logger, keep_on_device=keep_on_device,
+        on_done=on_done, release_hook=hook, group_of=groups, slot_bytes=slot_bytes,
+        host_ring_bytes=host_ring_bytes or int(STREAM_OPTS.get("host_ring_bytes", 0)),
+        dev_ring_bytes=dev_ring_bytes or int(STREAM_OPTS.get("dev_ring_bytes", 0)),
+        opts=STREAM_OPTS, timings=TIMINGS)
 
 
 def quantize_stream(loader, infos: List[TensorInfo], quantizer: AWQQuantizer, device: str, readers: int,
@@ -747,13 +588,16 @@ def quantize_stream(loader, infos: List[TensorInfo], quantizer: AWQQuantizer, de
                     batch_bytes: int = 1 << 30, export_autoawq: bool = False,
                     act_stats: Optional[Dict[str, Tuple[torch.Tensor, torch.Tensor]]] = None,
                     on_done: Optional[Callable[[str, Optional[Dict[str, torch.Tensor]]], None]] = None,
-                    chunk_of: Optional[Dict[str, int]] = None, engine: str = "native") -> None:
-    """Quantize `infos` on one GPU.  RTN to the packed or reference format runs on the native
-    pipeline (quantize_stream_native); the activation-aware search (`act_stats`), the
-    AutoAWQ export and `engine="python"` on the Python pipeline below."""
+                    writer: Optional["ChunkWriter"] = None, engine: str = "native") -> None:
+    """Quantize `infos` on one GPU.  RTN and the per-group clip search (scale_method
+    "search") to the packed or reference format run on the native pipeline
+    (quantize_stream_native; `writer`: the ChunkWriter consuming on_done, whose written
+    chunks release the pipeline's host ring — only when it serves this device alone); the
+    activation-aware search (`act_stats`), the AutoAWQ export and `engine="python"` on the
+    Python pipeline below."""
     if engine == "native" and not act_stats and not export_autoawq and hasattr(loader, "data_location"):
         return quantize_stream_native(loader, infos, quantizer, device, readers, packed, out, lock, logger,
-                                      keep_on_device=keep_on_device, on_done=on_done, chunk_of=chunk_of)
+                                      keep_on_device=keep_on_device, on_done=on_done, writer=writer)
     return quantize_stream_python(loader, infos, quantizer, device, readers, lookahead, packed, out, lock, logger,
                                   memory_efficient, keep_on_device, batch_bytes, export_autoawq, act_stats, on_done)
 
@@ -1069,7 +913,10 @@ def main(argv: Optional[List[str]] = None) -> int:
         if not autoawq:
             writer = ChunkWriter([i.name for i in ordered], args.output_dir, args.chunk_size, args.save_safetensors,
                                  logger, writers=writer_threads(ordered, packed))
-        chunk_of = {i.name: k // args.chunk_size for k, i in enumerate(ordered)}
+        if writer is not None:
+            # the writer owns every result until its chunk is on disk; a device's pipeline may
+            # then reuse (wrap) its host output ring — only when it is the writer's only producer
+            results = _NullSink()
         threads = []
         TIMINGS["pre_stream_s"] = time.time() - start
         for d, part in zip(devices, parts):
@@ -1078,7 +925,8 @@ def main(argv: Optional[List[str]] = None) -> int:
                                                                lookahead, packed, results, lock, logger,
                                                                args.memory_efficient, False, 1 << 30, autoawq),
                                   kwargs={"act_stats": act_stats, "on_done": writer.done if writer else None,
-                                          "chunk_of": chunk_of, "engine": args.stream_engine})
+                                          "writer": writer if len(devices) == 1 else None,
+                                          "engine": args.stream_engine})
             th.start()
             threads.append(th)
         for th in threads:
@@ -1194,8 +1042,7 @@ def _main_distributed(args, loader, ordered: List[TensorInfo], logger, start: fl
         quantize_stream(loader, mine, q, device, args.num_workers, max(1, args.prefetch_factor * args.batch_size),
                         args.output_format in ("packed", "autoawq"), sink, threading.Lock(), logger,
                         args.memory_efficient, keep_on_device=not per_rank, export_autoawq=autoawq,
-                        act_stats=act_stats, on_done=writer.done if writer else None,
-                        chunk_of={i.name: k // args.chunk_size for k, i in enumerate(mine)},
+                        act_stats=act_stats, on_done=writer.done if writer else None, writer=writer,
                         engine=args.stream_engine)
     except Exception as e:  # noqa: BLE001  (agreed below: every rank exits 1)
         logger.error(f"rank {rank}: quantization failed: {e}")
@@ -1256,10 +1103,16 @@ def _shared_output_dir(output_dir: str, rank: int, world: int, logger) -> bool:
 
 
 class _NullSink(dict):
-    """quantize_stream's result dict when a ChunkWriter already owns every result."""
+    """quantize_stream's result dict when a ChunkWriter already owns every result: it keeps
+    the names only (the results may be views of a ring the pipeline reuses once written)."""
+
+    def __setitem__(self, name, value) -> None:
+        super().__setitem__(name, None)
 
     def update(self, *a, **k) -> None:
-        pass
+        for d in a + (k,):
+            for name in d:
+                super().__setitem__(name, None)
 
 
 def _rank_stem(rank: int) -> str:

@@ -1,0 +1,396 @@
+"""The CLI's native read -> quantize -> copy-back loop (include/awq_hip.h awq_stream_*) with
+BOUNDED output memory.
+
+Replaces the reference's per-tensor loop (src/awq_quantizer/main.py:216-392: every file
+loaded whole, every tensor moved to the device eagerly, then quantized one by one).  Reader
+threads pread every tensor from its safetensors file into pinned staging slots, one H2D per
+slot, one ragged launch per dtype and batch, the D2H of the finished tensors — native,
+overlapped, no per-tensor Python in the loop.
+
+Output memory (round 4; ADVICE r3: one device arena plus one pinned buffer sized to the
+whole output does not fit a 70B model in the reference format):
+
+  * every tensor's outputs are one region (its fields back to back, 256-B aligned), placed
+    FIFO in a device ring and, for host results, in a pinned host ring;
+  * a region that overlaps earlier ones carries gates (awq_stream_item dev_gate /
+    host_gate): its kernels wait for the D2H of the items it overwrites (on the compute
+    stream), its D2H for the caller's release of their host results (awq_stream_release,
+    called once their chunk files are on disk: ChunkWriter.add_written_hook);
+  * the rings are sized by simulation against the pipeline's own batch plan
+    (awq_stream_plan): the smallest size, from a floor up, for which no batch waits on its
+    own items — so the pipeline cannot deadlock on the writer.  When the whole output fits
+    the floor, nothing wraps and nothing waits.
+
+Results handed to `on_done` are views of the host ring, valid until released: with a
+release hook the caller must not keep them past its write (the CLI's ChunkWriter does
+not); without one the host ring holds the whole output (no wrap).
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+import threading
+import time
+import weakref
+from typing import Callable, Dict, List, Optional, Sequence, Tuple
+
+import torch
+
+ALIGN = 256                  # byte alignment of every output field inside a region
+_ES = {torch.int32: 4, torch.float16: 2}
+HOST_RING_FLOOR = 512 << 20  # smallest host ring tried when the output does not fit it
+DEV_RING_FLOOR = 1 << 30
+
+
+def out_fields(shape, rows: int, K: int, gs: int, bits: int, packed: bool):
+    """(field, shape, dtype) of one tensor's results: the packed format (quantize_packed) or
+    the reference's result dict (awq.py:409-416)."""
+    per = 32 // bits
+    G = -(-K // gs)
+    if packed:
+        return [("qweight", (rows, -(-K // per)), torch.int32), ("qzeros", (rows, -(-G // per)), torch.int32),
+                ("scales", (rows, G), torch.float16)]
+    return [("tensor_q", tuple(shape), torch.int32), ("scales", (rows, G), torch.float16),
+            ("zero_points", (rows, G), torch.int32)]
+
+
+def region_layout(shape, rows: int, K: int, gs: int, bits: int, packed: bool):
+    """[(field, shape, dtype, byte offset, bytes)] of one region and its size (ALIGN multiple)."""
+    fields, off = [], 0
+    for f, shp, dt in out_fields(shape, rows, K, gs, bits, packed):
+        nb = math.prod(shp) * _ES[dt]
+        fields.append((f, shp, dt, off, nb))
+        off += -(-nb // ALIGN) * ALIGN
+    return fields, max(off, ALIGN)
+
+
+def ring_place(sizes: Sequence[int], cap: int) -> Optional[Tuple[List[int], List[int]]]:
+    """FIFO placement of consecutive regions in a ring of `cap` bytes (a region that does
+    not fit before the end starts at 0).  Returns (offsets, gates): gate[i] = 1 + the
+    latest earlier region that region i overwrites (0: none) — before i is written, every
+    region up to that one must be drained.  None if a region exceeds the ring."""
+    offs, gates = [], []
+    live: List[Tuple[int, int, int]] = []     # (start, end, index) of regions not yet overwritten
+    head = 0
+    for i, sz in enumerate(sizes):
+        if sz > cap:
+            return None
+        if head + sz > cap:
+            head = 0
+        lo, hi = head, head + sz
+        g, keep = 0, []
+        for (a, b, j) in live:
+            if a < hi and lo < b:
+                g = max(g, j + 1)
+            else:
+                keep.append((a, b, j))
+        keep.append((lo, hi, i))
+        live = keep
+        offs.append(lo)
+        gates.append(g)
+        head = hi
+    return offs, gates
+
+
+def dev_gates_ok(gates: Sequence[int], first_batch: Sequence[int], last_batch: Sequence[int]) -> bool:
+    """A device region may be overwritten by kernels of a batch after the one that copies
+    the old contents back (the pipeline waits on that D2H event)."""
+    return all(g == 0 or last_batch[g - 1] < first_batch[i] for i, g in enumerate(gates))
+
+
+def host_gates_ok(gates: Sequence[int], last_batch: Sequence[int], group_end: Sequence[int]) -> bool:
+    """A host region may be overwritten by the D2H of a batch only if everything its gate
+    waits for can be released before that batch completes: the caller releases an item
+    once its whole group (its output chunk) has completed, i.e. after the batch that
+    completes the group's last item, group_end[j]."""
+    return all(g == 0 or last_batch[group_end[g - 1]] < last_batch[i] for i, g in enumerate(gates))
+
+
+def size_ring(sizes: Sequence[int], floor: int, ok: Callable[[List[int]], bool]) -> Tuple[int, List[int], List[int]]:
+    """The smallest ring (floor, then x1.5 steps) whose placement passes `ok`; the whole
+    output (no wrap, no gates) when nothing smaller does."""
+    total = sum(sizes)
+    cap = max(floor, max(sizes, default=0))
+    while cap < total:
+        p = ring_place(sizes, cap)
+        if p is not None and ok(p[1]):
+            return cap, p[0], p[1]
+        cap = int(cap * 1.5) // ALIGN * ALIGN + ALIGN
+    offs, o = [], 0
+    for s in sizes:
+        offs.append(o)
+        o += s
+    return max(total, ALIGN), offs, [0] * len(sizes)
+
+
+# ---- page-locked host memory ------------------------------------------------------------
+_HIP = None
+
+
+def _hip_runtime():
+    global _HIP
+    if _HIP is None:
+        _HIP = ctypes.CDLL("libamdhip64.so")
+        _HIP.hipHostMalloc.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_size_t, ctypes.c_uint]
+        _HIP.hipHostFree.argtypes = [ctypes.c_void_p]
+    return _HIP
+
+
+def pinned_bytes(nbytes: int) -> torch.Tensor:
+    """A uint8 tensor over `nbytes` of page-locked host memory of EXACTLY that size
+    (hipHostMalloc; torch's caching host allocator rounds a request up to a power of two,
+    pinning up to twice the bytes — the first run's setup cost).  Freed when the last view
+    of it is gone."""
+    hip = _hip_runtime()
+    p = ctypes.c_void_p()
+    rc = hip.hipHostMalloc(ctypes.byref(p), ctypes.c_size_t(max(nbytes, 1)), 0)
+    if rc != 0 or not p.value:
+        raise MemoryError(f"hipHostMalloc({nbytes}) failed ({rc})")
+    arr = (ctypes.c_uint8 * max(nbytes, 1)).from_address(p.value)
+    weakref.finalize(arr, hip.hipHostFree, ctypes.c_void_p(p.value))
+    return torch.frombuffer(arr, dtype=torch.uint8, count=nbytes) if nbytes else torch.empty(0, dtype=torch.uint8)
+
+
+def _view(buf: torch.Tensor, off: int, nbytes: int, dt: torch.dtype, shape) -> torch.Tensor:
+    """A field view of a region: its own storage object over the bytes (torch.save and
+    ptfile write a storage whole, so a field must not share one with the ring)."""
+    if buf.device.type == "cpu":
+        arr = (ctypes.c_uint8 * max(nbytes, 1)).from_address(buf.data_ptr() + off)
+        arr._ring = buf          # keeps the ring alive as long as the view
+        return torch.frombuffer(arr, dtype=dt, count=nbytes // _ES[dt]).view(shape) if nbytes else \
+            torch.empty(shape, dtype=dt)
+    return buf[off:off + nbytes].view(dt).view(shape)
+
+
+_PTR = {"qweight": "qweight", "qzeros": "qzeros", "scales": "scales", "tensor_q": "tensor_q", "zero_points": "zeros"}
+
+
+class _Releaser:
+    """Advances awq_stream_release over the items whose results have been written."""
+
+    def __init__(self, lib, names: List[str]):
+        self.lib, self.index = lib, {n: k for k, n in enumerate(names)}
+        self.done = [False] * len(names)
+        self.prefix, self.handle = 0, None
+        self.mu = threading.Lock()
+
+    def written(self, names: Sequence[str]) -> None:
+        with self.mu:
+            for n in names:
+                k = self.index.get(n)
+                if k is not None:
+                    self.done[k] = True
+            p = self.prefix
+            while p < len(self.done) and self.done[p]:
+                p += 1
+            if p != self.prefix:
+                self.prefix = p
+                if self.handle is not None:
+                    self.lib.awq_stream_release(self.handle, p)
+
+    def attach(self, handle) -> None:
+        with self.mu:
+            self.handle = handle
+            if self.prefix:
+                self.lib.awq_stream_release(handle, self.prefix)
+
+    def detach(self) -> None:
+        with self.mu:
+            self.handle = None
+
+
+def quantize_stream_native(loader, infos, quantizer, device: str, readers: int, packed: bool, out: Dict,
+                           lock: threading.Lock, logger, keep_on_device: bool = False,
+                           on_done: Optional[Callable[[str, Optional[Dict[str, torch.Tensor]]], None]] = None,
+                           release_hook: Optional[Callable[[Callable[[Sequence[str]], None]], None]] = None,
+                           group_of: Optional[Dict[str, int]] = None, slot_bytes: int = 0,
+                           host_ring_bytes: int = 0, dev_ring_bytes: int = 0, opts: Optional[Dict] = None,
+                           timings: Optional[Dict] = None) -> None:
+    """Quantize `infos` on one GPU through the native pipeline.
+
+    on_done(name, result)   every tensor, in order (None: failed).  Tensors smaller than one
+                            group (awq.py:297-300) take the per-tensor path FIRST, so the
+                            pipeline's items are the only ones still open while it runs;
+    release_hook(fn)        registers fn(names), to be called once results are no longer
+                            read (written); with it the host ring may wrap;
+    group_of[name]          the output group (chunk) of every tensor the hook releases
+                            together — needed to size a wrapping host ring;
+    host_ring_bytes / dev_ring_bytes   ring sizes (0: sized by simulation, see module doc);
+    keep_on_device          results stay in one device arena (no host copy, no ring).
+    """
+    from . import _hip
+    opts = opts or {}
+    t_enter = time.perf_counter()
+    if not (device.startswith("cuda") and torch.cuda.is_available()):
+        quantizer.compute_device()   # raises HipUnavailable: no CPU path
+    dev = torch.device(device)
+    if dev.index is None:
+        dev = torch.device("cuda", torch.cuda.current_device())
+    torch.cuda.set_device(dev)
+    quantizer.compute_device()
+    quantizer._check_mode()
+    gs, bits = quantizer.group_size, quantizer.bits
+    scal = {"bits": torch.tensor(bits, dtype=torch.int32), "group_size": torch.tensor(gs, dtype=torch.int32),
+            "symmetric": torch.tensor(bool(quantizer.symmetric), dtype=torch.bool)}
+
+    def report(name, r):
+        if r is not None:
+            with lock:
+                out[name] = r
+        if on_done:
+            on_done(name, r)
+
+    items = []
+    for info in infos:
+        if info.dtype not in _hip.AWQ_DTYPE:
+            if logger:
+                logger.error(f"Error quantizing tensor: {info.name}, error: Expected floating point tensor, "
+                             f"got {info.dtype}")
+            report(info.name, None)
+        elif info.numel < gs:                  # awq.py:297-300: the per-tensor path, first
+            try:
+                x = loader.read(info)
+                res = quantizer.quantize_model_device({info.name: x}, packed=packed)
+                r = {k: (v.cpu() if isinstance(v, torch.Tensor) and not keep_on_device else v)
+                     for k, v in res.get(info.name, {}).items()} if info.name in res else None
+            except Exception as e:  # noqa: BLE001
+                if logger:
+                    logger.error(f"Error quantizing tensor: {info.name}, error: {e}")
+                r = None
+            report(info.name, r)
+        else:
+            rows = 1 if len(info.shape) <= 1 else info.shape[0]
+            items.append((info, rows, info.numel // rows))
+    lays = [region_layout(info.shape, rows, K, gs, bits, packed) for info, rows, K in items]
+    sizes = [s for _, s in lays]
+    lib = _hip.load_library()
+    n = len(items)
+    arr = (_hip.StreamItem * max(1, n))()
+    for k, (info, rows, K) in enumerate(items):
+        fd, at = loader.data_location(info)
+        it = arr[k]
+        it.fd, it.dtype, it.offset = fd, _hip.AWQ_DTYPE[info.dtype], at
+        it.rows, it.K = rows, K
+        it.qweight = 1          # (planning only looks at shapes; the real pointers follow)
+    total_in = sum(i.nbytes for i, _, _ in items)
+    max_row = max((K * (8 if i.dtype == torch.float64 else 4 if i.dtype == torch.float32 else 2)
+                   for i, _, K in items), default=0)
+    slot = slot_bytes or opts.get("slot_bytes") or min(256 << 20, max(32 << 20, total_in // 8))
+    slot = max(slot, max_row)                  # a row must fit a staging slot
+    slot = -(-slot // 4096) * 4096
+    nslots = int(opts.get("nslots", 3))
+    cand = quantizer.search_candidates
+    cfg = _hip.StreamConfig(bits=bits, symmetric=int(bool(quantizer.symmetric)), group_size=gs,
+                            readers=int(opts.get("readers", min(16, max(8, readers)))), nslots=nslots,
+                            search_grid=quantizer.search_grid if cand else 0, search_candidates=cand,
+                            slot_bytes=slot, first_batch_bytes=max(4096, slot // 4 // 4096 * 4096))
+    first = (ctypes.c_int32 * max(1, n))()
+    last = (ctypes.c_int32 * max(1, n))()
+    nb = lib.awq_stream_plan(arr, n, ctypes.byref(cfg), first, last)
+    if nb < 0:
+        raise RuntimeError(f"awq_stream_plan: {_hip.last_error()}")
+    first, last = list(first)[:n], list(last)[:n]
+    t_plan = time.perf_counter()
+    # ---- output placement ---------------------------------------------------------------
+    if keep_on_device:
+        dcap, doffs, dgates = size_ring(sizes, 1 << 62, lambda g: False)   # one arena, no wrap
+    else:
+        floor = dev_ring_bytes or (opts.get("dev_ring_bytes") or DEV_RING_FLOOR)
+        dcap, doffs, dgates = size_ring(sizes, floor, lambda g: dev_gates_ok(g, first, last))
+    hcap, hoffs, hgates = 0, [], [0] * n
+    releaser = None
+    if not keep_on_device:
+        if release_hook is not None and group_of is not None:
+            grp = [group_of.get(i.name, k) for k, (i, _, _) in enumerate(items)]
+            gend, e = [0] * n, n - 1
+            for k in range(n - 1, -1, -1):       # the last item of every item's group
+                if k < n - 1 and grp[k] != grp[k + 1]:
+                    e = k
+                gend[k] = e
+            floor = host_ring_bytes or (opts.get("host_ring_bytes") or HOST_RING_FLOOR)
+            hcap, hoffs, hgates = size_ring(sizes, floor, lambda g: host_gates_ok(g, last, gend))
+        else:
+            hcap, hoffs, hgates = size_ring(sizes, 1 << 62, lambda g: False)
+        if any(hgates):
+            releaser = _Releaser(lib, [i.name for i, _, _ in items])
+            release_hook(releaser.written)
+    t_place = time.perf_counter()
+    dbuf = torch.empty(dcap, dtype=torch.uint8, device=dev)
+    t_dev = time.perf_counter()
+    hbuf = pinned_bytes(hcap) if not keep_on_device else None
+    t_host = time.perf_counter()
+    dptr = dbuf.data_ptr()
+    hptr = hbuf.data_ptr() if hbuf is not None else 0
+    for k in range(n):
+        fields, size = lays[k]
+        it = arr[k]
+        it.qweight = None
+        for f, _, _, off, _ in fields:
+            setattr(it, _PTR[f], dptr + doffs[k] + off)
+        it.dev_out, it.out_bytes = dptr + doffs[k], fields[-1][3] + fields[-1][4]
+        if hbuf is not None:
+            it.host_out = hptr + hoffs[k]
+        it.dev_gate, it.host_gate = dgates[k], hgates[k]
+    tb = int(lib.awq_stream_table_bytes(slot))     # each slot: its table area, then its input
+    h_stage = pinned_bytes(nslots * (tb + slot))
+    d_stage = torch.empty(nslots * (tb + slot), dtype=torch.uint8, device=dev)
+    compute = torch.cuda.current_stream(dev)
+    h2d = torch.cuda.Stream(dev)
+    d2h = torch.cuda.Stream(dev)
+    cfg.host_staging, cfg.dev_staging = h_stage.data_ptr(), d_stage.data_ptr()
+    cfg.compute_stream, cfg.h2d_stream, cfg.d2h_stream = compute.cuda_stream, h2d.cuda_stream, d2h.cuda_stream
+    trace = None
+    if opts.get("trace"):
+        cap = nb + 2
+        trace = (ctypes.c_double * (cap * _hip.STREAM_TRACE_FIELDS))()
+        cfg.trace, cfg.trace_batches = ctypes.addressof(trace), cap
+    handle = ctypes.c_void_p()
+    t_run = time.perf_counter()
+    _hip.check(lib.awq_stream_start(arr, n, ctypes.byref(cfg), ctypes.byref(handle)), "awq_stream_start")
+    if releaser is not None:
+        releaser.attach(handle)
+    stats = _hip.StreamStats()
+    t_wait = 0.0
+    try:
+        results = []
+        for k, (info, rows, K) in enumerate(items):
+            fields, _ = lays[k]
+            if keep_on_device:
+                r = {f: _view(dbuf, doffs[k] + off, nbytes, dt, shp) for f, shp, dt, off, nbytes in fields}
+            else:
+                r = {f: _view(hbuf, hoffs[k] + off, nbytes, dt, shp) for f, shp, dt, off, nbytes in fields}
+            r.update(scal)
+            if packed:
+                r["shape"] = torch.tensor(list(info.shape), dtype=torch.int64)
+            results.append(r)
+        i0, i1 = ctypes.c_int32(), ctypes.c_int32()
+        for b in range(int(lib.awq_stream_batches(handle))):
+            t0 = time.perf_counter()
+            _hip.check(lib.awq_stream_wait(handle, b, ctypes.byref(i0), ctypes.byref(i1)), "awq_stream_wait")
+            t_wait += time.perf_counter() - t0
+            for k in range(i0.value, i1.value):
+                report(items[k][0].name, results[k])
+                results[k] = None
+    finally:
+        if releaser is not None:
+            releaser.detach()
+        rc = lib.awq_stream_end(handle, ctypes.byref(stats))
+    _hip.check(rc, "awq_stream_end")
+    if keep_on_device:
+        compute.wait_stream(d2h)
+    if timings is not None:
+        st = {"engine": "native", "wall_s": round(time.perf_counter() - t_enter, 4),
+              "setup_s": round(t_run - t_enter, 4), "plan_s": round(t_plan - t_enter, 4),
+              "place_s": round(t_place - t_plan, 4), "alloc_dev_s": round(t_dev - t_place, 4),
+              "alloc_host_out_s": round(t_host - t_dev, 4), "host_ring_MB": hcap >> 20, "dev_ring_MB": dcap >> 20,
+              "host_wraps": int(any(hgates)), "dev_wraps": int(any(dgates)) and not keep_on_device,
+              "batches": int(stats.batches), "pieces": int(stats.pieces), "slot_MB": slot >> 20,
+              "pipeline_s": round(stats.wall_s, 4), "wait_s": round(t_wait, 4),
+              "read_busy_s": round(stats.read_busy_s, 4), "submit_wait_read_s": round(stats.wait_read_s, 4),
+              "submit_wait_slot_s": round(stats.wait_slot_s, 4),
+              "submit_wait_release_s": round(stats.wait_release_s, 4), "bytes_read": int(stats.bytes_read)}
+        if trace is not None:
+            nf = _hip.STREAM_TRACE_FIELDS
+            st["trace"] = [dict(zip(_hip.STREAM_TRACE_NAMES, (round(v, 5) for v in trace[b * nf:(b + 1) * nf])))
+                           for b in range(min(int(stats.batches), cfg.trace_batches))]
+        timings[f"stream_{device}"] = st

@@ -59,6 +59,8 @@ struct Batch {
     int64_t bytes;
     std::vector<Piece> pieces;
     int item_begin, item_end;   // the items whose last piece is in this batch
+    int64_t dev_wait = -1;      // the batch whose D2H the kernels wait for (device ring reuse)
+    int32_t host_gate = 0;      // releases the D2H waits for (host ring reuse)
 };
 
 struct ReadJob {
@@ -80,13 +82,16 @@ struct Pipeline {
     std::mutex mu;
     std::condition_variable cv;
     std::vector<int64_t> reads_left;
+    std::vector<int32_t> first_batch, last_batch;   // per item
     int64_t h2d_recorded = -1, done_recorded = -1;
+    int32_t released = 0;              // awq_stream_release
+    bool abort = false;                // awq_stream_end before the last batch was copied back
     size_t next_job = 0;
     int err = 0;
     std::string err_msg;
     std::vector<std::thread> readers;
     std::thread submitter;
-    double t0 = 0, read_busy = 0, wait_read = 0, wait_slot = 0;
+    double t0 = 0, read_busy = 0, wait_read = 0, wait_slot = 0, wait_release = 0;
     int64_t bytes_read = 0;
 
     void fail(int code, const std::string& msg) {
@@ -147,6 +152,40 @@ int plan(Pipeline& P, std::string& why) {
         }
     }
     if (!cur.pieces.empty() || P.batches.empty() || cur.item_begin < n) close(n);
+    // every item's first / last batch
+    P.first_batch.assign(n, -1);
+    P.last_batch.assign(n, -1);
+    for (size_t b = 0; b < P.batches.size(); ++b) {
+        const Batch& B = P.batches[b];
+        for (const Piece& pc : B.pieces)
+            if (P.first_batch[pc.item] < 0) P.first_batch[pc.item] = (int32_t)b;
+        for (int i = B.item_begin; i < B.item_end; ++i) {
+            P.last_batch[i] = (int32_t)b;
+            if (P.first_batch[i] < 0) P.first_batch[i] = (int32_t)b;
+        }
+    }
+    // ring gates: a batch's kernels wait for the D2H the device ranges they overwrite
+    // needed; its D2H waits for the releases of the host ranges it overwrites
+    for (int i = 0; i < n; ++i) {
+        const awq_stream_item& it = P.items[i];
+        if (it.dev_gate < 0 || it.dev_gate > i || it.host_gate < 0 || it.host_gate > i) {
+            why = "item " + std::to_string(i) + ": a ring gate must name earlier items only";
+            return AWQ_EINVAL;
+        }
+        if (it.dev_gate > 0) {
+            const int32_t dep = P.last_batch[it.dev_gate - 1], at = P.first_batch[i];
+            if (dep >= at) {
+                why = "item " + std::to_string(i) + ": its device outputs overlap those of item " +
+                      std::to_string(it.dev_gate - 1) + ", copied back in batch " + std::to_string(dep) +
+                      ", not before its own kernels (batch " + std::to_string(at) + "): device output ring too small";
+                return AWQ_EINVAL;
+            }
+            Batch& B = P.batches[at];
+            B.dev_wait = std::max<int64_t>(B.dev_wait, dep);
+        }
+        Batch& L = P.batches[P.last_batch[i]];
+        L.host_gate = std::max(L.host_gate, it.host_gate);
+    }
     // reads: every piece in kReadPiece units, batch by batch
     P.reads_left.assign(P.batches.size(), 0);
     for (size_t b = 0; b < P.batches.size(); ++b) {
@@ -262,7 +301,7 @@ bool plan_batch(Pipeline& P, const Batch& B, BatchPlan& bp) {
             const awq_stream_item& it = P.items[pc.item];
             if (it.dtype != dt) continue;
             const awq_tensor_desc d = piece_desc(it, pc, dev_slot + pc.slot_off, c.bits, gs);
-            if (ragged_ok(d, dt, gs)) descs[nd++] = d;
+            if (c.search_candidates == 0 && ragged_ok(d, dt, gs)) descs[nd++] = d;
             else bp.rest.push_back({d, dt});
         }
         if (nd == first) continue;
@@ -309,10 +348,15 @@ bool launch_batch(Pipeline& P, const Batch& B, const BatchPlan& bp, hipStream_t 
     tp = now_s();
     for (const auto& r : bp.rest) {
         const awq_tensor_desc& d = r.first;
-        const int rc = awq_quantize_groups_ex(d.w, r.second, d.rows, d.K, (int32_t)gs, c.bits, c.symmetric, 0,
-                                              d.qweight, d.qzeros, d.scales, d.tensor_q, d.zeros, cs);
+        const int rc = c.search_candidates > 0
+                           ? awq_quantize_search_ex(d.w, r.second, d.rows, d.K, (int32_t)gs, c.bits, c.symmetric, 0,
+                                                    c.search_grid, c.search_candidates, d.qweight, d.qzeros, d.scales,
+                                                    d.tensor_q, d.zeros, cs)
+                           : awq_quantize_groups_ex(d.w, r.second, d.rows, d.K, (int32_t)gs, c.bits, c.symmetric, 0,
+                                                    d.qweight, d.qzeros, d.scales, d.tensor_q, d.zeros, cs);
         if (rc) {
-            P.fail(rc, std::string("awq_quantize_groups_ex: ") + awq_last_error());
+            P.fail(rc, std::string(c.search_candidates > 0 ? "awq_quantize_search_ex: " : "awq_quantize_groups_ex: ") +
+                           awq_last_error());
             return false;
         }
     }
@@ -331,8 +375,13 @@ void submitter_main(Pipeline* P) {
         double t = now_s();
         {
             std::unique_lock<std::mutex> lk(P->mu);
-            P->cv.wait(lk, [&] { return P->err || P->reads_left[b] == 0; });
+            P->cv.wait(lk, [&] { return P->err || P->abort || P->reads_left[b] == 0; });
             if (P->err) return;
+            if (P->abort) {
+                lk.unlock();
+                P->fail(AWQ_EINVAL, "stream cancelled (awq_stream_end before its last batch)");
+                return;
+            }
         }
         P->wait_read += now_s() - t;
         double t_slot = 0;
@@ -366,6 +415,8 @@ void submitter_main(Pipeline* P) {
         }
         P->cv.notify_all();
         if (!P->hip_ok(hipStreamWaitEvent(cs, P->ev_h2d[b], 0), "stream wait")) return;
+        // device output ring: the ranges this batch's kernels overwrite have been copied back
+        if (B.dev_wait >= 0 && !P->hip_ok(hipStreamWaitEvent(cs, P->ev_done[B.dev_wait], 0), "stream wait")) return;
         double ph[2] = {0, 0};
         if (!launch_batch(*P, B, bp, cs, ph)) return;
         if (!P->tr.empty())
@@ -373,6 +424,19 @@ void submitter_main(Pipeline* P) {
         if (!P->hip_ok(hipEventRecord(P->ev_kern[b], cs), "event")) return;
         if (!P->tr.empty()) P->tr[b * AWQ_STREAM_TRACE_FIELDS + 3] = now_s() - P->t0;
         if (!P->hip_ok(hipStreamWaitEvent(d2h, P->ev_kern[b], 0), "stream wait")) return;
+        // host output ring: the caller has released the ranges this batch's D2H overwrites
+        if (B.host_gate > 0) {
+            const double tw = now_s();
+            std::unique_lock<std::mutex> lk(P->mu);
+            P->cv.wait(lk, [&] { return P->err || P->abort || P->released >= B.host_gate; });
+            if (P->err) return;
+            if (P->abort) {
+                lk.unlock();
+                P->fail(AWQ_EINVAL, "stream cancelled (awq_stream_end before its last batch)");
+                return;
+            }
+            P->wait_release += now_s() - tw;
+        }
         // outputs of the items this batch completes (two ranges per item), adjacent ranges as
         // one copy
         struct Run {
@@ -445,6 +509,8 @@ int awq_stream_start(const awq_stream_item* items, int n, const awq_stream_confi
         !c.dev_staging)
         return awq::set_error(AWQ_EINVAL, "bad stream configuration (nslots >= 2, readers >= 1, slot_bytes a "
                                           "multiple of 4096, staging buffers)");
+    if (c.search_candidates < 0 || (c.search_candidates > 0 && (c.search_grid < 1 || c.search_candidates > c.search_grid)))
+        return awq::set_error(AWQ_EINVAL, "bad search configuration (1 <= search_candidates <= search_grid)");
     for (int i = 0; i < n; ++i) {
         const awq_stream_item& it = items[i];
         if (it.dtype < AWQ_DTYPE_BF16 || it.dtype > AWQ_DTYPE_F64 || it.rows < 0 || it.K < 0 || it.fd < 0 ||
@@ -491,6 +557,33 @@ int awq_stream_start(const awq_stream_item* items, int n, const awq_stream_confi
     return AWQ_OK;
 }
 
+int64_t awq_stream_plan(const awq_stream_item* items, int n, const awq_stream_config* cfg, int32_t* first_batch,
+                        int32_t* last_batch) {
+    if (!cfg || n < 0 || (n > 0 && !items)) return -awq::set_error(AWQ_EINVAL, "null argument");
+    if (cfg->nslots < 1 || cfg->slot_bytes <= 0) return -awq::set_error(AWQ_EINVAL, "bad stream configuration");
+    Pipeline P;
+    P.items.assign(items, items + n);
+    P.cfg = *cfg;
+    std::string why;
+    if (int rc = plan(P, why)) return -awq::set_error(rc, why.c_str());
+    for (int i = 0; i < n; ++i) {
+        if (first_batch) first_batch[i] = P.first_batch[i];
+        if (last_batch) last_batch[i] = P.last_batch[i];
+    }
+    return (int64_t)P.batches.size();
+}
+
+int awq_stream_release(void* handle, int32_t items) {
+    Pipeline* P = (Pipeline*)handle;
+    if (!P) return awq::set_error(AWQ_EINVAL, "null handle");
+    {
+        std::lock_guard<std::mutex> g(P->mu);
+        P->released = std::max(P->released, items);
+    }
+    P->cv.notify_all();
+    return AWQ_OK;
+}
+
 int64_t awq_stream_batches(void* handle) {
     return handle ? (int64_t)((Pipeline*)handle)->batches.size() : -1;
 }
@@ -513,6 +606,11 @@ int awq_stream_wait(void* handle, int64_t batch, int32_t* first_item, int32_t* e
 int awq_stream_end(void* handle, awq_stream_stats* stats) {
     Pipeline* P = (Pipeline*)handle;
     if (!P) return awq::set_error(AWQ_EINVAL, "null handle");
+    {   // a caller that stopped early may still read its host ranges: copy nothing more into them
+        std::lock_guard<std::mutex> g(P->mu);
+        P->abort = true;
+    }
+    P->cv.notify_all();
     if (P->submitter.joinable()) P->submitter.join();
     {   // a failed submitter leaves readers waiting for slots: release them
         std::lock_guard<std::mutex> g(P->mu);
@@ -542,6 +640,7 @@ int awq_stream_end(void* handle, awq_stream_stats* stats) {
         stats->read_busy_s = P->read_busy;
         stats->wait_read_s = P->wait_read;
         stats->wait_slot_s = P->wait_slot;
+        stats->wait_release_s = P->wait_release;
     }
     // nothing of the pipeline may still run once the caller's buffers are released
     for (void* s : {P->cfg.h2d_stream, P->cfg.compute_stream, P->cfg.d2h_stream}) (void)hipStreamSynchronize((hipStream_t)s);

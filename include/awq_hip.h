@@ -46,7 +46,7 @@
 extern "C" {
 #endif
 
-#define AWQ_HIP_ABI_VERSION 12
+#define AWQ_HIP_ABI_VERSION 13
 
 /* dtype codes of the input weights (torch dtypes the reference accepts, awq.py:397) */
 enum { AWQ_DTYPE_BF16 = 0, AWQ_DTYPE_F16 = 1, AWQ_DTYPE_F32 = 2, AWQ_DTYPE_F64 = 3 };
@@ -242,7 +242,26 @@ int awq_pack_rows(const int32_t* v, int64_t rows, int64_t n, int bits, int qmin,
  * Caller-owned memory (the library allocates none): staging slots (pinned host + device),
  * per-slot descriptor tables (pinned host + device, awq_stream_table_bytes each), every
  * item's device outputs and, when its results are wanted on the host, a pinned host range
- * of the same size.  The three streams may be any hipStream_t (NULL = legacy default). */
+ * of the same size.  The three streams may be any hipStream_t (NULL = legacy default).
+ *
+ * Bounded output memory (round 4): the caller may place the items' device outputs and host
+ * ranges in two RINGS that later items reuse, with two per-item gates:
+ *   dev_gate  = g > 0: the kernels writing this item's outputs first wait (on the compute
+ *               stream, no host block) for the D2H of items [0, g) — the earlier items whose
+ *               device ranges this item's overlap;
+ *   host_gate = g > 0: the D2H into this item's host range waits until the caller has
+ *               released items [0, g) (awq_stream_release: it no longer reads their host
+ *               results, e.g. once their output files are written).
+ * awq_stream_plan gives the batch of every item's first and last piece before the start,
+ * so the caller can place the rings; awq_stream_start rejects a dev_gate that would wait
+ * for a D2H of the same or a later batch, and a host_gate > the item's index.  A caller
+ * that releases only what the items before a batch let it release must size the host ring
+ * so that a batch's gate never needs that batch's own items (awq_stream_plan).
+ *
+ * scale_method="search" (awq_quantize_search) runs through the pipeline too: config
+ * search_candidates > 0 makes every piece's launch awq_quantize_search_ex with
+ * search_grid / search_candidates (rows are independent, so a row split gives the bits of
+ * the whole-tensor call). */
 #define AWQ_STREAM_MAX_BATCH_ITEMS 4096
 
 typedef struct awq_stream_item {
@@ -261,12 +280,15 @@ typedef struct awq_stream_item {
     void* dev_out2;      /* a second range (e.g. the fp16 scales, kept in a buffer of their */
     void* host_out2;     /* own dtype), NULL: none */
     int64_t out_bytes2;
+    int32_t dev_gate;    /* 0: none; see "Bounded output memory" above */
+    int32_t host_gate;   /* 0: none */
 } awq_stream_item;
 
 typedef struct awq_stream_config {
     int32_t bits, symmetric, group_size, readers;   /* readers: pread threads (>= 1) */
     int32_t nslots;                                 /* >= 2 */
     int32_t trace_batches;                          /* capacity of `trace`, in batches */
+    int32_t search_grid, search_candidates;         /* scale_method="search"; 0 candidates = RTN */
     int64_t slot_bytes;          /* input bytes per staging slot, multiple of 4096 */
     int64_t first_batch_bytes;   /* capacity of the first batch (<= slot_bytes; 0 = slot_bytes) */
     void* host_staging;          /* pinned host, nslots * (awq_stream_table_bytes(slot_bytes) +
@@ -296,15 +318,27 @@ typedef struct awq_stream_stats {
     double read_busy_s;          /* summed over reader threads */
     double wait_read_s;          /* submitter waiting for a batch's reads */
     double wait_slot_s;          /* submitter waiting for a slot's previous kernels */
+    double wait_release_s;       /* submitter waiting for host-ring releases (host_gate) */
 } awq_stream_stats;
 
 /* Per-slot descriptor / tensor-table bytes (descriptors + tensor tables of up to
  * AWQ_STREAM_MAX_BATCH_ITEMS pieces): the head of every staging slot; a multiple of 4096. */
 int64_t awq_stream_table_bytes(int64_t slot_bytes);
 
+/* HOST only: the batches awq_stream_start would plan for these items and this config
+ * (same slot_bytes / first_batch_bytes), without starting anything: first_batch[i] /
+ * last_batch[i] = the batch of item i's first / last piece (an item without elements:
+ * the batch that completes it, both).  Returns the number of batches (< 0: error). */
+int64_t awq_stream_plan(const awq_stream_item* items, int n, const awq_stream_config* cfg, int32_t* first_batch,
+                        int32_t* last_batch);
+
 /* Plan the batches and start the pipeline on its own native threads; returns at once.
  * *handle receives the pipeline (awq_stream_end frees it).  Items are processed in order. */
 int awq_stream_start(const awq_stream_item* items, int n, const awq_stream_config* cfg, void** handle);
+
+/* The caller no longer reads the host results of items [0, items) (monotone: a smaller
+ * count than an earlier call is ignored); wakes a D2H waiting on a host_gate. */
+int awq_stream_release(void* handle, int32_t items);
 
 /* Number of batches of a started pipeline. */
 int64_t awq_stream_batches(void* handle);
@@ -315,7 +349,9 @@ int64_t awq_stream_batches(void* handle);
 int awq_stream_wait(void* handle, int64_t batch, int32_t* first_item, int32_t* end_item);
 
 /* Wait for the whole pipeline, join its threads, release the handle; stats may be NULL.
- * Returns the first error of the pipeline. */
+ * Returns the first error of the pipeline.  Batches not yet copied back when it is called
+ * (the caller stopped early) are cancelled rather than copied into host ranges the caller
+ * may still be reading. */
 int awq_stream_end(void* handle, awq_stream_stats* stats);
 
 /* ---- Activation-aware per-input-channel scale search (scale_method="awq") ----------

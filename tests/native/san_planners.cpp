@@ -65,6 +65,17 @@ int main() {
         c.bits = 4; c.symmetric = 0; c.group_size = 128; c.readers = 3; c.nslots = 3;
         c.slot_bytes = 65536; c.first_batch_bytes = (next() & 1) ? 16384 : 0;
         c.host_staging = host_stage; c.dev_staging = (void*)(uintptr_t)0x5000000;
+        // the dry-run plan, then random ring gates (valid and invalid) for the start's checks
+        std::vector<int32_t> fb((size_t)n + 1), lb((size_t)n + 1);
+        const int64_t nb = awq_stream_plan(it.data(), n, &c, fb.data(), lb.data());
+        ++checks;
+        if (awq_stream_plan(it.data(), n, &c, nullptr, nullptr) != nb) { puts("plan repeat"); return 1; }
+        if (nb > 0)
+            for (int i = 0; i < n; ++i) {
+                if (fb[i] < 0 || lb[i] < fb[i] || lb[i] >= nb) { puts("plan batches"); return 1; }
+                if (i > 0 && next() % 4 == 0) it[i].dev_gate = 1 + (int32_t)(next() % (uint64_t)i);
+                if (next() % 4 == 0) it[i].host_gate = (int32_t)(next() % (uint64_t)(i + 2));
+            }
         void* h = nullptr;
         const int rc = awq_stream_start(it.data(), n, &c, &h);
         if (rc == 0) {   // (a GPU is present after all: run to completion would read fd 0; stop)
@@ -78,6 +89,10 @@ int main() {
     void* h = nullptr;
     if (awq_stream_start(nullptr, 0, &bad, &h) == 0) { puts("bad config accepted"); return 1; }
     if (awq_stream_table_bytes(1 << 28) <= 0) { puts("table bytes"); return 1; }
+    if (awq_stream_release(nullptr, 3) == 0 || awq_stream_plan(nullptr, 2, &bad, nullptr, nullptr) >= 0) {
+        puts("null handle / items accepted");
+        return 1;
+    }
     // ---- tuning + argument validation of the launch entry points (no launch reached) ----
     awq_tuning t;
     memset(&t, 0, sizeof t);

@@ -564,9 +564,8 @@ def test_native_stream_small_slots_split_rows(tmp_path, packed):
     infos = loader.tensor_index()
     q = AWQQuantizer(bits=4, group_size=128, symmetric=False, device="cuda", logger_level="ERROR")
     out, done = {}, []
-    chunk_of = {i.name: k // 5 for k, i in enumerate(infos)}
     quantize_stream_native(loader, infos, q, "cuda:0", 4, packed, out, threading.Lock(), None,
-                           on_done=lambda n, res: done.append(n), chunk_of=chunk_of, slot_bytes=64 << 10)
+                           on_done=lambda n, res: done.append(n), slot_bytes=64 << 10)
     assert sorted(done) == sorted(tensors) == sorted(out)
     for name, x in tensors.items():
         ref = orc.quantize(x, bits=4, group_size=128, symmetric=False)
@@ -618,3 +617,84 @@ def test_cli_llama3_8b_shaped_multifile(tmp_path, fmt):
             assert torch.equal(res["tensor_q"], ref["tensor_q"]), name
             assert torch.equal(res["zero_points"], ref["zero_points"]), name
         assert torch.equal(res["scales"].view(torch.int16), ref["scales"].view(torch.int16)), name
+
+
+def _ring_model():
+    """~70 tensors of mixed sizes (row splits over 64 KiB slots, many-tensor batches)."""
+    g = torch.Generator().manual_seed(11)
+    r = lambda *s, dt=torch.bfloat16: (torch.randn(*s, generator=g) * 0.02).to(dt)
+    t = {"big": r(700, 512), "f16": r(96, 384, dt=torch.float16), "f32": r(40, 256, dt=torch.float32),
+         "padded": r(50, 200), "t3": r(24, 3, 128)}
+    for i in range(30):
+        t[f"mid{i}"] = r(8 + 4 * i, 256)
+    for i in range(36):
+        t[f"tiny{i}"] = r(128 + 64 * (i % 5))
+    return t
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not torch.cuda.is_available(), reason="needs the GPU")
+@pytest.mark.parametrize("fmt", ["packed", "reference"])
+def test_native_stream_bounded_rings_wrap(tmp_path, monkeypatch, fmt):
+    """ADVICE r3 (bounded output memory): 64 KiB staging slots and host / device output
+    rings far smaller than the output, so both wrap — kernels wait on earlier D2H, copies
+    wait on the chunk writer's releases — and every chunk file still holds the oracle's
+    results."""
+    from oracle import awq_oracle as orc
+    from awq_quantizer import main as M
+    tensors = _ring_model()
+    d = _model_dir(tmp_path, tensors, files=3)
+    for k, v in (("slot_bytes", 64 << 10), ("host_ring_bytes", 64 << 10), ("dev_ring_bytes", 64 << 10)):
+        monkeypatch.setitem(M.STREAM_OPTS, k, v)
+    out = tmp_path / "out"
+    assert M.main(["--model_id", d, "--output_dir", str(out), "--log_level", "ERROR", "--chunk_size", "3",
+                   "--output_format", fmt]) == 0
+    st = M.TIMINGS["stream_cuda:0"]
+    assert st["host_wraps"] and st["dev_wraps"], st
+    total = sum(tensors[n].numel() for n in tensors) * (0.6 if fmt == "packed" else 4.2)
+    assert st["host_ring_MB"] * (1 << 20) < total
+    meta = json.load(open(out / "metadata.json"))
+    assert meta["num_tensors"] == len(tensors)
+    for name, ci in meta["tensor_to_chunk"].items():
+        res = _load_chunk(out, ci, False)[name]
+        x = tensors[name]
+        ref = orc.quantize(x, bits=4, group_size=128, symmetric=False)
+        if fmt == "packed":
+            rows = 1 if x.dim() <= 1 else x.shape[0]
+            assert torch.equal(res["qweight"], orc.pack_rows(ref["tensor_q"].reshape(rows, -1), 4, 0)), name
+            assert torch.equal(res["qzeros"], orc.pack_rows(ref["zero_points"], 4, 0)), name
+        else:
+            assert torch.equal(res["tensor_q"], ref["tensor_q"]), name
+            assert torch.equal(res["zero_points"], ref["zero_points"]), name
+        assert torch.equal(res["scales"].view(torch.int16), ref["scales"].view(torch.int16)), name
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not torch.cuda.is_available(), reason="needs the GPU")
+def test_cli_search_native_engine_equals_python_engine(tmp_path):
+    """--scale_method search through the default (native) engine runs the clip
+    search (awq_quantize_search_ex per piece), with the Python engine's exact bits — and
+    not plain RTN."""
+    from awq_quantizer.main import main
+    tensors = _tensors()
+    d = _model_dir(tmp_path, tensors, files=2)
+    got = {}
+    for engine in ("native", "python"):
+        out = tmp_path / engine
+        assert main(["--model_id", d, "--output_dir", str(out), "--log_level", "ERROR", "--scale_method", "search",
+                     "--output_format", "packed", "--stream_engine", engine]) == 0
+        meta = json.load(open(out / "metadata.json"))
+        got[engine] = {n: _load_chunk(out, c, False)[n] for n, c in meta["tensor_to_chunk"].items()}
+    rtn = tmp_path / "rtn"
+    assert main(["--model_id", d, "--output_dir", str(rtn), "--log_level", "ERROR", "--output_format", "packed"]) == 0
+    meta = json.load(open(rtn / "metadata.json"))
+    plain = {n: _load_chunk(rtn, c, False)[n] for n, c in meta["tensor_to_chunk"].items()}
+    assert sorted(got["native"]) == sorted(got["python"]) == sorted(plain)
+    differs = False
+    for n in plain:
+        for f in ("qweight", "qzeros", "scales"):
+            a, b = got["native"][n][f], got["python"][n][f]
+            assert torch.equal(a.view(torch.int16) if f == "scales" else a,
+                               b.view(torch.int16) if f == "scales" else b), (n, f)
+        differs |= not torch.equal(got["native"][n]["scales"].view(torch.int16), plain[n]["scales"].view(torch.int16))
+    assert differs

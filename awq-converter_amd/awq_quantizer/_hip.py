@@ -16,6 +16,9 @@ import torch
 
 LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib")
 LIB_PATH = os.path.join(LIB_DIR, "libawq_hip.so")
+# diagnostics build (`make -C awq-converter_amd/csrc diag`: -DAWQ_DIAG, awq_set_tuning + the A/B
+# kernel variants): loaded only by tuning() below and by scripts/, never by the product path
+DIAG_LIB_PATH = os.path.join(LIB_DIR, "libawq_hip_diag.so")
 ABI_VERSION = 13
 Q_SMALL_TENSOR = 1      # include/awq_hip.h AWQ_Q_SMALL_TENSOR
 
@@ -68,7 +71,7 @@ assert ctypes.sizeof(StreamItem) == 128 and ctypes.sizeof(StreamConfig) == 96
 
 
 class Tuning(ctypes.Structure):
-    """Mirror of awq_tuning (include/awq_hip_tuning.h): diagnostics / A-B controls only."""
+    """Mirror of awq_tuning (csrc/awq_diag.h, diagnostics build): diagnostics / A-B controls only."""
     _fields_ = [("max_blocks", _I32), ("tiles_per_wave", _I32), ("no_rowgroup", _I32), ("rg_waves", _I32),
                 ("rg_gpt", _I32), ("gen_noreg", _I32), ("dq_words_v1", _I32),
                 ("rg_p1", _I32), ("rg_lds_full", _I32)]
@@ -102,7 +105,6 @@ SIGNATURES = {
     "awq_dequantize_packed": (_I32, [_P, _P, _P, _I64, _I64, _I64, _I32, _I32, _P, _P]),
     "awq_pack_rows": (_I32, [_P, _I64, _I64, _I32, _I32, _P, _P]),
     "awq_selftest": (_I32, [_I32, _P, _P]),
-    "awq_set_tuning": (_I32, [ctypes.POINTER(Tuning)]),
     "awq_stream_table_bytes": (_I64, [_I64]),
     "awq_stream_start": (_I32, [ctypes.POINTER(StreamItem), _I32, ctypes.POINTER(StreamConfig),
                                 ctypes.POINTER(ctypes.c_void_p)]),
@@ -262,18 +264,50 @@ def plan_ragged(descs, bits: int, group_size: int = 128) -> int:
     return total
 
 
+_diag = None
+
+
+def load_diag_library(path: str = DIAG_LIB_PATH):
+    """The diagnostics build, bound like load_library() plus awq_set_tuning."""
+    global _diag
+    with _lock:
+        if _diag is None:
+            if not os.path.exists(path):
+                raise HipUnavailable(f"{path} is missing — build it with `make -C awq-converter_amd/csrc diag`")
+            lib = ctypes.CDLL(path)
+            for name, (res, args) in SIGNATURES.items():
+                fn = getattr(lib, name)
+                fn.restype, fn.argtypes = res, args
+            lib.awq_set_tuning.restype = _I32
+            lib.awq_set_tuning.argtypes = [ctypes.POINTER(Tuning)]
+            if lib.awq_abi_version() != ABI_VERSION:
+                raise HipUnavailable(f"libawq_hip_diag.so ABI {lib.awq_abi_version()} != {ABI_VERSION}")
+            _diag = lib
+        return _diag
+
+
 @contextlib.contextmanager
 def tuning(**kw):
-    """Diagnostics / A-B only (include/awq_hip_tuning.h): launches from this thread inside the
-    block use the given overrides (max_blocks, tiles_per_wave, no_rowgroup, rg_waves, rg_gpt,
-    gen_noreg); same results, other speed.  Restores the defaults on exit."""
-    lib = load_library()
+    """Diagnostics / A-B only (awq-converter_amd/csrc/awq_diag.h): inside the block every entry
+    point of this module calls the DIAGNOSTICS build (the shipped libawq_hip.so has no tuning
+    and no variant kernels) with the given overrides for this thread (max_blocks,
+    tiles_per_wave, no_rowgroup, rg_waves, rg_gpt, gen_noreg, dq_words_v1, rg_p1,
+    rg_lds_full); same results, other speed.  Restores the product library on exit."""
+    global _lib
+    diag = load_diag_library()
+    prev = load_library()
     t = Tuning(**{k: int(v) for k, v in kw.items()})
-    check(lib.awq_set_tuning(ctypes.byref(t)), "awq_set_tuning")
+    if diag.awq_set_tuning(ctypes.byref(t)) != 0:
+        raise RuntimeError(f"awq_set_tuning failed: {(diag.awq_last_error() or b'').decode()}")
+    with _lock:
+        _lib = diag
     try:
-        yield
+        yield diag
     finally:
-        lib.awq_set_tuning(None)
+        diag.awq_set_tuning(None)
+        with _lock:
+            _lib = prev
+
 
 
 def _upload(host: torch.Tensor, device: torch.device) -> torch.Tensor:

@@ -548,9 +548,8 @@ def _batches(infos: List[TensorInfo], budget: int) -> List[List[TensorInfo]]:
 def _batch_budget(total: int, batch_bytes: int) -> int:
     """Input bytes per batch: small enough that a small model still pipelines (read / H2D /
     kernel / D2H of neighbouring batches overlap) — about 8 batches per device, 32 MiB ..
-    batch_bytes each; AWQ_CLI_BATCH_MB overrides."""
-    forced = int(os.environ.get("AWQ_CLI_BATCH_MB", "0")) << 20
-    return forced or max(32 << 20, min(batch_bytes, total // 8))
+    batch_bytes each."""
+    return max(32 << 20, min(batch_bytes, total // 8))
 
 
 def _pinned_copy(t: torch.Tensor) -> torch.Tensor:
@@ -638,12 +637,11 @@ def quantize_stream_python(loader, infos: List[TensorInfo], quantizer: AWQQuanti
     clock = time.perf_counter
     t_read = t_submit = t_finish = 0.0
 
-    direct = hasattr(loader, "read_pinned") and os.environ.get("AWQ_CLI_MMAP_READ", "0") != "1"
+    direct = hasattr(loader, "read_pinned")
 
     def read(info, dst=None):
         # straight from the file into pinned memory (one copy) — into the batch's staging
-        # buffer when one is given; AWQ_CLI_MMAP_READ=1: the safetensors mmap read + a pinned
-        # copy (two)
+        # buffer when one is given (a loader without direct reads: its read + a pinned copy)
         if dst is not None:
             return loader.read_into(info, dst)
         return loader.read_pinned(info) if direct else _pinned_copy(loader.read(info))
@@ -814,12 +812,7 @@ def _device_worker(*args, **kwargs) -> None:
     logged; its tensors then count as not quantized."""
     logger, device = args[9], args[3]
     try:
-        prof_path = os.environ.get("AWQ_CLI_PROFILE")   # diagnostics: cProfile of this thread
-        if prof_path:
-            import cProfile
-            cProfile.runctx("quantize_stream(*args, **kwargs)", globals(), locals(), prof_path)
-        else:
-            quantize_stream(*args, **kwargs)
+        quantize_stream(*args, **kwargs)
     except Exception as e:  # noqa: BLE001
         if logger:
             logger.error(f"Quantization on {device} failed: {e}")

@@ -16,7 +16,9 @@
 namespace {
 
 thread_local std::string g_err;
-thread_local awq_tuning g_tuning{};   // include/awq_hip_tuning.h (diagnostics only)
+#ifdef AWQ_DIAG
+thread_local awq_tuning g_tuning{};   // awq_diag.h (diagnostics build only)
+#endif
 
 int fail(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
 int fail(int code, const char* fmt, ...) {
@@ -59,7 +61,7 @@ bool fast_eligible(int dtype, int64_t rows, int64_t K, int64_t group_size) {
 // the row-segment kernel (any group size <= 512, bf16 / fp16 / fp32): 16-B aligned input,
 // dword-aligned outputs, segment offsets within int range
 bool rowgroup_shape(int dtype, int64_t rows, int64_t K, int64_t group_size) {
-    if (g_tuning.no_rowgroup) return false;   // A/B against the generic kernel (scripts/generic_bench.py)
+    if (awq::tuning().no_rowgroup) return false;   // diagnostics A/B against the generic kernel
     const int gpt = awq::rowgroup_gpt(dtype, K, group_size);
     if (gpt == 0 || rows <= 0 || rows * K >= ((int64_t)1 << 40)) return false;
     const int64_t tiles = rows * (((K + group_size - 1) / group_size + gpt - 1) / gpt);
@@ -75,12 +77,15 @@ bool rowgroup_ok(int dtype, int64_t rows, int64_t K, int64_t group_size, const v
 
 }  // namespace
 
+#ifdef AWQ_DIAG
 namespace awq {
 const awq_tuning& tuning() { return g_tuning; }
 }  // namespace awq
+#endif
 
 extern "C" {
 
+#ifdef AWQ_DIAG
 int awq_set_tuning(const awq_tuning* t) {
     g_err.clear();
     if (!t) {
@@ -93,6 +98,7 @@ int awq_set_tuning(const awq_tuning* t) {
     g_tuning = *t;
     return AWQ_OK;
 }
+#endif
 
 int awq_packs_directly(int dtype, int64_t rows, int64_t K, int64_t group_size) {
     // every kernel writes qweight / qzeros directly since the generic kernel's span rewrite

@@ -1,14 +1,15 @@
 /*
- * awq_hip_tuning.h — diagnostics / A-B measurement controls of libawq_hip.so.
+ * awq_diag.h — diagnostics / A-B measurement controls, compiled ONLY into the diagnostics
+ * build libawq_hip_diag.so (`make -C awq-converter_amd/csrc diag`, -DAWQ_DIAG), which
+ * scripts/ and the variant tests load explicitly.  The shipped libawq_hip.so has one path
+ * per shape: no awq_set_tuning symbol, none of the A/B kernel variants, the measured
+ * defaults below compiled in.
  *
- * NOT part of the drop-in contract (include/awq_hip.h): a caller that never calls
- * awq_set_tuning gets the library's measured defaults, and nothing else (no environment
- * variable, no file) changes which kernel or grid produces a result.  Every setting here
- * gives the same bits as the default (the GPU tests check that); only speed differs.
- * Thread-local: it applies to launches made from the calling thread.
+ * Every setting gives the same bits as the default (the GPU tests check that); only speed
+ * differs.  Thread-local: it applies to launches made from the calling thread.
  */
-#ifndef AWQ_HIP_TUNING_H
-#define AWQ_HIP_TUNING_H
+#ifndef AWQ_DIAG_H
+#define AWQ_DIAG_H
 
 #include <stdint.h>
 
@@ -36,10 +37,12 @@ typedef struct awq_tuning {
                                 x group size, K)), 1 to its groups x group size (round-2 sizing, A/B) */
 } awq_tuning;
 
+#ifdef AWQ_DIAG
 /* Set (t != NULL) or reset to the defaults (t == NULL) this thread's tuning. */
 int awq_set_tuning(const awq_tuning* t);
+#endif
 
 #ifdef __cplusplus
 }
 #endif
-#endif /* AWQ_HIP_TUNING_H */
+#endif /* AWQ_DIAG_H */

@@ -268,28 +268,6 @@ __device__ __forceinline__ void compute_tile(const TileCtx& c, const Chunk<F::NW
     const int grp = lane / L;            // group of this lane inside each load
     const int ch = lane % L;             // 16-B chunk of the group
     const uint32_t ng = c.ng;
-#ifdef AWQ_TRIVIAL_COMPUTE
-    // timing-only build (scripts/kbench.py): same loads and stores, no arithmetic
-    if (c.qweight) {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const uint32_t word = v[j].w[0].x ^ v[j].w[0].y ^ v[j].w[0].z ^ v[j].w[F::NW - 1].w;
-            __amdgpu_buffer_rsrc_t rq = rsrc(c.qweight + c.qw_off, c.qw_n * 4u);
-            __builtin_amdgcn_raw_buffer_store_b32(word, rq, (uint32_t)((64 * j + lane) * 4), 0, AWQ_STORE_AUX);
-        }
-    }
-#ifndef AWQ_TRIVIAL_NOSMALL
-    if (ch < 4 && c.scales) {
-        __amdgpu_buffer_rsrc_t rs = rsrc(c.scales + c.start, ng * 2u);
-        __builtin_amdgcn_raw_buffer_store_b16((uint16_t)v[0].w[0].x, rs, (GPJ * ch + grp) * 2u, 0, AWQ_SMALL_AUX);
-    }
-    if (c.qzeros && (uint32_t)lane < c.nw) {
-        __amdgpu_buffer_rsrc_t rz = rsrc(c.qzeros + c.w0, c.nw * 4u);
-        __builtin_amdgcn_raw_buffer_store_b32(v[1].w[0].y, rz, (uint32_t)lane * 4u, 0, AWQ_SMALL_AUX);
-    }
-#endif
-    return;
-#endif
 
     // ---- 1. group min/max (awq.py:192-193) of the 4 groups this lane's group-lanes hold,
     //         from the raw 16-bit patterns: the SIGNED int16 max is the float max whenever
@@ -363,18 +341,10 @@ __device__ __forceinline__ void compute_tile(const TileCtx& c, const Chunk<F::NW
         }
         // this lane's 8 elements are tile elements 512 j + 8 lane: packed word 64 j + lane
         if (c.qweight) {
-#if AWQ_WIDE_STORE
             // staged in the wave's LDS block in output order (the lanes of one j write 64
             // consecutive words), stored below as one 16-B piece per lane
             if (BITS == 4) qstage[64 * j + lane] = word.x;
             else *(u2v*)(qstage + 128 * j + 2 * lane) = word;
-#else
-            __amdgpu_buffer_rsrc_t rq = rsrc(c.qweight + c.qw_off, c.qw_n * 4u);
-            if (BITS == 4)
-                __builtin_amdgcn_raw_buffer_store_b32(word.x, rq, (uint32_t)((64 * j + lane) * 4), 0, AWQ_STORE_AUX);
-            else
-                __builtin_amdgcn_raw_buffer_store_b64(word, rq, (uint32_t)((64 * j + lane) * 8), 0, AWQ_STORE_AUX);
-#endif
         }
         if (c.tensor_q) {   // reference-layout int32 tensor_q (parity mode)
             int32_t q[8];
@@ -396,7 +366,6 @@ __device__ __forceinline__ void compute_tile(const TileCtx& c, const Chunk<F::NW
             __builtin_amdgcn_raw_buffer_store_b128(hi, rt, (uint32_t)((512 * j + 8 * lane) * 4 + 16), 0, AWQ_STORE_AUX);
         }
     }
-#if AWQ_WIDE_STORE
     if (c.qweight) {   // 4-bit: 1 KiB per tile = one dwordx4 per lane; 8-bit: 2 KiB, two
         __amdgpu_buffer_rsrc_t rq = rsrc(c.qweight + c.qw_off, c.qw_n * 4u);
 #pragma unroll
@@ -405,7 +374,6 @@ __device__ __forceinline__ void compute_tile(const TileCtx& c, const Chunk<F::NW
             __builtin_amdgcn_raw_buffer_store_b128(w4, rq, (uint32_t)(h * 1024 + lane * 16), 0, AWQ_STORE_AUX);
         }
     }
-#endif
     // ---- 5. per-group scalars out (after the data registers are dead): lanes ch < 4 hold
     //         the S slots (one store each) ----
     if (ch < 4) {
@@ -471,17 +439,6 @@ __device__ __forceinline__ void compute_tile(const TileCtx& c, const Chunk<F::NW
 
 }
 
-// Bijective block renumbering for XCD runs (AWQ_XCD_RUN): block b, dealt to XCD b % 8,
-// takes the (b / 8) % R-th block of XCD b % 8's run inside super-chunk b / (8 R); blocks of
-// the last, partial super-chunk keep their index.
-__device__ __forceinline__ int64_t xcd_run_block(int64_t b, int64_t nblocks) {
-    constexpr int64_t R = AWQ_XCD_RUN > 0 ? AWQ_XCD_RUN : 1, X = 8;   // (only called when AWQ_XCD_RUN > 0)
-    const int64_t full = nblocks / (X * R) * (X * R);
-    if (b >= full) return b;
-    const int64_t x = b % X, i = b / X;
-    return (i / R) * (X * R) + x * R + (i % R);
-}
-
 // Index of the tensor owning tile t, searching descs[base..n) (tile_begin ascending,
 // descs[base].tile_begin <= t).  64 lanes probe 64 evenly spaced descriptors per round
 // and a ballot narrows the range: one dependent load per round, 1 round for <= 64
@@ -507,7 +464,7 @@ __device__ uint64_t* g_trace = nullptr;
 #endif
 
 // One wave per tile.  The grid normally covers every tile once (launch_fast); a smaller
-// grid (awq_hip_tuning.h max_blocks, tests) makes each wave walk tiles t, t + nwaves, ... with a
+// grid (awq_diag.h max_blocks, tests) makes each wave walk tiles t, t + nwaves, ... with a
 // tensor cursor.
 template <typename F, int BITS, bool SYM, bool SEARCH, int GS, bool PAD>
 __global__ __launch_bounds__(64 * kWavesPerBlock, SEARCH ? 4 : (F::kWide ? AWQ_MIN_WAVES_WIDE : AWQ_MIN_WAVES))
@@ -518,23 +475,15 @@ void awq_fast_kernel(
     const int32_t* __restrict__ block_tensor, const awq_tensor_desc* __restrict__ descs, int64_t total_tiles,
     int n, int n_grid, int n_cand, uint32_t nan_code, awq_tensor_desc single) {
     __shared__ uint32_t zwords[kWavesPerBlock][kTileElems / GS];
-#if AWQ_WIDE_STORE
     __shared__ __attribute__((aligned(16))) uint32_t qstage_all[kWavesPerBlock][BITS == 4 ? 256 : 512];
-#endif
     // wave index made provably uniform so tile/tensor bookkeeping and the buffer
     // descriptors live in SGPRs (no waterfall loops around the descriptors)
     const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int64_t nwaves = (int64_t)gridDim.x * kWavesPerBlock;
-    int64_t blk = blockIdx.x;
-    if (AWQ_XCD_RUN > 0 && nwaves >= total_tiles) blk = xcd_run_block(blk, gridDim.x);   // one-shot grid only
-    const int64_t wave = blk * kWavesPerBlock + wid;
+    const int64_t wave = (int64_t)blockIdx.x * kWavesPerBlock + wid;
     if (wave >= total_tiles) return;
     uint32_t* zw = zwords[wid];
-#if AWQ_WIDE_STORE
     uint32_t* qs = qstage_all[wid];
-#else
-    uint32_t* qs = nullptr;
-#endif
 #ifdef AWQ_TRACE
     // timing-only build: per wave (start, first tile's loads issued, landed, end) in
     // s_memrealtime ticks (100 MHz, chip-wide clock) -> scripts/trace_waves.py
@@ -640,7 +589,7 @@ hipError_t launch_fast(const awq_tensor_desc* descs_dev, const int32_t* block_te
                        int symmetric, int group_size, bool padded, hipStream_t stream, uint32_t nan_code, int n_grid,
                        int n_cand) {
     if (total_tiles <= 0) return hipSuccess;
-    // one wave per tile (diagnostics, include/awq_hip_tuning.h: tiles_per_wave, max_blocks =
+    // one wave per tile (diagnostics, csrc/awq_diag.h, diagnostics build: tiles_per_wave, max_blocks =
     // grid cap; either makes waves walk several tiles)
     int64_t tpw = 1, max_blocks = INT32_MAX;
     if (tuning().tiles_per_wave > 1) tpw = tuning().tiles_per_wave;

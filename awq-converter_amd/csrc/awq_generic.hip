@@ -496,6 +496,7 @@ __global__ __launch_bounds__(256) void awq_dequant_kernel(
 // at most 19 significand bits, so the f32 product is exact and one hardware RNE conversion
 // to fp16 gives RN_f16(h * s) bit for bit (NaN lanes take the software conversion, which
 // keeps the payload as torch does).  Memory-bound: 0.5 B (4-bit) read + 4 B written per element.
+#ifdef AWQ_DIAG   // round-2/3 dequantize variants: A/B builds only (scripts/, make diag)
 template <int BITS>
 __global__ __launch_bounds__(256) void awq_dequant_words_kernel(
     const int32_t* __restrict__ qweight, const uint16_t* __restrict__ scales, const int32_t* __restrict__ qzeros,
@@ -666,6 +667,8 @@ __global__ __launch_bounds__(256) void awq_dequant_quads_kernel(
     __builtin_nontemporal_store((f4){v[0], v[1], v[2], v[3]}, (f4*)(out + 4 * t));
 }
 
+#endif  // AWQ_DIAG
+
 // Batched four-output lanes: each thread converts U quads (4 outputs, one 16-B store each) of
 // its block's 256 * U consecutive quads, with every load of the U quads (qweight word, scale,
 // qzeros word) issued before the first conversion — U independent loads in flight per lane
@@ -743,15 +746,17 @@ __global__ __launch_bounds__(256) void awq_dequant_batch_kernel(
     }
 }
 
+template <int B> constexpr auto dq_batch4_run = awq_dequant_batch_kernel<B, 4, 4>;
+constexpr int kDqDefault = 8;   // batched lanes in XCD runs: profiles/round3/dequant (DESIGN.md §5.3)
+#ifdef AWQ_DIAG
 template <int B> constexpr auto dq_v2_remap = awq_dequant_words_v2_kernel<B, true>;
 template <int B> constexpr auto dq_v2_plain = awq_dequant_words_v2_kernel<B, false>;
 template <int B> constexpr auto dq_quads_plain = awq_dequant_quads_kernel<B, false>;
 template <int B> constexpr auto dq_quads_remap = awq_dequant_quads_kernel<B, true>;
 template <int B> constexpr auto dq_batch4 = awq_dequant_batch_kernel<B, 4, 0>;
 template <int B> constexpr auto dq_batch8 = awq_dequant_batch_kernel<B, 8, 0>;
-template <int B> constexpr auto dq_batch4_run = awq_dequant_batch_kernel<B, 4, 4>;
 template <int B> constexpr auto dq_batch8_run = awq_dequant_batch_kernel<B, 8, 2>;
-constexpr int kDqDefault = 8;   // batched lanes in XCD runs: profiles/round3/dequant (DESIGN.md §5.3)
+#endif
 
 inline unsigned grid_for(int64_t work, int64_t per_block, int64_t cap) {
     int64_t b = (work + per_block - 1) / per_block;
@@ -772,12 +777,13 @@ hipError_t launch_generic(const void* w, int dtype, int64_t rows, int64_t K, int
     const int64_t G = (K + L - 1) / L;
     const unsigned grid = grid_for(rows * ((G + per - 1) / per), 4, 256 * 16);
     const bool search = n_cand > 0;
-    // fp64 spans (A/B, tuning gen_noreg): 0 = the LDS span wherever the span fits 16 KiB
-    // (3.2-3.7 TB/s of input at gs 64 / 128, against the register span's 1.4-2.4:
-    // profiles/round3/r3n), 1 = the strided span only, 2 = the register span at gs 64 / 128
+    // fp64 spans: the LDS span wherever the span fits 16 KiB (3.2-3.7 TB/s of input at gs 64 /
+    // 128, against the register span's 1.4-2.4: profiles/round3/r3n), else the strided span.
+    // Diagnostics builds (AWQ_DIAG, tuning gen_noreg): 1 = the strided span only, 2 = the
+    // register span at gs 64 / 128
+#ifdef AWQ_DIAG
     const int f64_span = tuning().gen_noreg;
-    const bool noreg = f64_span != 2;
-    if (dtype == AWQ_DTYPE_F64 && !search && !s_exact && !z_exact && (L == 64 || L == 128) && !noreg) {
+    if (dtype == AWQ_DTYPE_F64 && !search && !s_exact && !z_exact && (L == 64 || L == 128) && f64_span == 2) {
         const unsigned blocks = (unsigned)((rows * ((G + per - 1) / per) + 3) / 4);
         const double* wd = (const double*)w;
 #define AWQ_SPAN_REG(LPI, PER)                                                                              \
@@ -792,6 +798,9 @@ hipError_t launch_generic(const void* w, int dtype, int64_t rows, int64_t K, int
 #undef AWQ_SPAN_REG
         return hipPeekAtLastError();
     }
+#else
+    constexpr int f64_span = 0;
+#endif
     if (dtype == AWQ_DTYPE_F64 && !search && !s_exact && !z_exact && L >= 2 && per * L * 8 <= 16384 &&
         f64_span != 1) {
         const int64_t SP = (G + per - 1) / per;
@@ -879,12 +888,15 @@ hipError_t launch_dequant(const int32_t* tensor_q, const int32_t* qweight, const
         const int64_t words = total / per;
         const uint32_t wpr = (uint32_t)(K / per), zpr = (uint32_t)((G + per - 1) / per);
         const dim3 grid((unsigned)((words + 255) / 256)), block(256);
-        // kernel choice (awq_hip_tuning.h dq_words_v1, A/B only): 1 round-2 word kernel, 2 / 3
-        // LDS-staged v2 with / without XCD-contiguous blocks, 4 / 5 four-output lanes without /
-        // with XCD-contiguous blocks, 6 / 7 batched lanes (4 / 8 quads), 8 / 9 the same with
-        // XCD runs of 4 / 2 blocks; 0 = the default
-        int v = tuning().dq_words_v1;
-        if (v <= 0 || v > 9) v = kDqDefault;
+        // the batched four-output lanes in XCD runs (kDqDefault = 8).  Diagnostics builds
+        // (AWQ_DIAG, awq_diag.h dq_words_v1) also reach the A/B variants: 1 round-2 word
+        // kernel, 2 / 3 LDS-staged v2 with / without XCD-contiguous blocks, 4 / 5 four-output
+        // lanes without / with XCD-contiguous blocks, 6 / 7 batched lanes (4 / 8 quads), 9 the
+        // batched lanes in XCD runs of 2 blocks
+        int v = kDqDefault;
+#ifdef AWQ_DIAG
+        if (tuning().dq_words_v1 > 0 && tuning().dq_words_v1 <= 9) v = tuning().dq_words_v1;
+#endif
 #define AWQ_DQ(KER, GRID)                                                                                   \
         do {                                                                                                \
             if (bits == 4)                                                                                  \
@@ -898,15 +910,17 @@ hipError_t launch_dequant(const int32_t* tensor_q, const int32_t* qweight, const
         const dim3 grid_b4((unsigned)((words * (per / 4) + 1023) / 1024)),
             grid_b8((unsigned)((words * (per / 4) + 2047) / 2048));
         switch (v) {
+#ifdef AWQ_DIAG
         case 6: AWQ_DQ(dq_batch4, grid_b4); break;
         case 7: AWQ_DQ(dq_batch8, grid_b8); break;
-        case 8: AWQ_DQ(dq_batch4_run, grid_b4); break;
         case 9: AWQ_DQ(dq_batch8_run, grid_b8); break;
         case 1: AWQ_DQ(awq_dequant_words_kernel, grid); break;
         case 2: AWQ_DQ(dq_v2_remap, grid); break;
         case 3: AWQ_DQ(dq_v2_plain, grid); break;
         case 4: AWQ_DQ(dq_quads_plain, grid_q); break;
-        default: AWQ_DQ(dq_quads_remap, grid_q); break;
+        case 5: AWQ_DQ(dq_quads_remap, grid_q); break;
+#endif
+        default: AWQ_DQ(dq_batch4_run, grid_b4); break;
         }
 #undef AWQ_DQ
         return hipPeekAtLastError();

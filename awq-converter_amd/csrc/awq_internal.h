@@ -5,7 +5,7 @@
 #include <stdint.h>
 
 #include "../../include/awq_hip.h"
-#include "../../include/awq_hip_tuning.h"
+#include "awq_diag.h"
 
 namespace awq {
 
@@ -173,8 +173,16 @@ __host__ __device__ inline uint32_t dq_nan_bits(uint16_t h, int64_t i, int64_t n
     return ((uint32_t)(h & 0x8000u) << 16) | 0x7F800000u | ((uint32_t)(h & 0x3FFu) << 13);
 }
 
-// the calling thread's diagnostics overrides (include/awq_hip_tuning.h; all zero = defaults)
-const awq_tuning& tuning();
+// the calling thread's diagnostics overrides (csrc/awq_diag.h, diagnostics build; all zero = defaults)
+#ifdef AWQ_DIAG
+const awq_tuning& tuning();   // awq_capi.hip: this thread's awq_set_tuning overrides
+#else
+// the product build: the measured defaults, compile-time constant (every override folds away)
+inline const awq_tuning& tuning() {
+    static constexpr awq_tuning kDefaults{};
+    return kDefaults;
+}
+#endif
 
 // launchers (awq_fast.hip / awq_generic.hip).  nan_code: nan_scale_code() of the call.
 hipError_t launch_fast(const awq_tensor_desc* descs_dev, const int32_t* block_tensor,

@@ -10,45 +10,17 @@
 
 #include "awq_internal.h"
 
-// Build-time knobs (scripts/kbench.py compares variants; defaults measured best).
-// cache-policy bits of the input loads and the qweight / tensor_q stores (gfx950: 2 = nt)
-#ifndef AWQ_LOAD_AUX
+// Cache-policy bits of the input loads and the qweight / tensor_q stores (gfx950: 2 = nt).
 #define AWQ_LOAD_AUX 2
-#endif
-#ifndef AWQ_STORE_AUX
 #define AWQ_STORE_AUX 2
-#endif
-// cache policy of the small per-tile stores (scales, zeros, qzeros: 8-32 B per tile).
+// Cache policy of the small per-tile stores (scales, zeros, qzeros: 8-32 B per tile).
 // Default policy (0), not nt: the L2 then merges the partial lines neighbouring tiles
 // write (measured +2-5 % over nt, profiles/r19-r20)
-#ifndef AWQ_SMALL_AUX
 #define AWQ_SMALL_AUX 0
-#endif
 // __launch_bounds__ minimum waves per SIMD (8 = 32 waves per CU: <= 64 VGPRs, <= 80 SGPRs)
-#ifndef AWQ_MIN_WAVES
 #define AWQ_MIN_WAVES 8
-#endif
 // same for fp32 inputs (32 data VGPRs per lane instead of 16)
-#ifndef AWQ_MIN_WAVES_WIDE
 #define AWQ_MIN_WAVES_WIDE 6
-#endif
-// qweight stores: 1 = staged through LDS into one 16-B store per lane (4-bit: 1 store
-// instruction per tile instead of 4), 0 = one dword per lane per group row
-#ifndef AWQ_WIDE_STORE
-#define AWQ_WIDE_STORE 1
-#endif
-
-#ifndef AWQ_F16_PLAIN
-#define AWQ_F16_PLAIN 1
-#endif
-// XCD runs: consecutive workgroups are dealt round-robin over the 8 XCDs (each with its
-// own L2), so with one-wave workgroups neighbouring tiles — which share the 128-B lines of
-// the scales (32 B per tile) and qzeros (8 B per tile) outputs — would write those lines
-// partially from different L2s.  Remapping block b so every XCD takes runs of
-// AWQ_XCD_RUN consecutive blocks keeps each line's writers on one L2 (0 = no remap)
-#ifndef AWQ_XCD_RUN
-#define AWQ_XCD_RUN 0
-#endif
 
 namespace awq {
 namespace {
@@ -246,7 +218,7 @@ struct FmtF16 {
     // weight group: 4-bit s = range/15) takes one multiply per element instead of the
     // Markstein quotient.  The barrier keeps the product rounded to f32 first (a fused
     // v_mad_mixlo_f16 would round once).
-    static constexpr bool kHasPlain = AWQ_F16_PLAIN;   // tuning builds: -DAWQ_F16_PLAIN=0
+    static constexpr bool kHasPlain = true;
     __device__ static bool plain_ok(float s) { return s < 14.0f; }
     __device__ static float quot_plain(float x, float r) { return rn(opaque(x * r)); }
     __device__ static float elem(const Chunk<1>& c, int i) {

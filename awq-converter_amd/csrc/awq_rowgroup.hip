@@ -118,14 +118,12 @@ __device__ __forceinline__ void rg_reduce(int& smax, uint32_t& umax, uint32_t& u
     }
 }
 
-#ifndef AWQ_RG_UNROLL
 #define AWQ_RG_UNROLL 8
-#endif
 
 // raw-bits (signed max, unsigned max, unsigned min) of the 16-bit stage slots [s_lo, s_hi),
 // s_hi > s_lo, from the identities: packed 16-bit max/min over whole dwords (two chains); an
 // edge dword holding one foreign element gets a copy of its own element there
-__device__ __forceinline__ void rg_range16(const uint32_t* st32, int s_lo, int s_hi, int& smax, uint32_t& umax,
+[[maybe_unused]] __device__ __forceinline__ void rg_range16(const uint32_t* st32, int s_lo, int s_hi, int& smax, uint32_t& umax,
                                            uint32_t& umin) {
     const int d_lo = s_lo >> 1, d_hi = (s_hi + 1) >> 1;
     s2 sm = {(short)-32768, (short)-32768}, sm_b = sm;
@@ -641,7 +639,7 @@ __global__ __launch_bounds__(128) void awq_rowgroup_kernel(const void* __restric
 // per-row cost fitted to measurements (profiles/round2/r2_rowgroup/r2r_*: 14336 x 4096,
 // group sizes 48 / 100, GPT 8..32): tiles x (fixed wave cost 8 + 0.6 per element of a
 // lane's pass-1 chunk C = L / (64 / GPT) + 2.3 per 512-element pass-2 sweep).  gpt = 0 if
-// the shape does not fit the LDS stage.  rg_gpt / rg_waves override (awq_hip_tuning.h).
+// the shape does not fit the LDS stage.  rg_gpt / rg_waves override (awq_diag.h).
 struct RgPlan {
     int gpt, waves;
 };
@@ -712,12 +710,21 @@ hipError_t launch_rowgroup(const void* w, int dtype, int64_t rows, int64_t K, in
                        gpt, (uint32_t)tpr, G, C, 1.0f / (float)L, qweight, qzeros, scales, tensor_q, zeros, nan_code, \
                        lgP_last, C_last)
     // (the pass-1 A/B variant is built for the packed outputs only; with tensor_q it takes the default)
+#ifdef AWQ_DIAG
 #define AWQ_RG_SPLIT(Fm, B, S, SP)                                                                                 \
     do {                                                                                                           \
         if (tensor_q) AWQ_RG_GO(Fm, B, S, SP, false, true);                                                         \
         else if (p1c) AWQ_RG_GO(Fm, B, S, SP, true, false);                                                         \
         else AWQ_RG_GO(Fm, B, S, SP, false, false);                                                                 \
     } while (0)
+#else
+#define AWQ_RG_SPLIT(Fm, B, S, SP)                                                                                 \
+    do {                                                                                                           \
+        (void)p1c;                                                                                                  \
+        if (tensor_q) AWQ_RG_GO(Fm, B, S, SP, false, true);                                                         \
+        else AWQ_RG_GO(Fm, B, S, SP, false, false);                                                                 \
+    } while (0)
+#endif
 #define AWQ_RG(Fm, B, S)                                                                                           \
     if (L % 8 == 0) AWQ_RG_SPLIT(Fm, B, S, 8);                                                                      \
     else if (L % 4 == 0) AWQ_RG_SPLIT(Fm, B, S, 4);                                                                 \

@@ -146,13 +146,17 @@ def main():
                 evict(model)
             out = os.path.join(work, f"out_{fmt}_{r}")
             cli_mod.TIMINGS.clear()
-            if args.cprofile and r == args.runs - 1:
-                os.environ["AWQ_CLI_PROFILE"] = args.cprofile + f".{fmt}.{eng}"
+            argv = ["--model_id", model, "--output_dir", out, "--log_level", "WARNING",
+                    "--output_format", fmt, "--stream_engine", eng] + args.extra.split()
             t0 = time.perf_counter()
-            rc = cli_mod.main(["--model_id", model, "--output_dir", out, "--log_level", "WARNING",
-                               "--output_format", fmt, "--stream_engine", eng] + args.extra.split())
+            if args.cprofile and r == args.runs - 1:
+                import cProfile
+                prof = cProfile.Profile()
+                rc = prof.runcall(cli_mod.main, argv)
+                prof.dump_stats(args.cprofile + f".{fmt}.{eng}")
+            else:
+                rc = cli_mod.main(argv)
             wall = time.perf_counter() - t0
-            os.environ.pop("AWQ_CLI_PROFILE", None)
             assert rc == 0
             ob = sum(os.path.getsize(os.path.join(out, f)) for f in os.listdir(out))
             print(json.dumps({"workload": args.workload, "format": fmt, "engine": eng, "opts": opts, "run": r,

@@ -31,7 +31,7 @@ def main():
     ap.add_argument("--bits", type=int, default=4)
     ap.add_argument("--compare-generic", action="store_true")
     ap.add_argument("--tunings", default="", help="'/'-separated awq_tuning settings to time the quantize under, "
-                    "each 'default' or k=v[,k=v] (include/awq_hip_tuning.h), e.g. default/rg_p1=1")
+                    "each 'default' or k=v[,k=v] (csrc/awq_diag.h, diagnostics build), e.g. default/rg_p1=1")
     ap.add_argument("--dequant", action="store_true", help="also time dequantize_packed of the packed result")
     ap.add_argument("--dq-variants", default="1,3,6,7,8,9", help="--dq-ab: tuning dq_words_v1 values to time")
     ap.add_argument("--lib", default="", help="load this in-tree build instead of _lib/libawq_hip.so (A/B of builds)")
@@ -60,7 +60,10 @@ def one(args, _hip, dev, shape, name, gs, generic, tun=None):
     qw = torch.empty(R, -(-K // per), dtype=torch.int32, device=dev)
     qz = torch.empty(R, -(-G // per), dtype=torch.int32, device=dev)
     sc = torch.empty(R, G, dtype=torch.float16, device=dev)
-    _hip.load_library().awq_set_tuning(ctypes.byref(_hip.Tuning(no_rowgroup=int(generic), **(tun or {}))))
+    import contextlib
+    # overrides run on the diagnostics build (_hip.tuning); the defaults on the shipped library
+    ctx = _hip.tuning(no_rowgroup=int(generic), **(tun or {})) if (generic or tun) else contextlib.nullcontext()
+    ctx.__enter__()
     stage = {}
     if args.search or generic or not _hip.packs_directly(DT[name], R, K, gs):
         stage = dict(tensor_q=torch.empty(R * K, dtype=torch.int32, device=dev),
@@ -80,7 +83,7 @@ def one(args, _hip, dev, shape, name, gs, generic, tun=None):
         run()
     b.record()
     torch.cuda.synchronize()
-    _hip.load_library().awq_set_tuning(None)
+    ctx.__exit__(None, None, None)
     us = a.elapsed_time(b) / args.iters * 1e3
     nbytes = x.numel() * x.element_size()
     algo = nbytes + sum(t.numel() * t.element_size() for t in (qw, qz, sc))
@@ -101,7 +104,7 @@ def one(args, _hip, dev, shape, name, gs, generic, tun=None):
         ref = None
         for rnd in range(3 if args.dq_ab else 1):
             for v in variants:
-                with _hip.tuning(dq_words_v1=v):
+                with (_hip.tuning(dq_words_v1=v) if v else contextlib.nullcontext()):
                     for _ in range(3):
                         dq()
                     a.record()

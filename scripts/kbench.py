@@ -138,7 +138,7 @@ def main():
                         tun.tiles_per_wave = int(blk[1:])
                     elif blk not in ("0", "nt"):     # nt: no per-block tensor table
                         tun.max_blocks = int(blk)
-                    if hasattr(lib, "awq_set_tuning"):   # (include/awq_hip_tuning.h; thread-local)
+                    if hasattr(lib, "awq_set_tuning"):   # (csrc/awq_diag.h, diagnostics build; thread-local)
                         lib.awq_set_tuning(ctypes.byref(tun))
                     evs = []
                     for it in range(args.iters + 3):

@@ -9,7 +9,6 @@
 #include <vector>
 
 #include "../../include/awq_hip.h"
-#include "../../include/awq_hip_tuning.h"
 
 static uint64_t rng = 0x9E3779B97F4A7C15ull;
 static uint64_t next() { rng ^= rng << 13; rng ^= rng >> 7; rng ^= rng << 17; return rng; }
@@ -93,12 +92,7 @@ int main() {
         puts("null handle / items accepted");
         return 1;
     }
-    // ---- tuning + argument validation of the launch entry points (no launch reached) ----
-    awq_tuning t;
-    memset(&t, 0, sizeof t);
-    t.rg_gpt = 13;
-    if (awq_set_tuning(&t) == 0) { puts("bad tuning accepted"); return 1; }
-    if (awq_set_tuning(nullptr) != 0) { puts("tuning reset"); return 1; }
+    // ---- argument validation of the launch entry points (no launch reached) ----
     if (awq_quantize_groups_ex(nullptr, 0, 4, 256, 128, 3, 0, 0, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr) == 0 ||
         awq_quantize_groups_ex(nullptr, 0, 4, 256, 0, 4, 0, 0, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr) == 0 ||
         awq_quantize_groups_ex(nullptr, 0, 4, 256, 128, 4, 0, 7, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr) == 0 ||

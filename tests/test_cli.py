@@ -75,13 +75,10 @@ def test_batch_budget_and_batches(monkeypatch):
     kept; a tensor larger than the budget is a batch of its own."""
     from awq_quantizer.main import _batch_budget, _batches
     from awq_quantizer.model_loading.safetensors_loader import TensorInfo
-    monkeypatch.delenv("AWQ_CLI_BATCH_MB", raising=False)
     MiB = 1 << 20
     assert _batch_budget(662 * MiB, 1 << 30) == 662 * MiB // 8        # opt-350m: ~83 MB batches
     assert _batch_budget(100 * MiB, 1 << 30) == 32 * MiB               # floor
     assert _batch_budget(16 << 30, 1 << 30) == 1 << 30                 # Llama-3-8B: the cap
-    monkeypatch.setenv("AWQ_CLI_BATCH_MB", "5")
-    assert _batch_budget(16 << 30, 1 << 30) == 5 * MiB
     infos = [TensorInfo(f"t{i}", "f", torch.bfloat16, (n,)) for i, n in enumerate([10, 20, 100, 5, 5, 30])]
     bs = _batches(infos, 60)                                           # bytes: 20 40 200 10 10 60
     assert [[i.name for i in b] for b in bs] == [["t0", "t1"], ["t2"], ["t3", "t4"], ["t5"]]

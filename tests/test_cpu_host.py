@@ -14,7 +14,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def declared_symbols():
-    """Every entry point declared by include/*.h (awq_hip.h, awq_hip_tuning.h, awq_ptfile.h)."""
+    """Every entry point declared by include/*.h (awq_hip.h, awq_ptfile.h)."""
     src = ""
     for h in sorted(os.listdir(os.path.join(ROOT, "include"))):
         if h.endswith(".h"):
@@ -32,6 +32,18 @@ def test_library_exports_every_declared_symbol():
         assert hasattr(lib, s), s
     assert set(syms) == set(_hip.SIGNATURES), "python binding out of sync with include/*.h"
     assert lib.awq_abi_version() == _hip.ABI_VERSION == 13
+
+
+def test_product_library_has_no_diagnostics_entry_points():
+    """one path per shape in the shipped library — no tuning entry point
+    (it lives in the diagnostics build only, with the A/B kernel variants)."""
+    from awq_quantizer import _hip
+    lib = _hip.load_library()
+    assert not hasattr(lib, "awq_set_tuning")
+    if os.path.exists(_hip.DIAG_LIB_PATH):
+        assert hasattr(_hip.load_diag_library(), "awq_set_tuning")
+    src = open(os.path.join(ROOT, "awq-converter_amd", "awq_quantizer", "main.py")).read()
+    assert "os.environ" not in src.replace('os.environ.get("AWQ_DIST_BACKEND"', "")
 
 
 def test_library_is_gfx950_code_object():

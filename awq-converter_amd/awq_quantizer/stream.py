@@ -213,8 +213,9 @@ def quantize_stream_native(loader, infos, quantizer, device: str, readers: int, 
                             pipeline's items are the only ones still open while it runs;
     release_hook(fn)        registers fn(names), to be called once results are no longer
                             read (written); with it the host ring may wrap;
-    group_of[name]          the output group (chunk) of every tensor the hook releases
-                            together — needed to size a wrapping host ring;
+    group_of                the output group (chunk) of every tensor the hook releases
+                            together, {name: group} or a callable returning it (called once
+                            the per-tensor path has run) — needed to size a wrapping host ring;
     host_ring_bytes / dev_ring_bytes   ring sizes (0: sized by simulation, see module doc);
     keep_on_device          results stay in one device arena (no host copy, no ring).
     """
@@ -301,7 +302,9 @@ def quantize_stream_native(loader, infos, quantizer, device: str, readers: int, 
     releaser = None
     if not keep_on_device:
         if release_hook is not None and group_of is not None:
-            grp = [group_of.get(i.name, k) for k, (i, _, _) in enumerate(items)]
+            # (a callable: evaluated now, after the per-tensor path above reported its tensors)
+            groups = group_of() if callable(group_of) else group_of
+            grp = [groups.get(i.name, k) for k, (i, _, _) in enumerate(items)]
             gend, e = [0] * n, n - 1
             for k in range(n - 1, -1, -1):       # the last item of every item's group
                 if k < n - 1 and grp[k] != grp[k + 1]:

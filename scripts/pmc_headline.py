@@ -34,9 +34,9 @@ for k, c in summ.items():
             if n in c:
                 r[n + "_over_wave_cycles"] = round(c[n] / wc, 4)
     if "FETCH_SIZE" in c:
-        r["hbm_read_bytes (FETCH_SIZE x2 KiB)"] = c["FETCH_SIZE"] * 2048
+        r["hbm_read_bytes (bytes = FETCH_SIZE KiB x 1024 x 2, gfx950 half-count)"] = c["FETCH_SIZE"] * 2048
     if "WRITE_SIZE" in c:
-        r["hbm_write_bytes (KiB)"] = c["WRITE_SIZE"] * 1024
+        r["hbm_write_bytes (bytes = WRITE_SIZE KiB x 1024)"] = c["WRITE_SIZE"] * 1024
     if "GRBM_GUI_ACTIVE" in c:
         r["GRBM_GUI_ACTIVE"] = c["GRBM_GUI_ACTIVE"]
     out[k] = r

@@ -35,6 +35,8 @@ typedef struct awq_tuning {
                                 merges, parameters by one lane per group) */
     int32_t rg_lds_full;     /* row-segment LDS stage: 0 sized to the elements a tile holds (min(groups
                                 x group size, K)), 1 to its groups x group size (round-2 sizing, A/B) */
+    int32_t rg_p2reg;        /* row-segment pass 2: 0 reads a 4-chunk stage's data from the stage's
+                                registers, 1 from LDS (round-3 behaviour, A/B) */
 } awq_tuning;
 
 #ifdef AWQ_DIAG

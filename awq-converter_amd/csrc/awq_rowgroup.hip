@@ -179,7 +179,7 @@ __global__ __launch_bounds__(128) void awq_rowgroup_kernel(const void* __restric
                                                              int32_t* __restrict__ qweight, int32_t* __restrict__ qzeros,
                                                              uint16_t* __restrict__ scales,
                                                              int32_t* __restrict__ tensor_q, int32_t* __restrict__ zeros,
-                                                             uint32_t nan_code, int lgP_last, int C_last) {
+                                                             uint32_t nan_code, int lgP_last, int C_last, int p2reg) {
     typedef RgSlot<F> SL;
     typedef typename SL::T S;
     constexpr int QMIN = SYM ? -(1 << (BITS - 1)) : 0;
@@ -225,6 +225,7 @@ __global__ __launch_bounds__(128) void awq_rowgroup_kernel(const void* __restric
     const uint64_t rem = total - a0;                              // bytes from a0 to the tensor end
     const uint32_t lim = (rem >> 32) ? 16u * (uint32_t)nch : min((uint32_t)rem, 16u * (uint32_t)nch);
     const __amdgpu_buffer_rsrc_t rw = rsrc((const char*)w + a0, lim);
+    u4 vreg[4];                              // the 4-chunk stage's loads, reused by pass 2
     if (__builtin_expect(16u * (uint32_t)nch <= lim, 1)) {
         // every 16-B load of the segment in flight before the first LDS store (a load ->
         // store loop waits out one memory round trip per load).  All 8 loads are issued
@@ -234,13 +235,13 @@ __global__ __launch_bounds__(128) void awq_rowgroup_kernel(const void* __restric
         // store nothing
         if (nch == 4 * NT) {
             // (exactly 4 chunks per lane — a 4 096-element bf16 row on two waves: 4 loads
-            //  and 4 unmasked stores, no range-checked dummy loads)
-            u4 v[4];
+            //  and 4 unmasked stores, no range-checked dummy loads; the chunks stay in
+            //  registers for pass 2, whose lane -> chunk map is the same)
 #pragma unroll
             for (int k = 0; k < 4; ++k)
-                v[k] = __builtin_amdgcn_raw_buffer_load_b128(rw, (uint32_t)(16 * (NT * k + lane)), 0, AWQ_LOAD_AUX);
+                vreg[k] = __builtin_amdgcn_raw_buffer_load_b128(rw, (uint32_t)(16 * (NT * k + lane)), 0, AWQ_LOAD_AUX);
 #pragma unroll
-            for (int k = 0; k < 4; ++k) *(u4*)((char*)stage + 16 * (NT * k + lane)) = v[k];
+            for (int k = 0; k < 4; ++k) *(u4*)((char*)stage + 16 * (NT * k + lane)) = vreg[k];
         } else
         for (int c0 = 0; c0 < nch; c0 += 8 * NT) {
             u4 v[8];
@@ -455,14 +456,15 @@ __global__ __launch_bounds__(128) void awq_rowgroup_kernel(const void* __restric
     int32_t* qdst = qweight ? qweight + r * wpr + kb / PER : nullptr;
     // one chunk: c = its index in the segment, efA = 8 c + 0.5 (exact float); ALIGNED: the
     // segment starts 16-B aligned (skew 0); FULL: the chunk holds 8 elements of the row
-    auto sweep = [&](int c, float efA, auto aligned_t, auto full_t, auto plain_t) {
+    auto sweep = [&](int c, float efA, auto aligned_t, auto full_t, auto plain_t, const u4* rv = nullptr) {
         constexpr bool ALIGNED = decltype(aligned_t)::value, FULL = decltype(full_t)::value;
         constexpr bool PLAIN = decltype(plain_t)::value;
         const int e0c = 8 * c;
         const bool tail = !FULL && e0c + 8 > n_el;        // the row's last, partial chunk
         float x[8];
         if constexpr (ALIGNED) {                          // 16-B aligned chunk (K % 8 == 0 rows)
-            const u4 v0 = *(const u4*)(stage + e0c);      // (past n_el: the stage's slack)
+            // (from the stage's registers when given; past n_el: the stage's slack)
+            const u4 v0 = (F::kBytes == 2 && rv) ? *rv : *(const u4*)(stage + e0c);
             if constexpr (F::kBytes == 2) {
 #pragma unroll
                 for (int i = 0; i < 4; ++i) {
@@ -590,6 +592,15 @@ __global__ __launch_bounds__(128) void awq_rowgroup_kernel(const void* __restric
     const float efStep = 8.0f * (float)NT;
     const int lgNT = NT == 128 ? 7 : 6;
     auto sweeps = [&](auto aligned_t, auto plain_t) {
+        if constexpr (F::kBytes == 2 && decltype(aligned_t)::value) {
+            if (p2reg && nch == 4 * NT && n_el == 32 * NT) {   // the 4-chunk stage: data in registers
+                float efA = 8.0f * (float)lane + 0.5f;
+#pragma unroll
+                for (int sw = 0; sw < 4; ++sw, efA += efStep)
+                    sweep(lane + (sw << lgNT), efA, aligned_t, std::true_type{}, plain_t, &vreg[sw]);
+                return;
+            }
+        }
         const int full_sweeps = (n_el >> 3) >> lgNT;
         float efA = 8.0f * (float)lane + 0.5f;
         for (int sw = 0; sw < full_sweeps; ++sw, efA += efStep)
@@ -705,10 +716,11 @@ hipError_t launch_rowgroup(const void* w, int dtype, int64_t rows, int64_t K, in
     const int64_t stage_el = tuning().rg_lds_full == 1 ? (int64_t)gpt * L : min((int64_t)gpt * L, K);
     const size_t lds = (size_t)((stage_el * es + 15) / 16 * 16 + 48);
     const bool p1c = tuning().rg_p1 == 2;   // pass 1 by groups (default) / evenly split runs (A/B)
+    const int p2reg = tuning().rg_p2reg == 1 ? 0 : 1;   // pass 2 from the stage's registers (A/B: 1 = off)
 #define AWQ_RG_GO(Fm, B, S, SP, P1, TQ)                                                                            \
     hipLaunchKernelGGL((awq_rowgroup_kernel<Fm, B, S, SP, P1, TQ>), grid, block, lds, stream, w, rows, K, L, lgP,  \
                        gpt, (uint32_t)tpr, G, C, 1.0f / (float)L, qweight, qzeros, scales, tensor_q, zeros, nan_code, \
-                       lgP_last, C_last)
+                       lgP_last, C_last, p2reg)
     // (the pass-1 A/B variant is built for the packed outputs only; with tensor_q it takes the default)
 #ifdef AWQ_DIAG
 #define AWQ_RG_SPLIT(Fm, B, S, SP)                                                                                 \

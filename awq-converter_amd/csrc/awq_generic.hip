@@ -500,7 +500,7 @@ __global__ __launch_bounds__(256) void awq_dequant_kernel(
 template <int BITS>
 __global__ __launch_bounds__(256) void awq_dequant_words_kernel(
     const int32_t* __restrict__ qweight, const uint16_t* __restrict__ scales, const int32_t* __restrict__ qzeros,
-    int64_t words, uint32_t wpr, uint32_t L, uint32_t G, uint32_t zpr, int qmin, float* __restrict__ out) {
+    int64_t words, uint32_t wpr, uint32_t L, uint32_t G, uint32_t zpr, int qmin, float* __restrict__ out, float /*invL*/) {
     constexpr int PER = 32 / BITS;
     constexpr uint32_t MASK = (1u << BITS) - 1u;
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -560,7 +560,7 @@ __device__ __forceinline__ uint32_t xcd_contiguous_block(uint32_t b, uint32_t nb
 template <int BITS, bool REMAP>
 __global__ __launch_bounds__(kDqThreads) void awq_dequant_words_v2_kernel(
     const int32_t* __restrict__ qweight, const uint16_t* __restrict__ scales, const int32_t* __restrict__ qzeros,
-    int64_t words, uint32_t wpr, uint32_t L, uint32_t G, uint32_t zpr, int qmin, float* __restrict__ out) {
+    int64_t words, uint32_t wpr, uint32_t L, uint32_t G, uint32_t zpr, int qmin, float* __restrict__ out, float /*invL*/) {
     constexpr int PER = 32 / BITS;
     constexpr uint32_t MASK = (1u << BITS) - 1u;
     __shared__ __attribute__((aligned(16))) float stage[kDqThreads * PER];
@@ -628,7 +628,7 @@ __global__ __launch_bounds__(kDqThreads) void awq_dequant_words_v2_kernel(
 template <int BITS, bool REMAP>
 __global__ __launch_bounds__(256) void awq_dequant_quads_kernel(
     const int32_t* __restrict__ qweight, const uint16_t* __restrict__ scales, const int32_t* __restrict__ qzeros,
-    int64_t words, uint32_t wpr, uint32_t L, uint32_t G, uint32_t zpr, int qmin, float* __restrict__ out) {
+    int64_t words, uint32_t wpr, uint32_t L, uint32_t G, uint32_t zpr, int qmin, float* __restrict__ out, float /*invL*/) {
     constexpr int PER = 32 / BITS;
     constexpr int LPW = PER / 4;                        // lanes per word: 2 (4-bit), 1 (8-bit)
     constexpr uint32_t MASK = (1u << BITS) - 1u;
@@ -684,20 +684,35 @@ __device__ __forceinline__ uint32_t dq_run_block(uint32_t b, uint32_t nb, uint32
     return (i / R) * (8u * R) + x * R + (i % R);
 }
 
-template <int BITS, int U, int RUN>
+// Group index e / L of column e by a float estimate and one correction step each way
+// (exact for e < 2^22: the estimate is within 1; the launcher admits K < 2^22 for GMODE > 0).
+__device__ __forceinline__ uint32_t dq_gdiv(uint32_t e, uint32_t L, float invL) {
+    uint32_t q = (uint32_t)((float)e * invL);
+    if (q * L > e) --q;
+    else if ((q + 1) * L <= e) ++q;
+    return q;
+}
+
+// GMODE: 0 = a qweight word's PER elements share one group (L % PER == 0); 1 = a quad's 4
+// elements do (L % 4 == 0); 2 = any L >= 4 (a quad meets at most two groups: the first
+// `bnd` elements take group A's parameters, the rest group B's).  Dequantize of any group
+// size at the batched kernel's memory structure (round 4: the per-element generic kernel ran
+// group size 100 at 0.10 of 8 TB/s).
+template <int BITS, int U, int RUN, int GMODE>
 __global__ __launch_bounds__(256) void awq_dequant_batch_kernel(
     const int32_t* __restrict__ qweight, const uint16_t* __restrict__ scales, const int32_t* __restrict__ qzeros,
-    int64_t words, uint32_t wpr, uint32_t L, uint32_t G, uint32_t zpr, int qmin, float* __restrict__ out) {
+    int64_t words, uint32_t wpr, uint32_t L, uint32_t G, uint32_t zpr, int qmin, float* __restrict__ out,
+    float invL) {
     constexpr int PER = 32 / BITS;
     constexpr int LPW = PER / 4;                        // lanes (quads) per word
     constexpr uint32_t MASK = (1u << BITS) - 1u;
     const int64_t blk = RUN > 0 ? dq_run_block(blockIdx.x, gridDim.x, RUN) : blockIdx.x;
     const int64_t quads = words * LPW;
     const int64_t q0 = blk * (256 * U) + threadIdx.x;
-    uint32_t wq[U], zq[U];
-    uint16_t sb[U];
+    uint32_t wq[U], zq[U], zq2[U];
+    uint16_t sb[U], sb2[U];
     int64_t ii[U];
-    uint32_t cc[U], gg[U];
+    uint32_t cc[U], gg[U], gg2[U], bnd[U];
 #pragma unroll
     for (int k = 0; k < U; ++k) {
         const int64_t q = min(q0 + 256 * k, quads - 1);   // (past the end: a valid address, no store)
@@ -712,13 +727,29 @@ __global__ __launch_bounds__(256) void awq_dequant_batch_kernel(
             r = i / wpr;
             c = (uint32_t)(i - r * wpr);
         }
-        const uint32_t g = (uint32_t)(((uint64_t)c * PER) / L);
+        uint32_t g, g2 = 0, b = 4;
+        if constexpr (GMODE == 0) {
+            g = (uint32_t)(((uint64_t)c * PER) / L);
+        } else {
+            const uint32_t e0 = c * PER + 4u * (uint32_t)(q - i * LPW);
+            g = dq_gdiv(e0, L, invL);
+            if constexpr (GMODE == 2) {
+                b = min((g + 1) * L - e0, 4u);
+                g2 = b < 4 ? g + 1 : g;
+            }
+        }
         ii[k] = i;
         cc[k] = c;
         gg[k] = g;
         wq[k] = (uint32_t)__builtin_nontemporal_load(qweight + i);
         sb[k] = scales[r * G + g];
         zq[k] = (uint32_t)qzeros[r * zpr + g / PER];
+        if constexpr (GMODE == 2) {
+            gg2[k] = g2;
+            bnd[k] = b;
+            sb2[k] = scales[r * G + g2];
+            zq2[k] = (uint32_t)qzeros[r * zpr + g2 / PER];
+        }
     }
     typedef float f4 __attribute__((ext_vector_type(4)));
 #pragma unroll
@@ -727,16 +758,18 @@ __global__ __launch_bounds__(256) void awq_dequant_batch_kernel(
         if (q >= quads) break;
         const int half = (int)(q - ii[k] * LPW);
         const uint32_t w = wq[k] >> (16 * half);
-        const float s = (float)__builtin_bit_cast(_Float16, sb[k]);
-        const int32_t z = (int32_t)((zq[k] >> (BITS * (gg[k] % PER))) & MASK) + qmin;
         float v[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
+            const bool a = GMODE != 2 || (uint32_t)j < bnd[k];
+            const uint32_t g = a ? gg[k] : gg2[k];
+            const float s = (float)__builtin_bit_cast(_Float16, a ? sb[k] : sb2[k]);
+            const int32_t z = (int32_t)(((a ? zq[k] : zq2[k]) >> (BITS * (g % PER))) & MASK) + qmin;
             const int32_t qv = (int32_t)((w >> (BITS * j)) & MASK) + qmin;
             const float p = (float)(qv - z) * s;
             if (__builtin_expect(__builtin_isnan(p), 0)) {   // NaN bits of the reference's fp32 copy
                 const int64_t kk = (int64_t)cc[k] * PER + 4 * half + j, K = (int64_t)wpr * PER,
-                              g0 = (int64_t)gg[k] * L;
+                              g0 = (int64_t)g * L;
                 v[j] = __uint_as_float(dq_nan_bits(sw_f32_to_f16(p), kk - g0, min((int64_t)L, K - g0)));
             } else {
                 v[j] = (float)(_Float16)p;
@@ -746,16 +779,18 @@ __global__ __launch_bounds__(256) void awq_dequant_batch_kernel(
     }
 }
 
-template <int B> constexpr auto dq_batch4_run = awq_dequant_batch_kernel<B, 4, 4>;
+template <int B> constexpr auto dq_batch4_run = awq_dequant_batch_kernel<B, 4, 4, 0>;
+template <int B> constexpr auto dq_batch4_run_q = awq_dequant_batch_kernel<B, 4, 4, 1>;
+template <int B> constexpr auto dq_batch4_run_e = awq_dequant_batch_kernel<B, 4, 4, 2>;
 constexpr int kDqDefault = 8;   // batched lanes in XCD runs: profiles/round3/dequant
 #ifdef AWQ_DIAG
 template <int B> constexpr auto dq_v2_remap = awq_dequant_words_v2_kernel<B, true>;
 template <int B> constexpr auto dq_v2_plain = awq_dequant_words_v2_kernel<B, false>;
 template <int B> constexpr auto dq_quads_plain = awq_dequant_quads_kernel<B, false>;
 template <int B> constexpr auto dq_quads_remap = awq_dequant_quads_kernel<B, true>;
-template <int B> constexpr auto dq_batch4 = awq_dequant_batch_kernel<B, 4, 0>;
-template <int B> constexpr auto dq_batch8 = awq_dequant_batch_kernel<B, 8, 0>;
-template <int B> constexpr auto dq_batch8_run = awq_dequant_batch_kernel<B, 8, 2>;
+template <int B> constexpr auto dq_batch4 = awq_dequant_batch_kernel<B, 4, 0, 0>;
+template <int B> constexpr auto dq_batch8 = awq_dequant_batch_kernel<B, 8, 0, 0>;
+template <int B> constexpr auto dq_batch8_run = awq_dequant_batch_kernel<B, 8, 2, 0>;
 #endif
 
 inline unsigned grid_for(int64_t work, int64_t per_block, int64_t cap) {
@@ -883,7 +918,11 @@ hipError_t launch_dequant(const int32_t* tensor_q, const int32_t* qweight, const
     if (total <= 0) return hipSuccess;
     const int per = 32 / bits;
     const int64_t G = (K + L - 1) / L;
-    if (!tensor_q && K % per == 0 && L % per == 0 && ((uintptr_t)out & 15) == 0 && K / per <= 0x7FFFFFFF &&
+    // the batched quad kernel: word-aligned groups (GMODE 0), quad-aligned (1), or any L >= 4 (2)
+    // for rows of < 2^22 elements
+    const int gmode = L % per == 0 ? 0 : (L % 4 == 0 ? 1 : 2);
+    if (!tensor_q && K % per == 0 && (gmode == 0 || (L >= 4 && K < ((int64_t)1 << 22))) &&
+        ((uintptr_t)out & 15) == 0 && K / per <= 0x7FFFFFFF &&
         L <= 0x7FFFFFFF && G <= 0x7FFFFFFF && total / per < ((int64_t)1 << 32) - 256) {   // one thread per word
         const int64_t words = total / per;
         const uint32_t wpr = (uint32_t)(K / per), zpr = (uint32_t)((G + per - 1) / per);
@@ -894,17 +933,18 @@ hipError_t launch_dequant(const int32_t* tensor_q, const int32_t* qweight, const
         // lanes without / with XCD-contiguous blocks, 6 / 7 batched lanes (4 / 8 quads), 9 the
         // batched lanes in XCD runs of 2 blocks
         int v = kDqDefault;
+        const float invL = 1.0f / (float)L;
 #ifdef AWQ_DIAG
-        if (tuning().dq_words_v1 > 0 && tuning().dq_words_v1 <= 9) v = tuning().dq_words_v1;
+        if (gmode == 0 && tuning().dq_words_v1 > 0 && tuning().dq_words_v1 <= 9) v = tuning().dq_words_v1;
 #endif
 #define AWQ_DQ(KER, GRID)                                                                                   \
         do {                                                                                                \
             if (bits == 4)                                                                                  \
                 hipLaunchKernelGGL(KER<4>, GRID, block, 0, stream, qweight, scales, qzeros, words, wpr,     \
-                                   (uint32_t)L, (uint32_t)G, zpr, qmin, out);                               \
+                                   (uint32_t)L, (uint32_t)G, zpr, qmin, out, invL);                         \
             else                                                                                            \
                 hipLaunchKernelGGL(KER<8>, GRID, block, 0, stream, qweight, scales, qzeros, words, wpr,     \
-                                   (uint32_t)L, (uint32_t)G, zpr, qmin, out);                               \
+                                   (uint32_t)L, (uint32_t)G, zpr, qmin, out, invL);                         \
         } while (0)
         const dim3 grid_q((unsigned)((words * (per / 4) + 255) / 256));
         const dim3 grid_b4((unsigned)((words * (per / 4) + 1023) / 1024)),
@@ -920,7 +960,11 @@ hipError_t launch_dequant(const int32_t* tensor_q, const int32_t* qweight, const
         case 4: AWQ_DQ(dq_quads_plain, grid_q); break;
         case 5: AWQ_DQ(dq_quads_remap, grid_q); break;
 #endif
-        default: AWQ_DQ(dq_batch4_run, grid_b4); break;
+        default:
+            if (gmode == 0) AWQ_DQ(dq_batch4_run, grid_b4);
+            else if (gmode == 1) AWQ_DQ(dq_batch4_run_q, grid_b4);
+            else AWQ_DQ(dq_batch4_run_e, grid_b4);
+            break;
         }
 #undef AWQ_DQ
         return hipPeekAtLastError();

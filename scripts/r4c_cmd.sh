@@ -1,4 +1,4 @@
-GB='python scripts/generic_bench.py --iters 30 --group-sizes 100,48,200,96 --shape 14336,4096;4096,14336 --dtypes bf16,f16'
+GB="python scripts/generic_bench.py --iters 30 --group-sizes 100,48,200,96 --shape '14336,4096;4096,14336' --dtypes bf16,f16"
 bash scripts/gpu_run.sh r4c \
  "pytest=tests/test_gpu_rowgroup.py tests/test_gpu_nan.py tests/test_gpu_odd_groups.py" \
  "ab1:300:$GB --tunings rg_waves=0/rg_p2reg=1" \

@@ -82,10 +82,15 @@ def test_generic_f64_search_packed(gs):
 @pytest.mark.parametrize("dtype,shape,gs", [(torch.bfloat16, (64, 4096), 128), (torch.float16, (33, 1024), 32),
                                             (torch.bfloat16, (17, 2000), 200), (torch.float32, (5, 4096), 256),
                                             (torch.bfloat16, (9, 1000), 100), (torch.bfloat16, (7, 1001), 91),
-                                            (torch.float64, (6, 1024), 64)], ids=str)
+                                            (torch.float64, (6, 1024), 64), (torch.bfloat16, (13, 2000), 50),
+                                            (torch.float16, (11, 1008), 7), (torch.bfloat16, (4, 4096), 100),
+                                            (torch.bfloat16, (6, 64), 3), (torch.float32, (8, 4104), 57),
+                                            (torch.bfloat16, (3, 512), 4)], ids=str)
 def test_dequantize_packed_vs_oracle(dtype, shape, gs, bits, sym):
-    """dequantize_packed (awq.py:459-539 arithmetic): word-aligned groups (K and L multiples of
-    32 / bits) take the word-per-thread kernel, the rest the per-element kernel; NaN / inf /
+    """dequantize_packed (awq.py:459-539 arithmetic): rows of whole qweight words (K a multiple
+    of 32 / bits) take the batched quad kernel — word-aligned groups, quad-aligned groups
+    (L % 4 == 0) or any L >= 4 (a quad meeting two groups) — the rest (L < 4, ragged K) the
+    per-element kernel; NaN / inf /
     constant groups included.  Bit-exact (NaN payloads compared as NaN) vs the oracle's
     dequantize of the oracle's quantize, its int32 values taken through the packed format
     first (a nibble / byte holds (v - qmin) mod 2^bits: the INT_MIN of an inf / inf element

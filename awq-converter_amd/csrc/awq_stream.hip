@@ -370,6 +370,19 @@ void submitter_main(Pipeline* P) {
     hipStream_t h2d = (hipStream_t)c.h2d_stream, cs = (hipStream_t)c.compute_stream, d2h = (hipStream_t)c.d2h_stream;
     const int64_t nb = (int64_t)P->batches.size();
     BatchPlan bp;
+    // The copy paths' first use in a process costs ~0.1 s (HIP's copy machinery; the first D2H
+    // into fresh pinned memory ran at 2.6 GB/s for 256 MiB against 57 later, profiles/round4/
+    // r4b/pin_probe.txt): take it now, on both copy streams, while the readers fill the first
+    // batch — through slot 0's table area, which nothing else touches until batch 0 is planned.
+    if (nb > 0) {
+        char* h = (char*)c.host_staging;
+        char* d = (char*)c.dev_staging;
+        if (!P->hip_ok(hipMemcpyAsync(d, h, 256, hipMemcpyHostToDevice, h2d), "warm-up H2D") ||
+            !P->hip_ok(hipStreamSynchronize(h2d), "warm-up H2D") ||
+            !P->hip_ok(hipMemcpyAsync(h, d, 256, hipMemcpyDeviceToHost, d2h), "warm-up D2H") ||
+            !P->hip_ok(hipStreamSynchronize(d2h), "warm-up D2H"))
+            return;
+    }
     for (int64_t b = 0; b < nb; ++b) {
         const Batch& B = P->batches[b];
         double t = now_s();

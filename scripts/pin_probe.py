@@ -29,6 +29,23 @@ def child(method, mb, threads):
     nbytes = mb << 20
     t0 = time.perf_counter()
     keep = None
+    if method == "twoalloc":
+        # is the first D2H's extra cost per process (copy machinery) or per allocation?
+        hip = _hip = ctypes.CDLL("libamdhip64.so")
+        bufs = []
+        for _ in range(2):
+            p = ctypes.c_void_p()
+            assert hip.hipHostMalloc(ctypes.byref(p), ctypes.c_size_t(nbytes), 0) == 0
+            bufs.append(torch.frombuffer((ctypes.c_char * nbytes).from_address(p.value), dtype=torch.uint8))
+        out = {"method": method, "MB": mb}
+        for k, b in enumerate(bufs + bufs):
+            torch.cuda.synchronize()
+            t = time.perf_counter()
+            b.copy_(src, non_blocking=True)
+            torch.cuda.synchronize()
+            out[f"d2h_{k}_GBs"] = round(nbytes / (time.perf_counter() - t) / 1e9, 1)
+        print(json.dumps(out), flush=True)
+        return
     if method == "torch":
         h = torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)
         ptr = h.data_ptr()

@@ -26,17 +26,21 @@ def build_model(path, workload, shards):
     shapes = bench.shapes_of(workload)
     if os.path.exists(os.path.join(path, "complete")):    # reuse a model built by an earlier run (--workdir)
         return sum(int(torch.Size(s).numel()) * 2 for s in shapes)
-    g = torch.Generator().manual_seed(0)
+    # generated on the GPU when there is one (a 16 GB checkpoint in seconds, not minutes), with
+    # a progress line per shard (a silent multi-minute build looks hung to the GPU runner)
+    dev = torch.device("cuda", 0) if torch.cuda.is_available() else torch.device("cpu")
+    g = torch.Generator(device=dev).manual_seed(0)
     names = [f"model.layers.{i // 8}.t{i}.weight" for i in range(len(shapes))]
     per = -(-len(shapes) // shards)
     nbytes = 0
     for sh in range(shards):
         part = {}
         for n, s in list(zip(names, shapes))[sh * per:(sh + 1) * per]:
-            part[n] = (torch.randn(*s, generator=g) * 0.02).to(torch.bfloat16)
+            part[n] = (torch.randn(*s, generator=g, device=dev) * 0.02).to(torch.bfloat16).cpu()
             nbytes += part[n].numel() * 2
         if part:
             save_file(part, os.path.join(path, f"model-{sh:05d}-of-{shards:05d}.safetensors"))
+            print(f"build_model: shard {sh + 1}/{shards} written ({nbytes / 1e9:.1f} GB so far)", flush=True)
     open(os.path.join(path, "complete"), "w").close()
     return nbytes
 

@@ -5,5 +5,6 @@ bash scripts/gpu_run.sh r4c \
  "ab2:300:$GB --tunings rg_p2reg=1/rg_waves=0" \
  "ceiling:120:python scripts/ceiling_probe.py --mb 117.440512,469.762048,1073.741824" \
  "dqprobe:120:scripts/dq_probe" \
+ "pin2:120:python scripts/pin_probe.py --sizes-mb 256 --methods twoalloc" \
  "cli350:600:python scripts/cli_first_run.py --workload opt-350m --shards 3 --formats packed,reference --runs 2" \
  "cli8b:900:python scripts/cli_first_run.py --workload llama3-8b --shards 4 --formats packed --runs 2"

@@ -37,6 +37,7 @@ typedef struct awq_tuning {
                                 x group size, K)), 1 to its groups x group size (round-2 sizing, A/B) */
     int32_t rg_p2reg;        /* row-segment pass 2: 0 reads a 4-chunk stage's data from the stage's
                                 registers, 1 from LDS (round-3 behaviour, A/B) */
+    int32_t rg_ldsdma;       /* row-segment 4-chunk stage: 1 = LDS-DMA (global_load_lds_dwordx4) */
 } awq_tuning;
 
 #ifdef AWQ_DIAG

@@ -179,7 +179,8 @@ __global__ __launch_bounds__(128) void awq_rowgroup_kernel(const void* __restric
                                                              int32_t* __restrict__ qweight, int32_t* __restrict__ qzeros,
                                                              uint16_t* __restrict__ scales,
                                                              int32_t* __restrict__ tensor_q, int32_t* __restrict__ zeros,
-                                                             uint32_t nan_code, int lgP_last, int C_last, int p2reg) {
+                                                             uint32_t nan_code, int lgP_last, int C_last, int p2reg,
+                                                             int ldsdma) {
     typedef RgSlot<F> SL;
     typedef typename SL::T S;
     constexpr int QMIN = SYM ? -(1 << (BITS - 1)) : 0;
@@ -233,7 +234,19 @@ __global__ __launch_bounds__(128) void awq_rowgroup_kernel(const void* __restric
         // read zeros without a memory access, and no register needs a value on a skipped
         // path (conditional loads cost 28 v_mov per wave of phi copies); lanes past the end
         // store nothing
-        if (nch == 4 * NT) {
+        if (nch == 4 * NT && ldsdma) {
+            // (diagnostics A/B: the 4 chunks straight from memory into the stage, LDS-DMA —
+            //  no VGPR round trip, no LDS store instructions; pass 2 then reads the stage)
+            const char* src = (const char*)w + a0;
+            const int wbase = __builtin_amdgcn_readfirstlane(lane & ~63);
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                __builtin_amdgcn_global_load_lds((const void*)(src + 16 * (NT * k + lane)),
+                                                 (__attribute__((address_space(3))) void*)((char*)stage +
+                                                                                          16 * (NT * k + wbase)),
+                                                 16, 0, 0);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        } else if (nch == 4 * NT) {
             // (exactly 4 chunks per lane — a 4 096-element bf16 row on two waves: 4 loads
             //  and 4 unmasked stores, no range-checked dummy loads; the chunks stay in
             //  registers for pass 2, whose lane -> chunk map is the same)
@@ -716,11 +729,12 @@ hipError_t launch_rowgroup(const void* w, int dtype, int64_t rows, int64_t K, in
     const int64_t stage_el = tuning().rg_lds_full == 1 ? (int64_t)gpt * L : min((int64_t)gpt * L, K);
     const size_t lds = (size_t)((stage_el * es + 15) / 16 * 16 + 48);
     const bool p1c = tuning().rg_p1 == 2;   // pass 1 by groups (default) / evenly split runs (A/B)
-    const int p2reg = tuning().rg_p2reg == 1 ? 0 : 1;   // pass 2 from the stage's registers (A/B: 1 = off)
+    const int ldsdma = tuning().rg_ldsdma == 1 ? 1 : 0;  // (A/B) the 4-chunk stage by LDS-DMA
+    const int p2reg = (tuning().rg_p2reg == 1 || ldsdma) ? 0 : 1;   // pass 2 from the stage's registers (A/B: 1 = off)
 #define AWQ_RG_GO(Fm, B, S, SP, P1, TQ)                                                                            \
     hipLaunchKernelGGL((awq_rowgroup_kernel<Fm, B, S, SP, P1, TQ>), grid, block, lds, stream, w, rows, K, L, lgP,  \
                        gpt, (uint32_t)tpr, G, C, 1.0f / (float)L, qweight, qzeros, scales, tensor_q, zeros, nan_code, \
-                       lgP_last, C_last, p2reg)
+                       lgP_last, C_last, p2reg, ldsdma)
     // (the pass-1 A/B variant is built for the packed outputs only; with tensor_q it takes the default)
 #ifdef AWQ_DIAG
 #define AWQ_RG_SPLIT(Fm, B, S, SP)                                                                                 \

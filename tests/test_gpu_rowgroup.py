@@ -158,3 +158,22 @@ def test_rowgroup_whole_row_tiles(dtype, K, gs):
     for bits, sym in ((4, False), (8, True)):
         _assert_parity(x, gs, bits, sym)
     _assert_parity(specials(rand((24, K), gs, 1.0), 3).to(dtype), gs, 4, False)
+
+
+@pytest.mark.parametrize("tun", [{"rg_p2reg": 1}, {"rg_ldsdma": 1}], ids=lambda t: next(iter(t)))
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16], ids=str)
+@pytest.mark.parametrize("K,gs", [(4096, 100), (4096, 48), (4096, 200), (3000, 100)], ids=str)
+def test_rowgroup_stage_variants_same_bits(dtype, K, gs, tun):
+    """The 4-chunk stage's pass 2 from registers (the default) gives the bits of the same
+    pass from the LDS stage (diagnostics build, rg_p2reg = 1) and of an LDS-DMA stage
+    (rg_ldsdma = 1); special values included."""
+    from awq_quantizer import _hip
+    x = specials(rand((40, K), K + gs + 7, 0.5), 9).to(dtype)
+    for bits, sym in ((4, False), (8, True)):
+        q = Q(bits=bits, group_size=gs, symmetric=sym)
+        a = q.quantize_packed(x)
+        with _hip.tuning(**tun):
+            b = Q(bits=bits, group_size=gs, symmetric=sym).quantize_packed(x)
+        for key in ("qweight", "qzeros"):
+            assert torch.equal(a[key], b[key]), key
+        assert gio.same_bits(a["scales"], b["scales"])

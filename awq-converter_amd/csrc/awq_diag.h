@@ -35,9 +35,10 @@ typedef struct awq_tuning {
                                 merges, parameters by one lane per group) */
     int32_t rg_lds_full;     /* row-segment LDS stage: 0 sized to the elements a tile holds (min(groups
                                 x group size, K)), 1 to its groups x group size (round-2 sizing, A/B) */
-    int32_t rg_p2reg;        /* row-segment pass 2: 0 reads a 4-chunk stage's data from the stage's
-                                registers, 1 from LDS (round-3 behaviour, A/B) */
-    int32_t rg_ldsdma;       /* row-segment 4-chunk stage: 1 = LDS-DMA (global_load_lds_dwordx4) */
+    int32_t rg_ldsdma;       /* row-segment stage: 0 LDS-DMA (buffer_load_dwordx4 ... lds, the default),
+                                1 the round-3 register stage (loads to VGPRs, LDS stores) */
+    int32_t rg_p2reg;        /* with rg_ldsdma = 1: pass 2 of a 4-chunk stage from the stage's
+                                registers (0) or from LDS (1) */
 } awq_tuning;
 
 #ifdef AWQ_DIAG

@@ -227,26 +227,30 @@ __global__ __launch_bounds__(128) void awq_rowgroup_kernel(const void* __restric
     const uint32_t lim = (rem >> 32) ? 16u * (uint32_t)nch : min((uint32_t)rem, 16u * (uint32_t)nch);
     const __amdgpu_buffer_rsrc_t rw = rsrc((const char*)w + a0, lim);
     u4 vreg[4];                              // the 4-chunk stage's loads, reused by pass 2
-    if (__builtin_expect(16u * (uint32_t)nch <= lim, 1)) {
+    if (__builtin_expect(16u * (uint32_t)nch <= lim, 1) && ldsdma) {
+        // every 16-B chunk of the segment straight from memory into its stage slot (LDS-DMA,
+        // buffer_load_dwordx4 ... lds: no VGPR round trip, no LDS store instructions, every
+        // load in flight before one wait; round 4, profiles/round4/r4c: -2..5 % on whole-row
+        // tiles against the register stage).  Lane t of wave w writes slot base + 16 t, so a
+        // wave's loads go to its own 64-chunk window of each NT-chunk step; lanes past the
+        // segment are masked off (no write beyond the stage).
+        const int wbase = __builtin_amdgcn_readfirstlane(lane & ~63);
+        for (int c0 = 0; c0 < nch; c0 += NT) {
+            if (c0 + lane < nch)
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                    rw, (__attribute__((address_space(3))) void*)((char*)stage + 16 * (c0 + wbase)), 16,
+                    (uint32_t)(16 * (c0 + lane)), 0, 0, AWQ_LOAD_AUX);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else if (__builtin_expect(16u * (uint32_t)nch <= lim, 1)) {
+        // (diagnostics A/B, rg_ldsdma = 1: the round-3 register stage)
         // every 16-B load of the segment in flight before the first LDS store (a load ->
         // store loop waits out one memory round trip per load).  All 8 loads are issued
         // unconditionally: offsets past the segment fall outside the buffer range (lim) and
         // read zeros without a memory access, and no register needs a value on a skipped
         // path (conditional loads cost 28 v_mov per wave of phi copies); lanes past the end
         // store nothing
-        if (nch == 4 * NT && ldsdma) {
-            // (diagnostics A/B: the 4 chunks straight from memory into the stage, LDS-DMA —
-            //  no VGPR round trip, no LDS store instructions; pass 2 then reads the stage)
-            const char* src = (const char*)w + a0;
-            const int wbase = __builtin_amdgcn_readfirstlane(lane & ~63);
-#pragma unroll
-            for (int k = 0; k < 4; ++k)
-                __builtin_amdgcn_global_load_lds((const void*)(src + 16 * (NT * k + lane)),
-                                                 (__attribute__((address_space(3))) void*)((char*)stage +
-                                                                                          16 * (NT * k + wbase)),
-                                                 16, 0, 0);
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        } else if (nch == 4 * NT) {
+        if (nch == 4 * NT) {
             // (exactly 4 chunks per lane — a 4 096-element bf16 row on two waves: 4 loads
             //  and 4 unmasked stores, no range-checked dummy loads; the chunks stay in
             //  registers for pass 2, whose lane -> chunk map is the same)
@@ -729,8 +733,10 @@ hipError_t launch_rowgroup(const void* w, int dtype, int64_t rows, int64_t K, in
     const int64_t stage_el = tuning().rg_lds_full == 1 ? (int64_t)gpt * L : min((int64_t)gpt * L, K);
     const size_t lds = (size_t)((stage_el * es + 15) / 16 * 16 + 48);
     const bool p1c = tuning().rg_p1 == 2;   // pass 1 by groups (default) / evenly split runs (A/B)
-    const int ldsdma = tuning().rg_ldsdma == 1 ? 1 : 0;  // (A/B) the 4-chunk stage by LDS-DMA
-    const int p2reg = (tuning().rg_p2reg == 1 || ldsdma) ? 0 : 1;   // pass 2 from the stage's registers (A/B: 1 = off)
+    // the stage by LDS-DMA (default); diagnostics A/B: rg_ldsdma = 1 the round-3 register
+    // stage, whose 4-chunk case then feeds pass 2 from its registers unless rg_p2reg = 1
+    const int ldsdma = tuning().rg_ldsdma == 1 ? 0 : 1;
+    const int p2reg = (tuning().rg_p2reg == 1 || ldsdma) ? 0 : 1;
 #define AWQ_RG_GO(Fm, B, S, SP, P1, TQ)                                                                            \
     hipLaunchKernelGGL((awq_rowgroup_kernel<Fm, B, S, SP, P1, TQ>), grid, block, lds, stream, w, rows, K, L, lgP,  \
                        gpt, (uint32_t)tpr, G, C, 1.0f / (float)L, qweight, qzeros, scales, tensor_q, zeros, nan_code, \

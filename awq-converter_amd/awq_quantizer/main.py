@@ -820,6 +820,7 @@ def _device_worker(*args, **kwargs) -> None:
 
 def main(argv: Optional[List[str]] = None) -> int:
     logger = None
+    t_main = time.time()
     try:
         args = parse_args(argv)
         logger = get_logger(name="awq_quantizer", level=args.log_level, to_file=args.log_file is not None,
@@ -848,6 +849,7 @@ def main(argv: Optional[List[str]] = None) -> int:
             elif d == "cpu":
                 logger.info("Using CPU for quantization")
 
+        TIMINGS["devices_s"] = round(time.time() - t_main, 4)
         logger.info(f"Loading model from {args.model_id}")
         try:
             loader = load_model_from_hub(args.model_id, logger_level=args.log_level)
@@ -856,6 +858,7 @@ def main(argv: Optional[List[str]] = None) -> int:
             logger.error(f"Failed to load model: {e}")
             return 1
 
+        TIMINGS["index_s"] = round(time.time() - t_main - TIMINGS["devices_s"], 4)
         logger.info("Preparing tensors for quantization")
         start = time.time()
         ordered = select_tensors(index, logger)

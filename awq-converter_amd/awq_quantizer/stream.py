@@ -230,6 +230,7 @@ def quantize_stream_native(loader, infos, quantizer, device: str, readers: int, 
     torch.cuda.set_device(dev)
     quantizer.compute_device()
     quantizer._check_mode()
+    t_dev = time.perf_counter()
     gs, bits = quantizer.group_size, quantizer.bits
     scal = {"bits": torch.tensor(bits, dtype=torch.int32), "group_size": torch.tensor(gs, dtype=torch.int32),
             "symmetric": torch.tensor(bool(quantizer.symmetric), dtype=torch.bool)}
@@ -262,6 +263,7 @@ def quantize_stream_native(loader, infos, quantizer, device: str, readers: int, 
         else:
             rows = 1 if len(info.shape) <= 1 else info.shape[0]
             items.append((info, rows, info.numel // rows))
+    t_small = time.perf_counter()
     lays = [region_layout(info.shape, rows, K, gs, bits, packed) for info, rows, K in items]
     sizes = [s for _, s in lays]
     lib = _hip.load_library()
@@ -335,7 +337,9 @@ def quantize_stream_native(loader, infos, quantizer, device: str, readers: int, 
             it.host_out = hptr + hoffs[k]
         it.dev_gate, it.host_gate = dgates[k], hgates[k]
     tb = int(lib.awq_stream_table_bytes(slot))     # each slot: its table area, then its input
+    t_items = time.perf_counter()
     h_stage = pinned_bytes(nslots * (tb + slot))
+    t_hstage = time.perf_counter()
     d_stage = torch.empty(nslots * (tb + slot), dtype=torch.uint8, device=dev)
     compute = torch.cuda.current_stream(dev)
     h2d = torch.cuda.Stream(dev)
@@ -383,7 +387,10 @@ def quantize_stream_native(loader, infos, quantizer, device: str, readers: int, 
         compute.wait_stream(d2h)
     if timings is not None:
         st = {"engine": "native", "wall_s": round(time.perf_counter() - t_enter, 4),
-              "setup_s": round(t_run - t_enter, 4), "plan_s": round(t_plan - t_enter, 4),
+              "setup_s": round(t_run - t_enter, 4), "device_s": round(t_dev - t_enter, 4),
+              "small_s": round(t_small - t_dev, 4), "plan_s": round(t_plan - t_small, 4),
+              "items_s": round(t_items - t_host, 4), "alloc_host_stage_s": round(t_hstage - t_items, 4),
+              "streams_s": round(t_run - t_hstage, 4),
               "place_s": round(t_place - t_plan, 4), "alloc_dev_s": round(t_dev - t_place, 4),
               "alloc_host_out_s": round(t_host - t_dev, 4), "host_ring_MB": hcap >> 20, "dev_ring_MB": dcap >> 20,
               "host_wraps": int(any(hgates)), "dev_wraps": int(any(dgates)) and not keep_on_device,

@@ -21,10 +21,12 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cerrno>
 #include <cstdint>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 
 namespace {
@@ -158,6 +160,55 @@ bool write_all(int fd, std::vector<iovec>& iov) {
     return true;
 }
 
+// CRC-32 of A || B from crc(A), crc(B) and len(B): zlib's crc32_combine (the GF(2) operator
+// that appends len(B) zero bytes, by repeated squaring), so a record's pieces can be
+// checksummed by different threads
+uint32_t gf2_times(const uint32_t* mat, uint32_t vec) {
+    uint32_t sum = 0;
+    for (; vec; vec >>= 1, ++mat)
+        if (vec & 1) sum ^= *mat;
+    return sum;
+}
+void gf2_square(uint32_t* sq, const uint32_t* mat) {
+    for (int n = 0; n < 32; ++n) sq[n] = gf2_times(mat, mat[n]);
+}
+uint32_t crc32_combine(uint32_t crc1, uint32_t crc2, uint64_t len2) {
+    if (len2 == 0) return crc1;
+    uint32_t even[32], odd[32];
+    odd[0] = 0xEDB88320u;   // the operator for one zero bit
+    for (uint32_t n = 1, row = 1; n < 32; ++n, row <<= 1) odd[n] = row;
+    gf2_square(even, odd);   // two zero bits
+    gf2_square(odd, even);   // four
+    do {
+        gf2_square(even, odd);
+        if (len2 & 1) crc1 = gf2_times(even, crc1);
+        len2 >>= 1;
+        if (!len2) break;
+        gf2_square(odd, even);
+        if (len2 & 1) crc1 = gf2_times(odd, crc1);
+        len2 >>= 1;
+    } while (len2);
+    return crc1 ^ crc2;
+}
+
+bool pwrite_all(int fd, const void* data, size_t n, uint64_t off) {
+    const char* p = (const char*)data;
+    while (n > 0) {
+        const ssize_t w = pwrite(fd, p, n, (off_t)off);
+        if (w < 0) {
+            if (errno == EINTR) continue;
+            return false;
+        }
+        p += w;
+        n -= (size_t)w;
+        off += (uint64_t)w;
+    }
+    return true;
+}
+
+constexpr uint64_t kPiece = 8ull << 20;            // checksum + write unit of a large archive
+constexpr uint64_t kParallelBytes = 32ull << 20;   // archives with more data go to a thread team
+
 }  // namespace
 
 extern "C" {
@@ -197,19 +248,21 @@ int awq_write_pt(const char* path, const char* archive, const char* pkl, int64_t
     recs.push_back({a + "/version", "3\n", 2, 0, 0});
     recs.push_back({a + "/.data/serialization_id", serialization_id, 40, 0, 0});
     const bool fold = have_clmul();
-    // layout, CRCs and headers (local header + FB padding so the data start on 64 B)
+    // layout and headers (local header + FB padding so the data start on 64 B); the data
+    // descriptors carry the CRCs and follow once they are known
     std::vector<std::string> heads(recs.size());
     static const char kPad[64] = {'Z', 'Z', 'Z', 'Z', 'Z', 'Z', 'Z', 'Z', 'Z', 'Z', 'Z', 'Z', 'Z', 'Z', 'Z', 'Z',
                                   'Z', 'Z', 'Z', 'Z', 'Z', 'Z', 'Z', 'Z', 'Z', 'Z', 'Z', 'Z', 'Z', 'Z', 'Z', 'Z',
                                   'Z', 'Z', 'Z', 'Z', 'Z', 'Z', 'Z', 'Z', 'Z', 'Z', 'Z', 'Z', 'Z', 'Z', 'Z', 'Z',
                                   'Z', 'Z', 'Z', 'Z', 'Z', 'Z', 'Z', 'Z', 'Z', 'Z', 'Z', 'Z', 'Z', 'Z', 'Z', 'Z'};
     std::vector<std::string> descs(recs.size());
-    uint64_t off = 0;
+    std::vector<uint64_t> data_off(recs.size());
+    uint64_t off = 0, total_data = 0;
     const uint64_t kLim = 0xFFFFFFFFull;
+    constexpr uint64_t kDesc = 16;                 // data descriptor: signature, crc, 2 sizes
     for (size_t i = 0; i < recs.size(); ++i) {
         Rec& r = recs[i];
         if (r.size >= kLim) return 2;
-        r.crc = r.size ? crc32_of(0, r.data, (size_t)r.size, fold) : 0u;
         r.offset = off;
         const uint64_t pre = 30 + r.name.size() + 4;
         const uint32_t pad = (uint32_t)((64 - (off + pre) % 64) % 64);
@@ -229,13 +282,67 @@ int awq_write_pt(const char* path, const char* archive, const char* pkl, int64_t
         h += "FB";
         put16(h, pad);
         h.append(kPad, pad);
+        data_off[i] = off + h.size();
+        off += h.size() + r.size + kDesc;
+        total_data += r.size;
+        if (off >= kLim) return 2;
+    }
+    // the EOCD's entry counts are 16-bit: a larger archive needs ZIP64 (torch.save writes it)
+    if (recs.size() >= 0xFFFF) return 2;
+    const int fd = open(path, O_WRONLY | O_CREAT | O_TRUNC | O_CLOEXEC, 0644);
+    if (fd < 0) return 1;
+    // CRCs (and, for a large archive, the data itself): a large archive's records are cut
+    // into 8 MiB pieces that a team of threads checksums and writes at their final offsets
+    // (pwrite), the pieces' CRCs combined per record — one chunk of a few GB (the reference
+    // format's int32 tensor_q) no longer serialises on one thread (round 4: it stalled the
+    // CLI pipeline's host-ring reuse)
+    const bool parallel = total_data >= kParallelBytes;
+    bool io_ok = true;
+    int io_errno = 0;
+    if (parallel) {
+        struct Piece {
+            size_t rec;
+            uint64_t at, len;
+            uint32_t crc;
+        };
+        std::vector<Piece> pieces;
+        for (size_t i = 0; i < recs.size(); ++i)
+            for (uint64_t a = 0; a < recs[i].size; a += kPiece)
+                pieces.push_back({i, a, std::min(kPiece, recs[i].size - a), 0u});
+        const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+        const int team = (int)std::min<uint64_t>({8ull, (uint64_t)hw, (total_data + kParallelBytes - 1) / kParallelBytes * 2,
+                                                  (uint64_t)pieces.size()});
+        std::atomic<size_t> next{0};
+        std::atomic<bool> failed{false};
+        std::atomic<int> err{0};
+        auto work = [&]() {
+            for (size_t k; (k = next.fetch_add(1)) < pieces.size() && !failed.load();) {
+                Piece& pc = pieces[k];
+                const unsigned char* src = (const unsigned char*)recs[pc.rec].data + pc.at;
+                pc.crc = crc32_of(0, src, (size_t)pc.len, fold);
+                if (!pwrite_all(fd, src, (size_t)pc.len, data_off[pc.rec] + pc.at)) {
+                    err.store(errno);
+                    failed.store(true);
+                }
+            }
+        };
+        std::vector<std::thread> th;
+        for (int t = 1; t < team; ++t) th.emplace_back(work);
+        work();
+        for (auto& t : th) t.join();
+        io_ok = !failed.load();
+        io_errno = err.load();
+        for (Rec& r : recs) r.crc = 0;
+        for (const Piece& pc : pieces) recs[pc.rec].crc = crc32_combine(recs[pc.rec].crc, pc.crc, pc.len);
+    } else {
+        for (Rec& r : recs) r.crc = r.size ? crc32_of(0, r.data, (size_t)r.size, fold) : 0u;
+    }
+    for (size_t i = 0; i < recs.size(); ++i) {
         std::string& d = descs[i];
         put32(d, 0x08074b50u);
-        put32(d, r.crc);
-        put32(d, (uint32_t)r.size);
-        put32(d, (uint32_t)r.size);
-        off += h.size() + r.size + d.size();
-        if (off >= kLim) return 2;
+        put32(d, recs[i].crc);
+        put32(d, (uint32_t)recs[i].size);
+        put32(d, (uint32_t)recs[i].size);
     }
     std::string cd;
     for (const Rec& r : recs) {
@@ -258,8 +365,11 @@ int awq_write_pt(const char* path, const char* archive, const char* pkl, int64_t
         put32(cd, (uint32_t)r.offset);
         cd += r.name;
     }
-    // the EOCD's entry counts are 16-bit: a larger archive needs ZIP64 (torch.save writes it)
-    if (off + cd.size() + 22 >= kLim || recs.size() >= 0xFFFF) return 2;
+    if (off + cd.size() + 22 >= kLim) {
+        close(fd);
+        unlink(path);
+        return 2;
+    }
     std::string eocd;
     put32(eocd, 0x06054b50u);
     put16(eocd, 0);
@@ -269,21 +379,29 @@ int awq_write_pt(const char* path, const char* archive, const char* pkl, int64_t
     put32(eocd, (uint32_t)cd.size());
     put32(eocd, (uint32_t)off);
     put16(eocd, 0);
-    std::vector<iovec> iov;
-    iov.reserve(recs.size() * 3 + 2);
-    for (size_t i = 0; i < recs.size(); ++i) {
-        iov.push_back({(void*)heads[i].data(), heads[i].size()});
-        if (recs[i].size) iov.push_back({const_cast<void*>(recs[i].data), (size_t)recs[i].size});
-        iov.push_back({(void*)descs[i].data(), descs[i].size()});
+    if (io_ok && parallel) {
+        // the data are in place: headers, descriptors, central directory, EOCD at their offsets
+        for (size_t i = 0; i < recs.size() && io_ok; ++i)
+            io_ok = pwrite_all(fd, heads[i].data(), heads[i].size(), recs[i].offset) &&
+                    pwrite_all(fd, descs[i].data(), descs[i].size(), data_off[i] + recs[i].size);
+        io_ok = io_ok && pwrite_all(fd, cd.data(), cd.size(), off) &&
+                pwrite_all(fd, eocd.data(), eocd.size(), off + cd.size());
+        if (!io_ok) io_errno = errno;
+    } else if (io_ok) {
+        std::vector<iovec> iov;
+        iov.reserve(recs.size() * 3 + 2);
+        for (size_t i = 0; i < recs.size(); ++i) {
+            iov.push_back({(void*)heads[i].data(), heads[i].size()});
+            if (recs[i].size) iov.push_back({const_cast<void*>(recs[i].data), (size_t)recs[i].size});
+            iov.push_back({(void*)descs[i].data(), descs[i].size()});
+        }
+        iov.push_back({(void*)cd.data(), cd.size()});
+        iov.push_back({(void*)eocd.data(), eocd.size()});
+        io_ok = write_all(fd, iov);
+        if (!io_ok) io_errno = errno;
     }
-    iov.push_back({(void*)cd.data(), cd.size()});
-    iov.push_back({(void*)eocd.data(), eocd.size()});
-    const int fd = open(path, O_WRONLY | O_CREAT | O_TRUNC | O_CLOEXEC, 0644);
-    if (fd < 0) return 1;
-    const bool ok = write_all(fd, iov);
-    const int e = errno;
-    if (close(fd) != 0 || !ok) {
-        errno = ok ? errno : e;
+    if (close(fd) != 0 || !io_ok) {
+        errno = io_ok ? errno : io_errno;
         return 1;
     }
     return 0;

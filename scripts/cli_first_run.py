@@ -26,7 +26,7 @@ import time
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def child(argv_json, t_spawn):
+def child(argv_json, t_spawn, trace="0"):
     t0 = time.time()
     sys.path[:0] = [ROOT, os.path.join(ROOT, "awq-converter_amd")]
     import torch
@@ -39,6 +39,8 @@ def child(argv_json, t_spawn):
     from awq_quantizer import _hip
     _hip.load_library()
     t3 = time.time()
+    if trace == "1":
+        cli.STREAM_OPTS["trace"] = 1
     rc = cli.main(json.loads(argv_json))
     t4 = time.time()
     ph = {k: v for k, v in cli.TIMINGS.items()}
@@ -61,10 +63,11 @@ def main():
     ap.add_argument("--formats", default="packed,reference")
     ap.add_argument("--runs", type=int, default=2)
     ap.add_argument("--workdir", default=None)
-    ap.add_argument("--child", nargs=2)
+    ap.add_argument("--trace", action="store_true", help="per-batch pipeline trace in the phases")
+    ap.add_argument("--child", nargs=3)
     a = ap.parse_args()
     if a.child:
-        child(a.child[0], float(a.child[1]))
+        child(a.child[0], float(a.child[1]), a.child[2])
         return
     sys.path[:0] = [ROOT, os.path.join(ROOT, "scripts")]
     import cli_bench
@@ -82,7 +85,8 @@ def main():
             out = os.path.join(work, f"out_{fmt}_{r}")
             argv = ["--model_id", model, "--output_dir", out, "--log_level", "WARNING", "--output_format", fmt]
             t_spawn = time.time()
-            p = subprocess.run([sys.executable, os.path.abspath(__file__), "--child", json.dumps(argv), repr(t_spawn)],
+            p = subprocess.run([sys.executable, os.path.abspath(__file__), "--child", json.dumps(argv), repr(t_spawn),
+                                "1" if a.trace else "0"],
                                capture_output=True, text=True, timeout=600, env=env)
             wall = time.time() - t_spawn
             res = [ln[7:] for ln in p.stdout.splitlines() if ln.startswith("RESULT ")]

@@ -136,3 +136,30 @@ def test_save_leaves_python_rng_alone(tmp_path):
     random.seed(1234)
     ptfile.save(_chunk(), str(tmp_path / "model_chunk_0000.pt"))
     assert random.random() == want
+
+
+def test_large_archive_parallel_pieces(tmp_path):
+    """An archive with > 32 MiB of data is checksummed and written by a thread team in 8 MiB
+    pieces at their final offsets (the pieces' CRC-32s combined per record): the file is
+    the same archive torch.load reads back, every record's CRC valid."""
+    g = torch.Generator().manual_seed(5)
+    d = {"big": {"qweight": torch.randint(-2 ** 31, 2 ** 31 - 1, (5000, 2003), generator=g, dtype=torch.int64)
+                 .to(torch.int32),                                   # 40 MB: 5 pieces, the last ragged
+                 "scales": torch.randn(5000, 17, generator=g).half(), "bits": torch.tensor(4, dtype=torch.int32)},
+         "mid": {"tensor_q": torch.randint(0, 16, (3001, 1000), generator=g, dtype=torch.int32)},
+         "empty": {"e": torch.empty(0, dtype=torch.int32)}}
+    p = str(tmp_path / "model_chunk_0001.pt")
+    ptfile.save(d, p)
+    z = zipfile.ZipFile(p)
+    assert z.testzip() is None
+    names = [i.filename for i in z.infolist()]
+    torch.save(d, str(tmp_path / "ref.pt"))
+    ref = [i.filename.replace("ref/", "model_chunk_0001/", 1) for i in zipfile.ZipFile(str(tmp_path / "ref.pt")).infolist()]
+    assert names == ref
+    _assert_same(torch.load(p, weights_only=True), d)
+    for i in z.infolist():
+        if "/data/" in i.filename:
+            with open(p, "rb") as f:
+                f.seek(i.header_offset + 26)
+                nlen, xlen = int.from_bytes(f.read(2), "little"), int.from_bytes(f.read(2), "little")
+            assert (i.header_offset + 30 + nlen + xlen) % 64 == 0

@@ -172,7 +172,7 @@ __device__ __forceinline__ void rg_reduce(int& smax, uint32_t& umax, uint32_t& u
 }
 
 // LDS: the segment's stage (dynamic, sized by the launch to the tile: 1.6-8 KiB) + 1.3 KiB
-template <typename F, int BITS, bool SYM, int SPLIT, bool P1C, bool TQ>
+template <typename F, int BITS, bool SYM, int SPLIT, bool P1C, bool TQ, bool PERSIST = false>
 __global__ __launch_bounds__(128) void awq_rowgroup_kernel(const void* __restrict__ w, int64_t rows, int64_t K,
                                                              int64_t L, int lgP, int GPT, uint32_t tiles_per_row,
                                                              int64_t G, int C, float invL,
@@ -180,7 +180,7 @@ __global__ __launch_bounds__(128) void awq_rowgroup_kernel(const void* __restric
                                                              uint16_t* __restrict__ scales,
                                                              int32_t* __restrict__ tensor_q, int32_t* __restrict__ zeros,
                                                              uint32_t nan_code, int lgP_last, int C_last, int p2reg,
-                                                             int ldsdma) {
+                                                             int ldsdma, int persist) {
     typedef RgSlot<F> SL;
     typedef typename SL::T S;
     constexpr int QMIN = SYM ? -(1 << (BITS - 1)) : 0;
@@ -188,11 +188,16 @@ __global__ __launch_bounds__(128) void awq_rowgroup_kernel(const void* __restric
     constexpr int PER = 32 / BITS;             // elements (and groups) per packed word
     constexpr uint32_t NANF = (uint32_t)(0u - (uint32_t)QMIN) & MASK;   // field of INT32_MIN - qmin
     extern __shared__ __attribute__((aligned(16))) unsigned char rg_lds[];
-    S* stage = (S*)rg_lds;                              // rg_stage_bytes(): the segment + its alignment skew
+    // rg_stage_bytes(): the segment + its alignment skew; a persistent workgroup (persist > 0:
+    // the stage's size in bytes) has two, the next tile's segment landing in one by LDS-DMA
+    // while the current tile is computed from the other
     __shared__ __attribute__((aligned(16))) uint32_t zst[64];
     __shared__ float4 prm[64];                          // per group: r, z, s, special
-    __shared__ int not_plain;                           // a group of the tile needs the full quotient
-    __shared__ int any_special;                         // a group of the tile has scale 0 / inf / NaN
+    __shared__ int not_plain_a[2];                      // a group of the tile needs the full quotient
+    __shared__ int any_special_a[2];                    // a group of the tile has scale 0 / inf / NaN
+                                                        // (by tile parity: a persistent workgroup
+                                                        //  resets the next tile's while the current
+                                                        //  tile's are still read)
     __shared__ int acc_smax[P1C ? 64 : 1];              // P1C: per-group raw-bits reductions
     __shared__ uint32_t acc_umax[P1C ? 64 : 1], acc_umin[P1C ? 64 : 1];
     // one tile per workgroup of 1 or 2 waves (host-chosen: two waves share a large tile's LDS
@@ -200,7 +205,21 @@ __global__ __launch_bounds__(128) void awq_rowgroup_kernel(const void* __restric
     const int lane = threadIdx.x, NT = blockDim.x;
     // (host-side G, C, log2 P and a 32-bit tile split: 64-bit divisions per wave on the
     //  CU's shared scalar unit were a visible part of the per-tile cost)
-    const uint32_t tile = blockIdx.x;   // (an XCD-contiguous tile order measured no different: r2z3)
+    const int lgP_full = lgP, C_full = C;
+    const uint32_t ntiles = (uint32_t)rows * tiles_per_row;
+    // (an XCD-contiguous tile order measured no different: r2z3)
+    int it = 0;
+    if constexpr (!PERSIST) persist = 0;   // (the shipped kernels: one tile, straight-line code)
+#ifndef AWQ_DIAG
+    ldsdma = 1;                            // the shipped library: LDS-DMA stage, no A/B switches
+    p2reg = 0;
+#endif
+    for (uint32_t tile = blockIdx.x;; ++it) {
+    lgP = lgP_full;
+    C = C_full;
+    S* stage = (S*)(rg_lds + ((persist && (it & 1)) ? persist : 0));
+    int& not_plain = not_plain_a[it & 1];
+    int& any_special = any_special_a[it & 1];
     // (whole-row tiles, the common case, need no division: the scalar unit has no divider)
     const uint32_t r32 = tiles_per_row == 1 ? tile : tile / tiles_per_row;
     const int64_t r = r32;
@@ -227,7 +246,21 @@ __global__ __launch_bounds__(128) void awq_rowgroup_kernel(const void* __restric
     const uint32_t lim = (rem >> 32) ? 16u * (uint32_t)nch : min((uint32_t)rem, 16u * (uint32_t)nch);
     const __amdgpu_buffer_rsrc_t rw = rsrc((const char*)w + a0, lim);
     u4 vreg[4];                              // the 4-chunk stage's loads, reused by pass 2
-    if (__builtin_expect(16u * (uint32_t)nch <= lim, 1) && ldsdma) {
+    // LDS-DMA of a segment's chunks into `stg` (lanes past the segment masked off)
+    auto dma = [&](const __amdgpu_buffer_rsrc_t& src, int nchunks, S* stg) {
+        const int wbase = __builtin_amdgcn_readfirstlane(lane & ~63);
+        for (int c0 = 0; c0 < nchunks; c0 += NT) {
+            if (c0 + lane < nchunks)
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                    src, (__attribute__((address_space(3))) void*)((char*)stg + 16 * (c0 + wbase)), 16,
+                    (uint32_t)(16 * (c0 + lane)), 0, 0, AWQ_LOAD_AUX);
+        }
+    };
+    if (persist) {
+        // (the host admits only tensors of whole 16-B chunks: no tile straddles the end)
+        if (it == 0) dma(rw, nch, stage);    // the first tile now; later ones were prefetched
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else if (__builtin_expect(16u * (uint32_t)nch <= lim, 1) && ldsdma) {
         // every 16-B chunk of the segment straight from memory into its stage slot (LDS-DMA,
         // buffer_load_dwordx4 ... lds: no VGPR round trip, no LDS store instructions, every
         // load in flight before one wait; round 4, profiles/round4/r4c: -2..5 % on whole-row
@@ -297,6 +330,20 @@ __global__ __launch_bounds__(128) void awq_rowgroup_kernel(const void* __restric
         }
     }
     __syncthreads();
+    if (persist && tile + gridDim.x < ntiles) {
+        // every wave is past its previous tile, so the other stage is free: prefetch the next
+        // tile's segment into it while this one is computed
+        const uint32_t t2 = tile + gridDim.x;
+        const uint32_t r2 = tiles_per_row == 1 ? t2 : t2 / tiles_per_row;
+        const int g2 = (int)(t2 - r2 * tiles_per_row) * GPT;
+        const int ng2 = min(GPT, (int)G - g2);
+        const int kb2 = g2 * L32g, n2 = min((g2 + ng2) * L32g, K32) - kb2;
+        const uint64_t b2 = ((uint64_t)r2 * (uint64_t)K32 + (uint64_t)kb2) * F::kBytes;
+        const uint64_t a2 = b2 & ~(uint64_t)15;
+        const int nch2 = ((int)(b2 - a2) + n2 * F::kBytes + 15) >> 4;
+        dma(rsrc((const char*)w + a2, 16u * (uint32_t)nch2), nch2,
+            (S*)(rg_lds + ((it & 1) ? 0 : persist)));
+    }
     if constexpr (P1C) {
         // ---- pass 1, lanes split evenly over the tile's groups: Q = NT / ng lanes per group
         //      (any count — not only a power of two; 3 for 41 groups of a 128-lane tile where
@@ -655,6 +702,10 @@ __global__ __launch_bounds__(128) void awq_rowgroup_kernel(const void* __restric
             qzeros[r * zpr + g0 / PER + lane] = (int32_t)word;
         }
     }
+    if constexpr (!PERSIST) break;
+    tile += gridDim.x;
+    if (tile >= ntiles) break;
+    }   // tiles (one, unless persistent)
 }
 
 }  // namespace
@@ -737,10 +788,38 @@ hipError_t launch_rowgroup(const void* w, int dtype, int64_t rows, int64_t K, in
     // stage, whose 4-chunk case then feeds pass 2 from its registers unless rg_p2reg = 1
     const int ldsdma = tuning().rg_ldsdma == 1 ? 0 : 1;
     const int p2reg = (tuning().rg_p2reg == 1 || ldsdma) ? 0 : 1;
+    // (diagnostics A/B, rg_persist = 1) persistent workgroups with two stages: each walks
+    // tiles t, t + grid, ..., the next tile's segment landing by LDS-DMA while the current
+    // one is computed; grid = every workgroup the LDS admits, evened out so each takes the
+    // same tile count.  Tensors of whole 16-B chunks only (no straddling last chunk).
+    int persist = 0;
+    dim3 grid_use = grid;
+    size_t lds_use = lds;
+    if (tuning().rg_persist == 1 && ldsdma && !tensor_q && !p1c &&
+        ((uint64_t)rows * (uint64_t)K * (uint64_t)es) % 16 == 0) {
+        const size_t st = (lds + 15) / 16 * 16;
+        lds_use = 2 * st;
+        persist = (int)st;
+        const int per_cu = (int)std::min<int64_t>(32 / (nt / 64), 163840 / (int64_t)(lds_use + 1536));
+        const int64_t ntl = rows * tpr;
+        int64_t g = std::min<int64_t>(ntl, 256LL * std::max(1, per_cu));
+        const int64_t tpw = (ntl + g - 1) / g;
+        g = (ntl + tpw - 1) / tpw;
+        grid_use = dim3((unsigned)g);
+    }
+#define AWQ_RG_GO1(Fm, B, S, SP, P1, TQ, PE)                                                                       \
+    hipLaunchKernelGGL((awq_rowgroup_kernel<Fm, B, S, SP, P1, TQ, PE>), grid_use, block, lds_use, stream, w, rows, K, \
+                       L, lgP, gpt, (uint32_t)tpr, G, C, 1.0f / (float)L, qweight, qzeros, scales, tensor_q, zeros, \
+                       nan_code, lgP_last, C_last, p2reg, ldsdma, persist)
+#ifdef AWQ_DIAG
 #define AWQ_RG_GO(Fm, B, S, SP, P1, TQ)                                                                            \
-    hipLaunchKernelGGL((awq_rowgroup_kernel<Fm, B, S, SP, P1, TQ>), grid, block, lds, stream, w, rows, K, L, lgP,  \
-                       gpt, (uint32_t)tpr, G, C, 1.0f / (float)L, qweight, qzeros, scales, tensor_q, zeros, nan_code, \
-                       lgP_last, C_last, p2reg, ldsdma)
+    do {                                                                                                           \
+        if (persist && !P1 && !TQ) AWQ_RG_GO1(Fm, B, S, SP, P1, TQ, true);                                          \
+        else AWQ_RG_GO1(Fm, B, S, SP, P1, TQ, false);                                                               \
+    } while (0)
+#else
+#define AWQ_RG_GO(Fm, B, S, SP, P1, TQ) AWQ_RG_GO1(Fm, B, S, SP, P1, TQ, false)
+#endif
     // (the pass-1 A/B variant is built for the packed outputs only; with tensor_q it takes the default)
 #ifdef AWQ_DIAG
 #define AWQ_RG_SPLIT(Fm, B, S, SP)                                                                                 \
@@ -779,6 +858,7 @@ hipError_t launch_rowgroup(const void* w, int dtype, int64_t rows, int64_t K, in
 #undef AWQ_RG
 #undef AWQ_RG_SPLIT
 #undef AWQ_RG_GO
+#undef AWQ_RG_GO1
     return hipPeekAtLastError();
 }
 

@@ -354,10 +354,69 @@ __device__ __forceinline__ void pack8_cvt(const float (&u)[8], uint32_t& w0, uin
     }
 }
 
+// fp16 weights whose scales are all < 14 (the plain quotient, FmtF16::plain_ok): the field
+// chain on packed f16 pairs (round 4).  t = RN_f16(x * r) is one v_cvt_pk_f16_f32 (RNE) per
+// pair of f32 products, u = RN_f16(t + z) one v_pk_add_f16 — the reference's two roundings
+// in the input dtype (awq.py:245-248) — then the clamp (v_pk_max / min_f16) and the round to
+// an integer by adding 1024: at 2^10 the f16 ulp is 1, so the sum's RNE is 1024 + rint(u)
+// and the half's bits are 0x6400 + field (rint(clamp(u)) == clamp(rint(u)) for integer
+// bounds; 1024 + 255 < 2048 covers 8 bits).  Symmetric: clamp(t, -HALF, HALF - 1) + 1024 +
+// HALF, whose RNE is 1024 + HALF + rint(t) (an even integer offset keeps ties to even) —
+// the field rint(t) + HALF.  No NaN or inf reaches here (such groups are special).  The
+// fields' low bytes are gathered by v_perm_b32 and, at 4 bits, folded into nibbles: ≈35
+// VALU per 8 elements against ≈64 for the per-element f32 chain + v_cvt_pk_u8_f32.
+typedef _Float16 h2v __attribute__((ext_vector_type(2)));
+template <int BITS, bool SYM>
+__device__ __forceinline__ void pack8_f16_plain(const uint32_t (&d)[4], const float (&r)[8], const float (&z)[8],
+                                                uint32_t& w0, uint32_t& w1) {
+    constexpr _Float16 HALF = (_Float16)(1 << (BITS - 1));
+    constexpr _Float16 QMAX = (_Float16)((1 << BITS) - 1);
+    uint32_t P[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const float x0 = (float)__builtin_bit_cast(_Float16, (uint16_t)(d[i] & 0xFFFFu));
+        const float x1 = (float)__builtin_bit_cast(_Float16, (uint16_t)(d[i] >> 16));
+        const float p0 = opaque(x0 * r[2 * i]), p1 = opaque(x1 * r[2 * i + 1]);   // f32 products
+        const h2v t = __builtin_convertvector((f2){p0, p1}, h2v);                  // RN_f16 (RNE)
+        h2v u;
+        if (SYM) {
+            u = __builtin_elementwise_min(__builtin_elementwise_max(t, (h2v){-HALF, -HALF}),
+                                          (h2v){HALF - (_Float16)1, HALF - (_Float16)1});
+            u = u + (h2v){(_Float16)1024 + HALF, (_Float16)1024 + HALF};
+        } else {
+            u = t + (h2v){(_Float16)z[2 * i], (_Float16)z[2 * i + 1]};             // RN_f16(t + z)
+            u = __builtin_elementwise_min(__builtin_elementwise_max(u, (h2v){0, 0}), (h2v){QMAX, QMAX});
+            u = u + (h2v){(_Float16)1024, (_Float16)1024};
+        }
+        P[i] = __builtin_bit_cast(uint32_t, u);
+    }
+    // bytes [q0 q1 q2 q3], [q4 q5 q6 q7] (each half's low byte)
+    const uint32_t G0 = __builtin_amdgcn_perm(P[1], P[0], 0x06040200u);
+    const uint32_t G1 = __builtin_amdgcn_perm(P[3], P[2], 0x06040200u);
+    if (BITS == 8) {
+        w0 = G0;
+        w1 = G1;
+    } else {
+        const uint32_t t0 = G0 | (G0 >> 4), t1 = G1 | (G1 >> 4);   // bytes 0 / 2: q0 | q1 << 4, ...
+        w0 = __builtin_amdgcn_perm(t1, t0, 0x06040200u);
+        w1 = 0;
+    }
+}
+
 // Quantize the 8 values of one lane (awq.py:245-248) for a group with a positive finite
 // scale and pack them: 4-bit -> w.x, 8-bit -> (w.x, w.y).  Field value = q - qmin.
 template <typename F, int BITS, bool SYM, bool PLAIN = false>
 __device__ __forceinline__ u2v quant8_fast(const Chunk<F::NW>& v, float r, float z, float s) {
+    if constexpr (std::is_same<F, FmtF16>::value && PLAIN) {
+        const uint32_t d[4] = {v.w[0].x, v.w[0].y, v.w[0].z, v.w[0].w};
+        const float rr[8] = {r, r, r, r, r, r, r, r}, zz[8] = {z, z, z, z, z, z, z, z};
+        uint32_t w0, w1;
+        pack8_f16_plain<BITS, SYM>(d, rr, zz, w0, w1);
+        u2v w;
+        w.x = w0;
+        w.y = w1;
+        return w;
+    }
     constexpr float HALF = (float)(1 << (BITS - 1));
     const float zf = F::as_fmt(z);
     float q[8];   // the field before rounding: clamp + RNE are the pack's v_cvt_pk_u8_f32

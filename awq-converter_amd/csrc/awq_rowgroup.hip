@@ -526,9 +526,11 @@ __global__ __launch_bounds__(128) void awq_rowgroup_kernel(const void* __restric
         const int e0c = 8 * c;
         const bool tail = !FULL && e0c + 8 > n_el;        // the row's last, partial chunk
         float x[8];
+        u4 vraw = {0u, 0u, 0u, 0u};                       // (fp16 packed chain: the raw pairs)
         if constexpr (ALIGNED) {                          // 16-B aligned chunk (K % 8 == 0 rows)
             // (from the stage's registers when given; past n_el: the stage's slack)
             const u4 v0 = (F::kBytes == 2 && rv) ? *rv : *(const u4*)(stage + e0c);
+            vraw = v0;
             if constexpr (F::kBytes == 2) {
 #pragma unroll
                 for (int i = 0; i < 4; ++i) {
@@ -591,6 +593,13 @@ __global__ __launch_bounds__(128) void awq_rowgroup_kernel(const void* __restric
         }
         int32_t qv[8];                                    // q (reference value), INT32_MIN for NaN
         uint32_t word0 = 0, word1 = 0;
+        if constexpr (std::is_same<F, FmtF16>::value && PLAIN && ALIGNED && !TQ) {
+            if (__builtin_expect(!spec && !tail, 1)) {    // fp16: the packed-pair chain
+                const uint32_t d[4] = {vraw.x, vraw.y, vraw.z, vraw.w};
+                pack8_f16_plain<BITS, SYM>(d, rr, zz, word0, word1);
+                goto store;
+            }
+        }
         if (__builtin_expect(!spec, 1)) {
             float q[8];
             if constexpr (std::is_same<F, FmtBF16>::value) {
@@ -629,6 +638,7 @@ __global__ __launch_bounds__(128) void awq_rowgroup_kernel(const void* __restric
                 else word1 |= f << (8 * (i - 4));
             }
         }
+    store:
         if (qdst) {
             if (BITS == 4) {
                 qdst[c] = (int32_t)word0;

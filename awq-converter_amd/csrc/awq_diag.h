@@ -39,7 +39,6 @@ typedef struct awq_tuning {
                                 1 the round-3 register stage (loads to VGPRs, LDS stores) */
     int32_t rg_p2reg;        /* with rg_ldsdma = 1: pass 2 of a 4-chunk stage from the stage's
                                 registers (0) or from LDS (1) */
-    int32_t rg_persist;      /* row-segment: 1 = persistent workgroups with a double LDS-DMA stage */
 } awq_tuning;
 
 #ifdef AWQ_DIAG

@@ -160,17 +160,15 @@ def test_rowgroup_whole_row_tiles(dtype, K, gs):
     _assert_parity(specials(rand((24, K), gs, 1.0), 3).to(dtype), gs, 4, False)
 
 
-@pytest.mark.parametrize("tun", [{"rg_ldsdma": 1}, {"rg_ldsdma": 1, "rg_p2reg": 1}, {"rg_persist": 1}],
-                         ids=lambda t: "_".join(t))
+@pytest.mark.parametrize("tun", [{"rg_ldsdma": 1}, {"rg_ldsdma": 1, "rg_p2reg": 1}], ids=lambda t: "_".join(t))
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16, torch.float32], ids=str)
 @pytest.mark.parametrize("K,gs", [(4096, 100), (4096, 48), (4096, 200), (3000, 100), (14336, 100), (1000, 60),
                                   (203, 50)], ids=str)
 def test_rowgroup_stage_variants_same_bits(dtype, K, gs, tun):
     """The LDS-DMA stage (the default) gives the bits of the round-3 register stage
     (diagnostics build, rg_ldsdma = 1), whose 4-chunk case feeds pass 2 from registers or
-    (rg_p2reg = 1) from LDS, and of persistent workgroups with a double stage (rg_persist =
-    1); whole-row, one-wave and partial tiles, the tensor's last bytes (K = 203), special
-    values."""
+    (rg_p2reg = 1) from LDS; whole-row, one-wave and partial tiles, the tensor's last bytes
+    (K = 203), special values."""
     if dtype == torch.float32 and gs > 256:
         pytest.skip("fp32 row segments take group sizes <= 256")
     from awq_quantizer import _hip

@@ -14,12 +14,10 @@ from typing import Optional
 
 import torch
 
-LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib")
-LIB_PATH = os.path.join(LIB_DIR, "libawq_hip.so")
+from ._early import ABI_VERSION, LIB_DIR, LIB_PATH
 # diagnostics build (`make -C awq-converter_amd/csrc diag`: -DAWQ_DIAG, awq_set_tuning + the A/B
 # kernel variants): loaded only by tuning() below and by scripts/, never by the product path
 DIAG_LIB_PATH = os.path.join(LIB_DIR, "libawq_hip_diag.so")
-ABI_VERSION = 13
 Q_SMALL_TENSOR = 1      # include/awq_hip.h AWQ_Q_SMALL_TENSOR
 
 AWQ_DTYPE = {torch.bfloat16: 0, torch.float16: 1, torch.float32: 2, torch.float64: 3}
@@ -64,7 +62,7 @@ class StreamStats(ctypes.Structure):
     """Mirror of awq_stream_stats (include/awq_hip.h)."""
     _fields_ = [("batches", _I64), ("pieces", _I64), ("bytes_read", _I64), ("wall_s", ctypes.c_double),
                 ("read_busy_s", ctypes.c_double), ("wait_read_s", ctypes.c_double), ("wait_slot_s", ctypes.c_double),
-                ("wait_release_s", ctypes.c_double)]
+                ("wait_release_s", ctypes.c_double), ("prepare_s", ctypes.c_double)]
 
 
 assert ctypes.sizeof(StreamItem) == 128 and ctypes.sizeof(StreamConfig) == 96
@@ -112,6 +110,8 @@ SIGNATURES = {
     "awq_stream_plan": (_I64, [ctypes.POINTER(StreamItem), _I32, ctypes.POINTER(StreamConfig),
                                ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int32)]),
     "awq_stream_release": (_I32, [_P, _I32]),
+    "awq_runtime_warmup": (_I32, [_I32]),
+    "awq_runtime_warmup_wait": (_I32, [_I32, ctypes.POINTER(ctypes.c_double)]),
     "awq_stream_wait": (_I32, [_P, _I64, ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int32)]),
     "awq_stream_end": (_I32, [_P, ctypes.POINTER(StreamStats)]),
     "awq_act_stats": (_I32, [_P, _I32, _I64, _I64, _P, _P, _P, _P]),

@@ -37,9 +37,19 @@ from collections import deque
 from concurrent.futures import ThreadPoolExecutor
 from typing import Callable, Dict, List, Optional, Tuple
 
+_T_MODULE = time.time()
+if __name__ == "__main__":
+    # the program itself (`python -m awq_quantizer.main`): HIP's first-use work starts on a
+    # native thread now and overlaps `import torch` (~1.5 s); see _early.py
+    from awq_quantizer import _early
+    _early.start(sys.argv[1:])
+
 import torch
 
+_IMPORT_TORCH_S = time.time() - _T_MODULE
+
 from . import ptfile
+from .stream import device_name, start_warmup
 from .model_loading import TensorInfo, load_model_from_hub
 from .quantization.awq import AWQQuantizer
 from .utils.logger import get_logger
@@ -115,7 +125,7 @@ def get_available_gpus(logger=None) -> List[str]:
     devs = []
     for i in range(torch.cuda.device_count()):
         if logger:
-            logger.info(f"Found CUDA device {i}: {torch.cuda.get_device_name(i)}")
+            logger.info(f"Found CUDA device {i}: {device_name(i)}")
         devs.append(f"cuda:{i}")
     return devs
 
@@ -840,7 +850,7 @@ def main(argv: Optional[List[str]] = None) -> int:
             if d.startswith("cuda") and torch.cuda.is_available():
                 idx = int(d.split(":")[1]) if ":" in d else 0
                 total, free = get_device_memory_info(idx)
-                logger.info(f"Using GPU {d}: {torch.cuda.get_device_name(idx)}")
+                logger.info(f"Using GPU {d}: {device_name(idx)}")
                 logger.info(f"  Total memory: {total:.2f} GB")
                 logger.info(f"  Free memory: {free:.2f} GB")
             elif d.startswith("cuda"):
@@ -849,7 +859,11 @@ def main(argv: Optional[List[str]] = None) -> int:
             elif d == "cpu":
                 logger.info("Using CPU for quantization")
 
+        from . import distributed as D
+        if len(devices) == 1 and D.env_world()[2] <= 1:
+            start_warmup(devices[0])    # HIP's first-use costs overlap the index and planning below
         TIMINGS["devices_s"] = round(time.time() - t_main, 4)
+        TIMINGS["module_import_torch_s"] = round(_IMPORT_TORCH_S, 4)
         logger.info(f"Loading model from {args.model_id}")
         try:
             loader = load_model_from_hub(args.model_id, logger_level=args.log_level)
@@ -950,6 +964,8 @@ def main(argv: Optional[List[str]] = None) -> int:
                                          "write_s_max": round(max(e - b for _, b, e in writer.times), 4),
                                          "last_submit_to_end_s": round(max(e for _, _, e in writer.times)
                                                                        - max(a for a, _, _ in writer.times), 4)}
+                    if STREAM_OPTS.get("trace"):   # per chunk: submitted, started, ended (s after `start`)
+                        TIMINGS["writer"]["trace"] = [tuple(round(v - start, 4) for v in t) for t in writer.times]
             else:
                 save_model_in_chunks(quantized, args.output_dir, chunk_size=args.chunk_size,
                                      use_safetensors=args.save_safetensors, logger=logger)

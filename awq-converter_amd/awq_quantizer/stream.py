@@ -27,6 +27,7 @@ not); without one the host ring holds the whole output (no wrap).
 """
 from __future__ import annotations
 
+import atexit
 import ctypes
 import math
 import threading
@@ -134,6 +135,43 @@ def _hip_runtime():
         _HIP.hipHostMalloc.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_size_t, ctypes.c_uint]
         _HIP.hipHostFree.argtypes = [ctypes.c_void_p]
     return _HIP
+
+
+_WARM: Dict[int, bool] = {}
+
+
+def start_warmup(device: str) -> None:
+    """Start HIP's first-use work for a CUDA device on a native thread (awq_runtime_warmup:
+    first queue, first large copy, the quantize kernels' code object — ~0.1 s in a fresh
+    process), so it overlaps the caller's host-side setup; the pipeline joins it.  Joined at
+    interpreter exit if nothing did."""
+    from . import _hip
+    if not device.startswith("cuda") or not torch.cuda.is_available():
+        return
+    d = torch.device(device)
+    idx = d.index if d.index is not None else torch.cuda.current_device()
+    try:
+        lib = _hip.load_library()
+    except _hip.HipUnavailable:
+        return                                 # (the pipeline reports the missing library)
+    if idx in _WARM:
+        return
+    _WARM[idx] = True
+    if lib.awq_runtime_warmup(idx) == 0:
+        atexit.register(lib.awq_runtime_warmup_wait, idx, None)
+
+
+def device_name(idx: int) -> str:
+    """torch.cuda.get_device_name(idx) without the hipGetDeviceProperties behind it, which
+    takes 0.1-0.18 s in a fresh process (scripts/init_probe.py, profiles/round4/r4e/):
+    hipDeviceGetName returns the same name."""
+    try:
+        buf = ctypes.create_string_buffer(256)
+        if _hip_runtime().hipDeviceGetName(buf, 256, int(idx)) == 0 and buf.value:
+            return buf.value.decode()
+    except (OSError, AttributeError, UnicodeDecodeError):
+        pass
+    return torch.cuda.get_device_name(idx)
 
 
 def pinned_bytes(nbytes: int) -> torch.Tensor:
@@ -321,7 +359,7 @@ def quantize_stream_native(loader, infos, quantizer, device: str, readers: int, 
             release_hook(releaser.written)
     t_place = time.perf_counter()
     dbuf = torch.empty(dcap, dtype=torch.uint8, device=dev)
-    t_dev = time.perf_counter()
+    t_dalloc = time.perf_counter()
     hbuf = pinned_bytes(hcap) if not keep_on_device else None
     t_host = time.perf_counter()
     dptr = dbuf.data_ptr()
@@ -341,11 +379,10 @@ def quantize_stream_native(loader, infos, quantizer, device: str, readers: int, 
     h_stage = pinned_bytes(nslots * (tb + slot))
     t_hstage = time.perf_counter()
     d_stage = torch.empty(nslots * (tb + slot), dtype=torch.uint8, device=dev)
-    compute = torch.cuda.current_stream(dev)
-    h2d = torch.cuda.Stream(dev)
-    d2h = torch.cuda.Stream(dev)
     cfg.host_staging, cfg.dev_staging = h_stage.data_ptr(), d_stage.data_ptr()
-    cfg.compute_stream, cfg.h2d_stream, cfg.d2h_stream = compute.cuda_stream, h2d.cuda_stream, d2h.cuda_stream
+    # streams left NULL: the pipeline creates its own on its submitter thread, where a fresh
+    # process's first-queue setup (~85 ms) overlaps the first reads (include/awq_hip.h)
+    cfg.compute_stream = cfg.h2d_stream = cfg.d2h_stream = None
     trace = None
     if opts.get("trace"):
         cap = nb + 2
@@ -382,21 +419,22 @@ def quantize_stream_native(loader, infos, quantizer, device: str, readers: int, 
         if releaser is not None:
             releaser.detach()
         rc = lib.awq_stream_end(handle, ctypes.byref(stats))
-    _hip.check(rc, "awq_stream_end")
-    if keep_on_device:
-        compute.wait_stream(d2h)
+    _hip.check(rc, "awq_stream_end")    # (it synchronized the pipeline's streams: results complete)
+    warm_s = ctypes.c_double(0.0)
+    lib.awq_runtime_warmup_wait(dev.index, ctypes.byref(warm_s))
     if timings is not None:
         st = {"engine": "native", "wall_s": round(time.perf_counter() - t_enter, 4),
               "setup_s": round(t_run - t_enter, 4), "device_s": round(t_dev - t_enter, 4),
               "small_s": round(t_small - t_dev, 4), "plan_s": round(t_plan - t_small, 4),
               "items_s": round(t_items - t_host, 4), "alloc_host_stage_s": round(t_hstage - t_items, 4),
-              "streams_s": round(t_run - t_hstage, 4),
-              "place_s": round(t_place - t_plan, 4), "alloc_dev_s": round(t_dev - t_place, 4),
-              "alloc_host_out_s": round(t_host - t_dev, 4), "host_ring_MB": hcap >> 20, "dev_ring_MB": dcap >> 20,
+              "alloc_dev_stage_s": round(t_run - t_hstage, 4),
+              "place_s": round(t_place - t_plan, 4), "alloc_dev_s": round(t_dalloc - t_place, 4),
+              "alloc_host_out_s": round(t_host - t_dalloc, 4), "host_ring_MB": hcap >> 20, "dev_ring_MB": dcap >> 20,
               "host_wraps": int(any(hgates)), "dev_wraps": int(any(dgates)) and not keep_on_device,
               "batches": int(stats.batches), "pieces": int(stats.pieces), "slot_MB": slot >> 20,
               "pipeline_s": round(stats.wall_s, 4), "wait_s": round(t_wait, 4),
               "read_busy_s": round(stats.read_busy_s, 4), "submit_wait_read_s": round(stats.wait_read_s, 4),
+              "prepare_s": round(stats.prepare_s, 4), "warmup_s": round(warm_s.value, 4),
               "submit_wait_slot_s": round(stats.wait_slot_s, 4),
               "submit_wait_release_s": round(stats.wait_release_s, 4), "bytes_read": int(stats.bytes_read)}
         if trace is not None:

@@ -78,6 +78,9 @@ struct Pipeline {
     std::vector<hipEvent_t> ev_h2d, ev_kern, ev_done;
     int64_t tb = 0, stride = 0;        // table area per slot; slot stride (tb + slot_bytes)
     hipEvent_t ev_start = nullptr;     // (trace only) the event clock's origin
+    double ev_start_host = 0;          // (trace only) host clock (from t0) when it was recorded
+    hipStream_t st_cs = nullptr, st_h2d = nullptr, st_d2h = nullptr;
+    bool own_cs = false, own_h2d = false, own_d2h = false;   // created by the pipeline
     std::vector<double> tr;            // (trace only) AWQ_STREAM_TRACE_FIELDS per batch, host part
     std::mutex mu;
     std::condition_variable cv;
@@ -91,7 +94,7 @@ struct Pipeline {
     std::string err_msg;
     std::vector<std::thread> readers;
     std::thread submitter;
-    double t0 = 0, read_busy = 0, wait_read = 0, wait_slot = 0, wait_release = 0;
+    double t0 = 0, read_busy = 0, wait_read = 0, wait_slot = 0, wait_release = 0, prepare = 0;
     int64_t bytes_read = 0;
 
     void fail(int code, const std::string& msg) {
@@ -364,25 +367,84 @@ bool launch_batch(Pipeline& P, const Batch& B, const BatchPlan& bp, hipStream_t 
     return true;
 }
 
+constexpr size_t kWarmBytes = 8 << 20;
+constexpr int kMaxDevices = 64;
+
+// HIP's per-process first-use costs, measured in a fresh process (profiles/round4/r4e/
+// init.txt): the first stream ~85 ms (the device's first hardware queue), the first H2D of
+// >= 8 MiB ~7 ms, the first launch of a kernel of awq_fast.hip ~8.6 ms (its code object is
+// loaded on first use).  warm_main pays them once per device and process: one stream, one
+// 8 MiB H2D, stream-copy launch and D2H, then frees what it made.
+struct Warmup {
+    std::mutex mu;                      // serialises the start and the join
+    std::thread th;
+    bool started = false;
+    int err = 0;
+    double secs = 0;
+    ~Warmup() {
+        if (th.joinable()) th.detach();   // (process exit without awq_runtime_warmup_wait)
+    }
+};
+Warmup g_warm[kMaxDevices];
+
+void warm_main(int device, Warmup* W) {
+    const double t = now_s();
+    hipStream_t s = nullptr;
+    void *h = nullptr, *d = nullptr;
+    hipError_t e = hipSetDevice(device);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipHostMalloc(&h, kWarmBytes, 0);
+    if (e == hipSuccess) e = hipMalloc(&d, kWarmBytes);
+    if (e == hipSuccess) e = hipMemcpyAsync(d, h, kWarmBytes, hipMemcpyHostToDevice, s);
+    if (e == hipSuccess) e = awq::launch_stream_copy(d, (char*)d + kWarmBytes / 2, kWarmBytes / 2, s);
+    if (e == hipSuccess) e = hipMemcpyAsync(h, d, kWarmBytes, hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    if (s) (void)hipStreamDestroy(s);
+    if (h) (void)hipHostFree(h);
+    if (d) (void)hipFree(d);
+    W->err = e == hipSuccess ? 0 : AWQ_EHIP;
+    W->secs = now_s() - t;
+}
+
+// The pipeline's device side: the device's first-use warm-up (joined if a caller started it
+// early with awq_runtime_warmup, else run here), then the streams the caller left NULL
+// (non-blocking) — all on the submitter thread, while the readers fill the first slots.
+bool prepare_device(Pipeline* P) {
+    if (P->device >= 0 && P->device < kMaxDevices) {
+        Warmup& W = g_warm[P->device];
+        std::lock_guard<std::mutex> g(W.mu);
+        if (!W.started) {
+            W.started = true;
+            warm_main(P->device, &W);
+        } else if (W.th.joinable()) {
+            W.th.join();
+        }
+        (void)hipSetDevice(P->device);
+    }
+    struct {
+        hipStream_t* s;
+        bool own;
+    } st[3] = {{&P->st_h2d, P->own_h2d}, {&P->st_cs, P->own_cs}, {&P->st_d2h, P->own_d2h}};
+    for (auto& e : st)
+        if (e.own && !P->hip_ok(hipStreamCreateWithFlags(e.s, hipStreamNonBlocking), "hipStreamCreate")) return false;
+    if (!P->tr.empty()) {
+        if (!P->hip_ok(hipEventCreate(&P->ev_start), "trace event") ||
+            !P->hip_ok(hipEventRecord(P->ev_start, P->st_h2d), "trace event"))
+            return false;
+        P->ev_start_host = now_s() - P->t0;
+    }
+    return true;
+}
+
 void submitter_main(Pipeline* P) {
     (void)hipSetDevice(P->device);
     const awq_stream_config& c = P->cfg;
-    hipStream_t h2d = (hipStream_t)c.h2d_stream, cs = (hipStream_t)c.compute_stream, d2h = (hipStream_t)c.d2h_stream;
+    const double tp = now_s();
+    if (!prepare_device(P)) return;
+    P->prepare = now_s() - tp;
+    hipStream_t h2d = P->st_h2d, cs = P->st_cs, d2h = P->st_d2h;
     const int64_t nb = (int64_t)P->batches.size();
     BatchPlan bp;
-    // The copy paths' first use in a process costs ~0.1 s (HIP's copy machinery; the first D2H
-    // into fresh pinned memory ran at 2.6 GB/s for 256 MiB against 57 later, profiles/round4/
-    // r4b/pin_probe.txt): take it now, on both copy streams, while the readers fill the first
-    // batch — through slot 0's table area, which nothing else touches until batch 0 is planned.
-    if (nb > 0) {
-        char* h = (char*)c.host_staging;
-        char* d = (char*)c.dev_staging;
-        if (!P->hip_ok(hipMemcpyAsync(d, h, 256, hipMemcpyHostToDevice, h2d), "warm-up H2D") ||
-            !P->hip_ok(hipStreamSynchronize(h2d), "warm-up H2D") ||
-            !P->hip_ok(hipMemcpyAsync(h, d, 256, hipMemcpyDeviceToHost, d2h), "warm-up D2H") ||
-            !P->hip_ok(hipStreamSynchronize(d2h), "warm-up D2H"))
-            return;
-    }
     for (int64_t b = 0; b < nb; ++b) {
         const Batch& B = P->batches[b];
         double t = now_s();
@@ -554,20 +616,39 @@ int awq_stream_start(const awq_stream_item* items, int n, const awq_stream_confi
                 delete P;   // (events created so far are reclaimed with the context)
                 return awq::set_error(AWQ_EHIP, "hipEventCreate failed");
             }
-    if (trace) {
-        P->tr.assign(nb * AWQ_STREAM_TRACE_FIELDS, -1.0);
-        if (hipEventCreate(&P->ev_start) != hipSuccess ||
-            hipEventRecord(P->ev_start, (hipStream_t)c.h2d_stream) != hipSuccess) {
-            delete P;
-            return awq::set_error(AWQ_EHIP, "trace event");
-        }
-    }
+    if (trace) P->tr.assign(nb * AWQ_STREAM_TRACE_FIELDS, -1.0);
+    P->st_cs = (hipStream_t)c.compute_stream;
+    P->st_h2d = (hipStream_t)c.h2d_stream;
+    P->st_d2h = (hipStream_t)c.d2h_stream;
+    P->own_cs = !P->st_cs;
+    P->own_h2d = !P->st_h2d;
+    P->own_d2h = !P->st_d2h;
     P->t0 = now_s();
     const int nr = std::max(1, std::min(c.readers, (int)std::max<size_t>(1, P->jobs.size())));
     for (int r = 0; r < nr; ++r) P->readers.emplace_back(reader_main, P);
     P->submitter = std::thread(submitter_main, P);
     *handle = P;
     return AWQ_OK;
+}
+
+int awq_runtime_warmup(int device) {
+    if (device < 0 || device >= kMaxDevices) return awq::set_error(AWQ_EINVAL, "bad device index");
+    Warmup& W = g_warm[device];
+    std::lock_guard<std::mutex> g(W.mu);
+    if (!W.started) {
+        W.started = true;
+        W.th = std::thread(warm_main, device, &W);
+    }
+    return AWQ_OK;
+}
+
+int awq_runtime_warmup_wait(int device, double* seconds) {
+    if (device < 0 || device >= kMaxDevices) return awq::set_error(AWQ_EINVAL, "bad device index");
+    Warmup& W = g_warm[device];
+    std::lock_guard<std::mutex> g(W.mu);
+    if (W.th.joinable()) W.th.join();
+    if (seconds) *seconds = W.secs;
+    return W.err ? awq::set_error(W.err, "device warm-up failed") : AWQ_OK;
 }
 
 int64_t awq_stream_plan(const awq_stream_item* items, int n, const awq_stream_config* cfg, int32_t* first_batch,
@@ -654,9 +735,15 @@ int awq_stream_end(void* handle, awq_stream_stats* stats) {
         stats->wait_read_s = P->wait_read;
         stats->wait_slot_s = P->wait_slot;
         stats->wait_release_s = P->wait_release;
+        stats->prepare_s = P->prepare;
     }
     // nothing of the pipeline may still run once the caller's buffers are released
-    for (void* s : {P->cfg.h2d_stream, P->cfg.compute_stream, P->cfg.d2h_stream}) (void)hipStreamSynchronize((hipStream_t)s);
+    const struct {
+        hipStream_t s;
+        bool own;
+    } streams[3] = {{P->st_h2d, P->own_h2d}, {P->st_cs, P->own_cs}, {P->st_d2h, P->own_d2h}};
+    for (const auto& e : streams)
+        if (e.s || !e.own) (void)hipStreamSynchronize(e.s);   // (an own stream not created: nothing ran)
     if (P->ev_start) {
         const size_t nt = std::min(P->batches.size(), (size_t)P->cfg.trace_batches);
         for (size_t b = 0; b < nt; ++b) {
@@ -666,7 +753,8 @@ int awq_stream_end(void* handle, awq_stream_stats* stats) {
             const hipEvent_t ev[3] = {P->ev_h2d[b], P->ev_kern[b], P->ev_done[b]};
             for (int k = 0; k < 3; ++k) {
                 float ms = -1.0f;
-                o[5 + k] = (!rc && hipEventElapsedTime(&ms, P->ev_start, ev[k]) == hipSuccess) ? ms * 1e-3 : -1.0;
+                o[5 + k] = (!rc && hipEventElapsedTime(&ms, P->ev_start, ev[k]) == hipSuccess)
+                               ? P->ev_start_host + ms * 1e-3 : -1.0;
             }
         }
         (void)hipEventDestroy(P->ev_start);
@@ -676,6 +764,8 @@ int awq_stream_end(void* handle, awq_stream_stats* stats) {
         (void)hipEventDestroy(P->ev_kern[b]);
         (void)hipEventDestroy(P->ev_done[b]);
     }
+    for (const auto& e : streams)
+        if (e.own && e.s) (void)hipStreamDestroy(e.s);
     delete P;
     if (rc) return awq::set_error(rc, msg.c_str());
     return AWQ_OK;

@@ -46,7 +46,7 @@
 extern "C" {
 #endif
 
-#define AWQ_HIP_ABI_VERSION 13
+#define AWQ_HIP_ABI_VERSION 14
 
 /* dtype codes of the input weights (torch dtypes the reference accepts, awq.py:397) */
 enum { AWQ_DTYPE_BF16 = 0, AWQ_DTYPE_F16 = 1, AWQ_DTYPE_F32 = 2, AWQ_DTYPE_F64 = 3 };
@@ -239,10 +239,27 @@ int awq_pack_rows(const int32_t* v, int64_t rows, int64_t n, int bits, int qmin,
  * what is left of a slot is split by rows (rows quantize independently, awq.py:332-368), so
  * slots stay small (pipeline fill) whatever the largest tensor.
  *
- * Caller-owned memory (the library allocates none): staging slots (pinned host + device),
- * per-slot descriptor tables (pinned host + device, awq_stream_table_bytes each), every
- * item's device outputs and, when its results are wanted on the host, a pinned host range
- * of the same size.  The three streams may be any hipStream_t (NULL = legacy default).
+ * Caller-owned memory: staging slots (pinned host + device), per-slot descriptor tables
+ * (pinned host + device, awq_stream_table_bytes each), every item's device outputs and, when
+ * its results are wanted on the host, a pinned host range of the same size.  Streams (ABI
+ * 14): a stream left NULL in the config is created by the pipeline (non-blocking) and
+ * destroyed by awq_stream_end, on its submitter thread while the readers fill the first
+ * slots; a non-NULL stream is the caller's.  The submitter first joins the device's
+ * first-use warm-up (awq_runtime_warmup below), or runs it if nobody started it. */
+
+/* HIP's first-use costs of a process on a device — its first hardware queue (~85 ms on
+ * MI355X), first large copy (~7 ms) and the code object of the quantize kernels (~9 ms) —
+ * paid on a native thread of its own: one stream, one 8 MiB H2D, copy kernel and D2H
+ * (buffers freed after).  Returns at once; a later call for the same device does nothing.
+ * A CLI starts it as soon as it knows its device, so the costs overlap its host-side setup
+ * (file index, planning, pinned allocations). */
+int awq_runtime_warmup(int device);
+
+/* Join the device's warm-up if it was started (else return at once); *seconds (may be NULL)
+ * = its duration.  Call it before the process exits if the warm-up may still run. */
+int awq_runtime_warmup_wait(int device, double* seconds);
+
+/* (awq_stream_*, continued)
  *
  * Bounded output memory (round 4): the caller may place the items' device outputs and host
  * ranges in two RINGS that later items reuse, with two per-item gates:
@@ -295,15 +312,16 @@ typedef struct awq_stream_config {
                                     slot_bytes): each slot = its batch's descriptor / tensor-table
                                     area, then its input; one H2D carries both */
     void* dev_staging;           /* device, the same size */
-    void* compute_stream;
+    void* compute_stream;        /* NULL: the pipeline's own (see above) */
     void* h2d_stream;
     void* d2h_stream;
     double* trace;               /* optional (NULL = off): AWQ_STREAM_TRACE_FIELDS doubles per
                                     batch, seconds from the start, filled by awq_stream_end:
                                     first read began, last read ended, H2D enqueued, kernels
                                     enqueued, D2H enqueued (host clock); H2D done, kernels done,
-                                    D2H done (HIP event clock, from an event on the H2D stream
-                                    recorded at start); seconds spent inside the H2D call and
+                                    D2H done (HIP event clock, from an event on the H2D stream,
+                                    offset to the host clock at its recording); seconds spent
+                                    inside the H2D call and
                                     inside the D2H calls; seconds of the batch's host planning,
                                     of waiting for the slot's previous kernels, of the ragged
                                     launches and of the per-tensor launches;
@@ -319,6 +337,7 @@ typedef struct awq_stream_stats {
     double wait_read_s;          /* submitter waiting for a batch's reads */
     double wait_slot_s;          /* submitter waiting for a slot's previous kernels */
     double wait_release_s;       /* submitter waiting for host-ring releases (host_gate) */
+    double prepare_s;            /* submitter's device preparation (streams, first-use warm-up) */
 } awq_stream_stats;
 
 /* Per-slot descriptor / tensor-table bytes (descriptors + tensor tables of up to

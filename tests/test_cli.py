@@ -326,6 +326,61 @@ def test_main_torchrun_two_ranks_gpu(tmp_path, mode):
         assert torch.equal(res["scales"].view(torch.int16), ref["scales"].view(torch.int16)), name
 
 
+@pytest.mark.gpu
+@pytest.mark.skipif(not torch.cuda.is_available(), reason="needs the GPU")
+def test_main_fresh_process_early_warmup_gpu(tmp_path):
+    """`python -m awq_quantizer.main` as users run it: a fresh process, where main() starts
+    the device's first-use warm-up (awq_runtime_warmup) before indexing and the pipeline
+    joins it — every tensor equal to the oracle; the INFO device line names the GPU."""
+    import subprocess
+    import sys
+    from oracle import awq_oracle as orc
+    tensors = _tensors()
+    d = _model_dir(tmp_path, tensors, files=2)
+    out = tmp_path / "out"
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, PYTHONPATH=os.pathsep.join([os.path.join(root, "awq-converter_amd"), root]))
+    r = subprocess.run([sys.executable, "-m", "awq_quantizer.main", "--model_id", d, "--output_dir", str(out),
+                        "--output_format", "packed", "--chunk_size", "2"], env=env, capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    assert f"Using GPU cuda: {torch.cuda.get_device_name(0)}" in r.stdout or \
+        f"Using GPU cuda:0: {torch.cuda.get_device_name(0)}" in r.stdout, r.stdout[-2000:]
+    meta = json.load(open(out / "metadata.json"))
+    assert meta["num_tensors"] == 6
+    for name, ci in meta["tensor_to_chunk"].items():
+        res = torch.load(str(out / f"model_chunk_{ci:04d}.pt"), weights_only=True)[name]
+        ref = orc.quantize(tensors[name], bits=4, group_size=128, symmetric=False)
+        rows = 1 if tensors[name].dim() <= 1 else tensors[name].shape[0]
+        assert torch.equal(res["qweight"], orc.pack_rows(ref["tensor_q"].reshape(rows, -1), 4, 0)), name
+        assert torch.equal(res["scales"].view(torch.int16), ref["scales"].view(torch.int16)), name
+
+
+def test_warmup_api_without_gpu():
+    """awq_runtime_warmup_wait for a device never warmed returns at once; bad indices fail."""
+    from awq_quantizer import _hip
+    import ctypes
+    lib = _hip.load_library()
+    secs = ctypes.c_double(-1.0)
+    assert lib.awq_runtime_warmup_wait(3, ctypes.byref(secs)) == 0 and secs.value == 0.0
+    assert lib.awq_runtime_warmup(-1) != 0 and lib.awq_runtime_warmup(64) != 0
+    assert lib.awq_runtime_warmup_wait(64, None) != 0
+
+
+def test_early_warmup_device_from_argv(monkeypatch):
+    """_early.device_index: the CLI's one GPU from its arguments alone, None whenever it
+    cannot be sure (CPU, several devices, torchrun, an abbreviated option)."""
+    from awq_quantizer._early import device_index
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+    assert device_index([]) == 0 and device_index(["--model_id", "m", "--output_dir", "o"]) == 0
+    assert device_index(["--device", "cuda:3"]) == 3 and device_index(["--device=cuda:1"]) == 1
+    for argv in (["--device", "cpu"], ["--device", "all"], ["--multi_gpu"], ["--dev", "cuda:1"],
+                 ["--device", "cuda:x"]):
+        assert device_index(argv) is None, argv
+    monkeypatch.setenv("WORLD_SIZE", "2")
+    assert device_index([]) is None
+
+
 def test_linear_selection_for_autoawq():
     from awq_quantizer.main import is_linear_weight
     from awq_quantizer.model_loading import TensorInfo

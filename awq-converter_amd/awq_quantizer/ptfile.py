@@ -12,6 +12,7 @@ which releases the GIL: same record names, order, 64-byte data alignment and CRC
 torch.save, read back by torch.load (weights_only=True included) into equal objects.
 Anything else (other value types, archives needing ZIP64) goes to torch.save."""
 import ctypes
+import functools
 import os
 import random
 import struct
@@ -35,6 +36,7 @@ class _Unsupported(Exception):
     pass
 
 
+@functools.lru_cache(maxsize=4096)
 def _uni(s: str) -> bytes:
     b = s.encode("utf-8")
     return b"X" + struct.pack("<I", len(b)) + b
@@ -42,7 +44,7 @@ def _uni(s: str) -> bytes:
 
 def _int(n: int) -> bytes:
     if 0 <= n < 256:
-        return b"K" + bytes((n,))
+        return _SMALL[n]
     if 0 <= n < 65536:
         return b"M" + struct.pack("<H", n)
     if -(1 << 31) <= n < (1 << 31):
@@ -51,7 +53,11 @@ def _int(n: int) -> bytes:
     return b"\x8a" + bytes((len(b),)) + b
 
 
-def _tuple(xs) -> bytes:
+_SMALL = [b"K" + bytes((n,)) for n in range(256)]
+
+
+@functools.lru_cache(maxsize=4096)
+def _tuple(xs: tuple) -> bytes:
     body = b"".join(_int(int(x)) for x in xs)
     n = len(xs)
     if n == 0:
@@ -61,17 +67,23 @@ def _tuple(xs) -> bytes:
     return b"(" + body + b"t"
 
 
+# per storage type: everything of a tensor's record before its storage key
+_HEAD = {dt: _REBUILD + b"((" + _uni("storage") + b"ctorch\n" + st + b"\n" for dt, st in _STORAGE.items()}
+_CPU = _uni("cpu")
+_MID = b"tQ" + _int(0)
+_TAIL = b"\x89" + _HOOKS + b"tR"
+
+
 def _pickle(obj: Any, tensors: List[torch.Tensor], out: List[bytes]) -> None:
-    if isinstance(obj, torch.Tensor):
-        st = _STORAGE.get(obj.dtype)
-        if st is None or obj.device.type != "cpu" or obj.requires_grad or not obj.is_contiguous() \
-                or type(obj) is not torch.Tensor:
+    # (the hot loop of a chunk write: every fragment that repeats is precomputed or cached —
+    #  the Python work here holds the GIL, which the writer threads share)
+    if type(obj) is torch.Tensor:
+        head = _HEAD.get(obj.dtype)
+        if head is None or obj.device.type != "cpu" or obj.requires_grad or not obj.is_contiguous():
             raise _Unsupported
-        key = str(len(tensors))
+        out.append(head + _uni(str(len(tensors))) + _CPU + _int(obj.numel()) + _MID + _tuple(tuple(obj.shape))
+                   + _tuple(obj.stride()) + _TAIL)
         tensors.append(obj)
-        out.append(_REBUILD + b"((" + _uni("storage") + b"ctorch\n" + st + b"\n" + _uni(key) + _uni("cpu")
-                   + _int(obj.numel()) + b"tQ" + _int(0) + _tuple(obj.shape) + _tuple(obj.stride()) + b"\x89"
-                   + _HOOKS + b"tR")
     elif type(obj) is dict:
         out.append(b"}")
         if obj:
@@ -106,7 +118,7 @@ def save(obj: Any, path: str) -> None:
     ptrs = (ctypes.c_void_p * max(n, 1))(*[t.data_ptr() for t in tensors])
     sizes = (ctypes.c_int64 * max(n, 1))(*[t.numel() * t.element_size() for t in tensors])
     archive = os.path.splitext(os.path.basename(path))[0]
-    sid = "".join(_SYSRAND.choice("0123456789") for _ in range(40))   # leaves the caller's RNG alone
+    sid = "%040d" % _SYSRAND.randrange(10 ** 40)   # 40 uniform digits; leaves the caller's RNG alone
     rc = _library().awq_write_pt(path.encode(), archive.encode(), pkl, len(pkl), n, ptrs, sizes, sid.encode())
     if rc in (1, 2):      # 2: would need ZIP64; 1: I/O error — torch.save raises it with its errno
         torch.save(obj, path)

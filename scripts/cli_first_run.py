@@ -36,8 +36,9 @@ def child(argv_json, t_spawn, trace="0", opts="{}"):
     t0 = time.time()
     sys.path[:0] = [ROOT, os.path.join(ROOT, "awq-converter_amd")]
     argv = json.loads(argv_json)
-    from awq_quantizer import _early
-    _early.start(argv)
+    if os.environ.get("CLI_FIRST_RUN_NO_EARLY") != "1":      # (A/B: the warm-up left to the pipeline)
+        from awq_quantizer import _early
+        _early.start(argv)
     t1 = time.time()
     import torch  # noqa: F401
     t2 = time.time()
@@ -72,6 +73,7 @@ def main():
     ap.add_argument("--workdir", default=None)
     ap.add_argument("--trace", action="store_true", help="per-batch pipeline trace in the phases")
     ap.add_argument("--opts", default="{}", help="JSON merged into main.STREAM_OPTS (A/B of pipeline sizes)")
+    ap.add_argument("--no-early", action="store_true", help="do not start the warm-up before import torch (A/B)")
     ap.add_argument("--child", nargs=4)
     a = ap.parse_args()
     if a.child:
@@ -86,7 +88,8 @@ def main():
     nbytes = cli_bench.build_model(model, a.workload, a.shards)
     print(json.dumps({"workload": a.workload, "files": a.shards, "input_GB": round(nbytes / 1e9, 3),
                       "build_s": round(time.time() - t, 1)}), flush=True)
-    env = dict(os.environ, PYTHONPATH=os.pathsep.join([os.path.join(ROOT, "awq-converter_amd"), ROOT]))
+    env = dict(os.environ, PYTHONPATH=os.pathsep.join([os.path.join(ROOT, "awq-converter_amd"), ROOT]),
+               CLI_FIRST_RUN_NO_EARLY="1" if a.no_early else "0")
     for fmt in a.formats.split(","):
         for r in range(a.runs):
             warm(model)
@@ -104,7 +107,7 @@ def main():
             d = json.loads(res[0])
             ob = sum(os.path.getsize(os.path.join(out, f)) for f in os.listdir(out))
             d.update({"workload": a.workload, "format": fmt, "run": r, "kind": "fresh process, page cache warm",
-                      "opts": json.loads(a.opts),
+                      "opts": json.loads(a.opts), "early_warmup": not a.no_early,
                       "process_wall_s": round(wall, 3), "input_GB": round(nbytes / 1e9, 3),
                       "output_GB": round(ob / 1e9, 3), "main_input_GBs": round(nbytes / d["main_s"] / 1e9, 2)})
             print(json.dumps(d), flush=True)

@@ -720,6 +720,16 @@ RgPlan rowgroup_plan(int dtype, int64_t K, int64_t L) {
         pl.waves = 2;
         return pl;
     }
+    // longer 16-bit rows whose group length is not a multiple of 8 (pass 2 looks parameters up
+    // per half-chunk or per element): two waves on tiles of <= 9.6 KB, <= 64 groups (round 4,
+    // profiles/round4/r4g/abk_k14336_tiles.txt, 4096 x 14336: gs 100 -5.4 / -8.4 % and gs 60
+    // -10 / -7.7 % for bf16 / fp16; the same tiles at L % 8 == 0 — gs 48 / 96 — lose up to 30 %
+    // and keep one wave)
+    if (!ew && es == 2 && G > 64 && L % 8 != 0 && L >= 56 && L <= 128) {
+        pl.gpt = (int)min((int64_t)64, 9600 / (L * es) / 8 * 8);
+        pl.waves = 2;
+        return pl;
+    }
     double best_cost = 0.0;
     for (int gpt = 8; gpt <= 64; gpt *= 2) {
         if (gpt * L * es > kRgStageBytes) break;

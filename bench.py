@@ -102,7 +102,7 @@ def parse(argv=None):
                     help="after the timed region: every rank copies its packed shard to the host and writes it as "
                          "chunk files into this directory (the CLI's per-rank output, main.ChunkWriter), reported as "
                          "\"write\" (max over ranks); the files are removed afterwards")
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "round3", "pmc_traffic.json"))
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "round4", "pmc_traffic.json"))
     a = ap.parse_args(argv)
     if a.replica and a.shard:
         ap.error("--replica and --shard are exclusive")

@@ -160,6 +160,19 @@ def test_rowgroup_whole_row_tiles(dtype, K, gs):
     _assert_parity(specials(rand((24, K), gs, 1.0), 3).to(dtype), gs, 4, False)
 
 
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16], ids=str)
+@pytest.mark.parametrize("K,gs", [(14336, 100), (14336, 60), (8192, 100), (6000, 124), (9001, 58), (14336, 76)],
+                         ids=str)
+def test_rowgroup_long_row_two_wave_tiles(dtype, K, gs):
+    """Rows longer than 64 groups with L % 8 != 0 (56 <= L <= 128) take two-wave tiles of
+    <= 9.6 KB (round 4): full tiles, the row's lighter last tile, K % gs != 0 and K % 8 != 0
+    tails, 4 / 8 bits, special values — same bits as the oracle."""
+    x = rand((24, K), K + gs, 0.5, dtype)
+    for bits, sym in ((4, False), (8, True)):
+        _assert_parity(x, gs, bits, sym)
+    _assert_parity(specials(rand((8, K), gs + 1, 1.0), 5).to(dtype), gs, 4, False)
+
+
 @pytest.mark.parametrize("tun", [{"rg_ldsdma": 1}, {"rg_ldsdma": 1, "rg_p2reg": 1}], ids=lambda t: "_".join(t))
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16, torch.float32], ids=str)
 @pytest.mark.parametrize("K,gs", [(4096, 100), (4096, 48), (4096, 200), (3000, 100), (14336, 100), (1000, 60),

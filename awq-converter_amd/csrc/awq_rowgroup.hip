@@ -721,12 +721,16 @@ RgPlan rowgroup_plan(int dtype, int64_t K, int64_t L) {
         return pl;
     }
     // longer 16-bit rows whose group length is not a multiple of 8 (pass 2 looks parameters up
-    // per half-chunk or per element): two waves on tiles of <= 9.6 KB, <= 64 groups (round 4,
-    // profiles/round4/r4g/abk_k14336_tiles.txt, 4096 x 14336: gs 100 -5.4 / -8.4 % and gs 60
-    // -10 / -7.7 % for bf16 / fp16; the same tiles at L % 8 == 0 — gs 48 / 96 — lose up to 30 %
-    // and keep one wave)
+    // per half-chunk or per element): two waves on tiles of <= 9.6 KB, <= 64 groups, the row
+    // split into that many tiles of equal multiples of 8 groups (round 4, profiles/round4/
+    // r4g/abk_k14336_tiles.txt and r4j/abr_long_rows.txt, 4096 x 14336: gs 100 -5..8 %, gs 60
+    // -3..10 %, gs 124 -7..8 %; gs 76 lost 11 % on 56-group tiles with a 21-group last one,
+    // hence the equal split; the same tiles at L % 8 == 0 — gs 48 / 96 — lose up to 30 % and
+    // keep one wave)
     if (!ew && es == 2 && G > 64 && L % 8 != 0 && L >= 56 && L <= 128) {
-        pl.gpt = (int)min((int64_t)64, 9600 / (L * es) / 8 * 8);
+        const int64_t gmax = min((int64_t)64, 9600 / (L * es) / 8 * 8);
+        const int64_t n = (G + gmax - 1) / gmax;                       // tiles per row
+        pl.gpt = (int)(((G + n - 1) / n + 7) / 8 * 8);
         pl.waves = 2;
         return pl;
     }

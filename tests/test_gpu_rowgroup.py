@@ -161,7 +161,8 @@ def test_rowgroup_whole_row_tiles(dtype, K, gs):
 
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16], ids=str)
-@pytest.mark.parametrize("K,gs", [(14336, 100), (14336, 60), (8192, 100), (6000, 124), (9001, 58), (14336, 76)],
+@pytest.mark.parametrize("K,gs", [(14336, 100), (14336, 60), (8192, 100), (12000, 124), (9001, 58), (14336, 76),
+                                  (8192, 60)],
                          ids=str)
 def test_rowgroup_long_row_two_wave_tiles(dtype, K, gs):
     """Rows longer than 64 groups with L % 8 != 0 (56 <= L <= 128) take two-wave tiles of

@@ -381,6 +381,30 @@ def test_early_warmup_device_from_argv(monkeypatch):
     assert device_index([]) is None
 
 
+def test_console_entry_starts_warmup_before_torch(tmp_path):
+    """The `awq_quantizer` console script (awq_quantizer.cli:run) imports neither torch nor the
+    CLI module before _early.start has run; on a missing model it exits 1 like main()."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, PYTHONPATH=os.path.join(root, "awq-converter_amd"))
+    code = ("import sys\n"
+            "from awq_quantizer import _early\n"
+            "real = _early.start\n"
+            "def spy(argv):\n"
+            "    assert 'torch' not in sys.modules and 'awq_quantizer.main' not in sys.modules\n"
+            "    print('EARLY', argv)\n"
+            "    return real(argv)\n"
+            "_early.start = spy\n"
+            "sys.argv = ['awq_quantizer', '--model_id', sys.argv[1], '--output_dir', sys.argv[2]]\n"
+            "from awq_quantizer.cli import run\n"
+            "run()\n")
+    r = subprocess.run([sys.executable, "-c", code, str(tmp_path / "missing"), str(tmp_path / "out")], env=env,
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 1, r.stdout[-2000:] + r.stderr[-2000:]
+    assert "EARLY ['--model_id'" in r.stdout
+
+
 def test_linear_selection_for_autoawq():
     from awq_quantizer.main import is_linear_weight
     from awq_quantizer.model_loading import TensorInfo

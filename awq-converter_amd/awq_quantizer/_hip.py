@@ -72,7 +72,8 @@ class Tuning(ctypes.Structure):
     """Mirror of awq_tuning (csrc/awq_diag.h, diagnostics build): diagnostics / A-B controls only."""
     _fields_ = [("max_blocks", _I32), ("tiles_per_wave", _I32), ("no_rowgroup", _I32), ("rg_waves", _I32),
                 ("rg_gpt", _I32), ("gen_noreg", _I32), ("dq_words_v1", _I32),
-                ("rg_p1", _I32), ("rg_lds_full", _I32), ("rg_ldsdma", _I32), ("rg_p2reg", _I32)]
+                ("rg_p1", _I32), ("rg_lds_full", _I32), ("rg_ldsdma", _I32), ("rg_p2reg", _I32),
+                ("rg_p1u", _I32)]
 
 # symbol -> (restype, argtypes); the CPU test suite checks every one is exported.
 SIGNATURES = {

@@ -39,6 +39,8 @@ typedef struct awq_tuning {
                                 1 the round-3 register stage (loads to VGPRs, LDS stores) */
     int32_t rg_p2reg;        /* with rg_ldsdma = 1: pass 2 of a 4-chunk stage from the stage's
                                 registers (0) or from LDS (1) */
+    int32_t rg_p1u;          /* row-segment pass 1: 0 the uniform form where it applies (round 4),
+                                1 always the per-lane bounds form (A/B) */
 } awq_tuning;
 
 #ifdef AWQ_DIAG

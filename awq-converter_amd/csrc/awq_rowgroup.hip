@@ -180,7 +180,7 @@ __global__ __launch_bounds__(128) void awq_rowgroup_kernel(const void* __restric
                                                              uint16_t* __restrict__ scales,
                                                              int32_t* __restrict__ tensor_q, int32_t* __restrict__ zeros,
                                                              uint32_t nan_code, int lgP_last, int C_last, int p2reg,
-                                                             int ldsdma) {
+                                                             int ldsdma, int p1u) {
     typedef RgSlot<F> SL;
     typedef typename SL::T S;
 #ifndef AWQ_DIAG
@@ -301,6 +301,15 @@ __global__ __launch_bounds__(128) void awq_rowgroup_kernel(const void* __restric
         not_plain = 0;
         any_special = 0;
     }
+    // uniform pass 1 (host: 16-bit, even K and L, P | L with an even L / P for every tile):
+    // the row's zero-padded last group gets its padding as real zeros in the stage
+    // (awq.py:337-339), so every lane reduces exactly C elements with no bounds.  Past a
+    // segment that ends inside a 16-B chunk the slots hold the chunk's foreign bytes, which
+    // another wave may have staged: there the zeros go in after a barrier.
+    const int pad = (F::kBytes == 2 && p1u) ? ng * L32g - n_el : 0;
+    const bool pad_late = pad > 0 && ((skew + n_el) & 7) != 0;
+    if (pad > 0 && !pad_late)
+        for (int i = lane; i < pad; i += NT) ((uint16_t*)stage)[skew + n_el + i] = 0;
     // TQ: the parity outputs (tensor_q) are wanted (a compile-time switch: the packed-only
     // kernel carries no per-sweep checks for them)
     if constexpr (!TQ) tensor_q = nullptr;
@@ -315,6 +324,10 @@ __global__ __launch_bounds__(128) void awq_rowgroup_kernel(const void* __restric
         }
     }
     __syncthreads();
+    if (pad_late) {
+        for (int i = lane; i < pad; i += NT) ((uint16_t*)stage)[skew + n_el + i] = 0;
+        __syncthreads();
+    }
     if constexpr (P1C) {
         // ---- pass 1, lanes split evenly over the tile's groups: Q = NT / ng lanes per group
         //      (any count — not only a power of two; 3 for 41 groups of a 128-lane tile where
@@ -381,12 +394,53 @@ __global__ __launch_bounds__(128) void awq_rowgroup_kernel(const void* __restric
     // ---- this lane's chunk of its group ----
     const int grp = lane >> lgP, j = lane & (P - 1);
     const bool active = grp < ng;
+    int smax;
+    uint32_t umax, umin;
+    if (F::kBytes == 2 && p1u) {
+        // uniform: C (even) elements from a dword boundary for every lane — lanes past the
+        // tile's groups re-read the last group (their results are not used) — in a loop whose
+        // trip count is the same for the whole wave
+        const uint32_t* p = (const uint32_t*)stage + ((skew + min(grp, ng - 1) * L32g + j * C) >> 1);
+        const int nd = C >> 1;
+        s2 sm = {(short)-32768, (short)-32768}, sm_b = sm;
+        us2 um = {0, 0}, um_b = um;
+        us2 un = {(unsigned short)0xFFFF, (unsigned short)0xFFFF}, un_b = un;
+        int d = 0;
+        for (; d + 4 <= nd; d += 4) {
+            const uint32_t v0 = p[d], v1 = p[d + 1], v2 = p[d + 2], v3 = p[d + 3];
+            sm = __builtin_elementwise_max(sm, as_s2(v0));
+            um = __builtin_elementwise_max(um, as_us2(v0));
+            un = __builtin_elementwise_min(un, as_us2(v0));
+            sm_b = __builtin_elementwise_max(sm_b, as_s2(v1));
+            um_b = __builtin_elementwise_max(um_b, as_us2(v1));
+            un_b = __builtin_elementwise_min(un_b, as_us2(v1));
+            sm = __builtin_elementwise_max(sm, as_s2(v2));
+            um = __builtin_elementwise_max(um, as_us2(v2));
+            un = __builtin_elementwise_min(un, as_us2(v2));
+            sm_b = __builtin_elementwise_max(sm_b, as_s2(v3));
+            um_b = __builtin_elementwise_max(um_b, as_us2(v3));
+            un_b = __builtin_elementwise_min(un_b, as_us2(v3));
+        }
+        for (; d < nd; ++d) {
+            const uint32_t v = p[d];
+            sm = __builtin_elementwise_max(sm, as_s2(v));
+            um = __builtin_elementwise_max(um, as_us2(v));
+            un = __builtin_elementwise_min(un, as_us2(v));
+        }
+        sm = __builtin_elementwise_max(sm, sm_b);
+        um = __builtin_elementwise_max(um, um_b);
+        un = __builtin_elementwise_min(un, un_b);
+        smax = max((int)sm.x, (int)sm.y);
+        umax = (uint32_t)max((int)um.x, (int)um.y);
+        umin = (uint32_t)min((int)un.x, (int)un.y);
+    } else {
     const int glen = active ? min((int)L, n_el - grp * (int)L) : 0;   // elements in the row (tail: fewer)
     const int cb = min(j * C, glen), ce = min(cb + C, glen);
     const int base = skew + grp * (int)L;
     const bool padded = active && glen < L;                    // awq.py:337-339: zeros join the min/max
-    int smax = padded ? 0 : INT_MIN;
-    uint32_t umax = 0, umin = padded ? 0u : F::kOnes;
+    smax = padded ? 0 : INT_MIN;
+    umax = 0;
+    umin = padded ? 0u : F::kOnes;
     if constexpr (F::kBytes == 2) {
         // raw 16-bit pairs with packed max/min (v_pk_*_i16/u16: two elements per instruction);
         // an edge dword holding one foreign element gets a copy of its own element there
@@ -460,6 +514,7 @@ __global__ __launch_bounds__(128) void awq_rowgroup_kernel(const void* __restric
             umin = min(umin, v);
         }
     }
+    }   // (per-lane bounds form)
     rg_reduce(smax, umax, umin, lgP);                          // the group's P lanes (aligned)
     float gmn, gmx;
     bool gnan;
@@ -773,7 +828,14 @@ hipError_t launch_rowgroup(const void* w, int dtype, int64_t rows, int64_t K, in
     //  rg_lds_full = 1 keeps the round-2 sizing for A/B)
     const int64_t es = dtype == AWQ_DTYPE_F32 ? 4 : 2;
     const int64_t stage_el = tuning().rg_lds_full == 1 ? (int64_t)gpt * L : min((int64_t)gpt * L, K);
-    const size_t lds = (size_t)((stage_el * es + 15) / 16 * 16 + 48);
+    size_t lds = (size_t)((stage_el * es + 15) / 16 * 16 + 48);
+    // uniform pass 1 (round 4): 16-bit, even K and L, and every tile's P lanes per group split
+    // L into P runs of the same even length (so runs start on dwords and the padding of the
+    // row's last group can be staged as zeros); the stage then holds the tile's groups whole
+    const bool lanes_ok = L % (1 << lgP) == 0 && (L >> lgP) % 2 == 0 &&
+                          (ng_last == gpt || (L % (1 << lgP_last) == 0 && (L >> lgP_last) % 2 == 0));
+    const int p1u = (es == 2 && K % 2 == 0 && L % 2 == 0 && lanes_ok && tuning().rg_p1u != 1) ? 1 : 0;
+    if (p1u) lds = std::max(lds, (size_t)(((7 + min((int64_t)gpt, G) * L) * es + 15) / 16 * 16));
     const bool p1c = tuning().rg_p1 == 2;   // pass 1 by groups (default) / evenly split runs (A/B)
     // the stage by LDS-DMA (default); diagnostics A/B: rg_ldsdma = 1 the round-3 register
     // stage, whose 4-chunk case then feeds pass 2 from its registers unless rg_p2reg = 1
@@ -782,7 +844,7 @@ hipError_t launch_rowgroup(const void* w, int dtype, int64_t rows, int64_t K, in
 #define AWQ_RG_GO(Fm, B, S, SP, P1, TQ)                                                                            \
     hipLaunchKernelGGL((awq_rowgroup_kernel<Fm, B, S, SP, P1, TQ>), grid, block, lds, stream, w, rows, K, L, lgP,  \
                        gpt, (uint32_t)tpr, G, C, 1.0f / (float)L, qweight, qzeros, scales, tensor_q, zeros, nan_code, \
-                       lgP_last, C_last, p2reg, ldsdma)
+                       lgP_last, C_last, p2reg, ldsdma, p1u)
     // (the pass-1 A/B variant is built for the packed outputs only; with tensor_q it takes the default)
 #ifdef AWQ_DIAG
 #define AWQ_RG_SPLIT(Fm, B, S, SP)                                                                                 \

@@ -149,7 +149,8 @@ def test_rowgroup_pass1_split_runs(dtype, shape, gs):
 
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16], ids=str)
-@pytest.mark.parametrize("K,gs", [(4096, 100), (4096, 96), (4096, 48), (4096, 200), (3000, 100), (4104, 100)], ids=str)
+@pytest.mark.parametrize("K,gs", [(4096, 100), (4096, 96), (4096, 48), (4096, 200), (3000, 100), (4104, 100),
+                                  (4098, 100), (2562, 52)], ids=str)
 def test_rowgroup_whole_row_tiles(dtype, K, gs):
     """Whole-row two-wave tiles (K >= 2 560, <= 64 groups): the exactly-4-chunks-per-lane
     stage (K = 4096: 512 chunks on 128 lanes), the uniform full sweeps of pass 2 and the
@@ -174,15 +175,18 @@ def test_rowgroup_long_row_two_wave_tiles(dtype, K, gs):
     _assert_parity(specials(rand((8, K), gs + 1, 1.0), 5).to(dtype), gs, 4, False)
 
 
-@pytest.mark.parametrize("tun", [{"rg_ldsdma": 1}, {"rg_ldsdma": 1, "rg_p2reg": 1}], ids=lambda t: "_".join(t))
+@pytest.mark.parametrize("tun", [{"rg_ldsdma": 1}, {"rg_ldsdma": 1, "rg_p2reg": 1}, {"rg_p1u": 1}],
+                         ids=lambda t: "_".join(t))
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16, torch.float32], ids=str)
 @pytest.mark.parametrize("K,gs", [(4096, 100), (4096, 48), (4096, 200), (3000, 100), (14336, 100), (1000, 60),
-                                  (203, 50)], ids=str)
+                                  (203, 50), (4098, 100), (8192, 60)], ids=str)
 def test_rowgroup_stage_variants_same_bits(dtype, K, gs, tun):
     """The LDS-DMA stage (the default) gives the bits of the round-3 register stage
     (diagnostics build, rg_ldsdma = 1), whose 4-chunk case feeds pass 2 from registers or
-    (rg_p2reg = 1) from LDS; whole-row, one-wave and partial tiles, the tensor's last bytes
-    (K = 203), special values."""
+    (rg_p2reg = 1) from LDS; the uniform pass 1 (default where it applies: zero-staged
+    padding, also past a segment ending inside a 16-B chunk, K = 4098) the bits of the
+    per-lane bounds form (rg_p1u = 1); whole-row, one-wave and partial tiles, the tensor's
+    last bytes (K = 203), special values."""
     if dtype == torch.float32 and gs > 256:
         pytest.skip("fp32 row segments take group sizes <= 256")
     from awq_quantizer import _hip

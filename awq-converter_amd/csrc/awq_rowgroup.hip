@@ -775,14 +775,14 @@ RgPlan rowgroup_plan(int dtype, int64_t K, int64_t L) {
         pl.waves = 2;
         return pl;
     }
-    // longer 16-bit rows whose group length is not a multiple of 8 (pass 2 looks parameters up
-    // per half-chunk or per element): two waves on tiles of <= 9.6 KB, <= 64 groups, the row
-    // split into that many tiles of equal multiples of 8 groups (round 4, profiles/round4/
-    // r4g/abk_k14336_tiles.txt and r4j/abr_long_rows.txt, 4096 x 14336: gs 100 -5..8 %, gs 60
-    // -3..10 %, gs 124 -7..8 %; gs 76 lost 11 % on 56-group tiles with a 21-group last one,
-    // hence the equal split; the same tiles at L % 8 == 0 — gs 48 / 96 — lose up to 30 % and
-    // keep one wave)
-    if (!ew && es == 2 && G > 64 && L % 8 != 0 && L >= 56 && L <= 128) {
+    // long 16-bit rows (>= 96 groups) whose group length is not a multiple of 8 (pass 2 looks
+    // parameters up per half-chunk or per element): two waves on tiles of <= 9.6 KB, <= 64
+    // groups, the row split into that many tiles of equal multiples of 8 groups (round 4,
+    // profiles/round4/r4g/abk_k14336_tiles.txt, r4j/abr_long_rows.txt, r4k/abr.txt: 4096 x
+    // 14336 gs 100 -11..22 %, gs 60 -5..11 %, gs 124 -2..3 %, 8192 x 8192 gs 76 -15 %, gs 60
+    // -2..5 %; rows of 65-95 groups lost up to 12 % (K = 4096 at gs 60: tiles of 40 + 29
+    // groups) and keep one wave, as do L % 8 == 0 sizes — gs 48 / 96 lost up to 30 %)
+    if (!ew && es == 2 && G >= 96 && L % 8 != 0 && L >= 56 && L <= 128) {
         const int64_t gmax = min((int64_t)64, 9600 / (L * es) / 8 * 8);
         const int64_t n = (G + gmax - 1) / gmax;                       // tiles per row
         pl.gpt = (int)(((G + n - 1) / n + 7) / 8 * 8);

@@ -546,9 +546,11 @@ __global__ __launch_bounds__(128) void awq_rowgroup_kernel(const void* __restric
     int32_t* qdst = qweight ? qweight + r * wpr + kb / PER : nullptr;
     // one chunk: c = its index in the segment, efA = 8 c + 0.5 (exact float); ALIGNED: the
     // segment starts 16-B aligned (skew 0); FULL: the chunk holds 8 elements of the row
-    auto sweep = [&](int c, float efA, auto aligned_t, auto full_t, auto plain_t, const u4* rv = nullptr) {
+    auto sweep = [&](int c, float efA, auto aligned_t, auto full_t, auto plain_t, auto special_t,
+                     const u4* rv = nullptr) {
         constexpr bool ALIGNED = decltype(aligned_t)::value, FULL = decltype(full_t)::value;
         constexpr bool PLAIN = decltype(plain_t)::value;
+        constexpr bool SPECIAL = decltype(special_t)::value;   // the tile has a special group
         const int e0c = 8 * c;
         const bool tail = !FULL && e0c + 8 > n_el;        // the row's last, partial chunk
         float x[8];
@@ -586,7 +588,7 @@ __global__ __launch_bounds__(128) void awq_rowgroup_kernel(const void* __restric
             const float4 pA = prm[gA];
             float4 pB = pA;
             if constexpr (SPLIT == 4) pB = prm[min((int)((efA + 4.0f) * invL), ng - 1)];
-            spec = tile_special && (pA.w != 0.0f || pB.w != 0.0f);
+            spec = SPECIAL && (pA.w != 0.0f || pB.w != 0.0f);
 #pragma unroll
             for (int i = 0; i < 8; ++i) {
                 rr[i] = i < 4 ? pA.x : pB.x;
@@ -597,7 +599,7 @@ __global__ __launch_bounds__(128) void awq_rowgroup_kernel(const void* __restric
             const int gA = (int)(((float)e0c + 0.5f) * invL);
             const int bnd = (gA + 1) * L32 - e0c;         // first element of the next group
             const float4 pA = prm[gA], pB = prm[min(gA + 1, ng - 1)];
-            spec = tile_special && (pA.w != 0.0f || (bnd < 8 && pB.w != 0.0f));
+            spec = SPECIAL && (pA.w != 0.0f || (bnd < 8 && pB.w != 0.0f));
 #pragma unroll
             for (int i = 0; i < 8; ++i) {
                 const bool a = i < bnd;
@@ -611,7 +613,7 @@ __global__ __launch_bounds__(128) void awq_rowgroup_kernel(const void* __restric
             for (int i = 0; i < 8; ++i) {
                 const int gi = min((int)(((float)(e0c + i) + 0.5f) * invL), ng - 1);
                 const float4 pi = prm[gi];
-                spec |= tile_special && pi.w != 0.0f;
+                spec |= SPECIAL && pi.w != 0.0f;
                 rr[i] = pi.x;
                 zz[i] = pi.y;
                 ss[i] = pi.z;
@@ -667,10 +669,10 @@ __global__ __launch_bounds__(128) void awq_rowgroup_kernel(const void* __restric
     store:
         if (qdst) {
             if (BITS == 4) {
-                qdst[c] = (int32_t)word0;
+                qdst[(uint32_t)c] = (int32_t)word0;            // (unsigned: a 32-bit offset on an SGPR base)
             } else {
-                qdst[2 * c] = (int32_t)word0;
-                if (!tail || e0c + 4 < n_el) qdst[2 * c + 1] = (int32_t)word1;
+                qdst[2u * (uint32_t)c] = (int32_t)word0;
+                if (!tail || e0c + 4 < n_el) qdst[2u * (uint32_t)c + 1u] = (int32_t)word1;
             }
         }
         if (tensor_q) {
@@ -691,31 +693,37 @@ __global__ __launch_bounds__(128) void awq_rowgroup_kernel(const void* __restric
     // checks, the rest (<= 1 sweep of full chunks + the row's last partial chunk) guarded
     const float efStep = 8.0f * (float)NT;
     const int lgNT = NT == 128 ? 7 : 6;
-    auto sweeps = [&](auto aligned_t, auto plain_t) {
+    auto sweeps = [&](auto aligned_t, auto plain_t, auto special_t) {
         if constexpr (F::kBytes == 2 && decltype(aligned_t)::value) {
             if (p2reg && nch == 4 * NT && n_el == 32 * NT) {   // the 4-chunk stage: data in registers
                 float efA = 8.0f * (float)lane + 0.5f;
 #pragma unroll
                 for (int sw = 0; sw < 4; ++sw, efA += efStep)
-                    sweep(lane + (sw << lgNT), efA, aligned_t, std::true_type{}, plain_t, &vreg[sw]);
+                    sweep(lane + (sw << lgNT), efA, aligned_t, std::true_type{}, plain_t, special_t, &vreg[sw]);
                 return;
             }
         }
         const int full_sweeps = (n_el >> 3) >> lgNT;
         float efA = 8.0f * (float)lane + 0.5f;
         for (int sw = 0; sw < full_sweeps; ++sw, efA += efStep)
-            sweep(lane + (sw << lgNT), efA, aligned_t, std::true_type{}, plain_t);
+            sweep(lane + (sw << lgNT), efA, aligned_t, std::true_type{}, plain_t, special_t);
         for (int c = lane + (full_sweeps << lgNT); c < nck; c += NT, efA += efStep)
-            sweep(c, efA, aligned_t, std::false_type{}, plain_t);
+            sweep(c, efA, aligned_t, std::false_type{}, plain_t, special_t);
     };
     // (uniform switches hoisted out of the sweeps: the alignment and, for fp16, whether every
     //  group of the tile admits the plain quotient)
+    // (and whether a group of the tile takes the IEEE-division path: without one the sweeps
+    //  carry no per-lane special-value test, round 4)
+    auto by_special = [&](auto aligned_t, auto plain_t) {
+        if (tile_special) sweeps(aligned_t, plain_t, std::true_type{});
+        else sweeps(aligned_t, plain_t, std::false_type{});
+    };
     auto by_plain = [&](auto aligned_t) {
         if constexpr (F::kHasPlain) {
-            if (plain) sweeps(aligned_t, std::true_type{});
-            else sweeps(aligned_t, std::false_type{});
+            if (plain) by_special(aligned_t, std::true_type{});
+            else by_special(aligned_t, std::false_type{});
         } else {
-            sweeps(aligned_t, std::false_type{});
+            by_special(aligned_t, std::false_type{});
         }
     };
     if (skew == 0) by_plain(std::true_type{});

@@ -667,7 +667,7 @@ __global__ __launch_bounds__(128) void awq_rowgroup_kernel(const void* __restric
             }
         }
     store:
-        if (qdst) {
+        if (TQ ? qdst != nullptr : true) {            // (packed-only: pass 2 runs only with qweight)
             if (BITS == 4) {
                 qdst[(uint32_t)c] = (int32_t)word0;            // (unsigned: a 32-bit offset on an SGPR base)
             } else {
@@ -726,8 +726,11 @@ __global__ __launch_bounds__(128) void awq_rowgroup_kernel(const void* __restric
             by_special(aligned_t, std::false_type{});
         }
     };
-    if (skew == 0) by_plain(std::true_type{});
-    else by_plain(std::false_type{});
+    // (the packed-only kernel's pass 2 exists for qweight: without it, none)
+    if (TQ || qdst) {
+        if (skew == 0) by_plain(std::true_type{});
+        else by_plain(std::false_type{});
+    }
     if (qzeros) {                                 // g0 is a word boundary: GPT % PER == 0
         const int64_t zpr = (G + PER - 1) / PER;
         const int nwz = (ng + PER - 1) / PER;

@@ -371,16 +371,19 @@ constexpr size_t kWarmBytes = 8 << 20;
 constexpr int kMaxDevices = 64;
 
 // HIP's per-process first-use costs, measured in a fresh process (profiles/round4/r4e/
-// init.txt): the first stream ~85 ms (the device's first hardware queue), the first H2D of
-// >= 8 MiB ~7 ms, the first launch of a kernel of awq_fast.hip ~8.6 ms (its code object is
-// loaded on first use).  warm_main pays them once per device and process: one stream, one
-// 8 MiB H2D, stream-copy launch and D2H, then frees what it made.
+// init.txt): the first stream ~85 ms (the device's first hardware queue), each further one
+// ~5 ms, the first H2D of >= 64 KiB ~7 ms, the first launch of a kernel of awq_fast.hip
+// ~8.6 ms (its code object is loaded on first use).  warm_main pays them once per device and
+// process: three streams (kept for the first pipeline), one 8 MiB H2D, stream-copy launch
+// and D2H, then frees its buffers.
 struct Warmup {
-    std::mutex mu;                      // serialises the start and the join
+    std::mutex mu;                      // serialises the start, the join and the pool
     std::thread th;
     bool started = false;
     int err = 0;
     double secs = 0;
+    hipStream_t pool[3] = {};           // non-blocking streams made by the warm-up, handed to
+    int npool = 0;                      // the device's first pipeline (each further one ~5 ms)
     ~Warmup() {
         if (th.joinable()) th.detach();   // (process exit without awq_runtime_warmup_wait)
     }
@@ -392,14 +395,21 @@ void warm_main(int device, Warmup* W) {
     hipStream_t s = nullptr;
     void *h = nullptr, *d = nullptr;
     hipError_t e = hipSetDevice(device);
-    if (e == hipSuccess) e = hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
+    for (int k = 0; k < 3 && e == hipSuccess; ++k) {
+        e = hipStreamCreateWithFlags(&W->pool[k], hipStreamNonBlocking);
+        if (e == hipSuccess) W->npool = k + 1;
+    }
+    if (e == hipSuccess) s = W->pool[0];
     if (e == hipSuccess) e = hipHostMalloc(&h, kWarmBytes, 0);
     if (e == hipSuccess) e = hipMalloc(&d, kWarmBytes);
     if (e == hipSuccess) e = hipMemcpyAsync(d, h, kWarmBytes, hipMemcpyHostToDevice, s);
     if (e == hipSuccess) e = awq::launch_stream_copy(d, (char*)d + kWarmBytes / 2, kWarmBytes / 2, s);
     if (e == hipSuccess) e = hipMemcpyAsync(h, d, kWarmBytes, hipMemcpyDeviceToHost, s);
     if (e == hipSuccess) e = hipStreamSynchronize(s);
-    if (s) (void)hipStreamDestroy(s);
+    if (e != hipSuccess) {                // (no pool after a failure: the pipeline makes its own)
+        for (int k = 0; k < W->npool; ++k) (void)hipStreamDestroy(W->pool[k]);
+        W->npool = 0;
+    }
     if (h) (void)hipHostFree(h);
     if (d) (void)hipFree(d);
     W->err = e == hipSuccess ? 0 : AWQ_EHIP;
@@ -410,6 +420,10 @@ void warm_main(int device, Warmup* W) {
 // early with awq_runtime_warmup, else run here), then the streams the caller left NULL
 // (non-blocking) — all on the submitter thread, while the readers fill the first slots.
 bool prepare_device(Pipeline* P) {
+    struct {
+        hipStream_t* s;
+        bool own;
+    } st[3] = {{&P->st_h2d, P->own_h2d}, {&P->st_cs, P->own_cs}, {&P->st_d2h, P->own_d2h}};
     if (P->device >= 0 && P->device < kMaxDevices) {
         Warmup& W = g_warm[P->device];
         std::lock_guard<std::mutex> g(W.mu);
@@ -420,13 +434,12 @@ bool prepare_device(Pipeline* P) {
             W.th.join();
         }
         (void)hipSetDevice(P->device);
+        for (auto& e : st)                // the warm-up's streams first (already created)
+            if (e.own && W.npool > 0) *e.s = W.pool[--W.npool];
     }
-    struct {
-        hipStream_t* s;
-        bool own;
-    } st[3] = {{&P->st_h2d, P->own_h2d}, {&P->st_cs, P->own_cs}, {&P->st_d2h, P->own_d2h}};
     for (auto& e : st)
-        if (e.own && !P->hip_ok(hipStreamCreateWithFlags(e.s, hipStreamNonBlocking), "hipStreamCreate")) return false;
+        if (e.own && !*e.s && !P->hip_ok(hipStreamCreateWithFlags(e.s, hipStreamNonBlocking), "hipStreamCreate"))
+            return false;
     if (!P->tr.empty()) {
         if (!P->hip_ok(hipEventCreate(&P->ev_start), "trace event") ||
             !P->hip_ok(hipEventRecord(P->ev_start, P->st_h2d), "trace event"))

@@ -249,8 +249,9 @@ int awq_pack_rows(const int32_t* v, int64_t rows, int64_t n, int bits, int qmin,
 
 /* HIP's first-use costs of a process on a device — its first hardware queue (~85 ms on
  * MI355X), first large copy (~7 ms) and the code object of the quantize kernels (~9 ms) —
- * paid on a native thread of its own: one stream, one 8 MiB H2D, copy kernel and D2H
- * (buffers freed after).  Returns at once; a later call for the same device does nothing.
+ * paid on a native thread of its own: three non-blocking streams (kept for the device's
+ * first pipeline, whose NULL config streams they become), one 8 MiB H2D, copy kernel and
+ * D2H (buffers freed after).  Returns at once; a later call for the same device does nothing.
  * A CLI starts it as soon as it knows its device, so the costs overlap its host-side setup
  * (file index, planning, pinned allocations). */
 int awq_runtime_warmup(int device);

@@ -336,17 +336,32 @@ class ChunkWriter:
         self.times: List[Tuple[float, float, float]] = []   # per chunk: submitted, started, ended (time.time)
         self.failed: set = set()
         self.hooks: List[Callable[[List[str]], None]] = []
+        self.n_reported = 0
+        self.widened = False
         os.makedirs(output_dir, exist_ok=True)
         self.thread = threading.Thread(target=self._run, daemon=True)
         self.thread.start()
 
     def done(self, name: str, result: Optional[Dict[str, torch.Tensor]]) -> None:
-        """A tensor finished: its host result dict, or None if it failed."""
+        """A tensor finished: its host result dict, or None if it failed.  Once every tensor
+        has reported, the producers' HIP work is over: the pool widens for the tail."""
         with self.cv:
             self.status[name] = result
             if result is None:
                 self.failed.add(name)
+            self.n_reported += 1
+            last = self.n_reported == len(self.order)
             self.cv.notify()
+        if last:
+            self._widen()
+
+    def _widen(self) -> None:
+        with self.cv:
+            if self.widened:
+                return
+            self.widened = True
+        for _ in range(self.tail_writers - self.writers):
+            self.gate.release()
 
     def add_written_hook(self, fn: Callable[[List[str]], None]) -> None:
         """fn(names) after each chunk file is written: its results are no longer read."""
@@ -412,8 +427,7 @@ class ChunkWriter:
         with self.cv:
             self.closed = True
             self.cv.notify()
-        for _ in range(self.tail_writers - self.writers):   # the producers are done: widen the pool
-            self.gate.release()
+        self._widen()                                       # the producers are done: widen the pool
         self.thread.join()
         if self.error is not None:
             raise self.error

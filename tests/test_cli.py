@@ -193,8 +193,8 @@ def test_writer_threads_by_output_size(monkeypatch):
 
 
 def test_chunk_writer_widens_pool_at_close(tmp_path, monkeypatch):
-    """While producers run at most `writers` chunk writes run at once; close() releases the
-    rest of the pool for the backlog (same files either way)."""
+    """While producers run at most `writers` chunk writes run at once; once every tensor has
+    reported (or at close()) the rest of the pool drains the backlog (same files either way)."""
     import threading
     import time as _t
     from awq_quantizer import main as m
@@ -213,12 +213,14 @@ def test_chunk_writer_widens_pool_at_close(tmp_path, monkeypatch):
     monkeypatch.setattr(m, "_write_chunk", slow_write)
     order = [f"t{i}" for i in range(16)]
     w = m.ChunkWriter(order, str(tmp_path), 1, False, writers=2)
-    for n in order:
+    for n in order[:-1]:
         w.done(n, {"q": torch.zeros(2), "bits": torch.tensor(4)})
     _t.sleep(0.12)
     assert peak[0] <= 2                                      # gated while "producing"
+    w.done(order[-1], {"q": torch.zeros(2), "bits": torch.tensor(4)})   # the last report widens
+    _t.sleep(0.12)
+    assert peak[0] > 2                                       # the backlog drains wider
     w.close()
-    assert peak[0] > 2                                       # the backlog drained wider
     assert json.load(open(tmp_path / "metadata.json"))["num_chunks"] == 16
 
 

@@ -21,6 +21,8 @@ DIAG_LIB_PATH = os.path.join(LIB_DIR, "libawq_hip_diag.so")
 Q_SMALL_TENSOR = 1      # include/awq_hip.h AWQ_Q_SMALL_TENSOR
 
 AWQ_DTYPE = {torch.bfloat16: 0, torch.float16: 1, torch.float32: 2, torch.float64: 3}
+APPLY_DTYPE = {**AWQ_DTYPE, torch.int32: 4}     # awq_apply_params_ex (AWQ_DTYPE_I32)
+APPLY_SCALE_ONE_ELEMENT, APPLY_ZERO_ONE_ELEMENT = 1, 2
 
 _P = ctypes.c_void_p
 _I64 = ctypes.c_int64
@@ -91,6 +93,7 @@ SIGNATURES = {
                                       _P]),
     "awq_group_params": (_I32, [_P, _I32, _I64, _I64, _I64, _I32, _I32, _P, _P, _P]),
     "awq_apply_params": (_I32, [_P, _I32, _I64, _I64, _I64, _P, _P, _I32, _I32, _I32, _P, _P]),
+    "awq_apply_params_ex": (_I32, [_P, _I32, _I64, _I64, _I64, _P, _P, _I32, _I32, _I32, _I32, _I32, _I32, _P, _P]),
     "awq_packs_directly": (_I32, [_I32, _I64, _I64, _I64]),
     "awq_ragged_eligible": (_I32, [_I32, _I64, _I64, _I64]),
     "awq_plan_ragged": (_I64, [ctypes.POINTER(TensorDesc), _I32, _I32, _I64]),
@@ -227,12 +230,15 @@ def group_params(x: torch.Tensor, rows: int, K: int, L: int, bits: int, symmetri
 
 
 def apply_params(x: torch.Tensor, rows: int, K: int, L: int, scales: torch.Tensor, zeros: torch.Tensor, qmin: int,
-                 qmax: int, mode: int) -> torch.Tensor:
-    """awq_apply_params: mode 0 quantize / mode 1 dequantize x (device, contiguous) with
-    float64 per-group parameters; result in x's dtype and shape."""
-    out = torch.empty_like(x)
-    check(load_library().awq_apply_params(ptr(x), AWQ_DTYPE[x.dtype], rows, K, L, ptr(scales), ptr(zeros), int(qmin),
-                                          int(qmax), int(mode), ptr(out), _stream(x)), "awq_apply_params")
+                 qmax: int, mode: int, op1_dtype: torch.dtype, op2_dtype: torch.dtype, flags: int) -> torch.Tensor:
+    """awq_apply_params_ex: mode 0 quantize / mode 1 dequantize x (device, contiguous) with
+    float64 per-group parameters, the first op in op1_dtype and the second in op2_dtype (torch's
+    result dtypes); result of op2_dtype, x's shape."""
+    out = torch.empty(x.shape, dtype=op2_dtype, device=x.device)
+    check(load_library().awq_apply_params_ex(ptr(x), APPLY_DTYPE[x.dtype], rows, K, L, ptr(scales), ptr(zeros),
+                                             int(qmin), int(qmax), int(mode), APPLY_DTYPE[op1_dtype],
+                                             APPLY_DTYPE[op2_dtype], int(flags), ptr(out), _stream(x)),
+          "awq_apply_params_ex")
     return out
 
 
@@ -289,11 +295,13 @@ def load_diag_library(path: str = DIAG_LIB_PATH):
 
 @contextlib.contextmanager
 def tuning(**kw):
-    """Diagnostics / A-B only (awq-converter_amd/csrc/awq_diag.h): inside the block every entry
-    point of this module calls the DIAGNOSTICS build (the shipped libawq_hip.so has no tuning
-    and no variant kernels) with the given overrides for this thread (max_blocks,
-    tiles_per_wave, no_rowgroup, rg_waves, rg_gpt, gen_noreg, dq_words_v1, rg_p1,
-    rg_lds_full); same results, other speed.  Restores the product library on exit."""
+    """Diagnostics / A-B only (awq-converter_amd/csrc/awq_diag.h).  PROCESS-WIDE: inside the
+    block every entry point of this module, on every thread, calls the DIAGNOSTICS build (the
+    shipped libawq_hip.so has no tuning and no variant kernels).  The overrides (max_blocks,
+    tiles_per_wave, no_rowgroup, rg_waves, rg_gpt, gen_noreg, dq_words_v1, rg_p1, rg_lds_full)
+    are thread-local inside that library: they apply to launches from the calling thread only
+    (not, e.g., to the native stream's submitter thread).  Same results, other speed.  Restores
+    the product library on exit; meant for single-threaded scripts."""
     global _lib
     diag = load_diag_library()
     prev = load_library()

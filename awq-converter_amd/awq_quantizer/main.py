@@ -344,8 +344,12 @@ class ChunkWriter:
 
     def done(self, name: str, result: Optional[Dict[str, torch.Tensor]]) -> None:
         """A tensor finished: its host result dict, or None if it failed.  Once every tensor
-        has reported, the producers' HIP work is over: the pool widens for the tail."""
+        has reported, the producers' HIP work is over: the pool widens for the tail.  Raises
+        once a chunk write has failed, so the producer stops (the native pipeline then cancels
+        its remaining batches) instead of quantizing into a run that cannot be saved."""
         with self.cv:
+            if self.error is not None:
+                raise RuntimeError(f"chunk writer failed: {self.error}") from self.error
             self.status[name] = result
             if result is None:
                 self.failed.add(name)
@@ -408,19 +412,36 @@ class ChunkWriter:
             if n_ok and self.metadata:
                 _write_metadata(self.dir, c, self.size, t2c, self.st, n_ok, qparams, self.logger)
         except BaseException as e:  # noqa: BLE001  (reported by close())
-            self.error = e
+            with self.cv:
+                if self.error is None:
+                    self.error = e
+            # nothing more will be written: release every result, so a producer blocked on a
+            # wrapping host ring (awq_stream_release) is never left waiting for this thread
+            self._report_written(list(self.order))
 
-    def _timed_write(self, chunk, c: int, t_submit: float) -> None:
-        with self.gate:
-            t0 = time.time()
-            _write_chunk(chunk, self.dir, c, self.st, self.logger, stem=self.stem)
-            self.times.append((t_submit, t0, time.time()))
-        names = list(chunk)
-        chunk.clear()               # the results are views of a ring the pipeline will reuse
+    def _report_written(self, names: List[str]) -> None:
         with self.cv:
             hooks = list(self.hooks)
         for fn in hooks:
             fn(names)
+
+    def _timed_write(self, chunk, c: int, t_submit: float) -> None:
+        names = list(chunk)
+        try:
+            with self.gate:
+                t0 = time.time()
+                _write_chunk(chunk, self.dir, c, self.st, self.logger, stem=self.stem)
+                self.times.append((t_submit, t0, time.time()))
+        except BaseException as e:  # noqa: BLE001  (first error wins; done() and close() report it)
+            with self.cv:
+                if self.error is None:
+                    self.error = e
+            raise
+        finally:
+            # written or failed, these results are never read again: the pipeline may reuse
+            # their ring range (a failed write must not leave it blocked)
+            chunk.clear()
+            self._report_written(names)
 
     def close(self) -> None:
         """Every producer has finished: unfinished tensors count as failed; wait for the writes."""

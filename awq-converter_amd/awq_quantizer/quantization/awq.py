@@ -310,49 +310,62 @@ class AWQQuantizer:
         s, z = _hip.group_params(x, C, K, K, self.bits, self.symmetric)
         return self._home(s.reshape(C).to(tensor.dtype)), self._home(z.reshape(C).to(tensor.dtype))
 
+    # parameter dtypes whose values float64 holds exactly (int64: checked per call)
+    _EXACT_PARAM = (torch.bfloat16, torch.float16, torch.float32, torch.float64, torch.int32, torch.int16,
+                    torch.int8, torch.uint8, torch.bool, torch.int64)
+
     def _apply(self, tensor: torch.Tensor, scale, zero_point, mode: int) -> torch.Tensor:
-        """_quantize_tensor (mode 0) / _dequantize_tensor (mode 1) with the reference's
-        broadcasting (awq.py:237-242, 274-279): per dim-0 channel when per_channel and the
-        parameters are 1-D, else torch broadcasting (one parameter per element)."""
+        """_quantize_tensor (mode 0) / _dequantize_tensor (mode 1) as the reference evaluates
+        awq.py:245 / awq.py:282: the per-channel reshape of awq.py:237-242 / 274-279, then
+        torch's broadcasting and type promotion.  The two ops' result dtypes come from torch's
+        own promotion (meta tensors: no data, no compute); the arithmetic runs in
+        awq_apply_params_ex in those dtypes, including the reduced-float rule for one-element
+        parameters (include/awq_hip.h).  Pinned by tests/golden/golden_promote.* (reference
+        calls: bf16 / fp16 tensors with fp32 / fp64 parameters, int32 tensor_q, mixed
+        parameter dtypes, non-per-channel broadcasts)."""
         scale, zero_point = torch.as_tensor(scale), torch.as_tensor(zero_point)
+        per_ch = self.per_channel and tensor.dim() > 1 and scale.dim() == 1
+        if per_ch:                                   # awq.py:238-242 (same errors as the reference)
+            shp = [scale.size(0)] + [1] * (tensor.dim() - 1)
+            scale, zero_point = scale.reshape(shp), zero_point.reshape(shp)
         meta = lambda t: torch.empty(t.shape, dtype=t.dtype, device="meta")
         x_m, s_m, z_m = meta(tensor), meta(scale), meta(zero_point)
-        per_ch = self.per_channel and tensor.dim() > 1 and scale.dim() == 1
-        if per_ch:
-            shp = [scale.size(0)] + [1] * (tensor.dim() - 1)
-            s_m, z_m = s_m.reshape(shp), z_m.reshape(shp)
-        first = (x_m / s_m) if mode == 0 else (x_m - z_m)
+        first = (x_m / s_m) if mode == 0 else (x_m - z_m)       # torch's broadcasting / promotion errors
         res = (first + z_m) if mode == 0 else (first * s_m)
-        if tuple(res.shape) != tuple(tensor.shape):
-            raise NotImplementedError(f"parameters of shape {tuple(scale.shape)} / {tuple(zero_point.shape)} "
-                                      f"broadcast {tuple(tensor.shape)} to {tuple(res.shape)}")
-        if not tensor.is_floating_point():          # e.g. quantize()'s int32 tensor_q: torch casts it
-            tensor = tensor.to(first.dtype)         # to the op's dtype first
-        if first.dtype != tensor.dtype or res.dtype != tensor.dtype:
-            raise NotImplementedError(f"{tensor.dtype} with {scale.dtype} / {zero_point.dtype} parameters promotes "
-                                      f"to {res.dtype}; pass parameters of the tensor's dtype")
-        # (0-d / scalar parameters of another dtype do not promote: they enter the op at their
-        # own value in its compute type, like torch's original_scalar_value — as the kernel does)
-        x = self._on_gpu(tensor)
-        dev = x.device
-        n = x.numel()
-        if scale.numel() == 1 and zero_point.numel() == 1:
-            rows, K, L = 1, n, max(n, 1)
-        elif per_ch:
-            rows = tensor.size(0)
-            K = n // max(rows, 1)
-            L = max(K, 1)
-        else:
-            rows, K, L = 1, n, 1
+        d1, d2, shape = first.dtype, res.dtype, tuple(res.shape)
+        for what, dt in (("tensor", tensor.dtype), ("result", d1), ("result", d2)):
+            if dt not in _hip.APPLY_DTYPE:
+                raise NotImplementedError(f"{what} dtype {dt} (this build computes bf16 / fp16 / fp32 / fp64 / "
+                                          f"int32)")
+        for p in (scale, zero_point):
+            if p.dtype not in self._EXACT_PARAM or p.is_complex():
+                raise NotImplementedError(f"parameter dtype {p.dtype}")
+            if p.dtype == torch.int64 and p.numel() and int(p.abs().max()) > 2 ** 53:
+                raise NotImplementedError("int64 parameters beyond 2^53")
+        dev = self.compute_device()
+        if math.prod(shape) == 0:
+            return self._home(torch.empty(shape, dtype=d2, device=dev))
+        x = tensor.detach().to(dev).contiguous()
         s64 = scale.detach().to(dev, torch.float64)
         z64 = zero_point.detach().to(dev, torch.float64)
-        if L == 1 and rows == 1 and n > 1:            # one parameter per element
-            s64 = s64.expand(tensor.shape).reshape(-1)
-            z64 = z64.expand(tensor.shape).reshape(-1)
-        elif per_ch:
-            s64, z64 = s64.reshape(-1).expand(rows), z64.reshape(-1).expand(rows)
-        out = _hip.apply_params(x, rows, K, L, s64.contiguous(), z64.contiguous(), self.qmin, self.qmax, mode)
-        return self._home(out)
+        n = x.numel()
+        if shape == tuple(tensor.shape) and scale.numel() == 1 and zero_point.numel() == 1:
+            rows, K, L = 1, n, n                     # one parameter pair for the whole tensor
+            s64, z64 = s64.reshape(1), z64.reshape(1)
+        elif shape == tuple(tensor.shape) and per_ch:
+            rows = tensor.size(0)                    # one pair per dim-0 channel
+            K = n // rows
+            L = max(K, 1)
+            s64, z64 = s64.reshape(rows), z64.reshape(rows)
+        else:                                        # any other broadcast: one pair per element
+            x = x.expand(shape).contiguous()
+            s64, z64 = s64.expand(shape).reshape(-1), z64.expand(shape).reshape(-1)
+            rows, K, L = 1, x.numel(), 1
+        flags = ((_hip.APPLY_SCALE_ONE_ELEMENT if scale.numel() == 1 else 0) |
+                 (_hip.APPLY_ZERO_ONE_ELEMENT if zero_point.numel() == 1 else 0))
+        out = _hip.apply_params(x, rows, K, L, s64.contiguous(), z64.contiguous(), self.qmin, self.qmax, mode, d1, d2,
+                                flags)
+        return self._home(out.reshape(shape))
 
     def _quantize_tensor(self, tensor: torch.Tensor, scale: torch.Tensor, zero_point: torch.Tensor) -> torch.Tensor:
         """awq.py:215-250: clamp(round(tensor / scale + zero_point), qmin, qmax), a float

@@ -30,6 +30,7 @@ from __future__ import annotations
 import atexit
 import ctypes
 import math
+import os
 import threading
 import time
 import weakref
@@ -129,11 +130,16 @@ _HIP = None
 
 
 def _hip_runtime():
+    """torch's own HIP runtime (the file torch/lib/libamdhip64.so, soname libamdhip64.so.7,
+    which torch and libawq_hip.so already use), opened by path: a bare "libamdhip64.so" could
+    resolve through the loader's search path to a second runtime."""
     global _HIP
     if _HIP is None:
-        _HIP = ctypes.CDLL("libamdhip64.so")
-        _HIP.hipHostMalloc.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_size_t, ctypes.c_uint]
-        _HIP.hipHostFree.argtypes = [ctypes.c_void_p]
+        path = os.path.join(os.path.dirname(torch.__file__), "lib", "libamdhip64.so")
+        lib = ctypes.CDLL(path)       # OSError when absent: callers fall back
+        lib.hipHostMalloc.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_size_t, ctypes.c_uint]
+        lib.hipHostFree.argtypes = [ctypes.c_void_p]
+        _HIP = lib
     return _HIP
 
 
@@ -178,8 +184,11 @@ def pinned_bytes(nbytes: int) -> torch.Tensor:
     """A uint8 tensor over `nbytes` of page-locked host memory of EXACTLY that size
     (hipHostMalloc; torch's caching host allocator rounds a request up to a power of two,
     pinning up to twice the bytes — the first run's setup cost).  Freed when the last view
-    of it is gone."""
-    hip = _hip_runtime()
+    of it is gone.  Falls back to torch's pinned allocator if the runtime cannot be opened."""
+    try:
+        hip = _hip_runtime()
+    except OSError:
+        return torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)
     p = ctypes.c_void_p()
     rc = hip.hipHostMalloc(ctypes.byref(p), ctypes.c_size_t(max(nbytes, 1)), 0)
     if rc != 0 or not p.value:

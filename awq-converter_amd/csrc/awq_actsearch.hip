@@ -439,10 +439,72 @@ __global__ __launch_bounds__(256) void group_absmax_kernel(const void* __restric
     }
 }
 
+// ---- the table's power function (include/awq_hip.h awq_act_scale_table: "awq_pow") ----
+// x^r from IEEE fp64 +, *, /, fma and rint only, in one fixed order, so that every
+// implementation of the definition (this kernel, oracle_act_scale_table) gets the same bits;
+// a libm pow differs between math libraries in the last ulp.  ~1e-16 relative accuracy.
+namespace detpow {
+constexpr double kLn2Hi = 6.93147180369123816490e-01;   // 0x3FE62E42FEE00000: e * kLn2Hi exact
+constexpr double kLn2Lo = 1.90821492927058770002e-10;
+constexpr double kInvLn2 = 1.44269504088896338700e+00;
+
+__device__ __forceinline__ double two_pow(int n) {       // 2^n, -1022 <= n <= 1023
+    return __longlong_as_double((long long)(n + 1023) << 52);
+}
+
+// ln x, x positive finite: x = m 2^e with m in [sqrt(2)/2, sqrt(2)), f = (m - 1) / (m + 1),
+// ln m = 2f + 2f f^2 P(f^2), P = sum_{j=1..12} f^(2j-2) / (2j + 1) by Horner
+__device__ double log_p(double x) {
+#pragma clang fp contract(off)
+    int e = 0;
+    if (x < 0x1p-1022) { x = x * 0x1p54; e = -54; }            // subnormal: exact rescale
+    const unsigned long long u = (unsigned long long)__double_as_longlong(x);
+    e += (int)((u >> 52) & 0x7FF) - 1023;
+    double m = __longlong_as_double((long long)((u & 0xFFFFFFFFFFFFFull) | 0x3FF0000000000000ull));  // [1, 2)
+    if (m > 1.4142135623730951) { m = m * 0.5; e += 1; }
+    const double f = (m - 1.0) / (m + 1.0);
+    const double f2 = f * f;
+    double p = 1.0 / 25.0;
+    for (int j = 11; j >= 1; --j) p = __builtin_fma(p, f2, 1.0 / (double)(2 * j + 1));
+    const double t = 2.0 * f;
+    const double lm = __builtin_fma(t * f2, p, t);
+    const double de = (double)e;
+    return __builtin_fma(de, kLn2Hi, __builtin_fma(de, kLn2Lo, lm));
+}
+
+// e^y: k = rint(y / ln 2), t = y - k ln 2 (two fma), e^t = 1 + t(1 + t/2(1 + ... (1 + t/15))),
+// times 2^k (two steps below 2^-1022: one rounding, into the subnormals)
+__device__ double exp_p(double y) {
+#pragma clang fp contract(off)
+    if (y != y) return y;
+    if (y > 709.8) return __builtin_inf();
+    if (y < -746.0) return 0.0;
+    const double k = __builtin_rint(y * kInvLn2);
+    double t = __builtin_fma(-k, kLn2Hi, y);
+    t = __builtin_fma(-k, kLn2Lo, t);
+    double p = 1.0;
+    for (int j = 15; j >= 1; --j) p = __builtin_fma(p, t / (double)j, 1.0);
+    const int ki = (int)k;
+    if (ki > 1023) return (p * two_pow(1023)) * two_pow(ki - 1023);
+    if (ki < -1022) return (p * two_pow(ki + 600)) * two_pow(-600);
+    return p * two_pow(ki);
+}
+
+// x^r for x >= 0 (a statistic), r in [0, 1]: C99 pow on the special values
+__device__ double pow_p(double x, double r) {
+#pragma clang fp contract(off)
+    if (r == 0.0) return 1.0;
+    if (x != x || x < 0.0) return __builtin_nan("");
+    if (x == 0.0) return 0.0;
+    if (__builtin_isinf(x)) return x;
+    return exp_p(r * log_p(x));
+}
+}  // namespace detpow
+
 // candidate i's raw scale of channel k (fp64): x_mean^r [/ (w_mean^(1-r) + 1e-4)], >= 1e-4
 __device__ __forceinline__ double raw_scale(const float* x_mean, const float* w_mean, int64_t k, double r) {
-    double s = pow((double)x_mean[k], r);
-    if (w_mean) s = s / (pow((double)w_mean[k], 1.0 - r) + 1e-4);
+    double s = detpow::pow_p((double)x_mean[k], r);
+    if (w_mean) s = s / (detpow::pow_p((double)w_mean[k], 1.0 - r) + 1e-4);
     return s < 1e-4 ? 1e-4 : s;   // NaN stays NaN
 }
 

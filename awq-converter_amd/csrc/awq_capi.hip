@@ -226,15 +226,30 @@ int awq_group_params(const void* w, int dtype, int64_t rows, int64_t K, int64_t 
 int awq_apply_params(const void* x, int dtype, int64_t rows, int64_t K, int64_t group_size, const double* scales,
                      const double* zeros, int qmin, int qmax, int mode, void* out, void* stream) {
     g_err.clear();
+    if (dtype < AWQ_DTYPE_BF16 || dtype > AWQ_DTYPE_F64) return fail(AWQ_EINVAL, "unknown dtype code %d", dtype);
+    // the parameters enter both ops at their own (fp32 / fp64) value: one-element semantics
+    return awq_apply_params_ex(x, dtype, rows, K, group_size, scales, zeros, qmin, qmax, mode, dtype, dtype,
+                               AWQ_APPLY_SCALE_ONE_ELEMENT | AWQ_APPLY_ZERO_ONE_ELEMENT, out, stream);
+}
+
+int awq_apply_params_ex(const void* x, int x_dtype, int64_t rows, int64_t K, int64_t group_size,
+                        const double* scales, const double* zeros, int qmin, int qmax, int mode, int op1_dtype,
+                        int op2_dtype, int flags, void* out, void* stream) {
+    g_err.clear();
     if (group_size <= 0) return fail(AWQ_EINVAL, "Group size must be a positive integer: %lld", (long long)group_size);
     if (rows < 0 || K < 0) return fail(AWQ_EINVAL, "negative shape (%lld, %lld)", (long long)rows, (long long)K);
-    if (dtype < AWQ_DTYPE_BF16 || dtype > AWQ_DTYPE_F64) return fail(AWQ_EINVAL, "unknown dtype code %d", dtype);
     if (mode != 0 && mode != 1) return fail(AWQ_EINVAL, "unknown mode %d (0 quantize, 1 dequantize)", mode);
+    for (int d : {x_dtype, op1_dtype, op2_dtype})
+        if (d < AWQ_DTYPE_BF16 || d > AWQ_DTYPE_I32) return fail(AWQ_EINVAL, "unknown dtype code %d", d);
+    if (mode == 0 && (op1_dtype == AWQ_DTYPE_I32 || op2_dtype == AWQ_DTYPE_I32))
+        return fail(AWQ_EINVAL, "quantize (mode 0) divides: its ops are floating point");
+    if (flags & ~(AWQ_APPLY_SCALE_ONE_ELEMENT | AWQ_APPLY_ZERO_ONE_ELEMENT))
+        return fail(AWQ_EINVAL, "unknown flags 0x%x", flags);
     if (mode == 0 && qmin > qmax) return fail(AWQ_EINVAL, "qmin %d > qmax %d", qmin, qmax);
     if (rows * K == 0) return AWQ_OK;
     if (!x || !scales || !zeros || !out) return fail(AWQ_EINVAL, "null argument");
-    return hip_status(awq::launch_apply(x, dtype, rows, K, group_size, scales, zeros, qmin, qmax, mode, out,
-                                        (hipStream_t)stream), "awq apply params");
+    return hip_status(awq::launch_apply(x, x_dtype, rows, K, group_size, scales, zeros, qmin, qmax, mode, op1_dtype,
+                                        op2_dtype, flags, out, (hipStream_t)stream), "awq apply params");
 }
 
 int64_t awq_plan_ragged(awq_tensor_desc* descs, int n, int bits, int64_t group_size) {

@@ -408,32 +408,100 @@ __global__ __launch_bounds__(64) void awq_f64_span_lds_kernel(const double* __re
     }
 }
 
-// Reference _quantize_tensor (awq.py:215-250, mode 0: clamp(round(RN(RN(x / s) + z))) and
-// _dequantize_tensor (awq.py:252-284, mode 1: RN(RN(x - z) * s)) with caller-given per-group
-// parameters, output in the input dtype.  The parameters (double) enter the op in its
-// compute type (fp32; fp64 for fp64 inputs) without a rounding to the dtype: what torch's
-// CPU kernels do with a 0-d / Python-number operand (its original value), and exact for
-// parameters of the tensor's own dtype.  Group g of row r covers elements [g L, g L + L) of
-// the row; L = 1 is a per-element parameter array (any broadcast).
-template <int DT>
-__global__ __launch_bounds__(256) void awq_apply_kernel(const void* __restrict__ xv, int64_t rows, int64_t K,
+// Reference _quantize_tensor (awq.py:215-250, mode 0: clamp(round(x / s + z))) and
+// _dequantize_tensor (awq.py:252-284, mode 1: (x - z) * s) with caller-given per-group
+// parameters, under torch's type promotion (include/awq_hip.h awq_apply_params_ex): the first
+// op is evaluated in dtype d1, the second in d2 (= the output's dtype), each in torch CPU's
+// per-op way — fp32 math for bf16 / fp16 / fp32 (fp64 for fp64), one rounding to the op's
+// dtype; int32 ops wrap.  An operand of another dtype is converted to the op's dtype first
+// (through fp32 for bf16 / fp16, as c10::convert does), except a one-element parameter of a
+// bf16 / fp16 op, which enters at its own value in fp32 (ATen's original_scalar_value; the
+// flags say which parameter is one).  Values travel as exact doubles between the steps.
+// Group g of row r covers elements [g L, g L + L) of the row; L = 1 is one parameter per
+// element (any broadcast, expanded by the caller).
+namespace apply {
+
+enum Op { kDiv, kAdd, kSub, kMul };
+
+__device__ __forceinline__ double load(const void* x, int dt, int64_t i) {
+    switch (dt) {
+    case AWQ_DTYPE_BF16: return (double)__uint_as_float((uint32_t)((const uint16_t*)x)[i] << 16);
+    case AWQ_DTYPE_F16: return (double)sw_f16_to_f32(((const uint16_t*)x)[i]);
+    case AWQ_DTYPE_F32: return (double)((const float*)x)[i];
+    case AWQ_DTYPE_F64: return ((const double*)x)[i];
+    default: return (double)((const int32_t*)x)[i];
+    }
+}
+
+__device__ __forceinline__ int32_t wrap32(int64_t v) { return (int32_t)(uint32_t)(uint64_t)v; }
+
+// fp32 result of an op rounded to a bf16 / fp16 / fp32 op dtype (a NaN to the dtype's own)
+__device__ __forceinline__ float round_to(float r, int d) {
+    if (d == AWQ_DTYPE_BF16) return __builtin_isnan(r) ? __uint_as_float(0x7FC00000u) : sw_rn_bf16(r);
+    if (d == AWQ_DTYPE_F16) return sw_f16_to_f32(sw_f32_to_f16(r));
+    return r;
+}
+
+// c10::convert of an exactly held value to dtype d
+__device__ __forceinline__ double convert(double v, int d) {
+    if (d == AWQ_DTYPE_F64) return v;
+    if (d == AWQ_DTYPE_I32) return (double)wrap32((int64_t)v);
+    return (double)round_to((float)v, d);
+}
+
+// a parameter as it enters an op of dtype d
+__device__ __forceinline__ double enter(double v, int d, bool one_element) {
+    if (one_element && (d == AWQ_DTYPE_BF16 || d == AWQ_DTYPE_F16)) return (double)(float)v;
+    return convert(v, d);
+}
+
+__device__ __forceinline__ double op(Op o, double a, double b, int d) {
+#pragma clang fp contract(off)
+    if (d == AWQ_DTYPE_I32) {
+        const uint32_t ua = (uint32_t)(int64_t)a, ub = (uint32_t)(int64_t)b;
+        return (double)(int32_t)(o == kSub ? ua - ub : o == kMul ? ua * ub : ua + ub);
+    }
+    if (d == AWQ_DTYPE_F64) return o == kDiv ? a / b : o == kAdd ? a + b : o == kSub ? a - b : a * b;
+    const float fa = (float)a, fb = (float)b;
+    const float r = o == kDiv ? fa / fb : o == kAdd ? fa + fb : o == kSub ? fa - fb : fa * fb;
+    return (double)round_to(r, d);
+}
+
+__device__ __forceinline__ void store(void* out, int d, int64_t i, double v) {
+    switch (d) {
+    case AWQ_DTYPE_BF16: ((uint16_t*)out)[i] = (uint16_t)(__float_as_uint((float)v) >> 16); break;
+    case AWQ_DTYPE_F16: ((uint16_t*)out)[i] = sw_f32_to_f16((float)v); break;
+    case AWQ_DTYPE_F32: ((float*)out)[i] = (float)v; break;
+    case AWQ_DTYPE_F64: ((double*)out)[i] = v; break;
+    default: ((int32_t*)out)[i] = (int32_t)v;
+    }
+}
+
+}  // namespace apply
+
+__global__ __launch_bounds__(256) void awq_apply_kernel(const void* __restrict__ x, int xdt, int64_t rows, int64_t K,
                                                         int64_t L, const double* __restrict__ sp,
                                                         const double* __restrict__ zp, int qmin, int qmax, int mode,
-                                                        void* __restrict__ outv) {
-    typedef Traits<DT> T;
-    typedef typename T::C C;
-    const typename T::S* x = (const typename T::S*)xv;
-    typename T::S* out = (typename T::S*)outv;
+                                                        int d1, int d2, int flags, void* __restrict__ out) {
+    using namespace apply;
+    const bool s_one = (flags & AWQ_APPLY_SCALE_ONE_ELEMENT) != 0, z_one = (flags & AWQ_APPLY_ZERO_ONE_ELEMENT) != 0;
     const int64_t G = (K + L - 1) / L;
     const int64_t total = rows * K;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
          i += (int64_t)gridDim.x * blockDim.x) {
         const int64_t r = i / K, k = i - r * K;
         const int64_t gi = r * G + k / L;
-        const C s = (C)sp[gi], z = (C)zp[gi];
-        const C v = T::load(x, i);
-        const C res = mode == 0 ? quant1<DT>(v, s, z, qmin, qmax) : T::rn(T::rn(v - z) * s);
-        out[i] = T::store(res);
+        const double v = convert(load(x, xdt, i), d1);
+        double t;
+        if (mode == 0) {
+            t = op(kDiv, v, enter(sp[gi], d1, s_one), d1);                          // awq.py:245
+            t = op(kAdd, convert(t, d2), enter(zp[gi], d2, z_one), d2);
+            t = clampq(__builtin_rint(t), (double)qmin, (double)qmax);             // awq.py:248
+        } else {
+            t = op(kSub, v, enter(zp[gi], d1, z_one), d1);                          // awq.py:282
+            t = op(kMul, convert(t, d2), enter(sp[gi], d2, s_one), d2);
+        }
+        store(out, d2, i, t);
     }
 }
 
@@ -874,30 +942,13 @@ hipError_t launch_generic(const void* w, int dtype, int64_t rows, int64_t K, int
     return hipPeekAtLastError();
 }
 
-hipError_t launch_apply(const void* x, int dtype, int64_t rows, int64_t K, int64_t L, const double* scales,
-                        const double* zeros, int qmin, int qmax, int mode, void* out, hipStream_t stream) {
+hipError_t launch_apply(const void* x, int xdt, int64_t rows, int64_t K, int64_t L, const double* scales,
+                        const double* zeros, int qmin, int qmax, int mode, int d1, int d2, int flags, void* out,
+                        hipStream_t stream) {
     const int64_t total = rows * K;
     if (total <= 0) return hipSuccess;
-    const dim3 grid(grid_for(total, 256, 256 * 16)), block(256);
-    switch (dtype) {
-    case AWQ_DTYPE_BF16:
-        hipLaunchKernelGGL((awq_apply_kernel<AWQ_DTYPE_BF16>), grid, block, 0, stream, x, rows, K, L, scales, zeros,
-                           qmin, qmax, mode, out);
-        break;
-    case AWQ_DTYPE_F16:
-        hipLaunchKernelGGL((awq_apply_kernel<AWQ_DTYPE_F16>), grid, block, 0, stream, x, rows, K, L, scales, zeros,
-                           qmin, qmax, mode, out);
-        break;
-    case AWQ_DTYPE_F32:
-        hipLaunchKernelGGL((awq_apply_kernel<AWQ_DTYPE_F32>), grid, block, 0, stream, x, rows, K, L, scales, zeros,
-                           qmin, qmax, mode, out);
-        break;
-    case AWQ_DTYPE_F64:
-        hipLaunchKernelGGL((awq_apply_kernel<AWQ_DTYPE_F64>), grid, block, 0, stream, x, rows, K, L, scales, zeros,
-                           qmin, qmax, mode, out);
-        break;
-    default: return hipErrorInvalidValue;
-    }
+    hipLaunchKernelGGL(awq_apply_kernel, dim3(grid_for(total, 256, 256 * 16)), dim3(256), 0, stream, x, xdt, rows, K,
+                       L, scales, zeros, qmin, qmax, mode, d1, d2, flags, out);
     return hipPeekAtLastError();
 }
 

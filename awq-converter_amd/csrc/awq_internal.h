@@ -195,8 +195,10 @@ hipError_t launch_generic(const void* w, int dtype, int64_t rows, int64_t K, int
                           int32_t* qweight, int32_t* qzeros, hipStream_t stream, bool small, int n_grid = 1,
                           int n_cand = 0, double* s_exact = nullptr,
                           double* z_exact = nullptr);
-hipError_t launch_apply(const void* x, int dtype, int64_t rows, int64_t K, int64_t L, const double* scales,
-                        const double* zeros, int qmin, int qmax, int mode, void* out, hipStream_t stream);
+// x of dtype xdt (AWQ_DTYPE_* incl. I32); first op in d1, second (= out) in d2; flags AWQ_APPLY_*
+hipError_t launch_apply(const void* x, int xdt, int64_t rows, int64_t K, int64_t L, const double* scales,
+                        const double* zeros, int qmin, int qmax, int mode, int d1, int d2, int flags, void* out,
+                        hipStream_t stream);
 // any group size <= 512 (fp32: 256), bf16 / fp16 / fp32, any K; rowgroup_gpt() = 0: not eligible
 int rowgroup_gpt(int dtype, int64_t K, int64_t L);
 hipError_t launch_rowgroup(const void* w, int dtype, int64_t rows, int64_t K, int64_t L, int bits, int symmetric,

@@ -46,10 +46,11 @@
 extern "C" {
 #endif
 
-#define AWQ_HIP_ABI_VERSION 14
+#define AWQ_HIP_ABI_VERSION 15
 
-/* dtype codes of the input weights (torch dtypes the reference accepts, awq.py:397) */
-enum { AWQ_DTYPE_BF16 = 0, AWQ_DTYPE_F16 = 1, AWQ_DTYPE_F32 = 2, AWQ_DTYPE_F64 = 3 };
+/* dtype codes of the input weights (torch dtypes the reference accepts, awq.py:397);
+ * AWQ_DTYPE_I32 only in awq_apply_params_ex (int32 tensor_q and integer ops) */
+enum { AWQ_DTYPE_BF16 = 0, AWQ_DTYPE_F16 = 1, AWQ_DTYPE_F32 = 2, AWQ_DTYPE_F64 = 3, AWQ_DTYPE_I32 = 4 };
 
 /* status codes */
 enum { AWQ_OK = 0, AWQ_EINVAL = 1, AWQ_EUNSUPPORTED = 2, AWQ_EHIP = 3, AWQ_ENODEV = 4 };
@@ -143,6 +144,29 @@ int awq_group_params(const void* w, int dtype, int64_t rows, int64_t K, int64_t 
  *   mode 1: RN(RN(x - z) * s)                             (_dequantize_tensor, awq.py:252-284) */
 int awq_apply_params(const void* x, int dtype, int64_t rows, int64_t K, int64_t group_size, const double* scales,
                      const double* zeros, int qmin, int qmax, int mode, void* out, void* stream);
+
+/* awq_apply_params_ex flags: the scale / zero point is a one-element operand of the
+ * reference's expression (any shape of numel 1) */
+#define AWQ_APPLY_SCALE_ONE_ELEMENT 1
+#define AWQ_APPLY_ZERO_ONE_ELEMENT 2
+
+/* The same two ops with torch's type promotion (ABI 15; replaces awq.py:245 and awq.py:282 for
+ * parameters of any dtype, e.g. bf16 weights with fp32 per-channel scales, or quantize()'s
+ * int32 tensor_q dequantized with fp16 scales):
+ *   mode 0: a = x / s in op1_dtype; t = a + z in op2_dtype; round, clamp(qmin, qmax)
+ *   mode 1: a = x - z in op1_dtype; t = a * s in op2_dtype
+ * op1_dtype / op2_dtype are torch's result dtypes of the two ops (the caller's promotion);
+ * out [rows, K] is op2_dtype.  x_dtype and the op dtypes may also be AWQ_DTYPE_I32 (int32
+ * tensor_q; an int32 op — mode 1 only — wraps like torch's int32 kernels).  Each op: operands
+ * converted to its dtype (c10::convert; bf16 / fp16 through fp32), fp32 math for bf16 / fp16 /
+ * fp32 (fp64 for fp64), result rounded to the dtype — except that a parameter flagged
+ * AWQ_APPLY_*_ONE_ELEMENT enters a bf16 / fp16 op at its own value in fp32 (ATen's reduced-float
+ * kernels read a one-element operand's original value).  scales / zeros: the parameters' exact
+ * values as doubles, [rows, G] as in awq_apply_params (group_size 1 = one per element).
+ * awq_apply_params(x, D, ...) = awq_apply_params_ex(x, D, ..., D, D, both flags, ...). */
+int awq_apply_params_ex(const void* x, int x_dtype, int64_t rows, int64_t K, int64_t group_size,
+                        const double* scales, const double* zeros, int qmin, int qmax, int mode, int op1_dtype,
+                        int op2_dtype, int flags, void* out, void* stream);
 
 /* 1 if awq_quantize_groups writes qweight / qzeros for this dtype / shape without the int32
  * tensor_q / zeros staging buffers.  Since round 2 every kernel does (the generic kernel packs
@@ -387,10 +411,22 @@ int awq_stream_end(void* handle, awq_stream_stats* stats);
  *       (duo scaling only; gmax = max |W| of the group; same fp64 block order, the
  *        linears' blocks in list order; awq_weight_colsum per linear + awq_column_mean)
  *   candidate i = 0 .. n_grid-1, r = i / n_grid (fp64):
- *       raw_k = max(x_mean_k^r [/ (w_mean_k^(1-r) + 1e-4)], 1e-4)
+ *       raw_k = max(awq_pow(x_mean_k, r) [/ (awq_pow(w_mean_k, 1-r) + 1e-4)], 1e-4)
  *       s_i[k] = fp32(raw_k / sqrt(max_k raw * min_k raw)), inf / NaN -> 1
- *       (awq_act_scale_table, fp64 pow / sqrt: the only step not bit-reproducible across
- *        math libraries; callers check it to 1 fp32 ulp and feed the table downstream)
+ *       (awq_act_scale_table; fp64, IEEE-rounded / and sqrt)
+ *   awq_pow(x, r) (round 5; not libm pow, whose last bit differs between math libraries):
+ *       r == 0 -> 1; NaN or x < 0 -> NaN; x == 0 -> 0; x == inf -> inf; else, in IEEE fp64
+ *       with explicit fma and no other contraction:
+ *       ln x: x = m 2^e, m in [sqrt(2)/2, sqrt(2)) (subnormal x scaled by 2^54 first),
+ *             f = (m-1)/(m+1); P = 1/25, P = fma(P, f*f, 1/(2j+1)) for j = 11 .. 1;
+ *             ln m = fma(2f * (f*f), P, 2f); ln x = fma(e, LN2_HI, fma(e, LN2_LO, ln m))
+ *             (LN2_HI = 0x1.62e42feep-1, LN2_LO = 1.90821492927058770002e-10)
+ *       e^y:  k = rint(y * 1.44269504088896338700), t = fma(-k, LN2_LO, fma(-k, LN2_HI, y)),
+ *             p = 1, p = fma(p, t / j, 1) for j = 15 .. 1; result p * 2^k (k > 1023:
+ *             (p 2^1023) 2^(k-1023); k < -1022: (p 2^(k+600)) 2^-600; y > 709.8 -> inf,
+ *             y < -746 -> 0)
+ *       x^r = e^(r * ln x) — within 2^-40 of x^r over the fp32 range, and the same bits in
+ *       every implementation (oracle_act_scale_table restates it)
  *   per element of every group, in the weight dtype D's per-op rounding:
  *       w' = RN_D(w * s_i[k]); RTN scale/zero of w' (awq.py:173-213); q (awq.py:245-248);
  *       dq = fp16(fp16(q - z) * fp16(scale)) (awq.py:459-539); e = fp32(dq / s_i[k]) - w;

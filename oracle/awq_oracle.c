@@ -337,6 +337,67 @@ int oracle_apply_params(const void* x, int dtype, int64_t rows, int64_t K, int64
     return 0;
 }
 
+/* awq.py:245 and awq.py:282 under torch's type promotion (round 5): the two ops of
+ *   mode 0  round(tensor / scale + zero_point).clamp(qmin, qmax)
+ *   mode 1  (tensor_q - zero_point) * scale
+ * are evaluated in their own result dtypes d1 (first op) and d2 (second op) — torch's
+ * result_type of the operands — one element per parameter (the caller has broadcast
+ * everything to the result's shape).  An operand of another dtype is converted to the op's
+ * dtype first (c10::convert: through fp32 for bf16 / fp16), EXCEPT a one-element parameter
+ * of a bf16 / fp16 op (flags bit 0: scale, bit 1: zero_point), which ATen's reduced-float
+ * kernels read at its original value in fp32 (TensorIterator::original_scalar_value) —
+ * checked against torch on CPU by tests/golden/golden_promote.* (reference calls).
+ * Dtype codes: the four float codes + AWQ_ORACLE_I32 (an int32 tensor_q, an int32 first op
+ * of mode 1: wrap-around arithmetic like torch's int32 kernels). */
+static inline double load_any(const void* x, int dtype, int64_t i) {
+    if (dtype == AWQ_ORACLE_I32) return (double)((const int32_t*)x)[i];
+    return load_elem(x, dtype, i);
+}
+static inline double wrap_i32(double v) { return (double)(int32_t)(uint32_t)(uint64_t)(int64_t)v; }
+static inline double convert_to(double v, int d) {          /* v held exactly */
+    if (d == AWQ_ORACLE_I32) return wrap_i32(v);
+    return d == AWQ_ORACLE_F64 ? v : rn((double)(float)v, d);
+}
+static inline double enter(double v, int d, int one_element) {
+    if (one_element && (d == AWQ_ORACLE_BF16 || d == AWQ_ORACLE_F16)) return (double)(float)v;
+    return convert_to(v, d);
+}
+static double op2(char op, double a, double b, int d) {
+    if (d == AWQ_ORACLE_I32) {
+        int64_t ia = (int64_t)a, ib = (int64_t)b;
+        return wrap_i32((double)(op == '-' ? ia - ib : op == '*' ? ia * ib : ia + ib));
+    }
+    if (d == AWQ_ORACLE_F64)
+        return op == '/' ? a / b : op == '-' ? a - b : op == '*' ? a * b : a + b;
+    float fa = (float)a, fb = (float)b;
+    float r = op == '/' ? fa / fb : op == '-' ? fa - fb : op == '*' ? fa * fb : fa + fb;
+    return rn((double)r, d);
+}
+static inline void store_any(void* out, int dtype, int64_t i, double v) {
+    if (dtype == AWQ_ORACLE_I32) ((int32_t*)out)[i] = (int32_t)v;
+    else store_elem(out, dtype, i, v);
+}
+int oracle_apply_params_ex(const void* x, int xdt, int64_t n, const double* scales, const double* zeros, int qmin,
+                           int qmax, int mode, int d1, int d2, int flags, void* out) {
+    if (!x || !scales || !zeros || !out || n < 0 || xdt < 0 || xdt > AWQ_ORACLE_I32 || d1 < 0 ||
+        d1 > AWQ_ORACLE_I32 || d2 < 0 || d2 > AWQ_ORACLE_I32 || (mode == 0 && (d1 == AWQ_ORACLE_I32 ||
+        d2 == AWQ_ORACLE_I32)))
+        return -1;
+    for (int64_t i = 0; i < n; ++i) {
+        double v = convert_to(load_any(x, xdt, i), d1), t;
+        if (mode == 0) {
+            t = op2('/', v, enter(scales[i], d1, flags & 1), d1);                       /* awq.py:245 */
+            t = op2('+', convert_to(t, d2), enter(zeros[i], d2, flags & 2), d2);
+            t = op_clamp(op_round(t, d2), qmin, qmax);                                  /* awq.py:248 */
+        } else {
+            t = op2('-', v, enter(zeros[i], d1, flags & 2), d1);                        /* awq.py:282 */
+            t = op2('*', convert_to(t, d2), enter(scales[i], d2, flags & 1), d2);
+        }
+        store_any(out, d2, i, t);
+    }
+    return 0;
+}
+
 /* Opt-in clip search (scale_method="search").  NOT in the reference (it stores
  * scale_method, awq.py:66, validates it, :111-112, and never reads it again), so this
  * restates the product's own definition (include/awq_hip.h, awq_quantize_search) — parity
@@ -601,11 +662,74 @@ int oracle_column_mean(const double* partial, int64_t nblk, int64_t K, double di
     return 0;
 }
 
+/* The scale table's power function as include/awq_hip.h defines it (round 5): not libm pow,
+ * whose last bit differs between math libraries, but a fixed sequence of IEEE fp64 +, *, /,
+ * fma and rint (this file is built with -ffp-contract=off, so the only fused ops are the
+ * explicit fma() calls):
+ *   ln x:  x = m 2^e, m in [sqrt(2)/2, sqrt(2)) (subnormal x rescaled by 2^54 first);
+ *          f = (m - 1) / (m + 1); P = 1/25, then P = fma(P, f^2, 1/(2j+1)) for j = 11 .. 1;
+ *          ln m = fma(2f * f^2, P, 2f); ln x = fma(e, LN2_HI, fma(e, LN2_LO, ln m))
+ *   e^y:   k = rint(y * INV_LN2); t = fma(-k, LN2_LO, fma(-k, LN2_HI, y));
+ *          p = 1, then p = fma(p, t / j, 1) for j = 15 .. 1; p * 2^k (k > 1023: p 2^1023 2^(k-1023);
+ *          k < -1022: (p 2^(k+600)) 2^-600); y > 709.8 -> inf, y < -746 -> 0, NaN -> NaN
+ *   x^r:   r == 0 -> 1; NaN or negative x -> NaN; 0 -> 0; inf -> inf; else e^(r * ln x) */
+static const double DET_LN2_HI = 6.93147180369123816490e-01, DET_LN2_LO = 1.90821492927058770002e-10,
+                    DET_INV_LN2 = 1.44269504088896338700e+00;
+
+static double det_pow2(int n) {
+    uint64_t b = (uint64_t)(n + 1023) << 52;
+    double d;
+    memcpy(&d, &b, 8);
+    return d;
+}
+
+static double det_log(double x) {
+    int e = 0;
+    if (x < 0x1p-1022) { x *= 0x1p54; e = -54; }
+    uint64_t u;
+    memcpy(&u, &x, 8);
+    e += (int)((u >> 52) & 0x7FF) - 1023;
+    uint64_t mb = (u & 0xFFFFFFFFFFFFFull) | 0x3FF0000000000000ull;
+    double m;
+    memcpy(&m, &mb, 8);
+    if (m > 1.4142135623730951) { m *= 0.5; e += 1; }
+    double f = (m - 1.0) / (m + 1.0), f2 = f * f, P = 1.0 / 25.0;
+    for (int j = 11; j >= 1; --j) P = fma(P, f2, 1.0 / (double)(2 * j + 1));
+    double t = 2.0 * f;
+    double lm = fma(t * f2, P, t);
+    return fma((double)e, DET_LN2_HI, fma((double)e, DET_LN2_LO, lm));
+}
+
+static double det_exp(double y) {
+    if (isnan(y)) return y;
+    if (y > 709.8) return INFINITY;
+    if (y < -746.0) return 0.0;
+    double k = rint(y * DET_INV_LN2);
+    double t = fma(-k, DET_LN2_LO, fma(-k, DET_LN2_HI, y));
+    double p = 1.0;
+    for (int j = 15; j >= 1; --j) p = fma(p, t / (double)j, 1.0);
+    int ki = (int)k;
+    if (ki > 1023) return (p * det_pow2(1023)) * det_pow2(ki - 1023);
+    if (ki < -1022) return (p * det_pow2(ki + 600)) * det_pow2(-600);
+    return p * det_pow2(ki);
+}
+
+static double det_pow(double x, double r) {
+    if (r == 0.0) return 1.0;
+    if (isnan(x) || x < 0.0) return NAN;
+    if (x == 0.0) return 0.0;
+    if (isinf(x)) return x;
+    return det_exp(r * det_log(x));
+}
+
 static double act_raw(const float* x_mean, const float* w_mean, int64_t k, double r) {
-    double s = pow((double)x_mean[k], r);
-    if (w_mean) s = s / (pow((double)w_mean[k], 1.0 - r) + 1e-4);
+    double s = det_pow((double)x_mean[k], r);
+    if (w_mean) s = s / (det_pow((double)w_mean[k], 1.0 - r) + 1e-4);
     return s < 1e-4 ? 1e-4 : s;   /* NaN stays NaN */
 }
+
+/* exported for the tests: det_pow against libm pow */
+double oracle_det_pow(double x, double r) { return det_pow(x, r); }
 
 int oracle_act_scale_table(const float* x_mean, const float* w_mean, int64_t K, int n_grid, float* table) {
     if (!x_mean || !table || K <= 0 || n_grid < 1) return -1;

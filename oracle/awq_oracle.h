@@ -28,6 +28,12 @@ int oracle_group_params(const void* x, int dtype, int64_t rows, int64_t K, int64
 /* awq.py:215-250 (mode 0) / 252-284 (mode 1) with given per-group parameters; out in dtype */
 int oracle_apply_params(const void* x, int dtype, int64_t rows, int64_t K, int64_t L, const double* scales,
                         const double* zeros, int qmin, int qmax, int mode, void* out);
+/* the same ops under torch's type promotion: x of dtype xdt (float codes or AWQ_ORACLE_I32),
+ * first op in d1, second in d2 (= out dtype), one parameter per element; flags bit 0 / 1: the
+ * scale / zero_point is a one-element operand (original value in a bf16 / fp16 op) */
+enum { AWQ_ORACLE_I32 = 4 };
+int oracle_apply_params_ex(const void* x, int xdt, int64_t n, const double* scales, const double* zeros, int qmin,
+                           int qmax, int mode, int d1, int d2, int flags, void* out);
 int oracle_dequantize(const int32_t* tensor_q, const uint16_t* scales_f16, const int32_t* zeros,
                       int64_t rows, int64_t K, int64_t L, float* out);
 int oracle_pack_rows(const int32_t* v, int64_t rows, int64_t n, int bits, int qmin, int32_t* packed);
@@ -37,6 +43,8 @@ int oracle_act_stats(const void* x, int dtype, int64_t T, int64_t K, float* x_me
 int oracle_weight_colsum(const void* w, int dtype, int64_t R, int64_t K, int64_t L, double* partial);
 int oracle_column_mean(const double* partial, int64_t nblk, int64_t K, double divisor, float* out);
 int oracle_act_scale_table(const float* x_mean, const float* w_mean, int64_t K, int n_grid, float* table);
+/* the table's power function (include/awq_hip.h awq_pow definition) */
+double oracle_det_pow(double x, double r);
 int oracle_act_search_losses(const void* w, int dtype, int64_t R, int64_t K, int64_t L, int bits, int sym,
                              const float* table, int n_grid, const float* x_sq, float* part, int64_t stride);
 int oracle_act_search_select(const float* part, int n_grid, int64_t stride, double* losses, int32_t* best);

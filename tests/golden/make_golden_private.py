@@ -13,6 +13,10 @@ writes inputs + outputs as data:
   tests/golden/golden_private.json          per-call method, parameters and tensor keys
 
 Re-run with:  PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden_private.py
+
+--promote (round 5): calls of _quantize_tensor / _dequantize_tensor whose parameters promote
+the tensor's dtype or broadcast it other than per channel -> golden_promote.{safetensors,json}
+(main_promote below).
 """
 import json
 import logging
@@ -98,5 +102,105 @@ def main():
     print(f"{n} calls, {len(tensors)} tensors")
 
 
+def promote_variants(x, s, z, gen):
+    """(name, scale, zero_point) parameter sets for the dtype-promotion / broadcast fixtures:
+    the reference's own parameters cast to every dtype, jittered off the narrow dtypes'
+    grids (so 'enters at its own value' and 'rounded to the op dtype' give different bits),
+    one-element and 0-d forms, integer zero points, mixed scale / zero dtypes, and broadcasts
+    that are not per-channel."""
+    jit = lambda t: t.double() * (1 + (torch.rand(t.shape, generator=gen, dtype=torch.float64) - 0.5) * 2 ** -7)
+    first = lambda t: t.reshape(-1)[:1]
+    out = []
+    for pn, pdt in DTYPES.items():
+        if pdt != x.dtype:
+            out.append((f"cast_{pn}", s.to(pdt), z.to(pdt)))
+        out.append((f"jit_{pn}", jit(s).to(pdt), z.to(pdt)))
+        out.append((f"0d_{pn}", jit(first(s)).reshape(()).to(pdt), first(z).reshape(()).to(pdt)))
+        out.append((f"1el_{pn}", jit(first(s)).to(pdt), first(z).to(pdt)))
+    out.append(("z_i32", jit(s).float(), z.to(torch.int32)))
+    out.append(("z_i64_0d", jit(first(s)).reshape(()).half(), torch.tensor(3, dtype=torch.int64)))
+    out.append(("s_f16_z_bf16", jit(s).half(), z.bfloat16()))
+    out.append(("s_bf16_z_f64", jit(s).bfloat16(), z.double()))
+    if x.dim() >= 2:
+        R, C = x.shape[0], x.shape[-1]
+        col = lambda n, dt: (0.01 + torch.rand(n, generator=gen, dtype=torch.float64) * 0.05).to(dt)
+        zc = lambda n, dt: torch.randint(0, 15, (n,), generator=gen).to(dt)
+        out.append(("bc_rowcol_f32", col(R, torch.float32).reshape([R] + [1] * (x.dim() - 1)),
+                    zc(R, torch.float32).reshape([R] + [1] * (x.dim() - 1))))
+        out.append(("bc_lastdim_own", col(C, x.dtype), zc(C, x.dtype)))
+        out.append(("bc_lastdim_f64", col(C, torch.float64), zc(C, torch.int32)))
+        out.append(("bc_1xC_Rx1", col(C, x.dtype).reshape(1, C) if x.dim() == 2 else col(C, x.dtype),
+                    zc(R, torch.float16).reshape([R] + [1] * (x.dim() - 1))))
+        out.append(("bc_elem_i32z", jit(first(s)).reshape(()).float(),
+                    torch.randint(0, 15, tuple(x.shape), generator=gen, dtype=torch.int32)))
+        out.append(("bad_rows", col(R + 1, torch.float32), zc(R + 1, torch.float32)))
+    else:
+        out.append(("bc_grow_4x1", (0.01 + torch.rand(4, 1, generator=gen) * 0.05).to(x.dtype),
+                    torch.randint(0, 15, (4, 1), generator=gen).to(torch.float32)))
+    return out
+
+
+def main_promote():
+    """Reference calls of _quantize_tensor / _dequantize_tensor whose parameters promote the
+    tensor's dtype (awq.py:245 tensor / scale + zero_point, awq.py:282 (tensor_q - zero_point)
+    * scale evaluated with torch's type promotion) or broadcast it other than per channel,
+    plus int32 tensor_q (quantize()'s dtype) dequantized with float parameters.  Calls that
+    raise in the reference are recorded with the exception type.
+      tests/golden/golden_promote.safetensors / golden_promote.json"""
+    tensors, calls = {}, []
+    gen = torch.Generator().manual_seed(5150)
+
+    def put(key, t):
+        tensors[key] = t.detach().contiguous().clone()
+        return key
+
+    def rec(method, params, xk, sk, zk, fn, out_key):
+        c = {"method": method, "params": params, "x": xk, "scale": sk, "zero_point": zk}
+        try:
+            c["out"] = [put(out_key, fn())]
+        except Exception as e:   # the reference raises: record the behaviour
+            c["raises"] = type(e).__name__
+            c["message"] = str(e)
+        calls.append(c)
+        return c
+
+    qparams = [{"bits": 4, "group_size": 128, "symmetric": False, "per_channel": True},
+               {"bits": 4, "group_size": 128, "symmetric": False, "per_channel": False},
+               {"bits": 8, "group_size": 128, "symmetric": True, "per_channel": True}]
+    for dn, dt in DTYPES.items():
+        edge = edge_rows_f32()[:8, 100:124].to(dt)
+        inputs = {"edge8x24": edge, "r6x24": rand_input((6, 24), 31, dt), "t3x2x8": rand_input((3, 2, 8), 32, dt),
+                  "v40": rand_input((40,), 33, dt, 0.02)}
+        for qi, params in enumerate(qparams):
+            q = AWQQuantizer(device="cpu", **params)
+            for name, x in inputs.items():
+                if name == "edge8x24" and qi != 0:
+                    continue
+                xk = put(f"in.{dn}.{name}", x)
+                s, z = q._calculate_scale_zp(x)
+                for vn, sv, zv in promote_variants(x, s, z, gen):
+                    base = f"{dn}.q{qi}.{name}.{vn}"
+                    sk, zk = put(f"{base}.s", sv), put(f"{base}.z", zv)
+                    c = rec("_quantize_tensor", params, xk, sk, zk, lambda: q._quantize_tensor(x, sv, zv), f"{base}.qt")
+                    if "out" not in c:
+                        continue
+                    q2 = tensors[c["out"][0]]
+                    rec("_dequantize_tensor", params, c["out"][0], sk, zk, lambda: q._dequantize_tensor(q2, sv, zv),
+                        f"{base}.dqt")
+                    qi32 = put(f"{base}.qt_i32", torch.nan_to_num(q2.double(), nan=0.0).to(torch.int32))
+                    rec("_dequantize_tensor", params, qi32, sk, zk,
+                        lambda: q._dequantize_tensor(tensors[qi32], sv, zv), f"{base}.dqt_i32")
+    save_file(tensors, os.path.join(HERE, "golden_promote.safetensors"))
+    with open(os.path.join(HERE, "golden_promote.json"), "w") as f:
+        json.dump({"generator": "tests/golden/make_golden_private.py --promote", "torch": torch.__version__,
+                   "reference": "shanefitch/AWQ-Converter src/awq_quantizer/quantization/awq.py:215-284",
+                   "calls": calls}, f, indent=0)
+    raised = sum("raises" in c for c in calls)
+    print(f"{len(calls)} calls ({raised} raise), {len(tensors)} tensors")
+
+
 if __name__ == "__main__":
-    main()
+    if "--promote" in sys.argv[1:]:
+        main_promote()
+    else:
+        main()

@@ -750,6 +750,78 @@ def test_native_stream_bounded_rings_wrap(tmp_path, monkeypatch, fmt):
 
 @pytest.mark.gpu
 @pytest.mark.skipif(not torch.cuda.is_available(), reason="needs the GPU")
+def test_native_stream_rings_wrap_with_failing_tensors(tmp_path, monkeypatch):
+    """the host ring's sizing relies on ChunkWriter.predict_groups() placing chunks
+    as the writer later does.  A float tensor the kernels do not take (float8: fails on the
+    per-tensor path, before the pipeline's items), an int32 tensor and a sub-group tensor
+    (both filtered by the CLI, main.py:241-253) next to the wrapping 64 KiB rings: every
+    chunk, and metadata.json, still hold exactly the successful tensors' oracle results."""
+    if not hasattr(torch, "float8_e4m3fn"):
+        pytest.skip("no float8 in this torch")
+    from oracle import awq_oracle as orc
+    from awq_quantizer import main as M
+    tensors = _ring_model()
+    g = torch.Generator().manual_seed(12)
+    extra = {"f8": (torch.randn(48, 256, generator=g) * 0.02).to(torch.float8_e4m3fn),
+             "ints": torch.randint(-5, 5, (64, 128), generator=g, dtype=torch.int32),
+             "small": (torch.randn(100, generator=g) * 0.02).to(torch.bfloat16)}
+    d = _model_dir(tmp_path, {**tensors, **extra}, files=3)
+    for k, v in (("slot_bytes", 64 << 10), ("host_ring_bytes", 64 << 10), ("dev_ring_bytes", 64 << 10)):
+        monkeypatch.setitem(M.STREAM_OPTS, k, v)
+    out = tmp_path / "out"
+    M.TIMINGS.clear()
+    assert M.main(["--model_id", d, "--output_dir", str(out), "--log_level", "ERROR", "--chunk_size", "3",
+                   "--output_format", "packed"]) == 0
+    (st,) = [v for k, v in M.TIMINGS.items() if k.startswith("stream_")]
+    assert st["host_wraps"] and st["dev_wraps"], st
+    meta = json.load(open(out / "metadata.json"))
+    assert meta["num_tensors"] == len(tensors) and sorted(meta["tensor_to_chunk"]) == sorted(tensors)
+    counts = {}
+    for name, ci in meta["tensor_to_chunk"].items():
+        counts[ci] = counts.get(ci, 0) + 1
+        res = _load_chunk(out, ci, False)[name]
+        x = tensors[name]
+        ref = orc.quantize(x, bits=4, group_size=128, symmetric=False)
+        rows = 1 if x.dim() <= 1 else x.shape[0]
+        assert torch.equal(res["qweight"], orc.pack_rows(ref["tensor_q"].reshape(rows, -1), 4, 0)), name
+        assert torch.equal(res["scales"].view(torch.int16), ref["scales"].view(torch.int16)), name
+    assert sorted(counts.values())[1:] == [3] * (len(counts) - 1)      # full chunks but the last
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not torch.cuda.is_available(), reason="needs the GPU")
+def test_native_stream_failed_chunk_write_does_not_hang(tmp_path, monkeypatch):
+    """a chunk write that raises (ENOSPC, I/O error) while the host
+    ring wraps used to leave the pipeline waiting forever for a release.  Now the failed
+    chunk's range is released, the producer stops at its next result, and main() returns
+    non-zero — within seconds."""
+    import threading as th
+    from awq_quantizer import main as M
+    d = _model_dir(tmp_path, _ring_model(), files=3)
+    for k, v in (("slot_bytes", 64 << 10), ("host_ring_bytes", 64 << 10), ("dev_ring_bytes", 64 << 10)):
+        monkeypatch.setitem(M.STREAM_OPTS, k, v)
+    real = M._write_chunk
+    calls = []
+
+    def failing(chunk, output_dir, c, *a, **kw):
+        calls.append(c)
+        if c == 2:
+            raise OSError(28, "No space left on device (injected)")
+        return real(chunk, output_dir, c, *a, **kw)
+
+    monkeypatch.setattr(M, "_write_chunk", failing)
+    rc = []
+    t = th.Thread(target=lambda: rc.append(M.main(["--model_id", d, "--output_dir", str(tmp_path / "out"),
+                                                  "--log_level", "CRITICAL", "--chunk_size", "3",
+                                                  "--output_format", "packed"])), daemon=True)
+    t.start()
+    t.join(90)
+    assert not t.is_alive(), "main() hung after a failed chunk write"
+    assert rc == [1] and 2 in calls
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not torch.cuda.is_available(), reason="needs the GPU")
 def test_cli_search_native_engine_equals_python_engine(tmp_path):
     """--scale_method search through the default (native) engine runs the clip
     search (awq_quantize_search_ex per piece), with the Python engine's exact bits — and

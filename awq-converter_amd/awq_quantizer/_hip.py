@@ -103,6 +103,7 @@ SIGNATURES = {
     "awq_plan_block_tensor": (_I64, [ctypes.POINTER(TensorDesc), _I32, _I64, _P, _I64]),
     "awq_ragged_flags": (_I32, [ctypes.POINTER(TensorDesc), _I32, _I64]),
     "awq_quantize_ragged": (_I32, [_P, _I32, _I64, _P, _I32, _I32, _I32, _I64, _I32, _P]),
+    "awq_quantize_ragged_search": (_I32, [_P, _I32, _I64, _P, _I32, _I32, _I32, _I64, _I32, _I32, _I32, _P]),
     "awq_dequantize": (_I32, [_P, _P, _P, _I64, _I64, _I64, _P, _P]),
     "awq_dequantize_packed": (_I32, [_P, _P, _P, _I64, _I64, _I64, _I32, _I32, _P, _P]),
     "awq_pack_rows": (_I32, [_P, _I64, _I64, _I32, _I32, _P, _P]),
@@ -351,7 +352,15 @@ def plan_block_tensor(descs, total_tiles: int, device: torch.device) -> torch.Te
 
 def quantize_ragged(descs_dev: torch.Tensor, n: int, total_tiles: int, bits: int, symmetric: bool,
                     stream: int, block_tensor: Optional[torch.Tensor] = None,
-                    dtype: torch.dtype = torch.bfloat16, group_size: int = 128, flags: int = 0) -> None:
+                    dtype: torch.dtype = torch.bfloat16, group_size: int = 128, flags: int = 0,
+                    search: Optional[tuple] = None) -> None:
+    """One ragged launch; search = (n_grid, n_candidates): the clip search (scale_method="search")."""
+    if search is not None and search[1] > 1:
+        rc = load_library().awq_quantize_ragged_search(ptr(descs_dev), n, total_tiles, ptr(block_tensor),
+                                                       AWQ_DTYPE[dtype], bits, int(bool(symmetric)), group_size,
+                                                       flags, int(search[0]), int(search[1]), ctypes.c_void_p(stream))
+        check(rc, "awq_quantize_ragged_search")
+        return
     rc = load_library().awq_quantize_ragged(ptr(descs_dev), n, total_tiles, ptr(block_tensor), AWQ_DTYPE[dtype],
                                             bits, int(bool(symmetric)), group_size, flags, ctypes.c_void_p(stream))
     check(rc, "awq_quantize_ragged")

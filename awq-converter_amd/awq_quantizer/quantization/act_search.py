@@ -50,7 +50,8 @@ def search_layer_group(weights: Dict[str, torch.Tensor], device: torch.device, *
                        x_sq: Optional[torch.Tensor] = None, table: Optional[torch.Tensor] = None) -> dict:
     """Run the search on the device; returns device tensors
     {"x_mean", "x_sq", "w_mean", "table", "losses", "best", "input_scale", "scaled": {name: W·diag(s)}}.
-    `table` overrides the scale table (tests: a table shared with the oracle)."""
+    `table` overrides the scale table (a caller's own table; since round 5 the kernel's table
+    is bit-exact with the oracle's from the inputs alone, include/awq_hip.h awq_pow)."""
     K = _check_group(weights, group_size)
     if not 1 <= n_grid <= _hip.ACT_MAX_GRID:
         raise ValueError(f"search_grid must be in [1, {_hip.ACT_MAX_GRID}] for scale_method='awq': {n_grid}")

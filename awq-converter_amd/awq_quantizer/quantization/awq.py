@@ -129,6 +129,10 @@ class AWQQuantizer:
             return 0
         return min(self.search_grid, max(1, int(self.search_max_shrink * self.search_grid)))
 
+    def _search_args(self):
+        """(n_grid, n_candidates) of scale_method="search" for ragged launches, else None."""
+        return (self.search_grid, self.search_candidates) if self.search_candidates > 1 else None
+
     def _launch(self, x, rows, K, L, small: bool = False, **outs) -> None:
         if self.scale_method == "search":
             _hip.quantize_search(x, rows, K, L, self.bits, self.symmetric, self.search_grid,
@@ -431,8 +435,9 @@ class AWQQuantizer:
 
     def quantize_model_packed(self, tensors: Dict[str, torch.Tensor]) -> Dict[str, Dict[str, torch.Tensor]]:
         """Packed quantization of many tensors: the fast-path-eligible tensors (bf16, fp16 or fp32,
-        group_size 32/64/128/256, K % group_size == 0) go into one ragged launch per dtype; the rest are
-        quantized one by one.  Outputs stay on the device.  Failures are logged and skipped."""
+        group_size 32/64/128/256, K % group_size == 0) go into one ragged launch per dtype (with the
+        clip search when scale_method="search"); the rest are quantized one by one.  Outputs stay
+        on the device.  Failures are logged and skipped."""
         from .batch import PackedBatch
         self._check_mode()
         eligible, rest = {}, {}
@@ -446,8 +451,7 @@ class AWQQuantizer:
                 self.logger.error(f"Error quantizing tensor: {name}, error: numel < group_size")
                 continue
             rows = 1 if t.dim() <= 1 else t.shape[0]
-            if not self.search_candidates and _hip.ragged_eligible(t.dtype, rows, t.numel() // rows,
-                                                                   self.group_size):
+            if _hip.ragged_eligible(t.dtype, rows, t.numel() // rows, self.group_size):
                 eligible[name] = t
             else:
                 rest[name] = t
@@ -458,7 +462,8 @@ class AWQQuantizer:
                 part = {k: _device_input(v, dev) for k, v in eligible.items() if v.dtype == dt}
                 if part:
                     try:
-                        batch = PackedBatch(part, bits=self.bits, symmetric=self.symmetric, group_size=self.group_size)
+                        batch = PackedBatch(part, bits=self.bits, symmetric=self.symmetric, group_size=self.group_size,
+                                            search=self._search_args())
                         batch.run()
                         out.update(batch.results())
                     except Exception as e:   # the batch as a whole failed: every tensor on its own
@@ -490,7 +495,7 @@ class AWQQuantizer:
                 self.logger.error(f"Error quantizing tensor: {name}, error: {e}")
                 continue
             rows = 1 if t.dim() <= 1 else t.shape[0]
-            if (not self.search_candidates and t.numel() >= self.group_size
+            if (t.numel() >= self.group_size
                     and _hip.ragged_eligible(t.dtype, rows, t.numel() // rows, self.group_size)):
                 eligible[name] = t
             else:
@@ -506,7 +511,7 @@ class AWQQuantizer:
                     continue
                 try:
                     batch = PackedBatch(part, bits=self.bits, symmetric=self.symmetric, parity=True, packed=False,
-                                        group_size=self.group_size)
+                                        group_size=self.group_size, search=self._search_args())
                     batch.run()
                     res = batch.results()
                 except Exception as e:   # the batch as a whole failed: every tensor on its own

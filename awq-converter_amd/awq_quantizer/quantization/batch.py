@@ -23,14 +23,18 @@ class PackedBatch:
     zero_points (6.05 B/element of output traffic instead of 0.52).
     use_block_table: upload the per-workgroup tensor table (awq_plan_block_tensor; 4 B per
     4 tiles) so no wave has to search the descriptors.
+    search: (n_grid, n_candidates) runs the clip search of scale_method="search" in the same
+    one launch (awq_quantize_ragged_search; the bits of awq_quantize_search per tensor).
     """
 
     def __init__(self, inputs: Dict[str, torch.Tensor], bits: int = 4, symmetric: bool = False,
-                 parity: bool = False, packed: bool = True, use_block_table: bool = True, group_size: int = 128):
+                 parity: bool = False, packed: bool = True, use_block_table: bool = True, group_size: int = 128,
+                 search: Optional[tuple] = None):
         if not inputs:
             raise ValueError("PackedBatch needs at least one tensor")
         self.bits, self.symmetric, self.parity = bits, bool(symmetric), parity
         self.group_size = gs = int(group_size)
+        self.search = tuple(search) if search is not None and search[1] > 1 else None
         self.names = list(inputs)
         first = next(iter(inputs.values()))
         dev, self.dtype = first.device, first.dtype
@@ -81,7 +85,8 @@ class PackedBatch:
         if s != self._stream0:       # the kernel reads the uploaded tables (raw output pointers)
             s.wait_event(self._ready)
         _hip.quantize_ragged(self.descs_dev, len(self.descs), self.total_tiles, self.bits, self.symmetric,
-                             s.cuda_stream, self.block_tensor, self.dtype, self.group_size, self.flags)
+                             s.cuda_stream, self.block_tensor, self.dtype, self.group_size, self.flags,
+                             search=self.search)
 
     def results(self) -> Dict[str, Dict[str, torch.Tensor]]:
         res = {}

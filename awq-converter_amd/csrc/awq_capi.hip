@@ -336,6 +336,31 @@ int awq_quantize_ragged(const awq_tensor_desc* descs_device, int n, int64_t tota
                       "awq ragged kernel");
 }
 
+int awq_quantize_ragged_search(const awq_tensor_desc* descs_device, int n, int64_t total_tiles,
+                               const int32_t* block_tensor_device, int dtype, int bits, int symmetric,
+                               int64_t group_size, int flags, int n_grid, int n_candidates, void* stream) {
+    g_err.clear();
+    if (n_grid < 1 || n_candidates < 1 || n_candidates > n_grid)
+        return fail(AWQ_EINVAL, "search grid needs 1 <= n_candidates (%d) <= n_grid (%d)", n_candidates, n_grid);
+    if (n_candidates == 1)   // candidate 0 alone is RTN
+        return awq_quantize_ragged(descs_device, n, total_tiles, block_tensor_device, dtype, bits, symmetric,
+                                   group_size, flags, stream);
+    if (bits != 4 && bits != 8) return fail(AWQ_EINVAL, "Unsupported bit width: %d. Supported: 4, 8.", bits);
+    if (!awq::fast_group_size(group_size))
+        return fail(AWQ_EUNSUPPORTED, "ragged launches take group_size 32, 64, 128 or 256 (got %lld)",
+                    (long long)group_size);
+    if (dtype != AWQ_DTYPE_BF16 && dtype != AWQ_DTYPE_F16 && dtype != AWQ_DTYPE_F32)
+        return fail(AWQ_EINVAL, "ragged launches take bf16, fp16 or fp32 tensors (dtype code %d)", dtype);
+    if (flags & ~AWQ_RAGGED_PADDED) return fail(AWQ_EINVAL, "unknown ragged flags 0x%x", flags);
+    if (n <= 0 || total_tiles <= 0) return AWQ_OK;
+    if (!descs_device) return fail(AWQ_EINVAL, "null descriptor array");
+    return hip_status(awq::launch_fast(descs_device, block_tensor_device, nullptr, n, total_tiles, dtype, bits,
+                                       symmetric, (int)group_size, (flags & AWQ_RAGGED_PADDED) != 0,
+                                       (hipStream_t)stream, awq::nan_scale_code(dtype, symmetric, false), n_grid,
+                                       n_candidates),
+                      "awq ragged search kernel");
+}
+
 int awq_dequantize(const int32_t* tensor_q, const uint16_t* scales, const int32_t* zeros, int64_t rows,
                    int64_t K, int64_t group_size, float* out, void* stream) {
     g_err.clear();

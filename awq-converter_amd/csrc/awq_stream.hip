@@ -304,7 +304,7 @@ bool plan_batch(Pipeline& P, const Batch& B, BatchPlan& bp) {
             const awq_stream_item& it = P.items[pc.item];
             if (it.dtype != dt) continue;
             const awq_tensor_desc d = piece_desc(it, pc, dev_slot + pc.slot_off, c.bits, gs);
-            if (c.search_candidates == 0 && ragged_ok(d, dt, gs)) descs[nd++] = d;
+            if (ragged_ok(d, dt, gs)) descs[nd++] = d;   // (the clip search too: awq_quantize_ragged_search)
             else bp.rest.push_back({d, dt});
         }
         if (nd == first) continue;
@@ -339,9 +339,13 @@ bool launch_batch(Pipeline& P, const Batch& B, const BatchPlan& bp, hipStream_t 
     const char* dslot = (const char*)c.dev_staging + (int64_t)B.slot * P.stride;
     double tp = now_s();
     for (const Group& g : bp.groups) {
-        const int rc = awq_quantize_ragged((const awq_tensor_desc*)dslot + g.first, g.n, g.tiles,
-                                           g.table_len ? (const int32_t*)(dslot + g.table_off) : nullptr, g.dtype,
-                                           c.bits, c.symmetric, gs, g.flags, cs);
+        const int32_t* table = g.table_len ? (const int32_t*)(dslot + g.table_off) : nullptr;
+        const int rc = c.search_candidates > 1
+                           ? awq_quantize_ragged_search((const awq_tensor_desc*)dslot + g.first, g.n, g.tiles, table,
+                                                        g.dtype, c.bits, c.symmetric, gs, g.flags, c.search_grid,
+                                                        c.search_candidates, cs)
+                           : awq_quantize_ragged((const awq_tensor_desc*)dslot + g.first, g.n, g.tiles, table,
+                                                 g.dtype, c.bits, c.symmetric, gs, g.flags, cs);
         if (rc) {
             P.fail(rc, std::string("awq_quantize_ragged: ") + awq_last_error());
             return false;

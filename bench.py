@@ -102,8 +102,20 @@ def parse(argv=None):
                     help="after the timed region: every rank copies its packed shard to the host and writes it as "
                          "chunk files into this directory (the CLI's per-rank output, main.ChunkWriter), reported as "
                          "\"write\" (max over ranks); the files are removed afterwards")
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "round4", "pmc_traffic.json"))
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "round5", "pmc_traffic.json"))
+    ap.add_argument("--mode", default="rtn", choices=["rtn", "search", "act"],
+                    help="rtn = the BASELINE metric (round-to-nearest, the reference's arithmetic); search = the "
+                         "opt-in per-group clip search (scale_method='search') in the same ragged launch; act = the "
+                         "activation-aware search (scale_method='awq') of one Llama-3-8B block's layer groups. "
+                         "search / act are VALU-bound: their roofline is the VALU issue rate (extra lines)")
+    ap.add_argument("--search-grid", type=int, default=20)
+    ap.add_argument("--search-candidates", type=int, default=10,
+                    help="--mode search: candidates of the grid (AWQQuantizer default: 20 x 0.5 = 10)")
+    ap.add_argument("--act-tokens", type=int, default=512, help="--mode act: calibration tokens per layer group")
+    ap.add_argument("--valu-json", default=os.path.join(ROOT, "profiles", "round5", "pmc_valu.json"))
     a = ap.parse_args(argv)
+    if a.mode == "search" and not 1 < a.search_candidates <= a.search_grid:
+        ap.error("--search-candidates must be in (1, --search-grid]")
     if a.replica and a.shard:
         ap.error("--replica and --shard are exclusive")
     return a
@@ -170,14 +182,14 @@ def host_cpus():
     return min(used, aff), node, aff
 
 
-def _time_oracle(x, rows, K, group_size, bits=4):
+def _time_oracle(x, rows, K, group_size, bits=4, search=None):
     from oracle import awq_oracle as orc
     t0 = time.perf_counter()
-    orc.quantize_groups(x, rows, K, group_size, bits, False)
+    orc.quantize_groups(x, rows, K, group_size, bits, False, search=search)
     return time.perf_counter() - t0
 
 
-def cpu_baseline(workload, budget_s, group_size=128, dtype=torch.bfloat16):
+def cpu_baseline(workload, budget_s, group_size=128, dtype=torch.bfloat16, search=None):
     """The oracle (oracle/awq_oracle.c, OpenMP over rows, bit-exact restatement of awq.py)
     on the host cores, SURVEY §8(d): C1 (1024x4096, sigma 1) in full, then a row sample of
     every distinct shape of the workload, each extrapolated to the shape's full row count
@@ -188,8 +200,8 @@ def cpu_baseline(workload, budget_s, group_size=128, dtype=torch.bfloat16):
     g = torch.Generator().manual_seed(1234)
     esize = torch.empty((), dtype=dtype).element_size()
     c1 = (torch.randn(1024, 4096, generator=torch.Generator().manual_seed(0))).to(dtype)
-    _time_oracle(c1, 1024, 4096, group_size)                             # warm (page-in, OpenMP pool)
-    c1_s = min(_time_oracle(c1, 1024, 4096, group_size) for _ in range(3))
+    _time_oracle(c1, 1024, 4096, group_size, search=search)              # warm (page-in, OpenMP pool)
+    c1_s = min(_time_oracle(c1, 1024, 4096, group_size, search=search) for _ in range(3))
     per_shape = budget_s / len(WORKLOADS[workload])
     rate0 = 1024 * 4096 * esize / c1_s                                   # bytes/s, for sizing the samples
     total_s, sampled, lines = 0.0, 0, []
@@ -201,7 +213,7 @@ def cpu_baseline(workload, budget_s, group_size=128, dtype=torch.bfloat16):
         x = (torch.randn(take, K, generator=g) * 0.02).to(dtype)
         t, reps = 0.0, 0
         while reps < 2 or (t < per_shape * 0.5 and reps < 1000):
-            t += _time_oracle(x, take, K, group_size)
+            t += _time_oracle(x, take, K, group_size, search=search)
             reps += 1
         t_full = t / reps * rows / take
         total_s += t_full * count
@@ -216,7 +228,8 @@ def cpu_baseline(workload, budget_s, group_size=128, dtype=torch.bfloat16):
                            f"GPU's job actually gets"),
             "c1_full": {"seconds": round(c1_s, 4), "GBs": round(1024 * 4096 * esize / c1_s / 1e9, 4)},
             "extrapolated_seconds": round(total_s, 2), "shapes_sampled": len(lines),
-            "sample": (f"oracle/awq_oracle.c (bit-exact restatement of awq.py, OpenMP over rows, {threads} "
+            "sample": (f"oracle/awq_oracle.c ({'clip search ' + str(search) + ', ' if search else ''}"
+                       f"bit-exact restatement of awq.py, OpenMP over rows, {threads} "
                        f"threads = the box's CPU share OMP_NUM_THREADS; node shows {node} CPUs) - C1 in full, "
                        f"then row samples of every {workload} shape ({'; '.join(lines)}; "
                        f"{sampled / 1e9:.2f} GB sampled), EXTRAPOLATED by row count and multiplicity to the whole "
@@ -313,11 +326,11 @@ KERNEL_SOURCES = ("awq-converter_amd/csrc/awq_fast.hip", "awq-converter_amd/csrc
                   "awq-converter_amd/csrc/awq_internal.h")
 
 
-def kernel_source_hash():
-    """sha256 of the streaming kernel's sources (what a recorded PMC traffic figure is valid for)."""
+def kernel_source_hash(sources=KERNEL_SOURCES):
+    """sha256 of a kernel's sources (what a recorded PMC figure is valid for)."""
     import hashlib
     h = hashlib.sha256()
-    for p in KERNEL_SOURCES:
+    for p in sources:
         with open(os.path.join(ROOT, p), "rb") as f:
             h.update(f.read())
     return h.hexdigest()[:16]
@@ -346,8 +359,57 @@ def recorded_traffic(path, key):
     return (None if stale else rec.get("hbm_bytes_per_launch")), src
 
 
+# VALU issue ceiling (MI355X_MICROARCH.md: 256 CUs x 4 SIMDs, one 64-lane VALU instruction
+# per SIMD every 2 cycles, 2.4 GHz max clock) = 78.6 T lane-instructions/s (= 157.3 TFLOP/s
+# of fp32 FMA, the guide's vector peak).  A VALU-bound kernel's peak rate of work units =
+# that / its VALU lane-instructions per unit (SQ_INSTS_VALU x 64 / units, recorded by a
+# rocprofv3 --pmc pass of this same command: scripts/pmc_valu.py).
+VALU_LANE_PEAK = 256 * 4 * 64 / 2 * 2.4e9
+ACT_SOURCES = ("awq-converter_amd/csrc/awq_actsearch.hip", "awq-converter_amd/csrc/awq_refmath.h",
+               "awq-converter_amd/csrc/awq_internal.h")
+
+
+def recorded_valu(path, key, sources):
+    """VALU lane-instructions per candidate-element recorded for `key` (scripts/pmc_valu.py),
+    None when absent or recorded on other kernel sources (stale)."""
+    try:
+        with open(path) as f:
+            rec = json.load(f).get(key)
+    except (OSError, ValueError):
+        return None, None
+    if not rec:
+        return None, None
+    now = kernel_source_hash(sources)
+    stale = rec.get("kernel_source_sha256") != now
+    src = {"file": os.path.relpath(path, ROOT), "key": key, "commit": rec.get("commit"), "date": rec.get("date"),
+           "kernel_source_sha256": rec.get("kernel_source_sha256"), "kernel_source_sha256_now": now, "stale": stale,
+           "counters": {k: rec[k] for k in ("valu_insts_per_dispatch", "valu_busy", "effective_clock_ghz",
+                                              "valu_active_frac") if k in rec},
+           "note": "recorded by a separate rocprofv3 --pmc pass (SQ_INSTS_VALU, SQ_ACTIVE_INST_VALU, SQ_BUSY_CYCLES, "
+                   "GRBM_GUI_ACTIVE) of this command, not this run"}
+    return (None if stale else rec.get("valu_lane_instr_per_unit")), src
+
+
+def valu_roofline(units, kern_s, per_unit, src, unit_name):
+    """roofline object of a VALU-bound kernel: achieved units/s against the VALU issue ceiling
+    for its own instruction count per unit."""
+    achieved = units / kern_s / 1e9
+    peak = VALU_LANE_PEAK / per_unit / 1e9 if per_unit else None
+    r = {"bound": "valu", "achieved": round(achieved, 2), "peak": round(peak, 2) if peak else None,
+         "unit": f"G {unit_name}/s", "frac": round(achieved / peak, 4) if peak else None, "traffic": None,
+         "units_per_launch": units, "valu_lane_instr_per_unit": per_unit,
+         "valu_lane_peak_per_s": VALU_LANE_PEAK,
+         "peak_basis": "MI355X VALU issue rate (256 CU x 4 SIMD x 64 lanes / 2 cycles x 2.4 GHz = 78.6 T lane-instr/s) "
+                       "/ the kernel's VALU lane-instructions per unit (SQ_INSTS_VALU x 64 / units)"}
+    if src:
+        r["valu_source"] = src
+    return r
+
+
 def main():
     args = parse()
+    if args.mode == "act":
+        return main_act(args)
     from awq_quantizer import _hip
     from awq_quantizer import distributed as D
     from awq_quantizer.quantization.batch import PackedBatch
@@ -393,8 +455,9 @@ def main():
             inputs = make_set(all_shapes, r * 100003, dev, dtype, only=set(mine))
         else:
             inputs = make_set(shapes, (rank * 64 + r) * 100003, dev, dtype)
+        search = (args.search_grid, args.search_candidates) if args.mode == "search" else None
         batches.append(PackedBatch(inputs, bits=args.bits, symmetric=args.symmetric, parity=args.parity,
-                                   group_size=args.group_size))
+                                   group_size=args.group_size, search=search))
         del inputs
     torch.cuda.synchronize()
     algo_bytes = batches[0].algorithmic_bytes()
@@ -455,11 +518,18 @@ def main():
         key += f".gs{args.group_size}"
     if args.dtype != "bf16":
         key += f".{args.dtype}"
+    if args.mode == "search":
+        key += f".search{args.search_candidates}of{args.search_grid}"
     if world > 1:
         key += f".{'shard' if shard else 'replica'}{world}"
     traffic, traffic_src = recorded_traffic(args.traffic_json, key)
+    metric = METRIC.replace("group_size=128", f"group_size={args.group_size}").replace("bf16", args.dtype)
+    if args.mode == "search":
+        metric = metric.replace(", 1/2/4/8", f" with the clip search ({args.search_candidates} of "
+                                             f"{args.search_grid} candidates), 1/2/4/8").replace("% HBM roofline",
+                                                                                             "% VALU roofline")
     line = {
-        "metric": METRIC.replace("group_size=128", f"group_size={args.group_size}").replace("bf16", args.dtype),
+        "metric": metric,
         "value": round(value, 3), "unit": "GB/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
         "scaling": "strong" if shard else "weak", "vs_baseline": None, "dtype": args.dtype, "data": "synthetic",
@@ -479,6 +549,19 @@ def main():
     }
     if traffic_src:
         line["roofline"]["traffic_source"] = traffic_src
+    if args.mode == "search":
+        # VALU-bound: candidate-elements (elements x candidates) against the VALU issue ceiling;
+        # the HBM view of the same launch stays beside it
+        hbm = line.pop("roofline")
+        per_unit, vsrc = recorded_valu(args.valu_json, key, KERNEL_SOURCES)
+        line["roofline"] = valu_roofline(elems * args.search_candidates, kern_avg_s, per_unit, vsrc,
+                                         "candidate-elements")
+        line["roofline"]["kernel_avg_us"] = hbm["kernel_avg_us"]
+        line["roofline"]["timing"] = hbm["timing"]
+        line["roofline"]["hbm_view"] = {k: hbm[k] for k in ("achieved", "peak", "unit", "frac", "traffic",
+                                                            "algorithmic_bytes_per_launch") if k in hbm}
+        line["config"]["search"] = {"grid": args.search_grid, "candidates": args.search_candidates,
+                                    "alpha": f"1 - i/{args.search_grid}, i < {args.search_candidates}"}
     if world > 1:       # the LPT shard's balance: per-rank kernel time and elements
         ku = [r[0] for r in per_rank]
         el = [int(r[1]) for r in per_rank]
@@ -492,13 +575,150 @@ def main():
     if ceiling:
         # read_dominant_ceiling: at the streamed footprint when the set is >= 4 GiB, else 1 GiB
         ref = ceiling_fp or ceiling
-        line["roofline"]["read_dominant_ceiling"] = round(ref, 1)
-        line["roofline"]["frac_of_ceiling"] = round(achieved / ref, 4)
-        line["roofline"]["ceiling_footprint_bytes"] = fp_bytes if ceiling_fp else 1 << 30
-        line["roofline"]["read_dominant_ceiling_1gib"] = round(ceiling, 1)
-        line["roofline"]["frac_of_ceiling_1gib"] = round(achieved / ceiling, 4)
+        hv = line["roofline"].get("hbm_view", line["roofline"])
+        hv["read_dominant_ceiling"] = round(ref, 1)
+        hv["frac_of_ceiling"] = round(achieved / ref, 4)
+        hv["ceiling_footprint_bytes"] = fp_bytes if ceiling_fp else 1 << 30
+        hv["read_dominant_ceiling_1gib"] = round(ceiling, 1)
+        hv["frac_of_ceiling_1gib"] = round(achieved / ceiling, 4)
     if not args.no_cpu_baseline and world == 1:
-        line["cpu_baseline"] = cpu_baseline(args.workload, args.cpu_sample_seconds, args.group_size, dtype)
+        line["cpu_baseline"] = cpu_baseline(args.workload, args.cpu_sample_seconds, args.group_size, dtype,
+                                            search=(args.search_grid, args.search_candidates)
+                                            if args.mode == "search" else None)
+    print(json.dumps(line), flush=True)
+    if world > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+
+
+# one Llama-3-8B decoder block: layer group -> (rows of the linears reading the same input, in_features)
+ACT_BLOCK = {"qkv": ([4096, 1024, 1024], 4096), "o": ([4096], 4096), "gate_up": ([14336, 14336], 4096),
+             "down": ([4096], 14336)}
+
+
+def act_cpu_baseline(budget_s, n_grid, tokens, dtype, bits, symmetric, gs):
+    """The oracle's activation-aware search (oracle_act_*, OpenMP over rows) on a row sample of
+    the block's o_proj group, rate in weight bytes / s (the oracle restates the product's own
+    definition: the reference has no such search)."""
+    from oracle import awq_oracle as orc
+    threads, node, aff = host_cpus()
+    orc.set_threads(threads)
+    g = torch.Generator().manual_seed(7)
+    K = 4096
+    esize = torch.empty((), dtype=dtype).element_size()
+    x = (torch.randn(tokens, K, generator=g) * 2).to(dtype)
+    rows, t, reps = 64, 0.0, 0
+    w = (torch.randn(rows, K, generator=g) * 0.02).to(dtype)
+    orc.awq_search([w], x, n_grid=n_grid, group_size=gs, bits=bits, symmetric=symmetric)     # warm
+    while reps < 2 or (t < budget_s and reps < 100):
+        t0 = time.perf_counter()
+        orc.awq_search([w], x, n_grid=n_grid, group_size=gs, bits=bits, symmetric=symmetric)
+        t += time.perf_counter() - t0
+        reps += 1
+    return {"value": round(rows * K * esize * reps / t / 1e9, 6), "unit": "GB/s", "cores": threads, "kind": "port",
+            "node_cpus": node, "affinity_cpus": aff,
+            "sample": (f"oracle/awq_oracle.c oracle_act_* (the product's definition restated; OpenMP over rows, "
+                       f"{threads} threads = the box's CPU share) on a {rows}x{K} slice of o_proj with {tokens} "
+                       f"tokens x {n_grid} candidates, {reps} runs in {t:.1f} s; rate in weight bytes")}
+
+
+def main_act(args):
+    """--mode act: the activation-aware search (scale_method="awq", AWQQuantizer.quantize_layer_group)
+    of one Llama-3-8B block — q/k/v, o, gate/up, down, each with its own synthetic calibration
+    input (tokens x in_features, 1/32 of the channels x30: salient channels).  A step = all four
+    layer groups: statistics, w_mean, scale table, the loss kernel over every candidate, select,
+    W·diag(s) and its packed quantization.  value = the block's weight bytes per second.  The
+    loss kernel (act_loss_kernel, ~all of the search's time) is then timed alone on the same
+    inputs and quoted against the VALU issue ceiling.  N > 1: every rank its own block (weak)."""
+    from awq_quantizer import _hip
+    from awq_quantizer import distributed as D
+    from awq_quantizer.quantization import AWQQuantizer
+    backend = os.environ.get("AWQ_DIST_BACKEND", "nccl")
+    rank, local, world = D.init(backend)
+    dev = torch.device("cuda", local % max(1, torch.cuda.device_count()))
+    torch.cuda.set_device(dev)
+    _hip.require_device(dev)
+    dtype = DTYPES[args.dtype]
+    esize = torch.empty((), dtype=dtype).element_size()
+    n_grid, gs = args.search_grid, args.group_size
+    q = AWQQuantizer(bits=args.bits, group_size=gs, symmetric=args.symmetric, scale_method="awq", search_grid=n_grid,
+                     device=str(dev), logger_level="ERROR")
+    groups = []
+    for gi, (gname, (rows, K)) in enumerate(ACT_BLOCK.items()):
+        g = torch.Generator(device=dev).manual_seed(1000 * rank + gi)
+        ws = {f"{gname}.{j}": (torch.randn(r, K, device=dev, generator=g) * 0.02).to(dtype) for j, r in enumerate(rows)}
+        amp = torch.ones(K, device=dev)
+        amp[torch.randperm(K, generator=g, device=dev)[: K // 32]] = 30.0
+        x = (torch.randn(args.act_tokens, K, device=dev, generator=g) * amp).to(dtype)
+        groups.append((ws, x))
+    elems = sum(w.numel() for ws, _ in groups for w in ws.values())
+    cand = elems * n_grid
+    stream = torch.cuda.current_stream(dev)
+
+    def step():
+        return [q.quantize_layer_group(ws, x) for ws, x in groups]
+
+    if not args.no_copy_ceiling:
+        stream_ceiling(dev, stream, args.clock_warm_ms)           # clock warm-up, as the main bench
+    for _ in range(max(1, args.warmup)):
+        res = step()
+    torch.cuda.synchronize()
+    D.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        res = step()
+    torch.cuda.synchronize()
+    D.barrier()
+    elapsed = D.max_over_ranks(time.perf_counter() - t0, dev)
+    best = [r["best"] for r in res]
+    # the loss kernel alone: same weights, statistics, table and reciprocal table
+    prep = []
+    for ws, x in groups:
+        wl = list(ws.values())
+        xm, xs = _hip.act_stats(x)
+        table = _hip.act_scale_table(xm, _hip.weight_mean(wl, gs), n_grid)
+        prep.append((wl, xs, table, _hip.act_recip_table(table)))
+    for wl, xs, table, rt in prep:
+        _hip.act_search_losses(wl, xs, table, gs, args.bits, args.symmetric, rtable=rt)
+    torch.cuda.synchronize()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record(stream)
+    for _ in range(args.steps):
+        for wl, xs, table, rt in prep:
+            _hip.act_search_losses(wl, xs, table, gs, args.bits, args.symmetric, rtable=rt)
+    b.record(stream)
+    torch.cuda.synchronize()
+    loss_s = a.elapsed_time(b) / 1e3 / args.steps                 # all loss launches of one step
+    if rank != 0:
+        if world > 1:
+            import torch.distributed as dist
+            dist.destroy_process_group()
+        return
+    key = f"act.llama3-8b-block.t{args.act_tokens}.g{n_grid}.{args.dtype}.b{args.bits}.{'sym' if args.symmetric else 'asym'}"
+    per_unit, vsrc = recorded_valu(args.valu_json, key, ACT_SOURCES)
+    roof = valu_roofline(cand, loss_s, per_unit, vsrc, "candidate-elements")
+    roof.update({"kernel": "act_loss_kernel (7 launches per step: one per linear)",
+                 "kernel_avg_us": round(loss_s / len([w for ws, _ in groups for w in ws]) * 1e6, 2),
+                 "loss_kernels_us_per_step": round(loss_s * 1e6, 2),
+                 "loss_share_of_step": round(loss_s / (elapsed / args.steps), 4),
+                 "timing": "hip events around the step's 7 loss launches (same inputs), repeated --steps times"})
+    wbytes = elems * esize
+    line = {"metric": (f"{args.dtype} GB/sec of Llama-3-8B block weights through the activation-aware search "
+                       f"({args.act_tokens} tokens x {n_grid} candidates, group_size={gs}) + packed quantization, "
+                       f"1 MI355X per block; % VALU roofline of the loss kernel"),
+            "value": round(wbytes * world * args.steps / elapsed / 1e9, 3), "unit": "GB/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": args.dtype,
+            "data": "synthetic (weights N(0, 0.02); activations N(0, 1) with 1/32 of the channels x30)",
+            "config": {"workload": "llama3-8b block: q/k/v, o, gate/up, down layer groups", "tensors": 7,
+                       "elements": elems, "tokens": args.act_tokens, "candidates": n_grid, "group_size": gs,
+                       "bits": args.bits, "symmetric": args.symmetric, "duo_scaling": True, "best_ratio": best,
+                       "parallelism": f"replica{world} (every rank its own block)"},
+            "roofline": roof}
+    if not args.no_cpu_baseline and world == 1:
+        line["cpu_baseline"] = act_cpu_baseline(min(args.cpu_sample_seconds, 15.0), n_grid, args.act_tokens, dtype,
+                                                args.bits, args.symmetric, gs)
     print(json.dumps(line), flush=True)
     if world > 1:
         import torch.distributed as dist

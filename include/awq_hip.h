@@ -215,6 +215,13 @@ int awq_quantize_ragged(const awq_tensor_desc* descs_device, int n, int64_t tota
                         const int32_t* block_tensor_device, int dtype, int bits, int symmetric, int64_t group_size,
                         int flags, void* stream);
 
+/* awq_quantize_ragged with the opt-in clip search of awq_quantize_search (round 5): the same
+ * bits as awq_quantize_search on every tensor of the batch, one launch for a model's tensor
+ * set.  1 <= n_candidates <= n_grid (n_candidates = 1: plain RTN, awq_quantize_ragged). */
+int awq_quantize_ragged_search(const awq_tensor_desc* descs_device, int n, int64_t total_tiles,
+                               const int32_t* block_tensor_device, int dtype, int bits, int symmetric,
+                               int64_t group_size, int flags, int n_grid, int n_candidates, void* stream);
+
 /* AutoAWQ "GEMM" layout (the reference has no packed format): from
  * this library's row-major packed 4-bit results of an [N = out_features, K = in_features]
  * weight (qweight [N, K/8], qzeros [N, ceil(G/8)], scales fp16 [N, G], G = K / group_size)

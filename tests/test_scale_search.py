@@ -194,3 +194,36 @@ def test_search_gpu_model_packed_routes_generic():
         rows = 1 if t.dim() == 1 else t.shape[0]
         assert torch.equal(out[n]["qweight"].cpu(), orc.pack_rows(ref["tensor_q"].reshape(rows, -1), 4, 0))
         assert gio.same_bits(out[n]["scales"].cpu(), ref["scales"])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16, torch.float32])
+@pytest.mark.parametrize("gs,bits,sym", [(128, 4, False), (64, 8, True), (32, 4, True), (256, 4, False)])
+def test_search_ragged_launch_equals_per_tensor(dtype, gs, bits, sym):
+    """Round 5: the clip search of a whole tensor set in ONE ragged launch
+    (awq_quantize_ragged_search, PackedBatch(search=...), quantize_model_packed /
+    quantize_model_device) gives the bits of the per-tensor search and of the oracle —
+    many shapes incl. padded rows (K % gs != 0, K % 8 == 0), 1-D tensors and a NaN group."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from awq_quantizer.quantization import AWQQuantizer
+    g = torch.Generator().manual_seed(gs + bits)
+    shapes = [(96, 1024), (1, 4096), (2048,), (33, 512), (7, 3 * gs), (5, gs * 2 + 8 * 3), (300, 256)]
+    ts = {f"t{i}": (torch.randn(*s, generator=g) * 0.03).to(dtype) for i, s in enumerate(shapes)}
+    ts["t0"][3, 17] = float("nan")
+    ts["t4"][1, 5] = 1.5
+    q = AWQQuantizer(bits=bits, group_size=gs, symmetric=sym, scale_method="search", device="cuda",
+                     logger_level="ERROR")
+    out = q.quantize_model_packed(ts)
+    dev_out = q.quantize_model_device(ts, packed=False)
+    assert sorted(out) == sorted(ts) == sorted(dev_out)
+    for n, t in ts.items():
+        ref = orc.quantize(t, bits=bits, group_size=gs, symmetric=sym, search=(20, 10))
+        rows = 1 if t.dim() == 1 else t.shape[0]
+        assert torch.equal(out[n]["qweight"].cpu(), orc.pack_rows(ref["tensor_q"].reshape(rows, -1), bits, q.qmin)), n
+        assert torch.equal(out[n]["qzeros"].cpu(), orc.pack_rows(ref["zero_points"], bits, q.qmin)), n
+        assert gio.same_bits(out[n]["scales"].cpu(), ref["scales"]), n
+        one = q.quantize_packed(t)
+        assert torch.equal(one["qweight"], out[n]["qweight"]) and torch.equal(one["qzeros"], out[n]["qzeros"]), n
+        assert torch.equal(dev_out[n]["tensor_q"].cpu(), ref["tensor_q"]), n
+        assert gio.same_bits(dev_out[n]["scales"].cpu(), ref["scales"]), n

@@ -850,7 +850,7 @@ __global__ __launch_bounds__(256) void awq_dequant_batch_kernel(
 template <int B> constexpr auto dq_batch4_run = awq_dequant_batch_kernel<B, 4, 4, 0>;
 template <int B> constexpr auto dq_batch4_run_q = awq_dequant_batch_kernel<B, 4, 4, 1>;
 template <int B> constexpr auto dq_batch4_run_e = awq_dequant_batch_kernel<B, 4, 4, 2>;
-constexpr int kDqDefault = 8;   // batched lanes in XCD runs: profiles/round3/dequant (DESIGN.md §5.3)
+constexpr int kDqDefault = 8;   // batched lanes in XCD runs: profiles/round3/dequant (DESIGN.md §5.4)
 #ifdef AWQ_DIAG
 template <int B> constexpr auto dq_v2_remap = awq_dequant_words_v2_kernel<B, true>;
 template <int B> constexpr auto dq_v2_plain = awq_dequant_words_v2_kernel<B, false>;

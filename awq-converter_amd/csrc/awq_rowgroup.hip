@@ -4,7 +4,7 @@
 // Serves the reference's arbitrary group_size (src/awq_quantizer/quantization/awq.py:102,
 // 286-374: groups along each row, the last zero-padded, awq.py:337-339) outside the
 // streaming kernel's 32 / 64 / 128 / 256, with the same per-group arithmetic
-// (awq.py:173-250; awq_quant.h) and packed outputs written directly (DESIGN.md §5.2).
+// (awq.py:173-250; awq_quant.h) and packed outputs written directly (DESIGN.md §5.3).
 #include "awq_quant.h"
 
 namespace awq {

@@ -18,7 +18,7 @@ run fetch rocprofv3 --kernel-include-regex 'awq_fast_kernel' --pmc FETCH_SIZE --
 run write rocprofv3 --kernel-include-regex 'awq_fast_kernel' --pmc WRITE_SIZE --output-format csv -d "$OUT/write" -o bench -- python bench.py $PMC_ARGS
 ALGO=$(grep '^{"metric"' "$OUT/trace.log" | tail -1 | python -c "import json,sys;print(json.loads(sys.stdin.read())['roofline']['algorithmic_bytes_per_launch'])")
 python scripts/pmc_traffic.py --fetch "$OUT/fetch" --write "$OUT/write" --key "${TRAFFIC_KEY:-llama3-70b.b4.asym.packed}" \
-  --algo-bytes "$ALGO" --commit "${COMMIT:-unknown}" --date "$(date -u +%Y-%m-%d)" --out "$OUT/pmc_traffic.json"
+  --algo-bytes "$ALGO" --commit "${COMMIT:-unknown}" --date "$(date -u +%Y-%m-%d)" --out "${TRAFFIC_OUT:-$OUT/pmc_traffic.json}"
 python scripts/trace_window.py "$OUT/trace/bench_kernel_trace.csv" --steps "$STEPS" > "$OUT/trace_window.json"
 cat "$OUT/trace_window.json"
 find "$OUT" -name '*counter_collection.csv' -size +2M -delete

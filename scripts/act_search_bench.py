@@ -7,6 +7,7 @@ sequence, candidate-elements per second for the loss kernel.
   python scripts/act_search_bench.py --tokens 512 --grid 20
 """
 import argparse
+import hashlib
 import json
 import os
 import sys
@@ -40,8 +41,11 @@ def main():
     ap.add_argument("--grid", type=int, default=20)
     ap.add_argument("--iters", type=int, default=3)
     ap.add_argument("--groups", default=",".join(GROUPS))
+    ap.add_argument("--lib", default="", help="load this in-tree build instead of _lib/libawq_hip.so (A/B of builds)")
     args = ap.parse_args()
     from awq_quantizer import _hip
+    if args.lib:
+        _hip.load_library(args.lib)
     from awq_quantizer.quantization import AWQQuantizer
     dev = torch.device("cuda", 0)
     _hip.require_device(dev)
@@ -68,7 +72,10 @@ def main():
                               "quantize_layer_group": round(t_all, 1)},
                           "loss_Gcand_elem_per_s": round(elems * args.grid / t_loss / 1e3, 1),
                           "loss_weight_GBs_per_candidate": round(elems * 2 * args.grid / t_loss / 1e3, 1),
-                          "best": int(best.item())}), flush=True)
+                          "best": int(best.item()),
+                          # the loss partials' bytes: equal across A/B builds = same results
+                          "part_sha": hashlib.sha256(part.cpu().numpy().tobytes()).hexdigest()[:16],
+                          "lib": os.path.basename(args.lib) if args.lib else "libawq_hip.so"}), flush=True)
 
 
 if __name__ == "__main__":

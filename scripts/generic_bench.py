@@ -10,6 +10,7 @@ int32 staging + pack passes), interleaved in this process.
 """
 import argparse
 import ctypes
+import hashlib
 import json
 import os
 import sys
@@ -56,7 +57,8 @@ def one(args, _hip, dev, shape, name, gs, generic, tun=None):
     R, K = (int(v) for v in shape.split(","))
     G = -(-K // gs)
     per = 32 // args.bits
-    x = (torch.randn(R, K, device=dev) * 0.02).to(DT[name])
+    g = torch.Generator(device=dev).manual_seed(R * 7919 + K * 31 + gs)   # same data in every process
+    x = (torch.randn(R, K, device=dev, generator=g) * 0.02).to(DT[name])
     qw = torch.empty(R, -(-K // per), dtype=torch.int32, device=dev)
     qz = torch.empty(R, -(-G // per), dtype=torch.int32, device=dev)
     sc = torch.empty(R, G, dtype=torch.float16, device=dev)
@@ -85,6 +87,10 @@ def one(args, _hip, dev, shape, name, gs, generic, tun=None):
     torch.cuda.synchronize()
     ctx.__exit__(None, None, None)
     us = a.elapsed_time(b) / args.iters * 1e3
+    # the outputs' bytes: equal across A/B builds = same results
+    h = hashlib.sha256()
+    for t in (qw, qz, sc, *stage.values()):
+        h.update(t.cpu().numpy().tobytes())
     nbytes = x.numel() * x.element_size()
     algo = nbytes + sum(t.numel() * t.element_size() for t in (qw, qz, sc))
     kernel = ("generic+pack" if stage and not args.search else "search" if args.search else
@@ -93,7 +99,8 @@ def one(args, _hip, dev, shape, name, gs, generic, tun=None):
     print(json.dumps({"dtype": name, "shape": [R, K], "group_size": gs, "bits": args.bits, "kernel": kernel, "tuning": tun or {},
                       "lib": os.path.basename(args.lib) if args.lib else "libawq_hip.so",
                       "search": args.search, "us": round(us, 1), "input_GBs": round(nbytes / us / 1e3, 1),
-                      "algorithmic_GBs": round(algo / us / 1e3, 1), "frac_8TBs": round(algo / us / 1e3 / 8000, 3)}),
+                      "algorithmic_GBs": round(algo / us / 1e3, 1), "frac_8TBs": round(algo / us / 1e3 / 8000, 3),
+                      "out_sha": h.hexdigest()[:16]}),
           flush=True)
     if args.dequant:
         out = torch.empty(R, K, dtype=torch.float32, device=dev)

@@ -3,12 +3,13 @@
 only) of a bench.py command, merged into the recorded file bench.py reads for its
 `roofline.peak` (bound "valu"):
 
-  valu_lane_instr_per_unit = mean SQ_INSTS_VALU per dispatch x 64 / units per dispatch
-  valu_busy                = SQ_INSTS_VALU x 2 / (dispatch cycles x 1024 SIMDs)
-                             (dispatch cycles = GRBM_GUI_ACTIVE / 8, summed over the 8 XCDs;
-                             one 64-lane VALU instruction per SIMD every 2 cycles)
-  valu_active_frac         = SQ_ACTIVE_INST_VALU x 4 / (dispatch cycles x 1024 SIMDs)
-                             (quad-cycles; waves of one SIMD can overlap, so an upper bound)
+  valu_slots_per_unit      = (SQ_ACTIVE_INST_VALU - SQ_ACTIVE_INST_VALU2) per dispatch / units
+                             (issue slots: one per SIMD per quad-cycle; a slot issues one VALU
+                             instruction or two of the dual-issue class; scripts/valu_classes.py)
+  valu_slot_occupancy      = those slots / (dispatch quad-cycles x 1024 SIMDs)
+                             (dispatch cycles = GRBM_GUI_ACTIVE / 8, summed over the 8 XCDs)
+  dual_issued_instr_frac   = 2 x SQ_ACTIVE_INST_VALU2 / SQ_INSTS_VALU
+  valu_lane_instr_per_unit = SQ_INSTS_VALU x 64 / units (for reference)
 
   pmc_valu.py --pmc-dir DIR --kernel REGEX --units-per-dispatch U --key KEY --sources fast|act
               --out profiles/round5/pmc_valu.json [--commit C] [--kernel-us T]
@@ -66,17 +67,19 @@ def main():
            "kernel_regex": a.kernel, "commit": a.commit, "date": datetime.date.today().isoformat(),
            "kernel_source_sha256": bench.kernel_source_hash(bench.KERNEL_SOURCES if a.sources == "fast"
                                                             else bench.ACT_SOURCES)}
+    act, act2 = mean("SQ_ACTIVE_INST_VALU"), mean("SQ_ACTIVE_INST_VALU2")
+    if act is not None and act2 is not None:
+        rec["valu_slots_per_unit"] = round((act - act2) / a.units_per_dispatch, 6)
+        rec["dual_issued_instr_frac"] = round(2 * act2 / valu, 4)
     if grbm:
         cycles = grbm / 8
         rec["dispatch_cycles"] = cycles
-        rec["valu_busy"] = round(valu * 2 / (cycles * 1024), 4)
-        act = mean("SQ_ACTIVE_INST_VALU")
-        if act:
-            rec["valu_active_frac"] = round(act * 4 / (cycles * 1024), 4)
+        if act is not None and act2 is not None:
+            rec["valu_slot_occupancy"] = round((act - act2) / (cycles / 4 * 1024), 4)
         if a.kernel_us:
             rec["effective_clock_ghz"] = round(cycles / (a.kernel_us * 1e3), 3)
     for c in ("SQ_WAVES", "SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES", "SQ_INSTS_SALU", "SQ_WAIT_INST_ANY",
-              "SQ_ACTIVE_INST_ANY", "SQ_ACTIVE_INST_VALU"):
+              "SQ_ACTIVE_INST_ANY", "SQ_ACTIVE_INST_VALU", "SQ_ACTIVE_INST_VALU2"):
         if c in by:
             rec[c] = mean(c)
     try:

@@ -190,3 +190,28 @@ def test_packed_shapes():
     assert sh["qweight"] == (4096, 1792) and sh["qzeros"] == (4096, 14) and sh["scales"] == (4096, 112)
     sh = AWQQuantizer(bits=8, logger_level="ERROR").packed_shapes((768,))
     assert sh["qweight"] == (1, 192) and sh["qzeros"] == (1, 2) and sh["scales"] == (1, 6)
+
+
+def test_bench_valu_roofline_issue_slot_model(tmp_path):
+    """bench.py's VALU roofline: peak = 614.4 G issue slots/s / the kernel's recorded slots per
+    unit ((SQ_ACTIVE_INST_VALU - SQ_ACTIVE_INST_VALU2) / units); records made on other kernel
+    sources or without the dual-issue counter are not used."""
+    import json
+    import sys
+    sys.path.insert(0, ROOT)
+    import bench
+    assert bench.VALU_SLOT_RATE == 256 * 4 * 2.4e9 / 4
+    now = bench.kernel_source_hash(bench.KERNEL_SOURCES)
+    p = tmp_path / "valu.json"
+    p.write_text(json.dumps({
+        "ok": {"valu_slots_per_unit": 0.25, "kernel_source_sha256": now},
+        "stale": {"valu_slots_per_unit": 0.25, "kernel_source_sha256": "0" * 16},
+        "old": {"valu_lane_instr_per_unit": 14.5, "kernel_source_sha256": now}}))
+    per, src = bench.recorded_valu(str(p), "ok", bench.KERNEL_SOURCES)
+    assert per == 0.25 and src["stale"] is False
+    r = bench.valu_roofline(1e12, 1.0, per, src, "candidate-elements")
+    assert r["peak"] == round(bench.VALU_SLOT_RATE / 0.25 / 1e9, 2)
+    assert r["frac"] == round(1000.0 / (bench.VALU_SLOT_RATE / 0.25 / 1e9), 4)
+    assert bench.recorded_valu(str(p), "stale", bench.KERNEL_SOURCES)[0] is None
+    assert bench.recorded_valu(str(p), "old", bench.KERNEL_SOURCES)[0] is None
+    assert bench.recorded_valu(str(p), "missing", bench.KERNEL_SOURCES) == (None, None)

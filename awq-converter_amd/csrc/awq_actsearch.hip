@@ -571,6 +571,72 @@ __device__ __forceinline__ float mquot(float a, float s, float rs) {
 // group) halves the per-candidate group work per element (reductions, RTN parameters, table
 // checks).  The loss tree is unchanged: each chunk is summed in order, the lane adds its two
 // chunks (the tree's first pairwise level; + is commutative), grp_sum does the rest.
+// (A/B builds: -DAWQ_ACT_LDS=0 restores round 4's per-candidate register loads of the tables)
+#ifndef AWQ_ACT_LDS
+#define AWQ_ACT_LDS 1
+#endif
+// The table ring's waits are explicit: the compiler's own wait before an LDS read that may
+// alias an LDS-DMA covers every DMA in flight (vmcnt(0)), which would serialise the prefetch,
+// so the ring is read by inline-asm ds_read_b128 it does not track, with explicit lgkmcnt
+// waits; vm_wait<N> = s_waitcnt vmcnt(N) (all but the wave's N youngest vector-memory
+// operations done; loads, stores and LDS-DMA count together in issue order).
+template <int N>
+__device__ __forceinline__ void vm_wait() {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+__device__ __forceinline__ uint32_t lds_addr(const float* p) {
+    return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) float*)p;
+}
+typedef float f4v __attribute__((ext_vector_type(4)));
+template <int OFF>
+__device__ __forceinline__ f4v lds_read4(uint32_t a) {
+    f4v t;
+    asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(t) : "v"(a), "n"(OFF) : "memory");
+    return t;
+}
+// A ring slot's 2 * EPL floats: EPL scale-table entries at a (into s, waited for here) and
+// EPL reciprocals at a + 4 GSZ (left in flight in rp until lds_slot_rs).  The lgkmcnt waits
+// take the loaded registers as operands, so no use of them can be scheduled above the wait;
+// LDS reads complete in order, so lgkmcnt(EPL / 4) means the scale reads are done.
+template <int EPL, int GSZ>
+__device__ __forceinline__ void lds_slot_s(uint32_t a, float (&s)[EPL], f4v (&rp)[EPL / 4]) {
+    static_assert(EPL == 8 || EPL == 16, "8 or 16 elements per lane");
+    f4v t[EPL / 4];
+    t[0] = lds_read4<0>(a);
+    t[1] = lds_read4<16>(a);
+    if constexpr (EPL == 16) {
+        t[2] = lds_read4<32>(a);
+        t[3] = lds_read4<48>(a);
+    }
+    rp[0] = lds_read4<4 * GSZ>(a);
+    rp[1] = lds_read4<4 * GSZ + 16>(a);
+    if constexpr (EPL == 16) {
+        rp[2] = lds_read4<4 * GSZ + 32>(a);
+        rp[3] = lds_read4<4 * GSZ + 48>(a);
+        asm volatile("s_waitcnt lgkmcnt(4)" : "+v"(t[0]), "+v"(t[1]), "+v"(t[2]), "+v"(t[3]) : : "memory");
+    } else {
+        asm volatile("s_waitcnt lgkmcnt(2)" : "+v"(t[0]), "+v"(t[1]) : : "memory");
+    }
+#pragma unroll
+    for (int q = 0; q < EPL / 4; ++q)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) s[4 * q + e] = t[q][e];
+}
+template <int EPL>
+__device__ __forceinline__ void lds_slot_rs(f4v (&rp)[EPL / 4], float (&rs)[EPL]) {
+    if constexpr (EPL == 16)
+        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(rp[0]), "+v"(rp[1]), "+v"(rp[2]), "+v"(rp[3]) : : "memory");
+    else
+        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(rp[0]), "+v"(rp[1]) : : "memory");
+#pragma unroll
+    for (int q = 0; q < EPL / 4; ++q)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) rs[4 * q + e] = rp[q][e];
+}
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t act_rsrc(const void* base, uint32_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
+}
+
 template <int DT, int LPG, bool SYM, int EPL>
 __global__ __launch_bounds__(256) void act_loss_kernel(const void* __restrict__ w, int64_t R, int64_t K, int lpg_rt,
                                                        int qmin, int qmax, const float* __restrict__ table,
@@ -584,9 +650,41 @@ __global__ __launch_bounds__(256) void act_loss_kernel(const void* __restrict__ 
     const int64_t nw = (int64_t)gridDim.x * 4;
     const bool leader = (threadIdx.x & 63) % lpg == 0;
     const float rq = 1.0f / (float)(qmax - qmin);   // RN_f32(1 / 15) or RN_f32(1 / 255)
+    // Compile-time group sizes: each candidate's [scale row | reciprocal row] slice of the
+    // wave's group column (8 B per element) comes in by LDS-DMA one candidate ahead, into a
+    // two-slot ring per wave — no VGPRs held for the prefetch (register prefetch cost a wave
+    // of occupancy and lost 9-12 %, round 5 r5h; this ring: bf16 -4 %, fp16 +-0, r5n).  Per
+    // candidate i: wait for slot i & 1 (vmcnt(1): only candidate i - 1's loss store may still
+    // be in flight — the store is a buffer store every lane issues, so the count is exact),
+    // read it, issue candidate i + 1's DMA into the other slot, compute, store.
+#if AWQ_ACT_LDS
+    constexpr bool kLds = LPG > 0;
+#else
+    constexpr bool kLds = false;
+#endif
+    constexpr int GSZ = (LPG > 0 ? LPG : 1) * EPL;                   // group size
+    constexpr int NQ = GSZ * 8 / 1024 > 0 ? GSZ * 8 / 1024 : 1;     // DMAs per candidate
+    __shared__ __attribute__((aligned(16))) float ring[kLds ? 4 * 2 * 2 * GSZ : 1];
+    float* const wr = ring + (kLds ? (threadIdx.x >> 6) * 2 * 2 * GSZ : 0);
+    const int lane = threadIdx.x & 63;
+    const float* const rt = rtable ? rtable : table;   // (no reciprocal table: that half is unread)
+    auto dma = [&](int64_t g, int cand, int slot) {
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+            const int e = q * 256 + 4 * lane;   // float index in [scale row | reciprocal row]
+            if (e < 2 * GSZ) {
+                const float* src = e < GSZ ? table + (int64_t)cand * K + g * GSZ + e
+                                           : rt + (int64_t)cand * K + g * GSZ + (e - GSZ);
+                __builtin_amdgcn_global_load_lds(
+                    src, (__attribute__((address_space(3))) void*)(wr + slot * 2 * GSZ + q * 256), 16, 0, 0);
+            }
+        }
+        asm volatile("" ::: "memory");   // the loss store stays younger than this DMA (vmcnt(1))
+    };
     for (int64_t item = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);; item += nw) {
         GroupLane gl;
         if (!group_lane<EPL>(item, R, G, lpg, gl)) break;
+        if constexpr (kLds) vm_wait<0>();   // the previous item's last DMA has landed in its slot
         float v[EPL], h[EPL];
 #pragma unroll
         for (int c = 0; c < EPL; c += 8) {
@@ -594,10 +692,23 @@ __global__ __launch_bounds__(256) void act_loss_kernel(const void* __restrict__ 
             else for (int j = 0; j < 8; ++j) v[c + j] = 0.0f;
             load8<AWQ_DTYPE_F32>(x_sq, gl.k0 + c, *(float(*)[8]) & h[c]);
         }
+        if constexpr (kLds) dma(gl.g, 0, 0);
+        const float* const cw = wr + (lane % lpg) * EPL;   // this lane's elements in a ring slot
         for (int i = 0; i < n_grid; ++i) {
             float s[EPL], ws[EPL];
+            float rs[EPL];
+            f4v rp[EPL / 4];
+            if constexpr (kLds) {
+                // slot i & 1 holds candidate i once every operation but the previous
+                // candidate's store is done (i = 0: the item's loads and first DMA)
+                if (i == 0) vm_wait<0>();
+                else vm_wait<1>();
+                lds_slot_s<EPL, GSZ>(lds_addr(cw + (i & 1) * 2 * GSZ), s, rp);   // (rp unused without rtable)
+                dma(gl.g, i + 1 < n_grid ? i + 1 : i, (i + 1) & 1);   // (last: a harmless reload)
+            } else {
 #pragma unroll
-            for (int c = 0; c < EPL; c += 8) load8<AWQ_DTYPE_F32>(table, (int64_t)i * K + gl.k0 + c, *(float(*)[8]) & s[c]);
+                for (int c = 0; c < EPL; c += 8) load8<AWQ_DTYPE_F32>(table, (int64_t)i * K + gl.k0 + c, *(float(*)[8]) & s[c]);
+            }
             // min / max skipping NaN (fmin / fmax; the signs of zero extrema cannot change the
             // scale or zero point) with NaN tracked on the side: torch's NaN-propagating
             // min / max once combined
@@ -618,12 +729,16 @@ __global__ __launch_bounds__(256) void act_loss_kernel(const void* __restrict__ 
 #pragma unroll
             for (int c = 0; c < EPL / 8; ++c) acc[c] = 0.0f;
             // channel reciprocals for ŵ = dq / s (0 = outside the proven range: IEEE division)
-            float rs[EPL];
             bool mq = false;
+            // (the ring's reciprocal reads are waited for with or without a reciprocal table:
+            //  registers an asm load is still writing must not be reused)
+            if constexpr (kLds) lds_slot_rs<EPL>(rp, rs);
             if (rtable != nullptr) {
+                if constexpr (!kLds) {
 #pragma unroll
-                for (int c = 0; c < EPL; c += 8)
-                    load8<AWQ_DTYPE_F32>(rtable, (int64_t)i * K + gl.k0 + c, *(float(*)[8]) & rs[c]);
+                    for (int c = 0; c < EPL; c += 8)
+                        load8<AWQ_DTYPE_F32>(rtable, (int64_t)i * K + gl.k0 + c, *(float(*)[8]) & rs[c]);
+                }
                 float m = rs[0];
 #pragma unroll
                 for (int j = 1; j < EPL; ++j) m = __builtin_fminf(m, rs[j]);
@@ -669,7 +784,16 @@ __global__ __launch_bounds__(256) void act_loss_kernel(const void* __restrict__ 
             float a = acc[0];
             if (EPL == 16) a = acc[0] + acc[EPL / 8 - 1];
             a = grp_sum(a, lpg);
-            if (gl.valid && leader) part[(int64_t)i * stride + gl.r * G + gl.g] = a;
+            if constexpr (kLds) {
+                // one store that every lane issues (no branch around it: the wait before the
+                // next candidate's LDS reads can then leave this store in flight); lanes other
+                // than valid group leaders address past the buffer range and write nothing
+                const uint32_t off = (gl.valid && leader) ? (uint32_t)((gl.r * G + gl.g) * 4) : 0x80000000u;
+                __builtin_amdgcn_raw_buffer_store_b32(
+                    __float_as_uint(a), act_rsrc(part + (int64_t)i * stride, (uint32_t)(stride * 4)), off, 0, 0);
+            } else if (gl.valid && leader) {
+                part[(int64_t)i * stride + gl.r * G + gl.g] = a;
+            }
         }
     }
 }

@@ -41,6 +41,7 @@ def main():
     ap.add_argument("--grid", type=int, default=20)
     ap.add_argument("--iters", type=int, default=3)
     ap.add_argument("--groups", default=",".join(GROUPS))
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "f16"])
     ap.add_argument("--lib", default="", help="load this in-tree build instead of _lib/libawq_hip.so (A/B of builds)")
     args = ap.parse_args()
     from awq_quantizer import _hip
@@ -54,8 +55,9 @@ def main():
     for gname in args.groups.split(","):
         rows, K = GROUPS[gname]
         g = torch.Generator(device=dev).manual_seed(0)
-        ws = [(torch.randn(r, K, device=dev, generator=g) * 0.02).bfloat16() for r in rows]
-        x = (torch.randn(args.tokens, K, device=dev, generator=g) * 2).bfloat16()
+        dt = torch.bfloat16 if args.dtype == "bf16" else torch.float16
+        ws = [(torch.randn(r, K, device=dev, generator=g) * 0.02).to(dt) for r in rows]
+        x = (torch.randn(args.tokens, K, device=dev, generator=g) * 2).to(dt)
         elems = sum(r * K for r in rows)
         t_stats, (xm, xs) = timed(lambda: _hip.act_stats(x), args.iters)
         t_wmean, wm = timed(lambda: _hip.weight_mean(ws, 128), args.iters)
@@ -64,7 +66,7 @@ def main():
         t_sel, (losses, best, s) = timed(lambda: _hip.act_search_select(part, table), args.iters)
         t_apply, _ = timed(lambda: [q.quantize_packed(_hip.apply_input_scale(w, s)) for w in ws], args.iters)
         t_all, _ = timed(lambda: q.quantize_layer_group({str(i): w for i, w in enumerate(ws)}, x), args.iters)
-        print(json.dumps({"group": gname, "rows": rows, "K": K, "tokens": args.tokens, "grid": args.grid,
+        print(json.dumps({"group": gname, "dtype": args.dtype, "rows": rows, "K": K, "tokens": args.tokens, "grid": args.grid,
                           "weights_MB": round(elems * 2 / 1e6, 1), "us": {
                               "act_stats": round(t_stats, 1), "weight_mean": round(t_wmean, 1),
                               "scale_table": round(t_table, 1), "losses": round(t_loss, 1),

@@ -288,6 +288,24 @@ def test_gpu_losses_bit_exact(dtype, gs, bits, sym):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("n_grid", [1, 2, 3])
+@pytest.mark.parametrize("dtype,gs", [(torch.bfloat16, 128), (torch.float16, 256), (torch.bfloat16, 32)], ids=str)
+def test_gpu_losses_short_grids(n_grid, dtype, gs):
+    """The loss kernel's LDS table ring at its edges: one, two and three candidates (the
+    first slot's wait, the harmless reload after the last candidate), two DMAs per candidate
+    (gs 256) and partial DMAs (gs 32), rows that leave row blocks partly empty."""
+    dev = _gpu()
+    from awq_quantizer import _hip
+    ws, x = _layer(40 + n_grid + gs, rows=(37, 8), K=512, dtype=dtype)
+    wl = list(ws.values())
+    xm, xs = orc.act_stats(x)
+    table = _hip.act_scale_table(xm.to(dev), None, n_grid)
+    part = _hip.act_search_losses([w.to(dev) for w in wl], xs.to(dev), table, gs, 4, False)
+    _, _, opart = orc.act_search_losses(wl, xs, table.cpu(), gs, 4, False)
+    assert torch.equal(part.cpu().view(torch.int32), opart.view(torch.int32))
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("n_grid,stride", [(1, 1), (5, 1023), (7, 64 * 1024 + 100), (20, 917504),
                                            (256, 40 * 1024), (64, 3200 * 1024)], ids=str)
 def test_gpu_select_bit_exact(n_grid, stride):

@@ -123,6 +123,7 @@ SIGNATURES = {
     "awq_weight_colsum": (_I32, [_P, _I32, _I64, _I64, _I64, _P, _P, _P]),
     "awq_column_mean": (_I32, [_P, _I64, _I64, ctypes.c_double, _P, _P]),
     "awq_act_scale_table": (_I32, [_P, _P, _I64, _I32, _P, _P]),
+    "awq_act_scale_table_ws": (_I32, [_P, _P, _I64, _I32, _P, _P, _P]),
     "awq_act_recip_table": (_I32, [_P, _I32, _I64, _P, _P]),
     "awq_act_search_losses": (_I32, [_P, _I32, _I64, _I64, _I64, _I32, _I32, _P, _P, _I32, _P, _P, _I64, _P]),
     "awq_act_search_select": (_I32, [_P, _I32, _I64, _P, _I64, _P, _P, _P, _P, _P]),
@@ -454,11 +455,20 @@ def weight_mean(weights, group_size: int) -> torch.Tensor:
     return out
 
 
-def act_scale_table(x_mean: torch.Tensor, w_mean: Optional[torch.Tensor], n_grid: int) -> torch.Tensor:
+def act_scale_table(x_mean: torch.Tensor, w_mean: Optional[torch.Tensor], n_grid: int,
+                    workspace: bool = True) -> torch.Tensor:
+    """table fp32 [n_grid, K] (awq_act_scale_table_ws; workspace=False: the workspace-free
+    awq_act_scale_table, same bits)."""
     K = x_mean.numel()
     table = torch.empty((n_grid, K), dtype=torch.float32, device=x_mean.device)
-    check(load_library().awq_act_scale_table(ptr(x_mean), ptr(w_mean), K, n_grid, ptr(table), _stream(table)),
-          "awq_act_scale_table")
+    lib = load_library()
+    if workspace:
+        work = torch.empty(n_grid * (K + 3 * (-(-K // 256))), dtype=torch.float64, device=x_mean.device)
+        check(lib.awq_act_scale_table_ws(ptr(x_mean), ptr(w_mean), K, n_grid, ptr(work), ptr(table), _stream(table)),
+              "awq_act_scale_table_ws")
+    else:
+        check(lib.awq_act_scale_table(ptr(x_mean), ptr(w_mean), K, n_grid, ptr(table), _stream(table)),
+              "awq_act_scale_table")
     return table
 
 

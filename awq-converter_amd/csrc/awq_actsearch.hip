@@ -410,6 +410,83 @@ __device__ __forceinline__ bool group_lane(int64_t item, int64_t R, int64_t G, i
     return true;
 }
 
+// awq_weight_colsum in ONE pass over W for group sizes 32 / 64 / 128 / 256 (K % gs == 0, 16-B
+// aligned): a workgroup takes one 256-row block x one group column (gs columns), in stages of
+// RS = 8192 / gs rows (32 KiB of fp32 terms in LDS): every thread loads 4 octets of the stage
+// (all in flight), the gs / 8 threads of a row reduce its group's NaN-propagating max |w|
+// (as group_absmax_kernel), and store fp32(|w| / fp32(gmax + 1e-6f)) into LDS; then, with the
+// next stage's loads in flight, each of the 256 threads runs one (column, 32-row sub-block)
+// chain of the stage in fp64, rows
+// ascending, and the sub-block sums are added ascending per column at the end — the
+// canonical order of colsum_kernel, so part[] is bit-identical, with W read once instead of
+// twice (round 5).  (A/B builds: -DAWQ_WMEAN_FUSED=0 keeps the two-pass path.)
+#ifndef AWQ_WMEAN_FUSED
+#define AWQ_WMEAN_FUSED 1
+#endif
+template <int DT, int GS>
+__global__ __launch_bounds__(256) void wcolsum_fused_kernel(const void* __restrict__ w, int64_t rows, int64_t K,
+                                                            double* __restrict__ part) {
+    constexpr int RS = 8192 / GS;                // rows per stage
+    constexpr int OPR = GS / 8;                  // octets (threads) per row
+    constexpr int RPP = 256 / OPR;               // rows per load pass
+    constexpr int NP = RS / RPP;                 // load passes per stage (4)
+    constexpr int SBS = RS / kRowSub;            // sub-blocks per stage
+    constexpr int NSB = kRowBlock / kRowSub;     // sub-blocks per block (8)
+    static_assert(NP * RPP == RS && SBS * GS == 256, "one chain per thread per stage");
+    __shared__ __attribute__((aligned(16))) float sv[RS][GS];
+    __shared__ double ssum[NSB][GS];
+    const int tid = threadIdx.x;
+    const int64_t kt = (int64_t)blockIdx.x * GS;
+    const int64_t b = blockIdx.y, r0 = b * kRowBlock;
+    const int nr = (int)((r0 + kRowBlock < rows) ? kRowBlock : rows - r0);
+    const int oc = tid % OPR, rl = tid / OPR;
+    const int c = tid % GS, sbl = tid / GS;      // this thread's chain: column, sub-block of the stage
+    float v[NP][8];
+    auto load_stage = [&](int st) {
+#pragma unroll
+        for (int it = 0; it < NP; ++it) {
+            const int rr = st * RS + rl + RPP * it;
+            if (rr < nr) load8<DT>(w, (r0 + rr) * K + kt + 8 * oc, v[it]);
+            else for (int j = 0; j < 8; ++j) v[it][j] = 0.0f;
+        }
+    };
+    load_stage(0);
+    for (int st = 0; st * RS < nr; ++st) {
+#pragma unroll
+        for (int it = 0; it < NP; ++it) {
+            float m = 0.0f, dummy = 0.0f;
+            int nan = 0;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const float a = __builtin_fabsf(v[it][j]);
+                nan |= a != a;
+                m = a > m ? a : m;
+            }
+            grp_minmax(dummy, m, nan, OPR);
+            const float den = (nan ? __builtin_nanf("") : m) + 1e-6f;
+            const int rr = rl + RPP * it;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) v[it][j] = __builtin_fabsf(v[it][j]) / den;
+            *(float4*)&sv[rr][8 * oc] = make_float4(v[it][0], v[it][1], v[it][2], v[it][3]);
+            *(float4*)&sv[rr][8 * oc + 4] = make_float4(v[it][4], v[it][5], v[it][6], v[it][7]);
+        }
+        __syncthreads();
+        if ((st + 1) * RS < nr) load_stage(st + 1);   // next stage's loads in flight during the chains
+        const int sb = st * SBS + sbl;           // sub-block in the block
+        const int ra = sbl * kRowSub, rb = min(ra + kRowSub, nr - st * RS);
+        if (ra < rb) {
+            double u = 0.0;
+            for (int r = ra; r < rb; ++r) u += (double)sv[r][c];
+            ssum[sb][c] = u;
+        }
+        __syncthreads();
+    }
+    if (tid >= GS) return;
+    double a = 0.0;
+    for (int u = 0; u < NSB && u * kRowSub < nr; ++u) a += ssum[u][tid];   // non-empty sub-blocks, ascending
+    part[b * K + kt + tid] = a;
+}
+
 // NaN-propagating max |w| of every group (awq_weight_mean's normaliser)
 template <int DT>
 __global__ __launch_bounds__(256) void group_absmax_kernel(const void* __restrict__ w, int64_t R, int64_t K,
@@ -549,6 +626,83 @@ __global__ __launch_bounds__(kTableThreads) void scale_table_kernel(const float*
         if (s != s || __builtin_isinf(s)) s = 1.0;
         table[(int64_t)i * K + k] = (float)s;
     }
+}
+
+// awq_act_scale_table_ws: the same table with every power evaluated once (round 5).  Pass 1:
+// thread (slice, k) of candidate blockIdx.y keeps raw_scale in work and its 256-channel
+// slice's NaN-skipping max / min and NaN flag go to part; pass 2: every workgroup folds its
+// candidate's slice partials (max / min are order-independent) into the normaliser and
+// writes its slice.  Same values as scale_table_kernel, which recomputes pass 1 per slice.
+constexpr int kTabSlice = 256;
+__global__ __launch_bounds__(kTabSlice) void table_raw_kernel(const float* __restrict__ x_mean,
+                                                              const float* __restrict__ w_mean, int64_t K, int n_grid,
+                                                              double* __restrict__ raw, double* __restrict__ part) {
+    __shared__ double smx[kTabSlice], smn[kTabSlice];
+    __shared__ int snan[kTabSlice];
+    const int i = blockIdx.y, tid = threadIdx.x;
+    const int64_t k = (int64_t)blockIdx.x * kTabSlice + tid;
+    const double r = (double)i / (double)n_grid;
+    double mx = -__builtin_inf(), mn = __builtin_inf();
+    int nan = 0;
+    if (k < K) {
+        const double s = raw_scale(x_mean, w_mean, k, r);
+        raw[(int64_t)i * K + k] = s;
+        if (s != s) nan = 1;
+        mx = s > mx ? s : mx;
+        mn = s < mn ? s : mn;
+    }
+    smx[tid] = mx;
+    smn[tid] = mn;
+    snan[tid] = nan;
+    __syncthreads();
+    for (int o = kTabSlice / 2; o > 0; o >>= 1) {
+        if (tid < o) {
+            smx[tid] = smx[tid + o] > smx[tid] ? smx[tid + o] : smx[tid];
+            smn[tid] = smn[tid + o] < smn[tid] ? smn[tid + o] : smn[tid];
+            snan[tid] |= snan[tid + o];
+        }
+        __syncthreads();
+    }
+    if (tid == 0) {
+        double* q = part + ((int64_t)i * gridDim.x + blockIdx.x) * 3;
+        q[0] = smx[0];
+        q[1] = smn[0];
+        q[2] = (double)snan[0];
+    }
+}
+__global__ __launch_bounds__(kTabSlice) void table_norm_kernel(const double* __restrict__ raw,
+                                                               const double* __restrict__ part, int64_t K,
+                                                               float* __restrict__ table) {
+    __shared__ double smx[kTabSlice], smn[kTabSlice];
+    __shared__ int snan[kTabSlice];
+    const int i = blockIdx.y, tid = threadIdx.x;
+    const int S = (int)gridDim.x;
+    double mx = -__builtin_inf(), mn = __builtin_inf();
+    int nan = 0;
+    for (int q = tid; q < S; q += kTabSlice) {
+        const double* p = part + ((int64_t)i * S + q) * 3;
+        mx = p[0] > mx ? p[0] : mx;
+        mn = p[1] < mn ? p[1] : mn;
+        nan |= p[2] != 0.0;
+    }
+    smx[tid] = mx;
+    smn[tid] = mn;
+    snan[tid] = nan;
+    __syncthreads();
+    for (int o = kTabSlice / 2; o > 0; o >>= 1) {
+        if (tid < o) {
+            smx[tid] = smx[tid + o] > smx[tid] ? smx[tid + o] : smx[tid];
+            smn[tid] = smn[tid + o] < smn[tid] ? smn[tid + o] : smn[tid];
+            snan[tid] |= snan[tid + o];
+        }
+        __syncthreads();
+    }
+    const double norm = snan[0] ? __builtin_nan("") : sqrt(smx[0] * smn[0]);
+    const int64_t k = (int64_t)blockIdx.x * kTabSlice + tid;
+    if (k >= K) return;
+    double s = raw[(int64_t)i * K + k] / norm;
+    if (s != s || __builtin_isinf(s)) s = 1.0;
+    table[(int64_t)i * K + k] = (float)s;
 }
 
 // Per group and candidate i: w' = RN(w * s_i), RTN parameters of w' (awq.py:173-213),
@@ -1009,6 +1163,19 @@ hipError_t launch_act_stats(const void* x, int dtype, int64_t T, int64_t K, doub
 
 hipError_t launch_weight_colsum(const void* w, int dtype, int64_t R, int64_t K, int64_t L, float* gmax,
                                 double* part, hipStream_t stream) {
+    const int64_t nb = (R + kRowBlock - 1) / kRowBlock;
+    if (AWQ_WMEAN_FUSED && (L == 32 || L == 64 || L == 128 || L == 256) && K % L == 0 && (uintptr_t)w % 16 == 0) {
+        const dim3 gf((unsigned)(K / L), (unsigned)nb);
+#define AWQ_WCF(G) AWQ_DT_SWITCH(dtype, hipLaunchKernelGGL((wcolsum_fused_kernel<D, G>), gf, dim3(256), 0, stream, w, R, K, part))
+        switch (L) {
+        case 32: AWQ_WCF(32) break;
+        case 64: AWQ_WCF(64) break;
+        case 128: AWQ_WCF(128) break;
+        default: AWQ_WCF(256) break;
+        }
+#undef AWQ_WCF
+        return hipPeekAtLastError();
+    }
     const int lpg = (int)(L / 8);
     const int64_t G = K / L;
     const int64_t items = ((R + (64 / lpg) - 1) / (64 / lpg)) * G;
@@ -1032,6 +1199,18 @@ hipError_t launch_colmean(const double* part, int64_t nblk, int64_t K, double di
                           hipStream_t stream) {
     hipLaunchKernelGGL(colmean_kernel, dim3((unsigned)((K + 255) / 256)), dim3(256), 0, stream, part, nblk, K,
                        divisor, out);
+    return hipPeekAtLastError();
+}
+
+hipError_t launch_scale_table_ws(const float* x_mean, const float* w_mean, int64_t K, int n_grid, double* work,
+                                 float* table, hipStream_t stream) {
+    const int64_t S = (K + kTabSlice - 1) / kTabSlice;
+    double* raw = work;
+    double* part = work + (int64_t)n_grid * K;
+    const dim3 grid((unsigned)S, (unsigned)n_grid);
+    hipLaunchKernelGGL(table_raw_kernel, grid, dim3(kTabSlice), 0, stream, x_mean, w_mean, K, n_grid, raw, part);
+    if (hipError_t e = hipPeekAtLastError()) return e;
+    hipLaunchKernelGGL(table_norm_kernel, grid, dim3(kTabSlice), 0, stream, raw, part, K, table);
     return hipPeekAtLastError();
 }
 

@@ -475,6 +475,17 @@ int awq_act_scale_table(const float* x_mean, const float* w_mean, int64_t K, int
                       "awq scale table");
 }
 
+int awq_act_scale_table_ws(const float* x_mean, const float* w_mean, int64_t K, int n_grid, double* work,
+                           float* table, void* stream) {
+    g_err.clear();
+    if (n_grid < 1 || n_grid > AWQ_ACT_MAX_GRID)
+        return fail(AWQ_EINVAL, "n_grid must be in [1, %d] (got %d)", AWQ_ACT_MAX_GRID, n_grid);
+    if (K <= 0) return fail(AWQ_EINVAL, "K must be positive");
+    if (!x_mean || !table || !work) return fail(AWQ_EINVAL, "null argument");
+    return hip_status(awq::launch_scale_table_ws(x_mean, w_mean, K, n_grid, work, table, (hipStream_t)stream),
+                      "awq scale table");
+}
+
 int awq_act_recip_table(const float* table, int n_grid, int64_t K, float* rtable, void* stream) {
     g_err.clear();
     if (n_grid < 1 || n_grid > AWQ_ACT_MAX_GRID)

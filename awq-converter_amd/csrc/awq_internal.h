@@ -225,6 +225,8 @@ hipError_t launch_colmean(const double* part, int64_t nblk, int64_t K, double di
                           hipStream_t stream);
 hipError_t launch_scale_table(const float* x_mean, const float* w_mean, int64_t K, int n_grid, float* table,
                               hipStream_t stream);
+hipError_t launch_scale_table_ws(const float* x_mean, const float* w_mean, int64_t K, int n_grid, double* work,
+                                 float* table, hipStream_t stream);
 hipError_t launch_act_losses(const void* w, int dtype, int64_t R, int64_t K, int64_t L, int bits, int symmetric,
                              const float* table, const float* rtable, int n_grid, const float* x_sq, float* part,
                              int64_t stride, hipStream_t stream);

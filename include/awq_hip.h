@@ -46,7 +46,7 @@
 extern "C" {
 #endif
 
-#define AWQ_HIP_ABI_VERSION 15
+#define AWQ_HIP_ABI_VERSION 16
 
 /* dtype codes of the input weights (torch dtypes the reference accepts, awq.py:397);
  * AWQ_DTYPE_I32 only in awq_apply_params_ex (int32 tensor_q and integer ops) */
@@ -455,6 +455,7 @@ int awq_stream_end(void* handle, awq_stream_stats* stats);
  *   awq_weight_colsum  gmax_work fp32 [R * K/gs]; partial fp64 [ceil(R/256) * K] (this
  *                      linear's slice of the group's [sum_j ceil(R_j/256), K] array)
  *   awq_act_search_select work fp64 [n_grid * ceil(part_stride / 1024)]
+ *   awq_act_scale_table_ws work fp64 [n_grid * (K + 3 * ceil(K / 256))]
  * n_grid <= AWQ_ACT_MAX_GRID; part_stride <= 6144 * 32 * 1024 groups (201 326 592: the
  * select kernel's super-block sums of one candidate fit its LDS), else hipErrorInvalidValue. */
 #define AWQ_ACT_MAX_GRID 256
@@ -468,6 +469,13 @@ int awq_column_mean(const double* partial, int64_t nblk, int64_t K, double divis
 /* table fp32 [n_grid, K]; w_mean NULL = no duo scaling */
 int awq_act_scale_table(const float* x_mean, const float* w_mean, int64_t K, int n_grid, float* table,
                         void* stream);
+/* The same table (bit for bit) with a caller workspace: every (candidate, channel) power is
+ * evaluated once, by one thread, the raw values kept in work between a pass that forms each
+ * 256-channel slice's max / min and one that normalises (awq_act_scale_table recomputes the
+ * normaliser's pass in each of its workgroups: ~10x the fp64 work, on n_grid x 8 CUs).
+ * work fp64 [n_grid * (K + 3 * ceil(K / 256))].  (ABI 16) */
+int awq_act_scale_table_ws(const float* x_mean, const float* w_mean, int64_t K, int n_grid, double* work,
+                           float* table, void* stream);
 /* rtable [n_grid, K] = RN_f32(1 / table) where table is in [2^-60, 2^60], else 0: lets the
  * loss kernel form fp32(dq / s) as one Markstein-corrected product (exact there: awq_selftest
  * 1), falling back to the IEEE division for a wave whose channels leave that range. */

@@ -62,6 +62,7 @@ def main():
         t_stats, (xm, xs) = timed(lambda: _hip.act_stats(x), args.iters)
         t_wmean, wm = timed(lambda: _hip.weight_mean(ws, 128), args.iters)
         t_table, table = timed(lambda: _hip.act_scale_table(xm, wm, args.grid), args.iters)
+        t_table1, _ = timed(lambda: _hip.act_scale_table(xm, wm, args.grid, workspace=False), args.iters)
         t_loss, part = timed(lambda: _hip.act_search_losses(ws, xs, table, 128, 4, False), args.iters)
         t_sel, (losses, best, s) = timed(lambda: _hip.act_search_select(part, table), args.iters)
         t_apply, _ = timed(lambda: [q.quantize_packed(_hip.apply_input_scale(w, s)) for w in ws], args.iters)
@@ -69,7 +70,8 @@ def main():
         print(json.dumps({"group": gname, "dtype": args.dtype, "rows": rows, "K": K, "tokens": args.tokens, "grid": args.grid,
                           "weights_MB": round(elems * 2 / 1e6, 1), "us": {
                               "act_stats": round(t_stats, 1), "weight_mean": round(t_wmean, 1),
-                              "scale_table": round(t_table, 1), "losses": round(t_loss, 1),
+                              "scale_table": round(t_table, 1), "scale_table_no_ws": round(t_table1, 1),
+                              "losses": round(t_loss, 1),
                               "select": round(t_sel, 1), "apply+quantize": round(t_apply, 1),
                               "quantize_layer_group": round(t_all, 1)},
                           "loss_Gcand_elem_per_s": round(elems * args.grid / t_loss / 1e3, 1),

@@ -215,13 +215,24 @@ def test_gpu_stats_bit_exact(dtype, T):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16, torch.float32])
-@pytest.mark.parametrize("gs", [8, 64, 128, 512])
-def test_gpu_weight_mean_bit_exact(dtype, gs):
+@pytest.mark.parametrize("gs", [8, 32, 64, 128, 256, 512])
+@pytest.mark.parametrize("special", [False, True])
+@pytest.mark.parametrize("K", [1024, 1280])
+def test_gpu_weight_mean_bit_exact(dtype, gs, special, K):
+    """gs 32 / 64 / 128 / 256 take the one-pass kernel, 8 / 512 the two-pass path; 300 rows
+    = a full 256-row block + a partial one (partial stage and sub-block); K 1280: a partial
+    column tile; special: NaN and inf groups."""
     dev = _gpu()
     from awq_quantizer import _hip
+    if K % gs:
+        pytest.skip("K % gs != 0")
     g = torch.Generator().manual_seed(gs)
-    ws = [(torch.randn(r, 1024, generator=g) * 0.05).to(dtype) for r in (300, 1, 17)]
+    ws = [(torch.randn(r, K, generator=g) * 0.05).to(dtype) for r in (300, 1, 17, 600)]
     ws[1][0, :gs] = 0.0                                            # an all-zero group
+    if special:
+        ws[0][5, 3] = float("nan")
+        ws[2][3, 700] = float("inf")
+        ws[3][599, K - 24] = float("-inf")
     got = _hip.weight_mean([w.to(dev) for w in ws], gs).cpu()
     assert torch.equal(got.view(torch.int32), orc.weight_mean(ws, gs).view(torch.int32))
 
@@ -252,13 +263,33 @@ def test_gpu_table_wide_range_bit_exact():
     wm = torch.exp2(torch.rand(4096, generator=g, dtype=torch.float64) * 250 - 140).float()
     xm[:6] = torch.tensor([0.0, 1e-45, 1e-40, 3e38, 1.0, 2.0])
     for duo in (False, True):
-        t = _hip.act_scale_table(xm.to(dev), wm.to(dev) if duo else None, 256).cpu()
         o = orc.act_scale_table(xm, wm if duo else None, 256)
-        assert torch.equal(t.view(torch.int32), o.view(torch.int32))
+        for ws_ in (True, False):   # awq_act_scale_table_ws and awq_act_scale_table
+            t = _hip.act_scale_table(xm.to(dev), wm.to(dev) if duo else None, 256, workspace=ws_).cpu()
+            assert torch.equal(t.view(torch.int32), o.view(torch.int32)), ws_
     bad = xm.clone()
     bad[7], bad[8] = float("inf"), float("nan")
-    t = _hip.act_scale_table(bad.to(dev), wm.to(dev), 16).cpu()
-    assert torch.equal(t.view(torch.int32), orc.act_scale_table(bad, wm, 16).view(torch.int32))
+    for ws_ in (True, False):
+        t = _hip.act_scale_table(bad.to(dev), wm.to(dev), 16, workspace=ws_).cpu()
+        assert torch.equal(t.view(torch.int32), orc.act_scale_table(bad, wm, 16).view(torch.int32)), ws_
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("K", [1, 255, 256, 257, 14336])
+def test_gpu_table_workspace_slices(K):
+    """awq_act_scale_table_ws at slice edges (256 channels per workgroup) == the oracle and
+    the workspace-free kernel."""
+    dev = _gpu()
+    from awq_quantizer import _hip
+    g = torch.Generator().manual_seed(K)
+    xm = torch.exp2(torch.rand(K, generator=g) * 20 - 10)
+    wm = torch.exp2(torch.rand(K, generator=g) * 20 - 10)
+    for duo in (False, True):
+        o = orc.act_scale_table(xm, wm if duo else None, 20)
+        a = _hip.act_scale_table(xm.to(dev), wm.to(dev) if duo else None, 20).cpu()
+        b = _hip.act_scale_table(xm.to(dev), wm.to(dev) if duo else None, 20, workspace=False).cpu()
+        assert torch.equal(a.view(torch.int32), o.view(torch.int32))
+        assert torch.equal(b.view(torch.int32), o.view(torch.int32))
 
 
 LOSS_CASES = [(torch.bfloat16, 128, 4, False), (torch.bfloat16, 128, 4, True), (torch.bfloat16, 128, 8, False),

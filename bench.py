@@ -411,6 +411,13 @@ def valu_roofline(units, kern_s, per_unit, src, unit_name):
                        "((SQ_ACTIVE_INST_VALU - SQ_ACTIVE_INST_VALU2) / units)"}
     if src:
         r["valu_source"] = src
+        # the same rate against the all-dual-issue ceiling (2 cycles per 64-lane instruction,
+        # the guide's 157.3 TFLOP/s fp32 vector figure): how far the instruction MIX is from a
+        # stream that pairs every instruction — not an issue-slot fraction
+        lane = (src.get("counters") or {}).get("valu_lane_instr_per_unit")
+        if lane and not src.get("stale"):
+            dual_peak = 256 * 4 * 64 / 2 * 2.4e9 / lane / 1e9
+            r["frac_of_dual_issue_rate"] = round(achieved / dual_peak, 4)
     return r
 
 

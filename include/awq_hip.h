@@ -452,8 +452,10 @@ int awq_stream_end(void* handle, awq_stream_stats* stats);
  * ||x (W' - W)^T||^2.  Weights: bf16 / fp16 / fp32, 2-D, K % gs == 0, gs a power of two in
  * [8, 512]; weights / table / x_sq 16-B aligned.  Sizes of the caller's workspaces:
  *   awq_act_stats      work    fp64 [2 * ceil(T/256) * K]
- *   awq_weight_colsum  gmax_work fp32 [R * K/gs]; partial fp64 [ceil(R/256) * K] (this
- *                      linear's slice of the group's [sum_j ceil(R_j/256), K] array)
+ *   awq_weight_colsum  gmax_work fp32 [R * K/gs] (scratch of the two-pass path; gs 32 / 64 /
+ *                      128 / 256 with 16-B aligned w take the one-pass kernel and leave it
+ *                      untouched); partial fp64 [ceil(R/256) * K] (this linear's slice of the
+ *                      group's [sum_j ceil(R_j/256), K] array)
  *   awq_act_search_select work fp64 [n_grid * ceil(part_stride / 1024)]
  *   awq_act_scale_table_ws work fp64 [n_grid * (K + 3 * ceil(K / 256))]
  * n_grid <= AWQ_ACT_MAX_GRID; part_stride <= 6144 * 32 * 1024 groups (201 326 592: the

@@ -124,6 +124,7 @@ SIGNATURES = {
     "awq_column_mean": (_I32, [_P, _I64, _I64, ctypes.c_double, _P, _P]),
     "awq_act_scale_table": (_I32, [_P, _P, _I64, _I32, _P, _P]),
     "awq_act_scale_table_ws": (_I32, [_P, _P, _I64, _I32, _P, _P, _P]),
+    "awq_quantize_groups_scaled": (_I32, [_P, _I32, _I64, _I64, _I32, _I32, _I32, _P, _P, _P, _P, _P]),
     "awq_act_recip_table": (_I32, [_P, _I32, _I64, _P, _P]),
     "awq_act_search_losses": (_I32, [_P, _I32, _I64, _I64, _I64, _I32, _I32, _P, _P, _I32, _P, _P, _I64, _P]),
     "awq_act_search_select": (_I32, [_P, _I32, _I64, _P, _I64, _P, _P, _P, _P, _P]),
@@ -517,6 +518,21 @@ def act_search_select(part: torch.Tensor, table: torch.Tensor):
     check(load_library().awq_act_search_select(ptr(part), n_grid, stride, ptr(table), K, ptr(work), ptr(losses),
                                                ptr(best), ptr(s_best), _stream(part)), "awq_act_search_select")
     return losses, best, s_best
+
+
+def scaled_eligible(dtype: torch.dtype, rows: int, K: int, L: int) -> bool:
+    """awq_quantize_groups_scaled takes this shape (one pass over W for W * diag(s))."""
+    return dtype in (torch.bfloat16, torch.float16, torch.float32) and L in (32, 64, 128, 256) and K % L == 0 \
+        and K % 8 == 0 and ragged_eligible(dtype, rows, K, L)
+
+
+def quantize_groups_scaled(w: torch.Tensor, s: torch.Tensor, L: int, bits: int, symmetric: bool, *,
+                           qweight=None, qzeros=None, scales=None) -> None:
+    """Packed RTN of w * diag(s) (w [rows, K] device, contiguous; s fp32 [K]) in one pass."""
+    rows, K = w.shape
+    check(load_library().awq_quantize_groups_scaled(ptr(w), AWQ_DTYPE[w.dtype], rows, K, L, bits, int(bool(symmetric)),
+                                                    ptr(s), ptr(qweight), ptr(qzeros), ptr(scales), _stream(w)),
+          "awq_quantize_groups_scaled")
 
 
 def apply_input_scale(w: torch.Tensor, s: torch.Tensor) -> torch.Tensor:

@@ -47,9 +47,12 @@ def _check_group(weights: Dict[str, torch.Tensor], group_size: int):
 def search_layer_group(weights: Dict[str, torch.Tensor], device: torch.device, *, group_size: int, bits: int,
                        symmetric: bool, n_grid: int, duo_scaling: bool,
                        activations: Optional[torch.Tensor] = None, x_mean: Optional[torch.Tensor] = None,
-                       x_sq: Optional[torch.Tensor] = None, table: Optional[torch.Tensor] = None) -> dict:
+                       x_sq: Optional[torch.Tensor] = None, table: Optional[torch.Tensor] = None,
+                       scale_weights: bool = True) -> dict:
     """Run the search on the device; returns device tensors
-    {"x_mean", "x_sq", "w_mean", "table", "losses", "best", "input_scale", "scaled": {name: W·diag(s)}}.
+    {"x_mean", "x_sq", "w_mean", "table", "losses", "best", "input_scale", "weights": {name: W on
+    the device}, "scaled": {name: W·diag(s)} (None with scale_weights=False: the caller
+    quantizes W·diag(s) in one pass, awq_quantize_groups_scaled)}.
     `table` overrides the scale table (a caller's own table; since round 5 the kernel's table
     is bit-exact with the oracle's from the inputs alone, include/awq_hip.h awq_pow)."""
     K = _check_group(weights, group_size)
@@ -77,6 +80,6 @@ def search_layer_group(weights: Dict[str, torch.Tensor], device: torch.device, *
             raise ValueError(f"table must be [{n_grid}, {K}]")
     part = _hip.act_search_losses(ws, x_sq, table, group_size, bits, symmetric)
     losses, best, s_best = _hip.act_search_select(part, table)
-    scaled = {name: _hip.apply_input_scale(w, s_best) for name, w in zip(weights, ws)}
+    scaled = {name: _hip.apply_input_scale(w, s_best) for name, w in zip(weights, ws)} if scale_weights else None
     return {"x_mean": x_mean, "x_sq": x_sq, "w_mean": w_mean, "table": table, "losses": losses, "best": best,
-            "input_scale": s_best, "scaled": scaled}
+            "input_scale": s_best, "weights": dict(zip(weights, ws)), "scaled": scaled}

@@ -433,6 +433,19 @@ class AWQQuantizer:
                 "symmetric": torch.tensor(self.symmetric, dtype=torch.bool),
                 "shape": torch.tensor(list(tensor.shape), dtype=torch.int64)}
 
+    def _packed_outputs(self, tensor: torch.Tensor) -> Dict[str, torch.Tensor]:
+        """quantize_packed()'s result dict for `tensor`'s shape, outputs allocated on the
+        compute device and not yet written."""
+        dev = self.compute_device()
+        sh = self.packed_shapes(tuple(tensor.shape))
+        return {"qweight": torch.empty(sh["qweight"], dtype=torch.int32, device=dev),
+                "qzeros": torch.empty(sh["qzeros"], dtype=torch.int32, device=dev),
+                "scales": torch.empty(sh["scales"], dtype=torch.float16, device=dev),
+                "bits": torch.tensor(self.bits, dtype=torch.int32),
+                "group_size": torch.tensor(self.group_size, dtype=torch.int32),
+                "symmetric": torch.tensor(self.symmetric, dtype=torch.bool),
+                "shape": torch.tensor(list(tensor.shape), dtype=torch.int64)}
+
     def quantize_model_packed(self, tensors: Dict[str, torch.Tensor]) -> Dict[str, Dict[str, torch.Tensor]]:
         """Packed quantization of many tensors: the fast-path-eligible tensors (bf16, fp16 or fp32,
         group_size 32/64/128/256, K % group_size == 0) go into one ragged launch per dtype (with the
@@ -547,12 +560,23 @@ class AWQQuantizer:
         _check_group(weights, self.group_size)
         self._check_mode()
         dev = self.compute_device()
+        # packed outputs of eligible shapes: W * diag(s) quantized in one pass (the scaled copy
+        # is never written: awq_quantize_groups_scaled); otherwise the copy, then quantize
+        one_pass = packed and all(
+            _hip.scaled_eligible(w.dtype, w.shape[0], w.shape[1], self.group_size) for w in weights.values())
         sr = search_layer_group(weights, dev, group_size=self.group_size, bits=self.bits, symmetric=self.symmetric,
                                 n_grid=self.search_grid, duo_scaling=self.duo_scaling, activations=activations,
-                                x_mean=x_mean, x_sq=x_sq, table=table)
+                                x_mean=x_mean, x_sq=x_sq, table=table, scale_weights=not one_pass)
         results = {}
-        for name, sw in sr["scaled"].items():
-            r = self.quantize_packed(sw) if packed else self._quantize_device(sw)   # RTN of W * diag(s)
+        for name in weights:
+            w = sr["weights"][name]
+            if one_pass and w.data_ptr() % 16 == 0:
+                r = self._packed_outputs(w)
+                _hip.quantize_groups_scaled(w, sr["input_scale"], self.group_size, self.bits, self.symmetric,
+                                            qweight=r["qweight"], qzeros=r["qzeros"], scales=r["scales"])
+            else:
+                sw = sr["scaled"][name] if sr["scaled"] is not None else _hip.apply_input_scale(w, sr["input_scale"])
+                r = self.quantize_packed(sw) if packed else self._quantize_device(sw)   # RTN of W * diag(s)
             r["input_scale"] = sr["input_scale"]
             results[name] = r
         best = int(sr["best"].item())

@@ -170,6 +170,31 @@ int awq_quantize_groups_ex(const void* w, int dtype, int64_t rows, int64_t K, in
                                           qweight, qzeros, s, small), "awq generic kernel");
 }
 
+int awq_quantize_groups_scaled(const void* w, int dtype, int64_t rows, int64_t K, int32_t group_size32, int bits,
+                               int symmetric, const float* col_scale, int32_t* qweight, int32_t* qzeros,
+                               uint16_t* scales, void* stream) {
+    g_err.clear();
+    const int64_t group_size = group_size32;
+    if (int rc = check_common(rows, K, group_size, bits)) return rc;
+    if (dtype < AWQ_DTYPE_BF16 || dtype > AWQ_DTYPE_F32) return fail(AWQ_EINVAL, "dtype must be bf16, fp16 or fp32");
+    if (!qweight && !qzeros && !scales) return fail(AWQ_EINVAL, "no output requested");
+    if (rows * K == 0) return AWQ_OK;
+    if (!w || !col_scale) return fail(AWQ_EINVAL, "null input");
+    if (!fast_eligible(dtype, rows, K, group_size) || K % group_size != 0 || K % 8 != 0 || !aligned(w, 16) ||
+        !aligned(col_scale, 16) || (qweight && !aligned(qweight, 8)) || (qzeros && !aligned(qzeros, 4)) ||
+        (scales && !aligned(scales, 2)))
+        return fail(AWQ_EINVAL, "awq_quantize_groups_scaled: shape / group size / alignment outside the one-pass "
+                                "kernel (group_size 32-256 dividing K, K %% 8 == 0, 16-B aligned w and col_scale)");
+    awq_tensor_desc d{};
+    d.w = w; d.rows = rows; d.K = K; d.qweight = qweight; d.qzeros = qzeros; d.scales = scales;
+    d.tile_begin = 0;
+    d.tile_count = awq::fast_tiles(rows, K, bits, (int)group_size);
+    return hip_status(awq::launch_fast(nullptr, nullptr, &d, 1, d.tile_count, dtype, bits, symmetric, (int)group_size,
+                                       false, (hipStream_t)stream, awq::nan_scale_code(dtype, symmetric, false), 1, 0,
+                                       col_scale),
+                      "awq fast kernel (scaled)");
+}
+
 int awq_quantize_search(const void* w, int dtype, int64_t rows, int64_t K, int32_t group_size32, int bits,
                         int symmetric, int n_grid, int n_candidates, int32_t* qweight, int32_t* qzeros,
                         uint16_t* scales, int32_t* tensor_q, int32_t* zeros, void* stream) {

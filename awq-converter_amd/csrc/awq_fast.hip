@@ -459,6 +459,41 @@ __device__ __forceinline__ void compute_tile(const TileCtx& c, const Chunk<F::NW
     return __builtin_amdgcn_readfirstlane(base);
 }
 
+// SCALED (awq_quantize_groups_scaled, the activation-aware search's last step): each loaded
+// element times its column's col_scale, rounded to the dtype — awq_apply_input_scale's
+// RN(w * s) — applied to the raw chunks in place, so compute_tile quantizes W * diag(s)
+// without the scaled copy ever being written.  A non-PAD tile is 2048 consecutive elements
+// starting at column col0 of its first row; chunks of 8 never straddle rows (K % 8 == 0).
+template <typename F>
+__device__ __forceinline__ void scale_chunks(Chunk<F::NW> (&v)[4], const float* __restrict__ cs, uint64_t el_off,
+                                             int64_t K) {
+    const int lane = threadIdx.x & 63;
+    const uint32_t k32 = (uint32_t)K;
+    const uint32_t col0 = (uint32_t)(el_off % (uint64_t)K);   // wave-uniform
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const uint32_t idx = col0 + 512u * j + 8u * lane;
+        const uint32_t col = k32 >= 2048u ? (idx >= k32 ? idx - k32 : idx) : idx % k32;
+        const float4 a = *(const float4*)(cs + col), b = *(const float4*)(cs + col + 4);
+        const float sv[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+        uint32_t bits[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const float y = F::rn(F::elem(v[j], i) * sv[i]);
+            if constexpr (F::NW == 2) bits[i] = __float_as_uint(y);
+            else if constexpr (std::is_same<F, FmtF16>::value) bits[i] = __builtin_bit_cast(uint16_t, (_Float16)y);
+            else bits[i] = __float_as_uint(y) >> 16;
+        }
+        if constexpr (F::NW == 2) {
+            v[j].w[0] = u4{bits[0], bits[1], bits[2], bits[3]};
+            v[j].w[1] = u4{bits[4], bits[5], bits[6], bits[7]};
+        } else {
+            v[j].w[0] = u4{bits[0] | (bits[1] << 16), bits[2] | (bits[3] << 16), bits[4] | (bits[5] << 16),
+                           bits[6] | (bits[7] << 16)};
+        }
+    }
+}
+
 #ifdef AWQ_TRACE
 __device__ uint64_t* g_trace = nullptr;
 #endif
@@ -466,14 +501,14 @@ __device__ uint64_t* g_trace = nullptr;
 // One wave per tile.  The grid normally covers every tile once (launch_fast); a smaller
 // grid (awq_diag.h max_blocks, tests) makes each wave walk tiles t, t + nwaves, ... with a
 // tensor cursor.
-template <typename F, int BITS, bool SYM, bool SEARCH, int GS, bool PAD>
+template <typename F, int BITS, bool SYM, bool SEARCH, int GS, bool PAD, bool SCALED = false>
 __global__ __launch_bounds__(64 * kWavesPerBlock, SEARCH ? 4 : (F::kWide ? AWQ_MIN_WAVES_WIDE : AWQ_MIN_WAVES))
 void awq_fast_kernel(
     // the scalars every wave needs first lead the argument block (they fit the kernarg
     // preload window of a -mllvm -amdgpu-kernarg-preload-count build); the 80-B single-
     // tensor descriptor goes last
     const int32_t* __restrict__ block_tensor, const awq_tensor_desc* __restrict__ descs, int64_t total_tiles,
-    int n, int n_grid, int n_cand, uint32_t nan_code, awq_tensor_desc single) {
+    int n, int n_grid, int n_cand, uint32_t nan_code, const float* __restrict__ col_scale, awq_tensor_desc single) {
     __shared__ uint32_t zwords[kWavesPerBlock][kTileElems / GS];
     __shared__ __attribute__((aligned(16))) uint32_t qstage_all[kWavesPerBlock][BITS == 4 ? 256 : 512];
     // wave index made provably uniform so tile/tensor bookkeeping and the buffer
@@ -545,6 +580,7 @@ void awq_fast_kernel(
         tile_src<BITS, GS, PAD>(src_rows, src_K, tile, el_off, valid);
         Chunk<F::NW> va[4];
         load_tile<F, GS>((const char*)src_w + el_off * F::kBytes, valid, va);
+        if constexpr (SCALED) scale_chunks<F>(va, col_scale, el_off, src_K);
         if (need_d) {   // the descriptor (outputs) while the loads are in flight
             d = descs[cur];
             need_d = false;
@@ -587,7 +623,7 @@ __global__ void awq_selftest_recip_kernel(unsigned long long* mismatches) {
 hipError_t launch_fast(const awq_tensor_desc* descs_dev, const int32_t* block_tensor,
                        const awq_tensor_desc* single, int n, int64_t total_tiles, int dtype, int bits,
                        int symmetric, int group_size, bool padded, hipStream_t stream, uint32_t nan_code, int n_grid,
-                       int n_cand) {
+                       int n_cand, const float* col_scale) {
     if (total_tiles <= 0) return hipSuccess;
     // one wave per tile (diagnostics, csrc/awq_diag.h, diagnostics build: tiles_per_wave, max_blocks =
     // grid cap; either makes waves walk several tiles)
@@ -604,18 +640,21 @@ hipError_t launch_fast(const awq_tensor_desc* descs_dev, const int32_t* block_te
     const dim3 grid((unsigned)blocks), block(64 * kWavesPerBlock);
 #define AWQ_LAUNCH_GS(Fm, B, S, G)                                                                                  \
     do {                                                                                                            \
-        if (n_cand > 1 && padded)                                                                                   \
+        if (col_scale)                                                                                              \
+            hipLaunchKernelGGL((awq_fast_kernel<Fm, B, S, false, G, false, true>), grid, block, 0, stream, bt,      \
+                               descs_dev, total_tiles, n, 1, 0, nan_code, col_scale, one);                          \
+        else if (n_cand > 1 && padded)                                                                              \
             hipLaunchKernelGGL((awq_fast_kernel<Fm, B, S, true, G, true>), grid, block, 0, stream, bt, descs_dev,   \
-                               total_tiles, n, n_grid, n_cand, nan_code, one);                                                \
+                               total_tiles, n, n_grid, n_cand, nan_code, nullptr, one);                             \
         else if (n_cand > 1)                                                                                        \
             hipLaunchKernelGGL((awq_fast_kernel<Fm, B, S, true, G, false>), grid, block, 0, stream, bt, descs_dev,  \
-                               total_tiles, n, n_grid, n_cand, nan_code, one);                                                \
+                               total_tiles, n, n_grid, n_cand, nan_code, nullptr, one);                             \
         else if (padded)                                                                                            \
             hipLaunchKernelGGL((awq_fast_kernel<Fm, B, S, false, G, true>), grid, block, 0, stream, bt, descs_dev,  \
-                               total_tiles, n, 1, 0, nan_code, one);                                                          \
+                               total_tiles, n, 1, 0, nan_code, nullptr, one);                                       \
         else                                                                                                        \
             hipLaunchKernelGGL((awq_fast_kernel<Fm, B, S, false, G, false>), grid, block, 0, stream, bt, descs_dev, \
-                               total_tiles, n, 1, 0, nan_code, one);                                                          \
+                               total_tiles, n, 1, 0, nan_code, nullptr, one);                                       \
     } while (0)
 #define AWQ_LAUNCH(Fm, B, S)                                   \
     switch (group_size) {                                      \
@@ -632,6 +671,7 @@ hipError_t launch_fast(const awq_tensor_desc* descs_dev, const int32_t* block_te
     default: AWQ_LAUNCH(Fm, 8, true); break;        \
     }
     if (!fast_group_size(group_size)) return hipErrorInvalidValue;
+    if (col_scale && (padded || n_cand > 1 || descs_dev)) return hipErrorInvalidValue;   // single, unpadded RTN
     if (dtype == AWQ_DTYPE_F16) {
         AWQ_LAUNCH_FMT(FmtF16)
     } else if (dtype == AWQ_DTYPE_F32) {

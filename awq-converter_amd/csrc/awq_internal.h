@@ -188,7 +188,7 @@ inline const awq_tuning& tuning() {
 hipError_t launch_fast(const awq_tensor_desc* descs_dev, const int32_t* block_tensor,
                        const awq_tensor_desc* single, int n, int64_t total_tiles, int dtype, int bits,
                        int symmetric, int group_size, bool padded, hipStream_t stream, uint32_t nan_code,
-                       int n_grid = 1, int n_cand = 0);
+                       int n_grid = 1, int n_cand = 0, const float* col_scale = nullptr);
 // small: the small-tensor path (NaN scale bits, see nan_scale_code)
 hipError_t launch_generic(const void* w, int dtype, int64_t rows, int64_t K, int64_t L, int bits,
                           int symmetric, int32_t* tensor_q, uint16_t* scales, int32_t* zeros,

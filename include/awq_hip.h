@@ -468,6 +468,15 @@ int awq_weight_colsum(const void* w, int dtype, int64_t rows, int64_t K, int64_t
                       double* partial, void* stream);
 /* out[k] = fp32(sum_{b < nblk, ascending} partial[b * K + k] / divisor) (fp64 sum) */
 int awq_column_mean(const double* partial, int64_t nblk, int64_t K, double divisor, float* out, void* stream);
+/* RTN of W * diag(col_scale) in one pass — the packed outputs of awq_apply_input_scale into a
+ * copy followed by awq_quantize_groups on the copy, bit for bit, without the copy (the
+ * activation-aware search's last step, round 5).  bf16 / fp16 / fp32 2-D w [rows, K],
+ * group_size 32 / 64 / 128 / 256 with K % group_size == 0 and K % 8 == 0, w and col_scale
+ * 16-B aligned, packed outputs only (NULL = not wanted); otherwise AWQ_EINVAL (make the two
+ * calls).  (ABI 16) */
+int awq_quantize_groups_scaled(const void* w, int dtype, int64_t rows, int64_t K, int32_t group_size, int bits,
+                               int symmetric, const float* col_scale, int32_t* qweight, int32_t* qzeros,
+                               uint16_t* scales, void* stream);
 /* table fp32 [n_grid, K]; w_mean NULL = no duo scaling */
 int awq_act_scale_table(const float* x_mean, const float* w_mean, int64_t K, int n_grid, float* table,
                         void* stream);

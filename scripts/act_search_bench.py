@@ -66,6 +66,13 @@ def main():
         t_loss, part = timed(lambda: _hip.act_search_losses(ws, xs, table, 128, 4, False), args.iters)
         t_sel, (losses, best, s) = timed(lambda: _hip.act_search_select(part, table), args.iters)
         t_apply, _ = timed(lambda: [q.quantize_packed(_hip.apply_input_scale(w, s)) for w in ws], args.iters)
+
+        def one_pass():
+            for w in ws:
+                r = q._packed_outputs(w)
+                _hip.quantize_groups_scaled(w, s, 128, 4, False, qweight=r["qweight"], qzeros=r["qzeros"],
+                                            scales=r["scales"])
+        t_scaled, _ = timed(one_pass, args.iters)
         t_all, _ = timed(lambda: q.quantize_layer_group({str(i): w for i, w in enumerate(ws)}, x), args.iters)
         print(json.dumps({"group": gname, "dtype": args.dtype, "rows": rows, "K": K, "tokens": args.tokens, "grid": args.grid,
                           "weights_MB": round(elems * 2 / 1e6, 1), "us": {
@@ -73,6 +80,7 @@ def main():
                               "scale_table": round(t_table, 1), "scale_table_no_ws": round(t_table1, 1),
                               "losses": round(t_loss, 1),
                               "select": round(t_sel, 1), "apply+quantize": round(t_apply, 1),
+                              "scaled_quantize_one_pass": round(t_scaled, 1),
                               "quantize_layer_group": round(t_all, 1)},
                           "loss_Gcand_elem_per_s": round(elems * args.grid / t_loss / 1e3, 1),
                           "loss_weight_GBs_per_candidate": round(elems * 2 * args.grid / t_loss / 1e3, 1),

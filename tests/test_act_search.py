@@ -481,3 +481,63 @@ def test_gpu_ratio0_is_rtn():
     assert out["best"] == 0
     assert torch.equal(out["results"]["w0"]["qweight"], rtn["qweight"])
     assert torch.equal(out["input_scale"].cpu(), torch.ones(512))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16, torch.float32], ids=str)
+@pytest.mark.parametrize("gs", [32, 64, 128, 256])
+@pytest.mark.parametrize("bits,sym", [(4, False), (4, True), (8, False)])
+@pytest.mark.parametrize("shape", [(70, 1024), (9, 3072), (33, 4096), (5, 512)], ids=str)
+def test_gpu_quantize_groups_scaled_equals_two_step(dtype, gs, bits, sym, shape):
+    """awq_quantize_groups_scaled == awq_apply_input_scale into a copy + awq_quantize_groups,
+    bit for bit: tiles inside one row (K 4096), spanning two rows (K 3072) and many rows
+    (K 512 / 1024: the modulo path), special values in W and in s (0, huge -> inf products,
+    NaN)."""
+    dev = _gpu()
+    from awq_quantizer import _hip
+    R, K = shape
+    if K % gs:
+        pytest.skip("K % gs != 0")
+    g = torch.Generator().manual_seed(R * K + gs + bits)
+    w = (torch.randn(R, K, generator=g) * 0.05).to(dtype)
+    w[0, 5] = float("nan")
+    w[R - 1, K - 3] = float("inf")
+    s = torch.exp2(torch.randn(K, generator=g) * 3)
+    s[7], s[K - 1] = 0.0, 3e38
+    if K > 40:
+        s[40] = float("nan")
+    w, s = w.to(dev), s.to(dev)
+    G, per = K // gs, 32 // bits
+
+    def outs():
+        return (torch.full((R, -(-K // per)), -1, dtype=torch.int32, device=dev),
+                torch.full((R, -(-G // per)), -1, dtype=torch.int32, device=dev),
+                torch.full((R, G), 0x7BCD, dtype=torch.int16, device=dev).view(torch.float16))
+    a, b = outs(), outs()
+    _hip.quantize_groups_scaled(w, s, gs, bits, sym, qweight=a[0], qzeros=a[1], scales=a[2])
+    sw = _hip.apply_input_scale(w, s)
+    kw = {}
+    if not _hip.packs_directly(dtype, R, K, gs):
+        kw = dict(tensor_q=torch.empty(R * K, dtype=torch.int32, device=dev),
+                  zeros=torch.empty(R, G, dtype=torch.int32, device=dev))
+    _hip.quantize_groups(sw, R, K, gs, bits, sym, qweight=b[0], qzeros=b[1], scales=b[2], **kw)
+    assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1])
+    assert torch.equal(a[2].view(torch.int16), b[2].view(torch.int16))
+
+
+@pytest.mark.gpu
+def test_gpu_layer_group_one_pass_equals_scaled_copy():
+    """quantize_layer_group's one-pass path == quantize_packed of the scaled weights."""
+    dev = _gpu()
+    from awq_quantizer import _hip
+    from awq_quantizer.quantization import AWQQuantizer
+    ws, x = _layer(91, rows=(96, 40), K=1024)
+    q = AWQQuantizer(bits=4, group_size=128, symmetric=False, scale_method="awq", search_grid=10, device="cuda",
+                     logger_level="ERROR")
+    res = q.quantize_layer_group({k: v.to(dev) for k, v in ws.items()}, x.to(dev))
+    for name, w in ws.items():
+        ref = q.quantize_packed(_hip.apply_input_scale(w.to(dev), res["input_scale"]))
+        got = res["results"][name]
+        for k in ("qweight", "qzeros"):
+            assert torch.equal(got[k], ref[k]), (name, k)
+        assert torch.equal(got["scales"].view(torch.int16), ref["scales"].view(torch.int16))

@@ -49,6 +49,24 @@ __device__ __forceinline__ void block(float (&a)[8], f2 (&p)[8], float b, float 
             if constexpr (OP == 27) asm volatile("v_rcp_f32 %0, %0" : "+v"(a[k]));
             if constexpr (OP == 28) asm volatile("v_add_u32 %0, %0, %1" : "+v"(a[k]) : "v"(b));
             if constexpr (OP == 29) asm volatile("v_min_f32 %0, %0, %1" : "+v"(a[k]) : "v"(b));
+            if constexpr (OP == 30) asm volatile("v_max_i32 %0, %0, %1" : "+v"(a[k]) : "v"(b));
+            if constexpr (OP == 31) asm volatile("v_max_u32 %0, %0, %1" : "+v"(a[k]) : "v"(b));
+            if constexpr (OP == 32) asm volatile("v_min_i32 %0, %0, %1" : "+v"(a[k]) : "v"(b));
+            if constexpr (OP == 33) asm volatile("v_or_b32 %0, %0, %1" : "+v"(a[k]) : "v"(b));
+            if constexpr (OP == 34) asm volatile("v_xor_b32 %0, %0, %1" : "+v"(a[k]) : "v"(b));
+            if constexpr (OP == 35) asm volatile("v_sub_u32 %0, %0, %1" : "+v"(a[k]) : "v"(b));
+            if constexpr (OP == 36) asm volatile("v_add_f16 %0, %0, %1" : "+v"(a[k]) : "v"(b));
+            if constexpr (OP == 37) asm volatile("v_fma_f16 %0, %0, %1, %2" : "+v"(a[k]) : "v"(b), "v"(c));
+            if constexpr (OP == 38) asm volatile("v_pk_add_f16 %0, %0, %1" : "+v"(a[k]) : "v"(b));
+            if constexpr (OP == 39) asm volatile("v_max_f16 %0, %0, %1" : "+v"(a[k]) : "v"(b));
+            if constexpr (OP == 40) asm volatile("v_perm_b32 %0, %0, %1, %2" : "+v"(a[k]) : "v"(b), "v"(c));
+            if constexpr (OP == 41) asm volatile("v_lshlrev_b32_e32 %0, %1, %0" : "+v"(a[k]) : "v"(b));
+            if constexpr (OP == 42) asm volatile("v_fmac_f32 %0, %1, %2" : "+v"(a[k]) : "v"(b), "v"(c));
+            if constexpr (OP == 43) asm volatile("v_sub_f16 %0, %0, %1" : "+v"(a[k]) : "v"(b));
+            if constexpr (OP == 44) asm volatile("v_cvt_f32_u32 %0, %0" : "+v"(a[k]));
+            if constexpr (OP == 45) asm volatile("v_mul_u32_u24 %0, %0, %1" : "+v"(a[k]) : "v"(b));
+            if constexpr (OP == 46) asm volatile("v_max3_f32 %0, %0, %1, %2" : "+v"(a[k]) : "v"(b), "v"(c));
+            if constexpr (OP == 47) asm volatile("v_add_co_u32 %0, vcc, %0, %1" : "+v"(a[k]) : "v"(b) : "vcc");
         }
     }
 }
@@ -76,7 +94,11 @@ static const char* kNames[] = {"v_fma_f32",  "v_pk_fma_f32", "v_add_f32",    "v_
                                "v_pk_add_f32", "v_cvt_pk_f16_f32", "v_pk_mul_f16", "v_cvt_f16_f32",
                                "v_and_b32",   "v_lshlrev_b32", "v_add3_u32",  "v_bfe_u32",
                                "v_mov_b32",   "v_add_f32_dpp", "v_mul_f32",   "v_rcp_f32",
-                               "v_add_u32",   "v_min_f32"};
+                               "v_add_u32",   "v_min_f32",   "v_max_i32",   "v_max_u32",
+                               "v_min_i32",   "v_or_b32",    "v_xor_b32",   "v_sub_u32",
+                               "v_add_f16",   "v_fma_f16",   "v_pk_add_f16", "v_max_f16",
+                               "v_perm_b32",  "v_lshlrev_b32_e32", "v_fmac_f32", "v_sub_f16",
+                               "v_cvt_f32_u32", "v_mul_u32_u24", "v_max3_f32", "v_add_co_u32"};
 
 template <int OP>
 static void run(float* out, int cus, double ghz) {
@@ -143,6 +165,24 @@ int main(int argc, char** argv) {
     run<27>(out, cus, ghz);
     run<28>(out, cus, ghz);
     run<29>(out, cus, ghz);
+    run<30>(out, cus, ghz);
+    run<31>(out, cus, ghz);
+    run<32>(out, cus, ghz);
+    run<33>(out, cus, ghz);
+    run<34>(out, cus, ghz);
+    run<35>(out, cus, ghz);
+    run<36>(out, cus, ghz);
+    run<37>(out, cus, ghz);
+    run<38>(out, cus, ghz);
+    run<39>(out, cus, ghz);
+    run<40>(out, cus, ghz);
+    run<41>(out, cus, ghz);
+    run<42>(out, cus, ghz);
+    run<43>(out, cus, ghz);
+    run<44>(out, cus, ghz);
+    run<45>(out, cus, ghz);
+    run<46>(out, cus, ghz);
+    run<47>(out, cus, ghz);
     hipFree(out);
     return 0;
 }

@@ -39,7 +39,11 @@ def test_export_validation_without_gpu():
 
 
 CASES = [((64, 256), 128, False), ((72, 384), 128, True), ((128, 4096), 128, False), ((8, 128), 128, False),
-         ((200, 768), 64, False), ((96, 1280), 128, True)]
+         ((200, 768), 64, False), ((96, 1280), 128, True),
+         # v2 qweight tiles are 256 x 256 nibbles: ragged n and k tiles, N/8 not a multiple of 4
+         ((296, 2304), 128, False), ((520, 8192), 128, True), ((776, 512), 64, False), ((136, 5120), 128, False),
+         # K % 32 != 0: the 4-B-load tile path
+         ((24, 264), 8, False), ((40, 2072), 8, True)]
 
 
 @pytest.mark.gpu
@@ -80,3 +84,47 @@ def test_export_rejects_8bit_and_3d():
     q = AWQQuantizer(bits=4, device="cuda", logger_level="ERROR")
     with pytest.raises(ValueError, match="2-D"):
         q.export_autoawq(q.quantize_packed(torch.randn(8, 2, 128).bfloat16()))
+
+
+def _torch_autoawq_layout(qweight, qzeros, scales, N, K, G):
+    """The AutoAWQ GEMM layout of row-major packed words, restated with torch tensor ops on
+    the device (unpack nibbles, transpose, AWQ_ORDER interleave, repack)."""
+    order = torch.tensor([0, 2, 4, 6, 1, 3, 5, 7], device=qweight.device)
+    sh = 4 * torch.arange(8, device=qweight.device, dtype=torch.int64)
+
+    def unpack(w, cols):
+        return ((w.to(torch.int64).unsqueeze(-1) >> sh) & 15).reshape(w.shape[0], -1)[:, :cols]
+
+    def pack(v):                                   # [R, C] nibbles -> [R, C / 8] AWQ_ORDER words
+        v8 = v.reshape(v.shape[0], -1, 8)[:, :, order]
+        x = (v8 << sh).sum(-1)
+        return torch.where(x >= 2 ** 31, x - 2 ** 32, x).to(torch.int32)
+
+    return (pack(unpack(qweight, K).t().contiguous()), pack(unpack(qzeros, G).t().contiguous()),
+            scales.t().contiguous())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("N,K,gs", [(32768, 8192, 128), (32776, 8200, 40)], ids=str)
+def test_export_large_nontemporal_path(N, K, gs):
+    """qweight exports of >= 128 MB take the nontemporal-store kernel (csrc/awq_export.hip
+    AWQ_EXPORT_NT_MIN): random packed words against the torch restatement of the layout.
+    The second shape is ragged in both tile dimensions and takes the 4-B-load path."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from awq_quantizer.quantization import AWQQuantizer
+    dev = torch.device("cuda", 0)
+    G = K // gs
+    g = torch.Generator(device=dev).manual_seed(N + K)
+    info = torch.iinfo(torch.int32)
+    pk = {"qweight": torch.randint(info.min, info.max, (N, K // 8), generator=g, device=dev, dtype=torch.int32),
+          "qzeros": torch.randint(info.min, info.max, (N, (G + 7) // 8), generator=g, device=dev, dtype=torch.int32),
+          "scales": torch.randn(N, G, generator=g, device=dev).half(),
+          "shape": torch.tensor([N, K]), "group_size": torch.tensor(gs), "bits": torch.tensor(4)}
+    assert N * K // 2 >= 128 << 20
+    q = AWQQuantizer(bits=4, group_size=gs, symmetric=False, device="cuda", logger_level="ERROR")
+    ex = q.export_autoawq(pk)
+    qw, qz, st = _torch_autoawq_layout(pk["qweight"], pk["qzeros"], pk["scales"], N, K, G)
+    assert torch.equal(ex["qweight"], qw)
+    assert torch.equal(ex["qzeros"], qz)
+    assert torch.equal(ex["scales"].view(torch.int16), st.view(torch.int16))

@@ -238,6 +238,26 @@ def test_gpu_weight_mean_bit_exact(dtype, gs, special, K):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16, torch.float32])
+@pytest.mark.parametrize("gs", [8, 32, 128])
+def test_gpu_weight_mean_wide_range_bit_exact(dtype, gs):
+    """Weights spanning the dtype's whole finite range (subnormals, |w| < 2^-60 next to normal
+    group maxima, group maxima > 2^60, zeros) against the oracle's division."""
+    dev = _gpu()
+    from awq_quantizer import _hip
+    g = torch.Generator().manual_seed(gs)
+    lo, hi = {torch.bfloat16: (-133, 127), torch.float16: (-24, 15), torch.float32: (-149, 127)}[dtype]
+    e = torch.rand(300, 1024, generator=g, dtype=torch.float64) * (hi - lo) + lo
+    sign = torch.where(torch.rand(300, 1024, generator=g) < 0.5, -1.0, 1.0).double()
+    w = (sign * torch.exp2(e)).to(dtype)
+    w[7, :gs] = 0.0
+    w[8, :gs] = torch.tensor(2.0 ** (lo + 2), dtype=torch.float64).to(dtype)
+    w[9, 1] = torch.tensor(2.0 ** -70).to(dtype) if dtype != torch.float16 else 0.0
+    got = _hip.weight_mean([w.to(dev)], gs).cpu()
+    assert torch.equal(got.view(torch.int32), orc.weight_mean([w], gs).view(torch.int32))
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("duo", [False, True])
 @pytest.mark.parametrize("n_grid,K", [(20, 2048), (64, 4096), (7, 384)])
 def test_gpu_table_bit_exact(duo, n_grid, K):

@@ -124,7 +124,7 @@ def one(args, _hip, dev, shape, name, gs, generic, tun=None):
                 same = bool(torch.equal(out.view(torch.int32), ref.view(torch.int32)))
                 us = a.elapsed_time(b) / args.iters * 1e3
                 algo = out.numel() * 4 + sum(t.numel() * t.element_size() for t in (qw, qz, sc))
-                print(json.dumps({"op": "dequantize_packed", "kernel": ["default", "words_v1", "words_v2_xcd", "words_v2", "quads", "quads_xcd", "batch4", "batch8", "batch4_run4", "batch8_run2"][v], "round": rnd,
+                print(json.dumps({"op": "dequantize_packed", "lib": os.path.basename(args.lib) if args.lib else "libawq_hip.so", "kernel": ["default", "words_v1", "words_v2_xcd", "words_v2", "quads", "quads_xcd", "batch4", "batch8", "batch4_run4", "batch8_run2"][v], "round": rnd,
                                   "shape": [R, K], "group_size": gs, "bits": args.bits, "same_bits": same,
                                   "us": round(us, 1), "algorithmic_GBs": round(algo / us / 1e3, 1),
                                   "frac_8TBs": round(algo / us / 1e3 / 8000, 3)}), flush=True)

@@ -809,7 +809,7 @@ __global__ __launch_bounds__(256) void awq_dequant_batch_kernel(
         ii[k] = i;
         cc[k] = c;
         gg[k] = g;
-        wq[k] = (uint32_t)__builtin_nontemporal_load(qweight + i);
+        wq[k] = (uint32_t)qweight[i];   // plain load: an nt load bypasses a cache-resident input (r5d1)
         sb[k] = scales[r * G + g];
         zq[k] = (uint32_t)qzeros[r * zpr + g / PER];
         if constexpr (GMODE == 2) {

@@ -22,7 +22,7 @@ from typing import List, Optional
 
 LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib")
 LIB_PATH = os.path.join(LIB_DIR, "libawq_hip.so")
-ABI_VERSION = 16          # include/awq_hip.h AWQ_HIP_ABI_VERSION
+ABI_VERSION = 17          # include/awq_hip.h AWQ_HIP_ABI_VERSION
 
 _started: Optional[int] = None
 

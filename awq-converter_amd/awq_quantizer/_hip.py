@@ -21,8 +21,12 @@ DIAG_LIB_PATH = os.path.join(LIB_DIR, "libawq_hip_diag.so")
 Q_SMALL_TENSOR = 1      # include/awq_hip.h AWQ_Q_SMALL_TENSOR
 
 AWQ_DTYPE = {torch.bfloat16: 0, torch.float16: 1, torch.float32: 2, torch.float64: 3}
-APPLY_DTYPE = {**AWQ_DTYPE, torch.int32: 4}     # awq_apply_params_ex (AWQ_DTYPE_I32)
+# awq_apply_params_ex tensor dtypes (AWQ_DTYPE_I32 .. AWQ_DTYPE_U64) and op dtypes (up to AWQ_DTYPE_U8)
+APPLY_DTYPE = {**AWQ_DTYPE, torch.int32: 4, torch.int64: 5, torch.int16: 6, torch.int8: 7, torch.uint8: 8,
+               torch.bool: 9, torch.uint16: 10, torch.uint32: 11, torch.uint64: 12}
+APPLY_OP_DTYPE = {d: c for d, c in APPLY_DTYPE.items() if c <= 8}
 APPLY_SCALE_ONE_ELEMENT, APPLY_ZERO_ONE_ELEMENT = 1, 2
+APPLY_SCALE_INT, APPLY_ZERO_INT, APPLY_SCALE_UNSIGNED, APPLY_ZERO_UNSIGNED, APPLY_IEEE_CLAMP = 4, 8, 16, 32, 64
 
 _P = ctypes.c_void_p
 _I64 = ctypes.c_int64
@@ -235,12 +239,13 @@ def group_params(x: torch.Tensor, rows: int, K: int, L: int, bits: int, symmetri
 def apply_params(x: torch.Tensor, rows: int, K: int, L: int, scales: torch.Tensor, zeros: torch.Tensor, qmin: int,
                  qmax: int, mode: int, op1_dtype: torch.dtype, op2_dtype: torch.dtype, flags: int) -> torch.Tensor:
     """awq_apply_params_ex: mode 0 quantize / mode 1 dequantize x (device, contiguous) with
-    float64 per-group parameters, the first op in op1_dtype and the second in op2_dtype (torch's
-    result dtypes); result of op2_dtype, x's shape."""
+    per-group parameters (8-byte words: float64 values, or int64 / uint64 under the *_INT /
+    *_UNSIGNED flags), the first op in op1_dtype and the second in op2_dtype (torch's result
+    dtypes); result of op2_dtype, x's shape."""
     out = torch.empty(x.shape, dtype=op2_dtype, device=x.device)
     check(load_library().awq_apply_params_ex(ptr(x), APPLY_DTYPE[x.dtype], rows, K, L, ptr(scales), ptr(zeros),
-                                             int(qmin), int(qmax), int(mode), APPLY_DTYPE[op1_dtype],
-                                             APPLY_DTYPE[op2_dtype], int(flags), ptr(out), _stream(x)),
+                                             int(qmin), int(qmax), int(mode), APPLY_OP_DTYPE[op1_dtype],
+                                             APPLY_OP_DTYPE[op2_dtype], int(flags), ptr(out), _stream(x)),
           "awq_apply_params_ex")
     return out
 

@@ -314,44 +314,72 @@ class AWQQuantizer:
         s, z = _hip.group_params(x, C, K, K, self.bits, self.symmetric)
         return self._home(s.reshape(C).to(tensor.dtype)), self._home(z.reshape(C).to(tensor.dtype))
 
-    # parameter dtypes whose values float64 holds exactly (int64: checked per call)
-    _EXACT_PARAM = (torch.bfloat16, torch.float16, torch.float32, torch.float64, torch.int32, torch.int16,
-                    torch.int8, torch.uint8, torch.bool, torch.int64)
+    @staticmethod
+    def _sub_check(a: torch.dtype, b: torch.dtype) -> None:
+        """ATen's sub_check: `-` with a bool operand raises (the meta ops below skip it)."""
+        if a == torch.bool and b == torch.bool:
+            raise RuntimeError("Subtraction, the `-` operator, with two bool tensors is not supported. "
+                               "Use the `^` or `logical_xor()` operator instead.")
+        if a == torch.bool or b == torch.bool:
+            raise RuntimeError("Subtraction, the `-` operator, with a bool tensor is not supported. "
+                               "If you are trying to invert a mask, use the `~` or `logical_not()` operator "
+                               "instead.")
+
+    @staticmethod
+    def _param_words(p: torch.Tensor, dev: torch.device) -> Tuple[torch.Tensor, int]:
+        """A parameter on the device as 8-byte words and its awq_apply_params_ex flag bits:
+        float64 values (exact for every float dtype), or int64 values for integer / bool
+        parameters (uint64: their bits) — exact whatever their magnitude."""
+        if p.is_floating_point():
+            return p.detach().to(dev, torch.float64), 0
+        if p.dtype == torch.uint64:
+            return p.detach().to(dev).view(torch.int64).view(torch.float64), 2
+        return p.detach().to(dev, torch.int64).view(torch.float64), 1
+
+    _UNSIGNED_NAMES = {torch.uint16: "UInt16", torch.uint32: "UInt32", torch.uint64: "UInt64"}
 
     def _apply(self, tensor: torch.Tensor, scale, zero_point, mode: int) -> torch.Tensor:
         """_quantize_tensor (mode 0) / _dequantize_tensor (mode 1) as the reference evaluates
         awq.py:245 / awq.py:282: the per-channel reshape of awq.py:237-242 / 274-279, then
-        torch's broadcasting and type promotion.  The two ops' result dtypes come from torch's
-        own promotion (meta tensors: no data, no compute); the arithmetic runs in
-        awq_apply_params_ex in those dtypes, including the reduced-float rule for one-element
-        parameters (include/awq_hip.h).  Pinned by tests/golden/golden_promote.* (reference
-        calls: bf16 / fp16 tensors with fp32 / fp64 parameters, int32 tensor_q, mixed
-        parameter dtypes, non-per-channel broadcasts)."""
+        torch's broadcasting and type promotion, for tensors and parameters of any float,
+        integer or bool dtype.  The two ops' result dtypes come from torch's own promotion
+        (meta tensors: no data, no compute; torch.result_type for the promotion errors the meta
+        ops skip); the arithmetic runs in awq_apply_params_ex in those dtypes.  A one-element
+        parameter of a bf16 / fp16 op enters at its own value when the reference would evaluate
+        on the CPU (device="cpu": ATen's CPU kernels read its original value) and converted to
+        the op dtype first when it would evaluate on the GPU (device="cuda": a device tensor,
+        cast like any operand; and there clamp(-0, 0, qmax) is +0, the GPU clamp's IEEE maximum).  Pinned by tests/golden/golden_promote.* and
+        golden_promote_int.* (reference calls on the CPU: float / int32 tensors with promoting
+        parameters; int64 / int16 / int8 / uint8 / bool / uint16 / uint32 / uint64 tensors with
+        float, integer and bool parameters) and, for device="cuda", by torch's own CUDA
+        evaluation of the same expressions (tests/test_private_methods.py)."""
         scale, zero_point = torch.as_tensor(scale), torch.as_tensor(zero_point)
+        if scale.is_complex() or zero_point.is_complex() or tensor.is_complex():
+            raise NotImplementedError("complex tensors or parameters")
         per_ch = self.per_channel and tensor.dim() > 1 and scale.dim() == 1
         if per_ch:                                   # awq.py:238-242 (same errors as the reference)
             shp = [scale.size(0)] + [1] * (tensor.dim() - 1)
             scale, zero_point = scale.reshape(shp), zero_point.reshape(shp)
         meta = lambda t: torch.empty(t.shape, dtype=t.dtype, device="meta")
         x_m, s_m, z_m = meta(tensor), meta(scale), meta(zero_point)
-        first = (x_m / s_m) if mode == 0 else (x_m - z_m)       # torch's broadcasting / promotion errors
+        if mode == 1:
+            self._sub_check(tensor.dtype, zero_point.dtype)
+        torch.result_type(x_m, s_m if mode == 0 else z_m)       # torch's promotion errors
+        first = (x_m / s_m) if mode == 0 else (x_m - z_m)       # torch's broadcasting / promotion
+        torch.result_type(first, z_m if mode == 0 else s_m)
         res = (first + z_m) if mode == 0 else (first * s_m)
         d1, d2, shape = first.dtype, res.dtype, tuple(res.shape)
-        for what, dt in (("tensor", tensor.dtype), ("result", d1), ("result", d2)):
-            if dt not in _hip.APPLY_DTYPE:
-                raise NotImplementedError(f"{what} dtype {dt} (this build computes bf16 / fp16 / fp32 / fp64 / "
-                                          f"int32)")
-        for p in (scale, zero_point):
-            if p.dtype not in self._EXACT_PARAM or p.is_complex():
-                raise NotImplementedError(f"parameter dtype {p.dtype}")
-            if p.dtype == torch.int64 and p.numel() and int(p.abs().max()) > 2 ** 53:
-                raise NotImplementedError("int64 parameters beyond 2^53")
+        for dt in (d1, d2):
+            if dt not in _hip.APPLY_OP_DTYPE:                    # torch has no such kernel either
+                raise NotImplementedError(f"\"add_stub\" not implemented for '{self._UNSIGNED_NAMES.get(dt, dt)}'")
+        if tensor.dtype not in _hip.APPLY_DTYPE:
+            raise NotImplementedError(f"tensor dtype {tensor.dtype}")
         dev = self.compute_device()
         if math.prod(shape) == 0:
             return self._home(torch.empty(shape, dtype=d2, device=dev))
         x = tensor.detach().to(dev).contiguous()
-        s64 = scale.detach().to(dev, torch.float64)
-        z64 = zero_point.detach().to(dev, torch.float64)
+        s64, s_kind = self._param_words(scale, dev)
+        z64, z_kind = self._param_words(zero_point, dev)
         n = x.numel()
         if shape == tuple(tensor.shape) and scale.numel() == 1 and zero_point.numel() == 1:
             rows, K, L = 1, n, n                     # one parameter pair for the whole tensor
@@ -365,8 +393,12 @@ class AWQQuantizer:
             x = x.expand(shape).contiguous()
             s64, z64 = s64.expand(shape).reshape(-1), z64.expand(shape).reshape(-1)
             rows, K, L = 1, x.numel(), 1
-        flags = ((_hip.APPLY_SCALE_ONE_ELEMENT if scale.numel() == 1 else 0) |
-                 (_hip.APPLY_ZERO_ONE_ELEMENT if zero_point.numel() == 1 else 0))
+        cpu_scalars = not self.device.startswith("cuda")
+        flags = ((_hip.APPLY_SCALE_ONE_ELEMENT if cpu_scalars and scale.numel() == 1 else 0) |
+                 (0 if cpu_scalars else _hip.APPLY_IEEE_CLAMP) |
+                 (_hip.APPLY_ZERO_ONE_ELEMENT if cpu_scalars and zero_point.numel() == 1 else 0) |
+                 (_hip.APPLY_SCALE_INT if s_kind else 0) | (_hip.APPLY_ZERO_INT if z_kind else 0) |
+                 (_hip.APPLY_SCALE_UNSIGNED if s_kind == 2 else 0) | (_hip.APPLY_ZERO_UNSIGNED if z_kind == 2 else 0))
         out = _hip.apply_params(x, rows, K, L, s64.contiguous(), z64.contiguous(), self.qmin, self.qmax, mode, d1, d2,
                                 flags)
         return self._home(out.reshape(shape))

@@ -264,12 +264,19 @@ int awq_apply_params_ex(const void* x, int x_dtype, int64_t rows, int64_t K, int
     if (group_size <= 0) return fail(AWQ_EINVAL, "Group size must be a positive integer: %lld", (long long)group_size);
     if (rows < 0 || K < 0) return fail(AWQ_EINVAL, "negative shape (%lld, %lld)", (long long)rows, (long long)K);
     if (mode != 0 && mode != 1) return fail(AWQ_EINVAL, "unknown mode %d (0 quantize, 1 dequantize)", mode);
-    for (int d : {x_dtype, op1_dtype, op2_dtype})
-        if (d < AWQ_DTYPE_BF16 || d > AWQ_DTYPE_I32) return fail(AWQ_EINVAL, "unknown dtype code %d", d);
-    if (mode == 0 && (op1_dtype == AWQ_DTYPE_I32 || op2_dtype == AWQ_DTYPE_I32))
+    if (x_dtype < AWQ_DTYPE_BF16 || x_dtype > AWQ_DTYPE_U64) return fail(AWQ_EINVAL, "unknown dtype code %d", x_dtype);
+    for (int d : {op1_dtype, op2_dtype})
+        if (d < AWQ_DTYPE_BF16 || d > AWQ_DTYPE_U8)
+            return fail(AWQ_EINVAL, "dtype code %d is not an op dtype (bf16 .. uint8)", d);
+    if (mode == 0 && (op1_dtype >= AWQ_DTYPE_I32 || op2_dtype >= AWQ_DTYPE_I32))
         return fail(AWQ_EINVAL, "quantize (mode 0) divides: its ops are floating point");
-    if (flags & ~(AWQ_APPLY_SCALE_ONE_ELEMENT | AWQ_APPLY_ZERO_ONE_ELEMENT))
-        return fail(AWQ_EINVAL, "unknown flags 0x%x", flags);
+    constexpr int known = AWQ_APPLY_SCALE_ONE_ELEMENT | AWQ_APPLY_ZERO_ONE_ELEMENT | AWQ_APPLY_SCALE_INT |
+                          AWQ_APPLY_ZERO_INT | AWQ_APPLY_SCALE_UNSIGNED | AWQ_APPLY_ZERO_UNSIGNED |
+                          AWQ_APPLY_IEEE_CLAMP;
+    if (flags & ~known) return fail(AWQ_EINVAL, "unknown flags 0x%x", flags);
+    if (((flags & AWQ_APPLY_SCALE_UNSIGNED) && !(flags & AWQ_APPLY_SCALE_INT)) ||
+        ((flags & AWQ_APPLY_ZERO_UNSIGNED) && !(flags & AWQ_APPLY_ZERO_INT)))
+        return fail(AWQ_EINVAL, "AWQ_APPLY_*_UNSIGNED needs AWQ_APPLY_*_INT");
     if (mode == 0 && qmin > qmax) return fail(AWQ_EINVAL, "qmin %d > qmax %d", qmin, qmax);
     if (rows * K == 0) return AWQ_OK;
     if (!x || !scales || !zeros || !out) return fail(AWQ_EINVAL, "null argument");

@@ -411,29 +411,61 @@ __global__ __launch_bounds__(64) void awq_f64_span_lds_kernel(const double* __re
 // Reference _quantize_tensor (awq.py:215-250, mode 0: clamp(round(x / s + z))) and
 // _dequantize_tensor (awq.py:252-284, mode 1: (x - z) * s) with caller-given per-group
 // parameters, under torch's type promotion (include/awq_hip.h awq_apply_params_ex): the first
-// op is evaluated in dtype d1, the second in d2 (= the output's dtype), each in torch CPU's
+// op is evaluated in dtype d1, the second in d2 (= the output's dtype), each in torch's
 // per-op way — fp32 math for bf16 / fp16 / fp32 (fp64 for fp64), one rounding to the op's
-// dtype; int32 ops wrap.  An operand of another dtype is converted to the op's dtype first
-// (through fp32 for bf16 / fp16, as c10::convert does), except a one-element parameter of a
-// bf16 / fp16 op, which enters at its own value in fp32 (ATen's original_scalar_value; the
-// flags say which parameter is one).  Values travel as exact doubles between the steps.
-// Group g of row r covers elements [g L, g L + L) of the row; L = 1 is one parameter per
-// element (any broadcast, expanded by the caller).
+// dtype; integer ops (mode 1) wrap at their width.  An operand of another dtype is converted
+// to the op's dtype first (c10::convert: a float to bf16 / fp16 through fp32; an integer to
+// a float dtype as RN_f32 of the exact integer, then RN to bf16 / fp16 — to fp64 directly;
+// to an integer dtype by truncation to its width), except a one-element parameter of a
+// bf16 / fp16 op under AWQ_APPLY_*_ONE_ELEMENT, which enters at its own value in fp32
+// (ATen CPU's original_scalar_value); AWQ_APPLY_IEEE_CLAMP: clamp(-0, 0, qmax) = +0 (torch's GPU
+// clamp; its CPU clamp keeps the -0).  Values travel between the steps as exact doubles
+// (floats) or exact 64-bit integers (integers; uint64 tensors keep their bits), so int64
+// tensors and parameters beyond 2^53 stay exact.  Group g of row r covers elements
+// [g L, g L + L) of the row; L = 1 is one parameter per element (any broadcast, expanded by
+// the caller).
 namespace apply {
 
 enum Op { kDiv, kAdd, kSub, kMul };
 
-__device__ __forceinline__ double load(const void* x, int dt, int64_t i) {
+struct Val {
+    double f;     // kind 0
+    int64_t i;    // kind 1 (signed) / 2 (uint64 bits)
+    int kind;
+};
+
+__device__ __forceinline__ Val of_f(double f) { return Val{f, 0, 0}; }
+__device__ __forceinline__ Val of_i(int64_t i, int kind = 1) { return Val{0.0, i, kind}; }
+__device__ __forceinline__ bool is_int(int d) { return d >= AWQ_DTYPE_I32; }
+
+__device__ __forceinline__ Val load(const void* x, int dt, int64_t i) {
     switch (dt) {
-    case AWQ_DTYPE_BF16: return (double)__uint_as_float((uint32_t)((const uint16_t*)x)[i] << 16);
-    case AWQ_DTYPE_F16: return (double)sw_f16_to_f32(((const uint16_t*)x)[i]);
-    case AWQ_DTYPE_F32: return (double)((const float*)x)[i];
-    case AWQ_DTYPE_F64: return ((const double*)x)[i];
-    default: return (double)((const int32_t*)x)[i];
+    case AWQ_DTYPE_BF16: return of_f((double)__uint_as_float((uint32_t)((const uint16_t*)x)[i] << 16));
+    case AWQ_DTYPE_F16: return of_f((double)sw_f16_to_f32(((const uint16_t*)x)[i]));
+    case AWQ_DTYPE_F32: return of_f((double)((const float*)x)[i]);
+    case AWQ_DTYPE_F64: return of_f(((const double*)x)[i]);
+    case AWQ_DTYPE_I32: return of_i(((const int32_t*)x)[i]);
+    case AWQ_DTYPE_I64: return of_i(((const int64_t*)x)[i]);
+    case AWQ_DTYPE_I16: return of_i(((const int16_t*)x)[i]);
+    case AWQ_DTYPE_I8: return of_i(((const int8_t*)x)[i]);
+    case AWQ_DTYPE_U8: return of_i(((const uint8_t*)x)[i]);
+    case AWQ_DTYPE_BOOL: return of_i(((const uint8_t*)x)[i] != 0);
+    case AWQ_DTYPE_U16: return of_i(((const uint16_t*)x)[i]);
+    case AWQ_DTYPE_U32: return of_i(((const uint32_t*)x)[i]);
+    default: return of_i(((const int64_t*)x)[i], 2);    // AWQ_DTYPE_U64
     }
 }
 
-__device__ __forceinline__ int32_t wrap32(int64_t v) { return (int32_t)(uint32_t)(uint64_t)v; }
+// truncation of a 64-bit pattern to integer dtype d (sign- or zero-extended back)
+__device__ __forceinline__ int64_t wrap_to(uint64_t v, int d) {
+    switch (d) {
+    case AWQ_DTYPE_I32: return (int32_t)(uint32_t)v;
+    case AWQ_DTYPE_I16: return (int16_t)(uint16_t)v;
+    case AWQ_DTYPE_I8: return (int8_t)(uint8_t)v;
+    case AWQ_DTYPE_U8: return (uint8_t)v;
+    default: return (int64_t)v;
+    }
+}
 
 // fp32 result of an op rounded to a bf16 / fp16 / fp32 op dtype (a NaN to the dtype's own)
 __device__ __forceinline__ float round_to(float r, int d) {
@@ -442,38 +474,57 @@ __device__ __forceinline__ float round_to(float r, int d) {
     return r;
 }
 
+// RN_f32 of an exact integer (int64 or uint64 bits)
+__device__ __forceinline__ float int_to_f32(const Val& v) {
+    return v.kind == 2 ? (float)(uint64_t)v.i : (float)v.i;
+}
+
 // c10::convert of an exactly held value to dtype d
-__device__ __forceinline__ double convert(double v, int d) {
-    if (d == AWQ_DTYPE_F64) return v;
-    if (d == AWQ_DTYPE_I32) return (double)wrap32((int64_t)v);
-    return (double)round_to((float)v, d);
+__device__ __forceinline__ Val convert(const Val& v, int d) {
+    if (is_int(d)) return of_i(wrap_to(v.kind ? (uint64_t)v.i : (uint64_t)(int64_t)v.f, d));
+    if (v.kind == 0) return of_f(d == AWQ_DTYPE_F64 ? v.f : (double)round_to((float)v.f, d));
+    if (d == AWQ_DTYPE_F64) return of_f(v.kind == 2 ? (double)(uint64_t)v.i : (double)v.i);
+    return of_f((double)round_to(int_to_f32(v), d));
+}
+
+// a parameter word (a double, or an int64 / uint64 under AWQ_APPLY_*_INT / _UNSIGNED)
+__device__ __forceinline__ Val param(const double* p, int64_t i, bool as_int, bool as_unsigned) {
+    if (!as_int) return of_f(p[i]);
+    return of_i(__double_as_longlong(p[i]), as_unsigned ? 2 : 1);
 }
 
 // a parameter as it enters an op of dtype d
-__device__ __forceinline__ double enter(double v, int d, bool one_element) {
-    if (one_element && (d == AWQ_DTYPE_BF16 || d == AWQ_DTYPE_F16)) return (double)(float)v;
+__device__ __forceinline__ Val enter(const Val& v, int d, bool one_element) {
+    if (one_element && (d == AWQ_DTYPE_BF16 || d == AWQ_DTYPE_F16))
+        return of_f(v.kind ? (double)int_to_f32(v) : (double)(float)v.f);
     return convert(v, d);
 }
 
-__device__ __forceinline__ double op(Op o, double a, double b, int d) {
+// a, b already in dtype d
+__device__ __forceinline__ Val op(Op o, const Val& a, const Val& b, int d) {
 #pragma clang fp contract(off)
-    if (d == AWQ_DTYPE_I32) {
-        const uint32_t ua = (uint32_t)(int64_t)a, ub = (uint32_t)(int64_t)b;
-        return (double)(int32_t)(o == kSub ? ua - ub : o == kMul ? ua * ub : ua + ub);
+    if (is_int(d)) {
+        const uint64_t ua = (uint64_t)a.i, ub = (uint64_t)b.i;
+        return of_i(wrap_to(o == kSub ? ua - ub : o == kMul ? ua * ub : ua + ub, d));
     }
-    if (d == AWQ_DTYPE_F64) return o == kDiv ? a / b : o == kAdd ? a + b : o == kSub ? a - b : a * b;
-    const float fa = (float)a, fb = (float)b;
+    if (d == AWQ_DTYPE_F64)
+        return of_f(o == kDiv ? a.f / b.f : o == kAdd ? a.f + b.f : o == kSub ? a.f - b.f : a.f * b.f);
+    const float fa = (float)a.f, fb = (float)b.f;
     const float r = o == kDiv ? fa / fb : o == kAdd ? fa + fb : o == kSub ? fa - fb : fa * fb;
-    return (double)round_to(r, d);
+    return of_f((double)round_to(r, d));
 }
 
-__device__ __forceinline__ void store(void* out, int d, int64_t i, double v) {
+__device__ __forceinline__ void store(void* out, int d, int64_t i, const Val& v) {
     switch (d) {
-    case AWQ_DTYPE_BF16: ((uint16_t*)out)[i] = (uint16_t)(__float_as_uint((float)v) >> 16); break;
-    case AWQ_DTYPE_F16: ((uint16_t*)out)[i] = sw_f32_to_f16((float)v); break;
-    case AWQ_DTYPE_F32: ((float*)out)[i] = (float)v; break;
-    case AWQ_DTYPE_F64: ((double*)out)[i] = v; break;
-    default: ((int32_t*)out)[i] = (int32_t)v;
+    case AWQ_DTYPE_BF16: ((uint16_t*)out)[i] = (uint16_t)(__float_as_uint((float)v.f) >> 16); break;
+    case AWQ_DTYPE_F16: ((uint16_t*)out)[i] = sw_f32_to_f16((float)v.f); break;
+    case AWQ_DTYPE_F32: ((float*)out)[i] = (float)v.f; break;
+    case AWQ_DTYPE_F64: ((double*)out)[i] = v.f; break;
+    case AWQ_DTYPE_I32: ((int32_t*)out)[i] = (int32_t)v.i; break;
+    case AWQ_DTYPE_I64: ((int64_t*)out)[i] = v.i; break;
+    case AWQ_DTYPE_I16: ((int16_t*)out)[i] = (int16_t)v.i; break;
+    case AWQ_DTYPE_I8: ((int8_t*)out)[i] = (int8_t)v.i; break;
+    default: ((uint8_t*)out)[i] = (uint8_t)v.i;    // AWQ_DTYPE_U8
     }
 }
 
@@ -485,21 +536,26 @@ __global__ __launch_bounds__(256) void awq_apply_kernel(const void* __restrict__
                                                         int d1, int d2, int flags, void* __restrict__ out) {
     using namespace apply;
     const bool s_one = (flags & AWQ_APPLY_SCALE_ONE_ELEMENT) != 0, z_one = (flags & AWQ_APPLY_ZERO_ONE_ELEMENT) != 0;
+    const bool s_int = (flags & AWQ_APPLY_SCALE_INT) != 0, z_int = (flags & AWQ_APPLY_ZERO_INT) != 0;
+    const bool s_uns = (flags & AWQ_APPLY_SCALE_UNSIGNED) != 0, z_uns = (flags & AWQ_APPLY_ZERO_UNSIGNED) != 0;
+    const bool ieee_clamp = (flags & AWQ_APPLY_IEEE_CLAMP) != 0;
     const int64_t G = (K + L - 1) / L;
     const int64_t total = rows * K;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
          i += (int64_t)gridDim.x * blockDim.x) {
         const int64_t r = i / K, k = i - r * K;
         const int64_t gi = r * G + k / L;
-        const double v = convert(load(x, xdt, i), d1);
-        double t;
+        const Val v = convert(load(x, xdt, i), d1);
+        const Val s = param(sp, gi, s_int, s_uns), z = param(zp, gi, z_int, z_uns);
+        Val t;
         if (mode == 0) {
-            t = op(kDiv, v, enter(sp[gi], d1, s_one), d1);                          // awq.py:245
-            t = op(kAdd, convert(t, d2), enter(zp[gi], d2, z_one), d2);
-            t = clampq(__builtin_rint(t), (double)qmin, (double)qmax);             // awq.py:248
+            t = op(kDiv, v, enter(s, d1, s_one), d1);                               // awq.py:245
+            t = op(kAdd, convert(t, d2), enter(z, d2, z_one), d2);
+            t.f = clampq(__builtin_rint(t.f), (double)qmin, (double)qmax);         // awq.py:248
+            if (ieee_clamp && t.f == 0.0 && qmin == 0) t.f = 0.0;                   // GPU clamp: +0
         } else {
-            t = op(kSub, v, enter(zp[gi], d1, z_one), d1);                          // awq.py:282
-            t = op(kMul, convert(t, d2), enter(sp[gi], d2, s_one), d2);
+            t = op(kSub, v, enter(z, d1, z_one), d1);                               // awq.py:282
+            t = op(kMul, convert(t, d2), enter(s, d2, s_one), d2);
         }
         store(out, d2, i, t);
     }

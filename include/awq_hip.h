@@ -46,11 +46,15 @@
 extern "C" {
 #endif
 
-#define AWQ_HIP_ABI_VERSION 16
+#define AWQ_HIP_ABI_VERSION 17
 
 /* dtype codes of the input weights (torch dtypes the reference accepts, awq.py:397);
- * AWQ_DTYPE_I32 only in awq_apply_params_ex (int32 tensor_q and integer ops) */
-enum { AWQ_DTYPE_BF16 = 0, AWQ_DTYPE_F16 = 1, AWQ_DTYPE_F32 = 2, AWQ_DTYPE_F64 = 3, AWQ_DTYPE_I32 = 4 };
+ * the integer codes only in awq_apply_params_ex (integer tensors such as quantize()'s int32
+ * tensor_q, and integer ops): I32 .. U8 as tensor and op dtypes, BOOL / U16 / U32 / U64 as
+ * tensor dtypes only (ABI 17) */
+enum { AWQ_DTYPE_BF16 = 0, AWQ_DTYPE_F16 = 1, AWQ_DTYPE_F32 = 2, AWQ_DTYPE_F64 = 3, AWQ_DTYPE_I32 = 4,
+       AWQ_DTYPE_I64 = 5, AWQ_DTYPE_I16 = 6, AWQ_DTYPE_I8 = 7, AWQ_DTYPE_U8 = 8, AWQ_DTYPE_BOOL = 9,
+       AWQ_DTYPE_U16 = 10, AWQ_DTYPE_U32 = 11, AWQ_DTYPE_U64 = 12 };
 
 /* status codes */
 enum { AWQ_OK = 0, AWQ_EINVAL = 1, AWQ_EUNSUPPORTED = 2, AWQ_EHIP = 3, AWQ_ENODEV = 4 };
@@ -146,9 +150,21 @@ int awq_apply_params(const void* x, int dtype, int64_t rows, int64_t K, int64_t 
                      const double* zeros, int qmin, int qmax, int mode, void* out, void* stream);
 
 /* awq_apply_params_ex flags: the scale / zero point is a one-element operand of the
- * reference's expression (any shape of numel 1) */
+ * reference's expression (any shape of numel 1) evaluated by torch's CPU kernels (a
+ * reference quantizer with device="cpu"; on CUDA a one-element device tensor is converted to
+ * the op dtype like any other operand: leave the flag off) */
 #define AWQ_APPLY_SCALE_ONE_ELEMENT 1
 #define AWQ_APPLY_ZERO_ONE_ELEMENT 2
+/* (ABI 17) the scales / zeros array holds int64 values, not doubles (an integer or bool
+ * parameter, exact beyond 2^53); _UNSIGNED: those 64-bit words are uint64 values */
+#define AWQ_APPLY_SCALE_INT 4
+#define AWQ_APPLY_ZERO_INT 8
+#define AWQ_APPLY_SCALE_UNSIGNED 16
+#define AWQ_APPLY_ZERO_UNSIGNED 32
+/* (ABI 17) mode 0's clamp as torch's GPU kernels evaluate it: clamp(-0, 0, qmax) = +0 (IEEE
+ * maximum); without it the -0 stays, as torch's CPU clamp keeps an operand equal to the bound.
+ * Together with the ONE_ELEMENT flags left off: the reference quantizer with device="cuda". */
+#define AWQ_APPLY_IEEE_CLAMP 64
 
 /* The same two ops with torch's type promotion (ABI 15; replaces awq.py:245 and awq.py:282 for
  * parameters of any dtype, e.g. bf16 weights with fp32 per-channel scales, or quantize()'s
@@ -156,13 +172,17 @@ int awq_apply_params(const void* x, int dtype, int64_t rows, int64_t K, int64_t 
  *   mode 0: a = x / s in op1_dtype; t = a + z in op2_dtype; round, clamp(qmin, qmax)
  *   mode 1: a = x - z in op1_dtype; t = a * s in op2_dtype
  * op1_dtype / op2_dtype are torch's result dtypes of the two ops (the caller's promotion);
- * out [rows, K] is op2_dtype.  x_dtype and the op dtypes may also be AWQ_DTYPE_I32 (int32
- * tensor_q; an int32 op — mode 1 only — wraps like torch's int32 kernels).  Each op: operands
- * converted to its dtype (c10::convert; bf16 / fp16 through fp32), fp32 math for bf16 / fp16 /
- * fp32 (fp64 for fp64), result rounded to the dtype — except that a parameter flagged
- * AWQ_APPLY_*_ONE_ELEMENT enters a bf16 / fp16 op at its own value in fp32 (ATen's reduced-float
- * kernels read a one-element operand's original value).  scales / zeros: the parameters' exact
- * values as doubles, [rows, G] as in awq_apply_params (group_size 1 = one per element).
+ * out [rows, K] is op2_dtype.  x_dtype may be any integer code too (int64 / int32 / int16 /
+ * int8 / uint8 / bool / uint16 / uint32 / uint64 tensors: the reference evaluates awq.py:245 and
+ * :282 for any tensor dtype), the op dtypes I32 .. U8 (mode 1 only; integer ops wrap at their
+ * width like torch's integer kernels).  Each op: operands converted to its dtype (c10::convert:
+ * a float to bf16 / fp16 through fp32; an integer to a float dtype as RN_f32 of the exact
+ * integer, then RN to bf16 / fp16, to fp64 directly; to an integer dtype by truncation), fp32
+ * math for bf16 / fp16 / fp32 (fp64 for fp64), result rounded to the dtype — except that a
+ * parameter flagged AWQ_APPLY_*_ONE_ELEMENT enters a bf16 / fp16 op at its own value in fp32
+ * (ATen's reduced-float CPU kernels read a one-element operand's original value).  scales /
+ * zeros: the parameters' exact values as doubles (or int64 / uint64 words, AWQ_APPLY_*_INT),
+ * [rows, G] as in awq_apply_params (group_size 1 = one per element).
  * awq_apply_params(x, D, ...) = awq_apply_params_ex(x, D, ..., D, D, both flags, ...). */
 int awq_apply_params_ex(const void* x, int x_dtype, int64_t rows, int64_t K, int64_t group_size,
                         const double* scales, const double* zeros, int qmin, int qmax, int mode, int op1_dtype,

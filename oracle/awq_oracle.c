@@ -337,63 +337,114 @@ int oracle_apply_params(const void* x, int dtype, int64_t rows, int64_t K, int64
     return 0;
 }
 
-/* awq.py:245 and awq.py:282 under torch's type promotion (round 5): the two ops of
+/* awq.py:245 and awq.py:282 under torch's type promotion (round 5; integer tensors round 6):
+ * the two ops of
  *   mode 0  round(tensor / scale + zero_point).clamp(qmin, qmax)
  *   mode 1  (tensor_q - zero_point) * scale
  * are evaluated in their own result dtypes d1 (first op) and d2 (second op) — torch's
  * result_type of the operands — one element per parameter (the caller has broadcast
  * everything to the result's shape).  An operand of another dtype is converted to the op's
- * dtype first (c10::convert: through fp32 for bf16 / fp16), EXCEPT a one-element parameter
- * of a bf16 / fp16 op (flags bit 0: scale, bit 1: zero_point), which ATen's reduced-float
- * kernels read at its original value in fp32 (TensorIterator::original_scalar_value) —
- * checked against torch on CPU by tests/golden/golden_promote.* (reference calls).
- * Dtype codes: the four float codes + AWQ_ORACLE_I32 (an int32 tensor_q, an int32 first op
- * of mode 1: wrap-around arithmetic like torch's int32 kernels). */
-static inline double load_any(const void* x, int dtype, int64_t i) {
-    if (dtype == AWQ_ORACLE_I32) return (double)((const int32_t*)x)[i];
-    return load_elem(x, dtype, i);
+ * dtype first (c10::convert: an integer to bf16 / fp16 through fp32, i.e. RN_f32 of the
+ * exact integer, then RN to the op dtype; to an integer dtype by truncation to its width),
+ * EXCEPT a one-element parameter of a bf16 / fp16 op (flags bit 0: scale, bit 1:
+ * zero_point), which ATen's reduced-float CPU kernels read at its original value in fp32
+ * (TensorIterator::original_scalar_value) — checked against torch on CPU by
+ * tests/golden/golden_promote*.* (reference calls).  Integer ops wrap at their width, like
+ * torch's integer kernels.
+ * Dtype codes: the four float codes, AWQ_ORACLE_I32 .. AWQ_ORACLE_U8 (tensor and op dtypes),
+ * AWQ_ORACLE_BOOL / U16 / U32 / U64 (tensor dtypes only: torch has no such op here).
+ * Parameters: doubles (exact float values), or — flags bit 2 (scale) / bit 3 (zero_point) —
+ * int64 values in the same arrays (bit 4 / 5: those int64 words are uint64).  Bit 6: torch's
+ * GPU clamp (IEEE maximum: clamp(-0, 0, qmax) = +0; the CPU clamp keeps the -0), with bits 0 / 1
+ * clear — the reference evaluated with device="cuda". */
+typedef struct { double f; int64_t i; int kind; } oval;     /* kind 0 float, 1 int64, 2 uint64 */
+static inline int is_int_code(int d) { return d >= AWQ_ORACLE_I32; }
+static inline oval of_f(double f) { oval v = {f, 0, 0}; return v; }
+static inline oval of_i(int64_t i, int kind) { oval v = {0.0, i, kind}; return v; }
+static oval load_val(const void* x, int dtype, int64_t i) {
+    switch (dtype) {
+    case AWQ_ORACLE_I32: return of_i(((const int32_t*)x)[i], 1);
+    case AWQ_ORACLE_I64: return of_i(((const int64_t*)x)[i], 1);
+    case AWQ_ORACLE_I16: return of_i(((const int16_t*)x)[i], 1);
+    case AWQ_ORACLE_I8: return of_i(((const int8_t*)x)[i], 1);
+    case AWQ_ORACLE_U8: return of_i(((const uint8_t*)x)[i], 1);
+    case AWQ_ORACLE_BOOL: return of_i(((const uint8_t*)x)[i] != 0, 1);
+    case AWQ_ORACLE_U16: return of_i(((const uint16_t*)x)[i], 1);
+    case AWQ_ORACLE_U32: return of_i(((const uint32_t*)x)[i], 1);
+    case AWQ_ORACLE_U64: return of_i(((const int64_t*)x)[i], 2);
+    default: return of_f(load_elem(x, dtype, i));
+    }
 }
-static inline double wrap_i32(double v) { return (double)(int32_t)(uint32_t)(uint64_t)(int64_t)v; }
-static inline double convert_to(double v, int d) {          /* v held exactly */
-    if (d == AWQ_ORACLE_I32) return wrap_i32(v);
-    return d == AWQ_ORACLE_F64 ? v : rn((double)(float)v, d);
+static inline int64_t wrap_to(uint64_t v, int d) {           /* truncation to d's width */
+    switch (d) {
+    case AWQ_ORACLE_I32: return (int32_t)(uint32_t)v;
+    case AWQ_ORACLE_I16: return (int16_t)(uint16_t)v;
+    case AWQ_ORACLE_I8: return (int8_t)(uint8_t)v;
+    case AWQ_ORACLE_U8: return (uint8_t)v;
+    default: return (int64_t)v;
+    }
 }
-static inline double enter(double v, int d, int one_element) {
-    if (one_element && (d == AWQ_ORACLE_BF16 || d == AWQ_ORACLE_F16)) return (double)(float)v;
-    return convert_to(v, d);
+static inline float int_to_f32(oval v) { return v.kind == 2 ? (float)(uint64_t)v.i : (float)v.i; }
+static oval convert_val(oval v, int d) {
+    if (is_int_code(d)) {
+        if (v.kind) return of_i(wrap_to((uint64_t)v.i, d), 1);
+        return of_i(wrap_to((uint64_t)(int64_t)v.f, d), 1);       /* not reached by torch's promotion */
+    }
+    if (v.kind == 0) return of_f(d == AWQ_ORACLE_F64 ? v.f : rn((double)(float)v.f, d));
+    if (d == AWQ_ORACLE_F64) return of_f(v.kind == 2 ? (double)(uint64_t)v.i : (double)v.i);
+    return of_f(rn((double)int_to_f32(v), d));
 }
-static double op2(char op, double a, double b, int d) {
-    if (d == AWQ_ORACLE_I32) {
-        int64_t ia = (int64_t)a, ib = (int64_t)b;
-        return wrap_i32((double)(op == '-' ? ia - ib : op == '*' ? ia * ib : ia + ib));
+static oval param_val(const double* a, int64_t i, int is_int, int is_unsigned) {
+    if (!is_int) return of_f(a[i]);
+    int64_t w;
+    memcpy(&w, &a[i], 8);
+    return of_i(w, is_unsigned ? 2 : 1);
+}
+static oval enter_val(oval v, int d, int one_element) {
+    if (one_element && (d == AWQ_ORACLE_BF16 || d == AWQ_ORACLE_F16))
+        return of_f(v.kind ? (double)int_to_f32(v) : (double)(float)v.f);
+    return convert_val(v, d);
+}
+static oval op2v(char op, oval a, oval b, int d) {               /* a, b already in dtype d */
+    if (is_int_code(d)) {
+        uint64_t ua = (uint64_t)a.i, ub = (uint64_t)b.i;
+        return of_i(wrap_to(op == '-' ? ua - ub : op == '*' ? ua * ub : ua + ub, d), 1);
     }
     if (d == AWQ_ORACLE_F64)
-        return op == '/' ? a / b : op == '-' ? a - b : op == '*' ? a * b : a + b;
-    float fa = (float)a, fb = (float)b;
+        return of_f(op == '/' ? a.f / b.f : op == '-' ? a.f - b.f : op == '*' ? a.f * b.f : a.f + b.f);
+    float fa = (float)a.f, fb = (float)b.f;
     float r = op == '/' ? fa / fb : op == '-' ? fa - fb : op == '*' ? fa * fb : fa + fb;
-    return rn((double)r, d);
+    return of_f(rn((double)r, d));
 }
-static inline void store_any(void* out, int dtype, int64_t i, double v) {
-    if (dtype == AWQ_ORACLE_I32) ((int32_t*)out)[i] = (int32_t)v;
-    else store_elem(out, dtype, i, v);
+static void store_val(void* out, int d, int64_t i, oval v) {
+    switch (d) {
+    case AWQ_ORACLE_I32: ((int32_t*)out)[i] = (int32_t)v.i; break;
+    case AWQ_ORACLE_I64: ((int64_t*)out)[i] = v.i; break;
+    case AWQ_ORACLE_I16: ((int16_t*)out)[i] = (int16_t)v.i; break;
+    case AWQ_ORACLE_I8: ((int8_t*)out)[i] = (int8_t)v.i; break;
+    case AWQ_ORACLE_U8: ((uint8_t*)out)[i] = (uint8_t)v.i; break;
+    default: store_elem(out, d, i, v.f);
+    }
 }
 int oracle_apply_params_ex(const void* x, int xdt, int64_t n, const double* scales, const double* zeros, int qmin,
                            int qmax, int mode, int d1, int d2, int flags, void* out) {
-    if (!x || !scales || !zeros || !out || n < 0 || xdt < 0 || xdt > AWQ_ORACLE_I32 || d1 < 0 ||
-        d1 > AWQ_ORACLE_I32 || d2 < 0 || d2 > AWQ_ORACLE_I32 || (mode == 0 && (d1 == AWQ_ORACLE_I32 ||
-        d2 == AWQ_ORACLE_I32)))
+    if (!x || !scales || !zeros || !out || n < 0 || xdt < 0 || xdt > AWQ_ORACLE_U64 || d1 < 0 ||
+        d1 > AWQ_ORACLE_U8 || d2 < 0 || d2 > AWQ_ORACLE_U8 || (mode == 0 && (is_int_code(d1) || is_int_code(d2))) ||
+        (flags & ~127))
         return -1;
     for (int64_t i = 0; i < n; ++i) {
-        double v = convert_to(load_any(x, xdt, i), d1), t;
+        oval v = convert_val(load_val(x, xdt, i), d1), t;
+        oval s = param_val(scales, i, flags & 4, flags & 16), z = param_val(zeros, i, flags & 8, flags & 32);
         if (mode == 0) {
-            t = op2('/', v, enter(scales[i], d1, flags & 1), d1);                       /* awq.py:245 */
-            t = op2('+', convert_to(t, d2), enter(zeros[i], d2, flags & 2), d2);
-            t = op_clamp(op_round(t, d2), qmin, qmax);                                  /* awq.py:248 */
+            t = op2v('/', v, enter_val(s, d1, flags & 1), d1);                          /* awq.py:245 */
+            t = op2v('+', convert_val(t, d2), enter_val(z, d2, flags & 2), d2);
+            t.f = op_clamp(op_round(t.f, d2), qmin, qmax);                              /* awq.py:248 */
+            if ((flags & 64) && t.f == 0.0 && qmin == 0) t.f = 0.0;   /* GPU clamp: max(-0, +0) = +0 */
         } else {
-            t = op2('-', v, enter(zeros[i], d1, flags & 2), d1);                        /* awq.py:282 */
-            t = op2('*', convert_to(t, d2), enter(scales[i], d2, flags & 1), d2);
+            t = op2v('-', v, enter_val(z, d1, flags & 2), d1);                          /* awq.py:282 */
+            t = op2v('*', convert_val(t, d2), enter_val(s, d2, flags & 1), d2);
         }
-        store_any(out, d2, i, t);
+        store_val(out, d2, i, t);
     }
     return 0;
 }

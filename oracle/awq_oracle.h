@@ -28,10 +28,13 @@ int oracle_group_params(const void* x, int dtype, int64_t rows, int64_t K, int64
 /* awq.py:215-250 (mode 0) / 252-284 (mode 1) with given per-group parameters; out in dtype */
 int oracle_apply_params(const void* x, int dtype, int64_t rows, int64_t K, int64_t L, const double* scales,
                         const double* zeros, int qmin, int qmax, int mode, void* out);
-/* the same ops under torch's type promotion: x of dtype xdt (float codes or AWQ_ORACLE_I32),
- * first op in d1, second in d2 (= out dtype), one parameter per element; flags bit 0 / 1: the
- * scale / zero_point is a one-element operand (original value in a bf16 / fp16 op) */
-enum { AWQ_ORACLE_I32 = 4 };
+/* the same ops under torch's type promotion: x of dtype xdt (float or integer codes), first op
+ * in d1, second in d2 (= out dtype; integer codes up to U8), one parameter per element; flags
+ * bit 0 / 1: the scale / zero_point is a one-element operand (original value in a bf16 / fp16
+ * op); bit 2 / 3: that parameter array holds int64 values (bit 4 / 5: uint64); bit 6: torch's
+ * GPU clamp (clamp(-0, 0, qmax) = +0) */
+enum { AWQ_ORACLE_I32 = 4, AWQ_ORACLE_I64 = 5, AWQ_ORACLE_I16 = 6, AWQ_ORACLE_I8 = 7, AWQ_ORACLE_U8 = 8,
+       AWQ_ORACLE_BOOL = 9, AWQ_ORACLE_U16 = 10, AWQ_ORACLE_U32 = 11, AWQ_ORACLE_U64 = 12 };
 int oracle_apply_params_ex(const void* x, int xdt, int64_t n, const double* scales, const double* zeros, int qmin,
                            int qmax, int mode, int d1, int d2, int flags, void* out);
 int oracle_dequantize(const int32_t* tensor_q, const uint16_t* scales_f16, const int32_t* zeros,

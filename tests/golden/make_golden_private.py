@@ -199,8 +199,131 @@ def main_promote():
     print(f"{len(calls)} calls ({raised} raise), {len(tensors)} tensors")
 
 
+INT_DTYPES = {"i64": torch.int64, "i32": torch.int32, "i16": torch.int16, "i8": torch.int8, "u8": torch.uint8,
+              "bool": torch.bool, "u16": torch.uint16, "u32": torch.uint32, "u64": torch.uint64}
+# int64 values whose conversions round twice (int64 -> fp32 -> bf16 at a bf16 tie, fp32 ties,
+# beyond 2^53) and the int64 extremes
+I64_SPECIAL = [2 ** 30 + 2 ** 22 + 1, -(2 ** 30 + 2 ** 22 + 1), 2 ** 62 + 2 ** 38 + 1, 2 ** 53 + 1, 2 ** 24 + 1,
+               -(2 ** 24 + 3), -2 ** 63, 2 ** 63 - 1, 2 ** 40 + 2 ** 32 + 1, 65519, 65520, -65536]
+
+
+def int_inputs(dt, gen):
+    """Integer / bool tensors: tensor_q-like values, the dtype's full range (int64: with the
+    double-rounding and extreme values above), 3-D, 1-D, 0-d and one-element forms."""
+    if dt == torch.bool:
+        rnd = lambda shape: torch.randint(0, 2, shape, generator=gen).bool()
+        full = rnd
+    else:
+        info = torch.iinfo(dt)
+        lo, hi = max(info.min, -2 ** 62), min(info.max, 2 ** 62)
+
+        def full(shape):
+            if dt == torch.uint64:     # the whole 64-bit range, values >= 2^63 included
+                v = torch.randint(-2 ** 62, 2 ** 62, shape, generator=gen, dtype=torch.int64) * 2
+                return v.view(torch.uint64)
+            return torch.randint(lo, hi, shape, generator=gen, dtype=torch.int64).to(dt)
+
+        def rnd(shape):
+            return torch.randint(0 if info.min == 0 else -8, 16, shape, generator=gen).to(dt)
+    w = full((6, 24))
+    if dt == torch.int64:
+        w.view(-1)[:len(I64_SPECIAL)] = torch.tensor(I64_SPECIAL, dtype=torch.int64)
+    out = {"q6x24": torch.randint(0, 2 if dt == torch.bool else 16, (6, 24), generator=gen).to(dt), "w6x24": w,
+           "v40": full((40,)), "s0d": rnd(()), "e1": full((1,))}
+    if dt in (torch.int64, torch.int8):
+        out["t3x2x8"] = rnd((3, 2, 8))
+    return out
+
+
+def int_variants(x, s, z, gen):
+    """(name, scale, zero_point) for integer tensors: float parameters per channel / 0-d /
+    one-element in every float dtype (jittered off the narrow grids), integer and bool
+    parameters (int / int true division, integer ops that wrap, exact int64 beyond 2^53),
+    and non-per-channel broadcasts."""
+    jit = lambda t: t.double() * (1 + (torch.rand(t.shape, generator=gen, dtype=torch.float64) - 0.5) * 2 ** -7)
+    first = lambda t: t.reshape(-1)[:1]
+    out = []
+    for pn, pdt in DTYPES.items():
+        out.append((f"pc_{pn}", jit(s).to(pdt), z.to(pdt)))
+        out.append((f"0d_{pn}", jit(first(s)).reshape(()).to(pdt), first(z).reshape(()).to(pdt)))
+        out.append((f"1el_{pn}", jit(first(s)).to(pdt), first(z).to(pdt)))
+    R = s.numel()
+    out.append(("z_i64", jit(s).float(), z.to(torch.int64)))
+    out.append(("z_i8_0d", jit(first(s)).reshape(()).bfloat16(), torch.tensor(3, dtype=torch.int8)))
+    out.append(("z_u8", jit(s).half(), z.to(torch.uint8)))
+    out.append(("z_i16_1el", jit(first(s)).bfloat16(), torch.tensor([-300], dtype=torch.int16)))
+    out.append(("si64_zi64_0d", torch.tensor(2, dtype=torch.int64), torch.tensor(5, dtype=torch.int64)))
+    out.append(("si16_zi16", torch.randint(1, 6, s.shape, generator=gen).to(torch.int16),
+                torch.randint(-3, 4, s.shape, generator=gen).to(torch.int16)))
+    out.append(("si8_zu8", torch.randint(-5, 6, s.shape, generator=gen).to(torch.int8),
+                torch.randint(0, 200, s.shape, generator=gen).to(torch.uint8)))
+    out.append(("big_i64_0d", torch.tensor(3, dtype=torch.int64), torch.tensor(2 ** 62 + 2 ** 38 + 1, dtype=torch.int64)))
+    out.append(("big_i64_pc", torch.tensor([-(2 ** 61) - 7] * R, dtype=torch.int64).reshape(s.shape),
+                torch.tensor([2 ** 55 + 3] * R, dtype=torch.int64).reshape(s.shape)))
+    out.append(("z_bool_0d", jit(first(s)).reshape(()).float(), torch.tensor(True)))
+    out.append(("s_bool_z_f16", torch.ones(s.shape, dtype=torch.bool), z.half()))
+    if x.dim() >= 2:
+        C = x.shape[-1]
+        col = lambda n, dt: (0.01 + torch.rand(n, generator=gen, dtype=torch.float64) * 0.05).to(dt)
+        out.append(("bc_lastdim_f32_i32", col(C, torch.float32), torch.randint(0, 15, (C,), generator=gen).int()))
+        out.append(("bc_lastdim_i64", torch.randint(1, 9, (C,), generator=gen), torch.randint(-9, 9, (C,),
+                                                                                               generator=gen)))
+    return out
+
+
+def main_promote_int():
+    """Reference calls of _quantize_tensor / _dequantize_tensor on INTEGER and bool tensors
+    (awq.py:245 / :282 evaluated for any tensor dtype: int64 / int32 / int16 / int8 / uint8 /
+    bool / uint16 / uint32 / uint64) with float, integer and bool parameters in per-channel,
+    0-d, one-element and broadcast forms.  Calls that raise in the reference are recorded with
+    the exception type.
+      tests/golden/golden_promote_int.safetensors / golden_promote_int.json"""
+    tensors, calls = {}, []
+    gen = torch.Generator().manual_seed(6160)
+
+    def put(key, t):
+        tensors[key] = t.detach().contiguous().clone()
+        return key
+
+    def rec(method, params, xk, sk, zk, fn, out_key):
+        c = {"method": method, "params": params, "x": xk, "scale": sk, "zero_point": zk}
+        try:
+            c["out"] = [put(out_key, fn())]
+        except Exception as e:   # the reference raises: record the behaviour
+            c["raises"] = type(e).__name__
+            c["message"] = str(e)
+        calls.append(c)
+
+    qparams = [{"bits": 4, "group_size": 128, "symmetric": False, "per_channel": True},
+               {"bits": 8, "group_size": 128, "symmetric": True, "per_channel": False}]
+    for dn, dt in INT_DTYPES.items():
+        for name, x in int_inputs(dt, gen).items():
+            xk = put(f"in.{dn}.{name}", x)
+            # realistic parameters: the reference's own per-channel scale / zero point of a
+            # float tensor of x's shape (values near tensor_q's range)
+            xf = torch.randn(tuple(x.shape), generator=torch.Generator().manual_seed(41))
+            for qi, params in enumerate(qparams):
+                q = AWQQuantizer(device="cpu", **params)
+                s, z = q._calculate_scale_zp(xf)
+                for vn, sv, zv in int_variants(x, s, z, gen):
+                    base = f"{dn}.q{qi}.{name}.{vn}"
+                    sk, zk = put(f"{base}.s", sv), put(f"{base}.z", zv)
+                    rec("_quantize_tensor", params, xk, sk, zk, lambda: q._quantize_tensor(x, sv, zv), f"{base}.qt")
+                    rec("_dequantize_tensor", params, xk, sk, zk, lambda: q._dequantize_tensor(x, sv, zv),
+                        f"{base}.dqt")
+    save_file(tensors, os.path.join(HERE, "golden_promote_int.safetensors"))
+    with open(os.path.join(HERE, "golden_promote_int.json"), "w") as f:
+        json.dump({"generator": "tests/golden/make_golden_private.py --promote-int", "torch": torch.__version__,
+                   "reference": "shanefitch/AWQ-Converter src/awq_quantizer/quantization/awq.py:215-284",
+                   "calls": calls}, f, indent=0)
+    raised = sum("raises" in c for c in calls)
+    print(f"{len(calls)} calls ({raised} raise), {len(tensors)} tensors")
+
+
 if __name__ == "__main__":
-    if "--promote" in sys.argv[1:]:
+    if "--promote-int" in sys.argv[1:]:
+        main_promote_int()
+    elif "--promote" in sys.argv[1:]:
         main_promote()
     else:
         main()

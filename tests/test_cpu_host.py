@@ -31,7 +31,7 @@ def test_library_exports_every_declared_symbol():
     for s in syms:
         assert hasattr(lib, s), s
     assert set(syms) == set(_hip.SIGNATURES), "python binding out of sync with include/*.h"
-    assert lib.awq_abi_version() == _hip.ABI_VERSION == 16
+    assert lib.awq_abi_version() == _hip.ABI_VERSION == 17
 
 
 def test_product_library_has_no_diagnostics_entry_points():

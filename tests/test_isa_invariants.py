@@ -31,31 +31,61 @@ def _regs(text):
     return out
 
 
+# instructions counted by LGKM_CNT: LDS (return in issue order, like the ring reads) and
+# SMEM / FLAT / messages (may return out of order: with one of them outstanding, only
+# lgkmcnt(0) says which reads are done)
+_LDS = re.compile(r"ds_\w+")
+_OUT_OF_ORDER = re.compile(r"(s_load_|s_buffer_load_|s_scratch_load_|s_memtime|s_memrealtime|s_sendmsg|s_dcache_|"
+                           r"s_atc_probe|flat_)\w*")
+
+
 def ring_violations(asm: str, func_rx: str):
     """(function, line, instruction) for every instruction that touches a register an
-    inline ds_read_b128 is still loading (lgkmcnt(N) retires all but the N youngest reads:
-    LDS reads complete in order)."""
+    inline-asm ds_read_b128 is still loading.  Every LGKM-counted instruction is modelled,
+    not only the asm reads: LDS instructions retire in issue order, so lgkmcnt(N) retires all
+    but the N youngest of them; an out-of-order one (SMEM, FLAT, s_sendmsg) still outstanding
+    at an lgkmcnt(N > 0) while ring reads are pending makes that wait ambiguous, and is
+    reported as a violation on the wait itself.  Inline-asm reads are told from the
+    compiler's own by the ;;#ASMSTART / ;;#ASMEND brackets."""
     bad, funcs = [], re.findall(r"^(" + func_rx + r"\w*):", asm, re.M)
     for f in funcs:
         i = asm.index(f + ":")
         body = asm[i:asm.index(".Lfunc_end", i)].split("\n")
-        pending = []                                   # [(issue order, registers)]
+        pending = []                                   # [(in order?, watched registers)] in issue order
+        in_asm = False
         for n, line in enumerate(body):
             s = line.strip()
-            if not s or s.startswith(";"):
+            if s.startswith(";;#ASMSTART"):
+                in_asm = True
                 continue
-            m = re.match(r"ds_read_b128 (v\[\d+:\d+\]), v\d+", s)
-            if m:
-                pending.append(_regs(m.group(1)))
+            if s.startswith(";;#ASMEND"):
+                in_asm = False
+                continue
+            if not s or s.startswith(";"):
                 continue
             m = re.match(r"s_waitcnt .*lgkmcnt\((\d+)\)", s)
             if m:
                 k = int(m.group(1))
+                watched = any(regs for _, regs in pending)
+                if k and watched and any(not in_order for in_order, _ in pending):
+                    bad.append((f, n, s + "  (ambiguous: an out-of-order LGKM op is outstanding)"))
                 pending = pending[len(pending) - k:] if k else []
+                continue
+            op = s.split()[0]
+            if _LDS.fullmatch(op):
+                m = re.match(r"ds_read_b128 (v\[\d+:\d+\]), v\d+", s)
+                watch = _regs(m.group(1)) if (m and in_asm) else set()
+                live = set().union(*(r for _, r in pending)) if pending else set()
+                if live & _regs(s):
+                    bad.append((f, n, s))
+                pending.append((True, watch))
+                continue
+            if _OUT_OF_ORDER.fullmatch(op):
+                pending.append((False, set()))
                 continue
             if re.match(r"(s_|\.|[A-Za-z_.$][\w.$]*:)", s):
                 continue
-            live = set().union(*pending) if pending else set()
+            live = set().union(*(r for _, r in pending)) if pending else set()
             if live & _regs(s):
                 bad.append((f, n, s))
     return funcs, bad
@@ -72,13 +102,18 @@ def test_act_loss_ring_registers_untouched_until_their_wait(tmp_path):
     funcs, bad = ring_violations(asm, r"_ZN3awq12_GLOBAL__N_115act_loss_kernel")
     assert len(funcs) >= 12, "loss-kernel instantiations not found in the ISA"
     assert "ds_read_b128" in asm and "global_load_lds_dwordx4" in asm, "the LDS ring is not in the build"
+    assert re.search(r";;#ASMSTART\s*\n\s*ds_read_b128 v\[", asm), "no inline-asm ring read to watch"
     assert not bad, bad[:5]
 
 
 def test_ring_checker_flags_an_early_use():
     asm = """_ZN3awq12_GLOBAL__N_115act_loss_kernelX:
+\t;;#ASMSTART
 \tds_read_b128 v[4:7], v1 offset:0
+\t;;#ASMEND
+\t;;#ASMSTART
 \tds_read_b128 v[8:11], v1 offset:16
+\t;;#ASMEND
 \ts_waitcnt lgkmcnt(1)
 \tv_mul_f32_e32 v2, v4, v3
 \tv_mov_b32_e32 v12, v9
@@ -89,3 +124,22 @@ def test_ring_checker_flags_an_early_use():
     funcs, bad = ring_violations(asm, r"_ZN3awq12_GLOBAL__N_115act_loss_kernel")
     assert len(funcs) == 1
     assert [b[2] for b in bad] == ["v_mov_b32_e32 v12, v9"]
+
+
+def test_ring_checker_models_other_lgkm_instructions():
+    """A compiler LDS op issued after the ring reads shifts what lgkmcnt(N) retires; an SMEM
+    load outstanding at lgkmcnt(N > 0) makes the wait ambiguous."""
+    head = "_ZN3awq12_GLOBAL__N_115act_loss_kernelX:\n\t;;#ASMSTART\n\tds_read_b128 v[4:7], v1 offset:0\n\t;;#ASMEND\n"
+    # ds_read_b32 by the compiler after the ring read: lgkmcnt(1) retires only the ring read
+    ok = head + "\tds_read_b32 v20, v1 offset:64\n\ts_waitcnt lgkmcnt(1)\n\tv_mov_b32_e32 v12, v5\n.Lfunc_end0:\n"
+    assert ring_violations(ok, r"_ZN3awq12_GLOBAL__N_115act_loss_kernel")[1] == []
+    # ... but lgkmcnt(2) with one younger compiler op leaves the ring read outstanding
+    early = head + "\tds_read_b32 v20, v1 offset:64\n\ts_waitcnt lgkmcnt(1)\n\tds_write_b32 v1, v3\n" \
+        "\ts_waitcnt lgkmcnt(1)\n\tv_mov_b32_e32 v12, v5\n.Lfunc_end0:\n"
+    assert ring_violations(early, r"_ZN3awq12_GLOBAL__N_115act_loss_kernel")[1] == []
+    late = head + "\tds_read_b32 v20, v1 offset:64\n\ts_waitcnt lgkmcnt(2)\n\tv_mov_b32_e32 v12, v5\n.Lfunc_end0:\n"
+    assert [b[2] for b in ring_violations(late, r"_ZN3awq12_GLOBAL__N_115act_loss_kernel")[1]] == \
+        ["v_mov_b32_e32 v12, v5"]
+    smem = head + "\ts_load_dword s4, s[0:1], 0x0\n\ts_waitcnt lgkmcnt(1)\n\tv_mov_b32_e32 v12, v5\n.Lfunc_end0:\n"
+    bad = ring_violations(smem, r"_ZN3awq12_GLOBAL__N_115act_loss_kernel")[1]
+    assert bad and "ambiguous" in bad[0][2]

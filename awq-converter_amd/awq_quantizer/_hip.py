@@ -103,6 +103,7 @@ SIGNATURES = {
     "awq_plan_ragged": (_I64, [ctypes.POINTER(TensorDesc), _I32, _I32, _I64]),
     "awq_stream_copy": (_I32, [_P, _P, _I64, _P]),
     "awq_stream_ceiling": (_I32, [_P, _P, _I64, _P]),
+    "awq_dequant_ceiling": (_I32, [_P, _P, _I64, _P]),
     "awq_export_autoawq_gemm": (_I32, [_P, _P, _P, _I64, _I64, _I64, _I32, _P, _P, _P, _P]),
     "awq_plan_block_tensor": (_I64, [ctypes.POINTER(TensorDesc), _I32, _I64, _P, _I64]),
     "awq_ragged_flags": (_I32, [ctypes.POINTER(TensorDesc), _I32, _I64]),
@@ -385,6 +386,14 @@ def stream_ceiling(src: torch.Tensor, dst: torch.Tensor, stream: int) -> None:
         raise ValueError("stream_ceiling: dst must hold a quarter of src's bytes")
     rc = load_library().awq_stream_ceiling(ptr(src), ptr(dst), n, ctypes.c_void_p(stream))
     check(rc, "awq_stream_ceiling")
+
+
+def dequant_ceiling(words: torch.Tensor, out: torch.Tensor, stream: int) -> None:
+    """awq_dequant_ceiling: read out.nbytes / 8 of words, write out whole (dequantize's structure)."""
+    n = out.numel() * out.element_size()
+    if words.numel() * words.element_size() < n // 8:
+        raise ValueError("dequant_ceiling: words must hold an eighth of out's bytes")
+    check(load_library().awq_dequant_ceiling(ptr(words), ptr(out), n, ctypes.c_void_p(stream)), "awq_dequant_ceiling")
 
 
 def export_autoawq_gemm(qweight, qzeros, scales, N: int, K: int, L: int, bits: int, qweight_t, qzeros_t,

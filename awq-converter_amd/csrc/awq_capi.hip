@@ -452,6 +452,15 @@ int awq_stream_ceiling(const void* src, void* dst, int64_t bytes, void* stream) 
     return hip_status(awq::launch_stream_ceiling(src, dst, bytes, (hipStream_t)stream), "awq stream ceiling");
 }
 
+int awq_dequant_ceiling(const void* words, void* out, int64_t out_bytes, void* stream) {
+    g_err.clear();
+    if (out_bytes < 0 || out_bytes % 16 != 0) return fail(AWQ_EINVAL, "out_bytes must be a non-negative multiple of 16");
+    if (out_bytes > 0 && (!words || !out || !aligned(words, 4) || !aligned(out, 16)))
+        return fail(AWQ_EINVAL, "null or misaligned buffer");
+    if (out_bytes / 16 > ((int64_t)1 << 40)) return fail(AWQ_EINVAL, "out_bytes too large");
+    return hip_status(awq::launch_dequant_ceiling(words, out, out_bytes, (hipStream_t)stream), "awq dequant ceiling");
+}
+
 // ---- activation-aware scale search (include/awq_hip.h awq_act_*) ----
 namespace {
 int check_act_shape(int dtype, int64_t rows, int64_t K, int64_t group_size) {

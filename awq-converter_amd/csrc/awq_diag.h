@@ -29,7 +29,8 @@ typedef struct awq_tuning {
                                 (per-thread stores), 2 / 3 LDS-staged words with / without
                                 XCD-contiguous blocks, 4 / 5 four-output lanes without / with,
                                 6 / 7 batched four-output lanes (4 / 8 per lane), 8 / 9 the
-                                same in XCD runs */
+                                same in XCD runs; 10 / 11 2 / 1 per lane in XCD runs of 4
+                                blocks, 12 2 per lane without runs, 13 2 per lane in runs of 8 */
     int32_t rg_p1;           /* row-segment pass 1: 0 / 1 by groups (2^k lanes per group, DPP
                                 merges), 2 evenly split runs (NT / groups lanes per group, LDS
                                 merges, parameters by one lane per group) */

@@ -915,7 +915,33 @@ template <int B> constexpr auto dq_quads_remap = awq_dequant_quads_kernel<B, tru
 template <int B> constexpr auto dq_batch4 = awq_dequant_batch_kernel<B, 4, 0, 0>;
 template <int B> constexpr auto dq_batch8 = awq_dequant_batch_kernel<B, 8, 0, 0>;
 template <int B> constexpr auto dq_batch8_run = awq_dequant_batch_kernel<B, 8, 2, 0>;
+template <int B> constexpr auto dq_batch2_run = awq_dequant_batch_kernel<B, 2, 4, 0>;
+template <int B> constexpr auto dq_batch1_run = awq_dequant_batch_kernel<B, 1, 4, 0>;
+template <int B> constexpr auto dq_batch2 = awq_dequant_batch_kernel<B, 2, 0, 0>;
+template <int B> constexpr auto dq_batch2_run8 = awq_dequant_batch_kernel<B, 2, 8, 0>;
 #endif
+
+// Measurement helper (awq_dequant_ceiling): the batched dequantize's memory structure without its
+// arithmetic and parameter loads — per quad one 4-B nt load of the packed word (a lane pair
+// shares it) and one 16-B nt store (1 KiB per wave instruction), U quads per lane with the loads
+// issued first: read 1 : write 8, the 4-bit dequantize's ratio.
+template <int U>
+__global__ __launch_bounds__(256) void awq_dequant_ceiling_kernel(const uint32_t* __restrict__ words,
+                                                                  float* __restrict__ out, int64_t quads) {
+    const int64_t q0 = (int64_t)blockIdx.x * (256 * U) + threadIdx.x;
+    uint32_t w[U];
+#pragma unroll
+    for (int k = 0; k < U; ++k) w[k] = __builtin_nontemporal_load(words + min(q0 + 256 * k, quads - 1) / 2);
+    typedef float f4 __attribute__((ext_vector_type(4)));
+#pragma unroll
+    for (int k = 0; k < U; ++k) {
+        const int64_t q = q0 + 256 * k;
+        if (q >= quads) break;
+        const uint32_t v = w[k] >> (16 * (int)(q & 1));
+        const f4 o = {(float)(v & 15u), (float)((v >> 4) & 15u), (float)((v >> 8) & 15u), (float)((v >> 12) & 15u)};
+        __builtin_nontemporal_store(o, (f4*)(out + 4 * q));
+    }
+}
 
 inline unsigned grid_for(int64_t work, int64_t per_block, int64_t cap) {
     int64_t b = (work + per_block - 1) / per_block;
@@ -1008,6 +1034,14 @@ hipError_t launch_apply(const void* x, int xdt, int64_t rows, int64_t K, int64_t
     return hipPeekAtLastError();
 }
 
+hipError_t launch_dequant_ceiling(const void* words, void* out, int64_t out_bytes, hipStream_t stream) {
+    const int64_t quads = out_bytes / 16;
+    if (quads <= 0) return hipSuccess;
+    hipLaunchKernelGGL(awq_dequant_ceiling_kernel<2>, dim3((unsigned)((quads + 511) / 512)), dim3(256), 0, stream,
+                       (const uint32_t*)words, (float*)out, quads);
+    return hipPeekAtLastError();
+}
+
 hipError_t launch_pack(const int32_t* v, int64_t rows, int64_t n, int bits, int qmin,
                        int32_t* packed, hipStream_t stream) {
     const int per = 32 / bits;
@@ -1042,7 +1076,7 @@ hipError_t launch_dequant(const int32_t* tensor_q, const int32_t* qweight, const
         int v = kDqDefault;
         const float invL = 1.0f / (float)L;
 #ifdef AWQ_DIAG
-        if (gmode == 0 && tuning().dq_words_v1 > 0 && tuning().dq_words_v1 <= 9) v = tuning().dq_words_v1;
+        if (gmode == 0 && tuning().dq_words_v1 > 0 && tuning().dq_words_v1 <= 13) v = tuning().dq_words_v1;
 #endif
 #define AWQ_DQ(KER, GRID)                                                                                   \
         do {                                                                                                \
@@ -1058,6 +1092,10 @@ hipError_t launch_dequant(const int32_t* tensor_q, const int32_t* qweight, const
             grid_b8((unsigned)((words * (per / 4) + 2047) / 2048));
         switch (v) {
 #ifdef AWQ_DIAG
+        case 10: AWQ_DQ(dq_batch2_run, dim3((unsigned)((words * (per / 4) + 511) / 512))); break;
+        case 11: AWQ_DQ(dq_batch1_run, grid_q); break;
+        case 12: AWQ_DQ(dq_batch2, dim3((unsigned)((words * (per / 4) + 511) / 512))); break;
+        case 13: AWQ_DQ(dq_batch2_run8, dim3((unsigned)((words * (per / 4) + 511) / 512))); break;
         case 6: AWQ_DQ(dq_batch4, grid_b4); break;
         case 7: AWQ_DQ(dq_batch8, grid_b8); break;
         case 9: AWQ_DQ(dq_batch8_run, grid_b8); break;

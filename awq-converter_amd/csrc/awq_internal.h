@@ -207,6 +207,7 @@ hipError_t launch_rowgroup(const void* w, int dtype, int64_t rows, int64_t K, in
 hipError_t launch_selftest(int which, unsigned long long* out, hipStream_t stream);
 hipError_t launch_stream_copy(const void* src, void* dst, int64_t bytes, hipStream_t stream);
 hipError_t launch_stream_ceiling(const void* src, void* dst, int64_t bytes, hipStream_t stream);
+hipError_t launch_dequant_ceiling(const void* words, void* out, int64_t out_bytes, hipStream_t stream);
 hipError_t launch_export_gemm(const int32_t* qweight, const int32_t* qzeros, const uint16_t* scales, int64_t N,
                               int64_t K, int64_t group_size, int32_t* qweight_t, int32_t* qzeros_t,
                               uint16_t* scales_t, hipStream_t stream);

@@ -263,6 +263,13 @@ int awq_stream_copy(const void* src, void* dst, int64_t bytes, void* stream);
  * against this stream's (read + write) rate. */
 int awq_stream_ceiling(const void* src, void* dst, int64_t bytes, void* stream);
 
+/* Measurement helper (ABI 17): awq_dequantize_packed's memory structure for 4-bit outputs without
+ * its arithmetic — reads out_bytes / 8 of `words` (4-B aligned; 4-B nt loads, a lane pair per
+ * dword) and writes out_bytes (16-B aligned, multiple of 16) as 16-B nt stores, 1 KiB per wave
+ * instruction: the 1 : 8 read : write stream the dequantize kernel is quoted against
+ * (scripts/dq_ceiling_bench.py). */
+int awq_dequant_ceiling(const void* words, void* out, int64_t out_bytes, void* stream);
+
 /* Reference dequantize (awq.py:459-539): out fp32 [rows, K] =
  * fp16( fp16(tensor_q - zeros) * scales ) per element.  A NaN result widens its fp16 bits,
  * except in the last n % 8 elements of a group of n = min(group_size, K - g group_size)

@@ -11,7 +11,7 @@
 typedef float f4 __attribute__((ext_vector_type(4)));
 
 // WR_ONLY: no loads.  Thread t of block b handles quads b * 256 U + 256 k + t, k < U.
-template <int U, bool WR_ONLY>
+template <int U, bool WR_ONLY, bool PLAIN = false>
 __global__ __launch_bounds__(256) void dq_mix_kernel(const uint32_t* __restrict__ words, float* __restrict__ out,
                                                      int64_t quads) {
     const int64_t q0 = (int64_t)blockIdx.x * (256 * U) + threadIdx.x;
@@ -19,7 +19,8 @@ __global__ __launch_bounds__(256) void dq_mix_kernel(const uint32_t* __restrict_
 #pragma unroll
     for (int k = 0; k < U; ++k) {
         const int64_t q = q0 + 256 * k;
-        w[k] = WR_ONLY ? (uint32_t)q : __builtin_nontemporal_load(words + min(q, quads - 1) / 2);
+        const uint32_t* a = words + min(q, quads - 1) / 2;
+        w[k] = WR_ONLY ? (uint32_t)q : PLAIN ? *a : __builtin_nontemporal_load(a);
     }
 #pragma unroll
     for (int k = 0; k < U; ++k) {
@@ -31,14 +32,64 @@ __global__ __launch_bounds__(256) void dq_mix_kernel(const uint32_t* __restrict_
     }
 }
 
-template <int U, bool WR_ONLY>
+// Persistent form: gridDim.x blocks loop over the chunks of 256 U quads, the next chunk's
+// words loaded before the current chunk's stores (software pipelined), so a wave keeps
+// stores and loads in flight without wave turnover.
+template <int U>
+__global__ __launch_bounds__(256) void dq_persist_kernel(const uint32_t* __restrict__ words, float* __restrict__ out,
+                                                         int64_t quads) {
+    const int64_t chunks = (quads + 256 * U - 1) / (256 * U);
+    int64_t c = blockIdx.x;
+    uint32_t w[U];
+    auto load = [&](int64_t cc) {
+#pragma unroll
+        for (int k = 0; k < U; ++k) w[k] = words[min(cc * (256 * U) + 256 * k + threadIdx.x, quads - 1) / 2];
+    };
+    if (c < chunks) load(c);
+    for (; c < chunks; c += gridDim.x) {
+        uint32_t cur[U];
+#pragma unroll
+        for (int k = 0; k < U; ++k) cur[k] = w[k];
+        if (c + gridDim.x < chunks) load(c + gridDim.x);
+#pragma unroll
+        for (int k = 0; k < U; ++k) {
+            const int64_t q = c * (256 * U) + 256 * k + threadIdx.x;
+            if (q >= quads) break;
+            const uint32_t v = cur[k] >> (16 * (int)(q & 1));
+            const f4 o = {(float)(v & 15u), (float)((v >> 4) & 15u), (float)((v >> 8) & 15u), (float)((v >> 12) & 15u)};
+            __builtin_nontemporal_store(o, (f4*)(out + 4 * q));
+        }
+    }
+}
+
+template <int U>
+static void run_persist(const char* name, int blocks_per_cu, const uint32_t* words, float* out, int64_t elems,
+                        hipEvent_t a, hipEvent_t b) {
+    const int64_t quads = elems / 4;
+    const dim3 grid(256u * blocks_per_cu);
+    for (int i = 0; i < 3; ++i) hipLaunchKernelGGL((dq_persist_kernel<U>), grid, dim3(256), 0, 0, words, out, quads);
+    const int iters = 20;
+    (void)hipEventRecord(a, 0);
+    for (int i = 0; i < iters; ++i) hipLaunchKernelGGL((dq_persist_kernel<U>), grid, dim3(256), 0, 0, words, out, quads);
+    (void)hipEventRecord(b, 0);
+    (void)hipEventSynchronize(b);
+    float ms = 0;
+    (void)hipEventElapsedTime(&ms, a, b);
+    const double us = ms * 1e3 / iters;
+    printf("{\"probe\": \"%s\", \"U\": %d, \"blocks_per_cu\": %d, \"elements\": %lld, \"us\": %.1f, \"GBs\": %.1f}\n",
+           name, U, blocks_per_cu, (long long)elems, us, ((double)elems * 4 + (double)elems / 2) / us / 1e3);
+}
+
+template <int U, bool WR_ONLY, bool PLAIN = false>
 static void run(const char* name, const uint32_t* words, float* out, int64_t elems, hipEvent_t a, hipEvent_t b) {
     const int64_t quads = elems / 4;
     const dim3 grid((unsigned)((quads + 256 * U - 1) / (256 * U)));
-    for (int i = 0; i < 3; ++i) hipLaunchKernelGGL((dq_mix_kernel<U, WR_ONLY>), grid, dim3(256), 0, 0, words, out, quads);
+    for (int i = 0; i < 3; ++i)
+        hipLaunchKernelGGL((dq_mix_kernel<U, WR_ONLY, PLAIN>), grid, dim3(256), 0, 0, words, out, quads);
     const int iters = 20;
     (void)hipEventRecord(a, 0);
-    for (int i = 0; i < iters; ++i) hipLaunchKernelGGL((dq_mix_kernel<U, WR_ONLY>), grid, dim3(256), 0, 0, words, out, quads);
+    for (int i = 0; i < iters; ++i)
+        hipLaunchKernelGGL((dq_mix_kernel<U, WR_ONLY, PLAIN>), grid, dim3(256), 0, 0, words, out, quads);
     (void)hipEventRecord(b, 0);
     (void)hipEventSynchronize(b);
     float ms = 0;
@@ -111,13 +162,20 @@ int main() {
         hipEvent_t a, b;
         (void)hipEventCreate(&a);
         (void)hipEventCreate(&b);
+        run<1, true>("store_only", words, out, elems, a, b);
+        run<2, true>("store_only", words, out, elems, a, b);
         run<4, true>("store_only", words, out, elems, a, b);
         run<8, true>("store_only", words, out, elems, a, b);
         run<1, false>("read1_write8", words, out, elems, a, b);
+        run<2, false>("read1_write8", words, out, elems, a, b);
         run<4, false>("read1_write8", words, out, elems, a, b);
         run<8, false>("read1_write8", words, out, elems, a, b);
+        run<4, false, true>("read1_write8_plain", words, out, elems, a, b);
+        run_persist<4>("persist_read1_write8", 4, words, out, elems, a, b);
+        run_persist<4>("persist_read1_write8", 8, words, out, elems, a, b);
+        run_persist<2>("persist_read1_write8", 8, words, out, elems, a, b);
+        run_persist<8>("persist_read1_write8", 4, words, out, elems, a, b);
         run_wide<true>("wide_load_lds", words, out, elems, a, b);
-        run_wide<false>("wide_load_lane_rows", words, out, elems, a, b);
         (void)hipFree(words);
         (void)hipFree(out);
     }

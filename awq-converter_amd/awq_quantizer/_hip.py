@@ -96,6 +96,7 @@ SIGNATURES = {
     "awq_quantize_search_ex": (_I32, [_P, _I32, _I64, _I64, _I32, _I32, _I32, _I32, _I32, _I32, _P, _P, _P, _P, _P,
                                       _P]),
     "awq_group_params": (_I32, [_P, _I32, _I64, _I64, _I64, _I32, _I32, _P, _P, _P]),
+    "awq_group_params_ex": (_I32, [_P, _I32, _I64, _I64, _I64, _I32, _I32, _I32, _P, _P, _P]),
     "awq_apply_params": (_I32, [_P, _I32, _I64, _I64, _I64, _P, _P, _I32, _I32, _I32, _P, _P]),
     "awq_apply_params_ex": (_I32, [_P, _I32, _I64, _I64, _I64, _P, _P, _I32, _I32, _I32, _I32, _I32, _I32, _P, _P]),
     "awq_packs_directly": (_I32, [_I32, _I64, _I64, _I64]),
@@ -226,14 +227,19 @@ def quantize_search(x: torch.Tensor, rows: int, K: int, L: int, bits: int, symme
     check(rc, "awq_quantize_search")
 
 
-def group_params(x: torch.Tensor, rows: int, K: int, L: int, bits: int, symmetric: bool):
-    """awq_group_params: the reference's per-group (scale, zero point) in x's own arithmetic,
-    as exact float64 device tensors [rows, ceil(K / L)]."""
+GP_TORCH_GPU = 1        # include/awq_hip.h AWQ_GP_TORCH_GPU
+
+
+def group_params(x: torch.Tensor, rows: int, K: int, L: int, bits: int, symmetric: bool, torch_gpu: bool = False):
+    """awq_group_params_ex: the reference's per-group (scale, zero point) in x's own arithmetic,
+    as exact float64 device tensors [rows, ceil(K / L)]; torch_gpu: as torch's GPU kernels
+    evaluate awq.py:202-211 (AWQ_GP_TORCH_GPU)."""
     G = -(-K // L) if K else 0
     s = torch.empty((rows, G), dtype=torch.float64, device=x.device)
     z = torch.empty((rows, G), dtype=torch.float64, device=x.device)
-    check(load_library().awq_group_params(ptr(x), AWQ_DTYPE[x.dtype], rows, K, L, bits, int(bool(symmetric)), ptr(s),
-                                          ptr(z), _stream(x)), "awq_group_params")
+    check(load_library().awq_group_params_ex(ptr(x), AWQ_DTYPE[x.dtype], rows, K, L, bits, int(bool(symmetric)),
+                                             GP_TORCH_GPU if torch_gpu else 0, ptr(s), ptr(z), _stream(x)),
+          "awq_group_params_ex")
     return s, z
 
 

@@ -271,15 +271,25 @@ class AWQQuantizer:
     # ------------------------------------------------------------------ reference private methods
     # awq.py:130-374.  Subclasses and callers of the reference reach into these; they keep the
     # reference's signatures, result dtypes and shapes (pinned bit for bit by
-    # tests/test_private_methods.py against 1 024 calls of the reference) and run on the HIP
-    # kernels: awq_group_params (scale / zero point of every group in the input dtype's own
-    # arithmetic), awq_apply_params (element-wise quantize / dequantize with given parameters)
-    # and awq_quantize_groups.  They are the reference's round-to-nearest whatever
-    # scale_method says (the clip search is reached through quantize / quantize_packed).
-    # Results are placed on self.device, as the reference places them.
+    # tests/test_private_methods.py against 1 024 + 2 668 + 4 484 calls of the reference) and
+    # run on the HIP kernels: awq_group_params_ex (scale / zero point of every group in the
+    # input dtype's own arithmetic), awq_apply_params_ex (element-wise quantize / dequantize with
+    # given parameters) and awq_quantize_groups.  They are the reference's round-to-nearest
+    # whatever scale_method says (the clip search is reached through quantize / quantize_packed).
+    # Results are placed where the reference places them (self.device; _compute_scale_zp_for_group:
+    # the input's device), and computed the way torch computes them THERE: the reference moves its
+    # tensors to self.device, whose torch kernels differ from the CPU's in four places — a GPU
+    # divides by a Python int as a product with its reciprocal (the scale, awq.py:202), clamps -0
+    # to +0 (awq.py:211, 248), converts a one-element device parameter to the op dtype first
+    # (awq.py:245, 282) and converts a NaN to int32 as 0 (awq.py:367).  The public API (quantize,
+    # quantize_packed, dequantize, ...) always gives the reference CPU awq.py's bits (north_star).
 
     def _home(self, t: torch.Tensor) -> torch.Tensor:
         return t.to(self.device) if self.device.startswith("cuda") else t.cpu()
+
+    def _torch_gpu(self) -> bool:
+        """The reference would evaluate on a GPU (self.device is a CUDA device)."""
+        return self.device.startswith("cuda")
 
     def _on_gpu(self, tensor: torch.Tensor) -> torch.Tensor:
         self._check_input(tensor)
@@ -287,21 +297,23 @@ class AWQQuantizer:
 
     def _compute_scale_zp_for_group(self, tensor: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
         """awq.py:173-213: (scale, zero_point) of the whole tensor as one group, 0-d tensors
-        of its dtype (zero_point = 0 when symmetric)."""
+        of its dtype (zero_point = 0 when symmetric), on the input's device and computed the way
+        torch computes there (the reference does not move this method's input)."""
         self._check_mode()
         x = self._on_gpu(tensor)
         n = x.numel()
         if n == 0:
             raise RuntimeError("min(): Expected reduction dim to be specified for input.numel() == 0. "
                                "Specify the reduction dim with the 'dim' argument.")
-        s, z = _hip.group_params(x, 1, n, n, self.bits, self.symmetric)
-        return self._home(s.reshape(()).to(tensor.dtype)), self._home(z.reshape(()).to(tensor.dtype))
+        s, z = _hip.group_params(x, 1, n, n, self.bits, self.symmetric, torch_gpu=tensor.is_cuda)
+        return s.reshape(()).to(tensor.device, tensor.dtype), z.reshape(()).to(tensor.device, tensor.dtype)
 
     def _calculate_scale_zp(self, tensor: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
         """awq.py:130-171: one group for the whole tensor (dim <= 1 or per_channel=False),
         else one per dim-0 channel ([C] tensors of the input dtype)."""
         if tensor.dim() <= 1 or not self.per_channel:
-            return self._compute_scale_zp_for_group(tensor)
+            s, z = self._compute_scale_zp_for_group(tensor.to(self._home_device()))   # awq.py:141
+            return s, z
         self._check_mode()
         C = tensor.size(0)
         if C == 0:
@@ -311,8 +323,12 @@ class AWQQuantizer:
         if K == 0:
             raise RuntimeError("min(): Expected reduction dim to be specified for input.numel() == 0. "
                                "Specify the reduction dim with the 'dim' argument.")
-        s, z = _hip.group_params(x, C, K, K, self.bits, self.symmetric)
+        s, z = _hip.group_params(x, C, K, K, self.bits, self.symmetric, torch_gpu=self._torch_gpu())
         return self._home(s.reshape(C).to(tensor.dtype)), self._home(z.reshape(C).to(tensor.dtype))
+
+    def _home_device(self) -> torch.device:
+        """Where the reference's tensor.to(self.device) puts a tensor (awq.py:141, 233, 303)."""
+        return self.compute_device() if self._torch_gpu() else torch.device("cpu")
 
     @staticmethod
     def _sub_check(a: torch.dtype, b: torch.dtype) -> None:
@@ -393,7 +409,7 @@ class AWQQuantizer:
             x = x.expand(shape).contiguous()
             s64, z64 = s64.expand(shape).reshape(-1), z64.expand(shape).reshape(-1)
             rows, K, L = 1, x.numel(), 1
-        cpu_scalars = not self.device.startswith("cuda")
+        cpu_scalars = not self._torch_gpu()
         flags = ((_hip.APPLY_SCALE_ONE_ELEMENT if cpu_scalars and scale.numel() == 1 else 0) |
                  (0 if cpu_scalars else _hip.APPLY_IEEE_CLAMP) |
                  (_hip.APPLY_ZERO_ONE_ELEMENT if cpu_scalars and zero_point.numel() == 1 else 0) |
@@ -423,9 +439,19 @@ class AWQQuantizer:
         x = self._on_gpu(tensor)
         rows = 1 if x.dim() <= 1 else x.shape[0]
         K = x.numel() // rows
-        tq = torch.empty(rows * K, dtype=torch.int32, device=x.device)
-        _hip.quantize_groups(x, rows, K, self.group_size, self.bits, self.symmetric, tensor_q=tq)
-        s, z = _hip.group_params(x, rows, K, self.group_size, self.bits, self.symmetric)
+        L = self.group_size
+        gpu = self._torch_gpu()
+        s, z = _hip.group_params(x, rows, K, L, self.bits, self.symmetric, torch_gpu=gpu)
+        if not gpu:
+            tq = torch.empty(rows * K, dtype=torch.int32, device=x.device)
+            _hip.quantize_groups(x, rows, K, L, self.bits, self.symmetric, tensor_q=tq)
+        else:
+            # awq.py:356-367 as the GPU evaluates it: each group quantized with its own 0-d
+            # parameters (awq_apply_params_ex, GPU clamp), the float result stored into the
+            # int32 tensor_q by torch's own GPU conversion (NaN -> 0; the reference's setitem)
+            tqf = _hip.apply_params(x.reshape(-1), rows, K, L, s.reshape(-1).contiguous(), z.reshape(-1).contiguous(),
+                                    self.qmin, self.qmax, 0, x.dtype, x.dtype, _hip.APPLY_IEEE_CLAMP)
+            tq = tqf.to(torch.int32)
         return self._home(tq.reshape(tensor.shape)), self._home(s.float()), self._home(z.float())
 
     # ------------------------------------------------------------------ packed extension

@@ -237,14 +237,21 @@ int awq_quantize_search_ex(const void* w, int dtype, int64_t rows, int64_t K, in
 
 int awq_group_params(const void* w, int dtype, int64_t rows, int64_t K, int64_t group_size, int bits,
                      int symmetric, double* scales, double* zeros, void* stream) {
+    return awq_group_params_ex(w, dtype, rows, K, group_size, bits, symmetric, 0, scales, zeros, stream);
+}
+
+int awq_group_params_ex(const void* w, int dtype, int64_t rows, int64_t K, int64_t group_size, int bits,
+                        int symmetric, int flags, double* scales, double* zeros, void* stream) {
     g_err.clear();
+    if (flags & ~AWQ_GP_TORCH_GPU) return fail(AWQ_EINVAL, "unknown flags 0x%x", flags);
     if (int rc = check_common(rows, K, group_size, bits)) return rc;
     if (dtype < AWQ_DTYPE_BF16 || dtype > AWQ_DTYPE_F64) return fail(AWQ_EINVAL, "unknown dtype code %d", dtype);
     if (!scales && !zeros) return fail(AWQ_EINVAL, "no output requested");
     if (rows * K == 0) return AWQ_OK;
     if (!w) return fail(AWQ_EINVAL, "null input");
     return hip_status(awq::launch_generic(w, dtype, rows, K, group_size, bits, symmetric, nullptr, nullptr, nullptr,
-                                          nullptr, nullptr, (hipStream_t)stream, false, 1, 0, scales, zeros),
+                                          nullptr, nullptr, (hipStream_t)stream, false, 1, 0, scales, zeros,
+                                          (flags & AWQ_GP_TORCH_GPU) != 0),
                       "awq group params");
 }
 

@@ -137,12 +137,12 @@ __global__ __launch_bounds__(256) void awq_generic_kernel(const void* __restrict
                 mx = T::rn(mx * al);
             }
             C s, z;
-            group_params<DT>(mn, mx, nan, qmin, qmax, sym, s, z);
+            group_params<DT>(mn, mx, nan, qmin, qmax, sym, s, z, (small & 2) != 0);
             sa[j] = s;
             za[j] = z;
             zword |= (((uint32_t)to_i32(z) - (uint32_t)qmin) & mask) << (bits * j);
             if (lane == 0) {
-                if (scales) scales[gi] = gen_scale_bits<DT>(s, nan, L, sym, small, w, base + k0);
+                if (scales) scales[gi] = gen_scale_bits<DT>(s, nan, L, sym, small & 1, w, base + k0);
                 if (zeros) zeros[gi] = to_i32(z);
                 if (s_exact) s_exact[gi] = (double)s;                 // the input dtype's values, exact
                 if (z_exact) z_exact[gi] = (double)z;
@@ -955,7 +955,9 @@ inline unsigned grid_for(int64_t work, int64_t per_block, int64_t cap) {
 hipError_t launch_generic(const void* w, int dtype, int64_t rows, int64_t K, int64_t L, int bits,
                           int symmetric, int32_t* tensor_q, uint16_t* scales, int32_t* zeros,
                           int32_t* qweight, int32_t* qzeros, hipStream_t stream, bool small, int n_grid,
-                          int n_cand, double* s_exact, double* z_exact) {
+                          int n_cand, double* s_exact, double* z_exact, bool torch_gpu) {
+    if (torch_gpu && (n_cand > 0 || tensor_q || scales || zeros || qweight || qzeros))
+        return hipErrorInvalidValue;   // (torch's GPU semantics: the exact-parameter outputs only)
     const int qmin = symmetric ? -(1 << (bits - 1)) : 0;
     const int qmax = symmetric ? (1 << (bits - 1)) - 1 : (1 << bits) - 1;
     const int per = 32 / bits;
@@ -1002,15 +1004,16 @@ hipError_t launch_generic(const void* w, int dtype, int64_t rows, int64_t K, int
                                qweight, qzeros);
         return hipPeekAtLastError();
     }
+    const int smallf = (small ? 1 : 0) | (torch_gpu ? 2 : 0);   // kernel flags: bit 1 = torch's GPU semantics
 #define AWQ_GEN(D)                                                                                   \
     do {                                                                                             \
         if (search)                                                                                  \
             hipLaunchKernelGGL((awq_generic_kernel<D, true>), dim3(grid), dim3(256), 0, stream, w, rows, \
-                               K, L, bits, qmin, qmax, symmetric, small, n_grid, n_cand, tensor_q,    \
+                               K, L, bits, qmin, qmax, symmetric, smallf, n_grid, n_cand, tensor_q,   \
                                scales, zeros, qweight, qzeros, s_exact, z_exact);                      \
         else                                                                                         \
             hipLaunchKernelGGL((awq_generic_kernel<D, false>), dim3(grid), dim3(256), 0, stream, w,     \
-                               rows, K, L, bits, qmin, qmax, symmetric, small, 1, 0, tensor_q, scales, \
+                               rows, K, L, bits, qmin, qmax, symmetric, smallf, 1, 0, tensor_q, scales, \
                                zeros, qweight, qzeros, s_exact, z_exact);                              \
     } while (0)
     switch (dtype) {

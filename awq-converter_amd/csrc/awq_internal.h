@@ -194,7 +194,7 @@ hipError_t launch_generic(const void* w, int dtype, int64_t rows, int64_t K, int
                           int symmetric, int32_t* tensor_q, uint16_t* scales, int32_t* zeros,
                           int32_t* qweight, int32_t* qzeros, hipStream_t stream, bool small, int n_grid = 1,
                           int n_cand = 0, double* s_exact = nullptr,
-                          double* z_exact = nullptr);
+                          double* z_exact = nullptr, bool torch_gpu = false);
 // x of dtype xdt (AWQ_DTYPE_* incl. I32); first op in d1, second (= out) in d2; flags AWQ_APPLY_*
 hipError_t launch_apply(const void* x, int xdt, int64_t rows, int64_t K, int64_t L, const double* scales,
                         const double* zeros, int qmin, int qmax, int mode, int d1, int d2, int flags, void* out,

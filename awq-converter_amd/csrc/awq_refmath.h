@@ -121,10 +121,14 @@ template <typename C> __device__ __forceinline__ C wave_sum(C v) {
 }
 
 // awq.py:196-213: scale and zero point of one group from its (NaN-propagated) min/max.
+// torch_gpu: as torch's GPU kernels evaluate the same lines (a reference quantizer with
+// device="cuda"): the division by the Python int qmax - qmin is a product with the opmath
+// reciprocal RN(1 / (qmax - qmin)) (ATen's div_true_kernel_cuda for a CPU-scalar divisor), and
+// clamp(-0, 0, qmax) is +0 (the GPU clamp's IEEE maximum).
 template <int DT>
 __device__ __forceinline__ void group_params(typename Traits<DT>::C mn, typename Traits<DT>::C mx, int nan,
                                              int qmin, int qmax, int sym, typename Traits<DT>::C& s_out,
-                                             typename Traits<DT>::C& z_out) {
+                                             typename Traits<DT>::C& z_out, bool torch_gpu = false) {
     typedef Traits<DT> T;
     typedef typename T::C C;
     if (sym) {                                   // awq.py:196-199 (Python max)
@@ -134,13 +138,15 @@ __device__ __forceinline__ void group_params(typename Traits<DT>::C mn, typename
         mn = -a;
         mx = a;
     }
-    C s = T::rn(T::rn(mx - mn) / (C)(qmax - qmin));          // awq.py:202
+    C s = torch_gpu ? T::rn(T::rn(mx - mn) * ((C)1 / (C)(qmax - qmin)))   // awq.py:202
+                    : T::rn(T::rn(mx - mn) / (C)(qmax - qmin));
     if (!(s != s) && s < T::lo()) s = T::lo();                 // awq.py:205
     C z = (C)0;
     if (!sym) {                                                // awq.py:210-211
         C y = T::rn(mn / s);
         z = T::rn((C)qmin - y);
         z = clampq(T::rn(rnd(z)), (C)qmin, (C)qmax);
+        if (torch_gpu && z == (C)0) z = (C)0;                  // GPU clamp: max(-0, +0) = +0
     }
     s_out = s;
     z_out = z;

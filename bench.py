@@ -421,6 +421,35 @@ def valu_roofline(units, kern_s, per_unit, src, unit_name):
     return r
 
 
+def add_valu_floor(roof, kind, dtype_name, bits, symmetric):
+    """The algorithmic floor beside the issue-slot roofline (scripts/valu_floor.py ->
+    profiles/round6/valu_floor.json): the per-candidate-element instruction chain the
+    reference's per-op rounding forces, priced in issue slots.  floor_frac = achieved rate /
+    (614.4 G slots/s / floor slots per unit); slots_over_floor = the kernel's recorded slots
+    per unit / the floor's."""
+    key = f"{kind}.{dtype_name}.{'sym' if symmetric else 'asym'}"
+    path = os.path.join(ROOT, "profiles", "round6", "valu_floor.json")
+    try:
+        with open(path) as f:
+            rec = json.load(f).get(key) if bits == 4 else None
+    except (OSError, ValueError):
+        rec = None
+    if not rec:
+        roof["floor_slots_per_unit"] = None
+        roof["floor_note"] = f"no floor derived for {key} at {bits} bits (scripts/valu_floor.py)"
+        return
+    fl = rec["floor_slots_per_unit"]
+    floor_peak = VALU_SLOT_RATE / fl / 1e9
+    roof["floor_slots_per_unit"] = fl
+    roof["floor_peak"] = round(floor_peak, 2)
+    roof["floor_frac"] = round(roof["achieved"] / floor_peak, 4)
+    if roof.get("valu_slots_per_unit"):
+        roof["slots_over_floor"] = round(roof["valu_slots_per_unit"] / fl, 3)
+    roof["floor_source"] = {"file": os.path.relpath(path, ROOT), "key": key,
+                            "floor_slots_per_element": rec["floor_slots_per_element"],
+                            "excess_instructions_by_type": rec.get("excess_instructions_by_type")}
+
+
 def main():
     args = parse()
     if args.mode == "act":
@@ -575,6 +604,7 @@ def main():
         line["roofline"]["timing"] = hbm["timing"]
         line["roofline"]["hbm_view"] = {k: hbm[k] for k in ("achieved", "peak", "unit", "frac", "traffic",
                                                             "algorithmic_bytes_per_launch") if k in hbm}
+        add_valu_floor(line["roofline"], "search", args.dtype, args.bits, args.symmetric)
         line["config"]["search"] = {"grid": args.search_grid, "candidates": args.search_candidates,
                                     "alpha": f"1 - i/{args.search_grid}, i < {args.search_candidates}"}
     if world > 1:       # the LPT shard's balance: per-rank kernel time and elements
@@ -713,6 +743,7 @@ def main_act(args):
     key = f"act.llama3-8b-block.t{args.act_tokens}.g{n_grid}.{args.dtype}.b{args.bits}.{'sym' if args.symmetric else 'asym'}"
     per_unit, vsrc = recorded_valu(args.valu_json, key, ACT_SOURCES)
     roof = valu_roofline(cand, loss_s, per_unit, vsrc, "candidate-elements")
+    add_valu_floor(roof, "act", args.dtype, args.bits, args.symmetric)
     roof.update({"kernel": "act_loss_kernel (7 launches per step: one per linear)",
                  "kernel_avg_us": round(loss_s / len([w for ws, _ in groups for w in ws]) * 1e6, 2),
                  "loss_kernels_us_per_step": round(loss_s * 1e6, 2),

@@ -139,6 +139,15 @@ int awq_quantize_search_ex(const void* w, int dtype, int64_t rows, int64_t K, in
 int awq_group_params(const void* w, int dtype, int64_t rows, int64_t K, int64_t group_size, int bits,
                      int symmetric, double* scales, double* zeros, void* stream);
 
+/* (ABI 17) awq_group_params with flags.  AWQ_GP_TORCH_GPU: the same lines as torch's GPU kernels
+ * evaluate them (the reference quantizer with device="cuda"): the scale's division by the Python
+ * int qmax - qmin is a product with the reciprocal RN(1 / (qmax - qmin)) in the op's compute
+ * type (ATen's GPU division by a CPU scalar), and a zero point clamped from -0 is +0 (the GPU
+ * clamp's IEEE maximum).  flags = 0: awq_group_params (torch's CPU semantics). */
+#define AWQ_GP_TORCH_GPU 1
+int awq_group_params_ex(const void* w, int dtype, int64_t rows, int64_t K, int64_t group_size, int bits,
+                        int symmetric, int flags, double* scales, double* zeros, void* stream);
+
 /* Elementwise with caller-given parameters per group (scales / zeros double [rows, G], used
  * in the op's compute type — fp32, fp64 for fp64 inputs — unrounded to the input dtype, as
  * torch's CPU kernels use a 0-d operand; group_size 1 = one parameter per element), result

@@ -202,16 +202,28 @@ static uint16_t scale_f16(double s, const void* x, int dtype, int64_t base, int6
     return oracle_nan_scale_f16(dtype, sym, small, L, has_nan, e);
 }
 
-/* awq.py:173-213 — scale and zero point of one group (values already in compute type). */
+/* awq.py:173-213 — scale and zero point of one group (values already in compute type).
+ * gpu = 1: as torch's GPU kernels evaluate these lines (device="cuda"): the division by the
+ * Python int qmax - qmin is a product with the compute type's RN(1 / (qmax - qmin)) (ATen's
+ * GPU division by a CPU scalar), and clamp(-0, 0, qmax) = +0 (IEEE maximum). */
+static void group_scale_zp_dev(double mn, double mx, int dtype, int qmin, int qmax, int sym, int gpu,
+                               double* s_out, double* z_out);
 static void group_scale_zp(double mn, double mx, int dtype, int qmin, int qmax, int sym,
                            double* s_out, double* z_out) {
+    group_scale_zp_dev(mn, mx, dtype, qmin, qmax, sym, 0, s_out, z_out);
+}
+static void group_scale_zp_dev(double mn, double mx, int dtype, int qmin, int qmax, int sym, int gpu,
+                               double* s_out, double* z_out) {
     if (sym) {                                   /* awq.py:196-199, Python builtin max() */
         double amn = fabs(mn), amx = fabs(mx);
         double a = (amx > amn) ? amx : amn;
         mn = -a;
         mx = a;
     }
-    double s = op_div(op_sub(mx, mn, dtype), (double)(qmax - qmin), dtype);   /* awq.py:202 */
+    double s;                                                                 /* awq.py:202 */
+    if (!gpu) s = op_div(op_sub(mx, mn, dtype), (double)(qmax - qmin), dtype);
+    else if (dtype == AWQ_ORACLE_F64) s = op_sub(mx, mn, dtype) * (1.0 / (double)(qmax - qmin));
+    else s = rn((double)((float)op_sub(mx, mn, dtype) * (1.0f / (float)(qmax - qmin))), dtype);
     double lo = rn(1e-10, dtype);                                             /* awq.py:205 */
     if (!isnan(s) && s < lo) s = lo;
     double z;
@@ -220,6 +232,7 @@ static void group_scale_zp(double mn, double mx, int dtype, int qmin, int qmax, 
     } else {
         z = op_sub((double)qmin, op_div(mn, s, dtype), dtype);                /* awq.py:210 */
         z = op_clamp(op_round(z, dtype), qmin, qmax);                         /* awq.py:211 */
+        if (gpu && z == 0.0) z = 0.0;                                         /* GPU clamp: +0 */
     }
     *s_out = s;
     *z_out = z;
@@ -273,8 +286,8 @@ int oracle_quantize_ex(const void* x, int dtype, int64_t rows, int64_t K, int64_
 /* awq.py:173-213 per group, the scale / zero point themselves (exact doubles of the dtype's
  * values): what _compute_scale_zp_for_group returns (0-d, dtype D) and, rounded to fp32,
  * what _quantize_per_group stores (awq.py:327-328, 352-353). */
-int oracle_group_params(const void* x, int dtype, int64_t rows, int64_t K, int64_t L, int bits, int sym,
-                        double* scales, double* zeros) {
+int oracle_group_params_ex(const void* x, int dtype, int64_t rows, int64_t K, int64_t L, int bits, int sym, int gpu,
+                           double* scales, double* zeros) {
     if (!x || rows < 0 || K < 0 || L <= 0 || (bits != 4 && bits != 8)) return -1;
     int qmin = sym ? -(1 << (bits - 1)) : 0;
     int qmax = sym ? (1 << (bits - 1)) - 1 : (1 << bits) - 1;
@@ -294,13 +307,19 @@ int oracle_group_params(const void* x, int dtype, int64_t rows, int64_t K, int64
             }
             if (nan) { mn = NAN; mx = NAN; }
             double s, z;
-            group_scale_zp(mn, mx, dtype, qmin, qmax, sym, &s, &z);
+            group_scale_zp_dev(mn, mx, dtype, qmin, qmax, sym, gpu, &s, &z);
             if (scales) scales[r * G + g] = s;
             if (zeros) zeros[r * G + g] = z;
         }
     }
     return 0;
 }
+
+int oracle_group_params(const void* x, int dtype, int64_t rows, int64_t K, int64_t L, int bits, int sym,
+                        double* scales, double* zeros) {
+    return oracle_group_params_ex(x, dtype, rows, K, L, bits, sym, 0, scales, zeros);
+}
+
 
 /* awq.py:215-250 (_quantize_tensor, mode 0) and awq.py:252-284 (_dequantize_tensor, mode 1)
  * with given per-group parameters (double), which enter each op in its compute type (fp32;

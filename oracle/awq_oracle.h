@@ -25,6 +25,9 @@ int oracle_quantize_search(const void* x, int dtype, int64_t rows, int64_t K, in
 /* awq.py:173-213 per group: scale / zero point as exact doubles [rows, G] */
 int oracle_group_params(const void* x, int dtype, int64_t rows, int64_t K, int64_t L, int bits, int sym,
                         double* scales, double* zeros);
+/* gpu = 1: as torch's GPU kernels evaluate awq.py:202-211 (reciprocal scale, +0 zero point) */
+int oracle_group_params_ex(const void* x, int dtype, int64_t rows, int64_t K, int64_t L, int bits, int sym, int gpu,
+                           double* scales, double* zeros);
 /* awq.py:215-250 (mode 0) / 252-284 (mode 1) with given per-group parameters; out in dtype */
 int oracle_apply_params(const void* x, int dtype, int64_t rows, int64_t K, int64_t L, const double* scales,
                         const double* zeros, int qmin, int qmax, int mode, void* out);

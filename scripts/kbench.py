@@ -25,6 +25,8 @@ SETS["k768"] = [((50272, 768), 4)]
 SETS["falcon7b-mlp"] = [((18176, 4544), 8), ((4544, 18176), 4)]   # K = 4544: padded rows at gs 128
 SETS["qwen05-odd"] = [((4864, 896), 8), ((151936, 896), 1)]   # K = 896: 7 groups (odd) at gs 128 -> word tiles (2 rows per tile)
 SETS.setdefault("c1", [((1024, 4096), 1)])
+SETS["lm-head-8b"] = [((128256, 4096), 1)]          # one large tensor per launch (quantize_packed per tensor)
+SETS["down-8b"] = [((4096, 14336), 1)]
 
 
 def shapes_of(name):

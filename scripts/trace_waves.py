@@ -73,7 +73,21 @@ def main():
             "load_wait_us_p50_p90": [q(landed - issued, .5), q(landed - issued, .9)],
             "compute_us_p50_p90": [q(end - landed, .5), q(end - landed, .9)],
             "mean_live_waves": round(float(life.sum()) / span, 1),
-            "first_wave_end_us": q(end, 0.0), "start_of_last_wave_us": round(float(start.max()), 2)}))
+            "first_wave_end_us": q(end, 0.0), "start_of_last_wave_us": round(float(start.max()), 2),
+            # live waves at 20 instants across the span (ramp at the start, tail at the end)
+            "live_waves_timeline": [int(((start <= t) & (end > t)).sum()) for t in
+                                    [span * (k + 0.5) / 20 for k in range(20)]],
+            "ramp_us_to_90pct_of_peak_live": ramp_time(start, end, span),
+            "tail_us_from_90pct_done": round(span - float(torch.quantile(end, 0.9)), 2)}))
+
+
+def ramp_time(start, end, span):
+    """First instant (0.25 us steps) at which the live-wave count reaches 90 % of its peak."""
+    ts = torch.arange(0, span, 0.25, dtype=torch.float64)
+    live = torch.tensor([int(((start <= t) & (end > t)).sum()) for t in ts.tolist()[:400]])
+    peak = int(live.max()) if live.numel() else 0
+    idx = (live >= 0.9 * peak).nonzero()
+    return round(float(ts[int(idx[0])]), 2) if idx.numel() else None
 
 
 if __name__ == "__main__":

@@ -181,6 +181,13 @@ __device__ __forceinline__ float grp_sum(float v) {
     return v;
 }
 
+// AWQ_SEARCH_FMA_MIX = 0: the round-5 error chain (A/B builds, scripts/build_variant.sh)
+#ifndef AWQ_SEARCH_FMA_MIX
+#define AWQ_SEARCH_FMA_MIX 1
+#endif
+#ifndef AWQ_SEARCH_S_LATE
+#define AWQ_SEARCH_S_LATE 1
+#endif
 // Squared error of this lane's 8-element chunk of a group for one candidate (r, z, s) —
 // quantize (awq.py:245-248), dequantize the reference's way (fp16(fp16(q - z) * fp16(s)),
 // awq.py:459-539), (x - dq)^2 summed in element order.  `special`: the candidate's scale
@@ -191,6 +198,37 @@ __device__ __forceinline__ float chunk_err(const Chunk<F::NW>& v, float r, float
     constexpr float QMAX = SYM ? (float)((1 << (BITS - 1)) - 1) : (float)((1 << BITS) - 1);
     const float zf = F::as_fmt(z);
     float acc = 0.0f;
+#if AWQ_SEARCH_FMA_MIX
+    // element pairs: the two fp16 products packed by one v_cvt_pk_f16_f32 (RNE), then x - dq as
+    // v_fma_mix_f32(dq_f16, -1, x) on each half — an exact product and one rounding, i.e. the
+    // subtraction's bits, with no fp16 -> f32 widening instruction
+    typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+#pragma unroll
+    for (int i = 0; i < 8; i += 2) {
+        float xq[2], qq[2];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const float x = F::elem(v, i + u);
+            float q;
+            if (__builtin_expect(special, 0)) {
+                const float t = F::rn(opaque(x) / s);
+                const float rr = __builtin_rintf(SYM ? t : F::rn(t + zf));
+                q = __builtin_isnan(rr) ? rr : __builtin_fminf(__builtin_fmaxf(rr, QMIN), QMAX);
+            } else {
+                const float t = F::quot(x, s, r);
+                q = __builtin_fminf(__builtin_fmaxf(__builtin_rintf(SYM ? t : F::rn(t + zf)), QMIN), QMAX);
+            }
+            xq[u] = x;
+            qq[u] = q;
+        }
+        const h2 dq = {(_Float16)((qq[0] - zf) * sh), (_Float16)((qq[1] - zf) * sh)};
+        float d0, d1;
+        asm("v_fma_mix_f32 %0, %1, -1.0, %2 op_sel_hi:[1,0,0]" : "=v"(d0) : "v"(dq), "v"(xq[0]));
+        asm("v_fma_mix_f32 %0, %1, -1.0, %2 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "=v"(d1) : "v"(dq), "v"(xq[1]));
+        acc = acc + d0 * d0;
+        acc = acc + d1 * d1;
+    }
+#else
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
         const float x = F::elem(v, i);
@@ -207,6 +245,7 @@ __device__ __forceinline__ float chunk_err(const Chunk<F::NW>& v, float r, float
         const float d = x - dq;
         acc = acc + d * d;
     }
+#endif
     return acc;
 }
 
@@ -226,6 +265,7 @@ template <typename F, int BITS, bool SYM, int GS>
 __device__ __forceinline__ void search_range(const Chunk<F::NW> (&v)[4], float& gmn, float& gmx, bool gnan, int n_grid,
                                           int n_cand) {
     const int jj = threadIdx.x & 3;
+    constexpr bool kLateS = AWQ_SEARCH_S_LATE && std::is_same<F, FmtBF16>::value;
     float best = __builtin_inff();
     int bi = 0;
     for (int i = 0; i < n_cand; ++i) {
@@ -236,12 +276,23 @@ __device__ __forceinline__ void search_range(const Chunk<F::NW> (&v)[4], float& 
         for (int j = 0; j < 4; ++j) {
             const float rj = bcast_j(j, cp.r);
             const float zj = SYM ? 0.0f : bcast_j(j, cp.z);
-            const float sj = bcast_j(j, cp.s);
             const float hj = bcast_j(j, csh);
             const bool special = !F::fast(rj);
             float e;
-            if (__builtin_expect(__ballot(special) != 0, 0)) e = chunk_err<F, BITS, SYM>(v[j], rj, zj, sj, hj, special);
-            else e = chunk_err<F, BITS, SYM>(v[j], rj, zj, sj, hj, false);
+            // (the scale itself only feeds the exact division of a 0 / inf / NaN scale: broadcast
+            //  in that rare wave only)
+            if constexpr (kLateS) {
+                // bf16: the common path's quotient is x * RN(1/s) (r alone); the scale itself only
+                // feeds the exact division of a 0 / inf / NaN scale — broadcast in that rare wave
+                if (__builtin_expect(__ballot(special) != 0, 0))
+                    e = chunk_err<F, BITS, SYM>(v[j], rj, zj, bcast_j(j, cp.s), hj, special);
+                else e = chunk_err<F, BITS, SYM>(v[j], rj, zj, 0.0f, hj, false);
+            } else {   // fp16 (Markstein correction) and fp32 (IEEE division) read s on every path
+                const float sj = bcast_j(j, cp.s);
+                if (__builtin_expect(__ballot(special) != 0, 0))
+                    e = chunk_err<F, BITS, SYM>(v[j], rj, zj, sj, hj, special);
+                else e = chunk_err<F, BITS, SYM>(v[j], rj, zj, sj, hj, false);
+            }
             e = grp_sum<GS / 8>(e);
             if (j == jj && e < best) {
                 best = e;

@@ -48,6 +48,8 @@ def main():
     ap.add_argument("--parity", action="store_true")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "f16", "f32"])
     ap.add_argument("--group-size", type=int, default=128)
+    ap.add_argument("--search", type=int, default=0, help="clip-search candidates of 20 (0 = RTN): "
+                    "awq_quantize_ragged_search")
     ap.add_argument("--arena", action="store_true",
                     help="inputs as views of ONE device buffer per replica instead of one allocation per tensor")
     args = ap.parse_args()
@@ -150,10 +152,16 @@ def main():
                         table = None if blk == "nt" else block_table(lp, lib, bt).data_ptr()
                         abi = lib.awq_abi_version()
                         gsa = ((bt.group_size,) if abi >= 5 else ()) + ((bt.flags,) if abi >= 7 else ())
-                        rc = lib.awq_quantize_ragged(ctypes.c_void_p(bt.descs_dev.data_ptr()), len(bt.descs),
-                                                     bt.total_tiles, ctypes.c_void_p(table),
-                                                     _hip.AWQ_DTYPE[bt.dtype], bt.bits, int(bt.symmetric),
-                                                     *gsa, ctypes.c_void_p(stream.cuda_stream))
+                        if args.search > 1:
+                            rc = lib.awq_quantize_ragged_search(
+                                ctypes.c_void_p(bt.descs_dev.data_ptr()), len(bt.descs), bt.total_tiles,
+                                ctypes.c_void_p(table), _hip.AWQ_DTYPE[bt.dtype], bt.bits, int(bt.symmetric), *gsa,
+                                20, args.search, ctypes.c_void_p(stream.cuda_stream))
+                        else:
+                            rc = lib.awq_quantize_ragged(ctypes.c_void_p(bt.descs_dev.data_ptr()), len(bt.descs),
+                                                         bt.total_tiles, ctypes.c_void_p(table),
+                                                         _hip.AWQ_DTYPE[bt.dtype], bt.bits, int(bt.symmetric),
+                                                         *gsa, ctypes.c_void_p(stream.cuda_stream))
                         s1.record(stream)
                         assert rc == 0, lib.awq_last_error()
                         if it >= 3:
@@ -172,8 +180,12 @@ def main():
         algo = bt.algorithmic_bytes() / (us / 1e6) / 1e9
         inp = bt.elements * bt.inputs[bt.names[0]].element_size() / (us / 1e6) / 1e9
         print(f"{sname:16s} {lname:28s} {blk:>6s} {us:9.1f} {algo:9.1f} {inp:8.1f} {algo / 8000:6.3f}")
-        print(json.dumps({"set": sname, "lib": lname, "blocks": blk, "us": round(us, 2), "algo_GBs": round(algo, 1),
-                          "in_GBs": round(inp, 1), "rounds_us": [round(x, 1) for x in v]}))
+        rec = {"set": sname, "lib": lname, "blocks": blk, "us": round(us, 2), "algo_GBs": round(algo, 1),
+               "in_GBs": round(inp, 1), "rounds_us": [round(x, 1) for x in v]}
+        if args.search > 1:
+            rec["search_candidates"] = args.search
+            rec["T_candidate_elements_per_s"] = round(bt.elements * args.search / (us / 1e6) / 1e12, 4)
+        print(json.dumps(rec))
 
 
 if __name__ == "__main__":

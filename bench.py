@@ -102,7 +102,7 @@ def parse(argv=None):
                     help="after the timed region: every rank copies its packed shard to the host and writes it as "
                          "chunk files into this directory (the CLI's per-rank output, main.ChunkWriter), reported as "
                          "\"write\" (max over ranks); the files are removed afterwards")
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "round5", "pmc_traffic.json"))
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "round6", "pmc_traffic.json"))
     ap.add_argument("--mode", default="rtn", choices=["rtn", "search", "act"],
                     help="rtn = the BASELINE metric (round-to-nearest, the reference's arithmetic); search = the "
                          "opt-in per-group clip search (scale_method='search') in the same ragged launch; act = the "
@@ -112,7 +112,7 @@ def parse(argv=None):
     ap.add_argument("--search-candidates", type=int, default=10,
                     help="--mode search: candidates of the grid (AWQQuantizer default: 20 x 0.5 = 10)")
     ap.add_argument("--act-tokens", type=int, default=512, help="--mode act: calibration tokens per layer group")
-    ap.add_argument("--valu-json", default=os.path.join(ROOT, "profiles", "round5", "pmc_valu.json"))
+    ap.add_argument("--valu-json", default=os.path.join(ROOT, "profiles", "round6", "pmc_valu.json"))
     a = ap.parse_args(argv)
     if a.mode == "search" and not 1 < a.search_candidates <= a.search_grid:
         ap.error("--search-candidates must be in (1, --search-grid]")

@@ -14,7 +14,8 @@ the floor: it is amortised over the group (128 elements) and is what the gap nam
 
 GAP: the kernel's hot loop in the ISA (`make -C awq-converter_amd/csrc isa ISA_SRC=awq_fast` /
 `ISA_SRC=awq_actsearch`), its VALU instructions per element priced the same way and grouped by
-what they do, beside the measured slots per unit (profiles/round5/pmc_valu.json).
+what they do, beside the measured slots per unit (profiles/round6/pmc_valu.json) and the
+per-type VALU counters of the same commands (profiles/round6/r6x/{search,act}_{a,b}).
 
   python scripts/valu_floor.py [--write profiles/round6/valu_floor.json]
 """
@@ -72,8 +73,8 @@ FLOOR = {
     ],
 }
 
-# the round-5 per-type counter passes of the same bench commands (profiles/round5/r5k/, scripts/
-# valu_classes.py's A / B counter sets): dynamic instructions per type for the kernel's launches
+# the per-type counter passes of the same bench commands (scripts/cmd/r6x.sh; the A / B counter sets
+# of scripts/valu_classes.py): dynamic instructions per type for the kernel's launches
 TYPE_PASSES = {"search.bf16.asym": ("search_a", "search_b", "awq_fast_kernel"),
                "act.bf16.asym": ("act_a", "act_b", "act_loss_kernel")}
 
@@ -178,7 +179,9 @@ KERNELS = {
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "round5", "pmc_valu.json"))
+    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "round6", "pmc_valu.json"))
+    ap.add_argument("--types-dir", default=os.path.join(ROOT, "profiles", "round6", "r6x"),
+                    help="the per-type counter passes (search_a/b, act_a/b: scripts/cmd/r6x.sh)")
     ap.add_argument("--write", default="")
     ap.add_argument("--no-isa", action="store_true", help="floors only (no hipcc)")
     a = ap.parse_args()
@@ -203,7 +206,8 @@ def main():
             r["measured_slots_per_element"] = round(meas * 64, 3)
         lane = rec.get("valu_lane_instr_per_unit")
         if lane:
-            dyn = dynamic_types(os.path.join(ROOT, "profiles", "round5", "r5k"), key, lane)
+            dyn = dynamic_types(a.types_dir, key, lane)
+            r["types_source"] = os.path.relpath(a.types_dir, ROOT)
             if dyn:
                 r["measured_instructions_by_type"] = dyn
                 r["excess_instructions_by_type"] = {t: round(v - floor_types.get(t, 0.0), 3) for t, v in dyn.items()}

@@ -34,6 +34,10 @@ def main():
     ap.add_argument("--tunings", default="", help="'/'-separated awq_tuning settings to time the quantize under, "
                     "each 'default' or k=v[,k=v] (csrc/awq_diag.h, diagnostics build), e.g. default/rg_p1=1")
     ap.add_argument("--dequant", action="store_true", help="also time dequantize_packed of the packed result")
+    ap.add_argument("--settle-ms", type=float, default=0.0,
+                    help="stream this long (awq_stream_ceiling) before every timed loop: the clocks of a busy "
+                         "chip (bench.py's ceiling probe does the same; an idle GPU's first ~5 ms run slower, "
+                         "profiles/round6/r6h)")
     ap.add_argument("--dq-variants", default="1,3,6,7,8,9", help="--dq-ab: tuning dq_words_v1 values to time")
     ap.add_argument("--lib", default="", help="load this in-tree build instead of _lib/libawq_hip.so (A/B of builds)")
     ap.add_argument("--dq-ab", action="store_true", help="--dequant: also the round-2 word kernel (tuning dq_words_v1), "
@@ -51,6 +55,25 @@ def main():
                     for tun in (args.tunings.split("/") if args.tunings else ["default"]):
                         kw = {} if tun == "default" else {k: int(v) for k, v in (t.split("=") for t in tun.split(","))}
                         one(args, _hip, dev, shape, name, gs, generic, kw)
+
+
+_settle_buf = {}
+
+
+def settle(args, _hip, dev):
+    """~args.settle_ms of streaming (1 GiB reads) so the timed loop starts at settled clocks."""
+    if args.settle_ms <= 0:
+        return
+    import time
+    if not _settle_buf:
+        _settle_buf["src"] = torch.empty(1 << 30, dtype=torch.uint8, device=dev)
+        _settle_buf["dst"] = torch.empty(1 << 28, dtype=torch.uint8, device=dev)
+    st = torch.cuda.current_stream(dev).cuda_stream
+    t0 = time.time()
+    while (time.time() - t0) * 1e3 < args.settle_ms:
+        for _ in range(8):
+            _hip.stream_ceiling(_settle_buf["src"], _settle_buf["dst"], st)
+        torch.cuda.synchronize()
 
 
 def one(args, _hip, dev, shape, name, gs, generic, tun=None):
@@ -79,6 +102,7 @@ def one(args, _hip, dev, shape, name, gs, generic, tun=None):
             _hip.quantize_groups(x, R, K, gs, args.bits, False, qweight=qw, qzeros=qz, scales=sc, **stage)
     for _ in range(3):
         run()
+    settle(args, _hip, dev)
     a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     a.record()
     for _ in range(args.iters):
@@ -100,7 +124,7 @@ def one(args, _hip, dev, shape, name, gs, generic, tun=None):
                       "lib": os.path.basename(args.lib) if args.lib else "libawq_hip.so",
                       "search": args.search, "us": round(us, 1), "input_GBs": round(nbytes / us / 1e3, 1),
                       "algorithmic_GBs": round(algo / us / 1e3, 1), "frac_8TBs": round(algo / us / 1e3 / 8000, 3),
-                      "out_sha": h.hexdigest()[:16]}),
+                      "out_sha": h.hexdigest()[:16], "settle_ms": args.settle_ms}),
           flush=True)
     if args.dequant:
         out = torch.empty(R, K, dtype=torch.float32, device=dev)
@@ -114,6 +138,7 @@ def one(args, _hip, dev, shape, name, gs, generic, tun=None):
                 with (_hip.tuning(dq_words_v1=v) if v else contextlib.nullcontext()):
                     for _ in range(3):
                         dq()
+                    settle(args, _hip, dev)
                     a.record()
                     for _ in range(args.iters):
                         dq()

@@ -186,6 +186,32 @@ __device__ __forceinline__ void grp_minmax(float& mn, float& mx, int& nan, int l
     if (lpg >= 64) minmax_cross<true>(mn, mx, nan);
 }
 
+// the group min / max alone (the weights' NaN flag is reduced once per item: grp_or)
+__device__ __forceinline__ void grp_minmax_nn(float& mn, float& mx, int lpg) {
+    if (lpg >= 2) { mn = min2(mn, dppf<0xB1>(mn)); mx = max2(mx, dppf<0xB1>(mx)); }
+    if (lpg >= 4) { mn = min2(mn, dppf<0x4E>(mn)); mx = max2(mx, dppf<0x4E>(mx)); }
+    if (lpg >= 8) { mn = min2(mn, dppf<0x141>(mn)); mx = max2(mx, dppf<0x141>(mx)); }
+    if (lpg >= 16) { mn = min2(mn, dppf<0x140>(mn)); mx = max2(mx, dppf<0x140>(mx)); }
+    if (lpg >= 32) {
+        int dummy = 0;
+        minmax_cross<false>(mn, mx, dummy);
+    }
+    if (lpg >= 64) {
+        int dummy = 0;
+        minmax_cross<true>(mn, mx, dummy);
+    }
+}
+__device__ __forceinline__ int grp_or(int v, int lpg) {
+    if (lpg >= 2) v |= dppi<0xB1>(v);
+    if (lpg >= 4) v |= dppi<0x4E>(v);
+    if (lpg >= 8) v |= dppi<0x141>(v);
+    if (lpg >= 16) v |= dppi<0x140>(v);
+    unsigned a, b;
+    if (lpg >= 32) { swap16((unsigned)v, a, b); v = (int)(a | b); }
+    if (lpg >= 64) { swap32((unsigned)v, a, b); v = (int)(a | b); }
+    return v;
+}
+
 __device__ __forceinline__ float grp_sum(float v, int lpg) {
     if (lpg >= 2) v = v + dppf<0xB1>(v);
     if (lpg >= 4) v = v + dppf<0x4E>(v);
@@ -719,6 +745,23 @@ __device__ __forceinline__ float mquot(float a, float s, float rs) {
     const float r = __builtin_fmaf(-s, q0, a);
     return __builtin_fmaf(r, rs, q0);
 }
+// the same with a = the low (HI = false) or high half of a packed fp16 pair: the two products
+// with a read the fp16 value directly (v_fma_mix_f32; q0 = a * rs + (-0): the product's bits,
+// signed zeros included), the bits of mquot((float)a, s, rs)
+typedef _Float16 h2v __attribute__((ext_vector_type(2)));
+template <bool HI>
+__device__ __forceinline__ float mquot_h(h2v a, float s, float rs) {
+    float q0, r;
+    const float nz = -0.0f;
+    if (HI) {
+        asm("v_fma_mix_f32 %0, %1, %2, %3 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "=v"(q0) : "v"(a), "v"(rs), "v"(nz));
+        asm("v_fma_mix_f32 %0, -%1, %2, %3 op_sel:[0,0,1] op_sel_hi:[0,0,1]" : "=v"(r) : "v"(s), "v"(q0), "v"(a));
+    } else {
+        asm("v_fma_mix_f32 %0, %1, %2, %3 op_sel_hi:[1,0,0]" : "=v"(q0) : "v"(a), "v"(rs), "v"(nz));
+        asm("v_fma_mix_f32 %0, -%1, %2, %3 op_sel_hi:[0,0,1]" : "=v"(r) : "v"(s), "v"(q0), "v"(a));
+    }
+    return __builtin_fmaf(r, rs, q0);
+}
 
 // LPG: lanes per group as a constant (0 = the run-time lpg argument); SYM: symmetric;
 // EPL: elements per lane — 16 (two consecutive 8-element chunks, LPG = gs / 16 lanes per
@@ -728,6 +771,23 @@ __device__ __forceinline__ float mquot(float a, float s, float rs) {
 // (A/B builds: -DAWQ_ACT_LDS=0 restores round 4's per-candidate register loads of the tables)
 #ifndef AWQ_ACT_LDS
 #define AWQ_ACT_LDS 1
+#endif
+// Round-6 trims of the loss kernel's per-element work (A/B builds: = 0 restores round 5's):
+//   AWQ_ACT_NAN_HOIST   the weights' NaN flag once per item, not per candidate and element
+//                       (RN(w * s) is NaN exactly when w is: s is a positive finite table entry)
+//   AWQ_ACT_NAN_RTABLE  out-of-range reciprocals as NaN: the Markstein path runs unchecked and a
+//                       wave whose loss came out NaN redoes the candidate with IEEE divisions
+//                       (no per-candidate min over the lane's reciprocals)
+//   AWQ_ACT_MIX_DQ      dq kept as packed fp16 pairs, fed to v_fma_mix_f32 in the Markstein
+//                       quotient (no fp16 -> f32 widening per element)
+#ifndef AWQ_ACT_NAN_HOIST
+#define AWQ_ACT_NAN_HOIST 1
+#endif
+#ifndef AWQ_ACT_NAN_RTABLE
+#define AWQ_ACT_NAN_RTABLE 1
+#endif
+#ifndef AWQ_ACT_MIX_DQ
+#define AWQ_ACT_MIX_DQ 1
 #endif
 // The table ring's waits are explicit: the compiler's own wait before an LDS read that may
 // alias an LDS-DMA covers every DMA in flight (vmcnt(0)), which would serialise the prefetch,
@@ -848,6 +908,12 @@ __global__ __launch_bounds__(256) void act_loss_kernel(const void* __restrict__ 
         }
         if constexpr (kLds) dma(gl.g, 0, 0);
         const float* const cw = wr + (lane % lpg) * EPL;   // this lane's elements in a ring slot
+#if AWQ_ACT_NAN_HOIST
+        int nan_w = 0;                                      // the group's weights hold a NaN
+#pragma unroll
+        for (int j = 0; j < EPL; ++j) nan_w |= v[j] != v[j];
+        nan_w = grp_or(nan_w, lpg);
+#endif
         for (int i = 0; i < n_grid; ++i) {
             float s[EPL], ws[EPL];
             float rs[EPL];
@@ -867,6 +933,16 @@ __global__ __launch_bounds__(256) void act_loss_kernel(const void* __restrict__ 
             // scale or zero point) with NaN tracked on the side: torch's NaN-propagating
             // min / max once combined
             float mn = __builtin_inff(), mx = -__builtin_inff();
+#if AWQ_ACT_NAN_HOIST
+            const int nan = nan_w;
+#pragma unroll
+            for (int j = 0; j < EPL; ++j) {
+                ws[j] = H::rn(v[j] * s[j]);
+                mn = __builtin_fminf(mn, ws[j]);
+                mx = __builtin_fmaxf(mx, ws[j]);
+            }
+            grp_minmax_nn(mn, mx, lpg);
+#else
             int nan = 0;
 #pragma unroll
             for (int j = 0; j < EPL; ++j) {
@@ -876,6 +952,7 @@ __global__ __launch_bounds__(256) void act_loss_kernel(const void* __restrict__ 
                 mx = __builtin_fmaxf(mx, ws[j]);
             }
             grp_minmax(mn, mx, nan, lpg);
+#endif
             if (nan) { mn = __builtin_nanf(""); mx = __builtin_nanf(""); }
             float cs, cz, r;
             hw_group_params<DT>(mn, mx, nan, qmin, qmax, sym, rq, cs, cz, r);
@@ -893,16 +970,35 @@ __global__ __launch_bounds__(256) void act_loss_kernel(const void* __restrict__ 
                     for (int c = 0; c < EPL; c += 8)
                         load8<AWQ_DTYPE_F32>(rtable, (int64_t)i * K + gl.k0 + c, *(float(*)[8]) & rs[c]);
                 }
+#if AWQ_ACT_NAN_RTABLE
+                mq = true;            // out-of-range entries are NaN: checked on the losses below
+#else
                 float m = rs[0];
 #pragma unroll
                 for (int j = 1; j < EPL; ++j) m = __builtin_fminf(m, rs[j]);
                 mq = __builtin_amdgcn_ballot_w64(!(m > 0.0f)) == 0;   // wave-uniform
+#endif
             }
             if (cs > 0.0f && cs < __builtin_inff()) {
                 // finite positive scale (every group but constant fp16 / inf / NaN ones):
                 // RN(w'/s) from the group's reciprocal, hardware RNE conversions; q - z is an
                 // integer |.| <= 510, exact in fp16, so only the product is rounded
                 const float sh = (float)(_Float16)cs;
+#if AWQ_ACT_MIX_DQ
+                h2v dqp[EPL / 2];     // (q - z) * sh rounded to fp16, two per register (v_cvt_pk_f16_f32)
+#pragma unroll
+                for (int j = 0; j < EPL; j += 2) {
+                    float qq[2];
+#pragma unroll
+                    for (int u2 = 0; u2 < 2; ++u2) {
+                        const float t = H::quot(ws[j + u2], cs, r);
+                        const float u = sym ? t : H::rn(t + cz);
+                        qq[u2] = __builtin_amdgcn_fmed3f(__builtin_rintf(u), (float)qmin, (float)qmax);
+                    }
+                    dqp[j / 2] = (h2v){(_Float16)opq((qq[0] - cz) * sh), (_Float16)opq((qq[1] - cz) * sh)};
+                }
+                auto dqf = [&](int j) { return (float)dqp[j / 2][j & 1]; };
+#else
                 float dq[EPL];
 #pragma unroll
                 for (int j = 0; j < EPL; ++j) {
@@ -911,18 +1007,39 @@ __global__ __launch_bounds__(256) void act_loss_kernel(const void* __restrict__ 
                     const float q = __builtin_amdgcn_fmed3f(__builtin_rintf(u), (float)qmin, (float)qmax);
                     dq[j] = hw_rn_f16((q - cz) * sh);
                 }
+                auto dqf = [&](int j) { return dq[j]; };
+#endif
+                auto ieee = [&]() {
+#pragma unroll
+                    for (int c = 0; c < EPL / 8; ++c) acc[c] = 0.0f;
+#pragma unroll
+                    for (int j = 0; j < EPL; ++j) {
+                        const float e = dqf(j) / s[j] - v[j];
+                        acc[j / 8] = acc[j / 8] + h[j] * (e * e);
+                    }
+                };
                 if (mq) {
 #pragma unroll
                     for (int j = 0; j < EPL; ++j) {
-                        const float e = mquot(dq[j], s[j], rs[j]) - v[j];
+#if AWQ_ACT_MIX_DQ
+                        const float w_hat = (j & 1) ? mquot_h<true>(dqp[j / 2], s[j], rs[j])
+                                                    : mquot_h<false>(dqp[j / 2], s[j], rs[j]);
+#else
+                        const float w_hat = mquot(dqf(j), s[j], rs[j]);
+#endif
+                        const float e = w_hat - v[j];
                         acc[j / 8] = acc[j / 8] + h[j] * (e * e);
                     }
-                } else {
+#if AWQ_ACT_NAN_RTABLE
+                    // a NaN loss: an out-of-range reciprocal (NaN), or a NaN / inf statistic —
+                    // the wave redoes the candidate with IEEE divisions (same bits in range)
+                    bool bad = false;
 #pragma unroll
-                    for (int j = 0; j < EPL; ++j) {
-                        const float e = dq[j] / s[j] - v[j];
-                        acc[j / 8] = acc[j / 8] + h[j] * (e * e);
-                    }
+                    for (int c = 0; c < EPL / 8; ++c) bad |= acc[c] != acc[c];
+                    if (__builtin_expect(__builtin_amdgcn_ballot_w64(bad) != 0, 0)) ieee();
+#endif
+                } else {
+                    ieee();
                 }
             } else {
                 const float sh = sw_f16_to_f32(canon_f16(cs));
@@ -1225,13 +1342,15 @@ hipError_t launch_scale_table(const float* x_mean, const float* w_mean, int64_t 
     return hipPeekAtLastError();
 }
 
-// rtable[i] = RN_f32(1 / table[i]) inside [2^-60, 2^60] (mquot's proven range), else 0
+// rtable[i] = RN_f32(1 / table[i]) inside [2^-60, 2^60] (mquot's proven range), else a NaN
+// (AWQ_ACT_NAN_RTABLE: a quotient through it is NaN, which sends its wave to the IEEE division;
+// 0 in the round-5 encoding, checked per wave and candidate)
 __global__ __launch_bounds__(256) void recip_table_kernel(const float* __restrict__ table, int64_t n,
                                                           float* __restrict__ rtable) {
     const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (i >= n) return;
     const float s = table[i];
-    rtable[i] = (s >= 0x1p-60f && s <= 0x1p60f) ? 1.0f / s : 0.0f;
+    rtable[i] = (s >= 0x1p-60f && s <= 0x1p60f) ? 1.0f / s : (AWQ_ACT_NAN_RTABLE ? __builtin_nanf("") : 0.0f);
 }
 
 // awq_selftest 1: mquot == IEEE division for every s in [1, 2) (all 2^23 mantissas) and every

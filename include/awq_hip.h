@@ -523,9 +523,10 @@ int awq_act_scale_table(const float* x_mean, const float* w_mean, int64_t K, int
  * work fp64 [n_grid * (K + 3 * ceil(K / 256))].  (ABI 16) */
 int awq_act_scale_table_ws(const float* x_mean, const float* w_mean, int64_t K, int n_grid, double* work,
                            float* table, void* stream);
-/* rtable [n_grid, K] = RN_f32(1 / table) where table is in [2^-60, 2^60], else 0: lets the
- * loss kernel form fp32(dq / s) as one Markstein-corrected product (exact there: awq_selftest
- * 1), falling back to the IEEE division for a wave whose channels leave that range. */
+/* rtable [n_grid, K] = RN_f32(1 / table) where table is in [2^-60, 2^60], else a NaN (ABI 17;
+ * was 0): lets the loss kernel form fp32(dq / s) as one Markstein-corrected product (exact there:
+ * awq_selftest 1); a quotient through an out-of-range entry is NaN, and a wave whose candidate
+ * loss comes out NaN redoes that candidate with IEEE divisions (the same bits in range). */
 int awq_act_recip_table(const float* table, int n_grid, int64_t K, float* rtable, void* stream);
 /* rtable: awq_act_recip_table's output for the same table, or NULL (IEEE divisions) */
 int awq_act_search_losses(const void* w, int dtype, int64_t rows, int64_t K, int64_t group_size, int bits,

@@ -180,8 +180,10 @@ KERNELS = {
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "round6", "pmc_valu.json"))
-    ap.add_argument("--types-dir", default=os.path.join(ROOT, "profiles", "round6", "r6x"),
-                    help="the per-type counter passes (search_a/b, act_a/b: scripts/cmd/r6x.sh)")
+    ap.add_argument("--types-dir", default="search=" + os.path.join(ROOT, "profiles", "round6", "r6x") + ",act="
+                    + os.path.join(ROOT, "profiles", "round6", "r6n"),
+                    help="kind=dir,...: the per-type counter passes (search_a/b: scripts/cmd/r6x.sh; act_a/b: "
+                         "r6n.sh, after the act kernel's round-6 trims)")
     ap.add_argument("--write", default="")
     ap.add_argument("--no-isa", action="store_true", help="floors only (no hipcc)")
     a = ap.parse_args()
@@ -206,8 +208,10 @@ def main():
             r["measured_slots_per_element"] = round(meas * 64, 3)
         lane = rec.get("valu_lane_instr_per_unit")
         if lane:
-            dyn = dynamic_types(a.types_dir, key, lane)
-            r["types_source"] = os.path.relpath(a.types_dir, ROOT)
+            tdirs = dict(kv.split("=", 1) for kv in a.types_dir.split(","))
+            tdir = tdirs[key.split(".")[0]]
+            dyn = dynamic_types(tdir, key, lane)
+            r["types_source"] = os.path.relpath(tdir, ROOT)
             if dyn:
                 r["measured_instructions_by_type"] = dyn
                 r["excess_instructions_by_type"] = {t: round(v - floor_types.get(t, 0.0), 3) for t, v in dyn.items()}

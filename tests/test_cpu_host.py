@@ -215,3 +215,34 @@ def test_bench_valu_roofline_issue_slot_model(tmp_path):
     assert bench.recorded_valu(str(p), "stale", bench.KERNEL_SOURCES)[0] is None
     assert bench.recorded_valu(str(p), "old", bench.KERNEL_SOURCES)[0] is None
     assert bench.recorded_valu(str(p), "missing", bench.KERNEL_SOURCES) == (None, None)
+
+
+def test_abi17_argument_validation_without_gpu():
+    """The round-6 entry points reject bad arguments before anything is launched: integer op
+    dtypes only in dequantize mode, no uint16/32/64 / bool op dtypes, _UNSIGNED only with _INT,
+    unknown flags; awq_group_params_ex flags; awq_dequant_ceiling sizes and alignment."""
+    from awq_quantizer import _hip
+    lib = _hip.load_library()
+    P = ctypes.c_void_p(64)
+    null = None
+    # x int64 (5) quantized with int64 op dtypes: mode 0 divides -> float ops only
+    assert lib.awq_apply_params_ex(P, 5, 1, 8, 8, P, P, 0, 15, 0, 5, 5, 0, P, null) != 0
+    assert "floating point" in _hip.last_error()
+    for bad_op in (9, 10, 11, 12, 13, -1):            # bool / uint16 / uint32 / uint64 / unknown
+        assert lib.awq_apply_params_ex(P, 5, 1, 8, 8, P, P, 0, 15, 1, bad_op, 2, 0, P, null) != 0
+        assert "op dtype" in _hip.last_error()
+    assert lib.awq_apply_params_ex(P, 13, 1, 8, 8, P, P, 0, 15, 1, 2, 2, 0, P, null) != 0   # x dtype 13
+    assert lib.awq_apply_params_ex(P, 5, 1, 8, 8, P, P, 0, 15, 1, 5, 5, _hip.APPLY_SCALE_UNSIGNED, P, null) != 0
+    assert "_INT" in _hip.last_error()
+    assert lib.awq_apply_params_ex(P, 5, 1, 8, 8, P, P, 0, 15, 1, 5, 5, 128, P, null) != 0
+    assert "unknown flags" in _hip.last_error()
+    # every valid combination of sizes 0 returns before touching a pointer or the device
+    allf = (_hip.APPLY_SCALE_ONE_ELEMENT | _hip.APPLY_ZERO_ONE_ELEMENT | _hip.APPLY_SCALE_INT | _hip.APPLY_ZERO_INT
+            | _hip.APPLY_SCALE_UNSIGNED | _hip.APPLY_ZERO_UNSIGNED | _hip.APPLY_IEEE_CLAMP)
+    assert lib.awq_apply_params_ex(null, 12, 0, 8, 8, null, null, 0, 15, 0, 2, 2, allf, null, null) == 0
+    assert lib.awq_group_params_ex(P, 0, 1, 128, 128, 4, 0, 2, P, P, null) != 0
+    assert "unknown flags" in _hip.last_error()
+    assert lib.awq_group_params_ex(null, 0, 0, 128, 128, 4, 0, _hip.GP_TORCH_GPU, P, P, null) == 0
+    assert lib.awq_dequant_ceiling(P, P, 24, null) != 0 and "multiple of 16" in _hip.last_error()
+    assert lib.awq_dequant_ceiling(ctypes.c_void_p(66), P, 32, null) != 0 and "misaligned" in _hip.last_error()
+    assert lib.awq_dequant_ceiling(null, null, 0, null) == 0

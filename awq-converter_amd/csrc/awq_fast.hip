@@ -261,15 +261,27 @@ __device__ __forceinline__ float shrink(float v, float al) {
     return F::rn(opaque(v * al));
 }
 
+// alpha_i = RN_f32((n_grid - i) / n_grid) from rn = RN(1 / n_grid) and one Markstein correction:
+// the IEEE quotient's bits for every n_grid <= 65536 (exhaustive, oracle/verify_recip.c alpha),
+// without an IEEE division per candidate; larger grids divide
+__device__ __forceinline__ float search_alpha(int n_grid, int i, float rn) {
+    const float a = (float)(n_grid - i), nf = (float)n_grid;
+    if (__builtin_expect(n_grid > 65536, 0)) return a / nf;
+    const float q = a * rn;
+    const float r = __builtin_fmaf(-nf, q, a);
+    return __builtin_fmaf(r, rn, q);
+}
+
 template <typename F, int BITS, bool SYM, int GS>
 __device__ __forceinline__ void search_range(const Chunk<F::NW> (&v)[4], float& gmn, float& gmx, bool gnan, int n_grid,
                                           int n_cand) {
     const int jj = threadIdx.x & 3;
+    const float rn = 1.0f / (float)n_grid;
     constexpr bool kLateS = AWQ_SEARCH_S_LATE && std::is_same<F, FmtBF16>::value;
     float best = __builtin_inff();
     int bi = 0;
     for (int i = 0; i < n_cand; ++i) {
-        const float al = (float)(n_grid - i) / (float)n_grid;
+        const float al = search_alpha(n_grid, i, rn);
         const GroupParams cp = params_from_range<F, BITS, SYM>(shrink<F>(gmn, al), shrink<F>(gmx, al));
         const float csh = F::dq_scale(cp.s);
 #pragma unroll
@@ -301,7 +313,7 @@ __device__ __forceinline__ void search_range(const Chunk<F::NW> (&v)[4], float& 
         }
     }
     if (!gnan && bi != 0) {
-        const float al = (float)(n_grid - bi) / (float)n_grid;
+        const float al = search_alpha(n_grid, bi, rn);
         gmn = shrink<F>(gmn, al);
         gmx = shrink<F>(gmx, al);
     }

@@ -78,7 +78,32 @@ static int check_f16_small(void) {
     return mismatches == 0 ? 0 : 1;
 }
 
+/* The clip search's candidate factor alpha_i = RN_f32((n - i) / n) (include/awq_hip.h
+ * awq_quantize_search) as the streaming kernel forms it without a division per candidate:
+ * q = a * RN(1/n), r = fma(-n, q, a), alpha = fma(r, RN(1/n), q) with a = n - i — equal to the
+ * IEEE quotient for every n <= 65536 and 0 <= i < n (2.1e9 pairs). */
+static int check_alpha(void) {
+    long long pairs = 0, mismatches = 0;
+#pragma omp parallel for reduction(+ : pairs, mismatches) schedule(dynamic, 256)
+    for (int n = 1; n <= 65536; ++n) {
+        volatile float one = 1.0f;
+        const float nf = (float)n, rn = one / nf;
+        for (int i = 0; i < n; ++i) {
+            const float a = (float)(n - i);
+            const float q = a * rn;
+            const float r = fmaf(-nf, q, a);
+            const float al = fmaf(r, rn, q);
+            volatile float want = a / nf;
+            pairs++;
+            if (memcmp(&al, (const void*)&want, 4) != 0) mismatches++;
+        }
+    }
+    printf("alpha (n - i) / n, n <= 65536: pairs=%lld mismatches=%lld\n", pairs, mismatches);
+    return mismatches == 0 ? 0 : 1;
+}
+
 int main(int argc, char** argv) {
+    if (argc > 1 && strcmp(argv[1], "alpha") == 0) return check_alpha();
     if (argc > 1 && strcmp(argv[1], "f16m") == 0) return check_f16_markstein();
     if (argc > 1 && strcmp(argv[1], "f16s") == 0) return check_f16_small();
     int bf = !(argc > 1 && strcmp(argv[1], "f16") == 0);

@@ -105,3 +105,16 @@ def test_f16_plain_product_small_scales_exhaustive():
                          capture_output=True, text=True, timeout=600)
     assert out.returncode == 0, out.stdout + out.stderr
     assert "mismatches=0" in out.stdout and "first_failing_scale=14" in out.stdout
+
+
+def test_search_alpha_markstein_exhaustive():
+    """The clip search's alpha_i = RN((n - i) / n) from RN(1/n) and one Markstein correction ==
+    the IEEE quotient for every n <= 65536 and i < n (2.1e9 pairs): the streaming kernel forms
+    it without a division per candidate (awq_fast.hip search_alpha)."""
+    import os
+    import subprocess
+    subprocess.run(["make", "-s", "-C", os.path.dirname(orc.__file__), "verify_recip"], check=True)
+    out = subprocess.run([os.path.join(os.path.dirname(orc.__file__), "verify_recip"), "alpha"],
+                         capture_output=True, text=True, timeout=600)
+    assert out.returncode == 0, out.stdout + out.stderr
+    assert "pairs=2147516416 mismatches=0" in out.stdout

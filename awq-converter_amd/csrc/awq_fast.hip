@@ -181,12 +181,55 @@ __device__ __forceinline__ float grp_sum(float v) {
     return v;
 }
 
+// The same tree for the 4 groups of this lane's loads at once, each lane keeping only the sum
+// of the group it scores (load p = lane & 3, the lane's jj): a reduce-scatter.  Pair sums (xor
+// 1) keep the two loads of this lane's parity, quad sums (xor 2) the lane's own load; the
+// position-preserving partners lane ^ 4 (two bank-masked row rotates) and lane ^ 8 (row_ror:8)
+// then add the quads and halves in the order grp_sum does.  Sums are commutative, so every
+// group's total is grp_sum's bits.  11.5 VALU slots for four groups instead of 4 x 4 DPP adds.
+template <int L>
+__device__ __forceinline__ float grp_sum_scatter(const float (&e)[4]) {
+    const int lane = threadIdx.x & 63;
+    const bool b0 = lane & 1, b1 = lane & 2;
+    const float m01 = b0 ? e[1] : e[0], s01 = b0 ? e[0] : e[1];
+    const float m23 = b0 ? e[3] : e[2], s23 = b0 ? e[2] : e[3];
+    const float u = m01 + __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, s01), 0xB1, 0xF, 0xF, true));
+    const float w = m23 + __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, s23), 0xB1, 0xF, 0xF, true));
+    const float m = b1 ? w : u, s = b1 ? u : w;
+    float t = m + __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, s), 0x4E, 0xF, 0xF, true));
+    if (L >= 8) {   // lane ^ 4: quads 1, 3 read lane - 4 (row_ror:4), quads 0, 2 lane + 4 (row_ror:12)
+        const int tb = __builtin_bit_cast(int, t);
+        int x = __builtin_amdgcn_update_dpp(tb, tb, 0x124, 0xF, 0xA, false);
+        x = __builtin_amdgcn_update_dpp(x, tb, 0x12C, 0xF, 0x5, false);
+        t = t + __builtin_bit_cast(float, x);
+    }
+    if (L >= 16) t = dpp_add<0x128>(t);    // lane ^ 8: row_ror:8
+    if (L >= 32) {                         // (row 2k) + (row 2k+1) on both rows
+        const auto p = __builtin_amdgcn_permlane16_swap(__builtin_bit_cast(unsigned, t), __builtin_bit_cast(unsigned, t),
+                                                        false, false);
+        t = __builtin_bit_cast(float, (unsigned)p[0]) + __builtin_bit_cast(float, (unsigned)p[1]);
+    }
+    return t;
+}
+
 // AWQ_SEARCH_FMA_MIX = 0: the round-5 error chain (A/B builds, scripts/build_variant.sh)
 #ifndef AWQ_SEARCH_FMA_MIX
 #define AWQ_SEARCH_FMA_MIX 1
 #endif
 #ifndef AWQ_SEARCH_S_LATE
 #define AWQ_SEARCH_S_LATE 1
+#endif
+// AWQ_SEARCH_F16_PACKED = 0: fp16 search always through the Markstein f32 chain
+#ifndef AWQ_SEARCH_F16_PACKED
+#define AWQ_SEARCH_F16_PACKED 1
+#endif
+// waves per SIMD the search instances are compiled for (the VGPR budget: 4 -> 128, 5 -> 96, 6 -> 80)
+#ifndef AWQ_SEARCH_MIN_WAVES
+#define AWQ_SEARCH_MIN_WAVES 4
+#endif
+// AWQ_SEARCH_SCATTER = 0: per-load group sums (grp_sum) and per-load special-scale ballots
+#ifndef AWQ_SEARCH_SCATTER
+#define AWQ_SEARCH_SCATTER 1
 #endif
 // Squared error of this lane's 8-element chunk of a group for one candidate (r, z, s) —
 // quantize (awq.py:245-248), dequantize the reference's way (fp16(fp16(q - z) * fp16(s)),
@@ -249,6 +292,42 @@ __device__ __forceinline__ float chunk_err(const Chunk<F::NW>& v, float r, float
     return acc;
 }
 
+// fp16 weights, every group of the wave with a scale < 14 (FmtF16::plain_ok, the common case):
+// the same error with the chain kept in packed fp16 — t = RN_f16(RN_f32(x * r)) (the verified
+// plain quotient; one rounding straight to fp16 would miss 890 pairs, oracle/verify_recip.c
+// f16f), u = RN_f16(t + z), the integer rint(u) as RN_f16(u + 1024) (unit spacing in
+// [1024, 2048), 1024 even: ties stay half-even) clamped to [1024 + qmin', 1024 + qmax'],
+// q - z = that - (1024 + z) (exact), dq = RN_f16((q - z) * s) (v_pk_mul_f16: one rounding of the
+// exact product, the reference's fp16 multiply), x - dq as v_fma_mix_f32 on the two fp16
+// operands.  Two elements per packed instruction.
+template <int BITS, bool SYM>
+__device__ __forceinline__ float chunk_err_f16p(const Chunk<1>& v, float r, float z, float s) {
+    constexpr float QLO = SYM ? -(float)(1 << (BITS - 1)) : 0.0f;
+    constexpr float QHI = SYM ? (float)((1 << (BITS - 1)) - 1) : (float)((1 << BITS) - 1);
+    constexpr _Float16 OFF = (_Float16)(SYM ? 1024 + (1 << (BITS - 1)) : 1024);   // rounding bias
+    constexpr _Float16 HI = (_Float16)(1024.0f + QHI - QLO);
+    const _Float16 zh = (_Float16)z, sh = (_Float16)s;   // exact: an integer <= 255, an fp16 scale
+    const h2v zz = {zh, zh}, ss = {sh, sh}, off = {OFF, OFF};
+    const h2v lo = {(_Float16)1024, (_Float16)1024}, hi = {HI, HI};
+    const h2v qz = SYM ? (h2v){OFF, OFF} : (h2v){(_Float16)1024 + zh, (_Float16)1024 + zh};
+    float acc = 0.0f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const uint32_t w = v.w[0][i];
+        const float x0 = FmtF16::lo(w), x1 = FmtF16::hi(w);
+        const h2v t = __builtin_convertvector((f2){opaque(x0 * r), opaque(x1 * r)}, h2v);   // RN_f16(RN_f32(x r))
+        const h2v u = SYM ? t : t + zz;                                                    // RN_f16(t + z)
+        const h2v q = __builtin_elementwise_min(__builtin_elementwise_max(u + off, lo), hi);   // 1024 + q - qmin
+        const h2v dq = (q - qz) * ss;                                                      // RN_f16((q - z) s)
+        float d0, d1;
+        asm("v_fma_mix_f32 %0, %1, 1.0, -%2 op_sel_hi:[1,0,1]" : "=v"(d0) : "v"(w), "v"(dq));
+        asm("v_fma_mix_f32 %0, %1, 1.0, -%2 op_sel:[1,0,1] op_sel_hi:[1,0,1]" : "=v"(d1) : "v"(w), "v"(dq));
+        acc = acc + d0 * d0;
+        acc = acc + d1 * d1;
+    }
+    return acc;
+}
+
 // Opt-in clip search (include/awq_hip.h awq_quantize_search) inside the streaming kernel:
 // candidates alpha_i = (n_grid - i) / n_grid shrink [mn, mx]; lane (grp, ch) evaluates the
 // candidate's parameters for its parameter group (the one in load ch & 3), the L lanes of a
@@ -275,7 +354,7 @@ __device__ __forceinline__ float search_alpha(int n_grid, int i, float rn) {
 template <typename F, int BITS, bool SYM, int GS>
 __device__ __forceinline__ void search_range(const Chunk<F::NW> (&v)[4], float& gmn, float& gmx, bool gnan, int n_grid,
                                           int n_cand) {
-    const int jj = threadIdx.x & 3;
+    [[maybe_unused]] const int jj = threadIdx.x & 3;
     const float rn = 1.0f / (float)n_grid;
     constexpr bool kLateS = AWQ_SEARCH_S_LATE && std::is_same<F, FmtBF16>::value;
     float best = __builtin_inff();
@@ -284,6 +363,33 @@ __device__ __forceinline__ void search_range(const Chunk<F::NW> (&v)[4], float& 
         const float al = search_alpha(n_grid, i, rn);
         const GroupParams cp = params_from_range<F, BITS, SYM>(shrink<F>(gmn, al), shrink<F>(gmx, al));
         const float csh = F::dq_scale(cp.s);
+#if AWQ_SEARCH_SCATTER
+        // one wave-wide test per candidate: any group of the tile with a 0 / inf / NaN scale sends
+        // all four loads through the per-lane special-aware chain (equal bits on the other lanes)
+        const bool any_special = __builtin_amdgcn_ballot_w64(!F::fast(cp.r)) != 0;
+        // fp16: every scale of the wave < 14 -> the packed plain chain (chunk_err_f16p)
+        const bool plain16 = AWQ_SEARCH_F16_PACKED && std::is_same<F, FmtF16>::value &&
+                             __builtin_amdgcn_ballot_w64(!F::plain_ok(cp.s)) == 0;
+        float e[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const float rj = bcast_j(j, cp.r);
+            const float zj = SYM ? 0.0f : bcast_j(j, cp.z);
+            const float hj = bcast_j(j, csh);
+            if (__builtin_expect(any_special, 0))
+                e[j] = chunk_err<F, BITS, SYM>(v[j], rj, zj, bcast_j(j, cp.s), hj, !F::fast(rj));
+            else if constexpr (std::is_same<F, FmtF16>::value) {
+                if (plain16) e[j] = chunk_err_f16p<BITS, SYM>(v[j], rj, zj, hj);
+                else e[j] = chunk_err<F, BITS, SYM>(v[j], rj, zj, bcast_j(j, cp.s), hj, false);
+            } else
+                e[j] = chunk_err<F, BITS, SYM>(v[j], rj, zj, kLateS ? 0.0f : bcast_j(j, cp.s), hj, false);
+        }
+        const float ej = grp_sum_scatter<GS / 8>(e);
+        if (ej < best) {
+            best = ej;
+            bi = i;
+        }
+#else
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             const float rj = bcast_j(j, cp.r);
@@ -311,6 +417,7 @@ __device__ __forceinline__ void search_range(const Chunk<F::NW> (&v)[4], float& 
                 bi = i;
             }
         }
+#endif
     }
     if (!gnan && bi != 0) {
         const float al = search_alpha(n_grid, bi, rn);
@@ -565,7 +672,7 @@ __device__ uint64_t* g_trace = nullptr;
 // grid (awq_diag.h max_blocks, tests) makes each wave walk tiles t, t + nwaves, ... with a
 // tensor cursor.
 template <typename F, int BITS, bool SYM, bool SEARCH, int GS, bool PAD, bool SCALED = false>
-__global__ __launch_bounds__(64 * kWavesPerBlock, SEARCH ? 4 : (F::kWide ? AWQ_MIN_WAVES_WIDE : AWQ_MIN_WAVES))
+__global__ __launch_bounds__(64 * kWavesPerBlock, SEARCH ? AWQ_SEARCH_MIN_WAVES : (F::kWide ? AWQ_MIN_WAVES_WIDE : AWQ_MIN_WAVES))
 void awq_fast_kernel(
     // the scalars every wave needs first lead the argument block (they fit the kernarg
     // preload window of a -mllvm -amdgpu-kernarg-preload-count build); the 80-B single-

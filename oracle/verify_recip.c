@@ -8,8 +8,9 @@
  * reproduces awq.py:245's `tensor / scale` (torch bf16 divide = fp32 divide + RNE)
  * and awq.py:210's `t_min / scale` bit for bit.  Also reports the fp16 analogue
  * (expected to FAIL, which is why fp16 inputs use a true division).
- * Usage: verify_recip [bf16|f16|f16m|f16s] -> prints mismatches, exit 0 iff none (bf16;
- * f16m: the fp16 Markstein-corrected quotient; f16s: the fp16 plain product for s < 14). */
+ * Usage: verify_recip [bf16|f16|f16m|f16s|f16f|alpha] -> prints mismatches, exit 0 iff none (bf16;
+ * f16m: the fp16 Markstein-corrected quotient; f16s: the fp16 plain product for s < 14;
+ * f16f: the same product rounded once, straight to fp16; alpha: the search's candidate factor). */
 #include <math.h>
 #include <stdio.h>
 #include <stdint.h>
@@ -78,6 +79,47 @@ static int check_f16_small(void) {
     return mismatches == 0 ? 0 : 1;
 }
 
+/* RN_f16 of a double (round to nearest even, fp16 subnormals, overflow to inf): the quantum of
+ * |d|'s binade (or the subnormal quantum 2^-24), nearbyint in the default RNE mode. */
+static double rn_f16_of_double(double d) {
+    if (d == 0.0 || d != d) return d;
+    const double a = fabs(d);
+    int e;
+    frexp(a, &e);                         /* a in [2^(e-1), 2^e) */
+    const int ex = (e - 1 < -14) ? -14 : e - 1;
+    const double q = ldexp(1.0, ex - 10);
+    double r = nearbyint(a / q) * q;
+    if (r >= 65520.0) r = INFINITY;       /* (65504 + 16: the RNE overflow threshold) */
+    else if (r > 65504.0) r = 65504.0;
+    return d < 0 ? -r : r;
+}
+
+/* The clip search's fp16 chain (csrc/awq_fast.hip chunk_err_f16p) forms t = RN_f16(x * r) with
+ * ONE rounding (v_fma_mixlo_f16 / v_fma_mixhi_f16: the exact product rounded to fp16): for every
+ * finite fp16 x and every positive fp16 s < 14 it must equal RN_f16(RN_f32(x / s)) (torch's fp16
+ * division), by value. */
+static int check_f16_fused(void) {
+    long long mismatches = 0, pairs = 0;
+#pragma omp parallel for reduction(+ : mismatches, pairs) schedule(dynamic, 64)
+    for (int si = 1; si < 0x7C00; ++si) {
+        const float s = oracle_f16_to_f32((uint16_t)si);
+        if (!(s < 14.0f)) continue;
+        volatile float one = 1.0f;
+        const float r = one / s;
+        for (int xi = 0; xi < 65536; ++xi) {
+            const uint16_t xh = (uint16_t)xi;
+            if ((xh & 0x7C00u) == 0x7C00u) continue;
+            const float x = oracle_f16_to_f32(xh);
+            const double a = rn_f16_of_double((double)x * (double)r);   /* exact product, one rounding */
+            const float b = oracle_f16_to_f32(oracle_f32_to_f16(x / s));
+            pairs++;
+            if (!(a == (double)b)) mismatches++;
+        }
+    }
+    printf("f16 fused small-scale product: pairs=%lld mismatches=%lld\n", pairs, mismatches);
+    return mismatches == 0 ? 0 : 1;
+}
+
 /* The clip search's candidate factor alpha_i = RN_f32((n - i) / n) (include/awq_hip.h
  * awq_quantize_search) as the streaming kernel forms it without a division per candidate:
  * q = a * RN(1/n), r = fma(-n, q, a), alpha = fma(r, RN(1/n), q) with a = n - i — equal to the
@@ -106,6 +148,7 @@ int main(int argc, char** argv) {
     if (argc > 1 && strcmp(argv[1], "alpha") == 0) return check_alpha();
     if (argc > 1 && strcmp(argv[1], "f16m") == 0) return check_f16_markstein();
     if (argc > 1 && strcmp(argv[1], "f16s") == 0) return check_f16_small();
+    if (argc > 1 && strcmp(argv[1], "f16f") == 0) return check_f16_fused();
     int bf = !(argc > 1 && strcmp(argv[1], "f16") == 0);
     float lo = dec(enc(1e-10f, bf), bf);
     long long mismatches = 0, pairs = 0;

@@ -159,6 +159,54 @@ def hot_loop(body, rint_per_iter):
     return best
 
 
+def common_path_loop(body, rint_per_iter):
+    """The candidate loop's common path, walked block by block from an inner-loop header: a
+    conditional branch falls through unless the fall-through block holds an IEEE division
+    (v_div_scale: the rare n_grid > 65536 / 0-inf-NaN-scale paths), s_branch is followed, and the
+    walk ends when it is back at the header.  Returns (header line, VALU opcodes) for the first
+    header whose walk holds `rint_per_iter` .. + 2 v_rndne, or None (hot_loop is the fallback)."""
+    starts, names = [], []
+    for n, line in enumerate(body):
+        s = line.strip()
+        m = re.match(r"^(\.LBB\w+):", s) or re.match(r"^; (%bb\.\d+):", s)
+        if m:
+            starts.append(n)
+            names.append(m.group(1))
+    idx = {nm: i for i, nm in enumerate(names)}
+    ends = starts[1:] + [len(body)]
+
+    def instrs(i):
+        return [x.strip() for x in body[starts[i] + 1:ends[i]]
+                if x.strip() and not x.strip().startswith((";", "."))]
+
+    headers = [i for i, n in enumerate(starts) if any("Inner Loop Header" in body[k] for k in (n, n + 1, n + 2)
+                                                      if k < len(body))]
+    for h in headers:
+        i, ops, steps = h, [], 0
+        while steps < 400:
+            steps += 1
+            ins = instrs(i)
+            ops += [x.split()[0] for x in ins if x.split()[0].startswith("v_")]
+            last = ins[-1].split() if ins else [""]
+            nxt = i + 1
+            if last[0] == "s_branch":
+                nxt = idx.get(last[1], -1)
+            elif last[0].startswith("s_cbranch_"):
+                tgt = idx.get(last[1], -1)
+                if tgt == h or nxt == h:
+                    nxt = h
+                elif nxt < len(starts) and any(x.startswith("v_div_scale") for x in instrs(nxt)):
+                    nxt = tgt
+            if nxt == h:
+                if rint_per_iter <= sum(o.startswith("v_rndne") for o in ops) <= rint_per_iter + 2:
+                    return starts[h], ops
+                break
+            if nxt < 0 or nxt >= len(starts):
+                break
+            i = nxt
+    return None
+
+
 def categorize(ops, elements):
     out = collections.OrderedDict((c, 0.0) for c, _ in CATEGORY)
     for o in ops:
@@ -220,11 +268,14 @@ def main():
             if not os.path.exists(sfile):
                 subprocess.run(["make", "-s", "-C", CSRC, "isa", f"ISA_SRC={k['src']}"], check=True)
             name, body = function_body(open(sfile).read(), k["fn"])
-            loop = hot_loop(body, k["elements"])
+            walk = common_path_loop(body, k["elements"])
+            loop = (walk[0], None, walk[1]) if walk else hot_loop(body, k["elements"])
             if loop:
                 a0, a1, ops = loop
                 cats = categorize(ops, k["elements"])
                 r["isa"] = {"function": name, "loop_lines": [a0, a1], "valu_instructions": len(ops),
+                            "loop_extraction": "common-path walk from the loop header" if walk
+                            else "smallest backward-branch region",
                             "elements_per_iteration": k["elements"],
                             "loop_slots_per_element": round(sum(slots(o) for o in ops) / k["elements"], 3),
                             "loop_slots_per_element_by_category": cats,

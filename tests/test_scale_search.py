@@ -160,6 +160,39 @@ def test_search_gpu_fast_path_special_groups(dtype):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("bits,sym", [(4, False), (4, True), (8, False), (8, True)])
+def test_search_gpu_f16_packed_chain_mixed_scales(bits, sym):
+    """Round 6: the fp16 search's packed chain (awq_fast.hip chunk_err_f16p, taken by waves whose
+    candidate scales are all < 14) next to the Markstein chain (a wave with one scale >= 14) and
+    the special path: small / large / near-constant large-magnitude (t overflows to inf) /
+    subnormal groups, rows mixing them inside one wave, against the oracle bit for bit."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from awq_quantizer.quantization import AWQQuantizer
+    g = torch.Generator().manual_seed(60 + bits + sym)
+    R, K = 48, 4096
+    x = torch.randn(R, K, generator=g) * 0.05
+    x[4:8] *= 1000.0                                              # s >= 14: Markstein waves
+    x[8:12] = 1000.0 + torch.randn(4, K, generator=g) * 0.3       # near-constant, large magnitude
+    x[12:16] = 4000.0 + torch.randn(4, K, generator=g) * 2.0      # x / s beyond the fp16 range
+    x[16:20] *= 2e-5                                              # subnormal fp16 values and scales
+    x[20:24, 128 * 5:128 * 6] *= 600.0                            # one large group inside plain waves
+    x[24:28, ::2] = torch.round(x[24:28, ::2] * 64) / 64          # coarse grid: quotient ties
+    x[28, 300] = float("nan")
+    x[29, 1000:1128] = 0.125                                      # constant group (s = 0)
+    x = x.half()
+    q = AWQQuantizer(bits=bits, group_size=128, symmetric=sym, scale_method="search", device="cuda",
+                     logger_level="ERROR")
+    ref = orc.quantize(x, bits=bits, group_size=128, symmetric=sym, search=(20, 10))
+    res = q.quantize(x)
+    assert torch.equal(res["tensor_q"], ref["tensor_q"])
+    assert torch.equal(res["zero_points"], ref["zero_points"])
+    assert gio.same_bits(res["scales"], ref["scales"])
+    pk = q.quantize_packed(x)
+    assert torch.equal(pk["qweight"].cpu(), orc.pack_rows(ref["tensor_q"], bits, q.qmin))
+
+
+@pytest.mark.gpu
 def test_search_gpu_special_values_and_rtn_identity():
     if not torch.cuda.is_available():
         pytest.skip("no GPU")

@@ -223,6 +223,10 @@ __device__ __forceinline__ float grp_sum_scatter(const float (&e)[4]) {
 #ifndef AWQ_SEARCH_F16_PACKED
 #define AWQ_SEARCH_F16_PACKED 1
 #endif
+// AWQ_SEARCH_BF16_HALF = 0: bf16 search's integer steps in f32 (chunk_err) instead of packed fp16
+#ifndef AWQ_SEARCH_BF16_HALF
+#define AWQ_SEARCH_BF16_HALF 1
+#endif
 // waves per SIMD the search instances are compiled for (the VGPR budget: 4 -> 128, 5 -> 96, 6 -> 80)
 #ifndef AWQ_SEARCH_MIN_WAVES
 #define AWQ_SEARCH_MIN_WAVES 4
@@ -300,16 +304,26 @@ __device__ __forceinline__ float chunk_err(const Chunk<F::NW>& v, float r, float
 // q - z = that - (1024 + z) (exact), dq = RN_f16((q - z) * s) (v_pk_mul_f16: one rounding of the
 // exact product, the reference's fp16 multiply), x - dq as v_fma_mix_f32 on the two fp16
 // operands.  Two elements per packed instruction.
+// (search_words packs the per-group fp16 operands once per lane: zs = {z, s}, qz = 1024 + z -
+// qmin in both halves; one DPP each instead of per-load conversions)
 template <int BITS, bool SYM>
-__device__ __forceinline__ float chunk_err_f16p(const Chunk<1>& v, float r, float z, float s) {
+__device__ __forceinline__ void search_words(float z, float s, uint32_t& zs, uint32_t& qzw) {
+    const _Float16 zh = (_Float16)z, sh = (_Float16)s;   // exact: an integer <= 255, an fp16 value
+    const _Float16 q = SYM ? (_Float16)(1024 + (1 << (BITS - 1))) : (_Float16)1024 + zh;
+    zs = __builtin_bit_cast(uint32_t, (h2v){zh, sh});
+    qzw = __builtin_bit_cast(uint32_t, (h2v){q, q});
+}
+
+template <int BITS, bool SYM>
+__device__ __forceinline__ float chunk_err_f16p(const Chunk<1>& v, float r, uint32_t zs, uint32_t qzw) {
     constexpr float QLO = SYM ? -(float)(1 << (BITS - 1)) : 0.0f;
     constexpr float QHI = SYM ? (float)((1 << (BITS - 1)) - 1) : (float)((1 << BITS) - 1);
     constexpr _Float16 OFF = (_Float16)(SYM ? 1024 + (1 << (BITS - 1)) : 1024);   // rounding bias
     constexpr _Float16 HI = (_Float16)(1024.0f + QHI - QLO);
-    const _Float16 zh = (_Float16)z, sh = (_Float16)s;   // exact: an integer <= 255, an fp16 scale
-    const h2v zz = {zh, zh}, ss = {sh, sh}, off = {OFF, OFF};
+    const h2v zsv = __builtin_bit_cast(h2v, zs);
+    const h2v zz = zsv.xx, ss = zsv.yy, off = {OFF, OFF};
     const h2v lo = {(_Float16)1024, (_Float16)1024}, hi = {HI, HI};
-    const h2v qz = SYM ? (h2v){OFF, OFF} : (h2v){(_Float16)1024 + zh, (_Float16)1024 + zh};
+    const h2v qz = __builtin_bit_cast(h2v, qzw);
     float acc = 0.0f;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -322,6 +336,47 @@ __device__ __forceinline__ float chunk_err_f16p(const Chunk<1>& v, float r, floa
         float d0, d1;
         asm("v_fma_mix_f32 %0, %1, 1.0, -%2 op_sel_hi:[1,0,1]" : "=v"(d0) : "v"(w), "v"(dq));
         asm("v_fma_mix_f32 %0, %1, 1.0, -%2 op_sel:[1,0,1] op_sel_hi:[1,0,1]" : "=v"(d1) : "v"(w), "v"(dq));
+        acc = acc + d0 * d0;
+        acc = acc + d1 * d1;
+    }
+    return acc;
+}
+
+// bf16 weights: the bf16 steps as in chunk_err (t = RN_bf16(x r), u = RN_bf16(t + z), f32 form),
+// then the integer steps in packed fp16: u is exact in fp16 wherever it matters (8 significant
+// bits; |u| < 2^-14 rounds to a value whose rint is 0 all the same, |u| > 65504 becomes inf and
+// clamps to the bound it would clamp to anyway), rint + clamp as in chunk_err_f16p, and
+// dq = RN_f16((q - z) s) by v_pk_mul_f16 (the exact product rounded once, as the f32 product +
+// v_cvt_pk_f16_f32 of chunk_err).
+// (qs = {1024 + z - qmin, s} in fp16, packed once per lane by search_words_bf16)
+template <int BITS, bool SYM>
+__device__ __forceinline__ uint32_t search_words_bf16(float z, float sh16) {
+    const _Float16 q = SYM ? (_Float16)(1024 + (1 << (BITS - 1))) : (_Float16)1024 + (_Float16)z;
+    return __builtin_bit_cast(uint32_t, (h2v){q, (_Float16)sh16});
+}
+
+template <int BITS, bool SYM>
+__device__ __forceinline__ float chunk_err_bf16h(const Chunk<1>& v, float r, float z, uint32_t qs) {
+    constexpr float QLO = SYM ? -(float)(1 << (BITS - 1)) : 0.0f;
+    constexpr float QHI = SYM ? (float)((1 << (BITS - 1)) - 1) : (float)((1 << BITS) - 1);
+    constexpr _Float16 OFF = (_Float16)(SYM ? 1024 + (1 << (BITS - 1)) : 1024);
+    constexpr _Float16 HI = (_Float16)(1024.0f + QHI - QLO);
+    const h2v qsv = __builtin_bit_cast(h2v, qs);
+    const h2v qz = qsv.xx, ss = qsv.yy, off = {OFF, OFF};
+    const h2v lo = {(_Float16)1024, (_Float16)1024}, hi = {HI, HI};
+    float acc = 0.0f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const uint32_t w = v.w[0][i];
+        const float x0 = FmtBF16::lo(w), x1 = FmtBF16::hi(w);
+        const float t0 = rn_bf16(x0 * r), t1 = rn_bf16(x1 * r);
+        const float u0 = SYM ? t0 : rn_bf16(t0 + z), u1 = SYM ? t1 : rn_bf16(t1 + z);
+        const h2v u = __builtin_convertvector((f2){u0, u1}, h2v);
+        const h2v q = __builtin_elementwise_min(__builtin_elementwise_max(u + off, lo), hi);
+        const h2v dq = (q - qz) * ss;
+        float d0, d1;
+        asm("v_fma_mix_f32 %0, %1, -1.0, %2 op_sel_hi:[1,0,0]" : "=v"(d0) : "v"(dq), "v"(x0));
+        asm("v_fma_mix_f32 %0, %1, -1.0, %2 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "=v"(d1) : "v"(dq), "v"(x1));
         acc = acc + d0 * d0;
         acc = acc + d1 * d1;
     }
@@ -370,19 +425,30 @@ __device__ __forceinline__ void search_range(const Chunk<F::NW> (&v)[4], float& 
         // fp16: every scale of the wave < 14 -> the packed plain chain (chunk_err_f16p)
         const bool plain16 = AWQ_SEARCH_F16_PACKED && std::is_same<F, FmtF16>::value &&
                              __builtin_amdgcn_ballot_w64(!F::plain_ok(cp.s)) == 0;
+        // the packed chains' fp16 operands, once per lane (a few instructions; unused in the
+        // waves that take another chain)
+        uint32_t w1 = 0, w2 = 0;
+        if constexpr (std::is_same<F, FmtF16>::value) search_words<BITS, SYM>(cp.z, csh, w1, w2);
+        else if constexpr (std::is_same<F, FmtBF16>::value) w1 = search_words_bf16<BITS, SYM>(cp.z, csh);
         float e[4];
+        // per load: the broadcasts, then a wave-uniform choice of chain (one chain's operands
+        // live at a time: the search instances stay at 80 / 96 VGPRs)
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             const float rj = bcast_j(j, cp.r);
-            const float zj = SYM ? 0.0f : bcast_j(j, cp.z);
-            const float hj = bcast_j(j, csh);
-            if (__builtin_expect(any_special, 0))
-                e[j] = chunk_err<F, BITS, SYM>(v[j], rj, zj, bcast_j(j, cp.s), hj, !F::fast(rj));
-            else if constexpr (std::is_same<F, FmtF16>::value) {
-                if (plain16) e[j] = chunk_err_f16p<BITS, SYM>(v[j], rj, zj, hj);
-                else e[j] = chunk_err<F, BITS, SYM>(v[j], rj, zj, bcast_j(j, cp.s), hj, false);
-            } else
-                e[j] = chunk_err<F, BITS, SYM>(v[j], rj, zj, kLateS ? 0.0f : bcast_j(j, cp.s), hj, false);
+            if (__builtin_expect(any_special, 0)) {
+                e[j] = chunk_err<F, BITS, SYM>(v[j], rj, SYM ? 0.0f : bcast_j(j, cp.z), bcast_j(j, cp.s), bcast_j(j, csh),
+                                               !F::fast(rj));
+            } else if constexpr (std::is_same<F, FmtF16>::value) {
+                if (plain16) e[j] = chunk_err_f16p<BITS, SYM>(v[j], rj, bcast_u(j, w1), bcast_u(j, w2));
+                else e[j] = chunk_err<F, BITS, SYM>(v[j], rj, SYM ? 0.0f : bcast_j(j, cp.z), bcast_j(j, cp.s),
+                                                    bcast_j(j, csh), false);
+            } else if constexpr (std::is_same<F, FmtBF16>::value && AWQ_SEARCH_BF16_HALF) {
+                e[j] = chunk_err_bf16h<BITS, SYM>(v[j], rj, SYM ? 0.0f : bcast_j(j, cp.z), bcast_u(j, w1));
+            } else {
+                e[j] = chunk_err<F, BITS, SYM>(v[j], rj, SYM ? 0.0f : bcast_j(j, cp.z), kLateS ? 0.0f : bcast_j(j, cp.s),
+                                               bcast_j(j, csh), false);
+            }
         }
         const float ej = grp_sum_scatter<GS / 8>(e);
         if (ej < best) {

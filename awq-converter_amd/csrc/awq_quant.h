@@ -83,6 +83,9 @@ __device__ __forceinline__ float quad_bcast(float v) {
 __device__ __forceinline__ float bcast_j(int j, float v) {   // j is a compile-time constant at every use
     return j == 0 ? quad_bcast<0>(v) : j == 1 ? quad_bcast<1>(v) : j == 2 ? quad_bcast<2>(v) : quad_bcast<3>(v);
 }
+__device__ __forceinline__ uint32_t bcast_u(int j, uint32_t v) {
+    return __builtin_bit_cast(uint32_t, bcast_j(j, __builtin_bit_cast(float, v)));
+}
 
 // RN_f32(1/s) for a bf16-valued s: v_rcp_f32 + one Newton step with fma is correctly
 // rounded for every bf16 s < 2^126 (checked exhaustively on the GPU by awq_selftest);

@@ -8,9 +8,10 @@
  * reproduces awq.py:245's `tensor / scale` (torch bf16 divide = fp32 divide + RNE)
  * and awq.py:210's `t_min / scale` bit for bit.  Also reports the fp16 analogue
  * (expected to FAIL, which is why fp16 inputs use a true division).
- * Usage: verify_recip [bf16|f16|f16m|f16s|f16f|alpha] -> prints mismatches, exit 0 iff none (bf16;
+ * Usage: verify_recip [bf16|f16|f16m|f16s|f16f|chain16|alpha] -> prints mismatches, exit 0 iff none (bf16;
  * f16m: the fp16 Markstein-corrected quotient; f16s: the fp16 plain product for s < 14;
- * f16f: the same product rounded once, straight to fp16; alpha: the search's candidate factor). */
+ * f16f: the same product rounded once, straight to fp16; chain16: the search's packed-fp16 rint
+ * and clamp; alpha: the search's candidate factor). */
 #include <math.h>
 #include <stdio.h>
 #include <stdint.h>
@@ -120,6 +121,37 @@ static int check_f16_fused(void) {
     return mismatches == 0 ? 0 : 1;
 }
 
+/* The clip search's packed-fp16 integer steps (csrc/awq_fast.hip chunk_err_f16p, chunk_err_bf16h):
+ * q = clamp(rint(u), qmin, qmax) formed as min(max(RN_f16(h + OFF), 1024), 1024 + qmax - qmin)
+ * - OFF + ... with OFF = 1024 - qmin, h = u for an fp16 u and h = RN_f16(u) for a bf16 u (f32
+ * form).  Every finite / infinite fp16 and bf16 u, 4 / 8 bit, asymmetric / symmetric. */
+static int check_chain16(void) {
+    long long cases = 0, mismatches = 0;
+    for (int bits = 4; bits <= 8; bits += 4)
+        for (int sym = 0; sym <= 1; ++sym) {
+            const double qmin = sym ? -(double)(1 << (bits - 1)) : 0.0;
+            const double qmax = sym ? (double)((1 << (bits - 1)) - 1) : (double)((1 << bits) - 1);
+            const double off = 1024.0 - qmin;
+            for (int bf = 0; bf <= 1; ++bf)
+                for (int i = 0; i < 65536; ++i) {
+                    const uint16_t hb = (uint16_t)i;
+                    const float u = dec(hb, bf);
+                    if (u != u) continue;
+                    const double h = bf ? (double)oracle_f16_to_f32(oracle_f32_to_f16(u)) : (double)u;
+                    double v = rn_f16_of_double(h + off);
+                    v = v < 1024.0 ? 1024.0 : v;
+                    v = v > 1024.0 + qmax - qmin ? 1024.0 + qmax - qmin : v;
+                    const double got = v - off;
+                    double want = nearbyint((double)u);
+                    want = want < qmin ? qmin : (want > qmax ? qmax : want);
+                    cases++;
+                    if (got != want) mismatches++;
+                }
+        }
+    printf("packed fp16 rint + clamp: cases=%lld mismatches=%lld\n", cases, mismatches);
+    return mismatches == 0 ? 0 : 1;
+}
+
 /* The clip search's candidate factor alpha_i = RN_f32((n - i) / n) (include/awq_hip.h
  * awq_quantize_search) as the streaming kernel forms it without a division per candidate:
  * q = a * RN(1/n), r = fma(-n, q, a), alpha = fma(r, RN(1/n), q) with a = n - i — equal to the
@@ -149,6 +181,7 @@ int main(int argc, char** argv) {
     if (argc > 1 && strcmp(argv[1], "f16m") == 0) return check_f16_markstein();
     if (argc > 1 && strcmp(argv[1], "f16s") == 0) return check_f16_small();
     if (argc > 1 && strcmp(argv[1], "f16f") == 0) return check_f16_fused();
+    if (argc > 1 && strcmp(argv[1], "chain16") == 0) return check_chain16();
     int bf = !(argc > 1 && strcmp(argv[1], "f16") == 0);
     float lo = dec(enc(1e-10f, bf), bf);
     long long mismatches = 0, pairs = 0;

@@ -113,6 +113,7 @@ CATEGORY = [   # (name, regex on the opcode) — first match wins
     ("rint / clamp", r"v_rndne.*|v_med3.*"),
     ("min / max", r"v_(min|max)(3)?_f32.*"),
     ("packed f32 arithmetic", r"v_pk_(add|mul|fma)_f32"),
+    ("packed fp16 arithmetic (rint by + 1024, clamp, q - z, * s)", r"v_pk_(add|mul|fma|max|min|sub)_f16"),
     ("f32 add / sub / mul / fma", r"v_(add|sub|subrev|mul|fma|fmac)_f32.*|v_fma_mix.*"),
     ("candidate parameters (division, reciprocal)", r"v_div_.*|v_rcp.*|v_frexp.*|v_ldexp.*"),
     ("compares / selects", r"v_cmp.*|v_cndmask.*"),
@@ -159,12 +160,13 @@ def hot_loop(body, rint_per_iter):
     return best
 
 
-def common_path_loop(body, rint_per_iter):
-    """The candidate loop's common path, walked block by block from an inner-loop header: a
-    conditional branch falls through unless the fall-through block holds an IEEE division
-    (v_div_scale: the rare n_grid > 65536 / 0-inf-NaN-scale paths), s_branch is followed, and the
-    walk ends when it is back at the header.  Returns (header line, VALU opcodes) for the first
-    header whose walk holds `rint_per_iter` .. + 2 v_rndne, or None (hot_loop is the fallback)."""
+def common_path_loop(body, rint_per_iter, marker="v_rndne"):
+    """The candidate loop's common path: over the blocks of an inner loop (the compiler's
+    "in Loop: Header=" block comments), the cheapest path in VALU slots from the header back to
+    it — the rare branches (IEEE divisions for n_grid > 65536, 0 / inf / NaN scales, fp16 scales
+    >= 14) are the longer ones.  Returns (header line, VALU opcodes) for the first inner-loop
+    header whose cheapest iteration holds `rint_per_iter` .. + 2 `marker` instructions (one per
+    element and candidate: KERNELS), or None (hot_loop is the fallback)."""
     starts, names = [], []
     for n, line in enumerate(body):
         s = line.strip()
@@ -179,31 +181,49 @@ def common_path_loop(body, rint_per_iter):
         return [x.strip() for x in body[starts[i] + 1:ends[i]]
                 if x.strip() and not x.strip().startswith((";", "."))]
 
-    headers = [i for i, n in enumerate(starts) if any("Inner Loop Header" in body[k] for k in (n, n + 1, n + 2)
-                                                      if k < len(body))]
-    for h in headers:
-        i, ops, steps = h, [], 0
-        while steps < 400:
-            steps += 1
+    def comment(i):
+        return " ".join(body[k] for k in range(starts[i], min(starts[i] + 3, len(body))))
+
+    for h in range(len(starts)):
+        if "Inner Loop Header" not in comment(h):
+            continue
+        hname = names[h].lstrip(".L")
+        member = {i for i in range(len(starts)) if f"Header={hname} " in comment(i) or i == h}
+        memo = {}
+
+        def best(i, need, depth=0):
+            """(slots, ops) of the cheapest path from block i to the back edge holding exactly
+            `need` marker instructions"""
+            key = (i, need)
+            if key in memo:
+                return memo[key]
+            memo[key] = (float("inf"), [])          # cycle guard
             ins = instrs(i)
-            ops += [x.split()[0] for x in ins if x.split()[0].startswith("v_")]
+            ops = [x.split()[0] for x in ins if x.split()[0].startswith("v_")]
+            left = need - sum(o.startswith(marker) for o in ops)
+            if left < 0:
+                return memo[key]
             last = ins[-1].split() if ins else [""]
-            nxt = i + 1
             if last[0] == "s_branch":
-                nxt = idx.get(last[1], -1)
+                succ = [idx.get(last[1], -1)]
             elif last[0].startswith("s_cbranch_"):
-                tgt = idx.get(last[1], -1)
-                if tgt == h or nxt == h:
-                    nxt = h
-                elif nxt < len(starts) and any(x.startswith("v_div_scale") for x in instrs(nxt)):
-                    nxt = tgt
-            if nxt == h:
-                if rint_per_iter <= sum(o.startswith("v_rndne") for o in ops) <= rint_per_iter + 2:
-                    return starts[h], ops
-                break
-            if nxt < 0 or nxt >= len(starts):
-                break
-            i = nxt
+                succ = [i + 1, idx.get(last[1], -1)]
+            else:
+                succ = [i + 1]
+            cands = []
+            for j in succ:
+                if j == h:
+                    cands.append((0.0, []) if left == 0 else (float("inf"), []))
+                elif j in member and depth < 300:
+                    cands.append(best(j, left, depth + 1))
+            c, o = min(cands, key=lambda t: t[0]) if cands else (float("inf"), [])
+            memo[key] = (c + sum(slots(x) for x in ops), ops + o)
+            return memo[key]
+
+        for need in range(rint_per_iter, rint_per_iter + 3):
+            cost, ops = best(h, need)
+            if cost < float("inf"):
+                return starts[h], ops
     return None
 
 
@@ -219,7 +239,7 @@ def categorize(ops, elements):
 
 KERNELS = {
     "search.bf16.asym": dict(src="awq_fast", fn=r"_ZN3awq12_GLOBAL__N_115awq_fast_kernelINS0_7FmtBF16ELi4ELb0ELb1ELi128ELb0ELb0EE\w*",
-                             elements=32, pmc_key="llama3-8b.b4.asym.packed.search10of20"),
+                             elements=32, marker="v_fma_mix_f32", pmc_key="llama3-8b.b4.asym.packed.search10of20"),
     "act.bf16.asym": dict(src="awq_actsearch", fn=r"_ZN3awq12_GLOBAL__N_115act_loss_kernelILi0ELi8ELb0ELi16EE\w*",
                           elements=16, pmc_key="act.llama3-8b-block.t512.g20.bf16.b4.asym"),
 }
@@ -268,7 +288,7 @@ def main():
             if not os.path.exists(sfile):
                 subprocess.run(["make", "-s", "-C", CSRC, "isa", f"ISA_SRC={k['src']}"], check=True)
             name, body = function_body(open(sfile).read(), k["fn"])
-            walk = common_path_loop(body, k["elements"])
+            walk = common_path_loop(body, k["elements"], k.get("marker", "v_rndne"))
             loop = (walk[0], None, walk[1]) if walk else hot_loop(body, k["elements"])
             if loop:
                 a0, a1, ops = loop

@@ -118,3 +118,23 @@ def test_search_alpha_markstein_exhaustive():
                          capture_output=True, text=True, timeout=600)
     assert out.returncode == 0, out.stdout + out.stderr
     assert "pairs=2147516416 mismatches=0" in out.stdout
+
+
+def _verify_recip(arg):
+    import os
+    import subprocess
+    subprocess.run(["make", "-s", "-C", os.path.dirname(orc.__file__), "verify_recip"], check=True)
+    return subprocess.run([os.path.join(os.path.dirname(orc.__file__), "verify_recip"), arg],
+                          capture_output=True, text=True, timeout=600)
+
+
+def test_search_packed_fp16_steps_exhaustive():
+    """The clip search's packed-fp16 chains (awq_fast.hip chunk_err_f16p / chunk_err_bf16h):
+    rint + clamp as RN_f16(u + 1024 - qmin) clamped to [1024, 1024 + qmax - qmin] equals
+    clamp(rint(u)) for every fp16 and bf16 u, 4 / 8 bit, sym / asym; and the fp16 quotient must
+    stay double-rounded (RN_f16(RN_f32(x r))): one rounding straight to fp16 misses pairs."""
+    out = _verify_recip("chain16")
+    assert out.returncode == 0, out.stdout + out.stderr
+    assert "cases=515088 mismatches=0" in out.stdout
+    fused = _verify_recip("f16f")
+    assert fused.returncode == 1 and "mismatches=890" in fused.stdout, fused.stdout

@@ -789,6 +789,11 @@ __device__ __forceinline__ float mquot_h(h2v a, float s, float rs) {
 #ifndef AWQ_ACT_MIX_DQ
 #define AWQ_ACT_MIX_DQ 1
 #endif
+//   AWQ_ACT_F16_TAIL    (round 6, later) bf16 / fp16 weights: rint, clamp and the fp16 product in
+//                       packed fp16 (two elements per instruction)
+#ifndef AWQ_ACT_F16_TAIL
+#define AWQ_ACT_F16_TAIL 1
+#endif
 // The table ring's waits are explicit: the compiler's own wait before an LDS read that may
 // alias an LDS-DMA covers every DMA in flight (vmcnt(0)), which would serialise the prefetch,
 // so the ring is read by inline-asm ds_read_b128 it does not track, with explicit lgkmcnt
@@ -985,17 +990,40 @@ __global__ __launch_bounds__(256) void act_loss_kernel(const void* __restrict__ 
                 // integer |.| <= 510, exact in fp16, so only the product is rounded
                 const float sh = (float)(_Float16)cs;
 #if AWQ_ACT_MIX_DQ
-                h2v dqp[EPL / 2];     // (q - z) * sh rounded to fp16, two per register (v_cvt_pk_f16_f32)
+                h2v dqp[EPL / 2];     // (q - z) * sh rounded to fp16, two per register
+                if constexpr (DT != AWQ_DTYPE_F32 && AWQ_ACT_F16_TAIL) {
+                    // bf16 / fp16 u: rint + clamp + (q - z) * s in packed fp16, as the clip search's
+                    // chunk_err_bf16h (u exact in fp16 where it matters; oracle/verify_recip.c
+                    // chain16): RN_f16(u + 1024 - qmin) clamped to [1024, 1024 + qmax - qmin], minus
+                    // 1024 - qmin + z (exact), times the fp16 scale (one rounding of the exact product)
+                    const _Float16 off = (_Float16)(1024 - qmin), hi1 = (_Float16)(1024 + qmax - qmin);
+                    const _Float16 qz1 = off + (_Float16)cz, sh1 = (_Float16)sh;
+                    const h2v offv = {off, off}, lov = {(_Float16)1024, (_Float16)1024}, hiv = {hi1, hi1};
+                    const h2v qzv = {qz1, qz1}, shv = {sh1, sh1};
 #pragma unroll
-                for (int j = 0; j < EPL; j += 2) {
-                    float qq[2];
+                    for (int j = 0; j < EPL; j += 2) {
+                        float uu[2];
 #pragma unroll
-                    for (int u2 = 0; u2 < 2; ++u2) {
-                        const float t = H::quot(ws[j + u2], cs, r);
-                        const float u = sym ? t : H::rn(t + cz);
-                        qq[u2] = __builtin_amdgcn_fmed3f(__builtin_rintf(u), (float)qmin, (float)qmax);
+                        for (int u2 = 0; u2 < 2; ++u2) {
+                            const float t = H::quot(ws[j + u2], cs, r);
+                            uu[u2] = sym ? t : H::rn(t + cz);
+                        }
+                        const h2v uh = __builtin_convertvector((float __attribute__((ext_vector_type(2)))){uu[0], uu[1]}, h2v);
+                        const h2v q = __builtin_elementwise_min(__builtin_elementwise_max(uh + offv, lov), hiv);
+                        dqp[j / 2] = (q - qzv) * shv;
                     }
-                    dqp[j / 2] = (h2v){(_Float16)opq((qq[0] - cz) * sh), (_Float16)opq((qq[1] - cz) * sh)};
+                } else {
+#pragma unroll
+                    for (int j = 0; j < EPL; j += 2) {
+                        float qq[2];
+#pragma unroll
+                        for (int u2 = 0; u2 < 2; ++u2) {
+                            const float t = H::quot(ws[j + u2], cs, r);
+                            const float u = sym ? t : H::rn(t + cz);
+                            qq[u2] = __builtin_amdgcn_fmed3f(__builtin_rintf(u), (float)qmin, (float)qmax);
+                        }
+                        dqp[j / 2] = (h2v){(_Float16)opq((qq[0] - cz) * sh), (_Float16)opq((qq[1] - cz) * sh)};
+                    }
                 }
                 auto dqf = [&](int j) { return (float)dqp[j / 2][j & 1]; };
 #else

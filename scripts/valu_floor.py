@@ -241,7 +241,8 @@ KERNELS = {
     "search.bf16.asym": dict(src="awq_fast", fn=r"_ZN3awq12_GLOBAL__N_115awq_fast_kernelINS0_7FmtBF16ELi4ELb0ELb1ELi128ELb0ELb0EE\w*",
                              elements=32, marker="v_fma_mix_f32", pmc_key="llama3-8b.b4.asym.packed.search10of20"),
     "act.bf16.asym": dict(src="awq_actsearch", fn=r"_ZN3awq12_GLOBAL__N_115act_loss_kernelILi0ELi8ELb0ELi16EE\w*",
-                          elements=16, pmc_key="act.llama3-8b-block.t512.g20.bf16.b4.asym"),
+                          elements=16, marker="v_fma_mix_f32", markers_per_element=2,
+                          pmc_key="act.llama3-8b-block.t512.g20.bf16.b4.asym"),
 }
 
 
@@ -288,7 +289,7 @@ def main():
             if not os.path.exists(sfile):
                 subprocess.run(["make", "-s", "-C", CSRC, "isa", f"ISA_SRC={k['src']}"], check=True)
             name, body = function_body(open(sfile).read(), k["fn"])
-            walk = common_path_loop(body, k["elements"], k.get("marker", "v_rndne"))
+            walk = common_path_loop(body, k["elements"] * k.get("markers_per_element", 1), k.get("marker", "v_rndne"))
             loop = (walk[0], None, walk[1]) if walk else hot_loop(body, k["elements"])
             if loop:
                 a0, a1, ops = loop

@@ -763,6 +763,17 @@ __device__ __forceinline__ float mquot_h(h2v a, float s, float rs) {
     return __builtin_fmaf(r, rs, q0);
 }
 
+// RN_f32(a * r) with a = the low / high fp16 half (v_fma_mix_f32 with a -0 addend: the product's
+// bits, signed zeros included)
+template <bool HI>
+__device__ __forceinline__ float mprod_h(h2v a, float r) {
+    float p;
+    const float nz = -0.0f;
+    if (HI) asm("v_fma_mix_f32 %0, %1, %2, %3 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "=v"(p) : "v"(a), "v"(r), "v"(nz));
+    else asm("v_fma_mix_f32 %0, %1, %2, %3 op_sel_hi:[1,0,0]" : "=v"(p) : "v"(a), "v"(r), "v"(nz));
+    return p;
+}
+
 // LPG: lanes per group as a constant (0 = the run-time lpg argument); SYM: symmetric;
 // EPL: elements per lane — 16 (two consecutive 8-element chunks, LPG = gs / 16 lanes per
 // group) halves the per-candidate group work per element (reductions, RTN parameters, table
@@ -793,6 +804,15 @@ __device__ __forceinline__ float mquot_h(h2v a, float s, float rs) {
 //                       packed fp16 (two elements per instruction)
 #ifndef AWQ_ACT_F16_TAIL
 #define AWQ_ACT_F16_TAIL 1
+#endif
+//   AWQ_ACT_F16_PLAIN   fp16 weights, a wave whose group scales are all < 14: the plain quotient
+#ifndef AWQ_ACT_F16_PLAIN
+#define AWQ_ACT_F16_PLAIN 1
+#endif
+//   AWQ_ACT_F16_PACKED  fp16 weights: w' kept as packed fp16 pairs (min / max, the quotient's
+//                       operand), t and t + z in packed fp16
+#ifndef AWQ_ACT_F16_PACKED
+#define AWQ_ACT_F16_PACKED 1
 #endif
 // The table ring's waits are explicit: the compiler's own wait before an LDS read that may
 // alias an LDS-DMA covers every DMA in flight (vmcnt(0)), which would serialise the prefetch,
@@ -863,6 +883,8 @@ __global__ __launch_bounds__(256) void act_loss_kernel(const void* __restrict__ 
                                                        const float* __restrict__ x_sq, float* __restrict__ part,
                                                        int64_t stride) {
     typedef HwFmt<DT> H;
+    constexpr bool kF16Packed = DT == AWQ_DTYPE_F16 && AWQ_ACT_F16_PACKED && AWQ_ACT_F16_TAIL && AWQ_ACT_MIX_DQ &&
+                                AWQ_ACT_NAN_HOIST;
     const int lpg = LPG ? LPG : lpg_rt;
     constexpr int sym = SYM ? 1 : 0;
     const int64_t G = K / (EPL * lpg);
@@ -940,11 +962,30 @@ __global__ __launch_bounds__(256) void act_loss_kernel(const void* __restrict__ 
             float mn = __builtin_inff(), mx = -__builtin_inff();
 #if AWQ_ACT_NAN_HOIST
             const int nan = nan_w;
+            [[maybe_unused]] h2v wsp[EPL / 2];   // fp16 weights: w' as packed fp16 pairs
+            if constexpr (kF16Packed) {
+                // RN_f16(RN_f32(w s)) two at a time (v_cvt_pk_f16_f32), min / max as v_pk_min_f16 /
+                // v_pk_max_f16 (NaN skipped like fminf / fmaxf; NaN is tracked by nan_w)
 #pragma unroll
-            for (int j = 0; j < EPL; ++j) {
-                ws[j] = H::rn(v[j] * s[j]);
-                mn = __builtin_fminf(mn, ws[j]);
-                mx = __builtin_fmaxf(mx, ws[j]);
+                for (int j = 0; j < EPL; j += 2)
+                    wsp[j / 2] = __builtin_convertvector((f2){opq(v[j] * s[j]), opq(v[j + 1] * s[j + 1])}, h2v);
+                h2v a = wsp[0], b = wsp[0];
+#pragma unroll
+                for (int k = 1; k < EPL / 2; ++k) {
+                    a = __builtin_elementwise_min(a, wsp[k]);
+                    b = __builtin_elementwise_max(b, wsp[k]);
+                }
+                mn = __builtin_fminf((float)a.x, (float)a.y);
+                mx = __builtin_fmaxf((float)b.x, (float)b.y);
+#pragma unroll
+                for (int j = 0; j < EPL; ++j) ws[j] = (float)wsp[j / 2][j & 1];   // (rare paths only)
+            } else {
+#pragma unroll
+                for (int j = 0; j < EPL; ++j) {
+                    ws[j] = H::rn(v[j] * s[j]);
+                    mn = __builtin_fminf(mn, ws[j]);
+                    mx = __builtin_fmaxf(mx, ws[j]);
+                }
             }
             grp_minmax_nn(mn, mx, lpg);
 #else
@@ -1000,17 +1041,55 @@ __global__ __launch_bounds__(256) void act_loss_kernel(const void* __restrict__ 
                     const _Float16 qz1 = off + (_Float16)cz, sh1 = (_Float16)sh;
                     const h2v offv = {off, off}, lov = {(_Float16)1024, (_Float16)1024}, hiv = {hi1, hi1};
                     const h2v qzv = {qz1, qz1}, shv = {sh1, sh1};
+                    if constexpr (kF16Packed) {
+                        // fp16: t from the packed w' directly (v_fma_mix_f32 reads the fp16 halves),
+                        // RN_f16 two at a time, + z as v_pk_add_f16 (RN_f16 of the exact sum: f32's
+                        // 24 bits >= 2 * 11 + 2 make torch's f32-then-fp16 rounding the same)
+                        const _Float16 czh = (_Float16)cz;
+                        const h2v czv = {czh, czh};
+                        auto tail16 = [&](auto plain) {
 #pragma unroll
-                    for (int j = 0; j < EPL; j += 2) {
-                        float uu[2];
+                            for (int k = 0; k < EPL / 2; ++k) {
+                                float p0, p1;
+                                if constexpr (decltype(plain)::value) {
+                                    p0 = mprod_h<false>(wsp[k], r);
+                                    p1 = mprod_h<true>(wsp[k], r);
+                                } else {
+                                    p0 = mquot_h<false>(wsp[k], cs, r);
+                                    p1 = mquot_h<true>(wsp[k], cs, r);
+                                }
+                                const h2v th = __builtin_convertvector((f2){opq(p0), opq(p1)}, h2v);
+                                const h2v uh = sym ? th : th + czv;
+                                const h2v q = __builtin_elementwise_min(__builtin_elementwise_max(uh + offv, lov), hiv);
+                                dqp[k] = (q - qzv) * shv;
+                            }
+                        };
+                        if (AWQ_ACT_F16_PLAIN && __builtin_amdgcn_ballot_w64(!(cs < 14.0f)) == 0)
+                            tail16(std::true_type{});
+                        else
+                            tail16(std::false_type{});
+                    } else {
+                    auto tail = [&](auto plain) {
 #pragma unroll
-                        for (int u2 = 0; u2 < 2; ++u2) {
-                            const float t = H::quot(ws[j + u2], cs, r);
-                            uu[u2] = sym ? t : H::rn(t + cz);
+                        for (int j = 0; j < EPL; j += 2) {
+                            float uu[2];
+#pragma unroll
+                            for (int u2 = 0; u2 < 2; ++u2) {
+                                // fp16, every group of the wave with s < 14: the plain quotient
+                                // RN_f16(RN_f32(w' r)) (oracle/verify_recip.c f16s)
+                                const float t = decltype(plain)::value ? hw_rn_f16(opq(ws[j + u2] * r))
+                                                                       : H::quot(ws[j + u2], cs, r);
+                                uu[u2] = sym ? t : H::rn(t + cz);
+                            }
+                            const h2v uh = __builtin_convertvector((float __attribute__((ext_vector_type(2)))){uu[0], uu[1]}, h2v);
+                            const h2v q = __builtin_elementwise_min(__builtin_elementwise_max(uh + offv, lov), hiv);
+                            dqp[j / 2] = (q - qzv) * shv;
                         }
-                        const h2v uh = __builtin_convertvector((float __attribute__((ext_vector_type(2)))){uu[0], uu[1]}, h2v);
-                        const h2v q = __builtin_elementwise_min(__builtin_elementwise_max(uh + offv, lov), hiv);
-                        dqp[j / 2] = (q - qzv) * shv;
+                    };
+                    if (DT == AWQ_DTYPE_F16 && AWQ_ACT_F16_PLAIN && __builtin_amdgcn_ballot_w64(!(cs < 14.0f)) == 0)
+                        tail(std::true_type{});
+                    else
+                        tail(std::false_type{});
                     }
                 } else {
 #pragma unroll

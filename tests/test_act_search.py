@@ -340,6 +340,38 @@ def test_gpu_losses_bit_exact(dtype, gs, bits, sym):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("bits,sym", [(4, False), (4, True), (8, False)])
+def test_gpu_losses_f16_packed_mixed_scales(bits, sym):
+    """Round 6: the fp16 loss path in packed fp16 (AWQ_ACT_F16_PACKED: w' pairs, the plain
+    quotient in waves whose scales are all < 14, the Markstein one otherwise, t + z as
+    v_pk_add_f16) — rows of small, large (s >= 14), near-constant large-magnitude, subnormal and
+    overflowing (w * s beyond the fp16 range) weights, a NaN, a constant group; the partial losses
+    against the oracle bit for bit."""
+    dev = _gpu()
+    from awq_quantizer import _hip
+    g = torch.Generator().manual_seed(90 + bits + sym)
+    K = 1024
+    w = torch.randn(72, K, generator=g) * 0.02
+    w[8:16] *= 3000.0                                            # s >= 14 groups
+    w[16:24] = 900.0 + torch.randn(8, K, generator=g) * 0.5      # near-constant, large magnitude
+    w[24:32] = 50000.0 + torch.randn(8, K, generator=g) * 30.0   # w * s overflows fp16 for s > ~1.31
+    w[32:40] *= 1e-4                                             # subnormal fp16 weights
+    w[40:48, 128 * 2:128 * 3] *= 5000.0                          # one large group in a small row
+    w[48:56, ::2] = torch.round(w[48:56, ::2] * 256) / 256        # coarse grid: ties
+    w[60, 7] = float("nan")
+    w[61, 256:384] = 0.5                                         # constant group
+    w = w.half()
+    amp = torch.ones(K)
+    amp[torch.randperm(K, generator=g)[: K // 32]] = 30.0
+    x = (torch.randn(200, K, generator=g) * amp).half()
+    xm, xs = orc.act_stats(x)
+    table = _hip.act_scale_table(xm.to(dev), _hip.weight_mean([w.to(dev)], 128), 12)
+    part = _hip.act_search_losses([w.to(dev)], xs.to(dev), table, 128, bits, sym)
+    _, _, opart = orc.act_search_losses([w], xs, table.cpu(), 128, bits, sym)
+    assert torch.equal(part.cpu().view(torch.int32), opart.view(torch.int32))
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("n_grid", [1, 2, 3])
 @pytest.mark.parametrize("dtype,gs", [(torch.bfloat16, 128), (torch.float16, 256), (torch.bfloat16, 32)], ids=str)
 def test_gpu_losses_short_grids(n_grid, dtype, gs):

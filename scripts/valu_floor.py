@@ -15,7 +15,7 @@ the floor: it is amortised over the group (128 elements) and is what the gap nam
 GAP: the kernel's hot loop in the ISA (`make -C awq-converter_amd/csrc isa ISA_SRC=awq_fast` /
 `ISA_SRC=awq_actsearch`), its VALU instructions per element priced the same way and grouped by
 what they do, beside the measured slots per unit (profiles/round6/pmc_valu.json) and the
-per-type VALU counters of the same commands (profiles/round6/r6x/{search,act}_{a,b}).
+per-type VALU counters of the same commands (profiles/round6/r6fa/{search,act}_{a,b}).
 
   python scripts/valu_floor.py [--write profiles/round6/valu_floor.json]
 """
@@ -41,11 +41,13 @@ FLOOR = {
         ("RN(x * r): round to bf16", "v_cvt_pk_bf16_f32 (zero low half)", 1.0, 1.0, "CVT"),
         ("+ z", "v_pk_add_f32", 0.5, 0.5, "ADD_F32"),
         ("RN to bf16", "v_cvt_pk_bf16_f32 (zero low half)", 1.0, 1.0, "CVT"),
-        ("rint (half even)", "v_rndne_f32", 1.0, 1.0, "OTHER"),
-        ("clamp(qmin, qmax)", "v_med3_f32", 1.0, 1.0, "OTHER"),
-        ("q - z (exact)", "v_pk_add_f32", 0.5, 0.5, "ADD_F32"),
-        ("(q - z) * fp16 scale (exact in f32)", "v_pk_mul_f32", 0.5, 0.5, "MUL_F32"),
-        ("RN to fp16 (the reference's fp16 product)", "v_cvt_pk_f16_f32 (2 elements)", 0.5, 0.5, "CVT"),
+        # (round 6: the integer steps in packed fp16, two elements per instruction — cheaper than
+        #  v_rndne + v_med3 + f32 (q - z) * s + v_cvt_pk_f16; exhaustive: verify_recip chain16)
+        ("u to fp16 (exact where it matters)", "v_cvt_pk_f16_f32 (2 elements)", 0.5, 0.5, "CVT"),
+        ("rint (half even): + (1024 - qmin)", "v_pk_add_f16", 0.5, 0.5, "ADD_F16"),
+        ("clamp(1024, 1024 + qmax - qmin)", "v_pk_max_f16 + v_pk_min_f16", 1.0, 1.0, "OTHER"),
+        ("q - z (exact)", "v_pk_add_f16", 0.5, 0.5, "ADD_F16"),
+        ("(q - z) * fp16 scale (the reference's fp16 product)", "v_pk_mul_f16", 0.5, 0.5, "MUL_F16"),
         ("x - dq (fp16 operand)", "v_fma_mix_f32", 1.0, 1.0, "FMA_F32"),
         ("square", "v_pk_mul_f32", 0.5, 0.5, "MUL_F32"),
         ("ordered add (two chunk accumulators per packed add)", "v_pk_add_f32", 0.5, 0.5, "ADD_F32"),
@@ -59,11 +61,11 @@ FLOOR = {
         ("RN to bf16", "v_cvt_pk_bf16_f32 (zero low half)", 1.0, 1.0, "CVT"),
         ("+ z", "v_pk_add_f32", 0.5, 0.5, "ADD_F32"),
         ("RN to bf16", "v_cvt_pk_bf16_f32 (zero low half)", 1.0, 1.0, "CVT"),
-        ("rint (half even)", "v_rndne_f32", 1.0, 1.0, "OTHER"),
-        ("clamp(qmin, qmax)", "v_med3_f32", 1.0, 1.0, "OTHER"),
-        ("q - z (exact)", "v_pk_add_f32", 0.5, 0.5, "ADD_F32"),
-        ("(q - z) * fp16 scale (exact)", "v_pk_mul_f32", 0.5, 0.5, "MUL_F32"),
-        ("RN to fp16", "v_cvt_pk_f16_f32 (2 elements)", 0.5, 0.5, "CVT"),
+        ("u to fp16 (exact where it matters)", "v_cvt_pk_f16_f32 (2 elements)", 0.5, 0.5, "CVT"),
+        ("rint (half even): + (1024 - qmin)", "v_pk_add_f16", 0.5, 0.5, "ADD_F16"),
+        ("clamp(1024, 1024 + qmax - qmin)", "v_pk_max_f16 + v_pk_min_f16", 1.0, 1.0, "OTHER"),
+        ("q - z (exact)", "v_pk_add_f16", 0.5, 0.5, "ADD_F16"),
+        ("(q - z) * fp16 scale", "v_pk_mul_f16", 0.5, 0.5, "MUL_F16"),
         ("dq / s_k: q0 = dq * rs (fp16 operand)", "v_fma_mix_f32", 1.0, 1.0, "FMA_F32"),
         ("dq / s_k: r = fma(-s, q0, dq) (fp16 operand)", "v_fma_mix_f32", 1.0, 1.0, "FMA_F32"),
         ("dq / s_k: fma(r, rs, q0)", "v_pk_fma_f32", 0.5, 0.5, "FMA_F32"),
@@ -73,7 +75,7 @@ FLOOR = {
     ],
 }
 
-# the per-type counter passes of the same bench commands (scripts/cmd/r6x.sh; the A / B counter sets
+# the per-type counter passes of the same bench commands (scripts/cmd/r6fa.sh; the A / B counter sets
 # of scripts/valu_classes.py): dynamic instructions per type for the kernel's launches
 TYPE_PASSES = {"search.bf16.asym": ("search_a", "search_b", "awq_fast_kernel"),
                "act.bf16.asym": ("act_a", "act_b", "act_loss_kernel")}
@@ -249,10 +251,10 @@ KERNELS = {
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "round6", "pmc_valu.json"))
-    ap.add_argument("--types-dir", default="search=" + os.path.join(ROOT, "profiles", "round6", "r6x") + ",act="
-                    + os.path.join(ROOT, "profiles", "round6", "r6n"),
-                    help="kind=dir,...: the per-type counter passes (search_a/b: scripts/cmd/r6x.sh; act_a/b: "
-                         "r6n.sh, after the act kernel's round-6 trims)")
+    ap.add_argument("--types-dir", default="search=" + os.path.join(ROOT, "profiles", "round6", "r6fa") + ",act="
+                    + os.path.join(ROOT, "profiles", "round6", "r6fa"),
+                    help="kind=dir,...: the per-type counter passes (search_a/b, act_a/b: scripts/cmd/r6fa.sh, "
+                         "the final tree)")
     ap.add_argument("--write", default="")
     ap.add_argument("--no-isa", action="store_true", help="floors only (no hipcc)")
     a = ap.parse_args()

@@ -73,7 +73,7 @@ def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     # Llama-3-70B: one launch is ~30 ms, so 20 timed launches are ~0.6 s of kernel time
-    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=60)   # ~1.7 s timed on the 70B set: long enough for a sampling GPU-busy probe
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", default="llama3-70b", choices=sorted(WORKLOADS))
     ap.add_argument("--bits", type=int, default=4, choices=[4, 8])

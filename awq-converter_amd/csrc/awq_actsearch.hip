@@ -814,6 +814,10 @@ __device__ __forceinline__ float mprod_h(h2v a, float r) {
 #ifndef AWQ_ACT_F16_PACKED
 #define AWQ_ACT_F16_PACKED 1
 #endif
+//   AWQ_ACT_PK_F32      bf16 weights: w s, w' r and t + z as v_pk_mul_f32 / v_pk_add_f32 pairs
+#ifndef AWQ_ACT_PK_F32
+#define AWQ_ACT_PK_F32 1
+#endif
 // The table ring's waits are explicit: the compiler's own wait before an LDS read that may
 // alias an LDS-DMA covers every DMA in flight (vmcnt(0)), which would serialise the prefetch,
 // so the ring is read by inline-asm ds_read_b128 it does not track, with explicit lgkmcnt
@@ -877,7 +881,7 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t act_rsrc(const void* base, uin
 }
 
 template <int DT, int LPG, bool SYM, int EPL>
-__global__ __launch_bounds__(256) void act_loss_kernel(const void* __restrict__ w, int64_t R, int64_t K, int lpg_rt,
+__global__ __launch_bounds__(256, 3) void act_loss_kernel(const void* __restrict__ w, int64_t R, int64_t K, int lpg_rt,
                                                        int qmin, int qmax, const float* __restrict__ table,
                                                        const float* __restrict__ rtable, int n_grid,
                                                        const float* __restrict__ x_sq, float* __restrict__ part,
@@ -979,6 +983,19 @@ __global__ __launch_bounds__(256) void act_loss_kernel(const void* __restrict__ 
                 mx = __builtin_fmaxf((float)b.x, (float)b.y);
 #pragma unroll
                 for (int j = 0; j < EPL; ++j) ws[j] = (float)wsp[j / 2][j & 1];   // (rare paths only)
+            } else if constexpr (DT == AWQ_DTYPE_BF16 && AWQ_ACT_PK_F32 >= 2) {
+                // the products two at a time (v_pk_mul_f32: the same IEEE ops in one instruction)
+#pragma unroll
+                for (int j = 0; j < EPL; j += 2) {
+                    const f2 p = (f2){v[j], v[j + 1]} * (f2){s[j], s[j + 1]};
+                    ws[j] = H::rn(p.x);
+                    ws[j + 1] = H::rn(p.y);
+                }
+#pragma unroll
+                for (int j = 0; j < EPL; ++j) {
+                    mn = __builtin_fminf(mn, ws[j]);
+                    mx = __builtin_fmaxf(mx, ws[j]);
+                }
             } else {
 #pragma unroll
                 for (int j = 0; j < EPL; ++j) {
@@ -1073,13 +1090,23 @@ __global__ __launch_bounds__(256) void act_loss_kernel(const void* __restrict__ 
 #pragma unroll
                         for (int j = 0; j < EPL; j += 2) {
                             float uu[2];
+                            if constexpr (DT == AWQ_DTYPE_BF16 && AWQ_ACT_PK_F32) {
+                                // bf16: RN(w' r) and RN(t + z) as packed pairs (v_pk_mul_f32 /
+                                // v_pk_add_f32, each half the IEEE op)
+                                const f2 p = (f2){ws[j], ws[j + 1]} * (f2){r, r};
+                                const float t0 = H::rn(p.x), t1 = H::rn(p.y);
+                                const f2 a = (f2){t0, t1} + (f2){cz, cz};
+                                uu[0] = sym ? t0 : H::rn(a.x);
+                                uu[1] = sym ? t1 : H::rn(a.y);
+                            } else {
 #pragma unroll
-                            for (int u2 = 0; u2 < 2; ++u2) {
-                                // fp16, every group of the wave with s < 14: the plain quotient
-                                // RN_f16(RN_f32(w' r)) (oracle/verify_recip.c f16s)
-                                const float t = decltype(plain)::value ? hw_rn_f16(opq(ws[j + u2] * r))
-                                                                       : H::quot(ws[j + u2], cs, r);
-                                uu[u2] = sym ? t : H::rn(t + cz);
+                                for (int u2 = 0; u2 < 2; ++u2) {
+                                    // fp16, every group of the wave with s < 14: the plain quotient
+                                    // RN_f16(RN_f32(w' r)) (oracle/verify_recip.c f16s)
+                                    const float t = decltype(plain)::value ? hw_rn_f16(opq(ws[j + u2] * r))
+                                                                           : H::quot(ws[j + u2], cs, r);
+                                    uu[u2] = sym ? t : H::rn(t + cz);
+                                }
                             }
                             const h2v uh = __builtin_convertvector((float __attribute__((ext_vector_type(2)))){uu[0], uu[1]}, h2v);
                             const h2v q = __builtin_elementwise_min(__builtin_elementwise_max(uh + offv, lov), hiv);

@@ -227,6 +227,10 @@ __device__ __forceinline__ float grp_sum_scatter(const float (&e)[4]) {
 #ifndef AWQ_SEARCH_BF16_HALF
 #define AWQ_SEARCH_BF16_HALF 1
 #endif
+// AWQ_SEARCH_PK_F32 = 0: the bf16 chain's products and + z as plain f32 ops (compiler's choice)
+#ifndef AWQ_SEARCH_PK_F32
+#define AWQ_SEARCH_PK_F32 1
+#endif
 // waves per SIMD the search instances are compiled for (the VGPR budget: 4 -> 128, 5 -> 96, 6 -> 80)
 #ifndef AWQ_SEARCH_MIN_WAVES
 #define AWQ_SEARCH_MIN_WAVES 4
@@ -369,8 +373,17 @@ __device__ __forceinline__ float chunk_err_bf16h(const Chunk<1>& v, float r, flo
     for (int i = 0; i < 4; ++i) {
         const uint32_t w = v.w[0][i];
         const float x0 = FmtBF16::lo(w), x1 = FmtBF16::hi(w);
+#if AWQ_SEARCH_PK_F32
+        // the pair's product and + z as one v_pk_mul_f32 / v_pk_add_f32 each (the same IEEE ops;
+        // two plain VOP2 ops only cost one slot when they dual-issue, ~11 % of the time here)
+        const f2 p = pk_mul(f2{x0, x1}, f2{r, r});
+        const float t0 = rn_bf16(p.x), t1 = rn_bf16(p.y);
+        const f2 a = SYM ? f2{t0, t1} : pk_add(f2{t0, t1}, f2{z, z});
+        const float u0 = SYM ? t0 : rn_bf16(a.x), u1 = SYM ? t1 : rn_bf16(a.y);
+#else
         const float t0 = rn_bf16(x0 * r), t1 = rn_bf16(x1 * r);
         const float u0 = SYM ? t0 : rn_bf16(t0 + z), u1 = SYM ? t1 : rn_bf16(t1 + z);
+#endif
         const h2v u = __builtin_convertvector((f2){u0, u1}, h2v);
         const h2v q = __builtin_elementwise_min(__builtin_elementwise_max(u + off, lo), hi);
         const h2v dq = (q - qz) * ss;

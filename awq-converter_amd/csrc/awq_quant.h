@@ -28,6 +28,9 @@ namespace {
 typedef short s2 __attribute__((ext_vector_type(2)));
 typedef unsigned short us2 __attribute__((ext_vector_type(2)));
 typedef float f2 __attribute__((ext_vector_type(2)));
+// two-element f32 ops (v_pk_mul_f32 / v_pk_add_f32 where the compiler keeps the pair packed)
+__device__ __forceinline__ f2 pk_mul(f2 a, f2 b) { return a * b; }
+__device__ __forceinline__ f2 pk_add(f2 a, f2 b) { return a + b; }
 typedef __bf16 b2 __attribute__((ext_vector_type(2)));
 typedef uint32_t u4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u2v __attribute__((ext_vector_type(2)));

@@ -333,7 +333,13 @@ __device__ __forceinline__ float chunk_err_f16p(const Chunk<1>& v, float r, uint
     for (int i = 0; i < 4; ++i) {
         const uint32_t w = v.w[0][i];
         const float x0 = FmtF16::lo(w), x1 = FmtF16::hi(w);
+#if AWQ_SEARCH_PK_F32
+        f2 p = pk_mul(f2{x0, x1}, f2{r, r});     // one v_pk_mul_f32; the barrier keeps it f32-rounded
+        asm volatile("" : "+v"(p));
+        const h2v t = __builtin_convertvector(p, h2v);                                     // RN_f16(RN_f32(x r))
+#else
         const h2v t = __builtin_convertvector((f2){opaque(x0 * r), opaque(x1 * r)}, h2v);   // RN_f16(RN_f32(x r))
+#endif
         const h2v u = SYM ? t : t + zz;                                                    // RN_f16(t + z)
         const h2v q = __builtin_elementwise_min(__builtin_elementwise_max(u + off, lo), hi);   // 1024 + q - qmin
         const h2v dq = (q - qz) * ss;                                                      // RN_f16((q - z) s)

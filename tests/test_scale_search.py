@@ -193,6 +193,30 @@ def test_search_gpu_f16_packed_chain_mixed_scales(bits, sym):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("n_grid", [65536, 65537, 100000])
+def test_search_gpu_large_grids_alpha(dtype, n_grid):
+    """Round 6: alpha_i = (n - i) / n by one Markstein correction for n <= 65536 (exhaustively the
+    IEEE quotient, verify_recip alpha) and by the IEEE division beyond — both sides of the switch
+    against the oracle, with candidates whose shrink still moves bf16 / fp16 extremes."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from awq_quantizer.quantization import AWQQuantizer
+    g = torch.Generator().manual_seed(n_grid % 97)
+    x = (torch.randn(16, 1024, generator=g) * 0.05).to(dtype)
+    x[0, 3] = 2.0
+    shrink = 300.0 / n_grid                     # 300 candidates: alpha down to ~0.995 .. 0.997
+    q = AWQQuantizer(bits=4, group_size=128, symmetric=False, scale_method="search", search_grid=n_grid,
+                     search_max_shrink=shrink, device="cuda", logger_level="ERROR")
+    n_cand = min(n_grid, max(1, int(shrink * n_grid)))
+    ref = orc.quantize(x, bits=4, group_size=128, symmetric=False, search=(n_grid, n_cand))
+    res = q.quantize(x)
+    assert torch.equal(res["tensor_q"], ref["tensor_q"])
+    assert torch.equal(res["zero_points"], ref["zero_points"])
+    assert gio.same_bits(res["scales"], ref["scales"])
+
+
+@pytest.mark.gpu
 def test_search_gpu_special_values_and_rtn_identity():
     if not torch.cuda.is_available():
         pytest.skip("no GPU")

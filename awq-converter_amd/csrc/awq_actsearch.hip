@@ -186,12 +186,44 @@ __device__ __forceinline__ void grp_minmax(float& mn, float& mx, int& nan, int l
     if (lpg >= 64) minmax_cross<true>(mn, mx, nan);
 }
 
+// v_min_f32 / v_max_f32 with the partner lane's operand through DPP, one instruction per step
+// (the compiler turns min2 / max2 into v_min / v_max behind a canonicalising v_max x, x and a
+// separate v_mov_dpp: three).  The s_nop covers the VALU-write -> DPP-read wait states (the
+// operand may have been written by the instruction just before).  No NaN reaches these (the
+// weights' NaN flag is tracked on the side), and the sign of a zero extreme cannot change the
+// scale or zero point.
+#define AWQ_DPP_MINMAX(NAME, OP, CTRL)                                                                   \
+    __device__ __forceinline__ float NAME(float v) {                                                    \
+        float r;                                                                                        \
+        asm("s_nop 1\n\t" OP "_dpp %0, %1, %1 " CTRL " row_mask:0xf bank_mask:0xf bound_ctrl:1" : "=v"(r) : "v"(v)); \
+        return r;                                                                                       \
+    }
+AWQ_DPP_MINMAX(min_xor1, "v_min_f32", "quad_perm:[1,0,3,2]")
+AWQ_DPP_MINMAX(max_xor1, "v_max_f32", "quad_perm:[1,0,3,2]")
+AWQ_DPP_MINMAX(min_xor2, "v_min_f32", "quad_perm:[2,3,0,1]")
+AWQ_DPP_MINMAX(max_xor2, "v_max_f32", "quad_perm:[2,3,0,1]")
+AWQ_DPP_MINMAX(min_hmir, "v_min_f32", "row_half_mirror")
+AWQ_DPP_MINMAX(max_hmir, "v_max_f32", "row_half_mirror")
+AWQ_DPP_MINMAX(min_mir, "v_min_f32", "row_mirror")
+AWQ_DPP_MINMAX(max_mir, "v_max_f32", "row_mirror")
+#undef AWQ_DPP_MINMAX
+#ifndef AWQ_ACT_DPP_MINMAX
+#define AWQ_ACT_DPP_MINMAX 1
+#endif
+
 // the group min / max alone (the weights' NaN flag is reduced once per item: grp_or)
 __device__ __forceinline__ void grp_minmax_nn(float& mn, float& mx, int lpg) {
+#if AWQ_ACT_DPP_MINMAX
+    if (lpg >= 2) { mn = min_xor1(mn); mx = max_xor1(mx); }
+    if (lpg >= 4) { mn = min_xor2(mn); mx = max_xor2(mx); }
+    if (lpg >= 8) { mn = min_hmir(mn); mx = max_hmir(mx); }
+    if (lpg >= 16) { mn = min_mir(mn); mx = max_mir(mx); }
+#else
     if (lpg >= 2) { mn = min2(mn, dppf<0xB1>(mn)); mx = max2(mx, dppf<0xB1>(mx)); }
     if (lpg >= 4) { mn = min2(mn, dppf<0x4E>(mn)); mx = max2(mx, dppf<0x4E>(mx)); }
     if (lpg >= 8) { mn = min2(mn, dppf<0x141>(mn)); mx = max2(mx, dppf<0x141>(mx)); }
     if (lpg >= 16) { mn = min2(mn, dppf<0x140>(mn)); mx = max2(mx, dppf<0x140>(mx)); }
+#endif
     if (lpg >= 32) {
         int dummy = 0;
         minmax_cross<false>(mn, mx, dummy);

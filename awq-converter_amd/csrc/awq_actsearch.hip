@@ -897,6 +897,52 @@ __device__ __forceinline__ void lds_slot_s(uint32_t a, float (&s)[EPL], f4v (&rp
 #pragma unroll
         for (int e = 0; e < 4; ++e) s[4 * q + e] = t[q][e];
 }
+// EPL 16 with AWQ_ACT_RS_PAIRS: the reciprocals read as (j, j + 8) pairs by ds_read2_b32 — the
+// register pairs the loss's packed ops want (the two 8-element chunks go through v_pk_fma_f32 /
+// v_pk_add_f32 side by side), instead of four ds_read_b128 and a v_mov per element to re-pair them
+#ifndef AWQ_ACT_RS_PAIRS
+#define AWQ_ACT_RS_PAIRS 1
+#endif
+template <int O0, int O1>
+__device__ __forceinline__ f2 lds_read2(uint32_t a) {
+    f2 t;
+    asm volatile("ds_read2_b32 %0, %1 offset0:%2 offset1:%3" : "=v"(t) : "v"(a), "n"(O0), "n"(O1) : "memory");
+    return t;
+}
+template <int GSZ>
+__device__ __forceinline__ void lds_slot_s_pairs(uint32_t a, float (&s)[16], f2 (&rq)[8]) {
+    f4v t[4];
+    t[0] = lds_read4<0>(a);
+    t[1] = lds_read4<16>(a);
+    t[2] = lds_read4<32>(a);
+    t[3] = lds_read4<48>(a);
+    const uint32_t b = a + 4 * GSZ;                      // the reciprocal row (dword offsets <= 15)
+    rq[0] = lds_read2<0, 8>(b);
+    rq[1] = lds_read2<1, 9>(b);
+    rq[2] = lds_read2<2, 10>(b);
+    rq[3] = lds_read2<3, 11>(b);
+    rq[4] = lds_read2<4, 12>(b);
+    rq[5] = lds_read2<5, 13>(b);
+    rq[6] = lds_read2<6, 14>(b);
+    rq[7] = lds_read2<7, 15>(b);
+    asm volatile("s_waitcnt lgkmcnt(8)" : "+v"(t[0]), "+v"(t[1]), "+v"(t[2]), "+v"(t[3]) : : "memory");
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) s[4 * q + e] = t[q][e];
+}
+__device__ __forceinline__ void lds_slot_rs_pairs(f2 (&rq)[8], float (&rs)[16]) {
+    asm volatile("s_waitcnt lgkmcnt(0)"
+                 : "+v"(rq[0]), "+v"(rq[1]), "+v"(rq[2]), "+v"(rq[3]), "+v"(rq[4]), "+v"(rq[5]), "+v"(rq[6]), "+v"(rq[7])
+                 :
+                 : "memory");
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        rs[k] = rq[k].x;
+        rs[k + 8] = rq[k].y;
+    }
+}
+
 template <int EPL>
 __device__ __forceinline__ void lds_slot_rs(f4v (&rp)[EPL / 4], float (&rs)[EPL]) {
     if constexpr (EPL == 16)
@@ -981,12 +1027,17 @@ __global__ __launch_bounds__(256, 3) void act_loss_kernel(const void* __restrict
             float s[EPL], ws[EPL];
             float rs[EPL];
             f4v rp[EPL / 4];
+            [[maybe_unused]] f2 rsp[8];   // (j, j + 8) reciprocal pairs
+            constexpr bool kPairs = EPL == 16 && AWQ_ACT_RS_PAIRS;
             if constexpr (kLds) {
                 // slot i & 1 holds candidate i once every operation but the previous
                 // candidate's store is done (i = 0: the item's loads and first DMA)
                 if (i == 0) vm_wait<0>();
                 else vm_wait<1>();
-                lds_slot_s<EPL, GSZ>(lds_addr(cw + (i & 1) * 2 * GSZ), s, rp);   // (rp unused without rtable)
+                if constexpr (kPairs)
+                    lds_slot_s_pairs<GSZ>(lds_addr(cw + (i & 1) * 2 * GSZ), *(float(*)[16]) & s, rsp);
+                else
+                    lds_slot_s<EPL, GSZ>(lds_addr(cw + (i & 1) * 2 * GSZ), s, rp);   // (rp unused without rtable)
                 dma(gl.g, i + 1 < n_grid ? i + 1 : i, (i + 1) & 1);   // (last: a harmless reload)
             } else {
 #pragma unroll
@@ -1058,7 +1109,10 @@ __global__ __launch_bounds__(256, 3) void act_loss_kernel(const void* __restrict
             bool mq = false;
             // (the ring's reciprocal reads are waited for with or without a reciprocal table:
             //  registers an asm load is still writing must not be reused)
-            if constexpr (kLds) lds_slot_rs<EPL>(rp, rs);
+            if constexpr (kLds) {
+                if constexpr (kPairs) lds_slot_rs_pairs(rsp, *(float(*)[16]) & rs);
+                else lds_slot_rs<EPL>(rp, rs);
+            }
             if (rtable != nullptr) {
                 if constexpr (!kLds) {
 #pragma unroll

@@ -40,7 +40,7 @@ _OUT_OF_ORDER = re.compile(r"(s_load_|s_buffer_load_|s_scratch_load_|s_memtime|s
 
 def ring_violations(asm: str, func_rx: str):
     """(function, line, instruction) for every instruction that touches a register an
-    inline-asm ds_read_b128 is still loading.  Every LGKM-counted instruction is modelled, not
+    inline-asm ds_read_b128 / ds_read2_b32 is still loading.  Every LGKM-counted instruction is modelled, not
     only the asm reads: s_waitcnt lgkmcnt(N) waits until at most N of them are outstanding, so
     at most N LDS operations are — and since LDS operations complete in issue order, everything
     but the N youngest LDS operations (compiler ds_* included) is done.  An outstanding SMEM /
@@ -72,7 +72,7 @@ def ring_violations(asm: str, func_rx: str):
             op = s.split()[0]
             live = set().union(*lds) if lds else set()
             if _LDS.fullmatch(op):
-                m = re.match(r"ds_read_b128 (v\[\d+:\d+\]), v\d+", s)
+                m = re.match(r"ds_read(?:_b128|2_b32) (v\[\d+:\d+\]), v\d+", s)
                 if live & _regs(s):
                     bad.append((f, n, s))
                 lds.append(_regs(m.group(1)) if (m and in_asm) else set())

@@ -218,6 +218,9 @@ __device__ __forceinline__ void grp_minmax_nn(float& mn, float& mx, int lpg) {
     if (lpg >= 4) { mn = min_xor2(mn); mx = max_xor2(mx); }
     if (lpg >= 8) { mn = min_hmir(mn); mx = max_hmir(mx); }
     if (lpg >= 16) { mn = min_mir(mn); mx = max_mir(mx); }
+    // the compiler's hazard tracking does not see into the asm: wait states before the cross-row
+    // swaps below read its results
+    if (lpg >= 32) asm volatile("s_nop 1" : "+v"(mn), "+v"(mx));
 #else
     if (lpg >= 2) { mn = min2(mn, dppf<0xB1>(mn)); mx = max2(mx, dppf<0xB1>(mx)); }
     if (lpg >= 4) { mn = min2(mn, dppf<0x4E>(mn)); mx = max2(mx, dppf<0x4E>(mx)); }

@@ -252,9 +252,9 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "round6", "pmc_valu.json"))
     ap.add_argument("--types-dir", default="search=" + os.path.join(ROOT, "profiles", "round6", "r6fe") + ",act="
-                    + os.path.join(ROOT, "profiles", "round6", "r6fe"),
-                    help="kind=dir,...: the per-type counter passes (search_a/b, act_a/b: scripts/cmd/r6fe.sh, "
-                         "the final tree)")
+                    + os.path.join(ROOT, "profiles", "round6", "r6fg"),
+                    help="kind=dir,...: the per-type counter passes (search_a/b: scripts/cmd/r6fe.sh, act_a/b: "
+                         "r6fg.sh, the final tree)")
     ap.add_argument("--write", default="")
     ap.add_argument("--no-isa", action="store_true", help="floors only (no hipcc)")
     a = ap.parse_args()

@@ -1009,6 +1009,7 @@ def main(argv: Optional[List[str]] = None) -> int:
             return 1
         TIMINGS["total_s"] = time.time() - start
         logger.info(f"Quantization complete in {time.time() - start:.2f} seconds")
+        logger.info("metrics " + json.dumps(run_metrics(ordered, quantized, TIMINGS)))
         return 0
     except SystemExit:
         raise
@@ -1018,6 +1019,18 @@ def main(argv: Optional[List[str]] = None) -> int:
         else:
             logger.error(f"Error during quantization: {e}")
         return 1
+
+
+def run_metrics(ordered, quantized, timings) -> Dict[str, float]:
+    """One JSON line per run (SURVEY.md §5 metrics): tensors quantized, their input bytes, the
+    quantize phase (read + H2D + kernels + D2H, overlapped) and the whole run incl. the final
+    writes, and the end-to-end rate over the input bytes.  (Not the kernel's roofline: that is
+    bench.py's, with inputs resident in HBM.)"""
+    nbytes = sum(i.nbytes for i in ordered if i.name in quantized)
+    total = max(float(timings.get("total_s", 0.0)), 1e-9)
+    return {"tensors": len(quantized), "input_bytes": int(nbytes),
+            "quantize_s": round(float(timings.get("quantize_s", 0.0)), 4), "total_s": round(total, 4),
+            "input_GB_per_s": round(nbytes / total / 1e9, 3)}
 
 
 _SCALARS = ("bits", "group_size", "symmetric", "shape")
@@ -1116,6 +1129,8 @@ def _main_distributed(args, loader, ordered: List[TensorInfo], logger, start: fl
         dist.destroy_process_group()
     if rank == 0 and rc == 0:
         logger.info(f"Quantization complete in {time.time() - start:.2f} seconds")
+        TIMINGS["total_s"] = time.time() - start
+        logger.info("metrics " + json.dumps(dict(run_metrics(ordered, {i.name for i in ordered}, TIMINGS), world=world)))
     return rc
 
 

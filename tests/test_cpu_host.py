@@ -246,3 +246,16 @@ def test_abi17_argument_validation_without_gpu():
     assert lib.awq_dequant_ceiling(P, P, 24, null) != 0 and "multiple of 16" in _hip.last_error()
     assert lib.awq_dequant_ceiling(ctypes.c_void_p(66), P, 32, null) != 0 and "misaligned" in _hip.last_error()
     assert lib.awq_dequant_ceiling(null, null, 0, null) == 0
+
+
+def test_cli_run_metrics_line():
+    """The CLI's per-run JSON metrics line (main.run_metrics): the quantized tensors' input
+    bytes over the run's wall time."""
+    from awq_quantizer.main import run_metrics
+    from awq_quantizer.model_loading.safetensors_loader import TensorInfo
+    ordered = [TensorInfo("a", "f", torch.bfloat16, (4, 256)), TensorInfo("b", "f", torch.float16, (8,)),
+               TensorInfo("c", "f", torch.float32, (2, 128))]
+    m = run_metrics(ordered, {"a": {}, "c": {}}, {"quantize_s": 0.25, "total_s": 0.5})
+    assert m["tensors"] == 2 and m["input_bytes"] == 4 * 256 * 2 + 2 * 128 * 4
+    assert m["quantize_s"] == 0.25 and m["total_s"] == 0.5
+    assert m["input_GB_per_s"] == round(m["input_bytes"] / 0.5 / 1e9, 3)

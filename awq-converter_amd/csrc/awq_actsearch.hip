@@ -66,8 +66,33 @@ template <> struct HwFmt<AWQ_DTYPE_BF16> {
         return hw_rn_bf16(x * r);
     }
 };
+// AWQ_F16_PARAMS_FAST = 0: the fp16 group parameters by IEEE divisions (as csrc/awq_quant.h)
+#ifndef AWQ_F16_PARAMS_FAST
+#define AWQ_F16_PARAMS_FAST 1
+#endif
+// rcp + one Newton step: IEEE 1/s for every positive finite fp16 s (awq_selftest 2)
+__device__ __forceinline__ float recip_f16(float s) {
+    if (__builtin_expect(!(s > 0.0f && s < __builtin_inff()), 0)) return 1.0f / s;
+    const float r0 = __builtin_amdgcn_rcpf(s);
+    const float e = __builtin_fmaf(-s, r0, 1.0f);
+    return __builtin_fmaf(r0, e, r0);
+}
 template <> struct HwFmt<AWQ_DTYPE_F16> {
     __device__ static float lo() { return 0.0f; }                           // RN_f16(1e-10) = 0
+#if AWQ_F16_PARAMS_FAST
+    // RN_f16(d / qr) == RN_f16(d * RN_f32(1/qr)), every non-negative fp16 d incl. inf
+    // (oracle/verify_recip.c f16scale)
+    __device__ static float scale(float d, float qr, float rq) {
+        (void)qr;
+        return hw_rn_f16(opq(hw_rn_f16(d)) * rq);
+    }
+    __device__ static float recip(float s) { return recip_f16(s); }
+    // the Markstein quotient for a positive finite s (verify_recip f16m), IEEE otherwise
+    __device__ static float quot_any(float x, float s, float r) {
+        if (__builtin_expect(!(s > 0.0f && s < __builtin_inff()), 0)) return hw_rn_f16(opq(x) / s);
+        return quot(x, s, r);
+    }
+#else
     __device__ static float scale(float d, float qr, float rq) {   // IEEE: d may be inf (Markstein would NaN)
         (void)rq;
         return hw_rn_f16(opq(d) / qr);
@@ -77,6 +102,7 @@ template <> struct HwFmt<AWQ_DTYPE_F16> {
         (void)r;
         return hw_rn_f16(opq(x) / s);
     }
+#endif
     __device__ static float rn(float a) { return hw_rn_f16(a); }
     // Markstein-corrected quotient, exact for every fp16 x and positive finite fp16 s
     // (oracle/verify_recip.c f16m)

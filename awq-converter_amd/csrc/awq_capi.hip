@@ -587,7 +587,7 @@ int awq_selftest(int which, unsigned long long* result, void* stream) {
     g_err.clear();
     if (!result) return fail(AWQ_EINVAL, "null result pointer");
     if (which == 1) return hip_status(awq::launch_selftest_mquot(result, (hipStream_t)stream), "awq selftest");
-    if (which != 0) return fail(AWQ_EINVAL, "unknown self-test %d", which);
+    if (which != 0 && which != 2) return fail(AWQ_EINVAL, "unknown self-test %d", which);
     return hip_status(awq::launch_selftest(which, result, (hipStream_t)stream), "awq selftest");
 }
 

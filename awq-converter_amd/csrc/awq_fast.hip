@@ -873,6 +873,16 @@ __global__ void awq_selftest_recip_kernel(unsigned long long* mismatches) {
         atomicAdd(mismatches, 1ull);
 }
 
+// which = 2: recip_f16 over every positive finite fp16 s against the IEEE division (bitwise)
+__global__ void awq_selftest_recip16_kernel(unsigned long long* mismatches) {
+    const uint32_t h = blockIdx.x * blockDim.x + threadIdx.x;
+    if (h == 0 || h >= 0x7C00u) return;
+    const float s = (float)__builtin_bit_cast(_Float16, (uint16_t)h);
+    const float a = recip_f16(s);
+    const float b = 1.0f / s;
+    if (__float_as_uint(a) != __float_as_uint(b)) atomicAdd(mismatches, 1ull);
+}
+
 }  // namespace
 
 hipError_t launch_fast(const awq_tensor_desc* descs_dev, const int32_t* block_tensor,
@@ -1003,6 +1013,10 @@ hipError_t launch_stream_ceiling(const void* src, void* dst, int64_t bytes, hipS
 }
 
 hipError_t launch_selftest(int which, unsigned long long* out, hipStream_t stream) {
+    if (which == 2) {
+        hipLaunchKernelGGL(awq_selftest_recip16_kernel, dim3(0x7C00 / 256), dim3(256), 0, stream, out);
+        return hipPeekAtLastError();
+    }
     if (which != 0) return hipErrorInvalidValue;
     hipLaunchKernelGGL(awq_selftest_recip_kernel, dim3(0x8000 / 256), dim3(256), 0, stream, out);
     return hipPeekAtLastError();

@@ -99,6 +99,14 @@ __device__ __forceinline__ float recip_bf16(float s) {
     const float e = __builtin_fmaf(-s, r0, 1.0f);
     return __builtin_fmaf(r0, e, r0);
 }
+// The same for an fp16-valued s: correctly rounded for every positive finite fp16 s (all 31 743,
+// awq_selftest 2 on the GPU); 0, inf and NaN go through the IEEE division.
+__device__ __forceinline__ float recip_f16(float s) {
+    if (__builtin_expect(!(s > 0.0f && s < __builtin_inff()), 0)) return 1.0f / s;
+    const float r0 = __builtin_amdgcn_rcpf(s);
+    const float e = __builtin_fmaf(-s, r0, 1.0f);
+    return __builtin_fmaf(r0, e, r0);
+}
 
 // ---- input formats ----------------------------------------------------------------
 // All are sign-magnitude floats, so the raw-bits min/max below works for each.  They
@@ -184,6 +192,11 @@ __device__ __forceinline__ float opaque_s(float a) {
     return a;
 }
 
+// AWQ_F16_PARAMS_FAST = 0: the fp16 group parameters by IEEE divisions (scale, reciprocal, zero
+// point) as before round 6's last trims
+#ifndef AWQ_F16_PARAMS_FAST
+#define AWQ_F16_PARAMS_FAST 1
+#endif
 struct FmtF16 {
     static constexpr int NW = 1, kBytes = 2;
     static constexpr bool kWide = false;
@@ -209,6 +222,20 @@ struct FmtF16 {
         // RN_f32 first, as verified: a fused fma -> f16 (v_fma_mixlo_f16) rounds once
         return rn(opaque(__builtin_fmaf(e, r, q0)));
     }
+#if AWQ_F16_PARAMS_FAST
+    // RN_f16(d / qr) == RN_f16(d * RN_f32(1/qr)) for every non-negative fp16 d, inf included, and
+    // qr = 2^bits - 1 (oracle/verify_recip.c f16scale); d * (1/qr) folds to a multiply by a constant
+    __device__ static float scale(float d, float qr) { return rn(opaque(rn(d)) * (1.0f / qr)); }
+    __device__ static float lo_clamp() { return 0.0f; }                            // RN_f16(1e-10) = 0
+    __device__ static float recip(float s) { return recip_f16(s); }
+    // RN(x / s): the Markstein quotient (exact for every fp16 x and positive finite fp16 s,
+    // verify_recip f16m, with r the IEEE reciprocal recip_f16 returns) — the IEEE division only
+    // for s = 0 / inf / NaN, in a branch the wave skips when no lane needs it
+    __device__ static float quot_any(float x, float s, float r) {
+        if (__builtin_expect(!(s > 0.0f && s < __builtin_inff()), 0)) return rn(opaque(x) / s);
+        return quot(x, s, r);
+    }
+#else
     __device__ static float scale(float d, float qr) { return rn(opaque(rn(d)) / qr); }   // IEEE division
     __device__ static float lo_clamp() { return 0.0f; }                            // RN_f16(1e-10) = 0
     __device__ static float recip(float s) { return 1.0f / s; }
@@ -216,6 +243,7 @@ struct FmtF16 {
         (void)r;
         return rn(opaque(x) / s);
     }
+#endif
     // s = 0 (constant group: the fp16 clamp min is 0), inf or NaN -> exact special path
     __device__ static bool fast(float r) { return r > 0.0f && r < __builtin_inff(); }
     // The plain RN_f16(RN_f32(x * RN_f32(1/s))) misses RN_f16(x / s) only for scales

@@ -542,8 +542,9 @@ int awq_apply_input_scale(const void* w, int dtype, int64_t rows, int64_t K, con
 /* Device self-test (diagnostics).  which = 0: the fast reciprocal used by the streaming
  * kernel against IEEE 1/s over every bf16 s >= RN_bf16(1e-10); which = 1: the loss kernel's
  * Markstein quotient against the IEEE division for every s in [1, 2) and every positive
- * finite fp16 dividend; adds the number of mismatches to *result (device unsigned long
- * long, caller-zeroed). */
+ * finite fp16 dividend; which = 2: the fp16 reciprocal (rcp + one Newton step) against IEEE
+ * 1/s over every positive finite fp16 s; adds the number of mismatches to *result (device
+ * unsigned long long, caller-zeroed). */
 int awq_selftest(int which, unsigned long long* result, void* stream);
 
 #ifdef __cplusplus

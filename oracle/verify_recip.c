@@ -8,7 +8,7 @@
  * reproduces awq.py:245's `tensor / scale` (torch bf16 divide = fp32 divide + RNE)
  * and awq.py:210's `t_min / scale` bit for bit.  Also reports the fp16 analogue
  * (expected to FAIL, which is why fp16 inputs use a true division).
- * Usage: verify_recip [bf16|f16|f16m|f16s|f16f|chain16|alpha] -> prints mismatches, exit 0 iff none (bf16;
+ * Usage: verify_recip [bf16|f16|f16m|f16s|f16f|chain16|f16scale|alpha] -> prints mismatches, exit 0 iff none (bf16;
  * f16m: the fp16 Markstein-corrected quotient; f16s: the fp16 plain product for s < 14;
  * f16f: the same product rounded once, straight to fp16; chain16: the search's packed-fp16 rint
  * and clamp; alpha: the search's candidate factor). */
@@ -152,6 +152,25 @@ static int check_chain16(void) {
     return mismatches == 0 ? 0 : 1;
 }
 
+/* fp16 scale without the IEEE division (csrc/awq_quant.h FmtF16::scale, act HwFmt<F16>::scale):
+ * RN_f16(d / qr) == RN_f16(d * RN_f32(1 / qr)) for every non-negative fp16 d (inf included) and
+ * qr = 2^bits - 1, bits 2..8 — the group scale awq.py:202 forms from RN_f16(max - min). */
+static int check_f16_scale(void) {
+    long long cases = 0, mismatches = 0;
+    for (int bits = 2; bits <= 8; ++bits) {
+        volatile float one = 1.0f;
+        const float qr = (float)((1 << bits) - 1), rq = one / qr;
+        for (int h = 0; h <= 0x7C00; ++h) {
+            const float d = oracle_f16_to_f32((uint16_t)h);
+            const uint16_t a = oracle_f32_to_f16(d * rq), b = oracle_f32_to_f16(d / qr);
+            cases++;
+            if (a != b) mismatches++;
+        }
+    }
+    printf("f16 scale d * RN(1/qr): cases=%lld mismatches=%lld\n", cases, mismatches);
+    return mismatches == 0 ? 0 : 1;
+}
+
 /* The clip search's candidate factor alpha_i = RN_f32((n - i) / n) (include/awq_hip.h
  * awq_quantize_search) as the streaming kernel forms it without a division per candidate:
  * q = a * RN(1/n), r = fma(-n, q, a), alpha = fma(r, RN(1/n), q) with a = n - i — equal to the
@@ -182,6 +201,7 @@ int main(int argc, char** argv) {
     if (argc > 1 && strcmp(argv[1], "f16s") == 0) return check_f16_small();
     if (argc > 1 && strcmp(argv[1], "f16f") == 0) return check_f16_fused();
     if (argc > 1 && strcmp(argv[1], "chain16") == 0) return check_chain16();
+    if (argc > 1 && strcmp(argv[1], "f16scale") == 0) return check_f16_scale();
     int bf = !(argc > 1 && strcmp(argv[1], "f16") == 0);
     float lo = dec(enc(1e-10f, bf), bf);
     long long mismatches = 0, pairs = 0;

@@ -263,6 +263,13 @@ def test_selftest_fast_reciprocal_exhaustive():
     assert _hip.selftest(0, torch.device(DEV, 0)) == 0
 
 
+def test_selftest_fast_reciprocal_f16_exhaustive():
+    """Round 6: recip_f16 (v_rcp + Newton) == IEEE 1/s for every positive finite fp16 scale (the
+    fp16 group parameters' reciprocal, AWQ_F16_PARAMS_FAST)."""
+    from awq_quantizer import _hip
+    assert _hip.selftest(2, torch.device(DEV, 0)) == 0
+
+
 def test_stream_copy_helper_copies_exactly():
     """bench.py's copy-ceiling kernel (awq_stream_copy) is a faithful copy, tail included."""
     from awq_quantizer import _hip

@@ -138,3 +138,12 @@ def test_search_packed_fp16_steps_exhaustive():
     assert "cases=515088 mismatches=0" in out.stdout
     fused = _verify_recip("f16f")
     assert fused.returncode == 1 and "mismatches=890" in fused.stdout, fused.stdout
+
+
+def test_f16_scale_by_reciprocal_exhaustive():
+    """The fp16 group scale without the IEEE division (awq_quant.h FmtF16::scale, act
+    HwFmt<F16>::scale): RN_f16(d * RN(1/qr)) == RN_f16(d / qr) for every non-negative fp16 d
+    (inf included) and qr = 2^bits - 1, bits 2..8."""
+    out = _verify_recip("f16scale")
+    assert out.returncode == 0, out.stdout + out.stderr
+    assert "cases=222215 mismatches=0" in out.stdout

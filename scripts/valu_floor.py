@@ -15,7 +15,7 @@ the floor: it is amortised over the group (128 elements) and is what the gap nam
 GAP: the kernel's hot loop in the ISA (`make -C awq-converter_amd/csrc isa ISA_SRC=awq_fast` /
 `ISA_SRC=awq_actsearch`), its VALU instructions per element priced the same way and grouped by
 what they do, beside the measured slots per unit (profiles/round6/pmc_valu.json) and the
-per-type VALU counters of the same commands (profiles/round6/r6fe/{search,act}_{a,b}).
+per-type VALU counters of the same commands (profiles/round6/r6fk/{search,act}_{a,b}).
 
   python scripts/valu_floor.py [--write profiles/round6/valu_floor.json]
 """
@@ -75,7 +75,7 @@ FLOOR = {
     ],
 }
 
-# the per-type counter passes of the same bench commands (scripts/cmd/r6fe.sh; the A / B counter sets
+# the per-type counter passes of the same bench commands (scripts/cmd/r6fk.sh; the A / B counter sets
 # of scripts/valu_classes.py): dynamic instructions per type for the kernel's launches
 TYPE_PASSES = {"search.bf16.asym": ("search_a", "search_b", "awq_fast_kernel"),
                "act.bf16.asym": ("act_a", "act_b", "act_loss_kernel")}
@@ -251,10 +251,10 @@ KERNELS = {
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "round6", "pmc_valu.json"))
-    ap.add_argument("--types-dir", default="search=" + os.path.join(ROOT, "profiles", "round6", "r6fe") + ",act="
-                    + os.path.join(ROOT, "profiles", "round6", "r6fg"),
-                    help="kind=dir,...: the per-type counter passes (search_a/b: scripts/cmd/r6fe.sh, act_a/b: "
-                         "r6fg.sh, the final tree)")
+    ap.add_argument("--types-dir", default="search=" + os.path.join(ROOT, "profiles", "round6", "r6fk") + ",act="
+                    + os.path.join(ROOT, "profiles", "round6", "r6fk"),
+                    help="kind=dir,...: the per-type counter passes (search_a/b, act_a/b: scripts/cmd/r6fk.sh, "
+                         "the final tree)")
     ap.add_argument("--write", default="")
     ap.add_argument("--no-isa", action="store_true", help="floors only (no hipcc)")
     a = ap.parse_args()
